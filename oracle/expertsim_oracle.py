@@ -1,0 +1,557 @@
+"""ORACLE — test infrastructure only.  CPU fp32 restatement of the expertsim GAN training step.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+this module, and only as the checker / CPU baseline.  The product path (the HIP kernels under
+generative-dnn-for-physics-simulations-cern_amd/csrc driven by the ``expertsim`` package) never
+imports it.
+
+What it restates (reference file:line, /root/reference):
+  * parameter construction order and default init of every model
+      neutron/generator.py:6-40, neutron/discriminator.py:7-39, neutron/aux_reg.py:9-68,
+      proton/generator.py:6-44, proton/discriminator.py:117-146, proton/aux_reg.py:12-31,57-121,
+      routers/router.py:7-19; torch default Linear/Conv2d init; spectral_norm u/v draws
+  * forward passes as functional torch CPU ops (generator/discriminator/aux/router forward
+    methods cited at each function)
+  * ``MoEWrapper.train_step`` (moe.py:52-504) with discriminator_train_step (506-527),
+    generator_train_step (529-571), sdi_gan_regularization (573-588),
+    intensity_regularization (590-642) and the router losses of train/utils.py:372-419,623-642
+  * torch.optim.Adam single-tensor update (training_setup.py:12-41 creates them)
+Gradients come from torch autograd on these functional graphs.
+
+Randomness is injected: generator noise and Gumbel exponentials are passed in; dropout masks
+are the counter-based masks of expertsim/utils/philox.py (the golden-capture script feeds the
+very same masks to the reference).  Pinned against tests/golden/*.npz (captured from the
+reference itself by tests/golden/make_goldens.py).
+"""
+from __future__ import annotations
+
+import importlib.util
+import math
+import os
+from collections import OrderedDict
+from itertools import combinations
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_PHILOX = os.path.join(os.path.dirname(_HERE), "generative-dnn-for-physics-simulations-cern_amd",
+                       "expertsim", "utils", "philox.py")
+_spec = importlib.util.spec_from_file_location("_oracle_philox", _PHILOX)
+philox = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(philox)
+
+SLOPE = 0.1
+
+
+# --------------------------------------------------------------------------------------------
+# parameter construction (same RNG consumption order as the reference's nn modules)
+# --------------------------------------------------------------------------------------------
+class _Builder:
+    def __init__(self):
+        self.sd = OrderedDict()
+
+    def _kaiming(self, shape, fan_in):
+        # torch.nn.init.kaiming_uniform_(w, a=sqrt(5)) exactly as torch computes the bound
+        gain = math.sqrt(2.0 / (1 + math.sqrt(5) ** 2))
+        bound = math.sqrt(3.0) * (gain / math.sqrt(fan_in))
+        return torch.empty(shape).uniform_(-bound, bound)
+
+    def _bias(self, n, fan_in):
+        bound = 1 / math.sqrt(fan_in)
+        return torch.empty(n).uniform_(-bound, bound)
+
+    def linear(self, name, fin, fout, sn=False):
+        w = self._kaiming((fout, fin), fin)
+        b = self._bias(fout, fin)
+        self._put(name, w, b, sn)
+
+    def conv(self, name, cin, cout, k, bias=True, sn=False):
+        kh, kw = (k, k) if isinstance(k, int) else k
+        fan = cin * kh * kw
+        w = self._kaiming((cout, cin, kh, kw), fan)
+        b = self._bias(cout, fan) if bias else None
+        self._put(name, w, b, sn)
+
+    def _put(self, name, w, b, sn):
+        if sn:
+            # torch.nn.utils.spectral_norm: u ~ N(0,1)[h], v ~ N(0,1)[w], normalised
+            h, wd = w.shape[0], w[0].numel()
+            u = F.normalize(torch.empty(h).normal_(0, 1), dim=0, eps=1e-12)
+            v = F.normalize(torch.empty(wd).normal_(0, 1), dim=0, eps=1e-12)
+            if b is not None:
+                self.sd[f"{name}.bias"] = b
+            self.sd[f"{name}.weight_orig"] = w
+            self.sd[f"{name}.weight_u"] = u
+            self.sd[f"{name}.weight_v"] = v
+        else:
+            self.sd[f"{name}.weight"] = w
+            if b is not None:
+                self.sd[f"{name}.bias"] = b
+
+    def bn(self, name, c):
+        self.sd[f"{name}.weight"] = torch.ones(c)
+        self.sd[f"{name}.bias"] = torch.zeros(c)
+        self.sd[f"{name}.running_mean"] = torch.zeros(c)
+        self.sd[f"{name}.running_var"] = torch.ones(c)
+        self.sd[f"{name}.num_batches_tracked"] = torch.tensor(0, dtype=torch.long)
+
+    def affine(self, name, c):       # GroupNorm / LayerNorm
+        self.sd[f"{name}.weight"] = torch.ones(c)
+        self.sd[f"{name}.bias"] = torch.zeros(c)
+
+
+def _gn_groups(c, groups=32):
+    g = min(groups, c)                  # proton/aux_reg.py:48-53 (Norm2d)
+    while c % g != 0 and g > 1:
+        g -= 1
+    return g
+
+
+def build_generator(arch, noise_dim=10, cond_dim=9):
+    b = _Builder()
+    if arch == "neutron":              # neutron/generator.py:10-40
+        b.linear("fc1.0", noise_dim + cond_dim, 256); b.bn("fc1.1", 256)
+        b.linear("fc2.0", 256, 128 * 13 * 13); b.bn("fc2.1", 128 * 13 * 13)
+        b.conv("conv_layers.0", 128, 256, 3); b.bn("conv_layers.1", 256)
+        b.conv("conv_layers.5", 256, 128, 3); b.bn("conv_layers.6", 128)
+        b.conv("conv_layers.9", 128, 64, 2); b.bn("conv_layers.10", 64)
+        b.conv("conv_layers.13", 64, 1, 2)
+    else:                              # proton/generator.py:13-44
+        b.linear("fc1.0", noise_dim + cond_dim, 256); b.affine("fc1.1", 256)
+        b.linear("fc2.0", 256, 512 * 18 * 10); b.affine("fc2.1", 512 * 18 * 10)
+        b.conv("conv_layers.1", 512, 256, 4); b.affine("conv_layers.2", 256)
+        b.conv("conv_layers.5", 256, 128, 4); b.affine("conv_layers.6", 128)
+        b.conv("conv_layers.8", 128, 64, 3); b.affine("conv_layers.9", 64)
+        b.conv("conv_layers.11", 64, 1, 2)
+    return b.sd
+
+
+def build_discriminator(arch, cond_dim=9):
+    b = _Builder()                     # neutron/discriminator.py:10-39, proton/discriminator.py:120-146
+    b.conv("conv_layers.0", 1, 32, 3, sn=True); b.affine("conv_layers.1", 32)
+    b.conv("conv_layers.4", 32, 16, 3, sn=True); b.affine("conv_layers.5", 16)
+    flat = 9 * 12 * 12 if arch == "neutron" else 16 * 12 * 12
+    b.linear("fc1.0", flat + cond_dim, 128, sn=True); b.affine("fc1.1", 128)
+    b.linear("fc2.0", 128, 64, sn=True); b.affine("fc2.1", 64)
+    b.linear("fc3", 64, 1, sn=True)
+    return b.sd
+
+
+def build_aux_reg(arch):
+    b = _Builder()
+    if arch == "neutron":              # neutron/aux_reg.py:9-68
+        p = "feature_extractor."
+        b.conv(p + "conv1", 1, 32, 3); b.bn(p + "conv1_bd.0", 32)
+        b.conv(p + "conv2", 32, 64, 3); b.bn(p + "conv2_bd.0", 64)
+        b.conv(p + "conv3", 64, 128, 3); b.bn(p + "conv3_bd.0", 128)
+        b.conv(p + "conv4", 128, 256, 3); b.bn(p + "conv4_bd.0", 256)
+        b.conv(p + "reduce.0", 256, 64, 1, bias=False); b.bn(p + "reduce.1", 64)
+        b.linear("dense", 64, 2)
+    else:                              # proton/aux_reg.py:12-31, 57-121
+        p = "feature_extractor."
+        b.conv(p + "conv1.0", 1, 32, 5); b.affine(p + "conv1.1", 32)
+        for blk, cin, cout in (("res1", 32, 32), ("res2", 32, 64)):
+            q = p + blk + "."
+            b.conv(q + "conv1.0", cin, cout, 5); b.affine(q + "conv1.1", cout)
+            b.conv(q + "conv2.0", cout, cout, 5); b.affine(q + "conv2.1", cout)
+            b.conv(q + "downsample.0", cin, cout, 1); b.affine(q + "downsample.1", cout)
+        b.linear("regressor.0", 64, 128); b.affine("regressor.1", 128)
+        b.linear("regressor.4", 128, 64); b.affine("regressor.5", 64)
+        b.linear("regressor.8", 64, 2)
+    return b.sd
+
+
+def build_router(cond_dim, n_experts):
+    b = _Builder()                     # routers/router.py:11-19
+    b.linear("fc_layers.0", cond_dim, 128)
+    b.linear("fc_layers.2", 128, 64)
+    b.linear("fc_layers.4", 64, 32)
+    b.linear("fc_layers.6", 32, n_experts)
+    return b.sd
+
+
+def build_all(arch, n_experts, seed, noise_dim=10, cond_dim=9):
+    """torch.manual_seed(seed) then G, D, A, router (loop.py:345-348); experts are deep copies."""
+    torch.manual_seed(seed)
+    g = build_generator(arch, noise_dim, cond_dim)
+    d = build_discriminator(arch, cond_dim)
+    a = build_aux_reg(arch)
+    r = build_router(cond_dim, n_experts)
+    clone = lambda sd: OrderedDict((k, v.clone()) for k, v in sd.items())
+    return {"G": [clone(g) for _ in range(n_experts)], "D": [clone(d) for _ in range(n_experts)],
+            "A": [clone(a) for _ in range(n_experts)], "R": r}
+
+
+# --------------------------------------------------------------------------------------------
+# functional layers
+# --------------------------------------------------------------------------------------------
+class Dropper:
+    """Counter-based dropout for one module pass (layer index advances per call)."""
+
+    def __init__(self, seed, step, expert, pass_id, rank=0):
+        self.seed, self.step, self.expert, self.pass_id, self.rank = seed, step, expert, pass_id, rank
+        self.layer = 0
+
+    def __call__(self, x, p):
+        stream = philox.dropout_stream(self.step, self.expert, self.pass_id, self.layer, self.rank)
+        self.layer += 1
+        mask = torch.from_numpy(philox.dropout_mask(tuple(x.shape), p, self.seed, stream))
+        noise = mask.to(x.dtype)
+        noise.div_(1 - p)
+        return x * noise
+
+
+def _bn_train(x, P, name):
+    P[f"{name}.num_batches_tracked"] += 1
+    return F.batch_norm(x, P[f"{name}.running_mean"], P[f"{name}.running_var"],
+                        P[f"{name}.weight"], P[f"{name}.bias"], True, 0.1, 1e-5)
+
+
+def _bn_eval(x, P, name):
+    return F.batch_norm(x, P[f"{name}.running_mean"], P[f"{name}.running_var"],
+                        P[f"{name}.weight"], P[f"{name}.bias"], False, 0.1, 1e-5)
+
+
+def _lin(x, P, name):
+    return F.linear(x, P[f"{name}.weight"], P.get(f"{name}.bias"))
+
+
+def _conv(x, P, name, stride=1, padding=0):
+    return F.conv2d(x, P[f"{name}.weight"], P.get(f"{name}.bias"), stride, padding)
+
+
+def _sn_weight(P, name, training=True):
+    """torch spectral_norm compute_weight: one power iteration in train mode (in-place u, v)."""
+    w = P[f"{name}.weight_orig"]
+    u = P[f"{name}.weight_u"]
+    v = P[f"{name}.weight_v"]
+    wm = w.reshape(w.shape[0], -1)
+    if training:
+        with torch.no_grad():
+            v.copy_(F.normalize(torch.mv(wm.t(), u), dim=0, eps=1e-12))
+            u.copy_(F.normalize(torch.mv(wm, v), dim=0, eps=1e-12))
+    u = u.clone()
+    v = v.clone()
+    sigma = torch.dot(u, torch.mv(wm, v))
+    return w / sigma
+
+
+def generator_forward(arch, P, noise, cond, drop=None, training=True):
+    """neutron/generator.py:42-49, proton/generator.py:46-52."""
+    x = torch.cat((noise, cond), dim=1)
+    lrelu = lambda t: F.leaky_relu(t, SLOPE)
+    if arch == "neutron":
+        bn = _bn_train if training else _bn_eval
+        dp = (lambda t: drop(t, 0.2)) if training else (lambda t: t)
+        x = lrelu(dp(bn(_lin(x, P, "fc1.0"), P, "fc1.1")))
+        x = lrelu(dp(bn(_lin(x, P, "fc2.0"), P, "fc2.1")))
+        x = x.view(-1, 128, 13, 13)
+        x = F.interpolate(x, scale_factor=(2, 2), mode="nearest")
+        x = lrelu(dp(bn(_conv(x, P, "conv_layers.0"), P, "conv_layers.1")))
+        x = F.interpolate(x, scale_factor=(2, 2), mode="nearest")
+        x = lrelu(dp(bn(_conv(x, P, "conv_layers.5"), P, "conv_layers.6")))
+        x = lrelu(dp(bn(_conv(x, P, "conv_layers.9"), P, "conv_layers.10")))
+        return F.relu(_conv(x, P, "conv_layers.13"))
+    ln = lambda t, n, shape: F.layer_norm(t, shape, P[f"{n}.weight"], P[f"{n}.bias"], 1e-5)
+    gn = lambda t, n, g: F.group_norm(t, g, P[f"{n}.weight"], P[f"{n}.bias"], 1e-5)
+    x = lrelu(ln(_lin(x, P, "fc1.0"), "fc1.1", (256,)))
+    x = lrelu(ln(_lin(x, P, "fc2.0"), "fc2.1", (512 * 18 * 10,)))
+    x = x.view(-1, 512, 18, 10)
+    x = F.interpolate(x, scale_factor=(2, 2), mode="nearest")
+    x = lrelu(gn(_conv(x, P, "conv_layers.1", padding=1), "conv_layers.2", 32))
+    x = F.interpolate(x, size=(56, 30), mode="nearest")
+    x = lrelu(gn(_conv(x, P, "conv_layers.5", padding=1), "conv_layers.6", 32))
+    x = lrelu(gn(_conv(x, P, "conv_layers.8", padding=1), "conv_layers.9", 32))
+    return F.relu(_conv(x, P, "conv_layers.11", padding=1))
+
+
+def discriminator_forward(arch, P, img, cond, training=True):
+    """neutron/discriminator.py:41-48, proton/discriminator.py:148-155 (spectral norm each call)."""
+    lrelu = lambda t: F.leaky_relu(t, SLOPE)
+    x = F.conv2d(img, _sn_weight(P, "conv_layers.0", training), P["conv_layers.0.bias"])
+    x = lrelu(F.group_norm(x, 8, P["conv_layers.1.weight"], P["conv_layers.1.bias"], 1e-5))
+    x = F.max_pool2d(x, (2, 2))
+    x = F.conv2d(x, _sn_weight(P, "conv_layers.4", training), P["conv_layers.4.bias"])
+    x = lrelu(F.group_norm(x, 8, P["conv_layers.5.weight"], P["conv_layers.5.bias"], 1e-5))
+    x = F.max_pool2d(x, (2, 2) if arch == "neutron" else (2, 1))
+    x = torch.cat((x.reshape(x.shape[0], -1), cond), dim=1)
+    x = F.linear(x, _sn_weight(P, "fc1.0", training), P["fc1.0.bias"])
+    x = lrelu(F.layer_norm(x, (128,), P["fc1.1.weight"], P["fc1.1.bias"], 1e-5))
+    x = F.linear(x, _sn_weight(P, "fc2.0", training), P["fc2.0.bias"])
+    latent = lrelu(F.layer_norm(x, (64,), P["fc2.1.weight"], P["fc2.1.bias"], 1e-5))
+    out = F.linear(latent, _sn_weight(P, "fc3", training), P["fc3.bias"])
+    return out, latent
+
+
+def aux_forward(arch, P, x, drop=None, training=True):
+    """neutron/aux_reg.py:51-59,76-81; proton/aux_reg.py:33-40,84-96,123-131."""
+    if x.dim() == 3:
+        x = x.unsqueeze(1)
+    p = "feature_extractor."
+    lrelu = lambda t: F.leaky_relu(t, SLOPE)
+    if arch == "neutron":
+        bn = _bn_train if training else _bn_eval
+        dp = (lambda t: drop(t, 0.2)) if training else (lambda t: t)
+        x = F.max_pool2d(dp(lrelu(bn(_conv(x, P, p + "conv1"), P, p + "conv1_bd.0"))), (2, 2))
+        x = F.max_pool2d(dp(lrelu(bn(_conv(x, P, p + "conv2"), P, p + "conv2_bd.0"))), (2, 1))
+        x = F.max_pool2d(dp(lrelu(bn(_conv(x, P, p + "conv3"), P, p + "conv3_bd.0"))), (2, 1))
+        x = dp(lrelu(bn(_conv(x, P, p + "conv4"), P, p + "conv4_bd.0")))
+        x = lrelu(bn(_conv(x, P, p + "reduce.0"), P, p + "reduce.1"))
+        f = F.adaptive_avg_pool2d(x, 1).flatten(1)
+        return _lin(f, P, "dense")
+    gn = lambda t, n: F.group_norm(t, _gn_groups(t.shape[1]) if n.count(".res") else 8,
+                                   P[f"{n}.weight"], P[f"{n}.bias"], 1e-5)
+    x = F.relu(gn(_conv(x, P, p + "conv1.0", 2, 1), p + "conv1.1"))
+    x = F.max_pool2d(x, 2, 1)
+    for blk in ("res1", "res2"):
+        q = p + blk + "."
+        o = F.relu(gn(_conv(x, P, q + "conv1.0", 2, 2), q + "conv1.1"))
+        o = gn(_conv(o, P, q + "conv2.0", 1, 2), q + "conv2.1")
+        idn = gn(_conv(x, P, q + "downsample.0", 2, 0), q + "downsample.1")
+        x = F.max_pool2d(F.relu(o + idn), 2, 1)
+    f = x.mean([2, 3])
+    dp = (lambda t: drop(t, 0.3)) if training else (lambda t: t)
+    h = dp(lrelu(F.layer_norm(_lin(f, P, "regressor.0"), (128,), P["regressor.1.weight"],
+                              P["regressor.1.bias"], 1e-5)))
+    h = dp(lrelu(F.layer_norm(_lin(h, P, "regressor.4"), (64,), P["regressor.5.weight"],
+                              P["regressor.5.bias"], 1e-5)))
+    return _lin(h, P, "regressor.8")
+
+
+def regressor_loss(real, fake):
+    """proton/aux_reg.py:42-45 == neutron/aux_reg.py:70-74 (log-cosh via softplus)."""
+    d = fake - real
+    return torch.mean(d + F.softplus(-2.0 * d) - math.log(2.0))
+
+
+def router_forward(P, cond, tau, gumbel_exp):
+    """routers/router.py:21-26 with torch's gumbel_softmax formula and injected Exp(1) draws."""
+    x = cond
+    for i, name in enumerate(("fc_layers.0", "fc_layers.2", "fc_layers.4", "fc_layers.6")):
+        x = _lin(x, P, name)
+        if i < 3:
+            x = F.leaky_relu(x, SLOPE)
+    logits = x
+    g = -gumbel_exp.log()
+    return ((logits + g) / tau).softmax(-1), logits
+
+
+def sdi_gan_regularization(l1, l2, n1, n2, std, di):
+    """moe.py:573-588 — keeps the [B_e,1] / [B_e] broadcast of the reference."""
+    adl = torch.mean(torch.abs(l1 - l2), dim=1)
+    adn = torch.mean(torch.abs(n1 - n2), dim=1)
+    div = adl / (adn + 1e-5)
+    dl = std / (div + 1e-5)
+    return torch.mean(std) * torch.mean(dl) * di
+
+
+def intensity_regularization(img, intensity, strength):
+    """moe.py:590-642."""
+    s = torch.sum(torch.exp(img) - 1, dim=[2, 3])
+    return F.l1_loss(s, intensity.view(-1, 1)) * strength, s, s.std(), s.mean()
+
+
+# --------------------------------------------------------------------------------------------
+# optimizer
+# --------------------------------------------------------------------------------------------
+class Adam:
+    """torch.optim.Adam single-tensor update (betas 0.9/0.999, eps 1e-8, no weight decay)."""
+
+    def __init__(self, lr, b1=0.9, b2=0.999, eps=1e-8):
+        self.lr, self.b1, self.b2, self.eps = lr, b1, b2, eps
+        self.state = {}
+
+    def step(self, params: dict, grads: dict):
+        for name, g in grads.items():
+            if g is None:
+                continue
+            p = params[name]
+            st = self.state.setdefault(name, {"step": 0, "m": torch.zeros_like(p),
+                                              "v": torch.zeros_like(p)})
+            st["step"] += 1
+            st["m"].lerp_(g, 1 - self.b1)
+            st["v"].mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+            bc1 = 1 - self.b1 ** st["step"]
+            bc2 = 1 - self.b2 ** st["step"]
+            denom = (st["v"].sqrt() / (bc2 ** 0.5)).add_(self.eps)
+            p.addcdiv_(st["m"], denom, value=-(self.lr / bc1))
+
+
+def trainable(sd):
+    """Names that are nn.Parameters in the reference (buffers excluded)."""
+    return [k for k in sd if not (k.endswith("running_mean") or k.endswith("running_var")
+                                  or k.endswith("num_batches_tracked") or k.endswith("weight_u")
+                                  or k.endswith("weight_v"))]
+
+
+# --------------------------------------------------------------------------------------------
+# the training step
+# --------------------------------------------------------------------------------------------
+class OracleMoE:
+    """State + optimizers for E experts; ``train_step`` restates moe.py:52-504."""
+
+    def __init__(self, arch, n_experts, cfg, seed=1234):
+        self.arch, self.E, self.cfg, self.seed = arch, n_experts, cfg, seed
+        self.state = build_all(arch, n_experts, seed, cfg["noise_dim"], cfg["cond_dim"])
+        self.opt_g = [Adam(cfg["lr_g"]) for _ in range(n_experts)]
+        self.opt_d = [Adam(cfg["lr_d"]) for _ in range(n_experts)]
+        self.opt_a = [Adam(cfg["lr_a"]) for _ in range(n_experts)]
+        self.opt_r = Adam(cfg["lr_r"])
+        self.step_count = 0
+
+    def _grad_leaves(self, sd):
+        leaves = {}
+        for k in trainable(sd):
+            sd[k] = sd[k].detach().requires_grad_(True)
+            leaves[k] = sd[k]
+        return leaves
+
+    @staticmethod
+    def _release(sd):
+        for k in list(sd):
+            sd[k] = sd[k].detach()
+
+    def train_step(self, epoch, cond, real, pos, std, intensity, noise_fn, gumbel_exp, trace=None):
+        """``noise_fn(expert, which, shape)`` supplies noise_1 (which=0) / noise_2 (which=1)."""
+        c = self.cfg
+        E, B, step = self.E, cond.shape[0], self.step_count
+        trace = trace if trace is not None else {}
+        tau = max(c["tau_min"], c["tau_start"] * (c["tau_decay"] ** epoch))
+        R = self.state["R"]
+        train_router = E > 1 and epoch < c["stop_router_training_epoch"]
+        rleaves = self._grad_leaves(R) if train_router else {}
+        gates_soft, logits = router_forward(R, cond, tau, gumbel_exp)
+        trace["R"] = (gates_soft.detach().clone(), logits.detach().clone())
+        idx = gates_soft.argmax(dim=1)
+        counts = torch.bincount(idx, minlength=E).to(real.dtype)
+        counts_adj = counts / B
+        gates = F.one_hot(idx, num_classes=E).float() + (gates_soft - gates_soft.detach())
+
+        gen_losses, disc_losses = [], []
+        div_l, aux_l, int_l = np.zeros(E), np.zeros(E), np.zeros(E)
+        mean_int, std_int = [], []
+        mean_in_batch = torch.zeros((B, 1))
+        for i in range(E):
+            mask = (idx == i).nonzero(as_tuple=True)[0]
+            be = mask.numel()
+            if be <= 1:                                              # moe.py:126-135
+                gen_losses.append(torch.tensor(0.0)); disc_losses.append(torch.tensor(0.0))
+                mean_int.append(torch.tensor(0.0)); std_int.append(torch.tensor(0.0))
+                continue
+            G, D, A = self.state["G"][i], self.state["D"][i], self.state["A"][i]
+            sc, sr, sp, si, ss = cond[mask], real[mask], pos[mask], intensity[mask], std[mask]
+            w = float(counts_adj[i])
+            n1 = noise_fn(i, 0, (be, c["noise_dim"]))
+            gl = self._grad_leaves(G)
+            fake = generator_forward(self.arch, G, n1, sc, Dropper(self.seed, step, i, philox.PASS_G1))
+            trace[f"G{i}/0"] = fake.detach().clone()
+            # ---- discriminator step (moe.py:506-527)
+            dl = self._grad_leaves(D)
+            ro, rl = discriminator_forward(self.arch, D, sr, sc)
+            fo, fl = discriminator_forward(self.arch, D, fake.detach(), sc)
+            trace[f"D{i}/0"] = (ro.detach().clone(), rl.detach().clone())
+            trace[f"D{i}/1"] = (fo.detach().clone(), fl.detach().clone())
+            d_loss = (F.relu(1.0 - ro).mean() + F.relu(1.0 + fo).mean()) * w
+            grads = torch.autograd.grad(d_loss, list(dl.values()), allow_unused=True)
+            gd = dict(zip(dl.keys(), grads))
+            trace[f"optD{i}/grad"] = {k: v.detach().clone() for k, v in gd.items()}
+            self._release(D)
+            with torch.no_grad():
+                self.opt_d[i].step(D, gd)
+            # ---- generator step (moe.py:529-571); D weights frozen (their grads are discarded)
+            n2 = noise_fn(i, 1, (be, c["noise_dim"]))
+            fake2 = generator_forward(self.arch, G, n2, sc, Dropper(self.seed, step, i, philox.PASS_G2))
+            trace[f"G{i}/1"] = fake2.detach().clone()
+            fo1, fl1 = discriminator_forward(self.arch, D, fake, sc)
+            fo2, fl2 = discriminator_forward(self.arch, D, fake2, sc)
+            trace[f"D{i}/2"] = (fo1.detach().clone(), fl1.detach().clone())
+            trace[f"D{i}/3"] = (fo2.detach().clone(), fl2.detach().clone())
+            g_loss = -fo1.mean()
+            div = sdi_gan_regularization(fl1, fl2, n1, n2, ss, c["di_strength"])
+            il, sums, s_std, s_mean = intensity_regularization(fake, si, c["in_strength"])
+            g_loss = g_loss + div + il
+            al_leaves = self._grad_leaves(A)
+            coords = aux_forward(self.arch, A, fake, Dropper(self.seed, step, i, philox.PASS_AUX))
+            trace[f"A{i}/0"] = coords.detach().clone()
+            aux = regressor_loss(sp, coords) * c["aux_strength"]
+            g_loss = (g_loss + aux) * w
+            keys = list(gl.keys()) + list(al_leaves.keys())
+            grads = torch.autograd.grad(g_loss, list(gl.values()) + list(al_leaves.values()),
+                                        allow_unused=True)
+            gg = dict(zip(keys[:len(gl)], grads[:len(gl)]))
+            ga = dict(zip(keys[len(gl):], grads[len(gl):]))
+            trace[f"optG{i}/grad"] = {k: v.detach().clone() for k, v in gg.items() if v is not None}
+            trace[f"optA{i}/grad"] = {k: v.detach().clone() for k, v in ga.items() if v is not None}
+            self._release(G); self._release(A)
+            with torch.no_grad():
+                self.opt_g[i].step(G, gg)
+                self.opt_a[i].step(A, ga)
+            mean_in_batch[mask] = sums.detach()
+            mean_int.append(s_mean.detach()); std_int.append(s_std.detach())
+            gen_losses.append(g_loss.detach()); disc_losses.append(d_loss.detach())
+            div_l[i], int_l[i], aux_l[i] = float(div.detach()), float(il.detach()), float(aux.detach())
+
+        rc = c
+        if E > 1:                                                     # moe.py:213-442
+            gan = torch.stack(gen_losses).mean() * rc["gan_strength"]
+            if rc["util_strength"] != 0:
+                avg = gates_soft.mean(0)
+                ent = -(-torch.sum(avg * torch.log(avg + 1e-9), dim=-1) * rc["util_strength"])
+            else:
+                ent = torch.tensor(0.0)
+            if rc["ed_strength"] != 0:
+                dist = torch.cdist(mean_in_batch, mean_in_batch, p=2)
+                sim = gates @ gates.T
+                ed = 0.1 * (torch.sum(sim * dist) / sim.size(0)) * rc["ed_strength"]
+            else:
+                ed = torch.tensor(0.0)
+            if rc["diff_strength"] != 0:
+                dli = sum(F.l1_loss(mean_int[a].unsqueeze(0), mean_int[b].unsqueeze(0))
+                          for a, b in combinations(range(E), 2)) * rc["diff_strength"]
+            else:
+                dli = torch.tensor(0.0)
+            diff = -dli * rc["diff_strength"]
+            alb = (torch.exp(1.0 / (gates_soft.sum(0) + 1e-6)).mean() * rc["alb_strength"]
+                   if rc["alb_strength"] != 0 else torch.tensor(0.0))
+            alpha = min(max(epoch / rc["alpha"], 0.0), 1.0)
+            dec_w = rc["min_weight"] + (1.0 - rc["min_weight"]) * alpha
+            router_loss = ed + gan + diff + ent + dec_w * alb
+            if train_router:
+                rg = torch.autograd.grad(router_loss, list(rleaves.values()), allow_unused=True)
+                grr = dict(zip(rleaves.keys(), rg))
+                trace["optR/grad"] = {k: v.detach().clone() for k, v in grr.items() if v is not None}
+                self._release(R)
+                with torch.no_grad():
+                    self.opt_r.step(R, grr)
+            else:
+                router_loss = torch.tensor(0.0)
+        else:
+            gan = router_loss = ed = diff = ent = alb = torch.tensor(0.0)
+        self._release(R)
+        self.step_count += 1
+        metrics = {
+            "gen_loss": torch.stack(gen_losses).mean(), "disc_loss": torch.stack(disc_losses).mean(),
+            "div_loss": float(np.mean(div_l)), "intensity_loss": float(np.mean(int_l)),
+            "aux_reg_loss": float(np.mean(aux_l)), "router_loss": router_loss,
+            "expert_distribution_loss": ed, "differentiation_loss": diff,
+            "expert_entropy_loss": ent, "adaptive_load_balancing_loss": alb, "gan_loss": gan,
+        }
+        for i in range(E):
+            metrics[f"gen_loss_{i}"] = gen_losses[i]
+            metrics[f"disc_loss_{i}"] = disc_losses[i]
+            metrics[f"div_loss_experts_{i}"] = div_l[i]
+            metrics[f"intensity_loss_experts_{i}"] = int_l[i]
+            metrics[f"aux_reg_loss_experts_{i}"] = aux_l[i]
+            metrics[f"std_intensities_experts_{i}"] = std_int[i]
+            metrics[f"mean_intensities_experts_{i}"] = mean_int[i]
+            metrics[f"n_choosen_experts_mean_epoch_{i}"] = counts[i]
+        return {k: float(v) for k, v in metrics.items()}, trace
+
+
+DEFAULT_CFG = dict(noise_dim=10, cond_dim=9, lr_g=1e-4, lr_d=1e-5, lr_a=1e-4, lr_r=1e-4,
+                   di_strength=0.1, in_strength=1e-3, aux_strength=1e-3, ed_strength=0.0,
+                   gan_strength=0.1, diff_strength=1e-6, util_strength=0.0, alb_strength=1e-5,
+                   stop_router_training_epoch=40, alpha=60, min_weight=0.2, tau_start=1.2,
+                   tau_min=0.8, tau_decay=0.985)

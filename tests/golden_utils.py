@@ -1,0 +1,72 @@
+"""Helpers to read the reference golden vectors (tests/golden/*.npz, see make_goldens.py)."""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+
+GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CASES = ["neutron_e1_b8", "neutron_e3_b12", "proton_e1_b8", "proton_e3_b12"]
+
+
+class Golden:
+    def __init__(self, case):
+        self.case = case
+        self.z = np.load(os.path.join(GOLDEN_DIR, f"{case}.npz"), allow_pickle=False)
+        self.meta = json.loads(str(self.z["meta"]))
+        self.arch = self.meta["arch"]
+        self.E = self.meta["n_experts"]
+        self.B = self.meta["batch"]
+        self.steps = self.meta["steps"]
+        self.seed = self.meta["seed"]
+        self.epoch = self.meta["epoch"]
+
+    def __getitem__(self, k):
+        return self.z[k]
+
+    def has(self, k):
+        return k in self.z.files
+
+    def keys(self, prefix):
+        return [k for k in self.z.files if k.startswith(prefix)]
+
+    def inputs(self, step):
+        p = f"s{step}/in/"
+        return {k[len(p):]: self.z[k] for k in self.keys(p)}
+
+    def router_idx(self, step):
+        gates = self.z[f"s{step}/R/call0/out0"]
+        return gates.argmax(1)
+
+    def noise(self, step):
+        """(expert, which) -> recorded torch.randn draw, mapped by reference call order."""
+        idx = self.router_idx(step)
+        out, k = {}, 0
+        for e in range(self.E):
+            if (idx == e).sum() <= 1:
+                continue
+            for which in (0, 1):
+                out[(e, which)] = self.z[f"s{step}/randn{k}"]
+                k += 1
+        return out
+
+    def gumbel(self, step):
+        return self.z[f"s{step}/gumbel_exp"]
+
+    def metrics(self, step):
+        p = f"s{step}/metric/"
+        return {k[len(p):]: float(self.z[k]) for k in self.keys(p)}
+
+
+def checksum(a):
+    a = np.asarray(a, dtype=np.float64).reshape(-1)
+    n = a.size
+    idx = (np.arange(64) * n) // 64 if n >= 64 else np.arange(n)
+    return np.concatenate([[a.sum(), np.abs(a).sum(), np.sqrt((a * a).sum())], a[idx]])
+
+
+def rel_err(a, b, floor=1e-12):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.max(np.abs(a - b)) / max(float(np.max(np.abs(b))), floor))
