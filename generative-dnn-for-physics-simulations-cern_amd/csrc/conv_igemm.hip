@@ -1,0 +1,511 @@
+// Implicit-GEMM convolution (and linear) forward / dgrad / wgrad on gfx950 MFMA.
+//
+// Replaces aten::convolution, aten::convolution_backward and aten::addmm/mm for every nn.Conv2d
+// and nn.Linear on the expertsim hot path (see include/expertsim_hip.h for the call sites).
+//
+// GEMM views (one kernel template, three operand gathers):
+//   FWD   : M = N*P*Q (output pixels), Ng = K (out channels), Kd = R*S*C  (c fastest)
+//           A[m][kk] = xu[n, c, p*st-pad+r, q*st-pad+s]    B[ng][kk] = Wk[k][r][s][c]
+//   DGRAD : M = N*Hu*Wu (upsampled input pixels), Ng = C, Kd = R*S*K (k fastest)
+//           A[m][kk] = dy[n, k, (hu+pad-r)/st, (wu+pad-s)/st] (0 unless divisible / in range)
+//           B[ng][kk] = Wd[c][r][s][k]
+//   WGRAD : M = K, Ng = R*S*C, Kd = N*P*Q (split over blockIdx.z, fp32 atomics)
+//           A[m][kk] = dy[pix][k]                        B[ng][kk] = xu[pix shifted by (r,s)][c]
+// The nearest upsample of the generators (neutron/generator.py:23,29; proton/generator.py:26,32)
+// is folded into the x gather through hmap/wmap (up row -> source row).
+//
+// Tiling: 256 threads = 4 waves in a 2x2 grid, block tile BM x BN, K-step = 128 bytes of operand
+// per row (bf16: 64, fp32: 32).  LDS holds both operands K-contiguous ([row][k], 144-byte padded
+// rows -> conflict-free 16-byte fragment reads), double buffered; global->register->LDS staging
+// with the next tile's loads issued before the current tile's MFMAs.
+//   bf16 : v_mfma_f32_16x16x32_bf16, lane l reads A[l&15][8*(l>>4)+0..7] as one 16-byte read
+//   fp32 : v_mfma_f32_16x16x4_f32 x4, lane l reads A[l&15][4*(l>>4)+0..3] once and feeds the
+//          four MFMAs with k = 4*(l>>4)+t (A and B use the same permutation of k, so the sum over
+//          k is unchanged; each MFMA is an exact fp32 FMA chain).
+#include "common.h"
+
+namespace {
+
+enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
+
+constexpr int KSTEP_BYTES = 128;               // operand bytes per row per K-step
+constexpr int ROW_BYTES = KSTEP_BYTES + 16;    // padded LDS row
+constexpr int NTHREADS = 256;
+
+struct ConvArgs {
+  es_conv_desc_t d;
+  const void* a_src;
+  const void* b_src;
+  int64_t as[4];      // FWD: x strides;  DGRAD/WGRAD: dy strides
+  int64_t bs[4];      // WGRAD: x strides
+  void* out;
+  int64_t os[4];      // FWD: y strides; DGRAD: dxu strides
+  const float* bias;
+  float beta;
+  int out_bf16;
+  int M, Ng, Kd;
+  int k_per_split;
+};
+
+template <typename T> struct Vec16;
+template <> struct Vec16<float> { typedef float4 type; static constexpr int N = 4; };
+template <> struct Vec16<bf16> { typedef uint4 type; static constexpr int N = 8; };
+
+__device__ __forceinline__ int src_row(const int32_t* map, int u) { return map ? map[u] : u; }
+
+// ---------------------------------------------------------------------------------------------
+// Element gathers (scalar); used by the generic path and by the vector path for the base address
+// ---------------------------------------------------------------------------------------------
+template <typename T, int MODE>
+__device__ __forceinline__ float gather_a(const ConvArgs& a, int m, int kk) {
+  const es_conv_desc_t& d = a.d;
+  const T* src = (const T*)a.a_src;
+  if (m >= a.M || kk >= a.Kd) return 0.f;
+  if constexpr (MODE == MODE_FWD) {
+    const int c = kk % d.C; const int rs = kk / d.C; const int s = rs % d.S; const int r = rs / d.S;
+    const int q = m % d.Q; const int np = m / d.Q; const int p = np % d.P; const int n = np / d.P;
+    const int hu = p * d.stride - d.pad + r, wu = q * d.stride - d.pad + s;
+    if (hu < 0 || hu >= d.Hu || wu < 0 || wu >= d.Wu) return 0.f;
+    return to_f(src[off4(a.as, n, c, src_row(d.hmap, hu), src_row(d.wmap, wu))]);
+  } else if constexpr (MODE == MODE_DGRAD) {
+    const int k = kk % d.K; const int rs = kk / d.K; const int s = rs % d.S; const int r = rs / d.S;
+    const int wu = m % d.Wu; const int nh = m / d.Wu; const int hu = nh % d.Hu; const int n = nh / d.Hu;
+    const int ph = hu + d.pad - r, pw = wu + d.pad - s;
+    if (ph < 0 || pw < 0 || ph % d.stride || pw % d.stride) return 0.f;
+    const int p = ph / d.stride, q = pw / d.stride;
+    if (p >= d.P || q >= d.Q) return 0.f;
+    return to_f(src[off4(a.as, n, k, p, q)]);
+  } else {  // WGRAD: A[m=k][kk=pix]
+    const int q = kk % d.Q; const int np = kk / d.Q; const int p = np % d.P; const int n = np / d.P;
+    return to_f(src[off4(a.as, n, m, p, q)]);
+  }
+}
+
+template <typename T, int MODE>
+__device__ __forceinline__ float gather_b(const ConvArgs& a, int ng, int kk) {
+  const es_conv_desc_t& d = a.d;
+  const T* src = (const T*)a.b_src;
+  if (ng >= a.Ng || kk >= a.Kd) return 0.f;
+  if constexpr (MODE == MODE_FWD || MODE == MODE_DGRAD) {
+    return to_f(src[(int64_t)ng * a.Kd + kk]);
+  } else {  // WGRAD: B[ng=(r,s,c)][kk=pix] = xu
+    const int c = ng % d.C; const int rs = ng / d.C; const int s = rs % d.S; const int r = rs / d.S;
+    const int q = kk % d.Q; const int np = kk / d.Q; const int p = np % d.P; const int n = np / d.P;
+    const int hu = p * d.stride - d.pad + r, wu = q * d.stride - d.pad + s;
+    if (hu < 0 || hu >= d.Hu || wu < 0 || wu >= d.Wu) return 0.f;
+    return to_f(src[off4(a.bs, n, c, src_row(d.hmap, hu), src_row(d.wmap, wu))]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Tile staging.  A "chunk" is 16 bytes of one LDS row (VEC elements along k).
+//   K-contiguous operands (FWD/DGRAD A, FWD/DGRAD B): a chunk = VEC consecutive kk of one row.
+//   WGRAD operands: global data is contiguous along m / ng, so a chunk holds VEC consecutive rows
+//   of one kk and is scattered into LDS element by element (transposing store).
+// ---------------------------------------------------------------------------------------------
+template <typename T, int MODE, int BROWS, bool IS_A, bool VEC>
+struct Stager {
+  typedef typename Vec16<T>::type V;
+  static constexpr int VN = Vec16<T>::N;
+  static constexpr int BK = KSTEP_BYTES / sizeof(T);
+  static constexpr int CHUNKS = BROWS * (KSTEP_BYTES / 16);
+  static constexpr int PER_THREAD = CHUNKS / NTHREADS;
+  static constexpr bool TRANS = (MODE == MODE_WGRAD);
+  V reg[PER_THREAD];
+
+  __device__ __forceinline__ void load(const ConvArgs& a, int row0, int k0) {
+#pragma unroll
+    for (int i = 0; i < PER_THREAD; ++i) {
+      const int idx = threadIdx.x + i * NTHREADS;
+      int row, kk;
+      if constexpr (!TRANS) {
+        row = row0 + idx / (KSTEP_BYTES / 16);
+        kk = k0 + (idx % (KSTEP_BYTES / 16)) * VN;
+      } else {
+        row = row0 + (idx % (BROWS / VN)) * VN;
+        kk = k0 + idx / (BROWS / VN);
+      }
+      reg[i] = fetch(a, row, kk);
+    }
+  }
+
+  __device__ __forceinline__ V fetch(const ConvArgs& a, int row, int kk) {
+    if constexpr (VEC) {
+      const T* p = vec_ptr(a, row, kk);
+      if (p) return *(const V*)p;
+      return V{};
+    } else {
+      T e[VN];
+#pragma unroll
+      for (int j = 0; j < VN; ++j) {
+        float f;
+        if constexpr (!TRANS) f = IS_A ? gather_a<T, MODE>(a, row, kk + j) : gather_b<T, MODE>(a, row, kk + j);
+        else f = IS_A ? gather_a<T, MODE>(a, row + j, kk) : gather_b<T, MODE>(a, row + j, kk);
+        e[j] = from_f<T>(f);
+      }
+      V v; memcpy(&v, e, sizeof(v)); return v;
+    }
+  }
+
+  // Address of the first element of a vector chunk, or nullptr when the chunk is all zero.
+  // Preconditions (checked on the host): the vector dimension is contiguous and VN-divisible.
+  __device__ __forceinline__ const T* vec_ptr(const ConvArgs& a, int row, int kk) {
+    const es_conv_desc_t& d = a.d;
+    if constexpr (MODE == MODE_FWD) {
+      if constexpr (IS_A) {
+        if (row >= a.M || kk >= a.Kd) return nullptr;
+        const int c = kk % d.C; const int rs = kk / d.C; const int s = rs % d.S; const int r = rs / d.S;
+        const int q = row % d.Q; const int np = row / d.Q; const int p = np % d.P; const int n = np / d.P;
+        const int hu = p * d.stride - d.pad + r, wu = q * d.stride - d.pad + s;
+        if (hu < 0 || hu >= d.Hu || wu < 0 || wu >= d.Wu) return nullptr;
+        return (const T*)a.a_src + off4(a.as, n, c, src_row(d.hmap, hu), src_row(d.wmap, wu));
+      } else {
+        if (row >= a.Ng || kk >= a.Kd) return nullptr;
+        return (const T*)a.b_src + (int64_t)row * a.Kd + kk;
+      }
+    } else if constexpr (MODE == MODE_DGRAD) {
+      if constexpr (IS_A) {
+        if (row >= a.M || kk >= a.Kd) return nullptr;
+        const int k = kk % d.K; const int rs = kk / d.K; const int s = rs % d.S; const int r = rs / d.S;
+        const int wu = row % d.Wu; const int nh = row / d.Wu; const int hu = nh % d.Hu; const int n = nh / d.Hu;
+        const int ph = hu + d.pad - r, pw = wu + d.pad - s;
+        if (ph < 0 || pw < 0 || ph % d.stride || pw % d.stride) return nullptr;
+        const int p = ph / d.stride, q = pw / d.stride;
+        if (p >= d.P || q >= d.Q) return nullptr;
+        return (const T*)a.a_src + off4(a.as, n, k, p, q);
+      } else {
+        if (row >= a.Ng || kk >= a.Kd) return nullptr;
+        return (const T*)a.b_src + (int64_t)row * a.Kd + kk;
+      }
+    } else {  // WGRAD: vector along rows (m = out channel for A, ng = (r,s,c) for B)
+      if (kk >= a.Kd) return nullptr;
+      const int q = kk % d.Q; const int np = kk / d.Q; const int p = np % d.P; const int n = np / d.P;
+      if constexpr (IS_A) {
+        if (row >= a.M) return nullptr;
+        return (const T*)a.a_src + off4(a.as, n, row, p, q);
+      } else {
+        if (row >= a.Ng) return nullptr;
+        const int c = row % d.C; const int rs = row / d.C; const int s = rs % d.S; const int r = rs / d.S;
+        const int hu = p * d.stride - d.pad + r, wu = q * d.stride - d.pad + s;
+        if (hu < 0 || hu >= d.Hu || wu < 0 || wu >= d.Wu) return nullptr;
+        return (const T*)a.b_src + off4(a.bs, n, c, src_row(d.hmap, hu), src_row(d.wmap, wu));
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(char* lds) {
+#pragma unroll
+    for (int i = 0; i < PER_THREAD; ++i) {
+      const int idx = threadIdx.x + i * NTHREADS;
+      if constexpr (!TRANS) {
+        const int row = idx / (KSTEP_BYTES / 16), ch = idx % (KSTEP_BYTES / 16);
+        *(V*)(lds + row * ROW_BYTES + ch * 16) = reg[i];
+      } else {
+        const int row = (idx % (BROWS / VN)) * VN, kk = idx / (BROWS / VN);
+        T e[VN];
+        memcpy(e, &reg[i], sizeof(e));
+#pragma unroll
+        for (int j = 0; j < VN; ++j) *(T*)(lds + (row + j) * ROW_BYTES + kk * sizeof(T)) = e[j];
+      }
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+// MFMA micro-kernel on one K-step held in LDS
+// ---------------------------------------------------------------------------------------------
+template <typename T, int RM, int RN>
+__device__ __forceinline__ void mma_kstep(const char* As, const char* Bs, int wm0, int wn0,
+                                          f32x4 (&acc)[RM][RN]) {
+  const int lane = threadIdx.x & 63;
+  const int r16 = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int seg = kk * 4 + g;
+    if constexpr (sizeof(T) == 2) {
+      bf16x8 af[RM], bfr[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) af[i] = *(const bf16x8*)(As + (wm0 + i * 16 + r16) * ROW_BYTES + seg * 16);
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bfr[j] = *(const bf16x8*)(Bs + (wn0 + j * 16 + r16) * ROW_BYTES + seg * 16);
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    } else {
+      float4 af[RM], bfr[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) af[i] = *(const float4*)(As + (wm0 + i * 16 + r16) * ROW_BYTES + seg * 16);
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bfr[j] = *(const float4*)(Bs + (wn0 + j * 16 + r16) * ROW_BYTES + seg * 16);
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i].x, bfr[j].x, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i].y, bfr[j].y, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i].z, bfr[j].z, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i].w, bfr[j].w, acc[i][j], 0, 0, 0);
+        }
+    }
+  }
+}
+
+template <typename T, int MODE, int BM, int BN, bool AVEC, bool BVEC>
+__global__ void __launch_bounds__(NTHREADS) conv_igemm_kernel(ConvArgs a) {
+  constexpr int BK = KSTEP_BYTES / sizeof(T);
+  constexpr int RM = BM / 32, RN = BN / 32;   // 16x16 tiles per wave (2x2 wave grid)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BUF = (BM + BN) * ROW_BYTES;   // one stage: A rows then B rows
+
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  int kbeg = 0, kend = a.Kd;
+  if constexpr (MODE == MODE_WGRAD) {
+    kbeg = blockIdx.z * a.k_per_split;
+    kend = min(a.Kd, kbeg + a.k_per_split);
+    if (kbeg >= kend) return;
+  }
+  const int wid = threadIdx.x >> 6;
+  const int wm0 = (wid >> 1) * (BM / 2), wn0 = (wid & 1) * (BN / 2);
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Stager<T, MODE, BM, true, AVEC> sa;
+  Stager<T, MODE, BN, false, BVEC> sb;
+  sa.load(a, m0, kbeg);
+  sb.load(a, n0, kbeg);
+  sa.store(smem);
+  sb.store(smem + BM * ROW_BYTES);
+  __syncthreads();
+  int cur = 0;
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+    const bool more = k0 + BK < kend;
+    if (more) {
+      sa.load(a, m0, k0 + BK);
+      sb.load(a, n0, k0 + BK);
+    }
+    mma_kstep<T, RM, RN>(smem + cur * BUF, smem + cur * BUF + BM * ROW_BYTES, wm0, wn0, acc);
+    if (more) {
+      sa.store(smem + (cur ^ 1) * BUF);
+      sb.store(smem + (cur ^ 1) * BUF + BM * ROW_BYTES);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  (void)BK;
+
+  // ---------------------------------------------------------------- epilogue
+  const int lane = threadIdx.x & 63;
+  const int col16 = lane & 15, rq = (lane >> 4) * 4;
+  const es_conv_desc_t& d = a.d;
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int m = m0 + wm0 + i * 16 + rq + jj;
+      if (m >= a.M) continue;
+      int64_t rowoff = 0;
+      if constexpr (MODE == MODE_FWD) {
+        const int q = m % d.Q; const int np = m / d.Q; const int p = np % d.P; const int n = np / d.P;
+        rowoff = n * a.os[0] + p * a.os[2] + q * a.os[3];
+      } else if constexpr (MODE == MODE_DGRAD) {
+        const int wu = m % d.Wu; const int nh = m / d.Wu; const int hu = nh % d.Hu; const int n = nh / d.Hu;
+        rowoff = n * a.os[0] + hu * a.os[2] + wu * a.os[3];
+      }
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int ng = n0 + wn0 + j * 16 + col16;
+        if (ng >= a.Ng) continue;
+        float v = acc[i][j][jj];
+        if constexpr (MODE == MODE_WGRAD) {
+          atomicAdd((float*)a.out + (int64_t)m * a.Ng + ng, v);
+        } else {
+          if constexpr (MODE == MODE_FWD) {
+            if (a.bias) v += a.bias[ng];
+          }
+          const int64_t o = rowoff + (int64_t)ng * a.os[1];
+          if (a.out_bf16) {
+            bf16* y = (bf16*)a.out + o;
+            if (a.beta != 0.f) v += a.beta * (float)(*y);
+            *y = (bf16)v;
+          } else {
+            float* y = (float*)a.out + o;
+            if (a.beta != 0.f) v += a.beta * (*y);
+            *y = v;
+          }
+        }
+      }
+    }
+  }
+}
+
+template <typename T, int MODE, int BM, int BN>
+int launch_tile(const ConvArgs& a, bool avec, bool bvec, hipStream_t st, int splits) {
+  dim3 grid((a.M + BM - 1) / BM, (a.Ng + BN - 1) / BN, splits);
+  const size_t lds = 2 * (BM + BN) * ROW_BYTES;
+#define ES_LAUNCH(AV, BV)                                                                     \
+  hipLaunchKernelGGL((conv_igemm_kernel<T, MODE, BM, BN, AV, BV>), grid, dim3(NTHREADS), lds, \
+                     st, a)
+  if (avec && bvec) ES_LAUNCH(true, true);
+  else if (avec) ES_LAUNCH(true, false);
+  else if (bvec) ES_LAUNCH(false, true);
+  else ES_LAUNCH(false, false);
+#undef ES_LAUNCH
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+template <typename T, int MODE>
+int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
+  constexpr int BK = KSTEP_BYTES / sizeof(T);
+  // tile choice: 128x128 for big GEMMs, 64x64 when either side is small
+  const bool big = a.M >= 128 && a.Ng >= 96;
+  const int BM = big ? 128 : 64, BN = big ? 128 : 64;
+  int splits = 1;
+  if (MODE == MODE_WGRAD) {
+    const int tiles = ((a.M + BM - 1) / BM) * ((a.Ng + BN - 1) / BN);
+    const int ksteps = (a.Kd + BK - 1) / BK;
+    int want = (2048 + tiles - 1) / tiles;            // ~2048 workgroups
+    want = max(1, min(want, ksteps / 4 > 0 ? ksteps / 4 : 1));  // >= 4 K-steps per split
+    const int per = ((ksteps + want - 1) / want) * BK;
+    a.k_per_split = per;
+    splits = (a.Kd + per - 1) / per;
+  } else {
+    a.k_per_split = a.Kd;
+  }
+  if (big) return launch_tile<T, MODE, 128, 128>(a, avec, bvec, st, splits);
+  return launch_tile<T, MODE, 64, 64>(a, avec, bvec, st, splits);
+}
+
+template <int MODE>
+int dispatch(ConvArgs& a, es_dtype_t dt, bool avec, bool bvec, hipStream_t st) {
+  if (dt == ES_F32) return launch<float, MODE>(a, avec, bvec, st);
+  if (dt == ES_BF16) return launch<bf16, MODE>(a, avec, bvec, st);
+  es_set_error("conv: unsupported dtype %d", (int)dt);
+  return ES_ERR_ARG;
+}
+
+int check_desc(const es_conv_desc_t* d) {
+  ES_CHECK_ARG(d && d->N > 0 && d->C > 0 && d->K > 0 && d->R > 0 && d->S > 0 && d->stride > 0,
+               "conv: bad descriptor");
+  ES_CHECK_ARG(d->P == (d->Hu + 2 * d->pad - d->R) / d->stride + 1 &&
+                   d->Q == (d->Wu + 2 * d->pad - d->S) / d->stride + 1,
+               "conv: output size %dx%d inconsistent with input %dx%d k%dx%d s%d p%d", d->P, d->Q,
+               d->Hu, d->Wu, d->R, d->S, d->stride, d->pad);
+  ES_CHECK_ARG((d->hmap == nullptr) == (d->wmap == nullptr), "conv: hmap/wmap must both be set");
+  ES_CHECK_ARG(d->hmap || (d->Hu == d->H && d->Wu == d->W), "conv: Hu/Wu != H/W without maps");
+  const int64_t M1 = (int64_t)d->N * d->P * d->Q, M2 = (int64_t)d->N * d->Hu * d->Wu;
+  ES_CHECK_ARG(M1 < (1ll << 31) && M2 < (1ll << 31), "conv: problem too large for int32 rows");
+  return ES_OK;
+}
+
+}  // namespace
+
+extern "C" int es_conv2d_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x,
+                             const int64_t xs[4], const void* wk, const float* bias, void* y,
+                             es_dtype_t ydt, const int64_t ys[4], es_stream_t stream) {
+  if (int e = check_desc(d)) return e;
+  ConvArgs a{};
+  a.d = *d; a.a_src = x; a.b_src = wk; a.out = y; a.bias = bias; a.beta = 0.f;
+  a.out_bf16 = ydt == ES_BF16;
+  for (int i = 0; i < 4; ++i) { a.as[i] = xs[i]; a.os[i] = ys[i]; }
+  a.M = d->N * d->P * d->Q; a.Ng = d->K; a.Kd = d->R * d->S * d->C;
+  const int vn = dt == ES_BF16 ? 8 : 4;
+  const bool avec = xs[1] == 1 && d->C % vn == 0;
+  const bool bvec = a.Kd % vn == 0;
+  return dispatch<MODE_FWD>(a, dt, avec, bvec, (hipStream_t)stream);
+}
+
+extern "C" int es_conv2d_dgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy,
+                               const int64_t ys[4], const void* wd, void* dxu, es_dtype_t dxdt,
+                               const int64_t dxs[4], float beta, es_stream_t stream) {
+  if (int e = check_desc(d)) return e;
+  ConvArgs a{};
+  a.d = *d; a.a_src = dy; a.b_src = wd; a.out = dxu; a.bias = nullptr; a.beta = beta;
+  a.out_bf16 = dxdt == ES_BF16;
+  for (int i = 0; i < 4; ++i) { a.as[i] = ys[i]; a.os[i] = dxs[i]; }
+  a.M = d->N * d->Hu * d->Wu; a.Ng = d->C; a.Kd = d->R * d->S * d->K;
+  const int vn = dt == ES_BF16 ? 8 : 4;
+  const bool avec = ys[1] == 1 && d->K % vn == 0;
+  const bool bvec = a.Kd % vn == 0;
+  return dispatch<MODE_DGRAD>(a, dt, avec, bvec, (hipStream_t)stream);
+}
+
+extern "C" int es_conv2d_wgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy,
+                               const int64_t ys[4], const void* x, const int64_t xs[4], float* dw,
+                               es_stream_t stream) {
+  if (int e = check_desc(d)) return e;
+  ConvArgs a{};
+  a.d = *d; a.a_src = dy; a.b_src = x; a.out = dw;
+  for (int i = 0; i < 4; ++i) { a.as[i] = ys[i]; a.bs[i] = xs[i]; }
+  a.M = d->K; a.Ng = d->R * d->S * d->C; a.Kd = d->N * d->P * d->Q;
+  const int vn = dt == ES_BF16 ? 8 : 4;
+  const bool avec = ys[1] == 1 && d->K % vn == 0;
+  const bool bvec = xs[1] == 1 && d->C % vn == 0;
+  return dispatch<MODE_WGRAD>(a, dt, avec, bvec, (hipStream_t)stream);
+}
+
+// ------------------------------------------------------------------------- weight (un)packing
+namespace {
+template <typename T>
+__global__ void pack_weight_kernel(const float* __restrict__ w, int K, int C, int R, int S, int mode,
+                                   const float* inv_scale, const int32_t* col_perm, T* out) {
+  const int64_t n = (int64_t)K * C * R * S;
+  const float sc = inv_scale ? 1.f / inv_scale[0] : 1.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    // i indexes the OUTPUT layout
+    int k, c, r, s;
+    if (mode == 0) {  // [K][R][S][C]
+      c = i % C; int64_t t = i / C; s = t % S; t /= S; r = t % R; k = t / R;
+    } else {          // [C][R][S][K]
+      k = i % K; int64_t t = i / K; s = t % S; t /= S; r = t % R; c = t / R;
+    }
+    const int cs = col_perm ? col_perm[c] : c;
+    out[i] = from_f<T>(w[(((int64_t)k * C + cs) * R + r) * S + s] * sc);
+  }
+}
+
+__global__ void unpack_grad_kernel(const float* __restrict__ dw, int K, int C, int R, int S,
+                                   const int32_t* col_perm, float* grad, float beta) {
+  const int64_t n = (int64_t)K * C * R * S;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    // i indexes dw layout [K][R][S][C]
+    const int c = i % C; int64_t t = i / C; const int s = t % S; t /= S; const int r = t % R; const int k = t / R;
+    const int cs = col_perm ? col_perm[c] : c;
+    float* g = grad + (((int64_t)k * C + cs) * R + r) * S + s;
+    *g = (beta != 0.f ? beta * *g : 0.f) + dw[i];
+  }
+}
+}  // namespace
+
+extern "C" int es_pack_conv_weight(const float* w, int K, int C, int R, int S, int mode,
+                                   const float* inv_scale, const int32_t* col_perm, void* out,
+                                   es_dtype_t dt, es_stream_t stream) {
+  ES_CHECK_ARG(mode == 0 || mode == 1, "pack: bad mode");
+  const int64_t n = (int64_t)K * C * R * S;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  if (dt == ES_F32)
+    hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       w, K, C, R, S, mode, inv_scale, col_perm, (float*)out);
+  else
+    hipLaunchKernelGGL(pack_weight_kernel<bf16>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       w, K, C, R, S, mode, inv_scale, col_perm, (bf16*)out);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_unpack_conv_grad(const float* dw, int K, int C, int R, int S,
+                                   const int32_t* col_perm, float* grad, float beta,
+                                   es_stream_t stream) {
+  const int64_t n = (int64_t)K * C * R * S;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(unpack_grad_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, dw, K, C,
+                     R, S, col_perm, grad, beta);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}

@@ -1,0 +1,257 @@
+// Loss kernels of the expertsim train step and their gradients (single-pass, no host syncs).
+//   hinge D          moe.py:518-523
+//   gen hinge        moe.py:544
+//   SDI diversity    moe.py:573-588 (closed form of the [B,1]/[B] broadcast: see es_gen_losses)
+//   intensity L1     moe.py:590-642
+//   log-cosh aux     proton/aux_reg.py:42-45 == neutron/aux_reg.py:70-74, x strength (moe.py:559)
+//   gumbel softmax   routers/router.py:23 (torch F.gumbel_softmax, hard=False)
+//   ALB router loss  train/utils.py:623-642, weighted as moe.py:407,418-434
+#include "common.h"
+
+namespace {
+struct View {
+  int n, c, h, w;
+  int64_t s[4];
+  __device__ __forceinline__ int64_t off(int in, int ic, int ih, int iw) const {
+    return in * s[0] + ic * s[1] + ih * s[2] + iw * s[3];
+  }
+};
+View mkview(const es_view_t* v) {
+  View r;
+  r.n = v->n; r.c = v->c; r.h = v->h; r.w = v->w;
+  for (int i = 0; i < 4; ++i) r.s[i] = v->s[i];
+  return r;
+}
+__device__ __forceinline__ float ldf(const void* p, int bf, int64_t i) {
+  return bf ? (float)((const bf16*)p)[i] : ((const float*)p)[i];
+}
+__device__ __forceinline__ float signf_(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
+
+__global__ void __launch_bounds__(256) hinge_d_kernel(const float* ro, const float* fo, int n, const float* wp,
+                                                      float* out, float* dro, float* dfo) {
+  __shared__ float sh[8];
+  const float w = wp[0];
+  float a = 0.f, b = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const float tr = 1.f - ro[i], tf = 1.f + fo[i];
+    a += fmaxf(tr, 0.f);
+    b += fmaxf(tf, 0.f);
+    if (dro) dro[i] = tr > 0.f ? -w / (float)n : 0.f;
+    if (dfo) dfo[i] = tf > 0.f ? w / (float)n : 0.f;
+  }
+  a = block_sum(a, sh);
+  b = block_sum(b, sh);
+  if (threadIdx.x == 0) out[0] = (a / (float)n + b / (float)n) * w;
+}
+
+// one block per sample: s[b] = sum_{c,h,w} exp(x) - 1
+__global__ void __launch_bounds__(256) expsum_kernel(View x, const void* xp, int bf, float* s) {
+  __shared__ float sh[8];
+  const int n = blockIdx.x;
+  const int per = x.c * x.h * x.w;
+  float a = 0.f;
+  for (int i = threadIdx.x; i < per; i += blockDim.x) {
+    const int w = i % x.w, t = i / x.w, h = t % x.h, c = t / x.h;
+    a += expf(ldf(xp, bf, x.off(n, c, h, w))) - 1.f;
+  }
+  a = block_sum(a, sh);
+  if (threadIdx.x == 0) s[n] = a;
+}
+
+__global__ void expsum_bwd_kernel(View x, const void* xp, int bf, const float* coef, View dx, float* dxp,
+                                  float beta) {
+  const int64_t total = (int64_t)x.n * x.c * x.h * x.w;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int w = e % x.w; int64_t t = e / x.w; const int h = t % x.h; t /= x.h; const int c = t % x.c;
+    const int n = t / x.c;
+    float g = coef[n] * expf(ldf(xp, bf, x.off(n, c, h, w)));
+    const int64_t o = dx.off(n, c, h, w);
+    if (beta != 0.f) g += beta * dxp[o];
+    dxp[o] = g;
+  }
+}
+
+__global__ void __launch_bounds__(256) gen_losses_kernel(es_gen_loss_t p, const float* fo, const float* l1,
+                                                         const float* l2, const float* n1, const float* n2,
+                                                         const float* sd, const float* s, const float* inten,
+                                                         const float* coord, const float* pos, const float* wp,
+                                                         float* out, float* dfo, float* dl1, float* dl2,
+                                                         float* dcoord, float* coef) {
+  __shared__ float sh[8];
+  __shared__ float sdiv[4096];  // div_j (n <= 4096 checked on host)
+  const int n = p.n;
+  const float w = wp[0];
+  const float fn = (float)n;
+  // gen hinge + sums of std
+  float sfo = 0.f, sstd = 0.f, ss = 0.f, sl1 = 0.f, saux = 0.f;
+  for (int b = threadIdx.x; b < n; b += blockDim.x) {
+    sfo += fo[b];
+    sstd += sd[b];
+    ss += s[b];
+    sl1 += fabsf(s[b] - inten[b]);
+    float adl = 0.f, adn = 0.f;
+    for (int k = 0; k < p.latent; ++k) adl += fabsf(l1[b * p.latent + k] - l2[b * p.latent + k]);
+    for (int k = 0; k < p.noise; ++k) adn += fabsf(n1[b * p.noise + k] - n2[b * p.noise + k]);
+    adl /= (float)p.latent;
+    adn /= (float)p.noise;
+    sdiv[b] = adl / (adn + 1e-5f);
+    for (int k = 0; k < 2; ++k) {
+      const float d = coord[b * 2 + k] - pos[b * 2 + k];
+      const float z = -2.f * d;
+      const float sp = z > 20.f ? z : log1pf(expf(z));
+      saux += d + sp - 0.69314718055994531f;
+    }
+  }
+  sfo = block_sum(sfo, sh);
+  sstd = block_sum(sstd, sh);
+  ss = block_sum(ss, sh);
+  sl1 = block_sum(sl1, sh);
+  saux = block_sum(saux, sh);
+  float sr = 0.f;
+  for (int b = threadIdx.x; b < n; b += blockDim.x) sr += 1.f / (sdiv[b] + 1e-5f);
+  sr = block_sum(sr, sh);
+  const float ms = sstd / fn;
+  const float smean = ss / fn;
+  float sq = 0.f;
+  for (int b = threadIdx.x; b < n; b += blockDim.x) { const float d = s[b] - smean; sq += d * d; }
+  sq = block_sum(sq, sh);
+  const float gen = -sfo / fn;
+  const float div = ms * (sstd * sr / (fn * fn)) * p.di_strength;
+  const float inl = sl1 / fn * p.in_strength;
+  const float aux = saux / (2.f * fn) * p.aux_strength;
+  // gradients (all scaled by w)
+  const float kdiv = -p.di_strength * ms * ms / fn * w;   // d/d div_j = kdiv / (div_j+eps)^2
+  for (int b = threadIdx.x; b < n; b += blockDim.x) {
+    dfo[b] = -w / fn;
+    coef[b] = w * p.in_strength / fn * signf_(s[b] - inten[b]);
+    float adn = 0.f;
+    for (int k = 0; k < p.noise; ++k) adn += fabsf(n1[b * p.noise + k] - n2[b * p.noise + k]);
+    adn /= (float)p.noise;
+    const float e = sdiv[b] + 1e-5f;
+    const float g = kdiv / (e * e) / (adn + 1e-5f) / (float)p.latent;
+    for (int k = 0; k < p.latent; ++k) {
+      const float sg = signf_(l1[b * p.latent + k] - l2[b * p.latent + k]);
+      dl1[b * p.latent + k] = g * sg;
+      dl2[b * p.latent + k] = -g * sg;
+    }
+    for (int k = 0; k < 2; ++k) {
+      const float d = coord[b * 2 + k] - pos[b * 2 + k];
+      const float z = -2.f * d;
+      const float spg = z > 20.f ? 1.f : 1.f / (1.f + expf(-z));   // softplus'(z) = sigmoid(z)
+      dcoord[b * 2 + k] = w * p.aux_strength / (2.f * fn) * (1.f - 2.f * spg);
+    }
+  }
+  if (threadIdx.x == 0) {
+    out[0] = (gen + div + inl + aux) * w;
+    out[1] = gen;
+    out[2] = div;
+    out[3] = inl;
+    out[4] = aux;
+    out[5] = n > 1 ? sqrtf(sq / (fn - 1.f)) : NAN;
+    out[6] = smean;
+    out[7] = w;
+  }
+}
+
+__global__ void router_gumbel_kernel(const float* logits, const float* expo, int B, int E, float tau, float* gates,
+                                     int32_t* idx, int32_t* counts) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float mx = -INFINITY;
+  for (int e = 0; e < E; ++e) {
+    const float z = (logits[b * E + e] + (-logf(expo[b * E + e]))) / tau;
+    mx = fmaxf(mx, z);
+  }
+  float sum = 0.f;
+  for (int e = 0; e < E; ++e) {
+    const float z = (logits[b * E + e] + (-logf(expo[b * E + e]))) / tau;
+    sum += expf(z - mx);
+  }
+  int best = 0;
+  float bv = -INFINITY;
+  for (int e = 0; e < E; ++e) {
+    const float z = (logits[b * E + e] + (-logf(expo[b * E + e]))) / tau;
+    const float gte = expf(z - mx) / sum;
+    gates[b * E + e] = gte;
+    if (gte > bv) { bv = gte; best = e; }
+  }
+  idx[b] = best;
+  if (counts) atomicAdd(&counts[best], 1);
+}
+
+__global__ void __launch_bounds__(256) router_alb_kernel(const float* gates, int B, int E, float tau, float coef,
+                                                         float* out, float* dlogits) {
+  __shared__ float sh[8];
+  __shared__ float gS[64];
+  float L = 0.f;
+  for (int e = 0; e < E; ++e) {
+    float s = 0.f;
+    for (int b = threadIdx.x; b < B; b += blockDim.x) s += gates[b * E + e];
+    s = block_sum(s, sh);
+    const float inv = 1.f / (s + 1e-6f);
+    const float ex = expf(inv);
+    L += ex;
+    if (threadIdx.x == 0) gS[e] = coef / (float)E * ex * (-inv * inv);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = coef * (L / (float)E);
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    float dot = 0.f;
+    for (int e = 0; e < E; ++e) dot += gates[b * E + e] * gS[e];
+    for (int e = 0; e < E; ++e) dlogits[b * E + e] = gates[b * E + e] * (gS[e] - dot) / tau;
+  }
+}
+}  // namespace
+
+extern "C" int es_hinge_d(const float* ro, const float* fo, int n, const float* w_ptr, float* out, float* dro,
+                          float* dfo, es_stream_t stream) {
+  ES_CHECK_ARG(n > 0, "hinge_d: n must be > 0");
+  hipLaunchKernelGGL(hinge_d_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, ro, fo, n, w_ptr, out, dro, dfo);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_image_expsum(const es_view_t* x, es_dtype_t dt, const void* xp, float* s, es_stream_t stream) {
+  hipLaunchKernelGGL(expsum_kernel, dim3(x->n), dim3(256), 0, (hipStream_t)stream, mkview(x), xp, dt == ES_BF16, s);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_image_expsum_bwd(const es_view_t* x, es_dtype_t dt, const void* xp, const float* coef,
+                                   const es_view_t* dx, void* dxp, float beta, es_stream_t stream) {
+  const int64_t total = (int64_t)x->n * x->c * x->h * x->w;
+  const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(expsum_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, mkview(x), xp,
+                     dt == ES_BF16, coef, mkview(dx), (float*)dxp, beta);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_gen_losses(const es_gen_loss_t* p, const float* fo, const float* l1, const float* l2,
+                             const float* n1, const float* n2, const float* std_, const float* s,
+                             const float* intensity, const float* coord, const float* pos, const float* w_ptr,
+                             float* out, float* dfo, float* dl1, float* dl2, float* dcoord, float* coef,
+                             es_stream_t stream) {
+  ES_CHECK_ARG(p->n > 0 && p->n <= 4096, "gen_losses: n=%d out of range (1..4096)", p->n);
+  hipLaunchKernelGGL(gen_losses_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, *p, fo, l1, l2, n1, n2, std_, s,
+                     intensity, coord, pos, w_ptr, out, dfo, dl1, dl2, dcoord, coef);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_router_gumbel(const float* logits, const float* expo, int B, int E, float tau, float* gates,
+                                int32_t* idx, int32_t* counts, es_stream_t stream) {
+  hipLaunchKernelGGL(router_gumbel_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, logits, expo,
+                     B, E, tau, gates, idx, counts);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_router_alb(const float* gates, int B, int E, float tau, float coef, float* out, float* dlogits,
+                             es_stream_t stream) {
+  ES_CHECK_ARG(E <= 64, "router_alb: E <= 64");
+  hipLaunchKernelGGL(router_alb_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, gates, B, E, tau, coef, out,
+                     dlogits);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}

@@ -1,0 +1,401 @@
+// Pooling, resampling, layout, spectral norm, Adam, RNG and the error/ABI plumbing.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "common.h"
+
+// ------------------------------------------------------------------------------------- errors
+static thread_local char g_err[512] = "";
+void es_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+extern "C" const char* es_last_error(void) { return g_err; }
+extern "C" int es_version(void) { return 1; }
+extern "C" int es_device_sync(void) {
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) { es_set_error("hipDeviceSynchronize: %s", hipGetErrorString(e)); return ES_ERR_HIP; }
+  return ES_OK;
+}
+
+namespace {
+struct View {
+  int n, c, h, w;
+  int64_t s[4];
+  __device__ __forceinline__ int64_t off(int in, int ic, int ih, int iw) const {
+    return in * s[0] + ic * s[1] + ih * s[2] + iw * s[3];
+  }
+};
+View mkview(const es_view_t* v) {
+  View r;
+  r.n = v->n; r.c = v->c; r.h = v->h; r.w = v->w;
+  for (int i = 0; i < 4; ++i) r.s[i] = v->s[i];
+  return r;
+}
+__device__ __forceinline__ float ldf(const void* p, int bf, int64_t i) {
+  return bf ? (float)((const bf16*)p)[i] : ((const float*)p)[i];
+}
+__device__ __forceinline__ void stf(void* p, int bf, int64_t i, float v) {
+  if (bf) ((bf16*)p)[i] = (bf16)v;
+  else ((float*)p)[i] = v;
+}
+__device__ __forceinline__ void decompose(const View& v, bool cl, int64_t e, int& n, int& c, int& h, int& w) {
+  if (cl) {
+    c = e % v.c; int64_t t = e / v.c; w = t % v.w; t /= v.w; h = t % v.h; n = t / v.h;
+  } else {
+    w = e % v.w; int64_t t = e / v.w; h = t % v.h; t /= v.h; c = t % v.c; n = t / v.c;
+  }
+}
+int grid_for(int64_t total) { return (int)std::min<int64_t>((total + 255) / 256, 8192); }
+#define GRID_STRIDE(e, total) \
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < (total); e += (int64_t)gridDim.x * blockDim.x)
+
+// ------------------------------------------------------------------------------------ max pool
+__global__ void maxpool_fwd_kernel(View x, const void* xp, int bf, int kh, int kw, int sh, int sw, View y,
+                                   void* yp, uint8_t* idx) {
+  const int64_t total = (int64_t)y.n * y.c * y.h * y.w;
+  const bool cl = y.s[1] == 1 && y.c > 1;
+  GRID_STRIDE(e, total) {
+    int n, c, h, w;
+    decompose(y, cl, e, n, c, h, w);
+    float best = -INFINITY;
+    int bi = 0;
+    for (int i = 0; i < kh; ++i)
+      for (int j = 0; j < kw; ++j) {
+        const float v = ldf(xp, bf, x.off(n, c, h * sh + i, w * sw + j));
+        if (v > best || (isnan(v) && !isnan(best))) { best = v; bi = i * kw + j; }
+      }
+    stf(yp, bf, y.off(n, c, h, w), best);
+    if (idx) idx[e] = (uint8_t)bi;
+  }
+}
+
+// gather form: every input position sums the output windows whose argmax it is
+__global__ void maxpool_bwd_kernel(View dy, const void* dyp, int bf, const uint8_t* idx, int kh, int kw, int sh,
+                                   int sw, View dx, void* dxp, float beta) {
+  const int64_t total = (int64_t)dx.n * dx.c * dx.h * dx.w;
+  const bool cl = dx.s[1] == 1 && dx.c > 1;
+  const bool ycl = dy.s[1] == 1 && dy.c > 1;
+  GRID_STRIDE(e, total) {
+    int n, c, h, w;
+    decompose(dx, cl, e, n, c, h, w);
+    float g = 0.f;
+    // output rows oh with oh*sh <= h < oh*sh + kh
+    const int oh0 = h >= kh ? (h - kh) / sh + 1 : 0, oh1 = min(dy.h - 1, h / sh);
+    const int ow0 = w >= kw ? (w - kw) / sw + 1 : 0, ow1 = min(dy.w - 1, w / sw);
+    for (int oh = oh0; oh <= oh1; ++oh)
+      for (int ow = ow0; ow <= ow1; ++ow) {
+        const int i = h - oh * sh, j = w - ow * sw;
+        if (i < 0 || i >= kh || j < 0 || j >= kw) continue;
+        // idx is stored in the dy view's element order (ycl)
+        const int64_t ye = ycl ? ((((int64_t)n * dy.h + oh) * dy.w + ow) * dy.c + c)
+                               : ((((int64_t)n * dy.c + c) * dy.h + oh) * dy.w + ow);
+        if (idx[ye] == i * kw + j) g += ldf(dyp, bf, dy.off(n, c, oh, ow));
+      }
+    const int64_t o = dx.off(n, c, h, w);
+    if (beta != 0.f) g += beta * ldf(dxp, bf, o);
+    stf(dxp, bf, o, g);
+  }
+}
+
+// ----------------------------------------------------------------------------- upsample bwd
+__global__ void upsample_bwd_kernel(View du, const void* dup, int ubf, const int32_t* hs, const int32_t* hc,
+                                    const int32_t* ws, const int32_t* wc, View dx, void* dxp, int xbf, float beta) {
+  const int64_t total = (int64_t)dx.n * dx.c * dx.h * dx.w;
+  const bool cl = dx.s[1] == 1 && dx.c > 1;
+  GRID_STRIDE(e, total) {
+    int n, c, h, w;
+    decompose(dx, cl, e, n, c, h, w);
+    float g = 0.f;
+    const int h0 = hs[h], w0 = ws[w];
+    for (int i = 0; i < hc[h]; ++i)
+      for (int j = 0; j < wc[w]; ++j) g += ldf(dup, ubf, du.off(n, c, h0 + i, w0 + j));
+    const int64_t o = dx.off(n, c, h, w);
+    if (beta != 0.f) g += beta * ldf(dxp, xbf, o);
+    stf(dxp, xbf, o, g);
+  }
+}
+
+// ------------------------------------------------------------------------------------- copy
+__global__ void copy_kernel(View x, const void* xp, int xbf, View y, void* yp, int ybf, float alpha, float beta) {
+  const int64_t total = (int64_t)x.n * x.c * x.h * x.w;
+  const bool cl = y.s[1] == 1 && y.c > 1;
+  GRID_STRIDE(e, total) {
+    int n, c, h, w;
+    decompose(y, cl, e, n, c, h, w);
+    float v = alpha * ldf(xp, xbf, x.off(n, c, h, w));
+    const int64_t o = y.off(n, c, h, w);
+    if (beta != 0.f) v += beta * ldf(yp, ybf, o);
+    stf(yp, ybf, o, v);
+  }
+}
+
+// ------------------------------------------------------------------------------- avg pool
+__global__ void avgpool_fwd_kernel(View x, const void* xp, int bf, View y, void* yp) {
+  // one wave per (n, c)
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  if (wave >= x.n * x.c) return;
+  const int n = wave / x.c, c = wave % x.c;
+  const int hw = x.h * x.w;
+  float s = 0.f;
+  for (int i = lane; i < hw; i += 64) s += ldf(xp, bf, x.off(n, c, i / x.w, i % x.w));
+  s = wave_sum(s);
+  if (lane == 0) ((float*)yp)[y.off(n, c, 0, 0)] = s / (float)hw;
+}
+__global__ void avgpool_bwd_kernel(View dy, const float* dyp, View dx, void* dxp, int bf, float beta) {
+  const int64_t total = (int64_t)dx.n * dx.c * dx.h * dx.w;
+  const bool cl = dx.s[1] == 1 && dx.c > 1;
+  const float inv = 1.f / (float)(dx.h * dx.w);
+  GRID_STRIDE(e, total) {
+    int n, c, h, w;
+    decompose(dx, cl, e, n, c, h, w);
+    float g = dyp[dy.off(n, c, 0, 0)] * inv;
+    const int64_t o = dx.off(n, c, h, w);
+    if (beta != 0.f) g += beta * ldf(dxp, bf, o);
+    stf(dxp, bf, o, g);
+  }
+}
+
+__global__ void gather_rows_kernel(const float* src, int64_t sld, const int32_t* idx, int rows, int cols,
+                                   float* dst, int64_t dld) {
+  const int64_t total = (int64_t)rows * cols;
+  GRID_STRIDE(e, total) {
+    const int r = e / cols, c = e % cols;
+    const int sr = idx ? idx[r] : r;
+    dst[r * dld + c] = src[sr * sld + c];
+  }
+}
+
+// --------------------------------------------------------------------------- spectral norm
+// One block.  v = normalize(W^T u); u = normalize(W v); sigma = u . (W v)
+// (torch.nn.utils.spectral_norm.SpectralNorm.compute_weight, eps = 1e-12)
+__global__ void __launch_bounds__(1024) sn_power_kernel(const float* w, int h, int wd, float* u, float* v,
+                                                        float* sigma, int update, float* scratch) {
+  __shared__ float sh[16];
+  float* wv = scratch;       // [h]
+  float* vt = scratch + h;   // [wd]
+  if (update) {
+    // t = W^T u
+    float ss = 0.f;
+    for (int j = threadIdx.x; j < wd; j += blockDim.x) {
+      float t = 0.f;
+      for (int i = 0; i < h; ++i) t += w[(int64_t)i * wd + j] * u[i];
+      vt[j] = t;
+      ss += t * t;
+    }
+    const float nv = fmaxf(sqrtf(block_sum(ss, sh)), 1e-12f);
+    for (int j = threadIdx.x; j < wd; j += blockDim.x) v[j] = vt[j] / nv;
+    __syncthreads();
+  }
+  // s = W v
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int i = wid; i < h; i += nw) {
+    float t = 0.f;
+    for (int j = lane; j < wd; j += 64) t += w[(int64_t)i * wd + j] * v[j];
+    t = wave_sum(t);
+    if (lane == 0) wv[i] = t;
+  }
+  __syncthreads();
+  if (update) {
+    float ss = 0.f;
+    for (int i = threadIdx.x; i < h; i += blockDim.x) ss += wv[i] * wv[i];
+    const float nu = fmaxf(sqrtf(block_sum(ss, sh)), 1e-12f);
+    for (int i = threadIdx.x; i < h; i += blockDim.x) u[i] = wv[i] / nu;
+    __syncthreads();
+  }
+  float d = 0.f;
+  for (int i = threadIdx.x; i < h; i += blockDim.x) d += u[i] * wv[i];
+  d = block_sum(d, sh);
+  if (threadIdx.x == 0) sigma[0] = d;
+}
+
+// dW_orig = beta*dW + G/s - (<G,W>/s^2) u v^T
+__global__ void __launch_bounds__(1024) sn_bwd_kernel(const float* w, const float* g, int h, int wd,
+                                                      const float* u, const float* v, const float* sigma,
+                                                      float* dw, float beta) {
+  __shared__ float sh[16];
+  const int64_t n = (int64_t)h * wd;
+  float d = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) d += g[i] * w[i];
+  d = block_sum(d, sh);
+  const float s = sigma[0];
+  const float c = d / (s * s);
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const int r = i / wd, col = i % wd;
+    const float val = g[i] / s - c * u[r] * v[col];
+    dw[i] = (beta != 0.f ? beta * dw[i] : 0.f) + val;
+  }
+}
+
+// ----------------------------------------------------------------------------------- Adam
+// torch.optim.Adam (single tensor): m.lerp_(g, 1-b1); v = b2*v + (1-b2)*g*g;
+// p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
+                            float step_size, float bc2_sqrt, float gscale) {
+  GRID_STRIDE(i, n) {
+    const float gi = g[i] * gscale;
+    float mi = m[i];
+    mi = mi + (1.f - b1) * (gi - mi);
+    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    p[i] = p[i] - step_size * (mi / (sqrtf(vi) / bc2_sqrt + eps));
+  }
+}
+
+// ------------------------------------------------------------------------------------ RNG
+__global__ void randn_kernel(float* out, int64_t n, uint64_t seed, uint32_t sid) {
+  // Box-Muller on pairs: counter = pair index
+  const int64_t pairs = (n + 1) / 2;
+  GRID_STRIDE(i, pairs) {
+    u32x4 r = philox4x32_10((uint32_t)i, (uint32_t)(i >> 32), sid, 0x5EED0001u, (uint32_t)seed,
+                            (uint32_t)(seed >> 32));
+    const float u1 = ((r.x >> 8) + 1) * (1.f / 16777217.f);   // (0, 1]
+    const float u2 = (r.y >> 8) * (1.f / 16777216.f);
+    const float rad = sqrtf(-2.f * logf(u1));
+    float s, c;
+    sincosf(6.2831853071795864f * u2, &s, &c);
+    out[2 * i] = rad * c;
+    if (2 * i + 1 < n) out[2 * i + 1] = rad * s;
+  }
+}
+__global__ void rand_exp_kernel(float* out, int64_t n, uint64_t seed, uint32_t sid) {
+  GRID_STRIDE(i, n) {
+    u32x4 r = philox4x32_10((uint32_t)i, (uint32_t)(i >> 32), sid, 0x5EED0002u, (uint32_t)seed,
+                            (uint32_t)(seed >> 32));
+    const float u = ((r.x >> 8) + 1) * (1.f / 16777217.f);
+    out[i] = -logf(u);
+  }
+}
+__global__ void dropout_mask_kernel(uint8_t* out, int64_t n, es_dropout_t d) {
+  GRID_STRIDE(i, n) out[i] = dropout_keep(d, (uint64_t)i) ? 1 : 0;
+}
+}  // namespace
+
+// ============================================================================= C ABI
+extern "C" int es_maxpool_fwd(const es_view_t* x, es_dtype_t dt, const void* xp, int kh, int kw, int sh,
+                              int sw, const es_view_t* y, void* yp, uint8_t* idx, es_stream_t stream) {
+  ES_CHECK_ARG(y->h == (x->h - kh) / sh + 1 && y->w == (x->w - kw) / sw + 1, "maxpool: output shape");
+  const int64_t total = (int64_t)y->n * y->c * y->h * y->w;
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
+                     mkview(x), xp, dt == ES_BF16, kh, kw, sh, sw, mkview(y), yp, idx);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_maxpool_bwd(const es_view_t* dy, es_dtype_t dt, const void* dyp, const uint8_t* idx, int kh,
+                              int kw, int sh, int sw, const es_view_t* dx, void* dxp, float beta,
+                              es_stream_t stream) {
+  const int64_t total = (int64_t)dx->n * dx->c * dx->h * dx->w;
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
+                     mkview(dy), dyp, dt == ES_BF16, idx, kh, kw, sh, sw, mkview(dx), dxp, beta);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_upsample_bwd(const es_view_t* dxu, es_dtype_t dt, const void* dxup, const int32_t* hstart,
+                               const int32_t* hcount, const int32_t* wstart, const int32_t* wcount,
+                               const es_view_t* dx, es_dtype_t dxdt, void* dxp, float beta, es_stream_t stream) {
+  const int64_t total = (int64_t)dx->n * dx->c * dx->h * dx->w;
+  hipLaunchKernelGGL(upsample_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
+                     mkview(dxu), dxup, dt == ES_BF16, hstart, hcount, wstart, wcount, mkview(dx), dxp,
+                     dxdt == ES_BF16, beta);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_copy(const es_view_t* x, es_dtype_t xdt, const void* xp, const es_view_t* y, es_dtype_t ydt,
+                       void* yp, float alpha, float beta, es_stream_t stream) {
+  ES_CHECK_ARG(x->n == y->n && x->c == y->c && x->h == y->h && x->w == y->w, "copy: shape mismatch");
+  const int64_t total = (int64_t)x->n * x->c * x->h * x->w;
+  if (total == 0) return ES_OK;
+  hipLaunchKernelGGL(copy_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, mkview(x), xp,
+                     xdt == ES_BF16, mkview(y), yp, ydt == ES_BF16, alpha, beta);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_avgpool_fwd(const es_view_t* x, es_dtype_t dt, const void* xp, const es_view_t* y, void* yp,
+                              es_stream_t stream) {
+  const int waves = x->n * x->c;
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((waves + 3) / 4), dim3(256), 0, (hipStream_t)stream, mkview(x), xp,
+                     dt == ES_BF16, mkview(y), yp);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_avgpool_bwd(const es_view_t* dy, const void* dyp, const es_view_t* dx, es_dtype_t dxdt,
+                              void* dxp, float beta, es_stream_t stream) {
+  const int64_t total = (int64_t)dx->n * dx->c * dx->h * dx->w;
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, mkview(dy),
+                     (const float*)dyp, mkview(dx), dxp, dxdt == ES_BF16, beta);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_gather_rows(const float* src, int64_t src_ld, const int32_t* idx, int rows, int cols, float* dst,
+                              int64_t dst_ld, es_stream_t stream) {
+  const int64_t total = (int64_t)rows * cols;
+  if (total == 0) return ES_OK;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, src, src_ld,
+                     idx, rows, cols, dst, dst_ld);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_sn_power_iter(const float* w, int h, int wd, float* u, float* v, float* sigma, int update,
+                                es_stream_t stream) {
+  // scratch lives after sigma[0] in the caller's buffer: sigma must have 1 + h + wd floats
+  hipLaunchKernelGGL(sn_power_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, w, h, wd, u, v, sigma, update,
+                     sigma + 1);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_sn_bwd(const float* w, const float* g, int h, int wd, const float* u, const float* v,
+                         const float* sigma, float* dw_orig, float beta, es_stream_t stream) {
+  hipLaunchKernelGGL(sn_bwd_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, w, g, h, wd, u, v, sigma,
+                     dw_orig, beta);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                       float beta2, float eps, int step, float grad_scale, es_stream_t stream) {
+  ES_CHECK_ARG(step >= 1, "adam: step must be >= 1");
+  const double bc1 = 1.0 - pow((double)beta1, step);
+  const double bc2 = 1.0 - pow((double)beta2, step);
+  const float step_size = (float)((double)lr / bc1);
+  const float bc2_sqrt = (float)sqrt(bc2);
+  if (n == 0) return ES_OK;
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr, beta1,
+                     beta2, eps, step_size, bc2_sqrt, grad_scale);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_randn(float* out, int64_t n, uint64_t seed, uint32_t stream_id, es_stream_t stream) {
+  if (n == 0) return ES_OK;
+  hipLaunchKernelGGL(randn_kernel, dim3(grid_for((n + 1) / 2)), dim3(256), 0, (hipStream_t)stream, out, n, seed,
+                     stream_id);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_rand_exponential(float* out, int64_t n, uint64_t seed, uint32_t stream_id, es_stream_t stream) {
+  if (n == 0) return ES_OK;
+  hipLaunchKernelGGL(rand_exp_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, out, n, seed,
+                     stream_id);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_dropout_mask(uint8_t* out, int64_t n, const es_dropout_t* d, es_stream_t stream) {
+  if (n == 0) return ES_OK;
+  hipLaunchKernelGGL(dropout_mask_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, out, n, *d);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}

@@ -1,0 +1,486 @@
+// Normalisation (BatchNorm / GroupNorm / LayerNorm) + dropout + activation, forward and backward.
+//
+// Replaces aten::native_batch_norm(+_backward) (neutron/generator.py:13,19,26,31,35;
+// neutron/aux_reg.py:15,23,31,39,47), native_group_norm(+_backward) (neutron/discriminator.py:13,
+// 18; proton/generator.py:28,34,39; proton/discriminator.py:123,128; proton/aux_reg.py:22,48-53),
+// native_layer_norm(+_backward) (neutron/discriminator.py:28,34; proton/generator.py:15,20;
+// proton/discriminator.py:135,141; proton/aux_reg.py:21,25), bernoulli_/mul of nn.Dropout and
+// leaky_relu / relu (+ backward), fused into: stats reduction -> one elementwise pass forward,
+// and reductions -> one elementwise pass backward.  The dropout mask is never stored: it is
+// regenerated from (seed, stream, NCHW-logical index) by Philox (common.h).
+//
+// Reduction shapes
+//   colred : per channel c over (n,h,w)   — BN stats, BN backward sums, GN/LN dgamma/dbeta,
+//            bias gradients.  Block = 64 channels x 4 row lanes, rows split over blockIdx.y,
+//            partials merged by a finalize kernel (Chan's parallel variance for stats).
+//   segred : per stats group (n, g) over (c in g, h, w) — GN/LN stats and backward sums.  One
+//            block per group, two passes (mean, then centred sum of squares).
+#include "common.h"
+
+namespace {
+
+struct View {
+  int n, c, h, w;
+  int64_t s[4];
+  __device__ __forceinline__ int64_t off(int in, int ic, int ih, int iw) const {
+    return in * s[0] + ic * s[1] + ih * s[2] + iw * s[3];
+  }
+};
+View mkview(const es_view_t* v) {
+  View r;
+  r.n = v->n; r.c = v->c; r.h = v->h; r.w = v->w;
+  for (int i = 0; i < 4; ++i) r.s[i] = v->s[i];
+  return r;
+}
+
+__device__ __forceinline__ float ldf(const void* p, int bf, int64_t i) {
+  return bf ? (float)((const bf16*)p)[i] : ((const float*)p)[i];
+}
+__device__ __forceinline__ void stf(void* p, int bf, int64_t i, float v) {
+  if (bf) ((bf16*)p)[i] = (bf16)v;
+  else ((float*)p)[i] = v;
+}
+
+struct Norm {
+  int kind, groups, cg;
+  const float *mean, *invstd, *gamma, *beta;
+  __device__ __forceinline__ int group(int n, int c) const {
+    return kind == ES_NORM_BN ? c : (kind == ES_NORM_GN ? n * groups + c / cg : n);
+  }
+  __device__ __forceinline__ float xhat(int n, int c, float x) const {
+    if (kind == ES_NORM_NONE) return x;
+    const int g = group(n, c);
+    return (x - mean[g]) * invstd[g];
+  }
+  // LN gamma is indexed by feature; LN views have h = w = 1 so feature == c.
+  __device__ __forceinline__ float gam(int c) const { return gamma ? gamma[c] : 1.f; }
+  __device__ __forceinline__ float bet(int c) const { return beta ? beta[c] : 0.f; }
+};
+Norm mknorm(const es_norm_t* nm, int C) {
+  Norm r{};
+  if (!nm) { r.kind = ES_NORM_NONE; return r; }
+  r.kind = nm->kind; r.groups = nm->groups > 0 ? nm->groups : 1;
+  r.cg = C / r.groups;
+  r.mean = nm->mean; r.invstd = nm->invstd; r.gamma = nm->gamma; r.beta = nm->beta;
+  return r;
+}
+
+struct Chain {
+  es_dropout_t drop;
+  int dfirst, act;
+  float slope;
+  __device__ __forceinline__ float actf(float v) const {
+    return act == ES_ACT_RELU ? fmaxf(v, 0.f) : (act == ES_ACT_LRELU ? lrelu(v, slope) : v);
+  }
+  __device__ __forceinline__ float dact(float v) const {  // derivative evaluated at input v
+    return act == ES_ACT_RELU ? (v > 0.f ? 1.f : 0.f) : (act == ES_ACT_LRELU ? (v > 0.f ? 1.f : slope) : 1.f);
+  }
+  __device__ __forceinline__ float fwd(float y, uint64_t li) const {
+    if (!drop.enabled) return actf(y);
+    const bool keep = dropout_keep(drop, li);
+    if (dfirst) return actf(keep ? y * drop.scale : 0.f);
+    const float u = actf(y);
+    return keep ? u * drop.scale : 0.f;
+  }
+  // d out / d y given dout; `ref` (if has_ref) replaces the activation input for the derivative
+  __device__ __forceinline__ float bwd(float y, float dout, uint64_t li, bool has_ref, float ref) const {
+    if (!drop.enabled) return dout * dact(has_ref ? ref : y);
+    const bool keep = dropout_keep(drop, li);
+    if (!keep) return 0.f;
+    if (dfirst) {
+      const float u = y * drop.scale;
+      return dout * dact(has_ref ? ref : u) * drop.scale;
+    }
+    return dout * drop.scale * dact(has_ref ? ref : y);
+  }
+};
+Chain mkchain(const es_chain_t* ch) {
+  Chain c{};
+  if (ch) { c.drop = ch->drop; c.dfirst = ch->dropout_first; c.act = ch->act; c.slope = ch->slope; }
+  else { c.drop.enabled = 0; c.act = ES_ACT_NONE; }
+  return c;
+}
+
+__device__ __forceinline__ uint64_t logical_index(const View& v, int n, int c, int h, int w) {
+  return (((uint64_t)n * v.c + c) * v.h + h) * v.w + w;
+}
+
+// element e of the logical tensor -> (n,c,h,w); channels-last order when the view says so
+__device__ __forceinline__ void decompose(const View& v, bool cl, int64_t e, int& n, int& c, int& h, int& w) {
+  if (cl) {
+    c = e % v.c; int64_t t = e / v.c; w = t % v.w; t /= v.w; h = t % v.h; n = t / v.h;
+  } else {
+    w = e % v.w; int64_t t = e / v.w; h = t % v.h; t /= v.h; c = t % v.c; n = t / v.c;
+  }
+}
+
+// ============================================================================ colred
+enum { RED_STATS = 0, RED_BWD = 1, RED_SUM = 2 };
+
+struct BwdIn {   // everything needed to evaluate dnorm and xhat per element
+  View x; const void* xp; int xbf;
+  View dy; const void* dyp; int dybf;
+  View ref; const void* refp; int refbf;  // refp may be null
+  View add; const void* addp; int addbf;  // addend (fwd residual) may be null
+  Norm nm; Chain ch;
+};
+
+__device__ __forceinline__ void bwd_elem(const BwdIn& b, int n, int c, int h, int w, float& dnorm, float& xh) {
+  const float x = ldf(b.xp, b.xbf, b.x.off(n, c, h, w));
+  xh = b.nm.xhat(n, c, x);
+  float y = xh * b.nm.gam(c) + b.nm.bet(c);
+  if (b.addp) y += ldf(b.addp, b.addbf, b.add.off(n, c, h, w));
+  const float dout = ldf(b.dyp, b.dybf, b.dy.off(n, c, h, w));
+  const float ref = b.refp ? ldf(b.refp, b.refbf, b.ref.off(n, c, h, w)) : 0.f;
+  dnorm = b.ch.bwd(y, dout, logical_index(b.x, n, c, h, w), b.refp != nullptr, ref);
+}
+
+template <int RED>
+__global__ void __launch_bounds__(256) colred_kernel(BwdIn b, int64_t rows, int64_t rows_per_chunk, float* part) {
+  // part layout: [chunk][3][C]
+  const View& v = b.x;
+  const int C = v.c;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  const int64_t r0 = blockIdx.y * rows_per_chunk;
+  const int64_t r1 = min(rows, r0 + rows_per_chunk);
+  float cnt = 0.f, a = 0.f, m2 = 0.f;   // STATS: Welford (cnt, mean, M2); BWD/SUM: (., s1, s2)
+  if (c < C) {
+    // row r -> (n, h, w), w fastest
+    for (int64_t r = r0 + ty; r < r1; r += 4) {
+      const int w = r % v.w; const int64_t t = r / v.w; const int h = t % v.h; const int n = t / v.h;
+      if (RED == RED_STATS) {
+        const float x = ldf(b.xp, b.xbf, v.off(n, c, h, w));
+        cnt += 1.f;
+        const float d = x - a;
+        a += d / cnt;
+        m2 += d * (x - a);
+      } else if (RED == RED_SUM) {
+        a += ldf(b.xp, b.xbf, v.off(n, c, h, w));
+      } else {
+        float dn, xh;
+        bwd_elem(b, n, c, h, w, dn, xh);
+        a += dn;
+        m2 += dn * xh;
+      }
+    }
+  }
+  __shared__ float sh[3][4][64];
+  sh[0][ty][tx] = cnt; sh[1][ty][tx] = a; sh[2][ty][tx] = m2;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    if (RED == RED_STATS) {
+      float n_ = sh[0][0][tx], mu = sh[1][0][tx], M = sh[2][0][tx];
+      for (int k = 1; k < 4; ++k) {
+        const float nb = sh[0][k][tx];
+        if (nb == 0.f) continue;
+        const float mb = sh[1][k][tx], Mb = sh[2][k][tx];
+        const float nt = n_ + nb, dl = mb - mu;
+        mu += dl * nb / nt;
+        M += Mb + dl * dl * n_ * nb / nt;
+        n_ = nt;
+      }
+      cnt = n_; a = mu; m2 = M;
+    } else {
+      a = sh[1][0][tx] + sh[1][1][tx] + sh[1][2][tx] + sh[1][3][tx];
+      m2 = sh[2][0][tx] + sh[2][1][tx] + sh[2][2][tx] + sh[2][3][tx];
+    }
+    float* p = part + (int64_t)blockIdx.y * 3 * C;
+    p[c] = cnt; p[C + c] = a; p[2 * C + c] = m2;
+  }
+}
+
+// BN stats finalize: merge chunk partials -> mean/invstd, running stats (torch semantics)
+__global__ void bn_finalize_kernel(const float* part, int chunks, int C, float eps, float* mean,
+                                   float* invstd, float* rmean, float* rvar, float mom) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double n_ = 0.0, mu = 0.0, M = 0.0;
+  for (int k = 0; k < chunks; ++k) {
+    const float* p = part + (int64_t)k * 3 * C;
+    const double nb = p[c];
+    if (nb == 0.0) continue;
+    const double mb = p[C + c], Mb = p[2 * C + c];
+    const double nt = n_ + nb, dl = mb - mu;
+    mu += dl * nb / nt;
+    M += Mb + dl * dl * n_ * nb / nt;
+    n_ = nt;
+  }
+  const double var = M / n_;
+  mean[c] = (float)mu;
+  invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (rmean) rmean[c] = (1.f - mom) * rmean[c] + mom * (float)mu;
+  if (rvar) rvar[c] = (1.f - mom) * rvar[c] + mom * (float)(n_ > 1.0 ? M / (n_ - 1.0) : var);
+}
+
+// BN backward finalize: per channel A1 = gamma*s1/cnt, A2 = gamma*s2/cnt ; dgamma += s2, dbeta += s1
+__global__ void bn_bwd_finalize_kernel(const float* part, int chunks, int C, float cnt, const float* gamma,
+                                       float* a1, float* a2, float* dgamma, float* dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s1 = 0.f, s2 = 0.f;
+  for (int k = 0; k < chunks; ++k) {
+    const float* p = part + (int64_t)k * 3 * C;
+    s1 += p[C + c]; s2 += p[2 * C + c];
+  }
+  const float g = gamma ? gamma[c] : 1.f;
+  if (a1) { a1[c] = g * s1 / cnt; a2[c] = g * s2 / cnt; }
+  if (dgamma) dgamma[c] += s2;
+  if (dbeta) dbeta[c] += s1;
+}
+
+__global__ void sum_finalize_kernel(const float* part, int chunks, int C, float* out, float beta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int k = 0; k < chunks; ++k) s += part[(int64_t)k * 3 * C + C + c];
+  out[c] = (beta != 0.f ? beta * out[c] : 0.f) + s;
+}
+
+void colred_geometry(const View& v, int& cblocks, int& chunks, int64_t& rows, int64_t& per) {
+  rows = (int64_t)v.n * v.h * v.w;
+  cblocks = (v.c + 63) / 64;
+  int want = std::max(1, 1024 / cblocks);
+  want = (int)std::min<int64_t>(want, std::max<int64_t>(1, rows / 64));
+  per = (rows + want - 1) / want;
+  chunks = (int)((rows + per - 1) / per);
+}
+
+// ============================================================================ segred
+// one block per stats group; RED_STATS writes mean/invstd, RED_BWD writes A1/A2 (means over group)
+template <int RED>
+__global__ void __launch_bounds__(256) segred_kernel(BwdIn b, float eps, float* o1, float* o2) {
+  const View& v = b.x;
+  const int G = b.nm.kind == ES_NORM_GN ? b.nm.groups : 1;
+  const int cg = v.c / G;
+  const int n = blockIdx.x / G, g = blockIdx.x % G;
+  const int64_t cnt = (int64_t)cg * v.h * v.w;
+  const bool cl = v.s[1] == 1 && cg > 1;
+  __shared__ float sh[8];
+  auto coords = [&](int64_t j, int& c, int& h, int& w) {
+    if (cl) { c = g * cg + j % cg; const int64_t t = j / cg; w = t % v.w; h = t / v.w; }
+    else { w = j % v.w; const int64_t t = j / v.w; h = t % v.h; c = g * cg + t / v.h; }
+  };
+  if (RED == RED_STATS) {
+    float s = 0.f;
+    for (int64_t j = threadIdx.x; j < cnt; j += blockDim.x) {
+      int c, h, w; coords(j, c, h, w);
+      s += ldf(b.xp, b.xbf, v.off(n, c, h, w));
+    }
+    const float mu = block_sum(s, sh) / (float)cnt;
+    float q = 0.f;
+    for (int64_t j = threadIdx.x; j < cnt; j += blockDim.x) {
+      int c, h, w; coords(j, c, h, w);
+      const float d = ldf(b.xp, b.xbf, v.off(n, c, h, w)) - mu;
+      q += d * d;
+    }
+    const float var = block_sum(q, sh) / (float)cnt;
+    if (threadIdx.x == 0) { o1[blockIdx.x] = mu; o2[blockIdx.x] = rsqrtf(var + eps); }
+  } else {
+    float s1 = 0.f, s2 = 0.f;
+    for (int64_t j = threadIdx.x; j < cnt; j += blockDim.x) {
+      int c, h, w; coords(j, c, h, w);
+      float dn, xh;
+      bwd_elem(b, n, c, h, w, dn, xh);
+      const float dxh = dn * b.nm.gam(c);
+      s1 += dxh; s2 += dxh * xh;
+    }
+    s1 = block_sum(s1, sh);
+    s2 = block_sum(s2, sh);
+    if (threadIdx.x == 0) { o1[blockIdx.x] = s1 / (float)cnt; o2[blockIdx.x] = s2 / (float)cnt; }
+  }
+}
+
+// ============================================================================ elementwise
+struct FwdArgs {
+  View x; const void* xp; int xbf;
+  View add; const void* addp; int addbf;
+  View y; void* yp; int ybf;
+  Norm nm; Chain ch;
+};
+
+__global__ void __launch_bounds__(256) norm_fwd_kernel(FwdArgs a) {
+  const int64_t total = (int64_t)a.x.n * a.x.c * a.x.h * a.x.w;
+  const bool cl = a.x.s[1] == 1 && a.x.c > 1;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    int n, c, h, w;
+    decompose(a.x, cl, e, n, c, h, w);
+    const float x = ldf(a.xp, a.xbf, a.x.off(n, c, h, w));
+    float y = a.nm.kind == ES_NORM_NONE ? x : a.nm.xhat(n, c, x) * a.nm.gam(c) + a.nm.bet(c);
+    if (a.addp) y += ldf(a.addp, a.addbf, a.add.off(n, c, h, w));
+    stf(a.yp, a.ybf, a.y.off(n, c, h, w), a.ch.fwd(y, logical_index(a.x, n, c, h, w)));
+  }
+}
+
+struct BwdApply {
+  BwdIn b;
+  View dx; void* dxp; int dxbf;
+  const float* a1; const float* a2;  // per stats group
+  float beta;
+};
+
+__global__ void __launch_bounds__(256) norm_bwd_apply_kernel(BwdApply a) {
+  const View& v = a.b.x;
+  const int64_t total = (int64_t)v.n * v.c * v.h * v.w;
+  const bool cl = v.s[1] == 1 && v.c > 1;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    int n, c, h, w;
+    decompose(v, cl, e, n, c, h, w);
+    float dn, xh;
+    bwd_elem(a.b, n, c, h, w, dn, xh);
+    float dx;
+    if (a.b.nm.kind == ES_NORM_NONE) {
+      dx = dn;
+    } else {
+      const int g = a.b.nm.group(n, c);
+      dx = a.b.nm.invstd[g] * (dn * a.b.nm.gam(c) - a.a1[g] - xh * a.a2[g]);
+    }
+    const int64_t o = a.dx.off(n, c, h, w);
+    if (a.beta != 0.f) dx += a.beta * ldf(a.dxp, a.dxbf, o);
+    stf(a.dxp, a.dxbf, o, dx);
+  }
+}
+
+int grid_for(int64_t total) { return (int)std::min<int64_t>((total + 255) / 256, 8192); }
+
+BwdIn mk_bwdin(const es_view_t* x, es_dtype_t xdt, const void* xp, const es_norm_t* nm,
+               const es_chain_t* ch) {
+  BwdIn b{};
+  b.x = mkview(x); b.xp = xp; b.xbf = xdt == ES_BF16;
+  b.nm = mknorm(nm, x->c); b.ch = mkchain(ch);
+  b.refp = nullptr; b.addp = nullptr; b.dyp = nullptr;
+  return b;
+}
+
+int64_t stats_groups(const es_view_t* x, int kind, int groups) {
+  if (kind == ES_NORM_BN) return x->c;
+  if (kind == ES_NORM_GN) return (int64_t)x->n * groups;
+  return x->n;
+}
+
+}  // namespace
+
+// ================================================================================ C ABI
+extern "C" int64_t es_norm_stats_ws_bytes(const es_view_t* x, int kind, int groups) {
+  (void)groups;
+  if (kind != ES_NORM_BN) return 0;
+  View v = mkview(x);
+  int cb, chunks; int64_t rows, per;
+  colred_geometry(v, cb, chunks, rows, per);
+  return (int64_t)chunks * 3 * v.c * sizeof(float);
+}
+
+extern "C" int es_norm_stats(const es_view_t* x, es_dtype_t xdt, const void* xp, int kind,
+                             int groups, float eps, float* mean, float* invstd, float* running_mean,
+                             float* running_var, float momentum, void* ws, es_stream_t stream) {
+  hipStream_t st = (hipStream_t)stream;
+  ES_CHECK_ARG(kind == ES_NORM_BN || kind == ES_NORM_GN || kind == ES_NORM_LN, "norm_stats: kind %d", kind);
+  ES_CHECK_ARG(kind != ES_NORM_GN || (groups > 0 && x->c % groups == 0), "norm_stats: groups");
+  ES_CHECK_ARG(kind != ES_NORM_LN || (x->h == 1 && x->w == 1), "norm_stats: LN needs (N,F,1,1) views");
+  es_norm_t nm{kind, groups, nullptr, nullptr, nullptr, nullptr};
+  BwdIn b = mk_bwdin(x, xdt, xp, &nm, nullptr);
+  if (kind == ES_NORM_BN) {
+    int cb, chunks; int64_t rows, per;
+    colred_geometry(b.x, cb, chunks, rows, per);
+    ES_CHECK_ARG(ws != nullptr, "norm_stats: BN needs workspace");
+    hipLaunchKernelGGL(colred_kernel<RED_STATS>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, (float*)ws);
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)ws,
+                       chunks, x->c, eps, mean, invstd, running_mean, running_var, momentum);
+  } else {
+    const int64_t ng = stats_groups(x, kind, groups);
+    hipLaunchKernelGGL(segred_kernel<RED_STATS>, dim3((unsigned)ng), dim3(256), 0, st, b, eps, mean, invstd);
+  }
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_norm_act_fwd(const es_view_t* x, es_dtype_t xdt, const es_norm_t* nm,
+                               const es_chain_t* ch, const es_view_t* addend, es_dtype_t adt,
+                               const void* addend_ptr, const void* xp, const es_view_t* y,
+                               es_dtype_t ydt, void* yp, es_stream_t stream) {
+  ES_CHECK_ARG(x->n == y->n && x->c == y->c && x->h == y->h && x->w == y->w, "norm_act_fwd: shape");
+  FwdArgs a{};
+  a.x = mkview(x); a.xp = xp; a.xbf = xdt == ES_BF16;
+  a.y = mkview(y); a.yp = yp; a.ybf = ydt == ES_BF16;
+  a.addp = addend_ptr;
+  if (addend_ptr) { a.add = mkview(addend); a.addbf = adt == ES_BF16; }
+  a.nm = mknorm(nm, x->c); a.ch = mkchain(ch);
+  const int64_t total = (int64_t)x->n * x->c * x->h * x->w;
+  hipLaunchKernelGGL(norm_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, a);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_act_fwd(const es_view_t* x, es_dtype_t xdt, const void* xp, const es_chain_t* ch,
+                          const es_view_t* y, es_dtype_t ydt, void* yp, es_stream_t stream) {
+  return es_norm_act_fwd(x, xdt, nullptr, ch, nullptr, ES_F32, nullptr, xp, y, ydt, yp, stream);
+}
+
+extern "C" int64_t es_norm_bwd_ws_bytes(const es_view_t* x, int kind, int groups) {
+  View v = mkview(x);
+  int cb, chunks; int64_t rows, per;
+  colred_geometry(v, cb, chunks, rows, per);
+  const int64_t part = (int64_t)chunks * 3 * v.c * sizeof(float);
+  const int64_t ng = kind == ES_NORM_NONE ? 0 : stats_groups(x, kind, groups);
+  return part + 2 * ng * (int64_t)sizeof(float) + 256;
+}
+
+extern "C" int es_norm_act_bwd(const es_view_t* x, es_dtype_t xdt, const void* xp, const es_norm_t* nm,
+                               const es_chain_t* ch, const es_view_t* dy, es_dtype_t dydt,
+                               const void* dyp, const es_view_t* act_ref, es_dtype_t rdt,
+                               const void* refp, const es_view_t* dx, es_dtype_t dxdt, void* dxp,
+                               float beta, float* dgamma, float* dbeta, void* ws, es_stream_t stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int kind = nm ? nm->kind : ES_NORM_NONE;
+  const int groups = nm ? nm->groups : 1;
+  ES_CHECK_ARG(kind != ES_NORM_LN || (x->h == 1 && x->w == 1), "norm_act_bwd: LN needs (N,F,1,1) views");
+  BwdIn b = mk_bwdin(x, xdt, xp, nm, ch);
+  b.dy = mkview(dy); b.dyp = dyp; b.dybf = dydt == ES_BF16;
+  if (refp) { b.ref = mkview(act_ref); b.refp = refp; b.refbf = rdt == ES_BF16; }
+  BwdApply ap{};
+  ap.b = b; ap.dx = mkview(dx); ap.dxp = dxp; ap.dxbf = dxdt == ES_BF16; ap.beta = beta;
+  const int64_t total = (int64_t)x->n * x->c * x->h * x->w;
+  int cb, chunks; int64_t rows, per;
+  colred_geometry(b.x, cb, chunks, rows, per);
+  float* part = (float*)ws;
+  float* g1 = part + (int64_t)chunks * 3 * x->c;
+  const int64_t ng = kind == ES_NORM_NONE ? 0 : stats_groups(x, kind, groups);
+  float* g2 = g1 + ng;
+  if (kind == ES_NORM_BN) {
+    hipLaunchKernelGGL(colred_kernel<RED_BWD>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, part);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)part,
+                       chunks, x->c, (float)rows, nm->gamma, g1, g2, dgamma, dbeta);
+    ap.a1 = g1; ap.a2 = g2;
+  } else if (kind == ES_NORM_GN || kind == ES_NORM_LN) {
+    hipLaunchKernelGGL(segred_kernel<RED_BWD>, dim3((unsigned)ng), dim3(256), 0, st, b, 0.f, g1, g2);
+    if (dgamma || dbeta) {
+      hipLaunchKernelGGL(colred_kernel<RED_BWD>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, part);
+      hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)part,
+                         chunks, x->c, (float)rows, nullptr, (float*)nullptr, (float*)nullptr, dgamma, dbeta);
+    }
+    ap.a1 = g1; ap.a2 = g2;
+  }
+  if (dxp) hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(grid_for(total)), dim3(256), 0, st, ap);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int64_t es_channel_sum_ws_bytes(const es_view_t* x) {
+  View v = mkview(x);
+  int cb, chunks; int64_t rows, per;
+  colred_geometry(v, cb, chunks, rows, per);
+  return (int64_t)chunks * 3 * v.c * sizeof(float);
+}
+
+extern "C" int es_channel_sum(const es_view_t* x, es_dtype_t xdt, const void* xp, float* out,
+                              float beta, void* ws, es_stream_t stream) {
+  hipStream_t st = (hipStream_t)stream;
+  BwdIn b = mk_bwdin(x, xdt, xp, nullptr, nullptr);
+  int cb, chunks; int64_t rows, per;
+  colred_geometry(b.x, cb, chunks, rows, per);
+  hipLaunchKernelGGL(colred_kernel<RED_SUM>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, (float*)ws);
+  hipLaunchKernelGGL(sum_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)ws,
+                     chunks, x->c, out, beta);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}

@@ -1,0 +1,180 @@
+"""ctypes binding of libexpertsim_hip.so (the C ABI in include/expertsim_hip.h).
+
+The library is built in-tree (``csrc/Makefile`` -> ``expertsim/_lib/libexpertsim_hip.so``).  There
+is no fallback: if the library or a HIP device is missing, every op raises.  Tensors are torch
+tensors used purely as device memory; all arithmetic happens in the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libexpertsim_hip.so")
+_lib = None
+
+ES_F32, ES_BF16 = 0, 1
+ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
+NORM_NONE, NORM_BN, NORM_GN, NORM_LN = 0, 1, 2, 3
+
+
+class View(C.Structure):
+    _fields_ = [("n", C.c_int), ("c", C.c_int), ("h", C.c_int), ("w", C.c_int), ("s", C.c_int64 * 4)]
+
+
+class Dropout(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("stream", C.c_uint32), ("threshold", C.c_uint32),
+                ("scale", C.c_float), ("enabled", C.c_int)]
+
+
+class ConvDesc(C.Structure):
+    _fields_ = [("N", C.c_int), ("C", C.c_int), ("H", C.c_int), ("W", C.c_int), ("Hu", C.c_int),
+                ("Wu", C.c_int), ("K", C.c_int), ("P", C.c_int), ("Q", C.c_int), ("R", C.c_int),
+                ("S", C.c_int), ("stride", C.c_int), ("pad", C.c_int), ("hmap", C.c_void_p),
+                ("wmap", C.c_void_p)]
+
+
+class Norm(C.Structure):
+    _fields_ = [("kind", C.c_int), ("groups", C.c_int), ("mean", C.c_void_p),
+                ("invstd", C.c_void_p), ("gamma", C.c_void_p), ("beta", C.c_void_p)]
+
+
+class Chain(C.Structure):
+    _fields_ = [("drop", Dropout), ("dropout_first", C.c_int), ("act", C.c_int), ("slope", C.c_float)]
+
+
+class GenLoss(C.Structure):
+    _fields_ = [("n", C.c_int), ("latent", C.c_int), ("noise", C.c_int), ("di_strength", C.c_float),
+                ("in_strength", C.c_float), ("aux_strength", C.c_float)]
+
+
+P = C.c_void_p
+I64 = C.c_int64
+_SIGS = {
+    "es_last_error": (C.c_char_p, []),
+    "es_version": (C.c_int, []),
+    "es_device_sync": (C.c_int, []),
+    "es_conv2d_fwd": (C.c_int, [P, C.c_int, P, P, P, P, P, C.c_int, P, P]),
+    "es_conv2d_dgrad": (C.c_int, [P, C.c_int, P, P, P, P, C.c_int, P, C.c_float, P]),
+    "es_conv2d_wgrad": (C.c_int, [P, C.c_int, P, P, P, P, P, P]),
+    "es_pack_conv_weight": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, C.c_int, P]),
+    "es_unpack_conv_grad": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, C.c_float, P]),
+    "es_norm_stats_ws_bytes": (I64, [P, C.c_int, C.c_int]),
+    "es_norm_stats": (C.c_int, [P, C.c_int, P, C.c_int, C.c_int, C.c_float, P, P, P, P, C.c_float, P, P]),
+    "es_norm_act_fwd": (C.c_int, [P, C.c_int, P, P, P, C.c_int, P, P, P, C.c_int, P, P]),
+    "es_norm_bwd_ws_bytes": (I64, [P, C.c_int, C.c_int]),
+    "es_norm_act_bwd": (C.c_int, [P, C.c_int, P, P, P, P, C.c_int, P, P, C.c_int, P, P, C.c_int, P,
+                                  C.c_float, P, P, P, P]),
+    "es_act_fwd": (C.c_int, [P, C.c_int, P, P, P, C.c_int, P, P]),
+    "es_channel_sum_ws_bytes": (I64, [P]),
+    "es_channel_sum": (C.c_int, [P, C.c_int, P, P, C.c_float, P, P]),
+    "es_maxpool_fwd": (C.c_int, [P, C.c_int, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P]),
+    "es_maxpool_bwd": (C.c_int, [P, C.c_int, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, C.c_float, P]),
+    "es_upsample_bwd": (C.c_int, [P, C.c_int, P, P, P, P, P, P, C.c_int, P, C.c_float, P]),
+    "es_copy": (C.c_int, [P, C.c_int, P, P, C.c_int, P, C.c_float, C.c_float, P]),
+    "es_avgpool_fwd": (C.c_int, [P, C.c_int, P, P, P, P]),
+    "es_avgpool_bwd": (C.c_int, [P, P, P, C.c_int, P, C.c_float, P]),
+    "es_gather_rows": (C.c_int, [P, I64, P, C.c_int, C.c_int, P, I64, P]),
+    "es_sn_power_iter": (C.c_int, [P, C.c_int, C.c_int, P, P, P, C.c_int, P]),
+    "es_sn_bwd": (C.c_int, [P, P, C.c_int, C.c_int, P, P, P, P, C.c_float, P]),
+    "es_hinge_d": (C.c_int, [P, P, C.c_int, P, P, P, P, P]),
+    "es_image_expsum": (C.c_int, [P, C.c_int, P, P, P]),
+    "es_gen_losses": (C.c_int, [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "es_image_expsum_bwd": (C.c_int, [P, C.c_int, P, P, P, P, C.c_float, P]),
+    "es_router_gumbel": (C.c_int, [P, P, C.c_int, C.c_int, C.c_float, P, P, P, P]),
+    "es_router_alb": (C.c_int, [P, C.c_int, C.c_int, C.c_float, C.c_float, P, P, P]),
+    "es_adam": (C.c_int, [P, P, P, P, I64, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int,
+                          C.c_float, P]),
+    "es_randn": (C.c_int, [P, I64, C.c_uint64, C.c_uint32, P]),
+    "es_rand_exponential": (C.c_int, [P, I64, C.c_uint64, C.c_uint32, P]),
+    "es_dropout_mask": (C.c_int, [P, I64, P, P]),
+}
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def lib_path() -> str:
+    return _LIB_PATH
+
+
+def lib():
+    """Load the kernel library (raises if it was not built: there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            raise HipError(f"{_LIB_PATH} missing: build it with `make -C csrc` "
+                           f"(or __graft_entry__.build()); expertsim has no CPU fallback")
+        L = C.CDLL(_LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise HipError(f"{name} failed ({rc}): {lib().es_last_error().decode()}")
+    return rc
+
+
+def require_device(t: torch.Tensor):
+    if not t.is_cuda:
+        raise HipError("expertsim kernels need tensors on a HIP device (no CPU fallback)")
+
+
+def stream_ptr() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def dt_of(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return ES_F32
+    if t.dtype == torch.bfloat16:
+        return ES_BF16
+    raise HipError(f"unsupported dtype {t.dtype}")
+
+
+def strides4(s):
+    arr = (C.c_int64 * 4)()
+    for i in range(4):
+        arr[i] = int(s[i])
+    return arr
+
+
+def make_view(dims, strides) -> View:
+    v = View()
+    v.n, v.c, v.h, v.w = (int(d) for d in dims)
+    for i in range(4):
+        v.s[i] = int(strides[i])
+    return v
+
+
+def dropout_struct(p: float = 0.0, seed: int = 0, stream: int = 0, enabled: bool = False) -> Dropout:
+    d = Dropout()
+    d.enabled = 1 if (enabled and p > 0.0) else 0
+    if d.enabled:
+        d.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        d.stream = int(stream) & 0xFFFFFFFF
+        d.threshold = int((1.0 - float(p)) * 16777216.0)   # floor, = philox.keep_threshold
+        d.scale = float(torch.tensor(1.0, dtype=torch.float32) / torch.tensor(1.0 - p, dtype=torch.float32))
+    return d
+
+
+def chain_struct(act=ACT_NONE, slope=0.1, drop: Dropout | None = None, dropout_first=True) -> Chain:
+    ch = Chain()
+    ch.act = act
+    ch.slope = slope
+    ch.dropout_first = 1 if dropout_first else 0
+    if drop is not None:
+        ch.drop = drop
+    return ch

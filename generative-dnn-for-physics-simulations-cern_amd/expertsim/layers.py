@@ -1,0 +1,400 @@
+"""Layer-level building blocks over the HIP kernels (explicit forward / backward, no autograd).
+
+Each block keeps the reference's parameter tensors (fp32 masters, torch layouts, so state_dicts
+match the reference's) and drives the C-ABI kernels of ``expertsim.hip``.  Activations are
+``Act`` objects: a flat device buffer plus a logical (n, c, h, w) shape and element strides, so
+conv activations live channels-last (NHWC) while linear activations are plain [rows][features].
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import numpy as np
+import torch
+
+from . import hip
+
+
+class Act:
+    """Logical (N, C, H, W) tensor over a flat device buffer with explicit element strides."""
+
+    __slots__ = ("t", "dims", "strides")
+
+    def __init__(self, t: torch.Tensor, dims, strides):
+        self.t = t
+        self.dims = tuple(int(d) for d in dims)
+        self.strides = tuple(int(s) for s in strides)
+
+    # ---- constructors
+    @staticmethod
+    def nhwc(N, Cc, H, W, dtype, device, zero=False):
+        f = torch.zeros if zero else torch.empty
+        t = f(N * H * W * Cc, dtype=dtype, device=device)
+        return Act(t, (N, Cc, H, W), (H * W * Cc, 1, W * Cc, Cc))
+
+    @staticmethod
+    def rows(N, F, dtype, device, zero=False):
+        f = torch.zeros if zero else torch.empty
+        return Act(f(N * F, dtype=dtype, device=device), (N, F, 1, 1), (F, 1, 1, 1))
+
+    @staticmethod
+    def of(t: torch.Tensor):
+        """Wrap a torch tensor of rank 2 ([N,F]) or 4 ([N,C,H,W], any strides)."""
+        if t.dim() == 2:
+            return Act(t, (t.shape[0], t.shape[1], 1, 1), (t.stride(0), t.stride(1), 1, 1))
+        assert t.dim() == 4, t.shape
+        return Act(t, tuple(t.shape), tuple(t.stride()))
+
+    def like_nhwc(self, dtype=None, zero=False):
+        N, Cc, H, W = self.dims
+        return Act.nhwc(N, Cc, H, W, dtype or self.t.dtype, self.t.device, zero)
+
+    # ---- properties
+    @property
+    def view(self):
+        return hip.make_view(self.dims, self.strides)
+
+    @property
+    def dt(self):
+        return hip.dt_of(self.t)
+
+    @property
+    def ptr(self):
+        return C.c_void_p(self.t.data_ptr())
+
+    @property
+    def numel(self):
+        n, c, h, w = self.dims
+        return n * c * h * w
+
+    def torch_nchw(self):
+        """Strided torch view [N, C, H, W] of the same memory (no copy)."""
+        base = self.t
+        off = 0
+        if base.dim() != 1:
+            off = base.storage_offset()
+            base = base.reshape(-1) if base.is_contiguous() else base
+        return torch.as_strided(self.t, self.dims, self.strides, self.t.storage_offset())
+
+    def rows2d(self):
+        n, c, h, w = self.dims
+        assert h == 1 and w == 1
+        return torch.as_strided(self.t, (n, c), (self.strides[0], self.strides[1]), self.t.storage_offset())
+
+
+def copy_act(src: Act, dst: Act, alpha=1.0, beta=0.0):
+    hip.call("es_copy", C.byref(src.view), src.dt, src.ptr, C.byref(dst.view), dst.dt, dst.ptr,
+             float(alpha), float(beta), hip.stream_ptr())
+    return dst
+
+
+def ws(nbytes, device):
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+# --------------------------------------------------------------------------------- upsample
+class Upsample:
+    """torch nearest upsample (``scale_factor`` or ``size``) as index maps for the conv gather.
+
+    Source index = min(floor(dst * scale), in - 1) with scale = float32(1/scale_factor) when a
+    scale factor is given, float32(in)/out otherwise (ATen upsample_nearest2d)."""
+
+    def __init__(self, in_hw, out_hw=None, scale=None):
+        self.in_hw = tuple(in_hw)
+        if out_hw is None:
+            out_hw = (int(math.floor(in_hw[0] * scale[0])), int(math.floor(in_hw[1] * scale[1])))
+        self.out_hw = tuple(out_hw)
+        self.maps = []
+        self.inv = []
+        for ax in range(2):
+            n_in, n_out = self.in_hw[ax], self.out_hw[ax]
+            if scale is not None:
+                sc = np.float32(1.0 / scale[ax])
+            else:
+                sc = np.float32(n_in) / np.float32(n_out)
+            dst = np.arange(n_out, dtype=np.float32)
+            src = np.minimum(np.floor(dst * sc).astype(np.int64), n_in - 1).astype(np.int32)
+            self.maps.append(src)
+            start = np.zeros(n_in, np.int32)
+            count = np.zeros(n_in, np.int32)
+            for i in range(n_in):
+                where = np.nonzero(src == i)[0]
+                assert where.size == 0 or (where[-1] - where[0] + 1 == where.size)
+                start[i] = where[0] if where.size else 0
+                count[i] = where.size
+            self.inv.append((start, count))
+        self._dev = {}
+
+    def device_maps(self, device):
+        key = str(device)
+        if key not in self._dev:
+            t = lambda a: torch.from_numpy(a).to(device)
+            self._dev[key] = (t(self.maps[0]), t(self.maps[1]), t(self.inv[0][0]), t(self.inv[0][1]),
+                              t(self.inv[1][0]), t(self.inv[1][1]))
+        return self._dev[key]
+
+
+# ------------------------------------------------------------------------------ conv / linear
+class ConvOp:
+    """nn.Conv2d / nn.Linear on the implicit-GEMM kernels.
+
+    ``weight``: fp32 master [K, C, R, S] (or [K, C] for a linear); ``bias`` fp32 [K] or None.
+    The packed GEMM copies (fwd [K][R][S][C], dgrad [C][R][S][K]) in the compute dtype are
+    rebuilt when ``invalidate()`` is called (after every optimizer step) or per call when a
+    spectral-norm sigma is given."""
+
+    def __init__(self, weight: torch.nn.Parameter, bias, stride=1, pad=0, upsample: Upsample = None):
+        self.weight = weight
+        self.bias = bias
+        self.stride = stride
+        self.pad = pad
+        self.up = upsample
+        w = weight
+        self.K = w.shape[0]
+        self.C = w.shape[1]
+        self.R = w.shape[2] if w.dim() == 4 else 1
+        self.S = w.shape[3] if w.dim() == 4 else 1
+        self._packed = {}
+
+    def invalidate(self):
+        self._packed.clear()
+
+    def packed(self, dtype, mode, inv_scale=None):
+        key = (dtype, mode)
+        if inv_scale is None and key in self._packed:
+            return self._packed[key]
+        w = self.weight
+        out = torch.empty(w.numel(), dtype=dtype, device=w.device)
+        hip.call("es_pack_conv_weight", hip.ptr(w), self.K, self.C, self.R, self.S, mode,
+                 hip.ptr(inv_scale), None, hip.ptr(out), hip.dt_of(out), hip.stream_ptr())
+        if inv_scale is None:
+            self._packed[key] = out
+        return out
+
+    def desc(self, x: Act):
+        N, Cc, H, W = x.dims
+        assert Cc == self.C, (Cc, self.C)
+        d = hip.ConvDesc()
+        d.N, d.C, d.H, d.W = N, Cc, H, W
+        if self.up is not None:
+            assert (H, W) == self.up.in_hw, ((H, W), self.up.in_hw)
+            d.Hu, d.Wu = self.up.out_hw
+            maps = self.up.device_maps(x.t.device)
+            d.hmap, d.wmap = maps[0].data_ptr(), maps[1].data_ptr()
+        else:
+            d.Hu, d.Wu = H, W
+            d.hmap = d.wmap = None
+        d.K, d.R, d.S, d.stride, d.pad = self.K, self.R, self.S, self.stride, self.pad
+        d.P = (d.Hu + 2 * self.pad - self.R) // self.stride + 1
+        d.Q = (d.Wu + 2 * self.pad - self.S) // self.stride + 1
+        return d
+
+    def fwd(self, x: Act, out_dtype=None, inv_scale=None, out: Act = None, with_bias=True) -> Act:
+        d = self.desc(x)
+        cdt = x.t.dtype
+        wk = self.packed(cdt, 0, inv_scale)
+        if out is None:
+            out = Act.nhwc(d.N, d.K, d.P, d.Q, out_dtype or cdt, x.t.device)
+        bias = self.bias if (with_bias and self.bias is not None) else None
+        hip.call("es_conv2d_fwd", C.byref(d), x.dt, x.ptr, hip.strides4(x.strides), hip.ptr(wk),
+                 hip.ptr(bias), out.ptr, out.dt, hip.strides4(out.strides), hip.stream_ptr())
+        return out
+
+    def dgrad(self, dy: Act, x: Act, dx_dtype=None, inv_scale=None, dx: Act = None, beta=0.0) -> Act:
+        """Gradient w.r.t. the conv input x (folded through the upsample when present)."""
+        d = self.desc(x)
+        cdt = dy.t.dtype
+        wd = self.packed(cdt, 1, inv_scale)
+        N, Cc, H, W = x.dims
+        ddt = dx_dtype or cdt
+        if self.up is None:
+            if dx is None:
+                dx = Act.nhwc(N, Cc, H, W, ddt, dy.t.device)
+            hip.call("es_conv2d_dgrad", C.byref(d), dy.dt, dy.ptr, hip.strides4(dy.strides), hip.ptr(wd),
+                     dx.ptr, dx.dt, hip.strides4(dx.strides), float(beta), hip.stream_ptr())
+            return dx
+        dxu = Act.nhwc(N, Cc, d.Hu, d.Wu, torch.float32, dy.t.device)
+        hip.call("es_conv2d_dgrad", C.byref(d), dy.dt, dy.ptr, hip.strides4(dy.strides), hip.ptr(wd),
+                 dxu.ptr, dxu.dt, hip.strides4(dxu.strides), 0.0, hip.stream_ptr())
+        if dx is None:
+            dx = Act.nhwc(N, Cc, H, W, ddt, dy.t.device)
+        maps = self.up.device_maps(dy.t.device)
+        hip.call("es_upsample_bwd", C.byref(dxu.view), dxu.dt, dxu.ptr, hip.ptr(maps[2]), hip.ptr(maps[3]),
+                 hip.ptr(maps[4]), hip.ptr(maps[5]), C.byref(dx.view), dx.dt, dx.ptr, float(beta),
+                 hip.stream_ptr())
+        return dx
+
+    def wgrad(self, dy: Act, x: Act, dw_out: torch.Tensor = None, db_out: torch.Tensor = None,
+              beta=1.0):
+        """dW (torch layout, fp32) accumulated into dw_out (beta=1) or written (beta=0)."""
+        d = self.desc(x)
+        dev = dy.t.device
+        dwk = torch.zeros(self.weight.numel(), dtype=torch.float32, device=dev)
+        assert dy.t.dtype == x.t.dtype, (dy.t.dtype, x.t.dtype)
+        hip.call("es_conv2d_wgrad", C.byref(d), dy.dt, dy.ptr, hip.strides4(dy.strides), x.ptr,
+                 hip.strides4(x.strides), hip.ptr(dwk), hip.stream_ptr())
+        if dw_out is not None:
+            hip.call("es_unpack_conv_grad", hip.ptr(dwk), self.K, self.C, self.R, self.S, None,
+                     hip.ptr(dw_out), float(beta), hip.stream_ptr())
+        if db_out is not None:
+            channel_sum(dy, db_out, beta)
+        return dwk
+
+
+def channel_sum(x: Act, out: torch.Tensor, beta=1.0):
+    wsb = ws(hip.lib().es_channel_sum_ws_bytes(C.byref(x.view)), x.t.device)
+    hip.call("es_channel_sum", C.byref(x.view), x.dt, x.ptr, hip.ptr(out), float(beta), hip.ptr(wsb),
+             hip.stream_ptr())
+
+
+# ------------------------------------------------------------------------------ norm + act
+class NormOp:
+    """BatchNorm (train: batch stats + running update), GroupNorm or LayerNorm, fused with the
+    dropout / activation chain that follows it in the reference's nn.Sequential."""
+
+    def __init__(self, kind, gamma=None, beta=None, groups=1, eps=1e-5, running_mean=None,
+                 running_var=None, momentum=0.1, num_batches=None):
+        self.kind, self.gamma, self.beta, self.groups, self.eps = kind, gamma, beta, groups, eps
+        self.rm, self.rv, self.momentum, self.nbt = running_mean, running_var, momentum, num_batches
+
+    def stats(self, x: Act, train=True):
+        dev = x.t.device
+        if self.kind == hip.NORM_BN and not train:
+            mean = self.rm
+            invstd = torch.empty_like(self.rv)
+            # eval: invstd from running var (tiny host-side torch op on device buffers)
+            invstd.copy_(torch.rsqrt(self.rv + self.eps))
+            return mean, invstd
+        n_groups = {hip.NORM_BN: x.dims[1], hip.NORM_GN: x.dims[0] * self.groups,
+                    hip.NORM_LN: x.dims[0]}[self.kind]
+        mean = torch.empty(n_groups, dtype=torch.float32, device=dev)
+        invstd = torch.empty(n_groups, dtype=torch.float32, device=dev)
+        wsb = ws(hip.lib().es_norm_stats_ws_bytes(C.byref(x.view), self.kind, self.groups), dev)
+        upd = self.kind == hip.NORM_BN and train
+        hip.call("es_norm_stats", C.byref(x.view), x.dt, x.ptr, self.kind, self.groups, float(self.eps),
+                 hip.ptr(mean), hip.ptr(invstd), hip.ptr(self.rm) if upd else None,
+                 hip.ptr(self.rv) if upd else None, float(self.momentum), hip.ptr(wsb), hip.stream_ptr())
+        if upd and self.nbt is not None:
+            self.nbt.add_(1)
+        return mean, invstd
+
+    def norm_struct(self, mean, invstd):
+        nm = hip.Norm()
+        nm.kind, nm.groups = self.kind, self.groups
+        nm.mean, nm.invstd = mean.data_ptr(), invstd.data_ptr()
+        nm.gamma = self.gamma.data_ptr() if self.gamma is not None else None
+        nm.beta = self.beta.data_ptr() if self.beta is not None else None
+        return nm
+
+    def fwd(self, x: Act, chain: hip.Chain, out_dtype=None, train=True, addend: Act = None, out: Act = None):
+        mean, invstd = self.stats(x, train)
+        nm = self.norm_struct(mean, invstd)
+        y = out if out is not None else x.like_nhwc(out_dtype or x.t.dtype)
+        hip.call("es_norm_act_fwd", C.byref(x.view), x.dt, C.byref(nm), C.byref(chain),
+                 C.byref(addend.view) if addend is not None else None,
+                 addend.dt if addend is not None else 0, addend.ptr if addend is not None else None,
+                 x.ptr, C.byref(y.view), y.dt, y.ptr, hip.stream_ptr())
+        return y, (mean, invstd)
+
+    def bwd(self, x: Act, stats, chain: hip.Chain, dy: Act, dx_dtype=None, act_ref: Act = None,
+            addend: Act = None, dgamma=None, dbeta=None, dx: Act = None, beta=0.0):
+        mean, invstd = stats
+        nm = self.norm_struct(mean, invstd)
+        if dx is None:
+            dx = x.like_nhwc(dx_dtype or dy.t.dtype)
+        wsb = ws(hip.lib().es_norm_bwd_ws_bytes(C.byref(x.view), self.kind, self.groups), x.t.device)
+        assert addend is None, "residual addend handled through act_ref"
+        hip.call("es_norm_act_bwd", C.byref(x.view), x.dt, x.ptr, C.byref(nm), C.byref(chain),
+                 C.byref(dy.view), dy.dt, dy.ptr,
+                 C.byref(act_ref.view) if act_ref is not None else None,
+                 act_ref.dt if act_ref is not None else 0, act_ref.ptr if act_ref is not None else None,
+                 C.byref(dx.view), dx.dt, dx.ptr, float(beta), hip.ptr(dgamma), hip.ptr(dbeta),
+                 hip.ptr(wsb), hip.stream_ptr())
+        return dx
+
+
+def act_fwd(x: Act, chain: hip.Chain, out: Act = None, out_dtype=None) -> Act:
+    y = out if out is not None else x.like_nhwc(out_dtype or x.t.dtype)
+    hip.call("es_act_fwd", C.byref(x.view), x.dt, x.ptr, C.byref(chain), C.byref(y.view), y.dt, y.ptr,
+             hip.stream_ptr())
+    return y
+
+
+def act_bwd(x: Act, chain: hip.Chain, dy: Act, act_ref: Act = None, dx: Act = None, dx_dtype=None, beta=0.0):
+    """Backward of a norm-free chain evaluated at x (or at act_ref)."""
+    if dx is None:
+        dx = x.like_nhwc(dx_dtype or dy.t.dtype)
+    wsb = ws(hip.lib().es_norm_bwd_ws_bytes(C.byref(x.view), hip.NORM_NONE, 1), x.t.device)
+    hip.call("es_norm_act_bwd", C.byref(x.view), x.dt, x.ptr, None, C.byref(chain), C.byref(dy.view), dy.dt,
+             dy.ptr, C.byref(act_ref.view) if act_ref is not None else None,
+             act_ref.dt if act_ref is not None else 0, act_ref.ptr if act_ref is not None else None,
+             C.byref(dx.view), dx.dt, dx.ptr, float(beta), None, None, hip.ptr(wsb), hip.stream_ptr())
+    return dx
+
+
+# ------------------------------------------------------------------------------------ pools
+class MaxPool:
+    def __init__(self, k, s=None):
+        self.kh, self.kw = (k, k) if isinstance(k, int) else k
+        s = s if s is not None else (self.kh, self.kw)
+        self.sh, self.sw = (s, s) if isinstance(s, int) else s
+
+    def out_hw(self, h, w):
+        return (h - self.kh) // self.sh + 1, (w - self.kw) // self.sw + 1
+
+    def fwd(self, x: Act, out: Act = None):
+        N, Cc, H, W = x.dims
+        ho, wo = self.out_hw(H, W)
+        y = out if out is not None else Act.nhwc(N, Cc, ho, wo, x.t.dtype, x.t.device)
+        idx = torch.empty(y.numel, dtype=torch.uint8, device=x.t.device)
+        hip.call("es_maxpool_fwd", C.byref(x.view), x.dt, x.ptr, self.kh, self.kw, self.sh, self.sw,
+                 C.byref(y.view), y.ptr, hip.ptr(idx), hip.stream_ptr())
+        return y, idx
+
+    def bwd(self, dy: Act, idx, x_dims, dtype, dx: Act = None, beta=0.0):
+        N, Cc, H, W = x_dims
+        dx = dx if dx is not None else Act.nhwc(N, Cc, H, W, dtype, dy.t.device)
+        assert dy.dt == dx.dt
+        hip.call("es_maxpool_bwd", C.byref(dy.view), dy.dt, dy.ptr, hip.ptr(idx), self.kh, self.kw, self.sh,
+                 self.sw, C.byref(dx.view), dx.ptr, float(beta), hip.stream_ptr())
+        return dx
+
+
+def avgpool_fwd(x: Act) -> Act:
+    N, Cc, H, W = x.dims
+    y = Act.rows(N, Cc, torch.float32, x.t.device)
+    hip.call("es_avgpool_fwd", C.byref(x.view), x.dt, x.ptr, C.byref(y.view), y.ptr, hip.stream_ptr())
+    return y
+
+
+def avgpool_bwd(dy: Act, x_dims, dtype, device) -> Act:
+    N, Cc, H, W = x_dims
+    dx = Act.nhwc(N, Cc, H, W, dtype, device)
+    hip.call("es_avgpool_bwd", C.byref(dy.view), dy.ptr, C.byref(dx.view), dx.dt, dx.ptr, 0.0, hip.stream_ptr())
+    return dx
+
+
+# ---------------------------------------------------------------------------- spectral norm
+class SpectralNorm:
+    """torch.nn.utils.spectral_norm state of one layer (weight_orig, weight_u, weight_v)."""
+
+    def __init__(self, module):
+        self.w = module.weight_orig
+        self.u = module.weight_u
+        self.v = module.weight_v
+        self.h = self.w.shape[0]
+        self.wd = self.w[0].numel()
+
+    def sigma(self, update=True):
+        """One power iteration (train mode) -> device tensor holding sigma (no host sync)."""
+        buf = torch.empty(1 + self.h + self.wd, dtype=torch.float32, device=self.w.device)
+        hip.call("es_sn_power_iter", hip.ptr(self.w), self.h, self.wd, hip.ptr(self.u), hip.ptr(self.v),
+                 hip.ptr(buf), 1 if update else 0, hip.stream_ptr())
+        # snapshot u, v used by this call (the next call updates them in place)
+        return buf[:1], self.u.clone(), self.v.clone()
+
+    def bwd(self, g_sn: torch.Tensor, sig, dw_orig: torch.Tensor, beta=1.0):
+        sigma, u, v = sig
+        hip.call("es_sn_bwd", hip.ptr(self.w), hip.ptr(g_sn), self.h, self.wd, hip.ptr(u), hip.ptr(v),
+                 hip.ptr(sigma), hip.ptr(dw_orig), float(beta), hip.stream_ptr())

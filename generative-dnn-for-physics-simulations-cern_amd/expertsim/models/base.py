@@ -1,0 +1,131 @@
+"""Shared plumbing of the expertsim model classes.
+
+* ``build_tree`` creates the reference's parameter tree (same dotted names, same construction
+  order -> identical default init under the same torch seed, identical state_dict keys) from a
+  declarative spec; layers without parameters (Dropout, LeakyReLU, Upsample, pools) are not
+  materialised — their behaviour lives in each model's forward/backward program.
+* ``ExpertModule.flatten`` moves every parameter into ONE contiguous fp32 buffer (and every
+  gradient into one grad buffer) so the optimizer is a single fused Adam launch and the DDP
+  all-reduce is a single bucket per model (see expertsim/train/training_setup.py).
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+
+def _container(root: nn.Module, path):
+    mod = root
+    for p in path:
+        if p not in mod._modules:
+            mod.add_module(p, nn.Module())
+        mod = mod._modules[p]
+    return mod
+
+
+def build_tree(root: nn.Module, specs):
+    """specs: list of (dotted_name, factory) in reference construction order."""
+    for name, factory in specs:
+        parts = name.split(".")
+        parent = _container(root, parts[:-1])
+        parent.add_module(parts[-1], factory())
+
+
+def get_module(root: nn.Module, name: str) -> nn.Module:
+    mod = root
+    for p in name.split("."):
+        mod = mod._modules[p]
+    return mod
+
+
+class ExpertModule(nn.Module):
+    """Base of generator / discriminator / aux-regressor / router.
+
+    Subclasses implement ``program(device)`` (build the HIP layer ops bound to the current
+    parameter storage) and explicit ``fwd`` / ``bwd`` methods used by MoEWrapper.train_step."""
+
+    compute_dtype = torch.float32
+
+    def __init__(self):
+        super().__init__()
+        self._flat = None
+        self._ops = None
+
+    # ----------------------------------------------------------------- flat parameter storage
+    def flatten(self):
+        params = [p for p in self.parameters()]
+        dev = params[0].device
+        total = sum(p.numel() for p in params)
+        if self._flat is not None and self._flat[0].device == dev and self._flat[0].numel() == total \
+                and all(p.data.data_ptr() == self._flat[0][o:o + p.numel()].data_ptr()
+                        for p, o in zip(params, self._offsets())):
+            return
+        flat_p = torch.empty(total, dtype=torch.float32, device=dev)
+        flat_g = torch.zeros(total, dtype=torch.float32, device=dev)
+        o = 0
+        for p in params:
+            n = p.numel()
+            flat_p[o:o + n].copy_(p.data.reshape(-1))
+            p.data = flat_p[o:o + n].view_as(p)
+            p.grad = flat_g[o:o + n].view_as(p)
+            o += n
+        self._flat = (flat_p, flat_g)
+        self._ops = None
+
+    def _offsets(self):
+        o, out = 0, []
+        for p in self.parameters():
+            out.append(o)
+            o += p.numel()
+        return out
+
+    @property
+    def flat_params(self):
+        self.flatten()
+        return self._flat[0]
+
+    @property
+    def flat_grads(self):
+        self.flatten()
+        return self._flat[1]
+
+    def zero_grads(self):
+        self.flatten()
+        self._flat[1].zero_()
+        for p, o in zip(self.parameters(), self._offsets()):
+            p.grad = self._flat[1][o:o + p.numel()].view_as(p)
+
+    def ops(self):
+        """Layer ops bound to the flat parameter storage (rebuilt after device moves)."""
+        self.flatten()
+        if self._ops is None:
+            self._ops = self.program()
+        return self._ops
+
+    def invalidate(self):
+        """Called after every optimizer step: packed GEMM weights must be rebuilt."""
+        if self._ops is not None:
+            for op in self._ops.values():
+                if hasattr(op, "invalidate"):
+                    op.invalidate()
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        self._flat = None
+        self._ops = None
+        return out
+
+    def __deepcopy__(self, memo):
+        # deep copies (moe.py:29-31) must not share flat storage
+        cls = self.__class__
+        new = cls.__new__(cls)
+        memo[id(self)] = new
+        import copy as _copy
+        for k, v in self.__dict__.items():
+            if k in ("_flat", "_ops"):
+                setattr(new, k, None)
+            else:
+                setattr(new, k, _copy.deepcopy(v, memo))
+        for p in new.parameters():
+            p.grad = None
+        return new

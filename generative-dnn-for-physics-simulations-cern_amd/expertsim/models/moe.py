@@ -1,0 +1,280 @@
+"""MoEWrapper — the expertsim GAN training step on MI355X.
+
+Reference: expertsim/models/moe.py:14-699 (``MoEWrapper.__init__`` 24-50, ``train_step`` 52-504,
+``discriminator_train_step`` 506-527, ``generator_train_step`` 529-571,
+``sdi_gan_regularization`` 573-588, ``intensity_regularization`` 590-642).
+
+Same constructor and ``train_step`` signature and the same metric keys (moe.py:480-502).  The step
+is an explicit program of HIP kernels (no autograd): router -> per expert {G fwd #1, D step
+(D(real), D(fake), hinge, D backward, fused Adam), G fwd #2, D(fake1), D(fake2), aux regressor,
+fused G losses, D/A/G backward, fused Adam} -> router loss + Adam.  Loss weights and metrics stay
+on the device; the only host synchronisation is the expert-size read when n_experts > 1
+(needed for the reference's ``B_e <= 1`` skip rule, moe.py:126).
+
+Randomness: noise / Gumbel draws come from device Philox streams unless ``noise_fn`` /
+``gumbel_fn`` inject them (parity tests); dropout masks are Philox streams keyed by
+(step, rank, expert, pass, layer) — expertsim/utils/philox.py.
+
+Data parallel (expertsim/train/ddp.py): with ``self.ddp`` set, each rank routes its own shard,
+gradients of every optimizer phase are all-reduced (RCCL) before the fused Adam.
+"""
+from __future__ import annotations
+
+import copy
+import ctypes as C
+from itertools import combinations
+
+import numpy as np
+import torch
+from torch import nn
+
+from .. import hip
+from ..config import cfg_get
+from ..layers import Act, copy_act
+from ..rng import DeviceRNG
+from ..utils import philox
+
+
+class MoEWrapper(nn.Module):
+    name = "separate-gumbal-gen-disc-shared-aux-reg-masked-router-multiple-aux-reg"
+    description = "MoEWrapper where expert is defined as a generator and discriminator." \
+                  "Auxiliary regressor is each for every expert "
+
+    def __init__(self, generator_cls, discriminator_cls, aux_reg_cls, router_cls, n_experts: int, cfg,
+                 image_shape: tuple = (56, 30)):
+        super().__init__()
+        self.image_shape = tuple(image_shape)
+        self.generators = nn.ModuleList([copy.deepcopy(generator_cls) for _ in range(n_experts)])
+        self.discriminators = nn.ModuleList([copy.deepcopy(discriminator_cls) for _ in range(n_experts)])
+        self.aux_regs = nn.ModuleList([copy.deepcopy(aux_reg_cls) for _ in range(n_experts)])
+        self.router = router_cls
+        self.n_experts = n_experts
+        self.noise_dim = int(cfg.model.noise_dim)
+        self.cfg = cfg
+        self.g_steps = [0 for _ in range(n_experts)]
+        self.d_steps = [0 for _ in range(n_experts)]
+        self.rng_seed = int(cfg_get(cfg, "train.rng_seed", 1234))
+        self.rng = DeviceRNG(self.rng_seed)
+        self.noise_fn = None       # optional injection: fn(expert, which, shape) -> tensor
+        self.gumbel_fn = None      # optional injection: fn(shape) -> Exp(1) tensor
+        self.ddp = None            # expertsim.train.ddp.DataParallel (set by the loop)
+        self.rank = 0
+        self.step_count = 0
+        self.set_precision(cfg_get(cfg, "train.precision", "fp32"))
+
+    def set_precision(self, precision: str):
+        """fp32: every GEMM on fp32 MFMA (parity mode).  bf16: generator and aux-regressor GEMM
+        operands and activations in bf16 (fp32 accumulation, statistics, parameters, optimizer);
+        the discriminator stays fp32."""
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision must be fp32 or bf16, got {precision!r}")
+        self.precision = precision
+        low = torch.bfloat16 if precision == "bf16" else torch.float32
+        for m in self.generators:
+            m.compute_dtype = low
+        for m in self.aux_regs:
+            m.compute_dtype = low
+        for m in self.discriminators:
+            m.compute_dtype = torch.float32
+
+    # ---------------------------------------------------------------------------- helpers
+    def _noise(self, expert, which, shape, device):
+        if self.noise_fn is not None:
+            return self.noise_fn(expert, which, shape).to(device=device, dtype=torch.float32).contiguous()
+        return self.rng.normal(torch.empty(shape, dtype=torch.float32, device=device))
+
+    def _gumbel(self, shape, device):
+        if self.gumbel_fn is not None:
+            return self.gumbel_fn(shape).to(device=device, dtype=torch.float32).contiguous()
+        return self.rng.exponential(torch.empty(shape, dtype=torch.float32, device=device))
+
+    def _allreduce(self, module):
+        if self.ddp is not None:
+            self.ddp.allreduce_grads(module)
+
+    # ---------------------------------------------------------------------------- the step
+    def train_step(self, epoch, cond, real_images, true_positions, std, intensity, aux_reg_optimizers,
+                   generator_optimizers, discriminator_optimizers, router_optimizer, ema_helper, device):
+        dev = torch.device(device) if not isinstance(device, torch.device) else device
+        if dev.type != "cuda":
+            raise hip.HipError("MoEWrapper.train_step runs on the HIP device only (no CPU fallback)")
+        E = self.n_experts
+        f32 = lambda t: t.to(device=dev, dtype=torch.float32).contiguous()
+        cond, real_images, true_positions, std, intensity = map(f32, (cond, real_images, true_positions,
+                                                                     std, intensity))
+        if real_images.dim() == 3:
+            real_images = real_images.unsqueeze(1)
+        B = cond.shape[0]
+        step = self.step_count
+        rc = self.cfg.model.router
+
+        tau = max(rc.tau_min, rc.tau_start * (rc.tau_decay ** epoch))          # moe.py:62-74
+        expo = self._gumbel((B, E), dev)
+        gates, logits, idx, counts, rctx = self.router.fwd(cond, expo, tau)
+
+        for i in range(E):                                                       # moe.py:115-119
+            aux_reg_optimizers[i].zero_grad(set_to_none=True)
+            generator_optimizers[i].zero_grad(set_to_none=True)
+            discriminator_optimizers[i].zero_grad(set_to_none=True)
+        router_optimizer.zero_grad(set_to_none=True)
+
+        # expert dispatch (moe.py:97-99,123): E == 1 needs no routing sync
+        if E == 1:
+            groups = [(0, None, B)]
+        else:
+            idx_h = idx.cpu().numpy()
+            groups = []
+            for e in range(E):
+                rows = np.nonzero(idx_h == e)[0].astype(np.int32)
+                groups.append((e, rows, rows.size))
+        if self.ddp is not None:
+            groups = self.ddp.global_groups(groups, B)
+
+        # metrics buffer: per expert [total, gen, div, int, aux, std_int, mean_int, w, disc]
+        mbuf = torch.zeros(E, 9, dtype=torch.float32, device=dev)
+        for e, rows, be in groups:
+            be_global = be if self.ddp is None else self.ddp.global_count(e)
+            if be_global <= 1:                                                   # moe.py:126-135
+                continue
+            self._expert_step(e, rows, be, B, cond, real_images, true_positions, std, intensity,
+                              generator_optimizers[e], discriminator_optimizers[e], aux_reg_optimizers[e],
+                              mbuf, step, dev)
+
+        # ---- router (moe.py:213-449)
+        zero = torch.zeros((), dtype=torch.float32, device=dev)
+        if E > 1:
+            if rc.util_strength != 0 or rc.ed_strength != 0:
+                raise NotImplementedError("util_strength / ed_strength != 0: not on the HIP path "
+                                          "(reference default is 0)")
+            gan = mbuf[:, 0].mean() * rc.gan_strength
+            if rc.diff_strength != 0:
+                dli = sum((mbuf[a, 6] - mbuf[b, 6]).abs() for a, b in combinations(range(E), 2)) * rc.diff_strength
+            else:
+                dli = zero
+            diff = -dli * rc.diff_strength
+            alpha = min(max(epoch / rc.alpha, 0.0), 1.0)
+            dec_w = rc.min_weight + (1.0 - rc.min_weight) * alpha
+            alb_out = torch.zeros(1, dtype=torch.float32, device=dev)
+            dlogits = torch.empty(B, E, dtype=torch.float32, device=dev)
+            if rc.alb_strength != 0:
+                hip.call("es_router_alb", hip.ptr(gates), B, E, float(tau), float(rc.alb_strength * dec_w),
+                         hip.ptr(alb_out), hip.ptr(dlogits), hip.stream_ptr())
+                alb = alb_out[0] / dec_w
+            else:
+                dlogits.zero_()
+                alb = zero
+            router_loss = gan + diff + dec_w * alb
+            if epoch < rc.stop_router_training_epoch:
+                self.router.bwd(rctx, dlogits)
+                self._allreduce(self.router)
+                router_optimizer.step()
+            else:
+                router_loss = zero
+            ed = ent = zero
+        else:
+            gan = router_loss = ed = diff = ent = alb = zero
+
+        self.step_count += 1
+        countsf = counts.to(torch.float32) if self.ddp is None else self.ddp.global_counts_tensor(dev)
+        metrics = {
+            "gen_loss": mbuf[:, 0].mean(), "disc_loss": mbuf[:, 8].mean(), "div_loss": mbuf[:, 2].mean(),
+            "intensity_loss": mbuf[:, 3].mean(), "aux_reg_loss": mbuf[:, 4].mean(),
+            "router_loss": router_loss, "expert_distribution_loss": ed, "differentiation_loss": diff,
+            "expert_entropy_loss": ent, "adaptive_load_balancing_loss": alb, "gan_loss": gan,
+        }
+        for i in range(E):
+            metrics[f"gen_loss_{i}"] = mbuf[i, 0]
+            metrics[f"disc_loss_{i}"] = mbuf[i, 8]
+            metrics[f"div_loss_experts_{i}"] = mbuf[i, 2]
+            metrics[f"intensity_loss_experts_{i}"] = mbuf[i, 3]
+            metrics[f"aux_reg_loss_experts_{i}"] = mbuf[i, 4]
+            metrics[f"std_intensities_experts_{i}"] = mbuf[i, 5]
+            metrics[f"mean_intensities_experts_{i}"] = mbuf[i, 6]
+            metrics[f"n_choosen_experts_mean_epoch_{i}"] = countsf[i]
+        return metrics
+
+    # ---------------------------------------------------------------------------- one expert
+    def _expert_step(self, e, rows, be, B, cond, real, pos, std, intensity, opt_g, opt_d, opt_a, mbuf, step, dev):
+        G, D, A = self.generators[e], self.discriminators[e], self.aux_regs[e]
+        H, W = real.shape[2], real.shape[3]
+        if rows is None:
+            sc, sr, sp, ss, si = cond, real, pos, std, intensity
+        else:
+            ridx = torch.from_numpy(rows).to(dev)
+            gather = lambda t, cols: _gather_rows(t, ridx, cols)
+            sc, sp, ss, si = gather(cond, cond.shape[1]), gather(pos, 2), gather(std, 1), gather(intensity, 1)
+            sr = gather(real.reshape(B, -1), H * W).view(be, 1, H, W)
+        # class_counts_adjusted[i] as float32 (moe.py:99-100,522,562)
+        w = float(np.float32(self.ddp.global_count(e) if self.ddp else be) / np.float32(self.ddp.global_batch if self.ddp else B))
+        w_dev = torch.full((1,), w, dtype=torch.float32, device=dev)
+        rank = self.rank
+        sb = lambda pid: philox.dropout_stream(step, e, pid, 0, rank)
+
+        # ---- generator forward #1 (moe.py:144-145)
+        n1 = self._noise(e, 0, (be, self.noise_dim), dev)
+        fake1, gctx1 = G.fwd(n1, sc, seed=self.rng_seed, stream_base=sb(philox.PASS_G1))
+
+        # ---- discriminator step (moe.py:506-527)
+        ro, _, dctx_r = D.fwd(Act.of(sr), sc)
+        fo, _, dctx_f = D.fwd(fake1, sc)
+        dro = torch.empty(be, 1, dtype=torch.float32, device=dev)
+        dfo = torch.empty(be, 1, dtype=torch.float32, device=dev)
+        hip.call("es_hinge_d", ro.ptr, fo.ptr, be, hip.ptr(w_dev), hip.ptr(mbuf[e, 8:9]), hip.ptr(dro),
+                 hip.ptr(dfo), hip.stream_ptr())
+        D.bwd(dctx_r, dout=Act.of(dro), weight_grads=True, input_grad=False)
+        D.bwd(dctx_f, dout=Act.of(dfo), weight_grads=True, input_grad=False)
+        self._allreduce(D)
+        opt_d.step()
+
+        # ---- generator step (moe.py:529-571)
+        n2 = self._noise(e, 1, (be, self.noise_dim), dev)
+        fake2, gctx2 = G.fwd(n2, sc, seed=self.rng_seed, stream_base=sb(philox.PASS_G2))
+        fo1, fl1, dctx1 = D.fwd(fake1, sc)
+        _, fl2, dctx2 = D.fwd(fake2, sc)
+        s = torch.empty(be, dtype=torch.float32, device=dev)
+        hip.call("es_image_expsum", C.byref(fake1.view), fake1.dt, fake1.ptr, hip.ptr(s), hip.stream_ptr())
+        coords, actx = A.fwd(fake1, seed=self.rng_seed, stream_base=sb(philox.PASS_AUX))
+        L = fl1.dims[1]
+        p = hip.GenLoss()
+        p.n, p.latent, p.noise = be, L, self.noise_dim
+        p.di_strength, p.in_strength = float(G.di_strength), float(G.in_strength)
+        p.aux_strength = float(self.cfg.model.aux_reg.strength)
+        dfo1 = torch.empty(be, 1, dtype=torch.float32, device=dev)
+        dl1 = torch.empty(be, L, dtype=torch.float32, device=dev)
+        dl2 = torch.empty(be, L, dtype=torch.float32, device=dev)
+        dcoord = torch.empty(be, 2, dtype=torch.float32, device=dev)
+        coef = torch.empty(be, dtype=torch.float32, device=dev)
+        hip.call("es_gen_losses", C.byref(p), fo1.ptr, fl1.ptr, fl2.ptr, hip.ptr(n1), hip.ptr(n2), hip.ptr(ss),
+                 hip.ptr(s), hip.ptr(si), coords.ptr, hip.ptr(sp), hip.ptr(w_dev), hip.ptr(mbuf[e, 0:8]),
+                 hip.ptr(dfo1), hip.ptr(dl1), hip.ptr(dl2), hip.ptr(dcoord), hip.ptr(coef), hip.stream_ptr())
+        dimg1 = D.bwd(dctx1, dout=Act.of(dfo1), dlat=Act.of(dl1), weight_grads=False, input_grad=True)
+        dimg2 = D.bwd(dctx2, dout=None, dlat=Act.of(dl2), weight_grads=False, input_grad=True)
+        dimga = A.bwd(actx, Act.of(dcoord), input_grad=True)
+        copy_act(dimga, dimg1, 1.0, 1.0)
+        hip.call("es_image_expsum_bwd", C.byref(fake1.view), fake1.dt, fake1.ptr, hip.ptr(coef),
+                 C.byref(dimg1.view), dimg1.ptr, 1.0, hip.stream_ptr())
+        G.bwd(gctx1, dimg1)
+        G.bwd(gctx2, dimg2)
+        self._allreduce(G)
+        self._allreduce(A)
+        opt_g.step()
+        opt_a.step()
+
+    # ---------------------------------------------------------------------------- evaluation
+    @torch.no_grad()
+    def evaluate(self, epoch, y_test, x_test, true_positions, std, intensity, cfg, device):
+        from ..train.evaluation import evaluate_moe
+        return evaluate_moe(self, epoch, y_test, x_test, cfg, device)
+
+    def get_expert_assignment_counts(self, expert_assignments: torch.Tensor) -> torch.Tensor:
+        counts = torch.bincount(expert_assignments.long(), minlength=self.n_experts).float()
+        return counts / expert_assignments.size(0)
+
+
+def _gather_rows(t: torch.Tensor, ridx: torch.Tensor, cols: int) -> torch.Tensor:
+    rows = ridx.numel()
+    out = torch.empty(rows, cols, dtype=torch.float32, device=t.device)
+    src = t.reshape(t.shape[0], -1)
+    hip.call("es_gather_rows", hip.ptr(src), src.stride(0), hip.ptr(ridx), rows, cols, hip.ptr(out), cols,
+             hip.stream_ptr())
+    return out

@@ -1,0 +1,141 @@
+"""Neutron-ZDC (44x44) generator — reference: expertsim/models/neutron/generator.py:5-49.
+
+Program (train mode), every step a HIP kernel:
+  x0 = [noise | cond]                                  es_copy into one [B,19] row buffer
+  fc1 Linear 19->256 -> BN1d -> Dropout(0.2) -> LReLU  implicit GEMM + fused norm/drop/act
+  fc2 Linear 256->21632 -> BN1d -> Dropout -> LReLU    (features in the reference's NCHW order)
+  view [B,128,13,13] -> NHWC copy
+  up x2 + conv3 128->256 -> BN2d -> Dropout -> LReLU   upsample folded into the conv gather
+  up x2 + conv3 256->128 -> BN2d -> Dropout -> LReLU   (72 % of the step's FLOPs)
+  conv2 128->64 -> BN2d -> Dropout -> LReLU
+  conv2 64->1 -> ReLU                                  -> image [B,1,44,44] fp32
+Dropout masks come from Philox streams (expertsim/utils/philox.py), layer index 0..4.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from ... import hip
+from ...layers import Act, ConvOp, NormOp, Upsample, act_bwd, act_fwd, copy_act
+from ...utils import philox
+from ..base import ExpertModule, build_tree, get_module
+
+SLOPE = 0.1
+P_DROP = 0.2
+
+
+class GeneratorNeutron(ExpertModule):
+    def __init__(self, noise_dim, cond_dim, di_strength, in_strength, **kwargs):
+        super().__init__()
+        self.name = "Generator-neutron-1-original-architecture"
+        self.di_strength = di_strength
+        self.in_strength = in_strength
+        self.noise_dim, self.cond_dim = int(noise_dim), int(cond_dim)
+        self.image_shape = (44, 44)
+        build_tree(self, [
+            ("fc1.0", lambda: nn.Linear(self.noise_dim + self.cond_dim, 256)),
+            ("fc1.1", lambda: nn.BatchNorm1d(256)),
+            ("fc2.0", lambda: nn.Linear(256, 128 * 13 * 13)),
+            ("fc2.1", lambda: nn.BatchNorm1d(128 * 13 * 13)),
+            ("conv_layers.0", lambda: nn.Conv2d(128, 256, kernel_size=(3, 3))),
+            ("conv_layers.1", lambda: nn.BatchNorm2d(256)),
+            ("conv_layers.5", lambda: nn.Conv2d(256, 128, kernel_size=(3, 3))),
+            ("conv_layers.6", lambda: nn.BatchNorm2d(128)),
+            ("conv_layers.9", lambda: nn.Conv2d(128, 64, kernel_size=(2, 2))),
+            ("conv_layers.10", lambda: nn.BatchNorm2d(64)),
+            ("conv_layers.13", lambda: nn.Conv2d(64, 1, kernel_size=(2, 2))),
+        ])
+
+    # --------------------------------------------------------------------------- program
+    def program(self):
+        m = lambda n: get_module(self, n)
+        conv = lambda n, up=None: ConvOp(m(n).weight, m(n).bias, upsample=up)
+
+        def bn(n):
+            b = m(n)
+            return NormOp(hip.NORM_BN, b.weight, b.bias, running_mean=b.running_mean,
+                          running_var=b.running_var, momentum=b.momentum, eps=b.eps,
+                          num_batches=b.num_batches_tracked)
+        return {
+            "fc1": conv("fc1.0"), "bn1": bn("fc1.1"),
+            "fc2": conv("fc2.0"), "bn2": bn("fc2.1"),
+            "c0": conv("conv_layers.0", Upsample((13, 13), scale=(2, 2))), "bn3": bn("conv_layers.1"),
+            "c5": conv("conv_layers.5", Upsample((24, 24), scale=(2, 2))), "bn4": bn("conv_layers.6"),
+            "c9": conv("conv_layers.9"), "bn5": bn("conv_layers.10"),
+            "c13": conv("conv_layers.13"),
+        }
+
+    def _chain(self, seed, stream_base, layer, train):
+        d = hip.dropout_struct(P_DROP, seed, stream_base + layer, enabled=train)
+        return hip.chain_struct(hip.ACT_LRELU, SLOPE, d, dropout_first=True)
+
+    # --------------------------------------------------------------------------- forward
+    def fwd(self, noise: torch.Tensor, cond: torch.Tensor, seed=0, stream_base=0, train=True):
+        """noise [B,10] fp32, cond [B,9] fp32 (device) -> (image Act [B,1,44,44] fp32 NHWC, ctx)."""
+        o = self.ops()
+        cdt = self.compute_dtype
+        dev = noise.device
+        B = noise.shape[0]
+        x0 = Act.rows(B, self.noise_dim + self.cond_dim, cdt, dev)
+        x0m = x0.t.view(B, -1)
+        copy_act(Act.of(noise), Act.of(x0m[:, :self.noise_dim]))
+        copy_act(Act.of(cond), Act.of(x0m[:, self.noise_dim:]))
+        ch = [self._chain(seed, stream_base, i, train) for i in range(5)]
+        h1 = o["fc1"].fwd(x0)
+        y1, s1 = o["bn1"].fwd(h1, ch[0], train=train)
+        h2 = o["fc2"].fwd(y1)
+        y2, s2 = o["bn2"].fwd(h2, ch[1], train=train)
+        # [B, 21632] rows are NCHW [B,128,13,13]; re-layout to NHWC for the vector gather
+        y2n = Act.nhwc(B, 128, 13, 13, cdt, dev)
+        copy_act(Act(y2.t, (B, 128, 13, 13), (21632, 169, 13, 1)), y2n)
+        h3 = o["c0"].fwd(y2n)
+        y3, s3 = o["bn3"].fwd(h3, ch[2], train=train)
+        h4 = o["c5"].fwd(y3)
+        y4, s4 = o["bn4"].fwd(h4, ch[3], train=train)
+        h5 = o["c9"].fwd(y4)
+        y5, s5 = o["bn5"].fwd(h5, ch[4], train=train)
+        h6 = o["c13"].fwd(y5, out_dtype=torch.float32)
+        img = act_fwd(h6, hip.chain_struct(hip.ACT_RELU))
+        ctx = dict(x0=x0, h1=h1, y1=y1, s1=s1, h2=h2, y2=y2, s2=s2, y2n=y2n, h3=h3, y3=y3, s3=s3,
+                   h4=h4, y4=y4, s4=s4, h5=h5, y5=y5, s5=s5, h6=h6, ch=ch)
+        return img, ctx
+
+    # --------------------------------------------------------------------------- backward
+    def bwd(self, ctx, dimg: Act):
+        """Accumulate parameter gradients (flat grad buffer) for d loss / d image."""
+        o = self.ops()
+        cdt = self.compute_dtype
+        g = lambda n, a: getattr(get_module(self, n), a).grad
+        ch = ctx["ch"]
+        dh6 = act_bwd(ctx["h6"], hip.chain_struct(hip.ACT_RELU), dimg, dx_dtype=cdt)
+        o["c13"].wgrad(dh6, ctx["y5"], g("conv_layers.13", "weight"), g("conv_layers.13", "bias"))
+        dy5 = o["c13"].dgrad(dh6, ctx["y5"])
+        dh5 = o["bn5"].bwd(ctx["h5"], ctx["s5"], ch[4], dy5, dgamma=g("conv_layers.10", "weight"),
+                           dbeta=g("conv_layers.10", "bias"))
+        o["c9"].wgrad(dh5, ctx["y4"], g("conv_layers.9", "weight"), g("conv_layers.9", "bias"))
+        dy4 = o["c9"].dgrad(dh5, ctx["y4"])
+        dh4 = o["bn4"].bwd(ctx["h4"], ctx["s4"], ch[3], dy4, dgamma=g("conv_layers.6", "weight"),
+                           dbeta=g("conv_layers.6", "bias"))
+        o["c5"].wgrad(dh4, ctx["y3"], g("conv_layers.5", "weight"), g("conv_layers.5", "bias"))
+        dy3 = o["c5"].dgrad(dh4, ctx["y3"])
+        dh3 = o["bn3"].bwd(ctx["h3"], ctx["s3"], ch[2], dy3, dgamma=g("conv_layers.1", "weight"),
+                           dbeta=g("conv_layers.1", "bias"))
+        o["c0"].wgrad(dh3, ctx["y2n"], g("conv_layers.0", "weight"), g("conv_layers.0", "bias"))
+        dy2n = o["c0"].dgrad(dh3, ctx["y2n"])
+        B = dy2n.dims[0]
+        dy2 = Act.rows(B, 21632, cdt, dy2n.t.device)
+        copy_act(dy2n, Act(dy2.t, (B, 128, 13, 13), (21632, 169, 13, 1)))
+        dh2 = o["bn2"].bwd(ctx["h2"], ctx["s2"], ch[1], dy2, dgamma=g("fc2.1", "weight"),
+                           dbeta=g("fc2.1", "bias"))
+        o["fc2"].wgrad(dh2, ctx["y1"], g("fc2.0", "weight"), g("fc2.0", "bias"))
+        dy1 = o["fc2"].dgrad(dh2, ctx["y1"])
+        dh1 = o["bn1"].bwd(ctx["h1"], ctx["s1"], ch[0], dy1, dgamma=g("fc1.1", "weight"),
+                           dbeta=g("fc1.1", "bias"))
+        o["fc1"].wgrad(dh1, ctx["x0"], g("fc1.0", "weight"), g("fc1.0", "bias"))
+
+    # --------------------------------------------------------------------------- nn.Module API
+    def forward(self, noise, cond):
+        """Reference signature (generator.py:42): image [B,1,44,44]."""
+        from ..autograd import generator_apply
+        return generator_apply(self, noise, cond)

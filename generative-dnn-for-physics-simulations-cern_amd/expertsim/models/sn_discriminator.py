@@ -1,0 +1,170 @@
+"""Spectral-norm conv discriminator shared by both ZDC families.
+
+References: expertsim/models/neutron/discriminator.py:6-48 (44x44 input, flatten 16*9*9 = 1296)
+and expertsim/models/proton/discriminator.py:116-155 (56x30 input, second pool (2,1), flatten
+16*12*12 = 2304).  Each forward in train mode runs one spectral-norm power iteration per layer
+(torch.nn.utils.spectral_norm semantics) whose sigma divides the weight inside the GEMM weight
+packing, so no host sync and no extra weight pass.
+
+Program:
+  SNconv3 1->32 -> GN(8) -> LReLU -> maxpool 2x2
+  SNconv3 32->16 -> GN(8) -> LReLU -> maxpool pool2    -> written straight into the fc1 input
+                                                         rows in NCHW-flatten order, cond after it
+  SNlinear F+9->128 -> LN -> LReLU -> SNlinear 128->64 -> LN -> LReLU (= latent) -> SNlinear 64->1
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+from torch.nn.utils import spectral_norm
+
+from .. import hip
+from ..layers import Act, ConvOp, MaxPool, NormOp, SpectralNorm, channel_sum, copy_act
+from .base import ExpertModule, build_tree, get_module
+
+SLOPE = 0.1
+LAYERS = ("conv_layers.0", "conv_layers.4", "fc1.0", "fc2.0", "fc3")
+
+
+class SNDiscriminator(ExpertModule):
+    compute_dtype = torch.float32
+
+    def __init__(self, cond_dim, image_shape, pool2, **kwargs):
+        super().__init__()
+        self.cond_dim = int(cond_dim)
+        self.image_shape = tuple(image_shape)
+        self.pool2 = tuple(pool2)
+        H, W = self.image_shape
+        h1, w1 = (H - 2) // 2, (W - 2) // 2
+        self.feat_hw = ((h1 - 2 - pool2[0]) // pool2[0] + 1, (w1 - 2 - pool2[1]) // pool2[1] + 1)
+        self.flat_dim = 16 * self.feat_hw[0] * self.feat_hw[1]
+        build_tree(self, [
+            ("conv_layers.0", lambda: spectral_norm(nn.Conv2d(1, 32, kernel_size=3))),
+            ("conv_layers.1", lambda: nn.GroupNorm(8, 32)),
+            ("conv_layers.4", lambda: spectral_norm(nn.Conv2d(32, 16, kernel_size=3))),
+            ("conv_layers.5", lambda: nn.GroupNorm(8, 16)),
+            ("fc1.0", lambda: spectral_norm(nn.Linear(self.flat_dim + self.cond_dim, 128))),
+            ("fc1.1", lambda: nn.LayerNorm(128)),
+            ("fc2.0", lambda: spectral_norm(nn.Linear(128, 64))),
+            ("fc2.1", lambda: nn.LayerNorm(64)),
+            ("fc3", lambda: spectral_norm(nn.Linear(64, 1))),
+        ])
+
+    def program(self):
+        m = lambda n: get_module(self, n)
+        ops = {}
+        for n in LAYERS:
+            mod = m(n)
+            ops[n] = ConvOp(mod.weight_orig, mod.bias)
+            ops["sn:" + n] = SpectralNorm(mod)
+        ops["gn1"] = NormOp(hip.NORM_GN, m("conv_layers.1").weight, m("conv_layers.1").bias, groups=8)
+        ops["gn2"] = NormOp(hip.NORM_GN, m("conv_layers.5").weight, m("conv_layers.5").bias, groups=8)
+        ops["ln1"] = NormOp(hip.NORM_LN, m("fc1.1").weight, m("fc1.1").bias)
+        ops["ln2"] = NormOp(hip.NORM_LN, m("fc2.1").weight, m("fc2.1").bias)
+        ops["pool1"] = MaxPool(2)
+        ops["pool2"] = MaxPool(self.pool2)
+        return ops
+
+    # --------------------------------------------------------------------------- forward
+    def fwd(self, img: Act, cond: torch.Tensor, train=True):
+        """img Act [B,1,H,W] (any dtype), cond [B,9] fp32 -> (out [B,1] fp32, latent [B,64] fp32, ctx)."""
+        o = self.ops()
+        cdt = self.compute_dtype
+        dev = cond.device
+        B = img.dims[0]
+        lr = hip.chain_struct(hip.ACT_LRELU, SLOPE)
+        x = img
+        if img.t.dtype != cdt:
+            x = img.like_nhwc(cdt)
+            copy_act(img, x)
+        sig = {n: o["sn:" + n].sigma(update=train) for n in LAYERS}
+        inv = lambda n: sig[n][0]
+        h1 = o["conv_layers.0"].fwd(x, inv_scale=inv("conv_layers.0"))
+        y1, s1 = o["gn1"].fwd(h1, lr)
+        p1, i1 = o["pool1"].fwd(y1)
+        h2 = o["conv_layers.4"].fwd(p1, inv_scale=inv("conv_layers.4"))
+        y2, s2 = o["gn2"].fwd(h2, lr)
+        F = self.flat_dim + self.cond_dim
+        fh, fw = self.feat_hw
+        X = Act.rows(B, F, cdt, dev)
+        Xm = X.t.view(B, F)
+        feat = Act(Xm, (B, 16, fh, fw), (F, fh * fw, fw, 1))       # NCHW flatten order (view(B,-1))
+        _, i2 = o["pool2"].fwd(y2, out=feat)
+        copy_act(Act.of(cond), Act.of(Xm[:, self.flat_dim:]))
+        h3 = o["fc1.0"].fwd(X, inv_scale=inv("fc1.0"))
+        y3, s3 = o["ln1"].fwd(h3, lr)
+        h4 = o["fc2.0"].fwd(y3, inv_scale=inv("fc2.0"))
+        lat, s4 = o["ln2"].fwd(h4, lr, out_dtype=torch.float32)
+        lat_c = lat
+        if cdt != torch.float32:
+            lat_c = lat.like_nhwc(cdt)
+            copy_act(lat, lat_c)
+        out = o["fc3"].fwd(lat_c, inv_scale=inv("fc3"), out_dtype=torch.float32)
+        ctx = dict(x=x, sig=sig, h1=h1, y1=y1, s1=s1, p1=p1, i1=i1, h2=h2, y2=y2, s2=s2, i2=i2, X=X,
+                   feat_dims=(B, 16, fh, fw), h3=h3, y3=y3, s3=s3, h4=h4, s4=s4, lat=lat_c)
+        return out, lat, ctx
+
+    # --------------------------------------------------------------------------- backward
+    def bwd(self, ctx, dout: Act = None, dlat: Act = None, weight_grads=True, input_grad=True):
+        """dout [B,1] fp32 (or None), dlat [B,64] fp32 (or None).  Returns d image (fp32 Act) or None."""
+        o = self.ops()
+        cdt = self.compute_dtype
+        dev = ctx["X"].t.device
+        B = ctx["X"].dims[0]
+        lr = hip.chain_struct(hip.ACT_LRELU, SLOPE)
+        m = lambda n: get_module(self, n)
+        sig = ctx["sig"]
+
+        def wgrad(name, dy, x):
+            if not weight_grads:
+                return
+            mod = m(name)
+            op = o[name]
+            g_sn = torch.empty_like(mod.weight_orig)
+            op.wgrad(dy, x, g_sn, None, beta=0.0)          # grad of W/sigma
+            channel_sum(dy, mod.bias.grad, beta=1.0)        # bias is not normalised
+            o["sn:" + name].bwd(g_sn, sig[name], mod.weight_orig.grad, beta=1.0)
+
+        # latent gradient: dlat (SDI) + fc3^T dout
+        dl = Act.rows(B, 64, cdt, dev, zero=True)
+        if dlat is not None:
+            copy_act(dlat, dl)
+        if dout is not None:
+            dout_c = dout
+            if cdt != torch.float32:
+                dout_c = dout.like_nhwc(cdt)
+                copy_act(dout, dout_c)
+            wgrad("fc3", dout_c, ctx["lat"])
+            o["fc3"].dgrad(dout_c, ctx["lat"], inv_scale=sig["fc3"][0], dx=dl, beta=1.0)
+        dh4 = o["ln2"].bwd(ctx["h4"], ctx["s4"], lr, dl,
+                           dgamma=m("fc2.1").weight.grad if weight_grads else None,
+                           dbeta=m("fc2.1").bias.grad if weight_grads else None)
+        wgrad("fc2.0", dh4, ctx["y3"])
+        dy3 = o["fc2.0"].dgrad(dh4, ctx["y3"], inv_scale=sig["fc2.0"][0])
+        dh3 = o["ln1"].bwd(ctx["h3"], ctx["s3"], lr, dy3,
+                           dgamma=m("fc1.1").weight.grad if weight_grads else None,
+                           dbeta=m("fc1.1").bias.grad if weight_grads else None)
+        wgrad("fc1.0", dh3, ctx["X"])
+        dX = o["fc1.0"].dgrad(dh3, ctx["X"], inv_scale=sig["fc1.0"][0])
+        F = self.flat_dim + self.cond_dim
+        B_, Cf, fh, fw = ctx["feat_dims"]
+        dfeat = Act(dX.t.view(B, F), (B, 16, fh, fw), (F, fh * fw, fw, 1))
+        dy2 = o["pool2"].bwd(dfeat, ctx["i2"], ctx["y2"].dims, cdt)
+        dh2 = o["gn2"].bwd(ctx["h2"], ctx["s2"], lr, dy2,
+                           dgamma=m("conv_layers.5").weight.grad if weight_grads else None,
+                           dbeta=m("conv_layers.5").bias.grad if weight_grads else None)
+        wgrad("conv_layers.4", dh2, ctx["p1"])
+        dp1 = o["conv_layers.4"].dgrad(dh2, ctx["p1"], inv_scale=sig["conv_layers.4"][0])
+        dy1 = o["pool1"].bwd(dp1, ctx["i1"], ctx["y1"].dims, cdt)
+        dh1 = o["gn1"].bwd(ctx["h1"], ctx["s1"], lr, dy1,
+                           dgamma=m("conv_layers.1").weight.grad if weight_grads else None,
+                           dbeta=m("conv_layers.1").bias.grad if weight_grads else None)
+        wgrad("conv_layers.0", dh1, ctx["x"])
+        if not input_grad:
+            return None
+        return o["conv_layers.0"].dgrad(dh1, ctx["x"], inv_scale=sig["conv_layers.0"][0],
+                                        dx_dtype=torch.float32)
+
+    def forward(self, img, cond):
+        from .autograd import discriminator_apply
+        return discriminator_apply(self, img, cond)

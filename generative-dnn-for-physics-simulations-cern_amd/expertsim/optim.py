@@ -1,0 +1,55 @@
+"""Fused Adam over a model's flat parameter buffer (one HIP launch per model per step).
+
+Drop-in for the ``torch.optim.Adam(module.parameters(), lr=...)`` objects the reference creates
+in expertsim/train/training_setup.py:20-40 and steps in moe.py:439,526,565,566: same
+hyper-parameters (betas 0.9/0.999, eps 1e-8, no weight decay), same update rule as torch's
+single-tensor Adam, ``zero_grad`` / ``step`` / ``state_dict`` API.  Moments live in two flat
+buffers whose per-parameter views are exposed as ``state[p]['exp_avg' / 'exp_avg_sq']``.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import hip
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, module, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        if weight_decay != 0.0:
+            raise NotImplementedError("the reference uses weight_decay=0")
+        self.module = module
+        super().__init__(list(module.parameters()), dict(lr=lr, betas=betas, eps=eps, weight_decay=0.0))
+        self._m = self._v = None
+        self._step = 0
+
+    def _buffers(self):
+        flat = self.module.flat_params
+        if self._m is None or self._m.numel() != flat.numel() or self._m.device != flat.device:
+            self._m = torch.zeros_like(flat)
+            self._v = torch.zeros_like(flat)
+            o = 0
+            for p in self.module.parameters():
+                n = p.numel()
+                self.state[p] = {"step": torch.tensor(float(self._step)),
+                                 "exp_avg": self._m[o:o + n].view_as(p),
+                                 "exp_avg_sq": self._v[o:o + n].view_as(p)}
+                o += n
+        return flat
+
+    def zero_grad(self, set_to_none: bool = True):
+        # the flat gradient buffer is kept (views stay valid); zeroing is one memset
+        self.module.zero_grads()
+
+    @torch.no_grad()
+    def step(self, closure=None, grad_scale: float = 1.0):
+        flat = self._buffers()
+        self._step += 1
+        g = self.param_groups[0]
+        b1, b2 = g["betas"]
+        hip.call("es_adam", hip.ptr(flat), hip.ptr(self.module.flat_grads), hip.ptr(self._m), hip.ptr(self._v),
+                 flat.numel(), float(g["lr"]), float(b1), float(b2), float(g["eps"]), self._step,
+                 float(grad_scale), hip.stream_ptr())
+        for p in self.module.parameters():
+            self.state[p]["step"] = torch.tensor(float(self._step))
+        self.module.invalidate()
+        return None

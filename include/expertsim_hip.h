@@ -1,0 +1,249 @@
+/*
+ * expertsim_hip.h — C ABI of the MI355X (gfx950) kernels behind the expertsim GAN training step.
+ *
+ * The reference (patrick-bedkowski/Generative-DNN-for-Physics-Simulations-CERN) has no FFI: its
+ * hot path is PyTorch ATen ops dispatched from Python.  This header is the boundary the build
+ * puts underneath the reference's own Python API (expertsim.models.* forward signatures and
+ * MoEWrapper.train_step); each entry point replaces the ATen ops named at it,
+ * with the reference call site cited as file:line (paths relative to the reference root).
+ *
+ * Conventions
+ *  - every pointer is a DEVICE pointer unless the comment says otherwise; kernels never allocate,
+ *    free or synchronise; everything is enqueued on `stream` (a hipStream_t);
+ *  - tensors are described logically as (n, c, h, w) with element strides s[4] — the device layout
+ *    (NHWC for conv activations, [rows][features] for linear activations) is the caller's choice;
+ *  - return 0 (ES_OK) or an error code; es_last_error() gives the message (thread-local);
+ *  - dtypes: ES_F32 (fp32 parity mode) and ES_BF16 (bf16 operands, fp32 accumulation).
+ */
+#ifndef EXPERTSIM_HIP_H
+#define EXPERTSIM_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum { ES_F32 = 0, ES_BF16 = 1 } es_dtype_t;
+enum { ES_OK = 0, ES_ERR_ARG = 1, ES_ERR_HIP = 2, ES_ERR_UNSUPPORTED = 3 };
+enum { ES_ACT_NONE = 0, ES_ACT_RELU = 1, ES_ACT_LRELU = 2 };
+enum { ES_NORM_NONE = 0, ES_NORM_BN = 1, ES_NORM_GN = 2, ES_NORM_LN = 3 };
+
+typedef void* es_stream_t; /* hipStream_t */
+
+/* Logical 4-D view: element (n,c,h,w) lives at base + n*s[0] + c*s[1] + h*s[2] + w*s[3]. */
+typedef struct {
+  int n, c, h, w;
+  int64_t s[4];
+} es_view_t;
+
+/* Counter-based dropout (expertsim/utils/philox.py).  keep(i) = (philox(seed, stream, i) >> 8) <
+ * threshold, i = NCHW-logical element index; kept values are multiplied by `scale` = 1/(1-p). */
+typedef struct {
+  uint64_t seed;
+  uint32_t stream;
+  uint32_t threshold;
+  float scale;
+  int enabled;
+} es_dropout_t;
+
+const char* es_last_error(void);
+int es_version(void);
+int es_device_sync(void); /* hipDeviceSynchronize, for tests only */
+
+/* ------------------------------------------------------------------------------------------
+ * Convolution / linear as MFMA implicit GEMM.
+ * Replaces aten::convolution / convolution_backward and aten::addmm / mm for nn.Conv2d and
+ * nn.Linear (neutron/generator.py:11,17,24,29,33,37; neutron/discriminator.py:12,17,27,33,39;
+ * neutron/aux_reg.py:13,20,27,34,45,68; proton/generator.py:14,19,27,33,38,41;
+ * proton/discriminator.py:122,127,134,140,146; proton/aux_reg.py:20-30,61,104-117;
+ * routers/router.py:12-19).  A Linear layer is the 1x1 convolution of a 1x1 image.
+ * The nearest upsample feeding a generator conv (neutron/generator.py:23,29;
+ * proton/generator.py:26,32) is folded into the input gather through hmap/wmap.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct {
+  int N, C, H, W;   /* conv input (before upsample): batch, in-channels, height, width      */
+  int Hu, Wu;       /* conv input after nearest upsample (== H, W when hmap/wmap are NULL)   */
+  int K, P, Q;      /* out-channels, output height, output width                             */
+  int R, S;         /* kernel height, width                                                  */
+  int stride, pad;
+  const int32_t* hmap; /* device [Hu]: source row of upsampled row (torch nearest), or NULL  */
+  const int32_t* wmap; /* device [Wu]                                                        */
+} es_conv_desc_t;
+
+/* y[n,k,p,q] = bias[k] + sum_{c,r,s} xu[n,c,p*stride-pad+r,q*stride-pad+s] * W[k,c,r,s]
+ * wk: packed weights [K][R][S][C] of dtype dt (es_pack_conv_weight, mode 0). bias may be NULL. */
+int es_conv2d_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x, const int64_t xs[4],
+                  const void* wk, const float* bias, void* y, es_dtype_t ydt, const int64_t ys[4],
+                  es_stream_t stream);
+/* dxu[n,c,hu,wu] = sum_{k,r,s} dy[n,k,p,q] * W[k,c,r,s] over (hu+pad-r) = p*stride, ...
+ * (gradient w.r.t. the UPSAMPLED input; es_upsample_bwd folds it to the source grid).
+ * wd: packed weights [C][R][S][K] (es_pack_conv_weight, mode 1).  beta=1 accumulates into dxu. */
+int es_conv2d_dgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, const int64_t ys[4],
+                    const void* wd, void* dxu, es_dtype_t dxdt, const int64_t dxs[4], float beta,
+                    es_stream_t stream);
+/* dw[k][r][s][c] += sum_{n,p,q} dy[n,k,p,q] * xu[n,c,...]   (fp32, split-K with atomics: the
+ * caller zeroes dw first; es_unpack_conv_grad converts to torch's [K][C][R][S]). */
+int es_conv2d_wgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, const int64_t ys[4],
+                    const void* x, const int64_t xs[4], float* dw, es_stream_t stream);
+
+/* Weight packing for the implicit GEMM (fp32 master [K][C][R][S] -> dt).
+ * mode 0: out[k][r][s][c] = w*scale ; mode 1: out[c][r][s][k] = w*scale.
+ * scale = (inv_scale ? 1/inv_scale[0] : 1)  — the spectral-norm division W/sigma
+ * (torch.nn.utils.spectral_norm compute_weight) is folded here.
+ * col_perm (optional, device [C*R*S] for R=S=1 linears): input column index permutation. */
+int es_pack_conv_weight(const float* w, int K, int C, int R, int S, int mode,
+                        const float* inv_scale, const int32_t* col_perm, void* out, es_dtype_t dt,
+                        es_stream_t stream);
+/* grad[k][c][r][s] = beta*grad + dw[k][r][s][c] * (inv_scale ? 1/inv_scale[0] : 1) */
+int es_unpack_conv_grad(const float* dw, int K, int C, int R, int S, const int32_t* col_perm,
+                        float* grad, float beta, es_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Normalisation + dropout + activation (aten::native_batch_norm / native_group_norm /
+ * native_layer_norm, aten::bernoulli_ + mul (nn.Dropout), leaky_relu / relu and their
+ * backward).  One fused elementwise pass forward, reductions + one pass backward.
+ * Stats groups: BN -> channel c (count N*H*W), GN -> (n, c / (C/groups)), LN -> n (count C*H*W).
+ * gamma/beta index: BN/GN -> c; LN -> (c*H + h)*W + w.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct {
+  int kind;            /* ES_NORM_*                                                       */
+  int groups;          /* GN only                                                         */
+  const float* mean;   /* per stats group                                                 */
+  const float* invstd; /* per stats group                                                 */
+  const float* gamma;  /* may be NULL (identity)                                          */
+  const float* beta;   /* may be NULL                                                     */
+} es_norm_t;
+
+typedef struct {
+  es_dropout_t drop;
+  int dropout_first; /* 1: act(drop(norm(x)))  [generator.py:13-15]; 0: drop(act(norm(x))) [aux_reg.py:15-17] */
+  int act;           /* ES_ACT_*                                                          */
+  float slope;       /* LeakyReLU negative slope (0.1 everywhere in the reference)        */
+} es_chain_t;
+
+/* Batch statistics of x (train-mode BN / GN / LN), written to mean/invstd per stats group.
+ * For BN, running_mean/var (may be NULL) are updated with `momentum` and the unbiased
+ * variance, as torch does.  ws: workspace of es_norm_stats_ws_bytes() bytes. */
+int64_t es_norm_stats_ws_bytes(const es_view_t* x, int kind, int groups);
+int es_norm_stats(const es_view_t* x, es_dtype_t xdt, const void* xp, int kind, int groups,
+                  float eps, float* mean, float* invstd, float* running_mean, float* running_var,
+                  float momentum, void* ws, es_stream_t stream);
+/* y = chain(norm(x) [+ addend]) ; addend may be NULL (residual add of proton/aux_reg.py:130) */
+int es_norm_act_fwd(const es_view_t* x, es_dtype_t xdt, const es_norm_t* nm, const es_chain_t* ch,
+                    const es_view_t* addend, es_dtype_t adt, const void* addend_ptr, const void* xp,
+                    const es_view_t* y, es_dtype_t ydt, void* yp, es_stream_t stream);
+/* Backward of es_norm_act_fwd.  dy: gradient of y.  act_ref (optional): evaluate the activation
+ * derivative on this stored tensor (the block output) instead of the recomputed pre-activation.
+ * Writes dx (beta=1 accumulates), accumulates dgamma/dbeta (fp32, may be NULL). */
+int64_t es_norm_bwd_ws_bytes(const es_view_t* x, int kind, int groups);
+int es_norm_act_bwd(const es_view_t* x, es_dtype_t xdt, const void* xp, const es_norm_t* nm,
+                    const es_chain_t* ch, const es_view_t* dy, es_dtype_t dydt, const void* dyp,
+                    const es_view_t* act_ref, es_dtype_t rdt, const void* refp,
+                    const es_view_t* dx, es_dtype_t dxdt, void* dxp, float beta, float* dgamma,
+                    float* dbeta, void* ws, es_stream_t stream);
+
+/* Plain elementwise chain without normalisation (router LeakyReLU, final ReLU, casts):
+ * y = chain(x). And its backward dx = beta*dx + dchain(dy) evaluated at x (or act_ref). */
+int es_act_fwd(const es_view_t* x, es_dtype_t xdt, const void* xp, const es_chain_t* ch,
+               const es_view_t* y, es_dtype_t ydt, void* yp, es_stream_t stream);
+
+/* Per-channel sum over (n,h,w): out[c] = beta*out[c] + sum x (conv/linear bias gradients). */
+int64_t es_channel_sum_ws_bytes(const es_view_t* x);
+int es_channel_sum(const es_view_t* x, es_dtype_t xdt, const void* xp, float* out, float beta,
+                   void* ws, es_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Pooling / resampling / layout (aten::max_pool2d_with_indices(+_backward),
+ * upsample_nearest2d_backward, adaptive_avg_pool2d, cat, copy_)
+ * ---------------------------------------------------------------------------------------- */
+/* max pool, kernel (kh,kw), stride (sh,sw), no padding, floor mode; idx: uint8 window argmax
+ * (first max in row-major window order, as torch). */
+int es_maxpool_fwd(const es_view_t* x, es_dtype_t dt, const void* xp, int kh, int kw, int sh, int sw,
+                   const es_view_t* y, void* yp, uint8_t* idx, es_stream_t stream);
+int es_maxpool_bwd(const es_view_t* dy, es_dtype_t dt, const void* dyp, const uint8_t* idx, int kh,
+                   int kw, int sh, int sw, const es_view_t* dx, void* dxp, float beta,
+                   es_stream_t stream);
+/* dx[n,c,h,w] = beta*dx + sum over upsampled positions mapping to (h,w).  hstart/hcount (device
+ * [H]) and wstart/wcount (device [W]) describe the contiguous preimage of each source row/col. */
+int es_upsample_bwd(const es_view_t* dxu, es_dtype_t dt, const void* dxup, const int32_t* hstart,
+                    const int32_t* hcount, const int32_t* wstart, const int32_t* wcount,
+                    const es_view_t* dx, es_dtype_t dxdt, void* dxp, float beta, es_stream_t stream);
+/* y = alpha*x (+ beta*y) elementwise between any two views of equal logical shape (also casts) */
+int es_copy(const es_view_t* x, es_dtype_t xdt, const void* xp, const es_view_t* y, es_dtype_t ydt,
+            void* yp, float alpha, float beta, es_stream_t stream);
+/* global average pool over (h,w): y[n,c] (view (N,C,1,1)) and its backward */
+int es_avgpool_fwd(const es_view_t* x, es_dtype_t dt, const void* xp, const es_view_t* y, void* yp,
+                   es_stream_t stream);
+int es_avgpool_bwd(const es_view_t* dy, const void* dyp, const es_view_t* dx, es_dtype_t dxdt,
+                   void* dxp, float beta, es_stream_t stream);
+/* rows gathered by index: dst[i,:] = src[idx[i],:] (fp32 rows of `cols`); idx NULL = identity */
+int es_gather_rows(const float* src, int64_t src_ld, const int32_t* idx, int rows, int cols,
+                   float* dst, int64_t dst_ld, es_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Spectral norm (torch.nn.utils.spectral_norm, n_power_iterations=1, eps=1e-12) for every
+ * discriminator layer (neutron/discriminator.py:12,17,27,33,39; proton/discriminator.py:122,
+ * 127,134,140,146).  One power iteration updates u,v in place and writes sigma = u.(W v).
+ * ---------------------------------------------------------------------------------------- */
+int es_sn_power_iter(const float* w, int h, int wd, float* u, float* v, float* sigma, int update,
+                     es_stream_t stream);
+/* dW_orig = beta*dW_orig + G/sigma - (<G, W>/sigma^2) u v^T   (G = grad of W/sigma) */
+int es_sn_bwd(const float* w, const float* g, int h, int wd, const float* u, const float* v,
+              const float* sigma, float* dw_orig, float beta, es_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Losses (moe.py:506-642, proton/aux_reg.py:42-45, train/utils.py:623-642) and their gradients.
+ * ---------------------------------------------------------------------------------------- */
+/* Discriminator hinge (moe.py:518-523): out[0] = w*(mean relu(1-ro) + mean relu(1+fo));
+ * dro/dfo = gradients of out[0].  w is read from device memory (w_ptr[0]) to avoid host syncs. */
+int es_hinge_d(const float* ro, const float* fo, int n, const float* w_ptr, float* out, float* dro,
+               float* dfo, es_stream_t stream);
+/* per-sample photon sum s[b] = sum_{h,w} (exp(x)-1) of the generated image (moe.py:611-616) */
+int es_image_expsum(const es_view_t* x, es_dtype_t dt, const void* xp, float* s, es_stream_t stream);
+/* Generator-step losses (moe.py:544-563): gen hinge, SDI diversity, intensity L1, log-cosh aux,
+ * weighted by w.  Writes out[0..7] = {total, gen_hinge, div, intensity, aux, std_int, mean_int, w}
+ * and gradients: dfo[n], dl1/dl2 [n,L], dcoord [n,2], coef[n] (= d total / d s[b]). */
+typedef struct {
+  int n, latent, noise;
+  float di_strength, in_strength, aux_strength;
+} es_gen_loss_t;
+int es_gen_losses(const es_gen_loss_t* p, const float* fo, const float* l1, const float* l2,
+                  const float* n1, const float* n2, const float* std_, const float* s,
+                  const float* intensity, const float* coord, const float* pos, const float* w_ptr,
+                  float* out, float* dfo, float* dl1, float* dl2, float* dcoord, float* coef,
+                  es_stream_t stream);
+/* dimg[b,..] = beta*dimg + coef[b]*exp(x)   (intensity-term gradient of the generated image) */
+int es_image_expsum_bwd(const es_view_t* x, es_dtype_t dt, const void* xp, const float* coef,
+                        const es_view_t* dx, void* dxp, float beta, es_stream_t stream);
+
+/* Router tail (routers/router.py:23 gumbel_softmax, moe.py:97-103 argmax/bincount):
+ * gates = softmax((logits - log(e))/tau); idx = argmax; counts[E] (int32) */
+int es_router_gumbel(const float* logits, const float* expo, int B, int E, float tau, float* gates,
+                     int32_t* idx, int32_t* counts, es_stream_t stream);
+/* Router loss gradient w.r.t. logits for the ALB term (train/utils.py:623-642, moe.py:407,429)
+ * and the loss value: out[0] = coef*mean_e exp(1/(S_e+1e-6)), S_e = sum_b gates[b,e]. */
+int es_router_alb(const float* gates, int B, int E, float tau, float coef, float* out,
+                  float* dlogits, es_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Optimizer (torch.optim.Adam, created at train/training_setup.py:20-40, stepped at
+ * moe.py:439,526,565,566): one launch over a flat fp32 parameter buffer.
+ * ---------------------------------------------------------------------------------------- */
+int es_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+            float beta2, float eps, int step, float grad_scale, es_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Random numbers (torch.randn at moe.py:144,535; exponential_ inside F.gumbel_softmax):
+ * Philox4x32-10 + Box-Muller, counter = element index.
+ * ---------------------------------------------------------------------------------------- */
+int es_randn(float* out, int64_t n, uint64_t seed, uint32_t stream_id, es_stream_t stream);
+int es_rand_exponential(float* out, int64_t n, uint64_t seed, uint32_t stream_id,
+                        es_stream_t stream);
+/* dropout mask materialisation (tests): out[i] = keep(i) */
+int es_dropout_mask(uint8_t* out, int64_t n, const es_dropout_t* d, es_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EXPERTSIM_HIP_H */

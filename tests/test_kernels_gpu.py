@@ -1,0 +1,240 @@
+"""HIP kernel unit tests: each kernel against a plain PyTorch fp32 CPU reference of the same op.
+
+Tolerances (fp32 mode): MFMA f32 is an exact fp32 FMA chain, so conv/linear results agree with
+torch's CPU fp32 to within summation-order rounding: rel <= 2e-5 of max|ref| (K up to 4608).
+bf16 mode: rel <= 2e-2 of max|ref| (bf16 operands, fp32 accumulation).
+Dropout masks are integer-exact against the host Philox restatement.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _hip():
+    from expertsim import hip
+    hip.lib()
+    return hip
+
+
+def to_act(x_nchw, dtype=torch.float32):
+    from expertsim.layers import Act
+    N, Cc, H, W = x_nchw.shape
+    a = Act.nhwc(N, Cc, H, W, dtype, DEV)
+    a.t.copy_(x_nchw.permute(0, 2, 3, 1).reshape(-1).to(dtype))
+    return a
+
+
+def from_act(a):
+    return a.torch_nchw().float().cpu()
+
+
+def rel(a, b):
+    return float((a - b).abs().max() / max(b.abs().max().item(), 1e-12))
+
+
+CONV_CASES = [
+    # (N, Cin, H, W, Cout, k, stride, pad, upsample(scale or size) or None)
+    (2, 128, 13, 13, 256, 3, 1, 0, (2, 2)),       # neutron G conv_layers.0 (after up x2)
+    (2, 256, 24, 24, 128, 3, 1, 0, (2, 2)),       # neutron G conv_layers.5
+    (3, 128, 46, 46, 64, 2, 1, 0, None),          # neutron G conv_layers.9
+    (3, 64, 45, 45, 1, 2, 1, 0, None),            # neutron G conv_layers.13
+    (2, 1, 44, 44, 32, 3, 1, 0, None),            # D / A first conv (Cin = 1)
+    (2, 32, 21, 21, 16, 3, 1, 0, None),           # D conv_layers.4
+    (2, 1, 56, 30, 32, 5, 2, 1, None),            # proton A conv1 (stride 2, pad 1)
+    (2, 32, 26, 13, 32, 5, 2, 2, None),           # proton A res conv1
+    (2, 32, 26, 13, 64, 1, 2, 0, None),           # proton A downsample 1x1 s2
+    (2, 256, 35, 19, 128, 4, 1, 1, "56x30"),      # proton G conv_layers.5 (resize 35x19 -> 56x30)
+    (2, 512, 18, 10, 256, 4, 1, 1, (2, 2)),       # proton G conv_layers.1
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conv_fwd_dgrad_wgrad(case, dtype):
+    _hip()
+    from expertsim.layers import ConvOp, Upsample, Act
+    N, Cin, H, W, Cout, k, st, pad, up = case
+    torch.manual_seed(0)
+    x = torch.randn(N, Cin, H, W)
+    w = (torch.randn(Cout, Cin, k, k) / np.sqrt(Cin * k * k)).requires_grad_(True)
+    b = torch.randn(Cout).requires_grad_(True)
+    xr = x.clone().requires_grad_(True)
+    if up is None:
+        xu, upsample = xr, None
+    elif up == "56x30":
+        xu, upsample = F.interpolate(xr, size=(56, 30), mode="nearest"), Upsample((H, W), out_hw=(56, 30))
+    else:
+        xu, upsample = F.interpolate(xr, scale_factor=up, mode="nearest"), Upsample((H, W), scale=up)
+    y = F.conv2d(xu, w, b, st, pad)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    wp = torch.nn.Parameter(w.detach().to(DEV))
+    bp = torch.nn.Parameter(b.detach().to(DEV))
+    op = ConvOp(wp, bp, stride=st, pad=pad, upsample=upsample)
+    xa = to_act(x, dtype)
+    ya = op.fwd(xa, out_dtype=torch.float32)
+    tol = 3e-5 if dtype == torch.float32 else 3e-2
+    assert ya.dims == tuple(y.shape)
+    assert rel(from_act(ya), y.detach()) < tol
+    gya = to_act(gy, dtype)
+    dxa = op.dgrad(gya, xa, dx_dtype=torch.float32)
+    assert rel(from_act(dxa), xr.grad) < tol
+    dw = torch.zeros(Cout, Cin, k, k, device=DEV)
+    db = torch.zeros(Cout, device=DEV)
+    op.wgrad(gya, xa, dw, db, beta=1.0)
+    assert rel(dw.cpu(), w.grad) < tol
+    assert rel(db.cpu(), b.grad) < tol
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_linear_as_conv(dtype):
+    _hip()
+    from expertsim.layers import Act, ConvOp
+    torch.manual_seed(1)
+    for (B, fin, fout) in [(8, 19, 256), (64, 256, 21632), (5, 1305, 128), (7, 64, 1), (3, 9, 128)]:
+        x = torch.randn(B, fin)
+        w = torch.randn(fout, fin).requires_grad_(True) / np.sqrt(fin)
+        w = w.detach().requires_grad_(True)
+        b = torch.randn(fout).requires_grad_(True)
+        xr = x.clone().requires_grad_(True)
+        y = F.linear(xr, w, b)
+        gy = torch.randn_like(y)
+        y.backward(gy)
+        op = ConvOp(torch.nn.Parameter(w.detach().to(DEV)), torch.nn.Parameter(b.detach().to(DEV)))
+        xa = Act.of(x.to(DEV, dtype).contiguous())
+        ya = op.fwd(xa, out_dtype=torch.float32)
+        tol = 3e-5 if dtype == torch.float32 else 3e-2
+        assert rel(ya.rows2d().cpu(), y.detach()) < tol
+        gya = Act.of(gy.to(DEV, dtype).contiguous())
+        dxa = op.dgrad(gya, xa, dx_dtype=torch.float32)
+        assert rel(dxa.rows2d().cpu(), xr.grad) < tol
+        dw = torch.zeros(fout, fin, device=DEV)
+        db = torch.zeros(fout, device=DEV)
+        op.wgrad(gya, xa, dw, db, beta=1.0)
+        assert rel(dw.cpu(), w.grad) < tol
+        assert rel(db.cpu(), b.grad) < tol
+
+
+def _chain_ref(y, p, mask, act, dropout_first):
+    lre = (lambda t: F.leaky_relu(t, 0.1)) if act == "lrelu" else (F.relu if act == "relu" else (lambda t: t))
+    if mask is None:
+        return lre(y)
+    scale = torch.tensor(1.0) / torch.tensor(1.0 - p)
+    if dropout_first:
+        return lre(y * (mask.float() * scale))
+    return lre(y) * (mask.float() * scale)
+
+
+@pytest.mark.parametrize("kind", ["bn2d", "bn1d", "gn", "ln"])
+@pytest.mark.parametrize("drop", [False, True])
+def test_norm_chain(kind, drop):
+    hip = _hip()
+    from expertsim.layers import Act, NormOp
+    from expertsim.utils import philox
+    torch.manual_seed(2)
+    if kind == "bn2d":
+        x = torch.randn(4, 32, 9, 7) * 3 + 1.5
+    elif kind == "gn":
+        x = torch.randn(3, 32, 6, 5) * 2 - 1
+    else:
+        x = torch.randn(6, 300) * 2 + 0.5
+    gamma = torch.rand(x.shape[1]) + 0.5
+    beta = torch.randn(x.shape[1])
+    p, seed, stream = 0.2, 1234, 77
+    mask = torch.from_numpy(philox.dropout_mask(tuple(x.shape), p, seed, stream)) if drop else None
+    xr = x.clone().requires_grad_(True)
+    g_, b_ = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    rm, rv = torch.zeros(x.shape[1]), torch.ones(x.shape[1])
+    if kind.startswith("bn"):
+        z = F.batch_norm(xr, rm, rv, g_, b_, True, 0.1, 1e-5)
+        nk = hip.NORM_BN
+    elif kind == "gn":
+        z = F.group_norm(xr, 8, g_, b_, 1e-5)
+        nk = hip.NORM_GN
+    else:
+        z = F.layer_norm(xr, (x.shape[1],), g_, b_, 1e-5)
+        nk = hip.NORM_LN
+    y = _chain_ref(z, p, mask, "lrelu", True)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    xa = to_act(x) if x.dim() == 4 else Act.of(x.to(DEV).contiguous())
+    dg = torch.zeros_like(gamma, device=DEV)
+    dbt = torch.zeros_like(beta, device=DEV)
+    rmd, rvd = torch.zeros(x.shape[1], device=DEV), torch.ones(x.shape[1], device=DEV)
+    op = NormOp(nk, gamma.to(DEV), beta.to(DEV), groups=8, running_mean=rmd, running_var=rvd)
+    d = hip.dropout_struct(p, seed, stream, enabled=drop)
+    ch = hip.chain_struct(hip.ACT_LRELU, 0.1, d, dropout_first=True)
+    ya, stats = op.fwd(xa, ch)
+    out = from_act(ya) if x.dim() == 4 else ya.rows2d().cpu()
+    assert rel(out, y.detach()) < 2e-5
+    if kind.startswith("bn"):
+        assert rel(rmd.cpu(), rm) < 1e-5 and rel(rvd.cpu(), rv) < 1e-5
+    gya = to_act(gy) if x.dim() == 4 else Act.of(gy.to(DEV).contiguous())
+    dxa = op.bwd(xa, stats, ch, gya, dgamma=dg, dbeta=dbt)
+    dx = from_act(dxa) if x.dim() == 4 else dxa.rows2d().cpu()
+    assert rel(dx, xr.grad) < 1e-4
+    assert rel(dg.cpu(), g_.grad) < 1e-4
+    assert rel(dbt.cpu(), b_.grad) < 1e-4
+
+
+def test_dropout_mask_bit_exact():
+    hip = _hip()
+    from expertsim.utils import philox
+    n = 100003
+    for p, stream in ((0.2, 5), (0.3, 1 << 20)):
+        d = hip.dropout_struct(p, 0x123456789, stream, enabled=True)
+        out = torch.empty(n, dtype=torch.uint8, device=DEV)
+        hip.call("es_dropout_mask", hip.ptr(out), n, C.byref(d), hip.stream_ptr())
+        ref = philox.dropout_mask((n,), p, 0x123456789, stream)
+        assert np.array_equal(out.cpu().numpy().astype(bool), ref)
+
+
+@pytest.mark.parametrize("k,s", [((2, 2), (2, 2)), ((2, 1), (2, 1)), ((2, 2), (1, 1))])
+def test_maxpool(k, s):
+    _hip()
+    from expertsim.layers import MaxPool
+    torch.manual_seed(3)
+    x = torch.randn(2, 8, 9, 7)
+    xr = x.clone().requires_grad_(True)
+    y = F.max_pool2d(xr, k, s)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    mp = MaxPool(k, s)
+    xa = to_act(x)
+    ya, idx = mp.fwd(xa)
+    assert torch.equal(from_act(ya), y.detach())
+    dxa = mp.bwd(to_act(gy), idx, xa.dims, torch.float32)
+    assert rel(from_act(dxa), xr.grad) < 1e-6
+
+
+def test_adam_matches_torch():
+    hip = _hip()
+    torch.manual_seed(4)
+    p = torch.randn(10007)
+    pt = p.clone().requires_grad_(True)
+    opt = torch.optim.Adam([pt], lr=1e-4)
+    pd, m, v = p.to(DEV), torch.zeros(10007, device=DEV), torch.zeros(10007, device=DEV)
+    for step in range(1, 4):
+        g = torch.randn(10007)
+        pt.grad = g.clone()
+        opt.step()
+        gd = g.to(DEV)
+        hip.call("es_adam", hip.ptr(pd), hip.ptr(gd), hip.ptr(m), hip.ptr(v), pd.numel(), 1e-4, 0.9, 0.999, 1e-8,
+                 step, 1.0, hip.stream_ptr())
+    assert float((pd.cpu() - pt.detach()).abs().max()) < 1e-7
+
+
+def test_randn_moments():
+    hip = _hip()
+    out = torch.empty(1 << 20, device=DEV)
+    hip.call("es_randn", hip.ptr(out), out.numel(), 99, 3, hip.stream_ptr())
+    assert abs(out.mean().item()) < 5e-3 and abs(out.std().item() - 1) < 5e-3
+    hip.call("es_rand_exponential", hip.ptr(out), out.numel(), 99, 4, hip.stream_ptr())
+    assert abs(out.mean().item() - 1) < 5e-3 and out.min().item() > 0
