@@ -83,6 +83,58 @@ class Act:
         return torch.as_strided(self.t, (n, c), (self.strides[0], self.strides[1]), self.t.storage_offset())
 
 
+# ------------------------------------------------------------------------------ kernel probe
+class KernelProbe:
+    """HIP-event timing of selected kernel launches (labels like "G0.c5.fwd") on the launch
+    stream, used by bench.py for the live roofline of the dominant kernel."""
+
+    def __init__(self, targets):
+        self.targets = set(targets)
+        self.events = {t: [] for t in targets}
+
+    def wants(self, label):
+        return label in self.targets
+
+    def record(self, label):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def add(self, label, start, end):
+        self.events[label].append((start, end))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for k, pairs in self.events.items():
+            if pairs:
+                ms = [a.elapsed_time(b) for a, b in pairs]
+                out[k] = {"count": len(ms), "total_ms": sum(ms), "avg_ms": sum(ms) / len(ms)}
+        return out
+
+
+_PROBE = None
+
+
+def set_probe(p):
+    global _PROBE
+    _PROBE = p
+
+
+class _probed:
+    def __init__(self, label):
+        self.label = label
+        self.on = _PROBE is not None and label is not None and _PROBE.wants(label)
+
+    def __enter__(self):
+        if self.on:
+            self.t0 = _PROBE.record(self.label)
+
+    def __exit__(self, *exc):
+        if self.on:
+            _PROBE.add(self.label, self.t0, _PROBE.record(self.label))
+
+
 def copy_act(src: Act, dst: Act, alpha=1.0, beta=0.0):
     hip.call("es_copy", C.byref(src.view), src.dt, src.ptr, C.byref(dst.view), dst.dt, dst.ptr,
              float(alpha), float(beta), hip.stream_ptr())
@@ -150,6 +202,7 @@ class ConvOp:
         self.stride = stride
         self.pad = pad
         self.up = upsample
+        self.label = None
         w = weight
         self.K = w.shape[0]
         self.C = w.shape[1]
@@ -197,7 +250,8 @@ class ConvOp:
         if out is None:
             out = Act.nhwc(d.N, d.K, d.P, d.Q, out_dtype or cdt, x.t.device)
         bias = self.bias if (with_bias and self.bias is not None) else None
-        hip.call("es_conv2d_fwd", C.byref(d), x.dt, x.ptr, hip.strides4(x.strides), hip.ptr(wk),
+        with _probed(self.label and self.label + ".fwd"):
+          hip.call("es_conv2d_fwd", C.byref(d), x.dt, x.ptr, hip.strides4(x.strides), hip.ptr(wk),
                  hip.ptr(bias), out.ptr, out.dt, hip.strides4(out.strides), hip.stream_ptr())
         return out
 
@@ -211,11 +265,13 @@ class ConvOp:
         if self.up is None:
             if dx is None:
                 dx = Act.nhwc(N, Cc, H, W, ddt, dy.t.device)
-            hip.call("es_conv2d_dgrad", C.byref(d), dy.dt, dy.ptr, hip.strides4(dy.strides), hip.ptr(wd),
+            with _probed(self.label and self.label + ".dgrad"):
+              hip.call("es_conv2d_dgrad", C.byref(d), dy.dt, dy.ptr, hip.strides4(dy.strides), hip.ptr(wd),
                      dx.ptr, dx.dt, hip.strides4(dx.strides), float(beta), hip.stream_ptr())
             return dx
         dxu = Act.nhwc(N, Cc, d.Hu, d.Wu, torch.float32, dy.t.device)
-        hip.call("es_conv2d_dgrad", C.byref(d), dy.dt, dy.ptr, hip.strides4(dy.strides), hip.ptr(wd),
+        with _probed(self.label and self.label + ".dgrad"):
+          hip.call("es_conv2d_dgrad", C.byref(d), dy.dt, dy.ptr, hip.strides4(dy.strides), hip.ptr(wd),
                  dxu.ptr, dxu.dt, hip.strides4(dxu.strides), 0.0, hip.stream_ptr())
         if dx is None:
             dx = Act.nhwc(N, Cc, H, W, ddt, dy.t.device)
@@ -232,7 +288,8 @@ class ConvOp:
         dev = dy.t.device
         dwk = torch.zeros(self.weight.numel(), dtype=torch.float32, device=dev)
         assert dy.t.dtype == x.t.dtype, (dy.t.dtype, x.t.dtype)
-        hip.call("es_conv2d_wgrad", C.byref(d), dy.dt, dy.ptr, hip.strides4(dy.strides), x.ptr,
+        with _probed(self.label and self.label + ".wgrad"):
+          hip.call("es_conv2d_wgrad", C.byref(d), dy.dt, dy.ptr, hip.strides4(dy.strides), x.ptr,
                  hip.strides4(x.strides), hip.ptr(dwk), hip.stream_ptr())
         if dw_out is not None:
             hip.call("es_unpack_conv_grad", hip.ptr(dwk), self.K, self.C, self.R, self.S, None,

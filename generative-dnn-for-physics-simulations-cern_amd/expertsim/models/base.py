@@ -100,6 +100,10 @@ class ExpertModule(nn.Module):
         self.flatten()
         if self._ops is None:
             self._ops = self.program()
+            prefix = getattr(self, "_probe_prefix", None)
+            for k, op in self._ops.items():
+                if hasattr(op, "label"):
+                    op.label = f"{prefix}.{k}" if prefix else None
         return self._ops
 
     def invalidate(self):

@@ -49,6 +49,10 @@ class MoEWrapper(nn.Module):
         self.aux_regs = nn.ModuleList([copy.deepcopy(aux_reg_cls) for _ in range(n_experts)])
         self.router = router_cls
         self.n_experts = n_experts
+        for i in range(n_experts):
+            self.generators[i]._probe_prefix = f"G{i}"
+            self.discriminators[i]._probe_prefix = f"D{i}"
+            self.aux_regs[i]._probe_prefix = f"A{i}"
         self.noise_dim = int(cfg.model.noise_dim)
         self.cfg = cfg
         self.g_steps = [0 for _ in range(n_experts)]
@@ -136,9 +140,15 @@ class MoEWrapper(nn.Module):
             be_global = be if self.ddp is None else self.ddp.global_count(e)
             if be_global <= 1:                                                   # moe.py:126-135
                 continue
-            self._expert_step(e, rows, be, B, cond, real_images, true_positions, std, intensity,
-                              generator_optimizers[e], discriminator_optimizers[e], aux_reg_optimizers[e],
-                              mbuf, step, dev)
+            og, od, oa = generator_optimizers[e], discriminator_optimizers[e], aux_reg_optimizers[e]
+            if be > 1:
+                self._expert_step(e, rows, be, B, cond, real_images, true_positions, std, intensity,
+                                  og, od, oa, mbuf, step, dev)
+            else:
+                # DDP: expert active globally but (almost) absent from this shard -> zero local
+                # gradients, but join the same collectives and optimizer steps as the other ranks
+                self._allreduce(self.discriminators[e]); od.step()
+                self._allreduce(self.generators[e]); self._allreduce(self.aux_regs[e]); og.step(); oa.step()
 
         # ---- router (moe.py:213-449)
         zero = torch.zeros((), dtype=torch.float32, device=dev)
@@ -205,7 +215,8 @@ class MoEWrapper(nn.Module):
             sc, sp, ss, si = gather(cond, cond.shape[1]), gather(pos, 2), gather(std, 1), gather(intensity, 1)
             sr = gather(real.reshape(B, -1), H * W).view(be, 1, H, W)
         # class_counts_adjusted[i] as float32 (moe.py:99-100,522,562)
-        w = float(np.float32(self.ddp.global_count(e) if self.ddp else be) / np.float32(self.ddp.global_batch if self.ddp else B))
+        # (DDP: local weight B_e^r / B_r; the all-reduce averages, see expertsim/train/ddp.py)
+        w = float(np.float32(be) / np.float32(B))
         w_dev = torch.full((1,), w, dtype=torch.float32, device=dev)
         rank = self.rank
         sb = lambda pid: philox.dropout_stream(step, e, pid, 0, rank)

@@ -60,7 +60,8 @@ class AuxReg(ExpertModule):
 
     def program(self):
         m = lambda n: get_module(self, n)
-        conv = lambda n: ConvOp(m(n).weight, m(n).bias, stride=m(n).stride[0], pad=m(n).padding[0])
+        conv = lambda n: ConvOp(m(n).weight, m(n).bias, stride=getattr(m(n), "stride", (1,))[0],
+                               pad=getattr(m(n), "padding", (0,))[0])
         gn = lambda n: NormOp(hip.NORM_GN, m(n).weight, m(n).bias, groups=m(n).num_groups, eps=m(n).eps)
         ops = {"c1": conv(FE + "conv1.0"), "g1": gn(FE + "conv1.1"), "pool": MaxPool(2, 1)}
         for blk in ("res1", "res2"):

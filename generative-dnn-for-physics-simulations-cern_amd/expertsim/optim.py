@@ -41,8 +41,10 @@ class FusedAdam(torch.optim.Optimizer):
         self.module.zero_grads()
 
     @torch.no_grad()
-    def step(self, closure=None, grad_scale: float = 1.0):
+    def step(self, closure=None, grad_scale: float = None):
         flat = self._buffers()
+        if grad_scale is None:
+            grad_scale = getattr(self.module, "_grad_scale", 1.0)
         self._step += 1
         g = self.param_groups[0]
         b1, b2 = g["betas"]

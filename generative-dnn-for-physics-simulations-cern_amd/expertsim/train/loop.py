@@ -1,0 +1,98 @@
+"""Training orchestration — reference: expertsim/train/loop.py:27-182,332-354.
+
+Same entry points (``train``, ``train_epoch``, ``train_step``, ``setup_moe_system``); the per-batch
+step is ``MoEWrapper.train_step`` on the HIP path.  Metrics are fetched to the host once per batch
+(the reference does ``.cpu().item()`` per key, loop.py:136-148).  With WORLD_SIZE > 1 (torchrun),
+every rank trains on its own shard and gradients are all-reduced over RCCL (expertsim/train/ddp.py).
+Evaluation (Wasserstein metrics), plotting, W&B and checkpoint callbacks are outside the hot-path
+scope of this build; ``evaluate_epoch`` is skipped when no test loader is given.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import time
+from typing import Dict, List
+
+import numpy as np
+import torch
+
+from ..models import build_model
+from ..models.moe import MoEWrapper
+from .training_setup import setup_optimizers
+
+logger = logging.getLogger(__name__)
+
+
+def setup_moe_system(cfg, device) -> MoEWrapper:
+    from ..config import inject_shared
+    inject_shared(cfg)
+    generator = build_model(f"{cfg.model.architecture}.generator", cfg.model.generator, device)
+    discriminator = build_model(f"{cfg.model.architecture}.discriminator", cfg.model.discriminator, device)
+    aux_reg = build_model(f"{cfg.model.architecture}.aux_reg", cfg.model.aux_reg, device)
+    router = build_model(f"{cfg.model.router.version}", cfg.model.router, device)
+    return MoEWrapper(generator, discriminator, aux_reg, router, cfg.model.n_experts, cfg,
+                      image_shape=tuple(cfg.dataset.input_image_shape)).to(device)
+
+
+def train_step(batch, moe, gen_optims, disc_optims, aux_reg_optim, router_optim, cfg, device, epoch,
+               ema_helper) -> Dict:
+    real_images, _, cond, std, intensity, true_positions = batch
+    real_images = real_images.unsqueeze(1).to(device, non_blocking=True)
+    return moe.train_step(epoch, cond.to(device, non_blocking=True), real_images,
+                          true_positions.to(device, non_blocking=True), std.to(device, non_blocking=True),
+                          intensity.to(device, non_blocking=True), aux_reg_optim, gen_optims, disc_optims,
+                          router_optim, ema_helper, device)
+
+
+def train_epoch(moe, train_loader, gen_optims, disc_optims, aux_reg_optims, router_optim, cfg, device, epoch,
+                ema_helper, max_steps=None) -> Dict:
+    moe.train()
+    sums: Dict[str, List[float]] = {}
+    for i, batch in enumerate(train_loader):
+        if max_steps is not None and i >= max_steps:
+            break
+        m = train_step(batch, moe, gen_optims, disc_optims, aux_reg_optims, router_optim, cfg, device, epoch,
+                       ema_helper)
+        keys = list(m)
+        vals = torch.stack([torch.as_tensor(m[k], dtype=torch.float32, device=device).reshape(())
+                            for k in keys]).cpu().numpy()   # ONE device->host copy per batch
+        for k, v in zip(keys, vals):
+            sums.setdefault(k, []).append(float(v))
+    out = {k: float(np.mean(v)) for k, v in sums.items()}
+    for i in range(moe.n_experts):
+        out[f"G_steps_{i}"] = moe.g_steps[i]
+        out[f"D_steps_{i}"] = moe.d_steps[i]
+    return out
+
+
+def train(cfg, train_loader, test_loader=None, max_steps_per_epoch=None) -> List[Dict]:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if not torch.cuda.is_available():
+        raise RuntimeError("expertsim trains on a HIP device only (no CPU fallback)")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    torch.manual_seed(int(cfg.train.get("rng_seed", 1234)))
+    moe = setup_moe_system(cfg, device)
+    if world > 1:
+        import torch.distributed as dist
+        from .ddp import DataParallel
+        if not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("nccl", device_id=device)
+        moe.ddp = DataParallel()
+        moe.rank = dist.get_rank()
+    gen_optims, disc_optims, aux_optims, router_optim = setup_optimizers(moe, cfg)
+    history = []
+    start = 0 if cfg.train.get("epoch_to_load") is None else int(cfg.train.epoch_to_load)
+    for epoch in range(start, int(cfg.train.epochs)):
+        t0 = time.time()
+        metrics = train_epoch(moe, train_loader, gen_optims, disc_optims, aux_optims, router_optim, cfg, device,
+                              epoch, None, max_steps=max_steps_per_epoch)
+        metrics["epoch_time"] = time.time() - t0
+        metrics["epoch"] = epoch
+        history.append(metrics)
+        logger.info("Epoch %d: %.2fs gen_loss %.4f disc_loss %.4f", epoch, metrics["epoch_time"],
+                    metrics.get("gen_loss", float("nan")), metrics.get("disc_loss", float("nan")))
+    return history
