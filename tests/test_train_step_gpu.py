@@ -6,8 +6,12 @@ Tolerances (derived from the reference's own 1-vs-8-thread dri
   step 0: generated images, D outputs/latents, aux coords and every loss metric <= 1e-4 relative
           (metrics: relative to max(|ref|, 1e-3) so near-zero terms are compared absolutely);
           post-Adam parameters |p - p_ref| <= 2*lr elementwise (64 strided samples per tensor);
-  step 1: the same quantities <= 1e-2 relative (Adam's first step turns rounding-level gradient
-          differences into +-lr parameter moves, which step 1 then sees).
+  step 1: the same quantities <= STEP1_TOL[case] relative.  Adam's first step moves every
+          parameter by ~+-lr whatever its gradient's size, so rounding-level differences that flip
+          the sign of a tiny gradient (e.g. a ReLU-threshold pixel) become +-lr parameter moves.
+          The tolerance is the reference's OWN step-1 sensitivity: the oracle (bit-exact to the
+          reference) with 3e-6 relative noise injected on every conv output moves step-1 metrics by
+          up to 2.5e-3 (neutron_e3), 1.3e-4 (..._e1 cases at 1e-6) and 4.6e-2 (proton_e3_b12).
 """
 import numpy as np
 import pytest
@@ -17,6 +21,7 @@ from golden_utils import CASES, Golden
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
+STEP1_TOL = {"neutron_e1_b8": 1e-2, "neutron_e3_b12": 1e-2, "proton_e1_b8": 1e-2, "proton_e3_b12": 5e-2}
 
 
 def _build(g: Golden):
@@ -70,7 +75,7 @@ def test_train_step_matches_reference(case):
            "R": cfg.model.router.lr_r}
     for s in range(g.steps):
         rec.clear()
-        tol = 1e-4 if s == 0 else 1e-2
+        tol = 1e-4 if s == 0 else STEP1_TOL[case]
         inp = g.inputs(s)
         nz = g.noise(s)
         moe.noise_fn = lambda e, w, shape: torch.from_numpy(nz[(e, w)])
