@@ -32,6 +32,25 @@ constexpr int KSTEP_BYTES = 128;               // operand bytes per row per K-st
 constexpr int ROW_BYTES = KSTEP_BYTES + 16;    // padded LDS row
 constexpr int NTHREADS = 256;
 
+// LDS image of one operand for one K-step.
+//  default : [rows][k] K-contiguous, 144-byte rows (fragments read with 16-byte ds_read)
+//  TR      : bf16 WGRAD operands, whose global data is contiguous along the GEMM row (m / n):
+//            [k][rows] row-contiguous image written with 16-byte stores (no transpose in
+//            registers) and read with ds_read_b64_tr_b16 (gfx950 transposing LDS read).
+//            Row stride = rows*2 + 32 bytes, and k-rows with bit 3 set XOR their byte column by
+//            rows bytes, so the two 16-lane groups of a half-wave (k rows 8 apart) hit disjoint
+//            banks.
+template <typename T, int MODE, int BROWS>
+struct LdsImg {
+  static constexpr bool TR = (MODE == 2) && sizeof(T) == 2;
+  static constexpr int BK = KSTEP_BYTES / sizeof(T);
+  static constexpr int ROWB = TR ? BROWS * 2 + 32 : ROW_BYTES;
+  static constexpr int BYTES = TR ? BK * ROWB : BROWS * ROW_BYTES;
+  __device__ static __forceinline__ int tr_off(int k, int row) {   // byte offset of (k, row)
+    return k * ROWB + ((row * 2) ^ (((k >> 3) & 1) * BROWS));
+  }
+};
+
 struct ConvArgs {
   es_conv_desc_t d;
   const void* a_src;
@@ -200,6 +219,9 @@ struct Stager {
       if constexpr (!TRANS) {
         const int row = idx / (KSTEP_BYTES / 16), ch = idx % (KSTEP_BYTES / 16);
         *(V*)(lds + row * ROW_BYTES + ch * 16) = reg[i];
+      } else if constexpr (LdsImg<T, MODE, BROWS>::TR) {
+        const int row = (idx % (BROWS / VN)) * VN, kk = idx / (BROWS / VN);
+        *(V*)(lds + LdsImg<T, MODE, BROWS>::tr_off(kk, row)) = reg[i];
       } else {
         const int row = (idx % (BROWS / VN)) * VN, kk = idx / (BROWS / VN);
         T e[VN];
@@ -252,12 +274,51 @@ __device__ __forceinline__ void mma_kstep(const char* As, const char* Bs, int wm
   }
 }
 
+typedef short short4_t __attribute__((ext_vector_type(4)));
+typedef short short8_t __attribute__((ext_vector_type(8)));
+
+template <int BROWS>
+__device__ __forceinline__ bf16x8 tr_frag(const char* img, int k0, int r0) {
+  // A/B fragment of v_mfma_f32_16x16x32_bf16 from a [k][rows] image: lane l gets rows r0+(l&15),
+  // k = k0 + 8*(l>>4) + 0..7, as two ds_read_b64_tr_b16 (4 k each).
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  typedef LdsImg<bf16, 2, BROWS> L;
+  const int ka = k0 + 8 * g + q;
+  const char* p0 = img + L::tr_off(ka, r0 + 4 * p);
+  const char* p1 = img + L::tr_off(ka + 4, r0 + 4 * p);
+  short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)p0);
+  short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)p1);
+  short8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int RM, int RN, int BM, int BN>
+__device__ __forceinline__ void mma_kstep_tr(const char* As, const char* Bs, int wm0, int wn0,
+                                             f32x4 (&acc)[RM][RN]) {
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    bf16x8 af[RM], bfr[RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i) af[i] = tr_frag<BM>(As, kk * 32, wm0 + i * 16);
+#pragma unroll
+    for (int j = 0; j < RN; ++j) bfr[j] = tr_frag<BN>(Bs, kk * 32, wn0 + j * 16);
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  }
+}
+
 template <typename T, int MODE, int BM, int BN, bool AVEC, bool BVEC>
 __global__ void __launch_bounds__(NTHREADS) conv_igemm_kernel(ConvArgs a) {
   constexpr int BK = KSTEP_BYTES / sizeof(T);
   constexpr int RM = BM / 32, RN = BN / 32;   // 16x16 tiles per wave (2x2 wave grid)
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int BUF = (BM + BN) * ROW_BYTES;   // one stage: A rows then B rows
+  typedef LdsImg<T, MODE, BM> LA;
+  typedef LdsImg<T, MODE, BN> LB;
+  constexpr int BUF = LA::BYTES + LB::BYTES;   // one stage: A image then B image
 
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   int kbeg = 0, kend = a.Kd;
@@ -280,7 +341,7 @@ __global__ void __launch_bounds__(NTHREADS) conv_igemm_kernel(ConvArgs a) {
   sa.load(a, m0, kbeg);
   sb.load(a, n0, kbeg);
   sa.store(smem);
-  sb.store(smem + BM * ROW_BYTES);
+  sb.store(smem + LA::BYTES);
   __syncthreads();
   int cur = 0;
   for (int k0 = kbeg; k0 < kend; k0 += BK) {
@@ -289,10 +350,13 @@ __global__ void __launch_bounds__(NTHREADS) conv_igemm_kernel(ConvArgs a) {
       sa.load(a, m0, k0 + BK);
       sb.load(a, n0, k0 + BK);
     }
-    mma_kstep<T, RM, RN>(smem + cur * BUF, smem + cur * BUF + BM * ROW_BYTES, wm0, wn0, acc);
+    if constexpr (LA::TR)
+      mma_kstep_tr<RM, RN, BM, BN>(smem + cur * BUF, smem + cur * BUF + LA::BYTES, wm0, wn0, acc);
+    else
+      mma_kstep<T, RM, RN>(smem + cur * BUF, smem + cur * BUF + LA::BYTES, wm0, wn0, acc);
     if (more) {
       sa.store(smem + (cur ^ 1) * BUF);
-      sb.store(smem + (cur ^ 1) * BUF + BM * ROW_BYTES);
+      sb.store(smem + (cur ^ 1) * BUF + LA::BYTES);
     }
     __syncthreads();
     cur ^= 1;
@@ -347,7 +411,7 @@ __global__ void __launch_bounds__(NTHREADS) conv_igemm_kernel(ConvArgs a) {
 template <typename T, int MODE, int BM, int BN>
 int launch_tile(const ConvArgs& a, bool avec, bool bvec, hipStream_t st, int splits) {
   dim3 grid((a.M + BM - 1) / BM, (a.Ng + BN - 1) / BN, splits);
-  const size_t lds = 2 * (BM + BN) * ROW_BYTES;
+  const size_t lds = 2 * (LdsImg<T, MODE, BM>::BYTES + LdsImg<T, MODE, BN>::BYTES);
 #define ES_LAUNCH(AV, BV)                                                                     \
   hipLaunchKernelGGL((conv_igemm_kernel<T, MODE, BM, BN, AV, BV>), grid, dim3(NTHREADS), lds, \
                      st, a)

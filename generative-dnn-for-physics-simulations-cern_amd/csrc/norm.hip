@@ -237,6 +237,69 @@ __global__ void sum_finalize_kernel(const float* part, int chunks, int C, float*
   out[c] = (beta != 0.f ? beta * out[c] : 0.f) + s;
 }
 
+// Block-per-channel variants of the finalize kernels (used when there are many chunks).
+__global__ void __launch_bounds__(256) bn_finalize_block_kernel(const float* part, int chunks, int C, float eps,
+                                                                float* mean, float* invstd, float* rmean,
+                                                                float* rvar, float mom) {
+  const int c = blockIdx.x;
+  double n_ = 0.0, mu = 0.0, M = 0.0;
+  for (int k = threadIdx.x; k < chunks; k += blockDim.x) {
+    const float* p = part + (int64_t)k * 3 * C;
+    const double nb = p[c];
+    if (nb == 0.0) continue;
+    const double mb = p[C + c], Mb = p[2 * C + c];
+    const double nt = n_ + nb, dl = mb - mu;
+    mu += dl * nb / nt;
+    M += Mb + dl * dl * n_ * nb / nt;
+    n_ = nt;
+  }
+  __shared__ double sn[256], sm[256], sM[256];
+  sn[threadIdx.x] = n_; sm[threadIdx.x] = mu; sM[threadIdx.x] = M;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) {
+      const double na = sn[threadIdx.x], nb = sn[threadIdx.x + off];
+      if (nb > 0.0) {
+        const double ma = sm[threadIdx.x], mb = sm[threadIdx.x + off];
+        const double nt = na + nb, dl = mb - ma;
+        sm[threadIdx.x] = ma + dl * nb / nt;
+        sM[threadIdx.x] = sM[threadIdx.x] + sM[threadIdx.x + off] + dl * dl * na * nb / nt;
+        sn[threadIdx.x] = nt;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double nt = sn[0], mt = sm[0], Mt = sM[0];
+    const double var = Mt / nt;
+    mean[c] = (float)mt;
+    invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+    if (rmean) rmean[c] = (1.f - mom) * rmean[c] + mom * (float)mt;
+    if (rvar) rvar[c] = (1.f - mom) * rvar[c] + mom * (float)(nt > 1.0 ? Mt / (nt - 1.0) : var);
+  }
+}
+
+__global__ void __launch_bounds__(256) sums_finalize_block_kernel(const float* part, int chunks, int C, float cnt,
+                                                                  const float* gamma, float* a1, float* a2,
+                                                                  float* out1, float* out2, float beta1) {
+  // out1 (+)= s1 (beta1: scale of old out1), out2 += s2; a1/a2 = gamma*s/cnt (BN backward)
+  const int c = blockIdx.x;
+  __shared__ float sh[8];
+  float s1 = 0.f, s2 = 0.f;
+  for (int k = threadIdx.x; k < chunks; k += blockDim.x) {
+    const float* p = part + (int64_t)k * 3 * C;
+    s1 += p[C + c]; s2 += p[2 * C + c];
+  }
+  s1 = block_sum(s1, sh);
+  s2 = block_sum(s2, sh);
+  if (threadIdx.x == 0) {
+    const float g = gamma ? gamma[c] : 1.f;
+    if (a1) { a1[c] = g * s1 / cnt; a2[c] = g * s2 / cnt; }
+    if (out1) out1[c] = (beta1 != 0.f ? beta1 * out1[c] : 0.f) + s1;
+    if (out2) out2[c] += s2;
+  }
+}
+
 void colred_geometry(const View& v, int& cblocks, int& chunks, int64_t& rows, int64_t& per) {
   rows = (int64_t)v.n * v.h * v.w;
   cblocks = (v.c + 63) / 64;
@@ -317,12 +380,18 @@ struct BwdApply {
   View dx; void* dxp; int dxbf;
   const float* a1; const float* a2;  // per stats group
   float beta;
+  float* csum;                        // optional: per-channel sum of dx (conv-bias gradient), C <= 1024
 };
 
 __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(BwdApply a) {
   const View& v = a.b.x;
   const int64_t total = (int64_t)v.n * v.c * v.h * v.w;
   const bool cl = v.s[1] == 1 && v.c > 1;
+  __shared__ float sacc[1024];
+  if (a.csum) {
+    for (int i = threadIdx.x; i < v.c; i += blockDim.x) sacc[i] = 0.f;
+    __syncthreads();
+  }
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     int n, c, h, w;
     decompose(v, cl, e, n, c, h, w);
@@ -336,8 +405,14 @@ __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(BwdApply a) {
       dx = a.b.nm.invstd[g] * (dn * a.b.nm.gam(c) - a.a1[g] - xh * a.a2[g]);
     }
     const int64_t o = a.dx.off(n, c, h, w);
+    if (a.csum) atomicAdd(&sacc[c], dx);
     if (a.beta != 0.f) dx += a.beta * ldf(a.dxp, a.dxbf, o);
     stf(a.dxp, a.dxbf, o, dx);
+  }
+  if (a.csum) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < v.c; i += blockDim.x)
+      if (sacc[i] != 0.f) atomicAdd(&a.csum[i], sacc[i]);
   }
 }
 
@@ -384,8 +459,12 @@ extern "C" int es_norm_stats(const es_view_t* x, es_dtype_t xdt, const void* xp,
     colred_geometry(b.x, cb, chunks, rows, per);
     ES_CHECK_ARG(ws != nullptr, "norm_stats: BN needs workspace");
     hipLaunchKernelGGL(colred_kernel<RED_STATS>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, (float*)ws);
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)ws,
-                       chunks, x->c, eps, mean, invstd, running_mean, running_var, momentum);
+    if (chunks > 32)
+      hipLaunchKernelGGL(bn_finalize_block_kernel, dim3(x->c), dim3(256), 0, st, (const float*)ws, chunks, x->c,
+                         eps, mean, invstd, running_mean, running_var, momentum);
+    else
+      hipLaunchKernelGGL(bn_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)ws,
+                         chunks, x->c, eps, mean, invstd, running_mean, running_var, momentum);
   } else {
     const int64_t ng = stats_groups(x, kind, groups);
     hipLaunchKernelGGL(segred_kernel<RED_STATS>, dim3((unsigned)ng), dim3(256), 0, st, b, eps, mean, invstd);
@@ -429,16 +508,18 @@ extern "C" int es_norm_act_bwd(const es_view_t* x, es_dtype_t xdt, const void* x
                                const es_chain_t* ch, const es_view_t* dy, es_dtype_t dydt,
                                const void* dyp, const es_view_t* act_ref, es_dtype_t rdt,
                                const void* refp, const es_view_t* dx, es_dtype_t dxdt, void* dxp,
-                               float beta, float* dgamma, float* dbeta, void* ws, es_stream_t stream) {
+                               float beta, float* dgamma, float* dbeta, float* dsum, void* ws,
+                               es_stream_t stream) {
   hipStream_t st = (hipStream_t)stream;
   const int kind = nm ? nm->kind : ES_NORM_NONE;
+  ES_CHECK_ARG(dsum == nullptr || x->c <= 1024, "norm_act_bwd: dsum needs C <= 1024");
   const int groups = nm ? nm->groups : 1;
   ES_CHECK_ARG(kind != ES_NORM_LN || (x->h == 1 && x->w == 1), "norm_act_bwd: LN needs (N,F,1,1) views");
   BwdIn b = mk_bwdin(x, xdt, xp, nm, ch);
   b.dy = mkview(dy); b.dyp = dyp; b.dybf = dydt == ES_BF16;
   if (refp) { b.ref = mkview(act_ref); b.refp = refp; b.refbf = rdt == ES_BF16; }
   BwdApply ap{};
-  ap.b = b; ap.dx = mkview(dx); ap.dxp = dxp; ap.dxbf = dxdt == ES_BF16; ap.beta = beta;
+  ap.b = b; ap.dx = mkview(dx); ap.dxp = dxp; ap.dxbf = dxdt == ES_BF16; ap.beta = beta; ap.csum = dsum;
   const int64_t total = (int64_t)x->n * x->c * x->h * x->w;
   int cb, chunks; int64_t rows, per;
   colred_geometry(b.x, cb, chunks, rows, per);
@@ -448,15 +529,23 @@ extern "C" int es_norm_act_bwd(const es_view_t* x, es_dtype_t xdt, const void* x
   float* g2 = g1 + ng;
   if (kind == ES_NORM_BN) {
     hipLaunchKernelGGL(colred_kernel<RED_BWD>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, part);
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)part,
-                       chunks, x->c, (float)rows, nm->gamma, g1, g2, dgamma, dbeta);
+    if (chunks > 32)
+      hipLaunchKernelGGL(sums_finalize_block_kernel, dim3(x->c), dim3(256), 0, st, (const float*)part, chunks,
+                         x->c, (float)rows, nm->gamma, g1, g2, dbeta, dgamma, 1.f);
+    else
+      hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)part,
+                         chunks, x->c, (float)rows, nm->gamma, g1, g2, dgamma, dbeta);
     ap.a1 = g1; ap.a2 = g2;
   } else if (kind == ES_NORM_GN || kind == ES_NORM_LN) {
     hipLaunchKernelGGL(segred_kernel<RED_BWD>, dim3((unsigned)ng), dim3(256), 0, st, b, 0.f, g1, g2);
     if (dgamma || dbeta) {
       hipLaunchKernelGGL(colred_kernel<RED_BWD>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, part);
-      hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)part,
-                         chunks, x->c, (float)rows, nullptr, (float*)nullptr, (float*)nullptr, dgamma, dbeta);
+      if (chunks > 32)
+        hipLaunchKernelGGL(sums_finalize_block_kernel, dim3(x->c), dim3(256), 0, st, (const float*)part, chunks,
+                           x->c, (float)rows, nullptr, (float*)nullptr, (float*)nullptr, dbeta, dgamma, 1.f);
+      else
+        hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)part,
+                           chunks, x->c, (float)rows, nullptr, (float*)nullptr, (float*)nullptr, dgamma, dbeta);
     }
     ap.a1 = g1; ap.a2 = g2;
   }
@@ -479,8 +568,12 @@ extern "C" int es_channel_sum(const es_view_t* x, es_dtype_t xdt, const void* xp
   int cb, chunks; int64_t rows, per;
   colred_geometry(b.x, cb, chunks, rows, per);
   hipLaunchKernelGGL(colred_kernel<RED_SUM>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, (float*)ws);
-  hipLaunchKernelGGL(sum_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)ws,
-                     chunks, x->c, out, beta);
+  if (chunks > 32)
+    hipLaunchKernelGGL(sums_finalize_block_kernel, dim3(x->c), dim3(256), 0, st, (const float*)ws, chunks, x->c,
+                       1.f, nullptr, (float*)nullptr, (float*)nullptr, out, (float*)nullptr, beta);
+  else
+    hipLaunchKernelGGL(sum_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)ws,
+                       chunks, x->c, out, beta);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }

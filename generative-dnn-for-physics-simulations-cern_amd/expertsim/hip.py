@@ -9,6 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
+import numpy as np
 import torch
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libexpertsim_hip.so")
@@ -65,7 +66,7 @@ _SIGS = {
     "es_norm_act_fwd": (C.c_int, [P, C.c_int, P, P, P, C.c_int, P, P, P, C.c_int, P, P]),
     "es_norm_bwd_ws_bytes": (I64, [P, C.c_int, C.c_int]),
     "es_norm_act_bwd": (C.c_int, [P, C.c_int, P, P, P, P, C.c_int, P, P, C.c_int, P, P, C.c_int, P,
-                                  C.c_float, P, P, P, P]),
+                                  C.c_float, P, P, P, P, P]),
     "es_act_fwd": (C.c_int, [P, C.c_int, P, P, P, C.c_int, P, P]),
     "es_channel_sum_ws_bytes": (I64, [P]),
     "es_channel_sum": (C.c_int, [P, C.c_int, P, P, C.c_float, P, P]),
@@ -166,7 +167,7 @@ def dropout_struct(p: float = 0.0, seed: int = 0, stream: int = 0, enabled: bool
         d.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         d.stream = int(stream) & 0xFFFFFFFF
         d.threshold = int((1.0 - float(p)) * 16777216.0)   # floor, = philox.keep_threshold
-        d.scale = float(torch.tensor(1.0, dtype=torch.float32) / torch.tensor(1.0 - p, dtype=torch.float32))
+        d.scale = float(np.float32(1.0) / np.float32(1.0 - p))   # torch: bernoulli_(1-p).div_(1-p) in fp32
     return d
 
 

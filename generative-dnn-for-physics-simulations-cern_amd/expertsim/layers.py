@@ -355,7 +355,9 @@ class NormOp:
         return y, (mean, invstd)
 
     def bwd(self, x: Act, stats, chain: hip.Chain, dy: Act, dx_dtype=None, act_ref: Act = None,
-            addend: Act = None, dgamma=None, dbeta=None, dx: Act = None, beta=0.0):
+            addend: Act = None, dgamma=None, dbeta=None, dx: Act = None, beta=0.0, dsum=None):
+        """dsum: optional fp32 [C] accumulating sum(dx) per channel = grad of the conv bias feeding
+        this norm (fused into the apply pass; falls back to a reduction for C > 1024)."""
         mean, invstd = stats
         nm = self.norm_struct(mean, invstd)
         if dx is None:
@@ -367,7 +369,10 @@ class NormOp:
                  C.byref(act_ref.view) if act_ref is not None else None,
                  act_ref.dt if act_ref is not None else 0, act_ref.ptr if act_ref is not None else None,
                  C.byref(dx.view), dx.dt, dx.ptr, float(beta), hip.ptr(dgamma), hip.ptr(dbeta),
+                 hip.ptr(dsum) if (dsum is not None and x.dims[1] <= 1024) else None,
                  hip.ptr(wsb), hip.stream_ptr())
+        if dsum is not None and x.dims[1] > 1024:
+            channel_sum(dx, dsum, 1.0)
         return dx
 
 
@@ -386,7 +391,7 @@ def act_bwd(x: Act, chain: hip.Chain, dy: Act, act_ref: Act = None, dx: Act = No
     hip.call("es_norm_act_bwd", C.byref(x.view), x.dt, x.ptr, None, C.byref(chain), C.byref(dy.view), dy.dt,
              dy.ptr, C.byref(act_ref.view) if act_ref is not None else None,
              act_ref.dt if act_ref is not None else 0, act_ref.ptr if act_ref is not None else None,
-             C.byref(dx.view), dx.dt, dx.ptr, float(beta), None, None, hip.ptr(wsb), hip.stream_ptr())
+             C.byref(dx.view), dx.dt, dx.ptr, float(beta), None, None, None, hip.ptr(wsb), hip.stream_ptr())
     return dx
 
 

@@ -108,20 +108,20 @@ class AuxRegNeutron(ExpertModule):
         dh5 = o["rb"].bwd(c["h5"], c["s5"], ch[4], dy5, dgamma=g(FE + "reduce.1"), dbeta=g(FE + "reduce.1", "bias"))
         o["r"].wgrad(dh5, c["y4"], g(FE + "reduce.0"), None)
         dy4 = o["r"].dgrad(dh5, c["y4"])
-        dh4 = o["b4"].bwd(c["h4"], c["s4"], ch[3], dy4, dgamma=g(FE + "conv4_bd.0"), dbeta=g(FE + "conv4_bd.0", "bias"))
-        o["c4"].wgrad(dh4, c["q3"], g(FE + "conv4"), g(FE + "conv4", "bias"))
+        dh4 = o["b4"].bwd(c["h4"], c["s4"], ch[3], dy4, dgamma=g(FE + "conv4_bd.0"), dbeta=g(FE + "conv4_bd.0", "bias"), dsum=g(FE + "conv4", "bias"))
+        o["c4"].wgrad(dh4, c["q3"], g(FE + "conv4"), None)
         dq3 = o["c4"].dgrad(dh4, c["q3"])
         dy3 = o["p3"].bwd(dq3, c["i3"], c["y3"].dims, cdt)
-        dh3 = o["b3"].bwd(c["h3"], c["s3"], ch[2], dy3, dgamma=g(FE + "conv3_bd.0"), dbeta=g(FE + "conv3_bd.0", "bias"))
-        o["c3"].wgrad(dh3, c["q2"], g(FE + "conv3"), g(FE + "conv3", "bias"))
+        dh3 = o["b3"].bwd(c["h3"], c["s3"], ch[2], dy3, dgamma=g(FE + "conv3_bd.0"), dbeta=g(FE + "conv3_bd.0", "bias"), dsum=g(FE + "conv3", "bias"))
+        o["c3"].wgrad(dh3, c["q2"], g(FE + "conv3"), None)
         dq2 = o["c3"].dgrad(dh3, c["q2"])
         dy2 = o["p2"].bwd(dq2, c["i2"], c["y2"].dims, cdt)
-        dh2 = o["b2"].bwd(c["h2"], c["s2"], ch[1], dy2, dgamma=g(FE + "conv2_bd.0"), dbeta=g(FE + "conv2_bd.0", "bias"))
-        o["c2"].wgrad(dh2, c["q1"], g(FE + "conv2"), g(FE + "conv2", "bias"))
+        dh2 = o["b2"].bwd(c["h2"], c["s2"], ch[1], dy2, dgamma=g(FE + "conv2_bd.0"), dbeta=g(FE + "conv2_bd.0", "bias"), dsum=g(FE + "conv2", "bias"))
+        o["c2"].wgrad(dh2, c["q1"], g(FE + "conv2"), None)
         dq1 = o["c2"].dgrad(dh2, c["q1"])
         dy1 = o["p1"].bwd(dq1, c["i1"], c["y1"].dims, cdt)
-        dh1 = o["b1"].bwd(c["h1"], c["s1"], ch[0], dy1, dgamma=g(FE + "conv1_bd.0"), dbeta=g(FE + "conv1_bd.0", "bias"))
-        o["c1"].wgrad(dh1, c["x"], g(FE + "conv1"), g(FE + "conv1", "bias"))
+        dh1 = o["b1"].bwd(c["h1"], c["s1"], ch[0], dy1, dgamma=g(FE + "conv1_bd.0"), dbeta=g(FE + "conv1_bd.0", "bias"), dsum=g(FE + "conv1", "bias"))
+        o["c1"].wgrad(dh1, c["x"], g(FE + "conv1"), None)
         if not input_grad:
             return None
         return o["c1"].dgrad(dh1, c["x"], dx_dtype=torch.float32)

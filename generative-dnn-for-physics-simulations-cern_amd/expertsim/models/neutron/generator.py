@@ -112,27 +112,27 @@ class GeneratorNeutron(ExpertModule):
         o["c13"].wgrad(dh6, ctx["y5"], g("conv_layers.13", "weight"), g("conv_layers.13", "bias"))
         dy5 = o["c13"].dgrad(dh6, ctx["y5"])
         dh5 = o["bn5"].bwd(ctx["h5"], ctx["s5"], ch[4], dy5, dgamma=g("conv_layers.10", "weight"),
-                           dbeta=g("conv_layers.10", "bias"))
-        o["c9"].wgrad(dh5, ctx["y4"], g("conv_layers.9", "weight"), g("conv_layers.9", "bias"))
+                           dbeta=g("conv_layers.10", "bias"), dsum=g("conv_layers.9", "bias"))
+        o["c9"].wgrad(dh5, ctx["y4"], g("conv_layers.9", "weight"), None)
         dy4 = o["c9"].dgrad(dh5, ctx["y4"])
         dh4 = o["bn4"].bwd(ctx["h4"], ctx["s4"], ch[3], dy4, dgamma=g("conv_layers.6", "weight"),
-                           dbeta=g("conv_layers.6", "bias"))
-        o["c5"].wgrad(dh4, ctx["y3"], g("conv_layers.5", "weight"), g("conv_layers.5", "bias"))
+                           dbeta=g("conv_layers.6", "bias"), dsum=g("conv_layers.5", "bias"))
+        o["c5"].wgrad(dh4, ctx["y3"], g("conv_layers.5", "weight"), None)
         dy3 = o["c5"].dgrad(dh4, ctx["y3"])
         dh3 = o["bn3"].bwd(ctx["h3"], ctx["s3"], ch[2], dy3, dgamma=g("conv_layers.1", "weight"),
-                           dbeta=g("conv_layers.1", "bias"))
-        o["c0"].wgrad(dh3, ctx["y2n"], g("conv_layers.0", "weight"), g("conv_layers.0", "bias"))
+                           dbeta=g("conv_layers.1", "bias"), dsum=g("conv_layers.0", "bias"))
+        o["c0"].wgrad(dh3, ctx["y2n"], g("conv_layers.0", "weight"), None)
         dy2n = o["c0"].dgrad(dh3, ctx["y2n"])
         B = dy2n.dims[0]
         dy2 = Act.rows(B, 21632, cdt, dy2n.t.device)
         copy_act(dy2n, Act(dy2.t, (B, 128, 13, 13), (21632, 169, 13, 1)))
         dh2 = o["bn2"].bwd(ctx["h2"], ctx["s2"], ch[1], dy2, dgamma=g("fc2.1", "weight"),
-                           dbeta=g("fc2.1", "bias"))
-        o["fc2"].wgrad(dh2, ctx["y1"], g("fc2.0", "weight"), g("fc2.0", "bias"))
+                           dbeta=g("fc2.1", "bias"), dsum=g("fc2.0", "bias"))
+        o["fc2"].wgrad(dh2, ctx["y1"], g("fc2.0", "weight"), None)
         dy1 = o["fc2"].dgrad(dh2, ctx["y1"])
         dh1 = o["bn1"].bwd(ctx["h1"], ctx["s1"], ch[0], dy1, dgamma=g("fc1.1", "weight"),
-                           dbeta=g("fc1.1", "bias"))
-        o["fc1"].wgrad(dh1, ctx["x0"], g("fc1.0", "weight"), g("fc1.0", "bias"))
+                           dbeta=g("fc1.1", "bias"), dsum=g("fc1.0", "bias"))
+        o["fc1"].wgrad(dh1, ctx["x0"], g("fc1.0", "weight"), None)
 
     # --------------------------------------------------------------------------- nn.Module API
     def forward(self, noise, cond):

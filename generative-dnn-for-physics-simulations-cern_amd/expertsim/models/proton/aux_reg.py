@@ -136,11 +136,11 @@ class AuxReg(ExpertModule):
             copy_act(dout, d)
         o["l8"].wgrad(d, c["r5"], g("regressor.8"), g("regressor.8", "bias"))
         dr5 = o["l8"].dgrad(d, c["r5"])
-        dr4 = o["n5"].bwd(c["r4"], c["rs5"], c["ch1"], dr5, dgamma=g("regressor.5"), dbeta=g("regressor.5", "bias"))
-        o["l4"].wgrad(dr4, c["r1"], g("regressor.4"), g("regressor.4", "bias"))
+        dr4 = o["n5"].bwd(c["r4"], c["rs5"], c["ch1"], dr5, dgamma=g("regressor.5"), dbeta=g("regressor.5", "bias"), dsum=g("regressor.4", "bias"))
+        o["l4"].wgrad(dr4, c["r1"], g("regressor.4"), None)
         dr1 = o["l4"].dgrad(dr4, c["r1"])
-        dr0 = o["n1"].bwd(c["r0"], c["rs1"], c["ch0"], dr1, dgamma=g("regressor.1"), dbeta=g("regressor.1", "bias"))
-        o["l0"].wgrad(dr0, c["fc"], g("regressor.0"), g("regressor.0", "bias"))
+        dr0 = o["n1"].bwd(c["r0"], c["rs1"], c["ch0"], dr1, dgamma=g("regressor.1"), dbeta=g("regressor.1", "bias"), dsum=g("regressor.0", "bias"))
+        o["l0"].wgrad(dr0, c["fc"], g("regressor.0"), None)
         df = o["l0"].dgrad(dr0, c["fc"], dx_dtype=torch.float32)
         last = c["res2"]["q"]
         dcur = avgpool_bwd(df, last.dims, cdt, df.t.device)
@@ -150,20 +150,20 @@ class AuxReg(ExpertModule):
             dout_blk = o["pool"].bwd(dcur, r["qi"], r["out"].dims, cdt)
             # out = relu(gn2(b) + gn_ds(d)): both branches see dout * (out > 0)
             db = o[blk + "conv2n"].bwd(r["b"], r["bs"], relu, dout_blk, act_ref=r["out"],
-                                       dgamma=g(q + "conv2.1"), dbeta=g(q + "conv2.1", "bias"))
+                                       dgamma=g(q + "conv2.1"), dbeta=g(q + "conv2.1", "bias"), dsum=g(q + "conv2.0", "bias"))
             dd = o[blk + "downsamplen"].bwd(r["d"], r["ds"], relu, dout_blk, act_ref=r["out"],
-                                            dgamma=g(q + "downsample.1"), dbeta=g(q + "downsample.1", "bias"))
-            o[blk + "conv2"].wgrad(db, r["ay"], g(q + "conv2.0"), g(q + "conv2.0", "bias"))
+                                            dgamma=g(q + "downsample.1"), dbeta=g(q + "downsample.1", "bias"), dsum=g(q + "downsample.0", "bias"))
+            o[blk + "conv2"].wgrad(db, r["ay"], g(q + "conv2.0"), None)
             day = o[blk + "conv2"].dgrad(db, r["ay"])
-            da = o[blk + "conv1n"].bwd(r["a"], r["as"], relu, day, dgamma=g(q + "conv1.1"), dbeta=g(q + "conv1.1", "bias"))
-            o[blk + "conv1"].wgrad(da, r["in"], g(q + "conv1.0"), g(q + "conv1.0", "bias"))
-            o[blk + "downsample"].wgrad(dd, r["in"], g(q + "downsample.0"), g(q + "downsample.0", "bias"))
+            da = o[blk + "conv1n"].bwd(r["a"], r["as"], relu, day, dgamma=g(q + "conv1.1"), dbeta=g(q + "conv1.1", "bias"), dsum=g(q + "conv1.0", "bias"))
+            o[blk + "conv1"].wgrad(da, r["in"], g(q + "conv1.0"), None)
+            o[blk + "downsample"].wgrad(dd, r["in"], g(q + "downsample.0"), None)
             din = o[blk + "conv1"].dgrad(da, r["in"])
             o[blk + "downsample"].dgrad(dd, r["in"], dx=din, beta=1.0)
             dcur = din
         dy1 = o["pool"].bwd(dcur, c["i1"], c["y1"].dims, cdt)
-        dh1 = o["g1"].bwd(c["h1"], c["s1"], relu, dy1, dgamma=g(FE + "conv1.1"), dbeta=g(FE + "conv1.1", "bias"))
-        o["c1"].wgrad(dh1, c["x"], g(FE + "conv1.0"), g(FE + "conv1.0", "bias"))
+        dh1 = o["g1"].bwd(c["h1"], c["s1"], relu, dy1, dgamma=g(FE + "conv1.1"), dbeta=g(FE + "conv1.1", "bias"), dsum=g(FE + "conv1.0", "bias"))
+        o["c1"].wgrad(dh1, c["x"], g(FE + "conv1.0"), None)
         if not input_grad:
             return None
         return o["c1"].dgrad(dh1, c["x"], dx_dtype=torch.float32)

@@ -115,15 +115,18 @@ class SNDiscriminator(ExpertModule):
         m = lambda n: get_module(self, n)
         sig = ctx["sig"]
 
-        def wgrad(name, dy, x):
+        def wgrad(name, dy, x, bias_done=True):
             if not weight_grads:
                 return
             mod = m(name)
             op = o[name]
             g_sn = torch.empty_like(mod.weight_orig)
             op.wgrad(dy, x, g_sn, None, beta=0.0)          # grad of W/sigma
-            channel_sum(dy, mod.bias.grad, beta=1.0)        # bias is not normalised
+            if not bias_done:                               # bias is not normalised
+                channel_sum(dy, mod.bias.grad, beta=1.0)
             o["sn:" + name].bwd(g_sn, sig[name], mod.weight_orig.grad, beta=1.0)
+
+        bias_g = (lambda n: m(n).bias.grad) if weight_grads else (lambda n: None)
 
         # latent gradient: dlat (SDI) + fc3^T dout
         dl = Act.rows(B, 64, cdt, dev, zero=True)
@@ -134,16 +137,16 @@ class SNDiscriminator(ExpertModule):
             if cdt != torch.float32:
                 dout_c = dout.like_nhwc(cdt)
                 copy_act(dout, dout_c)
-            wgrad("fc3", dout_c, ctx["lat"])
+            wgrad("fc3", dout_c, ctx["lat"], bias_done=False)
             o["fc3"].dgrad(dout_c, ctx["lat"], inv_scale=sig["fc3"][0], dx=dl, beta=1.0)
         dh4 = o["ln2"].bwd(ctx["h4"], ctx["s4"], lr, dl,
                            dgamma=m("fc2.1").weight.grad if weight_grads else None,
-                           dbeta=m("fc2.1").bias.grad if weight_grads else None)
+                           dbeta=m("fc2.1").bias.grad if weight_grads else None, dsum=bias_g("fc2.0"))
         wgrad("fc2.0", dh4, ctx["y3"])
         dy3 = o["fc2.0"].dgrad(dh4, ctx["y3"], inv_scale=sig["fc2.0"][0])
         dh3 = o["ln1"].bwd(ctx["h3"], ctx["s3"], lr, dy3,
                            dgamma=m("fc1.1").weight.grad if weight_grads else None,
-                           dbeta=m("fc1.1").bias.grad if weight_grads else None)
+                           dbeta=m("fc1.1").bias.grad if weight_grads else None, dsum=bias_g("fc1.0"))
         wgrad("fc1.0", dh3, ctx["X"])
         dX = o["fc1.0"].dgrad(dh3, ctx["X"], inv_scale=sig["fc1.0"][0])
         F = self.flat_dim + self.cond_dim
@@ -152,13 +155,15 @@ class SNDiscriminator(ExpertModule):
         dy2 = o["pool2"].bwd(dfeat, ctx["i2"], ctx["y2"].dims, cdt)
         dh2 = o["gn2"].bwd(ctx["h2"], ctx["s2"], lr, dy2,
                            dgamma=m("conv_layers.5").weight.grad if weight_grads else None,
-                           dbeta=m("conv_layers.5").bias.grad if weight_grads else None)
+                           dbeta=m("conv_layers.5").bias.grad if weight_grads else None,
+                           dsum=bias_g("conv_layers.4"))
         wgrad("conv_layers.4", dh2, ctx["p1"])
         dp1 = o["conv_layers.4"].dgrad(dh2, ctx["p1"], inv_scale=sig["conv_layers.4"][0])
         dy1 = o["pool1"].bwd(dp1, ctx["i1"], ctx["y1"].dims, cdt)
         dh1 = o["gn1"].bwd(ctx["h1"], ctx["s1"], lr, dy1,
                            dgamma=m("conv_layers.1").weight.grad if weight_grads else None,
-                           dbeta=m("conv_layers.1").bias.grad if weight_grads else None)
+                           dbeta=m("conv_layers.1").bias.grad if weight_grads else None,
+                           dsum=bias_g("conv_layers.0"))
         wgrad("conv_layers.0", dh1, ctx["x"])
         if not input_grad:
             return None

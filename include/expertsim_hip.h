@@ -135,13 +135,14 @@ int es_norm_act_fwd(const es_view_t* x, es_dtype_t xdt, const es_norm_t* nm, con
                     const es_view_t* y, es_dtype_t ydt, void* yp, es_stream_t stream);
 /* Backward of es_norm_act_fwd.  dy: gradient of y.  act_ref (optional): evaluate the activation
  * derivative on this stored tensor (the block output) instead of the recomputed pre-activation.
- * Writes dx (beta=1 accumulates), accumulates dgamma/dbeta (fp32, may be NULL). */
+ * Writes dx (beta=1 accumulates), accumulates dgamma/dbeta (fp32, may be NULL) and, when dsum is
+ * given (C <= 1024), the per-channel sum of dx (the gradient of a conv bias feeding the norm). */
 int64_t es_norm_bwd_ws_bytes(const es_view_t* x, int kind, int groups);
 int es_norm_act_bwd(const es_view_t* x, es_dtype_t xdt, const void* xp, const es_norm_t* nm,
                     const es_chain_t* ch, const es_view_t* dy, es_dtype_t dydt, const void* dyp,
                     const es_view_t* act_ref, es_dtype_t rdt, const void* refp,
                     const es_view_t* dx, es_dtype_t dxdt, void* dxp, float beta, float* dgamma,
-                    float* dbeta, void* ws, es_stream_t stream);
+                    float* dbeta, float* dsum, void* ws, es_stream_t stream);
 
 /* Plain elementwise chain without normalisation (router LeakyReLU, final ReLU, casts):
  * y = chain(x). And its backward dx = beta*dx + dchain(dy) evaluated at x (or act_ref). */
