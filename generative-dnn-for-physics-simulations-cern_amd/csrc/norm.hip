@@ -17,6 +17,23 @@
 //            block per group, two passes (mean, then centred sum of squares).
 #include "common.h"
 
+// fast path for dense channels-last BatchNorm (norm_fast.hip)
+bool es_fast_dense_nhwc(const es_view_t* v);
+int64_t es_fast_part_floats(const es_view_t* v);
+int es_fast_bn_stats(const es_view_t* v, es_dtype_t dt, const void* xp, float* part, hipStream_t st);
+void es_fast_bn_fwd(const es_view_t* v, es_dtype_t dt, const void* xp, void* yp, const es_norm_t* nm,
+                    const es_chain_t* ch, hipStream_t st);
+int es_fast_bn_bwd_reduce(const es_view_t* v, es_dtype_t dt, const void* xp, const void* dyp, const es_norm_t* nm,
+                          const es_chain_t* ch, float* part, hipStream_t st);
+void es_fast_bn_bwd_apply(const es_view_t* v, es_dtype_t dt, const void* xp, const void* dyp, void* dxp,
+                          const es_norm_t* nm, const es_chain_t* ch, const float* a1, const float* a2,
+                          float* dsum, hipStream_t st);
+
+static bool same_view(const es_view_t* a, const es_view_t* b) {
+  return a->n == b->n && a->c == b->c && a->h == b->h && a->w == b->w && a->s[0] == b->s[0] &&
+         a->s[1] == b->s[1] && a->s[2] == b->s[2] && a->s[3] == b->s[3];
+}
+
 namespace {
 
 struct View {
@@ -442,7 +459,9 @@ extern "C" int64_t es_norm_stats_ws_bytes(const es_view_t* x, int kind, int grou
   View v = mkview(x);
   int cb, chunks; int64_t rows, per;
   colred_geometry(v, cb, chunks, rows, per);
-  return (int64_t)chunks * 3 * v.c * sizeof(float);
+  int64_t b = (int64_t)chunks * 3 * v.c * sizeof(float);
+  if (es_fast_dense_nhwc(x)) b = std::max<int64_t>(b, es_fast_part_floats(x) * (int64_t)sizeof(float));
+  return b;
 }
 
 extern "C" int es_norm_stats(const es_view_t* x, es_dtype_t xdt, const void* xp, int kind,
@@ -458,7 +477,10 @@ extern "C" int es_norm_stats(const es_view_t* x, es_dtype_t xdt, const void* xp,
     int cb, chunks; int64_t rows, per;
     colred_geometry(b.x, cb, chunks, rows, per);
     ES_CHECK_ARG(ws != nullptr, "norm_stats: BN needs workspace");
-    hipLaunchKernelGGL(colred_kernel<RED_STATS>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, (float*)ws);
+    if (es_fast_dense_nhwc(x))
+      chunks = es_fast_bn_stats(x, xdt, xp, (float*)ws, st);
+    else
+      hipLaunchKernelGGL(colred_kernel<RED_STATS>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, (float*)ws);
     if (chunks > 32)
       hipLaunchKernelGGL(bn_finalize_block_kernel, dim3(x->c), dim3(256), 0, st, (const float*)ws, chunks, x->c,
                          eps, mean, invstd, running_mean, running_var, momentum);
@@ -478,6 +500,11 @@ extern "C" int es_norm_act_fwd(const es_view_t* x, es_dtype_t xdt, const es_norm
                                const void* addend_ptr, const void* xp, const es_view_t* y,
                                es_dtype_t ydt, void* yp, es_stream_t stream) {
   ES_CHECK_ARG(x->n == y->n && x->c == y->c && x->h == y->h && x->w == y->w, "norm_act_fwd: shape");
+  if (nm && nm->kind == ES_NORM_BN && !addend_ptr && xdt == ydt && es_fast_dense_nhwc(x) && same_view(x, y)) {
+    es_fast_bn_fwd(x, xdt, xp, yp, nm, ch, (hipStream_t)stream);
+    ES_CHECK_LAUNCH();
+    return ES_OK;
+  }
   FwdArgs a{};
   a.x = mkview(x); a.xp = xp; a.xbf = xdt == ES_BF16;
   a.y = mkview(y); a.yp = yp; a.ybf = ydt == ES_BF16;
@@ -499,7 +526,8 @@ extern "C" int64_t es_norm_bwd_ws_bytes(const es_view_t* x, int kind, int groups
   View v = mkview(x);
   int cb, chunks; int64_t rows, per;
   colred_geometry(v, cb, chunks, rows, per);
-  const int64_t part = (int64_t)chunks * 3 * v.c * sizeof(float);
+  int64_t part = (int64_t)chunks * 3 * v.c * sizeof(float);
+  if (es_fast_dense_nhwc(x)) part = std::max<int64_t>(part, es_fast_part_floats(x) * (int64_t)sizeof(float));
   const int64_t ng = kind == ES_NORM_NONE ? 0 : stats_groups(x, kind, groups);
   return part + 2 * ng * (int64_t)sizeof(float) + 256;
 }
@@ -524,9 +552,25 @@ extern "C" int es_norm_act_bwd(const es_view_t* x, es_dtype_t xdt, const void* x
   int cb, chunks; int64_t rows, per;
   colred_geometry(b.x, cb, chunks, rows, per);
   float* part = (float*)ws;
-  float* g1 = part + (int64_t)chunks * 3 * x->c;
+  int64_t part_floats = (int64_t)chunks * 3 * x->c;
+  const bool fast = kind == ES_NORM_BN && !refp && beta == 0.f && xdt == dydt && dydt == dxdt &&
+                    es_fast_dense_nhwc(x) && same_view(x, dy) && same_view(x, dx);
+  if (es_fast_dense_nhwc(x)) part_floats = std::max<int64_t>(part_floats, es_fast_part_floats(x));
+  float* g1 = part + part_floats;
   const int64_t ng = kind == ES_NORM_NONE ? 0 : stats_groups(x, kind, groups);
   float* g2 = g1 + ng;
+  if (fast) {
+    const int fchunks = es_fast_bn_bwd_reduce(x, xdt, xp, dyp, nm, ch, part, st);
+    if (fchunks > 32)
+      hipLaunchKernelGGL(sums_finalize_block_kernel, dim3(x->c), dim3(256), 0, st, (const float*)part, fchunks,
+                         x->c, (float)rows, nm->gamma, g1, g2, dbeta, dgamma, 1.f);
+    else
+      hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)part,
+                         fchunks, x->c, (float)rows, nm->gamma, g1, g2, dgamma, dbeta);
+    if (dxp) es_fast_bn_bwd_apply(x, xdt, xp, dyp, dxp, nm, ch, g1, g2, dsum, st);
+    ES_CHECK_LAUNCH();
+    return ES_OK;
+  }
   if (kind == ES_NORM_BN) {
     hipLaunchKernelGGL(colred_kernel<RED_BWD>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, part);
     if (chunks > 32)

@@ -1,0 +1,394 @@
+// Fast path of the BatchNorm + dropout + activation pipeline for dense channels-last tensors.
+//
+// Covers every BatchNorm of the neutron generator and aux regressor (neutron/generator.py:13,19,
+// 26,31,35; neutron/aux_reg.py:15,23,31,39,47) when x, y / dy, dx are NHWC-dense ([rows][C],
+// rows = N*H*W) of one dtype and C % 8 == 0.  Layout of the work: a thread owns 8 consecutive
+// channels (one 16-byte bf16 / 32-byte fp32 vector) of 4 consecutive rows, so
+//   * no per-element index division (one division per 4 rows),
+//   * 16-byte vector loads and stores,
+//   * one Philox4x32 call serves the 4 rows of a channel when H*W % 4 == 0 (the 4 rows then hold
+//     the 4 consecutive NCHW-logical indices that share a Philox counter), or 4 channels of a row
+//     when H*W == 1 (linear BatchNorm1d) — instead of one call per element.
+// Statistics / backward sums are reduced per block in LDS into [chunk][3][C] partials that the
+// finalize kernels of norm.hip merge.
+#include "common.h"
+
+namespace {
+
+template <typename T> __device__ __forceinline__ void ld8(const T* p, float* f);
+template <> __device__ __forceinline__ void ld8<bf16>(const bf16* p, float* f) {
+  const bf16x8 v = *(const bf16x8*)p;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) f[k] = (float)v[k];
+}
+template <> __device__ __forceinline__ void ld8<float>(const float* p, float* f) {
+  const float4 a = ((const float4*)p)[0], b = ((const float4*)p)[1];
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+template <typename T> __device__ __forceinline__ void st8(T* p, const float* f);
+template <> __device__ __forceinline__ void st8<bf16>(bf16* p, const float* f) {
+  bf16x8 v;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = (bf16)f[k];
+  *(bf16x8*)p = v;
+}
+template <> __device__ __forceinline__ void st8<float>(float* p, const float* f) {
+  ((float4*)p)[0] = make_float4(f[0], f[1], f[2], f[3]);
+  ((float4*)p)[1] = make_float4(f[4], f[5], f[6], f[7]);
+}
+
+struct FastArgs {
+  const void* x; const void* dy; void* out;   // out: y (fwd) or dx (bwd apply)
+  int rows, C, HW;
+  const float *mean, *invstd, *gamma, *beta;
+  const float *a1, *a2;                       // bwd apply: per-channel gamma*mean(dnorm), gamma*mean(dnorm*xhat)
+  float* part;                                // [chunk][3][C] partials (stats / bwd sums)
+  float* dsum;                                // bwd apply: per-channel sum of dx (conv-bias gradient)
+  es_dropout_t drop;
+  int dfirst, act;
+  float slope;
+};
+
+__device__ __forceinline__ float actf(const FastArgs& a, float v) {
+  return a.act == ES_ACT_RELU ? fmaxf(v, 0.f) : (a.act == ES_ACT_LRELU ? lrelu(v, a.slope) : v);
+}
+__device__ __forceinline__ float dactf(const FastArgs& a, float v) {
+  return a.act == ES_ACT_RELU ? (v > 0.f ? 1.f : 0.f) : (a.act == ES_ACT_LRELU ? (v > 0.f ? 1.f : a.slope) : 1.f);
+}
+
+// keep bits for rows r0..r0+3 (bit k = channel c0+k)
+__device__ __forceinline__ void keep_bits(const FastArgs& a, int r0, int c0, uint32_t (&keep)[4]) {
+  if (!a.drop.enabled) { keep[0] = keep[1] = keep[2] = keep[3] = 0xFFu; return; }
+  keep[0] = keep[1] = keep[2] = keep[3] = 0u;
+  const uint32_t thr = a.drop.threshold;
+  const uint32_t k0 = (uint32_t)a.drop.seed, k1 = (uint32_t)(a.drop.seed >> 32);
+  if ((a.HW & 3) == 0) {
+    const int n = r0 / a.HW, hw0 = r0 - n * a.HW;     // r0 % 4 == 0 -> same n for the 4 rows
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint64_t base = ((uint64_t)n * a.C + c0 + k) * (uint64_t)a.HW + hw0;
+      const uint64_t q = base >> 2;
+      const u32x4 w = philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), a.drop.stream, 0u, k0, k1);
+      keep[0] |= (uint32_t)((w.x >> 8) < thr) << k;
+      keep[1] |= (uint32_t)((w.y >> 8) < thr) << k;
+      keep[2] |= (uint32_t)((w.z >> 8) < thr) << k;
+      keep[3] |= (uint32_t)((w.w >> 8) < thr) << k;
+    }
+  } else if (a.HW == 1 && (a.C & 3) == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = r0 + j;
+      if (r >= a.rows) break;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint64_t q = ((uint64_t)r * a.C + c0 + 4 * h) >> 2;
+        const u32x4 w = philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), a.drop.stream, 0u, k0, k1);
+        keep[j] |= ((uint32_t)((w.x >> 8) < thr) | ((uint32_t)((w.y >> 8) < thr) << 1) |
+                    ((uint32_t)((w.z >> 8) < thr) << 2) | ((uint32_t)((w.w >> 8) < thr) << 3)) << (4 * h);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = r0 + j;
+      if (r >= a.rows) break;
+      const int n = r / a.HW, hw = r - n * a.HW;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint64_t i = ((uint64_t)n * a.C + c0 + k) * (uint64_t)a.HW + hw;
+        keep[j] |= (uint32_t)((philox_word(a.drop.seed, a.drop.stream, i) >> 8) < thr) << k;
+      }
+    }
+  }
+}
+
+// forward chain on a normalised value z with keep bit
+__device__ __forceinline__ float chain_fwd(const FastArgs& a, float z, bool keep) {
+  if (!a.drop.enabled) return actf(a, z);
+  if (a.dfirst) return actf(a, keep ? z * a.drop.scale : 0.f);
+  return keep ? actf(a, z) * a.drop.scale : 0.f;
+}
+// d out / d z
+__device__ __forceinline__ float chain_bwd(const FastArgs& a, float z, float dout, bool keep) {
+  if (!a.drop.enabled) return dout * dactf(a, z);
+  if (!keep) return 0.f;
+  if (a.dfirst) return dout * dactf(a, z * a.drop.scale) * a.drop.scale;
+  return dout * a.drop.scale * dactf(a, z);
+}
+
+struct Geo {
+  int CV, TCV, RGB, cv, rg, c0;
+  bool active;
+};
+__device__ __forceinline__ Geo geo(const FastArgs& a) {
+  Geo g;
+  g.CV = a.C >> 3;
+  g.TCV = min(g.CV, 64);
+  g.RGB = 256 / g.TCV;
+  g.cv = blockIdx.x * g.TCV + (int)(threadIdx.x % g.TCV);
+  g.rg = threadIdx.x / g.TCV;
+  g.active = g.rg < g.RGB && g.cv < g.CV;
+  g.c0 = g.cv * 8;
+  return g;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bn_fwd_fast(FastArgs a) {
+  const Geo g = geo(a);
+  if (!g.active) return;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = g.c0 + k;
+    const float s = (a.gamma ? a.gamma[c] : 1.f) * a.invstd[c];
+    sc[k] = s;
+    sh[k] = (a.beta ? a.beta[c] : 0.f) - a.mean[c] * s;
+  }
+  const T* x = (const T*)a.x;
+  T* y = (T*)a.out;
+  const int ngroups = (a.rows + 3) >> 2;
+  for (int grp = blockIdx.y * g.RGB + g.rg; grp < ngroups; grp += gridDim.y * g.RGB) {
+    const int r0 = grp * 4;
+    uint32_t keep[4];
+    keep_bits(a, r0, g.c0, keep);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = r0 + j;
+      if (r >= a.rows) break;
+      float v[8];
+      ld8<T>(x + (int64_t)r * a.C + g.c0, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = chain_fwd(a, v[k] * sc[k] + sh[k], (keep[j] >> k) & 1u);
+      st8<T>(y + (int64_t)r * a.C + g.c0, v);
+    }
+  }
+}
+
+// MODE 0: Welford stats of x.  MODE 1: backward sums (sum dnorm, sum dnorm*xhat).
+template <typename T, int MODE>
+__global__ void __launch_bounds__(256) bn_reduce_fast(FastArgs a) {
+  const Geo g = geo(a);
+  float s0[8], s1[8], s2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s0[k] = s1[k] = s2[k] = 0.f;
+  float sc[8], sh[8], mu[8], is[8];
+  if (g.active) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = g.c0 + k;
+      if (MODE == 1) {
+        mu[k] = a.mean[c]; is[k] = a.invstd[c];
+        const float s = (a.gamma ? a.gamma[c] : 1.f) * is[k];
+        sc[k] = s; sh[k] = (a.beta ? a.beta[c] : 0.f) - mu[k] * s;
+      }
+    }
+    const T* x = (const T*)a.x;
+    const T* dy = (const T*)a.dy;
+    const int ngroups = (a.rows + 3) >> 2;
+    for (int grp = blockIdx.y * g.RGB + g.rg; grp < ngroups; grp += gridDim.y * g.RGB) {
+      const int r0 = grp * 4;
+      uint32_t keep[4];
+      if (MODE == 1) keep_bits(a, r0, g.c0, keep);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = r0 + j;
+        if (r >= a.rows) break;
+        float v[8];
+        ld8<T>(x + (int64_t)r * a.C + g.c0, v);
+        if (MODE == 0) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            s0[k] += 1.f;
+            const float d = v[k] - s1[k];
+            s1[k] += d / s0[k];
+            s2[k] += d * (v[k] - s1[k]);
+          }
+        } else {
+          float d[8];
+          ld8<T>(dy + (int64_t)r * a.C + g.c0, d);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float dn = chain_bwd(a, v[k] * sc[k] + sh[k], d[k], (keep[j] >> k) & 1u);
+            const float xh = (v[k] - mu[k]) * is[k];
+            s1[k] += dn;
+            s2[k] += dn * xh;
+          }
+        }
+      }
+    }
+  }
+  // block merge across row groups (same channels) through LDS
+  __shared__ float l0[256 * 8], l1[256 * 8], l2[256 * 8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    l0[threadIdx.x * 8 + k] = s0[k]; l1[threadIdx.x * 8 + k] = s1[k]; l2[threadIdx.x * 8 + k] = s2[k];
+  }
+  __syncthreads();
+  if (g.active && g.rg == 0) {
+    for (int r = 1; r < g.RGB; ++r) {
+      const int o = (r * g.TCV + (int)(threadIdx.x % g.TCV)) * 8;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (MODE == 0) {
+          const float nb = l0[o + k];
+          if (nb == 0.f) continue;
+          const float mb = l1[o + k], Mb = l2[o + k];
+          const float nt = s0[k] + nb, dl = mb - s1[k];
+          s1[k] += dl * nb / nt;
+          s2[k] += Mb + dl * dl * s0[k] * nb / nt;
+          s0[k] = nt;
+        } else {
+          s1[k] += l1[o + k];
+          s2[k] += l2[o + k];
+        }
+      }
+    }
+    float* p = a.part + (int64_t)blockIdx.y * 3 * a.C;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      p[g.c0 + k] = s0[k]; p[a.C + g.c0 + k] = s1[k]; p[2 * a.C + g.c0 + k] = s2[k];
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bn_bwd_apply_fast(FastArgs a) {
+  const Geo g = geo(a);
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  if (g.active) {
+    float sc[8], sh[8], mu[8], is[8], ga[8], c1[8], c2[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = g.c0 + k;
+      mu[k] = a.mean[c]; is[k] = a.invstd[c];
+      ga[k] = a.gamma ? a.gamma[c] : 1.f;
+      sc[k] = ga[k] * is[k]; sh[k] = (a.beta ? a.beta[c] : 0.f) - mu[k] * sc[k];
+      c1[k] = a.a1[c]; c2[k] = a.a2[c];
+    }
+    const T* x = (const T*)a.x;
+    const T* dy = (const T*)a.dy;
+    T* dx = (T*)a.out;
+    const int ngroups = (a.rows + 3) >> 2;
+    for (int grp = blockIdx.y * g.RGB + g.rg; grp < ngroups; grp += gridDim.y * g.RGB) {
+      const int r0 = grp * 4;
+      uint32_t keep[4];
+      keep_bits(a, r0, g.c0, keep);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = r0 + j;
+        if (r >= a.rows) break;
+        float v[8], d[8];
+        ld8<T>(x + (int64_t)r * a.C + g.c0, v);
+        ld8<T>(dy + (int64_t)r * a.C + g.c0, d);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float dn = chain_bwd(a, v[k] * sc[k] + sh[k], d[k], (keep[j] >> k) & 1u);
+          const float xh = (v[k] - mu[k]) * is[k];
+          d[k] = is[k] * (dn * ga[k] - c1[k] - xh * c2[k]);
+          acc[k] += d[k];
+        }
+        st8<T>(dx + (int64_t)r * a.C + g.c0, d);
+      }
+    }
+  }
+  if (a.dsum) {
+    __shared__ float l1[256 * 8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) l1[threadIdx.x * 8 + k] = acc[k];
+    __syncthreads();
+    if (g.active && g.rg == 0) {
+      for (int r = 1; r < g.RGB; ++r) {
+        const int o = (r * g.TCV + (int)(threadIdx.x % g.TCV)) * 8;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += l1[o + k];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) atomicAdd(&a.dsum[g.c0 + k], acc[k]);
+    }
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------- host dispatch
+// Returns true when the fast path applies to these views (dense NHWC, same dtype, C % 8 == 0).
+bool es_fast_dense_nhwc(const es_view_t* v) {
+  const int64_t C = v->c, W = v->w, H = v->h;
+  return v->c % 8 == 0 && v->s[1] == 1 && v->s[3] == C && v->s[2] == W * C && v->s[0] == H * W * C;
+}
+
+static void fast_geometry(const es_view_t* v, dim3& grid, int& chunks) {
+  const int CV = v->c / 8;
+  const int TCV = CV < 64 ? CV : 64;
+  const int RGB = 256 / TCV;
+  const int gx = (CV + TCV - 1) / TCV;
+  const int64_t rows = (int64_t)v->n * v->h * v->w;
+  const int64_t ngroups = (rows + 3) / 4;
+  int64_t gy = std::max<int64_t>(1, 2048 / gx);
+  gy = std::min<int64_t>(gy, (ngroups + RGB - 1) / RGB);
+  grid = dim3(gx, (unsigned)gy);
+  chunks = (int)gy;
+}
+
+int64_t es_fast_part_floats(const es_view_t* v) {
+  dim3 g; int chunks;
+  fast_geometry(v, g, chunks);
+  return (int64_t)chunks * 3 * v->c;
+}
+
+static FastArgs mk(const es_view_t* v, const es_chain_t* ch) {
+  FastArgs a{};
+  a.rows = v->n * v->h * v->w;
+  a.C = v->c;
+  a.HW = v->h * v->w;
+  if (ch) { a.drop = ch->drop; a.dfirst = ch->dropout_first; a.act = ch->act; a.slope = ch->slope; }
+  return a;
+}
+
+// stats -> partials (caller runs the BN finalize); returns chunks
+int es_fast_bn_stats(const es_view_t* v, es_dtype_t dt, const void* xp, float* part, hipStream_t st) {
+  dim3 grid; int chunks;
+  fast_geometry(v, grid, chunks);
+  FastArgs a = mk(v, nullptr);
+  a.x = xp; a.part = part;
+  if (dt == ES_BF16) hipLaunchKernelGGL((bn_reduce_fast<bf16, 0>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((bn_reduce_fast<float, 0>), grid, dim3(256), 0, st, a);
+  return chunks;
+}
+
+void es_fast_bn_fwd(const es_view_t* v, es_dtype_t dt, const void* xp, void* yp, const es_norm_t* nm,
+                    const es_chain_t* ch, hipStream_t st) {
+  dim3 grid; int chunks;
+  fast_geometry(v, grid, chunks);
+  FastArgs a = mk(v, ch);
+  a.x = xp; a.out = yp;
+  a.mean = nm->mean; a.invstd = nm->invstd; a.gamma = nm->gamma; a.beta = nm->beta;
+  if (dt == ES_BF16) hipLaunchKernelGGL(bn_fwd_fast<bf16>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(bn_fwd_fast<float>, grid, dim3(256), 0, st, a);
+}
+
+int es_fast_bn_bwd_reduce(const es_view_t* v, es_dtype_t dt, const void* xp, const void* dyp, const es_norm_t* nm,
+                          const es_chain_t* ch, float* part, hipStream_t st) {
+  dim3 grid; int chunks;
+  fast_geometry(v, grid, chunks);
+  FastArgs a = mk(v, ch);
+  a.x = xp; a.dy = dyp; a.part = part;
+  a.mean = nm->mean; a.invstd = nm->invstd; a.gamma = nm->gamma; a.beta = nm->beta;
+  if (dt == ES_BF16) hipLaunchKernelGGL((bn_reduce_fast<bf16, 1>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((bn_reduce_fast<float, 1>), grid, dim3(256), 0, st, a);
+  return chunks;
+}
+
+void es_fast_bn_bwd_apply(const es_view_t* v, es_dtype_t dt, const void* xp, const void* dyp, void* dxp,
+                          const es_norm_t* nm, const es_chain_t* ch, const float* a1, const float* a2,
+                          float* dsum, hipStream_t st) {
+  dim3 grid; int chunks;
+  fast_geometry(v, grid, chunks);
+  FastArgs a = mk(v, ch);
+  a.x = xp; a.dy = dyp; a.out = dxp; a.a1 = a1; a.a2 = a2; a.dsum = dsum;
+  a.mean = nm->mean; a.invstd = nm->invstd; a.gamma = nm->gamma; a.beta = nm->beta;
+  if (dt == ES_BF16) hipLaunchKernelGGL(bn_bwd_apply_fast<bf16>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(bn_bwd_apply_fast<float>, grid, dim3(256), 0, st, a);
+}

@@ -132,15 +132,20 @@ def _chain_ref(y, p, mask, act, dropout_first):
     return lre(y) * (mask.float() * scale)
 
 
-@pytest.mark.parametrize("kind", ["bn2d", "bn1d", "gn", "ln"])
+@pytest.mark.parametrize("kind", ["bn2d", "bn1d", "gn", "ln", "bn2d_hw4", "bn1d_c8", "bn2d_bf16"])
 @pytest.mark.parametrize("drop", [False, True])
 def test_norm_chain(kind, drop):
     hip = _hip()
     from expertsim.layers import Act, NormOp
     from expertsim.utils import philox
     torch.manual_seed(2)
-    if kind == "bn2d":
-        x = torch.randn(4, 32, 9, 7) * 3 + 1.5
+    dtype = torch.bfloat16 if kind.endswith("bf16") else torch.float32
+    if kind in ("bn2d", "bn2d_bf16"):
+        x = torch.randn(4, 32, 9, 7) * 3 + 1.5          # H*W % 4 != 0 (per-element Philox)
+    elif kind == "bn2d_hw4":
+        x = torch.randn(3, 64, 8, 6) * 2 + 0.5          # H*W % 4 == 0 (4 rows per Philox call)
+    elif kind == "bn1d_c8":
+        x = torch.randn(7, 304) * 2 + 0.5               # linear BN1d, C % 8 == 0 (fast path)
     elif kind == "gn":
         x = torch.randn(3, 32, 6, 5) * 2 - 1
     else:
@@ -149,6 +154,8 @@ def test_norm_chain(kind, drop):
     beta = torch.randn(x.shape[1])
     p, seed, stream = 0.2, 1234, 77
     mask = torch.from_numpy(philox.dropout_mask(tuple(x.shape), p, seed, stream)) if drop else None
+    if dtype == torch.bfloat16:
+        x = x.to(torch.bfloat16).float()                 # reference sees the bf16-rounded input
     xr = x.clone().requires_grad_(True)
     g_, b_ = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
     rm, rv = torch.zeros(x.shape[1]), torch.ones(x.shape[1])
@@ -163,8 +170,10 @@ def test_norm_chain(kind, drop):
         nk = hip.NORM_LN
     y = _chain_ref(z, p, mask, "lrelu", True)
     gy = torch.randn_like(y)
+    if dtype == torch.bfloat16:
+        gy = gy.to(torch.bfloat16).float()
     y.backward(gy)
-    xa = to_act(x) if x.dim() == 4 else Act.of(x.to(DEV).contiguous())
+    xa = to_act(x, dtype) if x.dim() == 4 else Act.of(x.to(DEV, dtype).contiguous())
     dg = torch.zeros_like(gamma, device=DEV)
     dbt = torch.zeros_like(beta, device=DEV)
     rmd, rvd = torch.zeros(x.shape[1], device=DEV), torch.ones(x.shape[1], device=DEV)
@@ -172,16 +181,21 @@ def test_norm_chain(kind, drop):
     d = hip.dropout_struct(p, seed, stream, enabled=drop)
     ch = hip.chain_struct(hip.ACT_LRELU, 0.1, d, dropout_first=True)
     ya, stats = op.fwd(xa, ch)
-    out = from_act(ya) if x.dim() == 4 else ya.rows2d().cpu()
-    assert rel(out, y.detach()) < 2e-5
+    out = from_act(ya) if x.dim() == 4 else ya.rows2d().float().cpu()
+    ftol = 2e-5 if dtype == torch.float32 else 1e-2
+    assert rel(out, y.detach()) < ftol
     if kind.startswith("bn"):
         assert rel(rmd.cpu(), rm) < 1e-5 and rel(rvd.cpu(), rv) < 1e-5
-    gya = to_act(gy) if x.dim() == 4 else Act.of(gy.to(DEV).contiguous())
-    dxa = op.bwd(xa, stats, ch, gya, dgamma=dg, dbeta=dbt)
-    dx = from_act(dxa) if x.dim() == 4 else dxa.rows2d().cpu()
-    assert rel(dx, xr.grad) < 1e-4
-    assert rel(dg.cpu(), g_.grad) < 1e-4
-    assert rel(dbt.cpu(), b_.grad) < 1e-4
+    gya = to_act(gy, dtype) if x.dim() == 4 else Act.of(gy.to(DEV, dtype).contiguous())
+    dsum = torch.zeros(x.shape[1], device=DEV)
+    dxa = op.bwd(xa, stats, ch, gya, dgamma=dg, dbeta=dbt, dsum=dsum)
+    dx = from_act(dxa) if x.dim() == 4 else dxa.rows2d().float().cpu()
+    btol = 1e-4 if dtype == torch.float32 else 2e-2
+    assert rel(dx, xr.grad) < btol
+    assert rel(dg.cpu(), g_.grad) < btol
+    assert rel(dbt.cpu(), b_.grad) < btol
+    red = (0, 2, 3) if x.dim() == 4 else (0,)
+    assert float((dsum.cpu() - xr.grad.sum(red)).abs().max()) < 1e-3 * max(1.0, float(xr.grad.abs().max()))
 
 
 def test_dropout_mask_bit_exact():
