@@ -51,7 +51,24 @@ struct LdsImg {
   }
 };
 
+// Unsigned division by a run-time constant (x < 2^31): q = (umulhi(x, m) + x) >> l.
+struct FastDiv {
+  uint32_t m;
+  int l;
+};
+inline FastDiv mkdiv(uint32_t d) {
+  FastDiv f;
+  f.l = 0;
+  while ((1ull << f.l) < d) ++f.l;
+  f.m = (uint32_t)(((1ull << 32) * ((1ull << f.l) - d)) / d + 1);
+  return f;
+}
+__device__ __forceinline__ int fdiv(int x, FastDiv f) {
+  return (int)((__umulhi((uint32_t)x, f.m) + (uint32_t)x) >> f.l);
+}
+
 struct ConvArgs {
+  FastDiv fC, fS, fK, fQ, fP, fWu, fHu;
   es_conv_desc_t d;
   const void* a_src;
   const void* b_src;
@@ -127,87 +144,148 @@ struct Stager {
   typedef typename Vec16<T>::type V;
   static constexpr int VN = Vec16<T>::N;
   static constexpr int BK = KSTEP_BYTES / sizeof(T);
-  static constexpr int CHUNKS = BROWS * (KSTEP_BYTES / 16);
+  static constexpr int CPR = KSTEP_BYTES / 16;          // chunks per LDS row (K-contiguous image)
+  static constexpr int CHUNKS = BROWS * CPR;
   static constexpr int PER_THREAD = CHUNKS / NTHREADS;
   static constexpr bool TRANS = (MODE == MODE_WGRAD);
   V reg[PER_THREAD];
+  // per-chunk state precomputed once per block (vector path): a base offset and two coordinates
+  int64_t boff[PER_THREAD];
+  int c0_[PER_THREAD], c1_[PER_THREAD];
 
-  __device__ __forceinline__ void load(const ConvArgs& a, int row0, int k0) {
+  // --------------------------------------------------------------- precomputation (vector path)
+  __device__ __forceinline__ void init(const ConvArgs& a, int row0) {
+    if constexpr (!VEC) return;
+    const es_conv_desc_t& d = a.d;
 #pragma unroll
     for (int i = 0; i < PER_THREAD; ++i) {
       const int idx = threadIdx.x + i * NTHREADS;
-      int row, kk;
       if constexpr (!TRANS) {
-        row = row0 + idx / (KSTEP_BYTES / 16);
-        kk = k0 + (idx % (KSTEP_BYTES / 16)) * VN;
+        const int row = row0 + idx / CPR;
+        if constexpr (IS_A) {
+          const int rr = row < a.M ? row : 0;
+          if constexpr (MODE == MODE_FWD) {       // row = (n, p, q)
+            const int np = fdiv(rr, a.fQ), q = rr - np * d.Q;
+            const int n = fdiv(np, a.fP), p = np - n * d.P;
+            boff[i] = row < a.M ? (int64_t)n * a.as[0] : -1;
+            c0_[i] = p * d.stride - d.pad;
+            c1_[i] = q * d.stride - d.pad;
+          } else {                                  // DGRAD: row = (n, hu, wu)
+            const int nh = fdiv(rr, a.fWu), wu = rr - nh * d.Wu;
+            const int n = fdiv(nh, a.fHu), hu = nh - n * d.Hu;
+            boff[i] = row < a.M ? (int64_t)n * a.as[0] : -1;
+            c0_[i] = hu + d.pad;
+            c1_[i] = wu + d.pad;
+          }
+        } else {
+          boff[i] = row < a.Ng ? (int64_t)row * a.Kd : -1;
+          c0_[i] = c1_[i] = 0;
+        }
       } else {
-        row = row0 + (idx % (BROWS / VN)) * VN;
-        kk = k0 + idx / (BROWS / VN);
+        const int row = row0 + (idx % (BROWS / VN)) * VN;
+        if constexpr (IS_A) {                       // WGRAD A: m = out channel
+          boff[i] = row < a.M ? (int64_t)row * a.as[1] : -1;
+          c0_[i] = c1_[i] = 0;
+        } else {                                    // WGRAD B: ng = (r, s, c)
+          const int rr = row < a.Ng ? row : 0;
+          const int rs = fdiv(rr, a.fC), c = rr - rs * d.C;
+          const int r = fdiv(rs, a.fS), s_ = rs - r * d.S;
+          boff[i] = row < a.Ng ? (int64_t)c * a.bs[1] : -1;
+          c0_[i] = r - d.pad;
+          c1_[i] = s_ - d.pad;
+        }
       }
-      reg[i] = fetch(a, row, kk);
     }
   }
 
-  __device__ __forceinline__ V fetch(const ConvArgs& a, int row, int kk) {
+  __device__ __forceinline__ void load(const ConvArgs& a, int row0, int k0) {
     if constexpr (VEC) {
-      const T* p = vec_ptr(a, row, kk);
-      if (p) return *(const V*)p;
-      return V{};
+      load_vec(a, k0);
     } else {
-      T e[VN];
 #pragma unroll
-      for (int j = 0; j < VN; ++j) {
-        float f;
-        if constexpr (!TRANS) f = IS_A ? gather_a<T, MODE>(a, row, kk + j) : gather_b<T, MODE>(a, row, kk + j);
-        else f = IS_A ? gather_a<T, MODE>(a, row + j, kk) : gather_b<T, MODE>(a, row + j, kk);
-        e[j] = from_f<T>(f);
+      for (int i = 0; i < PER_THREAD; ++i) {
+        const int idx = threadIdx.x + i * NTHREADS;
+        int row, kk;
+        if constexpr (!TRANS) {
+          row = row0 + idx / CPR;
+          kk = k0 + (idx % CPR) * VN;
+        } else {
+          row = row0 + (idx % (BROWS / VN)) * VN;
+          kk = k0 + idx / (BROWS / VN);
+        }
+        reg[i] = fetch_scalar(a, row, kk);
       }
-      V v; memcpy(&v, e, sizeof(v)); return v;
     }
   }
 
-  // Address of the first element of a vector chunk, or nullptr when the chunk is all zero.
-  // Preconditions (checked on the host): the vector dimension is contiguous and VN-divisible.
-  __device__ __forceinline__ const T* vec_ptr(const ConvArgs& a, int row, int kk) {
+  __device__ __forceinline__ V fetch_scalar(const ConvArgs& a, int row, int kk) {
+    T e[VN];
+#pragma unroll
+    for (int j = 0; j < VN; ++j) {
+      float f;
+      if constexpr (!TRANS) f = IS_A ? gather_a<T, MODE>(a, row, kk + j) : gather_b<T, MODE>(a, row, kk + j);
+      else f = IS_A ? gather_a<T, MODE>(a, row + j, kk) : gather_b<T, MODE>(a, row + j, kk);
+      e[j] = from_f<T>(f);
+    }
+    V v; memcpy(&v, e, sizeof(v)); return v;
+  }
+
+  // vector path: the vector dimension is contiguous and VN-divisible (checked on the host)
+  __device__ __forceinline__ void load_vec(const ConvArgs& a, int k0) {
     const es_conv_desc_t& d = a.d;
-    if constexpr (MODE == MODE_FWD) {
+    const T* src = IS_A ? (const T*)a.a_src : (const T*)a.b_src;
+    if constexpr (!TRANS) {
+      const int kk = k0 + (int)(threadIdx.x % CPR) * VN;   // same column for all chunks
+      const bool kin = kk < a.Kd;
       if constexpr (IS_A) {
-        if (row >= a.M || kk >= a.Kd) return nullptr;
-        const int c = kk % d.C; const int rs = kk / d.C; const int s = rs % d.S; const int r = rs / d.S;
-        const int q = row % d.Q; const int np = row / d.Q; const int p = np % d.P; const int n = np / d.P;
-        const int hu = p * d.stride - d.pad + r, wu = q * d.stride - d.pad + s;
-        if (hu < 0 || hu >= d.Hu || wu < 0 || wu >= d.Wu) return nullptr;
-        return (const T*)a.a_src + off4(a.as, n, c, src_row(d.hmap, hu), src_row(d.wmap, wu));
+        // kk -> (r, s, ch): ch = input channel (FWD) / output channel (DGRAD), fastest
+        const FastDiv fch = MODE == MODE_FWD ? a.fC : a.fK;
+        const int nch = MODE == MODE_FWD ? d.C : d.K;
+        const int rs = fdiv(kk, fch), ch = kk - rs * nch;
+        const int r = fdiv(rs, a.fS), s_ = rs - r * d.S;
+#pragma unroll
+        for (int i = 0; i < PER_THREAD; ++i) {
+          const T* p = nullptr;
+          if (kin && boff[i] >= 0) {
+            if constexpr (MODE == MODE_FWD) {
+              const int hu = c0_[i] + r, wu = c1_[i] + s_;
+              if (hu >= 0 && hu < d.Hu && wu >= 0 && wu < d.Wu)
+                p = src + boff[i] + (int64_t)ch * a.as[1] + (int64_t)src_row(d.hmap, hu) * a.as[2] +
+                    (int64_t)src_row(d.wmap, wu) * a.as[3];
+            } else {
+              int ph = c0_[i] - r, pw = c1_[i] - s_;
+              bool ok = ph >= 0 && pw >= 0;
+              if (d.stride == 2) { ok = ok && !(ph & 1) && !(pw & 1); ph >>= 1; pw >>= 1; }
+              if (ok && ph < d.P && pw < d.Q)
+                p = src + boff[i] + (int64_t)ch * a.as[1] + (int64_t)ph * a.as[2] + (int64_t)pw * a.as[3];
+            }
+          }
+          reg[i] = p ? *(const V*)p : V{};
+        }
       } else {
-        if (row >= a.Ng || kk >= a.Kd) return nullptr;
-        return (const T*)a.b_src + (int64_t)row * a.Kd + kk;
+#pragma unroll
+        for (int i = 0; i < PER_THREAD; ++i)
+          reg[i] = (kin && boff[i] >= 0) ? *(const V*)(src + boff[i] + kk) : V{};
       }
-    } else if constexpr (MODE == MODE_DGRAD) {
-      if constexpr (IS_A) {
-        if (row >= a.M || kk >= a.Kd) return nullptr;
-        const int k = kk % d.K; const int rs = kk / d.K; const int s = rs % d.S; const int r = rs / d.S;
-        const int wu = row % d.Wu; const int nh = row / d.Wu; const int hu = nh % d.Hu; const int n = nh / d.Hu;
-        const int ph = hu + d.pad - r, pw = wu + d.pad - s;
-        if (ph < 0 || pw < 0 || ph % d.stride || pw % d.stride) return nullptr;
-        const int p = ph / d.stride, q = pw / d.stride;
-        if (p >= d.P || q >= d.Q) return nullptr;
-        return (const T*)a.a_src + off4(a.as, n, k, p, q);
-      } else {
-        if (row >= a.Ng || kk >= a.Kd) return nullptr;
-        return (const T*)a.b_src + (int64_t)row * a.Kd + kk;
-      }
-    } else {  // WGRAD: vector along rows (m = out channel for A, ng = (r,s,c) for B)
-      if (kk >= a.Kd) return nullptr;
-      const int q = kk % d.Q; const int np = kk / d.Q; const int p = np % d.P; const int n = np / d.P;
-      if constexpr (IS_A) {
-        if (row >= a.M) return nullptr;
-        return (const T*)a.a_src + off4(a.as, n, row, p, q);
-      } else {
-        if (row >= a.Ng) return nullptr;
-        const int c = row % d.C; const int rs = row / d.C; const int s = rs % d.S; const int r = rs / d.S;
-        const int hu = p * d.stride - d.pad + r, wu = q * d.stride - d.pad + s;
-        if (hu < 0 || hu >= d.Hu || wu < 0 || wu >= d.Wu) return nullptr;
-        return (const T*)a.b_src + off4(a.bs, n, c, src_row(d.hmap, hu), src_row(d.wmap, wu));
+    } else {
+#pragma unroll
+      for (int i = 0; i < PER_THREAD; ++i) {
+        const int idx = threadIdx.x + i * NTHREADS;
+        const int kk = k0 + idx / (BROWS / VN);                 // pixel (n, p, q)
+        const T* p = nullptr;
+        if (kk < a.Kd && boff[i] >= 0) {
+          const int np = fdiv(kk, a.fQ), q = kk - np * d.Q;
+          const int n = fdiv(np, a.fP), pp = np - n * d.P;
+          if constexpr (IS_A) {
+            p = src + boff[i] + (int64_t)n * a.as[0] + (int64_t)pp * a.as[2] + (int64_t)q * a.as[3];
+          } else {
+            const int hu = pp * d.stride + c0_[i], wu = q * d.stride + c1_[i];
+            if (hu >= 0 && hu < d.Hu && wu >= 0 && wu < d.Wu)
+              p = src + boff[i] + (int64_t)n * a.bs[0] + (int64_t)src_row(d.hmap, hu) * a.bs[2] +
+                  (int64_t)src_row(d.wmap, wu) * a.bs[3];
+          }
+        }
+        reg[i] = p ? *(const V*)p : V{};
       }
     }
   }
@@ -338,6 +416,8 @@ __global__ void __launch_bounds__(NTHREADS) conv_igemm_kernel(ConvArgs a) {
 
   Stager<T, MODE, BM, true, AVEC> sa;
   Stager<T, MODE, BN, false, BVEC> sb;
+  sa.init(a, m0);
+  sb.init(a, n0);
   sa.load(a, m0, kbeg);
   sb.load(a, n0, kbeg);
   sa.store(smem);
@@ -375,10 +455,12 @@ __global__ void __launch_bounds__(NTHREADS) conv_igemm_kernel(ConvArgs a) {
       if (m >= a.M) continue;
       int64_t rowoff = 0;
       if constexpr (MODE == MODE_FWD) {
-        const int q = m % d.Q; const int np = m / d.Q; const int p = np % d.P; const int n = np / d.P;
+        const int np = fdiv(m, a.fQ), q = m - np * d.Q;
+        const int n = fdiv(np, a.fP), p = np - n * d.P;
         rowoff = n * a.os[0] + p * a.os[2] + q * a.os[3];
       } else if constexpr (MODE == MODE_DGRAD) {
-        const int wu = m % d.Wu; const int nh = m / d.Wu; const int hu = nh % d.Hu; const int n = nh / d.Hu;
+        const int nh = fdiv(m, a.fWu), wu = m - nh * d.Wu;
+        const int n = fdiv(nh, a.fHu), hu = nh - n * d.Hu;
         rowoff = n * a.os[0] + hu * a.os[2] + wu * a.os[3];
       }
 #pragma unroll
@@ -448,6 +530,9 @@ int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
 
 template <int MODE>
 int dispatch(ConvArgs& a, es_dtype_t dt, bool avec, bool bvec, hipStream_t st) {
+  a.fC = mkdiv(a.d.C); a.fS = mkdiv(a.d.S); a.fK = mkdiv(a.d.K); a.fQ = mkdiv(a.d.Q);
+  a.fP = mkdiv(a.d.P); a.fWu = mkdiv(a.d.Wu); a.fHu = mkdiv(a.d.Hu);
+  if (a.d.stride > 2) avec = bvec = false;   // vector DGRAD gather handles strides 1 and 2
   if (dt == ES_F32) return launch<float, MODE>(a, avec, bvec, st);
   if (dt == ES_BF16) return launch<bf16, MODE>(a, avec, bvec, st);
   es_set_error("conv: unsupported dtype %d", (int)dt);
