@@ -68,7 +68,8 @@ __device__ __forceinline__ int fdiv(int x, FastDiv f) {
 }
 
 struct ConvArgs {
-  FastDiv fC, fS, fK, fQ, fP, fWu, fHu;
+  FastDiv fC, fS, fK, fQ, fP, fWu, fHu, fUh, fUw, fRSK, fW, fH;
+  int fold;            // DGRAD with integer upsample folded (rows on the source grid)
   es_conv_desc_t d;
   const void* a_src;
   const void* b_src;
@@ -83,11 +84,20 @@ struct ConvArgs {
   int k_per_split;
 };
 
+__device__ __forceinline__ int src_row(const int32_t* map, int u) { return map ? map[u] : u; }
+// nearest-upsample source index of upsampled row / column u
+__device__ __forceinline__ int src_h(const ConvArgs& a, int u) {
+  return a.d.up_h > 0 ? fdiv(u, a.fUh) : src_row(a.d.hmap, u);
+}
+__device__ __forceinline__ int src_w(const ConvArgs& a, int u) {
+  return a.d.up_w > 0 ? fdiv(u, a.fUw) : src_row(a.d.wmap, u);
+}
+
 template <typename T> struct Vec16;
 template <> struct Vec16<float> { typedef float4 type; static constexpr int N = 4; };
 template <> struct Vec16<bf16> { typedef uint4 type; static constexpr int N = 8; };
 
-__device__ __forceinline__ int src_row(const int32_t* map, int u) { return map ? map[u] : u; }
+
 
 // ---------------------------------------------------------------------------------------------
 // Element gathers (scalar); used by the generic path and by the vector path for the base address
@@ -102,10 +112,19 @@ __device__ __forceinline__ float gather_a(const ConvArgs& a, int m, int kk) {
     const int q = m % d.Q; const int np = m / d.Q; const int p = np % d.P; const int n = np / d.P;
     const int hu = p * d.stride - d.pad + r, wu = q * d.stride - d.pad + s;
     if (hu < 0 || hu >= d.Hu || wu < 0 || wu >= d.Wu) return 0.f;
-    return to_f(src[off4(a.as, n, c, src_row(d.hmap, hu), src_row(d.wmap, wu))]);
+    return to_f(src[off4(a.as, n, c, src_h(a, hu), src_w(a, wu))]);
   } else if constexpr (MODE == MODE_DGRAD) {
-    const int k = kk % d.K; const int rs = kk / d.K; const int s = rs % d.S; const int r = rs / d.S;
-    const int wu = m % d.Wu; const int nh = m / d.Wu; const int hu = nh % d.Hu; const int n = nh / d.Hu;
+    int kr = kk, hu, wu, n;
+    if (a.fold) {   // rows on the source grid, kk = (a, b, r, s, k)
+      const int ab = kk / (d.R * d.S * d.K);
+      kr = kk - ab * (d.R * d.S * d.K);
+      const int ua = ab / d.up_w, ub = ab - ua * d.up_w;
+      const int j = m % d.W; const int nh = m / d.W; const int i = nh % d.H; n = nh / d.H;
+      hu = i * d.up_h + ua; wu = j * d.up_w + ub;
+    } else {
+      wu = m % d.Wu; const int nh = m / d.Wu; hu = nh % d.Hu; n = nh / d.Hu;
+    }
+    const int k = kr % d.K; const int rs = kr / d.K; const int s = rs % d.S; const int r = rs / d.S;
     const int ph = hu + d.pad - r, pw = wu + d.pad - s;
     if (ph < 0 || pw < 0 || ph % d.stride || pw % d.stride) return 0.f;
     const int p = ph / d.stride, q = pw / d.stride;
@@ -122,14 +141,17 @@ __device__ __forceinline__ float gather_b(const ConvArgs& a, int ng, int kk) {
   const es_conv_desc_t& d = a.d;
   const T* src = (const T*)a.b_src;
   if (ng >= a.Ng || kk >= a.Kd) return 0.f;
-  if constexpr (MODE == MODE_FWD || MODE == MODE_DGRAD) {
+  if constexpr (MODE == MODE_FWD) {
     return to_f(src[(int64_t)ng * a.Kd + kk]);
+  } else if constexpr (MODE == MODE_DGRAD) {
+    const int rsk = d.R * d.S * d.K;
+    return to_f(src[(int64_t)ng * rsk + (a.fold ? kk % rsk : kk)]);
   } else {  // WGRAD: B[ng=(r,s,c)][kk=pix] = xu
     const int c = ng % d.C; const int rs = ng / d.C; const int s = rs % d.S; const int r = rs / d.S;
     const int q = kk % d.Q; const int np = kk / d.Q; const int p = np % d.P; const int n = np / d.P;
     const int hu = p * d.stride - d.pad + r, wu = q * d.stride - d.pad + s;
     if (hu < 0 || hu >= d.Hu || wu < 0 || wu >= d.Wu) return 0.f;
-    return to_f(src[off4(a.bs, n, c, src_row(d.hmap, hu), src_row(d.wmap, wu))]);
+    return to_f(src[off4(a.bs, n, c, src_h(a, hu), src_w(a, wu))]);
   }
 }
 
@@ -170,6 +192,12 @@ struct Stager {
             boff[i] = row < a.M ? (int64_t)n * a.as[0] : -1;
             c0_[i] = p * d.stride - d.pad;
             c1_[i] = q * d.stride - d.pad;
+          } else if (a.fold) {                      // DGRAD, folded upsample: row = (n, i, j) source grid
+            const int nh = fdiv(rr, a.fW), j = rr - nh * d.W;
+            const int n = fdiv(nh, a.fH), ii = nh - n * d.H;
+            boff[i] = row < a.M ? (int64_t)n * a.as[0] : -1;
+            c0_[i] = ii * d.up_h + d.pad;
+            c1_[i] = j * d.up_w + d.pad;
           } else {                                  // DGRAD: row = (n, hu, wu)
             const int nh = fdiv(rr, a.fWu), wu = rr - nh * d.Wu;
             const int n = fdiv(nh, a.fHu), hu = nh - n * d.Hu;
@@ -178,7 +206,8 @@ struct Stager {
             c1_[i] = wu + d.pad;
           }
         } else {
-          boff[i] = row < a.Ng ? (int64_t)row * a.Kd : -1;
+          const int ldb = (MODE == MODE_DGRAD && a.fold) ? d.R * d.S * d.K : a.Kd;
+          boff[i] = row < a.Ng ? (int64_t)row * ldb : -1;
           c0_[i] = c1_[i] = 0;
         }
       } else {
@@ -241,7 +270,13 @@ struct Stager {
         // kk -> (r, s, ch): ch = input channel (FWD) / output channel (DGRAD), fastest
         const FastDiv fch = MODE == MODE_FWD ? a.fC : a.fK;
         const int nch = MODE == MODE_FWD ? d.C : d.K;
-        const int rs = fdiv(kk, fch), ch = kk - rs * nch;
+        int kr = kk, ua = 0, ub = 0;
+        if (MODE == MODE_DGRAD && a.fold) {        // kk = (phase a, phase b, r, s, k)
+          const int ab = fdiv(kk, a.fRSK);
+          kr = kk - ab * (d.R * d.S * d.K);
+          ua = fdiv(ab, a.fUw); ub = ab - ua * d.up_w;
+        }
+        const int rs = fdiv(kr, fch), ch = kr - rs * nch;
         const int r = fdiv(rs, a.fS), s_ = rs - r * d.S;
 #pragma unroll
         for (int i = 0; i < PER_THREAD; ++i) {
@@ -250,10 +285,10 @@ struct Stager {
             if constexpr (MODE == MODE_FWD) {
               const int hu = c0_[i] + r, wu = c1_[i] + s_;
               if (hu >= 0 && hu < d.Hu && wu >= 0 && wu < d.Wu)
-                p = src + boff[i] + (int64_t)ch * a.as[1] + (int64_t)src_row(d.hmap, hu) * a.as[2] +
-                    (int64_t)src_row(d.wmap, wu) * a.as[3];
+                p = src + boff[i] + (int64_t)ch * a.as[1] + (int64_t)src_h(a, hu) * a.as[2] +
+                    (int64_t)src_w(a, wu) * a.as[3];
             } else {
-              int ph = c0_[i] - r, pw = c1_[i] - s_;
+              int ph = c0_[i] + ua - r, pw = c1_[i] + ub - s_;
               bool ok = ph >= 0 && pw >= 0;
               if (d.stride == 2) { ok = ok && !(ph & 1) && !(pw & 1); ph >>= 1; pw >>= 1; }
               if (ok && ph < d.P && pw < d.Q)
@@ -263,9 +298,11 @@ struct Stager {
           reg[i] = p ? *(const V*)p : V{};
         }
       } else {
+        int kb = kk;
+        if (MODE == MODE_DGRAD && a.fold) kb = kk - fdiv(kk, a.fRSK) * (d.R * d.S * d.K);
 #pragma unroll
         for (int i = 0; i < PER_THREAD; ++i)
-          reg[i] = (kin && boff[i] >= 0) ? *(const V*)(src + boff[i] + kk) : V{};
+          reg[i] = (kin && boff[i] >= 0) ? *(const V*)(src + boff[i] + kb) : V{};
       }
     } else {
 #pragma unroll
@@ -281,8 +318,8 @@ struct Stager {
           } else {
             const int hu = pp * d.stride + c0_[i], wu = q * d.stride + c1_[i];
             if (hu >= 0 && hu < d.Hu && wu >= 0 && wu < d.Wu)
-              p = src + boff[i] + (int64_t)n * a.bs[0] + (int64_t)src_row(d.hmap, hu) * a.bs[2] +
-                  (int64_t)src_row(d.wmap, wu) * a.bs[3];
+              p = src + boff[i] + (int64_t)n * a.bs[0] + (int64_t)src_h(a, hu) * a.bs[2] +
+                  (int64_t)src_w(a, wu) * a.bs[3];
           }
         }
         reg[i] = p ? *(const V*)p : V{};
@@ -459,9 +496,15 @@ __global__ void __launch_bounds__(NTHREADS) conv_igemm_kernel(ConvArgs a) {
         const int n = fdiv(np, a.fP), p = np - n * d.P;
         rowoff = n * a.os[0] + p * a.os[2] + q * a.os[3];
       } else if constexpr (MODE == MODE_DGRAD) {
-        const int nh = fdiv(m, a.fWu), wu = m - nh * d.Wu;
-        const int n = fdiv(nh, a.fHu), hu = nh - n * d.Hu;
-        rowoff = n * a.os[0] + hu * a.os[2] + wu * a.os[3];
+        if (a.fold) {
+          const int nh = fdiv(m, a.fW), j = m - nh * d.W;
+          const int n = fdiv(nh, a.fH), ii = nh - n * d.H;
+          rowoff = n * a.os[0] + ii * a.os[2] + j * a.os[3];
+        } else {
+          const int nh = fdiv(m, a.fWu), wu = m - nh * d.Wu;
+          const int n = fdiv(nh, a.fHu), hu = nh - n * d.Hu;
+          rowoff = n * a.os[0] + hu * a.os[2] + wu * a.os[3];
+        }
       }
 #pragma unroll
       for (int j = 0; j < RN; ++j) {
@@ -532,6 +575,8 @@ template <int MODE>
 int dispatch(ConvArgs& a, es_dtype_t dt, bool avec, bool bvec, hipStream_t st) {
   a.fC = mkdiv(a.d.C); a.fS = mkdiv(a.d.S); a.fK = mkdiv(a.d.K); a.fQ = mkdiv(a.d.Q);
   a.fP = mkdiv(a.d.P); a.fWu = mkdiv(a.d.Wu); a.fHu = mkdiv(a.d.Hu);
+  a.fUh = mkdiv(a.d.up_h > 0 ? a.d.up_h : 1); a.fUw = mkdiv(a.d.up_w > 0 ? a.d.up_w : 1);
+  a.fRSK = mkdiv(a.d.R * a.d.S * a.d.K); a.fW = mkdiv(a.d.W); a.fH = mkdiv(a.d.H);
   if (a.d.stride > 2) avec = bvec = false;   // vector DGRAD gather handles strides 1 and 2
   if (dt == ES_F32) return launch<float, MODE>(a, avec, bvec, st);
   if (dt == ES_BF16) return launch<bf16, MODE>(a, avec, bvec, st);
@@ -547,7 +592,10 @@ int check_desc(const es_conv_desc_t* d) {
                "conv: output size %dx%d inconsistent with input %dx%d k%dx%d s%d p%d", d->P, d->Q,
                d->Hu, d->Wu, d->R, d->S, d->stride, d->pad);
   ES_CHECK_ARG((d->hmap == nullptr) == (d->wmap == nullptr), "conv: hmap/wmap must both be set");
-  ES_CHECK_ARG(d->hmap || (d->Hu == d->H && d->Wu == d->W), "conv: Hu/Wu != H/W without maps");
+  ES_CHECK_ARG((d->up_h > 0) == (d->up_w > 0), "conv: up_h/up_w must both be set");
+  ES_CHECK_ARG(d->up_h <= 0 || (d->Hu == d->H * d->up_h && d->Wu == d->W * d->up_w),
+               "conv: Hu/Wu must equal H*up_h / W*up_w");
+  ES_CHECK_ARG(d->hmap || d->up_h > 0 || (d->Hu == d->H && d->Wu == d->W), "conv: Hu/Wu != H/W without maps");
   const int64_t M1 = (int64_t)d->N * d->P * d->Q, M2 = (int64_t)d->N * d->Hu * d->Wu;
   ES_CHECK_ARG(M1 < (1ll << 31) && M2 < (1ll << 31), "conv: problem too large for int32 rows");
   return ES_OK;
@@ -578,7 +626,10 @@ extern "C" int es_conv2d_dgrad(const es_conv_desc_t* d, es_dtype_t dt, const voi
   a.d = *d; a.a_src = dy; a.b_src = wd; a.out = dxu; a.bias = nullptr; a.beta = beta;
   a.out_bf16 = dxdt == ES_BF16;
   for (int i = 0; i < 4; ++i) { a.as[i] = ys[i]; a.os[i] = dxs[i]; }
-  a.M = d->N * d->Hu * d->Wu; a.Ng = d->C; a.Kd = d->R * d->S * d->K;
+  a.fold = d->up_h > 0;
+  if (a.fold) { a.M = d->N * d->H * d->W; a.Kd = d->up_h * d->up_w * d->R * d->S * d->K; }
+  else { a.M = d->N * d->Hu * d->Wu; a.Kd = d->R * d->S * d->K; }
+  a.Ng = d->C;
   const int vn = dt == ES_BF16 ? 8 : 4;
   const bool avec = ys[1] == 1 && d->K % vn == 0;
   const bool bvec = a.Kd % vn == 0;

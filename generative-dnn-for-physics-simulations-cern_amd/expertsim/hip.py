@@ -33,7 +33,7 @@ class ConvDesc(C.Structure):
     _fields_ = [("N", C.c_int), ("C", C.c_int), ("H", C.c_int), ("W", C.c_int), ("Hu", C.c_int),
                 ("Wu", C.c_int), ("K", C.c_int), ("P", C.c_int), ("Q", C.c_int), ("R", C.c_int),
                 ("S", C.c_int), ("stride", C.c_int), ("pad", C.c_int), ("hmap", C.c_void_p),
-                ("wmap", C.c_void_p)]
+                ("wmap", C.c_void_p), ("up_h", C.c_int), ("up_w", C.c_int)]
 
 
 class Norm(C.Structure):

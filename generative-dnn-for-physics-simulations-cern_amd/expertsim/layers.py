@@ -154,6 +154,10 @@ class Upsample:
 
     def __init__(self, in_hw, out_hw=None, scale=None):
         self.in_hw = tuple(in_hw)
+        # exact integer factors (x2 of the generators) are handled arithmetically in the kernels
+        self.factor = None
+        if scale is not None and all(float(f).is_integer() for f in scale):
+            self.factor = (int(scale[0]), int(scale[1]))
         if out_hw is None:
             out_hw = (int(math.floor(in_hw[0] * scale[0])), int(math.floor(in_hw[1] * scale[1])))
         self.out_hw = tuple(out_hw)
@@ -234,10 +238,16 @@ class ConvOp:
             assert (H, W) == self.up.in_hw, ((H, W), self.up.in_hw)
             d.Hu, d.Wu = self.up.out_hw
             maps = self.up.device_maps(x.t.device)
-            d.hmap, d.wmap = maps[0].data_ptr(), maps[1].data_ptr()
+            if self.up.factor is not None:
+                d.hmap = d.wmap = None
+                d.up_h, d.up_w = self.up.factor
+            else:
+                d.hmap, d.wmap = maps[0].data_ptr(), maps[1].data_ptr()
+                d.up_h = d.up_w = 0
         else:
             d.Hu, d.Wu = H, W
             d.hmap = d.wmap = None
+            d.up_h = d.up_w = 0
         d.K, d.R, d.S, d.stride, d.pad = self.K, self.R, self.S, self.stride, self.pad
         d.P = (d.Hu + 2 * self.pad - self.R) // self.stride + 1
         d.Q = (d.Wu + 2 * self.pad - self.S) // self.stride + 1
@@ -262,7 +272,7 @@ class ConvOp:
         wd = self.packed(cdt, 1, inv_scale)
         N, Cc, H, W = x.dims
         ddt = dx_dtype or cdt
-        if self.up is None:
+        if self.up is None or self.up.factor is not None:   # no upsample, or folded in the GEMM
             if dx is None:
                 dx = Act.nhwc(N, Cc, H, W, ddt, dy.t.device)
             with _probed(self.label and self.label + ".dgrad"):

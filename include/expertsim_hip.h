@@ -69,6 +69,9 @@ typedef struct {
   int stride, pad;
   const int32_t* hmap; /* device [Hu]: source row of upsampled row (torch nearest), or NULL  */
   const int32_t* wmap; /* device [Wu]                                                        */
+  int up_h, up_w;      /* integer nearest-upsample factors (Hu = H*up_h), or 0 to use the maps.
+                          With factors set, es_conv2d_dgrad folds the upsample backward: it
+                          writes dx on the SOURCE grid (H x W) with dxs strides.               */
 } es_conv_desc_t;
 
 /* y[n,k,p,q] = bias[k] + sum_{c,r,s} xu[n,c,p*stride-pad+r,q*stride-pad+s] * W[k,c,r,s]
@@ -77,7 +80,9 @@ int es_conv2d_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x, const i
                   const void* wk, const float* bias, void* y, es_dtype_t ydt, const int64_t ys[4],
                   es_stream_t stream);
 /* dxu[n,c,hu,wu] = sum_{k,r,s} dy[n,k,p,q] * W[k,c,r,s] over (hu+pad-r) = p*stride, ...
- * (gradient w.r.t. the UPSAMPLED input; es_upsample_bwd folds it to the source grid).
+ * (gradient w.r.t. the UPSAMPLED input; es_upsample_bwd folds it to the source grid).  With
+ * integer factors d->up_h/up_w the fold happens inside the GEMM (K grows by up_h*up_w) and the
+ * output is dx on the source grid.
  * wd: packed weights [C][R][S][K] (es_pack_conv_weight, mode 1).  beta=1 accumulates into dxu. */
 int es_conv2d_dgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, const int64_t ys[4],
                     const void* wd, void* dxu, es_dtype_t dxdt, const int64_t dxs[4], float beta,
