@@ -22,11 +22,25 @@
 //   fp32 : v_mfma_f32_16x16x4_f32 x4, lane l reads A[l&15][4*(l>>4)+0..3] once and feeds the
 //          four MFMAs with k = 4*(l>>4)+t (A and B use the same permutation of k, so the sum over
 //          k is unchanged; each MFMA is an exact fp32 FMA chain).
+#include <cstdlib>
+
 #include "common.h"
+
+// direct kernels for one-input-channel / one-output-channel convolutions (conv_thin.hip)
+int es_thin_conv_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x, const int64_t xs[4], const void* wk,
+                     const float* bias, void* y, es_dtype_t ydt, const int64_t ys[4], hipStream_t st);
+int es_thin_conv_dgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, const int64_t ys[4],
+                       const void* wd, void* dx, es_dtype_t dxdt, const int64_t dxs[4], float beta,
+                       hipStream_t st);
+int es_thin_conv_wgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, const int64_t ys[4], const void* x,
+                       const int64_t xs[4], float* dw, hipStream_t st);
 
 namespace {
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
+
+// ES_NO_GLDS=1 (or es_conv_set_glds(0)) forces the register-staged kernels (A/B measurement)
+bool g_no_glds = [] { const char* e = getenv("ES_NO_GLDS"); return e && e[0] == '1'; }();
 
 constexpr int KSTEP_BYTES = 128;               // operand bytes per row per K-step
 constexpr int ROW_BYTES = KSTEP_BYTES + 16;    // padded LDS row
@@ -82,6 +96,8 @@ struct ConvArgs {
   int out_bf16;
   int M, Ng, Kd;
   int k_per_split;
+  int dense_f32_out;   // host: output is fp32, dense [M][Ng] and beta == 0 (split-K allowed)
+  int splitk;          // FWD / DGRAD split over blockIdx.z: fp32 atomics into a zeroed dense output
 };
 
 __device__ __forceinline__ int src_row(const int32_t* map, int u) { return map ? map[u] : u; }
@@ -426,6 +442,66 @@ __device__ __forceinline__ void mma_kstep_tr(const char* As, const char* Bs, int
   }
 }
 
+// Epilogue shared by the GEMM kernels: row -> output offset, bias (FWD, split 0), beta, dtype,
+// fp32 atomics for WGRAD and split-K.
+template <typename T, int MODE, int BM, int BN>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const f32x4 (&acc)[BM / 32][BN / 32], int m0,
+                                              int n0, int wm0, int wn0) {
+  constexpr int RM = BM / 32, RN = BN / 32;
+  const int lane = threadIdx.x & 63;
+  const int col16 = lane & 15, rq = (lane >> 4) * 4;
+  const es_conv_desc_t& d = a.d;
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int m = m0 + wm0 + i * 16 + rq + jj;
+      if (m >= a.M) continue;
+      int64_t rowoff = 0;
+      if constexpr (MODE == MODE_FWD) {
+        const int np = fdiv(m, a.fQ), q = m - np * d.Q;
+        const int n = fdiv(np, a.fP), p = np - n * d.P;
+        rowoff = n * a.os[0] + p * a.os[2] + q * a.os[3];
+      } else if constexpr (MODE == MODE_DGRAD) {
+        if (a.fold) {
+          const int nh = fdiv(m, a.fW), j = m - nh * d.W;
+          const int n = fdiv(nh, a.fH), ii = nh - n * d.H;
+          rowoff = n * a.os[0] + ii * a.os[2] + j * a.os[3];
+        } else {
+          const int nh = fdiv(m, a.fWu), wu = m - nh * d.Wu;
+          const int n = fdiv(nh, a.fHu), hu = nh - n * d.Hu;
+          rowoff = n * a.os[0] + hu * a.os[2] + wu * a.os[3];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int ng = n0 + wn0 + j * 16 + col16;
+        if (ng >= a.Ng) continue;
+        float v = acc[i][j][jj];
+        if constexpr (MODE == MODE_WGRAD) {
+          atomicAdd((float*)a.out + (int64_t)m * a.Ng + ng, v);
+        } else {
+          if constexpr (MODE == MODE_FWD) {
+            if (a.bias && blockIdx.z == 0) v += a.bias[ng];
+          }
+          const int64_t o = rowoff + (int64_t)ng * a.os[1];
+          if (a.splitk) {
+            atomicAdd((float*)a.out + o, v);
+          } else if (a.out_bf16) {
+            bf16* y = (bf16*)a.out + o;
+            if (a.beta != 0.f) v += a.beta * (float)(*y);
+            *y = (bf16)v;
+          } else {
+            float* y = (float*)a.out + o;
+            if (a.beta != 0.f) v += a.beta * (*y);
+            *y = v;
+          }
+        }
+      }
+    }
+  }
+}
+
 template <typename T, int MODE, int BM, int BN, bool AVEC, bool BVEC>
 __global__ void __launch_bounds__(NTHREADS) conv_igemm_kernel(ConvArgs a) {
   constexpr int BK = KSTEP_BYTES / sizeof(T);
@@ -436,12 +512,9 @@ __global__ void __launch_bounds__(NTHREADS) conv_igemm_kernel(ConvArgs a) {
   constexpr int BUF = LA::BYTES + LB::BYTES;   // one stage: A image then B image
 
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  int kbeg = 0, kend = a.Kd;
-  if constexpr (MODE == MODE_WGRAD) {
-    kbeg = blockIdx.z * a.k_per_split;
-    kend = min(a.Kd, kbeg + a.k_per_split);
-    if (kbeg >= kend) return;
-  }
+  const int kbeg = blockIdx.z * a.k_per_split;
+  const int kend = min(a.Kd, kbeg + a.k_per_split);
+  if (kbeg >= kend) return;
   const int wid = threadIdx.x >> 6;
   const int wm0 = (wid >> 1) * (BM / 2), wn0 = (wid & 1) * (BN / 2);
 
@@ -480,57 +553,179 @@ __global__ void __launch_bounds__(NTHREADS) conv_igemm_kernel(ConvArgs a) {
   }
   (void)BK;
 
-  // ---------------------------------------------------------------- epilogue
+  conv_epilogue<T, MODE, BM, BN>(a, acc, m0, n0, wm0, wn0);
+}
+
+// ---------------------------------------------------------------------------------------------
+// bf16 FWD / DGRAD with LDS-DMA staging (global_load_lds_dwordx4).
+//
+// Used when every K-step (64 bf16) is ONE filter tap over 64 contiguous channels (C % 64 == 0 for
+// FWD, K % 64 == 0 for DGRAD), so each GEMM row of a K-step is one contiguous 128-byte segment of
+// an NHWC activation row (or all zero: padding / outside the image / stride-2 holes).
+//   * A wave instruction moves 8 rows x 128 B straight into LDS (no register round trip); lanes
+//     of padded rows read a 16-byte-aligned zero block instead.
+//   * LDS image per operand: [rows][128 B] unpadded; logical 16-byte chunk lc of row r sits at
+//     physical chunk lc ^ ((r >> 1) & 7) (the swizzle is applied on the global source address,
+//     since the DMA destination is lane-linear), which makes the 16-row ds_read_b128 fragment
+//     reads conflict-free.
+//   * Two stages; one barrier per K-step: wait(stage t) + barrier, issue stage t+1, MFMAs on t.
+//   * Block ids are remapped so that consecutive M tiles run on the same XCD (shared halo rows
+//     stay in that XCD's L2).
+// ---------------------------------------------------------------------------------------------
+__device__ __attribute__((aligned(16))) char g_zero_row[128];   // zero-initialised at load
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+template <int RM, int RN>
+__device__ __forceinline__ void mma_kstep_swz(const char* As, const char* Bs, int wm0, int wn0,
+                                              f32x4 (&acc)[RM][RN]) {
   const int lane = threadIdx.x & 63;
-  const int col16 = lane & 15, rq = (lane >> 4) * 4;
+  const int r16 = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int seg = kk * 4 + g;
+    bf16x8 af[RM], bfr[RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i) af[i] = *(const bf16x8*)(As + swz(wm0 + i * 16 + r16, seg));
+#pragma unroll
+    for (int j = 0; j < RN; ++j) bfr[j] = *(const bf16x8*)(Bs + swz(wn0 + j * 16 + r16, seg));
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  }
+}
+
+template <int MODE, int BM, int BN>
+__global__ void __launch_bounds__(NTHREADS) conv_glds_kernel(ConvArgs a) {
+  constexpr int RM = BM / 32, RN = BN / 32;
+  constexpr int AI = BM / 32, BI = BN / 32;            // 8-row DMA pieces per wave (4 waves)
+  constexpr int ABYTES = BM * 128, STAGE = (BM + BN) * 128;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
   const es_conv_desc_t& d = a.d;
+
+  // XCD-aware tile order: consecutive tile ids on one XCD (bijective remap)
+  const int mt = (a.M + BM - 1) / BM;
+  const int nwg = mt * gridDim.y;
+  const int orig = blockIdx.x + blockIdx.y * gridDim.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int m0 = (wgid % mt) * BM, n0 = (wgid / mt) * BN;
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm0 = (wid >> 1) * (BM / 2), wn0 = (wid & 1) * (BN / 2);
+  const int lrow = lane >> 3, pc = lane & 7;          // row within an 8-row piece, physical chunk
+
+  // per-lane rows of the A pieces: base offset (or -1) and two coordinates
+  int64_t aoff[AI];
+  int ac0[AI], ac1[AI], alc[AI];
 #pragma unroll
-  for (int i = 0; i < RM; ++i) {
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int m = m0 + wm0 + i * 16 + rq + jj;
-      if (m >= a.M) continue;
-      int64_t rowoff = 0;
-      if constexpr (MODE == MODE_FWD) {
-        const int np = fdiv(m, a.fQ), q = m - np * d.Q;
-        const int n = fdiv(np, a.fP), p = np - n * d.P;
-        rowoff = n * a.os[0] + p * a.os[2] + q * a.os[3];
-      } else if constexpr (MODE == MODE_DGRAD) {
-        if (a.fold) {
-          const int nh = fdiv(m, a.fW), j = m - nh * d.W;
-          const int n = fdiv(nh, a.fH), ii = nh - n * d.H;
-          rowoff = n * a.os[0] + ii * a.os[2] + j * a.os[3];
-        } else {
-          const int nh = fdiv(m, a.fWu), wu = m - nh * d.Wu;
-          const int n = fdiv(nh, a.fHu), hu = nh - n * d.Hu;
-          rowoff = n * a.os[0] + hu * a.os[2] + wu * a.os[3];
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < RN; ++j) {
-        const int ng = n0 + wn0 + j * 16 + col16;
-        if (ng >= a.Ng) continue;
-        float v = acc[i][j][jj];
-        if constexpr (MODE == MODE_WGRAD) {
-          atomicAdd((float*)a.out + (int64_t)m * a.Ng + ng, v);
-        } else {
-          if constexpr (MODE == MODE_FWD) {
-            if (a.bias) v += a.bias[ng];
-          }
-          const int64_t o = rowoff + (int64_t)ng * a.os[1];
-          if (a.out_bf16) {
-            bf16* y = (bf16*)a.out + o;
-            if (a.beta != 0.f) v += a.beta * (float)(*y);
-            *y = (bf16)v;
-          } else {
-            float* y = (float*)a.out + o;
-            if (a.beta != 0.f) v += a.beta * (*y);
-            *y = v;
-          }
-        }
-      }
+  for (int j = 0; j < AI; ++j) {
+    const int rr = (wid * AI + j) * 8 + lrow;
+    const int row = m0 + rr;
+    alc[j] = pc ^ ((rr >> 1) & 7);
+    const int rw = row < a.M ? row : 0;
+    if constexpr (MODE == MODE_FWD) {
+      const int np = fdiv(rw, a.fQ), q = rw - np * d.Q;
+      const int n = fdiv(np, a.fP), p = np - n * d.P;
+      aoff[j] = row < a.M ? (int64_t)n * a.as[0] + alc[j] * 8 : -1;
+      ac0[j] = p * d.stride - d.pad;
+      ac1[j] = q * d.stride - d.pad;
+    } else if (a.fold) {
+      const int nh = fdiv(rw, a.fW), jj = rw - nh * d.W;
+      const int n = fdiv(nh, a.fH), ii = nh - n * d.H;
+      aoff[j] = row < a.M ? (int64_t)n * a.as[0] + alc[j] * 8 : -1;
+      ac0[j] = ii * d.up_h + d.pad;
+      ac1[j] = jj * d.up_w + d.pad;
+    } else {
+      const int nh = fdiv(rw, a.fWu), wu = rw - nh * d.Wu;
+      const int n = fdiv(nh, a.fHu), hu = nh - n * d.Hu;
+      aoff[j] = row < a.M ? (int64_t)n * a.as[0] + alc[j] * 8 : -1;
+      ac0[j] = hu + d.pad;
+      ac1[j] = wu + d.pad;
     }
   }
+  const int ldb = (MODE == MODE_DGRAD && a.fold) ? d.R * d.S * d.K : a.Kd;
+  int64_t boff[BI];
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    const int rr = (wid * BI + j) * 8 + lrow;
+    const int row = n0 + rr;
+    boff[j] = row < a.Ng ? (int64_t)row * ldb + ((pc ^ ((rr >> 1) & 7)) * 8) : -1;
+  }
+  const bf16* asrc = (const bf16*)a.a_src;
+  const bf16* bsrc = (const bf16*)a.b_src;
+  const char* zero = g_zero_row;
+
+  auto issue = [&](int kk, char* stage) {
+    // K-step decode (uniform): tap (r, s), channel offset, upsample phase (folded DGRAD)
+    int r, s_, ch0, ua = 0, ub = 0, kb = kk;
+    if constexpr (MODE == MODE_FWD) {
+      const int rs = fdiv(kk, a.fC);
+      ch0 = kk - rs * d.C;
+      r = fdiv(rs, a.fS); s_ = rs - r * d.S;
+    } else {
+      int kr = kk;
+      if (a.fold) {
+        const int ab = fdiv(kk, a.fRSK);
+        kr = kk - ab * (d.R * d.S * d.K);
+        kb = kr;
+        ua = fdiv(ab, a.fUw); ub = ab - ua * d.up_w;
+      }
+      const int rs = fdiv(kr, a.fK);
+      ch0 = kr - rs * d.K;
+      r = fdiv(rs, a.fS); s_ = rs - r * d.S;
+    }
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+      const void* src = zero;
+      if (aoff[j] >= 0) {
+        if constexpr (MODE == MODE_FWD) {
+          const int hu = ac0[j] + r, wu = ac1[j] + s_;
+          if (hu >= 0 && hu < d.Hu && wu >= 0 && wu < d.Wu)
+            // integer upsample only on this path (no map loads: an ordinary load here would make
+            // the compiler drain the in-flight DMA with vmcnt(0))
+            src = asrc + aoff[j] + ch0 + (int64_t)(d.up_h > 0 ? fdiv(hu, a.fUh) : hu) * a.as[2] +
+                  (int64_t)(d.up_w > 0 ? fdiv(wu, a.fUw) : wu) * a.as[3];
+        } else {
+          int ph = ac0[j] + ua - r, pw = ac1[j] + ub - s_;
+          bool ok = ph >= 0 && pw >= 0;
+          if (d.stride == 2) { ok = ok && !(ph & 1) && !(pw & 1); ph >>= 1; pw >>= 1; }
+          if (ok && ph < d.P && pw < d.Q)
+            src = asrc + aoff[j] + ch0 + (int64_t)ph * a.as[2] + (int64_t)pw * a.as[3];
+        }
+      }
+      glds16(src, stage + (wid * AI + j) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+      const void* src = boff[j] >= 0 ? (const void*)(bsrc + boff[j] + kb) : (const void*)zero;
+      glds16(src, stage + ABYTES + (wid * BI + j) * 1024);
+    }
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = a.Kd / 64;
+  issue(0, smem);
+  for (int t = 0; t < nk; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();                                   // stage t landed; stage t-1 fully read
+    char* cur = smem + (t & 1) * STAGE;
+    if (t + 1 < nk) issue((t + 1) * 64, smem + ((t + 1) & 1) * STAGE);
+    mma_kstep_swz<RM, RN>(cur, cur + ABYTES, wm0, wn0, acc);
+  }
+  conv_epilogue<bf16, MODE, BM, BN>(a, acc, m0, n0, wm0, wn0);
 }
 
 template <typename T, int MODE, int BM, int BN>
@@ -549,23 +744,55 @@ int launch_tile(const ConvArgs& a, bool avec, bool bvec, hipStream_t st, int spl
   return ES_OK;
 }
 
+template <int MODE, int BM, int BN>
+int launch_glds(ConvArgs& a, hipStream_t st) {
+  const int mt = (a.M + BM - 1) / BM;
+  dim3 grid(mt, (a.Ng + BN - 1) / BN, 1);
+  a.k_per_split = a.Kd;
+  a.splitk = 0;
+  hipLaunchKernelGGL((conv_glds_kernel<MODE, BM, BN>), grid, dim3(NTHREADS), 2 * (BM + BN) * 128, st, a);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
 template <typename T, int MODE>
 int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
   constexpr int BK = KSTEP_BYTES / sizeof(T);
+  if constexpr (sizeof(T) == 2 && MODE != MODE_WGRAD) {
+    // LDS-DMA path: one tap x 64 channels per K-step, big enough to fill the chip without split-K
+    const int nch = MODE == MODE_FWD ? a.d.C : a.d.K;
+    if (avec && bvec && nch % 64 == 0 && a.d.stride <= 2 && a.d.hmap == nullptr && a.M >= 128 && !g_no_glds) {
+      if (a.Ng > 64) return launch_glds<MODE, 128, 128>(a, st);
+      return launch_glds<MODE, 128, 64>(a, st);
+    }
+  }
   // tile choice: 128x128 for big GEMMs, 64x64 when either side is small
   const bool big = a.M >= 128 && a.Ng >= 96;
   const int BM = big ? 128 : 64, BN = big ? 128 : 64;
   int splits = 1;
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.Ng + BN - 1) / BN);
+  const int ksteps = (a.Kd + BK - 1) / BK;
+  a.k_per_split = a.Kd;
+  a.splitk = 0;
   if (MODE == MODE_WGRAD) {
-    const int tiles = ((a.M + BM - 1) / BM) * ((a.Ng + BN - 1) / BN);
-    const int ksteps = (a.Kd + BK - 1) / BK;
     int want = (2048 + tiles - 1) / tiles;            // ~2048 workgroups
     want = max(1, min(want, ksteps / 4 > 0 ? ksteps / 4 : 1));  // >= 4 K-steps per split
     const int per = ((ksteps + want - 1) / want) * BK;
     a.k_per_split = per;
     splits = (a.Kd + per - 1) / per;
-  } else {
-    a.k_per_split = a.Kd;
+  } else if (a.dense_f32_out && tiles < 256 && ksteps >= 16) {
+    // few output tiles and a long K (the linears at batch 512): split K over ~512 workgroups
+    int want = min((512 + tiles - 1) / tiles, ksteps / 8);
+    if (want > 1) {
+      const int per = ((ksteps + want - 1) / want) * BK;
+      a.k_per_split = per;
+      splits = (a.Kd + per - 1) / per;
+      a.splitk = splits > 1;
+      if (a.splitk && hipMemsetAsync(a.out, 0, (size_t)a.M * a.Ng * sizeof(float), st) != hipSuccess) {
+        es_set_error("conv: split-K memset failed");
+        return ES_ERR_HIP;
+      }
+    }
   }
   if (big) return launch_tile<T, MODE, 128, 128>(a, avec, bvec, st, splits);
   return launch_tile<T, MODE, 64, 64>(a, avec, bvec, st, splits);
@@ -582,6 +809,11 @@ int dispatch(ConvArgs& a, es_dtype_t dt, bool avec, bool bvec, hipStream_t st) {
   if (dt == ES_BF16) return launch<bf16, MODE>(a, avec, bvec, st);
   es_set_error("conv: unsupported dtype %d", (int)dt);
   return ES_ERR_ARG;
+}
+
+// strides (n, c, h, w) describe a dense [n][h][w][c] tensor (rows of c contiguous values)
+bool dense_rows(const int64_t s[4], int c, int h, int w) {
+  return s[1] == 1 && (w == 1 || s[3] == c) && (h == 1 || s[2] == (int64_t)w * c) && s[0] == (int64_t)h * w * c;
 }
 
 int check_desc(const es_conv_desc_t* d) {
@@ -603,15 +835,26 @@ int check_desc(const es_conv_desc_t* d) {
 
 }  // namespace
 
+extern "C" int es_conv_set_glds(int on) {
+  const int old = !g_no_glds;
+  g_no_glds = !on;
+  return old;
+}
+
 extern "C" int es_conv2d_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x,
                              const int64_t xs[4], const void* wk, const float* bias, void* y,
                              es_dtype_t ydt, const int64_t ys[4], es_stream_t stream) {
   if (int e = check_desc(d)) return e;
+  if (es_thin_conv_fwd(d, dt, x, xs, wk, bias, y, ydt, ys, (hipStream_t)stream)) {
+    ES_CHECK_LAUNCH();
+    return ES_OK;
+  }
   ConvArgs a{};
   a.d = *d; a.a_src = x; a.b_src = wk; a.out = y; a.bias = bias; a.beta = 0.f;
   a.out_bf16 = ydt == ES_BF16;
   for (int i = 0; i < 4; ++i) { a.as[i] = xs[i]; a.os[i] = ys[i]; }
   a.M = d->N * d->P * d->Q; a.Ng = d->K; a.Kd = d->R * d->S * d->C;
+  a.dense_f32_out = ydt == ES_F32 && dense_rows(ys, d->K, d->P, d->Q);
   const int vn = dt == ES_BF16 ? 8 : 4;
   const bool avec = xs[1] == 1 && d->C % vn == 0;
   const bool bvec = a.Kd % vn == 0;
@@ -622,6 +865,10 @@ extern "C" int es_conv2d_dgrad(const es_conv_desc_t* d, es_dtype_t dt, const voi
                                const int64_t ys[4], const void* wd, void* dxu, es_dtype_t dxdt,
                                const int64_t dxs[4], float beta, es_stream_t stream) {
   if (int e = check_desc(d)) return e;
+  if (es_thin_conv_dgrad(d, dt, dy, ys, wd, dxu, dxdt, dxs, beta, (hipStream_t)stream)) {
+    ES_CHECK_LAUNCH();
+    return ES_OK;
+  }
   ConvArgs a{};
   a.d = *d; a.a_src = dy; a.b_src = wd; a.out = dxu; a.bias = nullptr; a.beta = beta;
   a.out_bf16 = dxdt == ES_BF16;
@@ -630,6 +877,10 @@ extern "C" int es_conv2d_dgrad(const es_conv_desc_t* d, es_dtype_t dt, const voi
   if (a.fold) { a.M = d->N * d->H * d->W; a.Kd = d->up_h * d->up_w * d->R * d->S * d->K; }
   else { a.M = d->N * d->Hu * d->Wu; a.Kd = d->R * d->S * d->K; }
   a.Ng = d->C;
+  {
+    const int64_t oh = a.fold ? d->H : d->Hu, ow = a.fold ? d->W : d->Wu;
+    a.dense_f32_out = dxdt == ES_F32 && beta == 0.f && dense_rows(dxs, d->C, (int)oh, (int)ow);
+  }
   const int vn = dt == ES_BF16 ? 8 : 4;
   const bool avec = ys[1] == 1 && d->K % vn == 0;
   const bool bvec = a.Kd % vn == 0;
@@ -640,6 +891,10 @@ extern "C" int es_conv2d_wgrad(const es_conv_desc_t* d, es_dtype_t dt, const voi
                                const int64_t ys[4], const void* x, const int64_t xs[4], float* dw,
                                es_stream_t stream) {
   if (int e = check_desc(d)) return e;
+  if (es_thin_conv_wgrad(d, dt, dy, ys, x, xs, dw, (hipStream_t)stream)) {
+    ES_CHECK_LAUNCH();
+    return ES_OK;
+  }
   ConvArgs a{};
   a.d = *d; a.a_src = dy; a.b_src = x; a.out = dw;
   for (int i = 0; i < 4; ++i) { a.as[i] = ys[i]; a.bs[i] = xs[i]; }

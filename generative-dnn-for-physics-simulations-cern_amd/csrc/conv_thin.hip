@@ -1,0 +1,451 @@
+// Direct (non-GEMM) convolutions for the layers with ONE input or ONE output channel.
+//
+// These layers have almost no arithmetic (<= 0.3 GFLOP per launch at B = 512) but move the largest
+// activations of the step, and as implicit GEMMs they waste >= 3/4 of every MFMA tile (N or K
+// collapses to 1), so they run here as HBM-bound direct kernels:
+//   Cin  == 1 : the discriminators' conv_layers.0 (neutron/discriminator.py:12, proton/
+//               discriminator.py:122; 1->32, 3x3) and the neutron aux regressor conv1
+//               (neutron/aux_reg.py:14; 1->32, 3x3)                       fwd / dgrad / wgrad
+//   Cout == 1 : the generators' last conv (neutron/generator.py:34, proton/generator.py:42;
+//               64->1, 2x2)                                               fwd / dgrad / wgrad
+// Same operands as the GEMM path (conv_igemm.hip): packed weights (fwd [K][R][S][C], dgrad
+// [C][R][S][K]) in the compute dtype, fp32 accumulation, wgrad accumulated into fp32 [K][R*S*C]
+// with atomics.  Stride 1 (Cin == 1 also stride 2), any zero padding, no upsample.
+#include <algorithm>
+
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+template <typename T> struct V16;
+template <> struct V16<float> { static constexpr int N = 4; };
+template <> struct V16<bf16> { static constexpr int N = 8; };
+
+// 8 consecutive elements <-> floats
+template <typename T> __device__ __forceinline__ void ld8(const T* p, float* f);
+template <> __device__ __forceinline__ void ld8<bf16>(const bf16* p, float* f) {
+  const bf16x8 v = *(const bf16x8*)p;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) f[k] = (float)v[k];
+}
+template <> __device__ __forceinline__ void ld8<float>(const float* p, float* f) {
+  const float4 a = ((const float4*)p)[0], b = ((const float4*)p)[1];
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+template <typename T> __device__ __forceinline__ void st8(T* p, const float* f);
+template <> __device__ __forceinline__ void st8<bf16>(bf16* p, const float* f) {
+  bf16x8 v;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = (bf16)f[k];
+  *(bf16x8*)p = v;
+}
+template <> __device__ __forceinline__ void st8<float>(float* p, const float* f) {
+  ((float4*)p)[0] = make_float4(f[0], f[1], f[2], f[3]);
+  ((float4*)p)[1] = make_float4(f[4], f[5], f[6], f[7]);
+}
+
+struct Thin {
+  es_conv_desc_t d;
+  const void* a; int64_t as[4];    // fwd: x;  dgrad / wgrad: dy
+  const void* b; int64_t bs[4];    // wgrad: x
+  const void* w;                   // packed weights (fwd / dgrad)
+  const float* bias;
+  void* out; int64_t os[4];        // fwd: y; dgrad: dx; wgrad: fp32 dw [K][R*S*C]
+  float beta;
+  int M;                           // output pixels (fwd, wgrad: N*P*Q; dgrad: N*H*W)
+};
+
+__device__ __forceinline__ void pix3(int m, int A, int B, int& n, int& i, int& j) {
+  j = m % B; const int t = m / B; i = t % A; n = t / A;
+}
+
+// ============================================================ Cin == 1
+// fwd: LP = K / VO lanes per output pixel, each producing VO consecutive channels (one 16-byte
+// store; a pixel's K outputs are one contiguous run written by consecutive lanes).
+template <typename T, typename TO, int RS>
+__global__ void __launch_bounds__(NT) c1_fwd(Thin t) {
+  constexpr int VO = 16 / sizeof(TO);
+  const es_conv_desc_t& d = t.d;
+  __shared__ float wf[64 * RS], bs[64];
+  for (int i = threadIdx.x; i < d.K * RS; i += NT) wf[i] = to_f(((const T*)t.w)[i]);
+  for (int i = threadIdx.x; i < d.K; i += NT) bs[i] = t.bias ? t.bias[i] : 0.f;
+  __syncthreads();
+  const int LP = d.K / VO, PPB = NT / LP;
+  const int m = blockIdx.x * PPB + threadIdx.x / LP, k0 = (threadIdx.x % LP) * VO;
+  if (m >= t.M) return;
+  int n, p, q;
+  pix3(m, d.P, d.Q, n, p, q);
+  const T* x = (const T*)t.a + n * t.as[0];
+  float xv[RS];
+#pragma unroll
+  for (int j = 0; j < RS; ++j) {
+    const int hu = p * d.stride - d.pad + j / d.S, wu = q * d.stride - d.pad + j % d.S;
+    xv[j] = (hu >= 0 && hu < d.H && wu >= 0 && wu < d.W) ? to_f(x[hu * t.as[2] + wu * t.as[3]]) : 0.f;
+  }
+  float o[8];
+#pragma unroll
+  for (int kk = 0; kk < VO; ++kk) {
+    float s = bs[k0 + kk];
+#pragma unroll
+    for (int j = 0; j < RS; ++j) s += xv[j] * wf[(k0 + kk) * RS + j];
+    o[kk] = s;
+  }
+  TO* y = (TO*)t.out + n * t.os[0] + p * t.os[2] + q * t.os[3] + k0;
+  if constexpr (VO == 8) st8<TO>(y, o);
+  else *(float4*)y = make_float4(o[0], o[1], o[2], o[3]);
+}
+
+// dgrad: LP = K / VN lanes per input pixel; lane l dots its 16-byte chunk of each tap's dy row
+// with the weights (coalesced row reads), then the LP partial sums are reduced by shuffles.
+template <typename T, typename TO, int RS>
+__global__ void __launch_bounds__(NT) c1_dgrad(Thin t) {
+  constexpr int VN = V16<T>::N;
+  const es_conv_desc_t& d = t.d;
+  __shared__ float wf[64 * RS];
+  for (int i = threadIdx.x; i < d.K * RS; i += NT) wf[i] = to_f(((const T*)t.w)[i]);
+  __syncthreads();
+  const int LP = d.K / VN, PPB = NT / LP;
+  const int m = blockIdx.x * PPB + threadIdx.x / LP, l = threadIdx.x % LP;
+  const bool live = m < t.M;
+  int n, h, w;
+  pix3(live ? m : 0, d.H, d.W, n, h, w);
+  const T* dy = (const T*)t.a + n * t.as[0] + l * VN;
+  float acc = 0.f;
+#pragma unroll
+  for (int j = 0; j < RS; ++j) {
+    int ph = h + d.pad - j / d.S, pw = w + d.pad - j % d.S;
+    if (!live || ph < 0 || pw < 0) continue;
+    if (d.stride == 2) {
+      if ((ph | pw) & 1) continue;
+      ph >>= 1; pw >>= 1;
+    }
+    if (ph >= d.P || pw >= d.Q) continue;
+    const T* row = dy + ph * t.as[2] + pw * t.as[3];
+    const float* wr = wf + j * d.K + l * VN;
+    if constexpr (VN == 8) {
+      float v[8];
+      ld8<T>(row, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc += v[e] * wr[e];
+    } else {
+      const float4 v = *(const float4*)row;
+      acc += v.x * wr[0] + v.y * wr[1] + v.z * wr[2] + v.w * wr[3];
+    }
+  }
+  for (int o = LP >> 1; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (live && l == 0) {
+    TO* o = (TO*)t.out + n * t.os[0] + h * t.os[2] + w * t.os[3];
+    if (t.beta != 0.f) acc += t.beta * to_f(*o);
+    *o = from_f<TO>(acc);
+  }
+}
+
+// wgrad: thread = (pixel lane, 8-channel group); acc[8][RS] over a strided pixel range, then a
+// shuffle + LDS reduction over the pixel lanes and one atomic per (k, tap) per block.
+template <typename T, int RS>
+__global__ void __launch_bounds__(NT) c1_wgrad(Thin t) {
+  const es_conv_desc_t& d = t.d;
+  const int KO = d.K / 8;                 // 1..8, power of two (host-checked)
+  const int ko = threadIdx.x % KO, pl = threadIdx.x / KO, PL = NT / KO;
+  float acc[8][RS];
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+    for (int j = 0; j < RS; ++j) acc[kk][j] = 0.f;
+  for (int m = blockIdx.x * PL + pl; m < t.M; m += gridDim.x * PL) {
+    int n, p, q;
+    pix3(m, d.P, d.Q, n, p, q);
+    float g[8];
+    ld8<T>((const T*)t.a + n * t.as[0] + p * t.as[2] + q * t.as[3] + ko * 8, g);
+    const T* x = (const T*)t.b + n * t.bs[0];
+#pragma unroll
+    for (int j = 0; j < RS; ++j) {
+      const int hu = p * d.stride - d.pad + j / d.S, wu = q * d.stride - d.pad + j % d.S;
+      const float xv = (hu >= 0 && hu < d.H && wu >= 0 && wu < d.W) ? to_f(x[hu * t.bs[2] + wu * t.bs[3]]) : 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) acc[kk][j] += g[kk] * xv;
+    }
+  }
+  // lanes l and l ^ (KO * 2^i) share the channel group inside a wave
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+    for (int j = 0; j < RS; ++j)
+      for (int o = KO; o < 64; o <<= 1) acc[kk][j] += __shfl_xor(acc[kk][j], o, 64);
+  __shared__ float red[4][64 * RS];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane < KO) {
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+      for (int j = 0; j < RS; ++j) red[wid][(ko * 8 + kk) * RS + j] = acc[kk][j];
+  }
+  __syncthreads();
+  float* dw = (float*)t.out;
+  for (int i = threadIdx.x; i < d.K * RS; i += NT)
+    atomicAdd(&dw[i], red[0][i] + red[1][i] + red[2][i] + red[3][i]);
+}
+
+// ============================================================ Cout == 1
+// A pixel is served by LP = C/VN lanes (one 16-byte channel chunk each); 64/LP pixels per wave.
+// fwd: y = bias + sum over taps of <x row chunk, w chunk>, reduced over the LP lanes.
+template <typename T, typename TO, int RS>
+__global__ void __launch_bounds__(NT) k1_fwd(Thin t, int LP) {
+  constexpr int VN = V16<T>::N;
+  const es_conv_desc_t& d = t.d;
+  __shared__ float wf[1024];
+  for (int i = threadIdx.x; i < RS * d.C; i += NT) wf[i] = to_f(((const T*)t.w)[i]);   // [R][S][C]
+  __syncthreads();
+  const int PPB = NT / LP;
+  const int m = blockIdx.x * PPB + threadIdx.x / LP, l = threadIdx.x % LP;
+  const bool live = m < t.M;
+  int n, p, q;
+  pix3(live ? m : 0, d.P, d.Q, n, p, q);
+  const T* x = (const T*)t.a + n * t.as[0] + l * VN;
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < RS; ++j) {
+    const int hu = p - d.pad + j / d.S, wu = q - d.pad + j % d.S;
+    if (!live || hu < 0 || hu >= d.H || wu < 0 || wu >= d.W) continue;
+    const T* px = x + hu * t.as[2] + wu * t.as[3];
+    const float* pw = wf + j * d.C + l * VN;
+    if constexpr (VN == 8) {
+      float v[8];
+      ld8<T>(px, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += v[e] * pw[e];
+    } else {
+      const float4 v = *(const float4*)px;
+      s += v.x * pw[0] + v.y * pw[1] + v.z * pw[2] + v.w * pw[3];
+    }
+  }
+  for (int o = LP >> 1; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (live && l == 0) {
+    TO* y = (TO*)t.out + n * t.os[0] + p * t.os[2] + q * t.os[3];
+    *y = from_f<TO>(s + (t.bias ? t.bias[0] : 0.f));
+  }
+}
+
+// dgrad: dx[n,h,w,c] = sum over taps of dy[n, h+pad-r, w+pad-s] * w[c][r][s]   (wd = [C][R][S])
+template <typename T, typename TO, int RS>
+__global__ void __launch_bounds__(NT) k1_dgrad(Thin t, int LP) {
+  constexpr int VN = V16<T>::N;
+  const es_conv_desc_t& d = t.d;
+  __shared__ float wf[1024];                                  // transposed to [R*S][C]
+  for (int i = threadIdx.x; i < RS * d.C; i += NT) {
+    const int c = i / RS, j = i % RS;
+    wf[j * d.C + c] = to_f(((const T*)t.w)[i]);
+  }
+  __syncthreads();
+  const int PPB = NT / LP;
+  const int m = blockIdx.x * PPB + threadIdx.x / LP, l = threadIdx.x % LP;
+  if (m >= t.M) return;
+  int n, h, w;
+  pix3(m, d.H, d.W, n, h, w);
+  const T* dy = (const T*)t.a + n * t.as[0];
+  float acc[VN];
+#pragma unroll
+  for (int e = 0; e < VN; ++e) acc[e] = 0.f;
+#pragma unroll
+  for (int j = 0; j < RS; ++j) {
+    const int ph = h + d.pad - j / d.S, pw = w + d.pad - j % d.S;
+    if (ph < 0 || pw < 0 || ph >= d.P || pw >= d.Q) continue;
+    const float g = to_f(dy[ph * t.as[2] + pw * t.as[3]]);
+    const float* wr = wf + j * d.C + l * VN;
+#pragma unroll
+    for (int e = 0; e < VN; ++e) acc[e] += g * wr[e];
+  }
+  TO* o = (TO*)t.out + n * t.os[0] + h * t.os[2] + w * t.os[3] + l * VN;
+  if constexpr (VN == 8) {
+    if (t.beta != 0.f) {
+      float old[8];
+      ld8<TO>(o, old);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += t.beta * old[e];
+    }
+    st8<TO>(o, acc);
+  } else {
+#pragma unroll
+    for (int e = 0; e < VN; ++e) {
+      float v = acc[e];
+      if (t.beta != 0.f) v += t.beta * to_f(o[e]);
+      o[e] = from_f<TO>(v);
+    }
+  }
+}
+
+// wgrad: dw[r][s][c] = sum over pixels of dy[pix] * x[pix + (r,s)][c]; lane = channel chunk
+template <typename T, int RS>
+__global__ void __launch_bounds__(NT) k1_wgrad(Thin t, int LP) {
+  constexpr int VN = V16<T>::N;
+  const es_conv_desc_t& d = t.d;
+  const int PPB = NT / LP;
+  const int l = threadIdx.x % LP;
+  float acc[RS][VN];
+#pragma unroll
+  for (int j = 0; j < RS; ++j)
+#pragma unroll
+    for (int e = 0; e < VN; ++e) acc[j][e] = 0.f;
+  for (int m = blockIdx.x * PPB + threadIdx.x / LP; m < t.M; m += gridDim.x * PPB) {
+    int n, p, q;
+    pix3(m, d.P, d.Q, n, p, q);
+    const float g = to_f(((const T*)t.a)[n * t.as[0] + p * t.as[2] + q * t.as[3]]);
+    const T* x = (const T*)t.b + n * t.bs[0] + l * VN;
+#pragma unroll
+    for (int j = 0; j < RS; ++j) {
+      const int hu = p - d.pad + j / d.S, wu = q - d.pad + j % d.S;
+      if (hu < 0 || hu >= d.H || wu < 0 || wu >= d.W) continue;
+      const T* px = x + hu * t.bs[2] + wu * t.bs[3];
+      if constexpr (VN == 8) {
+        float v[8];
+        ld8<T>(px, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[j][e] += g * v[e];
+      } else {
+        const float4 v = *(const float4*)px;
+        acc[j][0] += g * v.x; acc[j][1] += g * v.y; acc[j][2] += g * v.z; acc[j][3] += g * v.w;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < RS; ++j)
+#pragma unroll
+    for (int e = 0; e < VN; ++e)
+      for (int o = LP; o < 64; o <<= 1) acc[j][e] += __shfl_xor(acc[j][e], o, 64);
+  __shared__ float red[4][1024];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane < LP) {
+#pragma unroll
+    for (int j = 0; j < RS; ++j)
+#pragma unroll
+      for (int e = 0; e < VN; ++e) red[wid][j * d.C + l * VN + e] = acc[j][e];
+  }
+  __syncthreads();
+  float* dw = (float*)t.out;
+  for (int i = threadIdx.x; i < RS * d.C; i += NT)
+    atomicAdd(&dw[i], red[0][i] + red[1][i] + red[2][i] + red[3][i]);
+}
+
+bool plain(const es_conv_desc_t* d) {
+  return d->hmap == nullptr && d->up_h <= 0 && d->Hu == d->H && d->Wu == d->W;
+}
+bool pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
+// every row start of a channels-last view is a multiple of v elements (vector loads / stores)
+bool aligned(const int64_t s[4], int v) { return s[0] % v == 0 && s[2] % v == 0 && s[3] % v == 0; }
+
+// Cin == 1 path: K % 8 == 0, K <= 64, stride 1 or 2, R*S in {4, 9}
+bool c1_ok(const es_conv_desc_t* d, int rs) {
+  return plain(d) && d->C == 1 && d->K % 8 == 0 && pow2(d->K) && d->K <= 64 && (d->stride == 1 || d->stride == 2) &&
+         (rs == 4 || rs == 9);
+}
+// Cout == 1 path: stride 1, C / VN lanes per pixel dividing 64, R*S in {4, 9}, R*S*C <= 4096
+bool k1_ok(const es_conv_desc_t* d, int rs, int vn) {
+  return plain(d) && d->K == 1 && d->stride == 1 && d->C % vn == 0 && pow2(d->C / vn) && d->C / vn <= 64 &&
+         (rs == 4 || rs == 9) && rs * d->C <= 1024;
+}
+
+unsigned blocks(int64_t items, int per) { return (unsigned)((items + per - 1) / per); }
+
+template <typename T, typename TO>
+void launch_fwd(const Thin& t, int rs, int LP, hipStream_t st) {
+  const es_conv_desc_t& d = t.d;
+  if (d.C == 1) {
+    const dim3 grid(blocks(t.M, NT / (d.K / (16 / (int)sizeof(TO)))));
+    if (rs == 4) hipLaunchKernelGGL((c1_fwd<T, TO, 4>), grid, dim3(NT), 0, st, t);
+    else hipLaunchKernelGGL((c1_fwd<T, TO, 9>), grid, dim3(NT), 0, st, t);
+  } else {
+    const dim3 grid(blocks(t.M, NT / LP));
+    if (rs == 4) hipLaunchKernelGGL((k1_fwd<T, TO, 4>), grid, dim3(NT), 0, st, t, LP);
+    else hipLaunchKernelGGL((k1_fwd<T, TO, 9>), grid, dim3(NT), 0, st, t, LP);
+  }
+}
+
+template <typename T, typename TO>
+void launch_dgrad(const Thin& t, int rs, int LP, hipStream_t st) {
+  const es_conv_desc_t& d = t.d;
+  if (d.C == 1) {
+    const dim3 grid(blocks(t.M, NT / (d.K / V16<T>::N)));
+    if (rs == 4) hipLaunchKernelGGL((c1_dgrad<T, TO, 4>), grid, dim3(NT), 0, st, t);
+    else hipLaunchKernelGGL((c1_dgrad<T, TO, 9>), grid, dim3(NT), 0, st, t);
+  } else {
+    const dim3 grid(blocks(t.M, NT / LP));
+    if (rs == 4) hipLaunchKernelGGL((k1_dgrad<T, TO, 4>), grid, dim3(NT), 0, st, t, LP);
+    else hipLaunchKernelGGL((k1_dgrad<T, TO, 9>), grid, dim3(NT), 0, st, t, LP);
+  }
+}
+
+template <typename T>
+void launch_wgrad(const Thin& t, int rs, int LP, hipStream_t st) {
+  const es_conv_desc_t& d = t.d;
+  // ~4 blocks per CU, each reducing a strided slice of the pixels
+  const int per = d.C == 1 ? NT / (d.K / 8) : NT / LP;
+  const dim3 grid(std::min<unsigned>(1024u, blocks(t.M, per)));
+  if (d.C == 1) {
+    if (rs == 4) hipLaunchKernelGGL((c1_wgrad<T, 4>), grid, dim3(NT), 0, st, t);
+    else hipLaunchKernelGGL((c1_wgrad<T, 9>), grid, dim3(NT), 0, st, t);
+  } else {
+    if (rs == 4) hipLaunchKernelGGL((k1_wgrad<T, 4>), grid, dim3(NT), 0, st, t, LP);
+    else hipLaunchKernelGGL((k1_wgrad<T, 9>), grid, dim3(NT), 0, st, t, LP);
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------- entry points
+// Each returns 1 if it launched (caller checks the launch), 0 if the shape is not a thin conv.
+int es_thin_conv_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x, const int64_t xs[4], const void* wk,
+                     const float* bias, void* y, es_dtype_t ydt, const int64_t ys[4], hipStream_t st) {
+  const int rs = d->R * d->S, vn = dt == ES_BF16 ? 8 : 4;
+  const bool c1 = c1_ok(d, rs) && ys[1] == 1 && aligned(ys, 8);
+  const bool k1 = k1_ok(d, rs, vn) && xs[1] == 1 && xs[3] == d->C && aligned(xs, vn);
+  if (!c1 && !k1) return 0;
+  Thin t{};
+  t.d = *d; t.a = x; t.w = wk; t.bias = bias; t.out = y;
+  for (int i = 0; i < 4; ++i) { t.as[i] = xs[i]; t.os[i] = ys[i]; }
+  t.M = d->N * d->P * d->Q;
+  const int LP = k1 ? d->C / vn : 1;
+  if (dt == ES_BF16) {
+    if (ydt == ES_BF16) launch_fwd<bf16, bf16>(t, rs, LP, st); else launch_fwd<bf16, float>(t, rs, LP, st);
+  } else {
+    if (ydt == ES_BF16) launch_fwd<float, bf16>(t, rs, LP, st); else launch_fwd<float, float>(t, rs, LP, st);
+  }
+  return 1;
+}
+
+int es_thin_conv_dgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, const int64_t ys[4],
+                       const void* wd, void* dx, es_dtype_t dxdt, const int64_t dxs[4], float beta,
+                       hipStream_t st) {
+  const int rs = d->R * d->S, vn = dt == ES_BF16 ? 8 : 4;
+  const bool c1 = c1_ok(d, rs) && ys[1] == 1 && aligned(ys, 8);
+  const bool k1 = k1_ok(d, rs, vn) && dxs[1] == 1 && dxs[3] == d->C && aligned(dxs, vn);
+  if (!c1 && !k1) return 0;
+  Thin t{};
+  t.d = *d; t.a = dy; t.w = wd; t.out = dx; t.beta = beta;
+  for (int i = 0; i < 4; ++i) { t.as[i] = ys[i]; t.os[i] = dxs[i]; }
+  t.M = d->N * d->H * d->W;
+  const int LP = k1 ? d->C / vn : 1;
+  if (dt == ES_BF16) {
+    if (dxdt == ES_BF16) launch_dgrad<bf16, bf16>(t, rs, LP, st); else launch_dgrad<bf16, float>(t, rs, LP, st);
+  } else {
+    if (dxdt == ES_BF16) launch_dgrad<float, bf16>(t, rs, LP, st); else launch_dgrad<float, float>(t, rs, LP, st);
+  }
+  return 1;
+}
+
+int es_thin_conv_wgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, const int64_t ys[4], const void* x,
+                       const int64_t xs[4], float* dw, hipStream_t st) {
+  const int rs = d->R * d->S, vn = dt == ES_BF16 ? 8 : 4;
+  const bool c1 = c1_ok(d, rs) && ys[1] == 1 && aligned(ys, 8) && pow2(d->K / 8) && d->K / 8 <= 8;
+  const bool k1 = k1_ok(d, rs, vn) && xs[1] == 1 && xs[3] == d->C && aligned(xs, vn);
+  if (!c1 && !k1) return 0;
+  Thin t{};
+  t.d = *d; t.a = dy; t.b = x; t.out = dw;
+  for (int i = 0; i < 4; ++i) { t.as[i] = ys[i]; t.bs[i] = xs[i]; }
+  t.M = d->N * d->P * d->Q;
+  const int LP = k1 ? d->C / vn : 1;
+  if (dt == ES_BF16) launch_wgrad<bf16>(t, rs, LP, st);
+  else launch_wgrad<float>(t, rs, LP, st);
+  return 1;
+}

@@ -42,6 +42,17 @@ __device__ __forceinline__ void stf(void* p, int bf, int64_t i, float v) {
   else ((float*)p)[i] = v;
 }
 __device__ __forceinline__ void decompose(const View& v, bool cl, int64_t e, int& n, int& c, int& h, int& w) {
+  if (e < 0x7fffffff) {   // 32-bit index math (64-bit division is a long software sequence)
+    uint32_t t = (uint32_t)e;
+    if (cl) {
+      c = t % (uint32_t)v.c; t /= (uint32_t)v.c; w = t % (uint32_t)v.w; t /= (uint32_t)v.w;
+      h = t % (uint32_t)v.h; n = t / (uint32_t)v.h;
+    } else {
+      w = t % (uint32_t)v.w; t /= (uint32_t)v.w; h = t % (uint32_t)v.h; t /= (uint32_t)v.h;
+      c = t % (uint32_t)v.c; n = t / (uint32_t)v.c;
+    }
+    return;
+  }
   if (cl) {
     c = e % v.c; int64_t t = e / v.c; w = t % v.w; t /= v.w; h = t % v.h; n = t / v.h;
   } else {

@@ -17,17 +17,25 @@
 //            block per group, two passes (mean, then centred sum of squares).
 #include "common.h"
 
-// fast path for dense channels-last BatchNorm (norm_fast.hip)
+// fast path for dense channels-last BatchNorm / GroupNorm (norm_fast.hip); G = 0 means BN
 bool es_fast_dense_nhwc(const es_view_t* v);
-int64_t es_fast_part_floats(const es_view_t* v);
-int es_fast_bn_stats(const es_view_t* v, es_dtype_t dt, const void* xp, float* part, hipStream_t st);
-void es_fast_bn_fwd(const es_view_t* v, es_dtype_t dt, const void* xp, void* yp, const es_norm_t* nm,
-                    const es_chain_t* ch, hipStream_t st);
-int es_fast_bn_bwd_reduce(const es_view_t* v, es_dtype_t dt, const void* xp, const void* dyp, const es_norm_t* nm,
-                          const es_chain_t* ch, float* part, hipStream_t st);
-void es_fast_bn_bwd_apply(const es_view_t* v, es_dtype_t dt, const void* xp, const void* dyp, void* dxp,
-                          const es_norm_t* nm, const es_chain_t* ch, const float* a1, const float* a2,
-                          float* dsum, hipStream_t st);
+int64_t es_fast_part_floats(const es_view_t* v, int G);
+int es_fast_norm_stats(const es_view_t* v, int G, es_dtype_t dt, const void* xp, float* part, hipStream_t st);
+void es_fast_norm_fwd(const es_view_t* v, int G, es_dtype_t dt, const void* xp, void* yp, const es_norm_t* nm,
+                      const es_chain_t* ch, hipStream_t st);
+int es_fast_norm_bwd_reduce(const es_view_t* v, int G, es_dtype_t dt, const void* xp, const void* dyp,
+                            const es_norm_t* nm, const es_chain_t* ch, float* part, hipStream_t st);
+int es_fast_norm_bwd_apply(const es_view_t* v, int G, es_dtype_t dt, const void* xp, const void* dyp, void* dxp,
+                           const es_norm_t* nm, const es_chain_t* ch, const float* a1, const float* a2,
+                           float* dsum, float* part, hipStream_t st);
+
+// which fast variant serves a norm of this kind on this view: -1 none, 0 BN, G > 0 GroupNorm
+static int fast_kind(const es_view_t* v, int kind, int groups) {
+  if (!es_fast_dense_nhwc(v)) return -1;
+  if (kind == ES_NORM_BN) return 0;
+  if (kind == ES_NORM_GN && groups > 0 && v->c % groups == 0 && v->h * v->w > 1) return groups;
+  return -1;
+}
 
 static bool same_view(const es_view_t* a, const es_view_t* b) {
   return a->n == b->n && a->c == b->c && a->h == b->h && a->w == b->w && a->s[0] == b->s[0] &&
@@ -124,6 +132,17 @@ __device__ __forceinline__ uint64_t logical_index(const View& v, int n, int c, i
 
 // element e of the logical tensor -> (n,c,h,w); channels-last order when the view says so
 __device__ __forceinline__ void decompose(const View& v, bool cl, int64_t e, int& n, int& c, int& h, int& w) {
+  if (e < 0x7fffffff) {   // 32-bit index math (64-bit division is a long software sequence)
+    uint32_t t = (uint32_t)e;
+    if (cl) {
+      c = t % (uint32_t)v.c; t /= (uint32_t)v.c; w = t % (uint32_t)v.w; t /= (uint32_t)v.w;
+      h = t % (uint32_t)v.h; n = t / (uint32_t)v.h;
+    } else {
+      w = t % (uint32_t)v.w; t /= (uint32_t)v.w; h = t % (uint32_t)v.h; t /= (uint32_t)v.h;
+      c = t % (uint32_t)v.c; n = t / (uint32_t)v.c;
+    }
+    return;
+  }
   if (cl) {
     c = e % v.c; int64_t t = e / v.c; w = t % v.w; t /= v.w; h = t % v.h; n = t / v.h;
   } else {
@@ -165,7 +184,8 @@ __global__ void __launch_bounds__(256) colred_kernel(BwdIn b, int64_t rows, int6
   if (c < C) {
     // row r -> (n, h, w), w fastest
     for (int64_t r = r0 + ty; r < r1; r += 4) {
-      const int w = r % v.w; const int64_t t = r / v.w; const int h = t % v.h; const int n = t / v.h;
+      const uint32_t r32 = (uint32_t)r, t = r32 / (uint32_t)v.w;   // rows < 2^31 (host-checked sizes)
+      const int w = r32 - t * v.w, h = t % (uint32_t)v.h, n = t / (uint32_t)v.h;
       if (RED == RED_STATS) {
         const float x = ldf(b.xp, b.xbf, v.off(n, c, h, w));
         cnt += 1.f;
@@ -317,6 +337,47 @@ __global__ void __launch_bounds__(256) sums_finalize_block_kernel(const float* p
   }
 }
 
+// GroupNorm stats finalize from fast partials [n][chunk][3][C]: one thread per (n, g), Chan merge
+// over the chunks and the cg channels of the group.
+__global__ void gn_finalize_kernel(const float* part, int N, int chunks, int C, int G, float eps, float* mean,
+                                   float* invstd) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * G) return;
+  const int n = i / G, g = i % G, cg = C / G;
+  double n_ = 0.0, mu = 0.0, M = 0.0;
+  for (int k = 0; k < chunks; ++k) {
+    const float* p = part + ((int64_t)n * chunks + k) * 3 * C;
+    for (int c = g * cg; c < (g + 1) * cg; ++c) {
+      const double nb = p[c];
+      if (nb == 0.0) continue;
+      const double mb = p[C + c], Mb = p[2 * C + c];
+      const double nt = n_ + nb, dl = mb - mu;
+      mu += dl * nb / nt;
+      M += Mb + dl * dl * n_ * nb / nt;
+      n_ = nt;
+    }
+  }
+  mean[i] = (float)mu;
+  invstd[i] = (float)(1.0 / sqrt(M / n_ + (double)eps));
+}
+
+// GroupNorm backward finalize from fast partials: a1/a2[n, g] = mean over the group of gamma*s
+__global__ void gn_bwd_finalize_kernel(const float* part, int N, int chunks, int C, int G, float cnt,
+                                       const float* gamma, float* a1, float* a2) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * G) return;
+  const int n = i / G, g = i % G, cg = C / G;
+  float s1 = 0.f, s2 = 0.f;
+  for (int k = 0; k < chunks; ++k) {
+    const float* p = part + ((int64_t)n * chunks + k) * 3 * C;
+    for (int c = g * cg; c < (g + 1) * cg; ++c) {
+      const float ga = gamma ? gamma[c] : 1.f;
+      s1 += ga * p[C + c]; s2 += ga * p[2 * C + c];
+    }
+  }
+  a1[i] = s1 / cnt; a2[i] = s2 / cnt;
+}
+
 void colred_geometry(const View& v, int& cblocks, int& chunks, int64_t& rows, int64_t& per) {
   rows = (int64_t)v.n * v.h * v.w;
   cblocks = (v.c + 63) / 64;
@@ -337,9 +398,10 @@ __global__ void __launch_bounds__(256) segred_kernel(BwdIn b, float eps, float* 
   const int64_t cnt = (int64_t)cg * v.h * v.w;
   const bool cl = v.s[1] == 1 && cg > 1;
   __shared__ float sh[8];
-  auto coords = [&](int64_t j, int& c, int& h, int& w) {
-    if (cl) { c = g * cg + j % cg; const int64_t t = j / cg; w = t % v.w; h = t / v.w; }
-    else { w = j % v.w; const int64_t t = j / v.w; h = t % v.h; c = g * cg + t / v.h; }
+  auto coords = [&](int64_t j64, int& c, int& h, int& w) {
+    const uint32_t j = (uint32_t)j64;   // j < cnt = cg*h*w (one sample)
+    if (cl) { c = g * cg + j % cg; const uint32_t t = j / cg; w = t % v.w; h = t / v.w; }
+    else { w = j % v.w; const uint32_t t = j / v.w; h = t % v.h; c = g * cg + t / v.h; }
   };
   if (RED == RED_STATS) {
     float s = 0.f;
@@ -444,6 +506,16 @@ BwdIn mk_bwdin(const es_view_t* x, es_dtype_t xdt, const void* xp, const es_norm
   return b;
 }
 
+// dsum += sum of the fast apply's per-block partials (s1 slot of [chunk][3][C])
+void fast_dsum_finalize(int C, int chunks, const float* part, float* dsum, hipStream_t st) {
+  if (chunks <= 0 || dsum == nullptr) return;
+  if (chunks > 32)
+    hipLaunchKernelGGL(sums_finalize_block_kernel, dim3(C), dim3(256), 0, st, part, chunks, C, 1.f, nullptr,
+                       (float*)nullptr, (float*)nullptr, dsum, (float*)nullptr, 1.f);
+  else
+    hipLaunchKernelGGL(sum_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, chunks, C, dsum, 1.f);
+}
+
 int64_t stats_groups(const es_view_t* x, int kind, int groups) {
   if (kind == ES_NORM_BN) return x->c;
   if (kind == ES_NORM_GN) return (int64_t)x->n * groups;
@@ -454,13 +526,15 @@ int64_t stats_groups(const es_view_t* x, int kind, int groups) {
 
 // ================================================================================ C ABI
 extern "C" int64_t es_norm_stats_ws_bytes(const es_view_t* x, int kind, int groups) {
-  (void)groups;
-  if (kind != ES_NORM_BN) return 0;
-  View v = mkview(x);
-  int cb, chunks; int64_t rows, per;
-  colred_geometry(v, cb, chunks, rows, per);
-  int64_t b = (int64_t)chunks * 3 * v.c * sizeof(float);
-  if (es_fast_dense_nhwc(x)) b = std::max<int64_t>(b, es_fast_part_floats(x) * (int64_t)sizeof(float));
+  const int fk = fast_kind(x, kind, groups);
+  int64_t b = 0;
+  if (kind == ES_NORM_BN) {
+    View v = mkview(x);
+    int cb, chunks; int64_t rows, per;
+    colred_geometry(v, cb, chunks, rows, per);
+    b = (int64_t)chunks * 3 * v.c * sizeof(float);
+  }
+  if (fk >= 0) b = std::max<int64_t>(b, es_fast_part_floats(x, fk) * (int64_t)sizeof(float));
   return b;
 }
 
@@ -473,12 +547,19 @@ extern "C" int es_norm_stats(const es_view_t* x, es_dtype_t xdt, const void* xp,
   ES_CHECK_ARG(kind != ES_NORM_LN || (x->h == 1 && x->w == 1), "norm_stats: LN needs (N,F,1,1) views");
   es_norm_t nm{kind, groups, nullptr, nullptr, nullptr, nullptr};
   BwdIn b = mk_bwdin(x, xdt, xp, &nm, nullptr);
-  if (kind == ES_NORM_BN) {
+  const int fk = fast_kind(x, kind, groups);
+  if (fk > 0) {
+    ES_CHECK_ARG(ws != nullptr, "norm_stats: fast GroupNorm needs workspace");
+    const int chunks = es_fast_norm_stats(x, fk, xdt, xp, (float*)ws, st);
+    const int ng = x->n * groups;
+    hipLaunchKernelGGL(gn_finalize_kernel, dim3((ng + 255) / 256), dim3(256), 0, st, (const float*)ws, x->n,
+                       chunks, x->c, groups, eps, mean, invstd);
+  } else if (kind == ES_NORM_BN) {
     int cb, chunks; int64_t rows, per;
     colred_geometry(b.x, cb, chunks, rows, per);
     ES_CHECK_ARG(ws != nullptr, "norm_stats: BN needs workspace");
-    if (es_fast_dense_nhwc(x))
-      chunks = es_fast_bn_stats(x, xdt, xp, (float*)ws, st);
+    if (fk == 0)
+      chunks = es_fast_norm_stats(x, 0, xdt, xp, (float*)ws, st);
     else
       hipLaunchKernelGGL(colred_kernel<RED_STATS>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, (float*)ws);
     if (chunks > 32)
@@ -500,8 +581,9 @@ extern "C" int es_norm_act_fwd(const es_view_t* x, es_dtype_t xdt, const es_norm
                                const void* addend_ptr, const void* xp, const es_view_t* y,
                                es_dtype_t ydt, void* yp, es_stream_t stream) {
   ES_CHECK_ARG(x->n == y->n && x->c == y->c && x->h == y->h && x->w == y->w, "norm_act_fwd: shape");
-  if (nm && nm->kind == ES_NORM_BN && !addend_ptr && xdt == ydt && es_fast_dense_nhwc(x) && same_view(x, y)) {
-    es_fast_bn_fwd(x, xdt, xp, yp, nm, ch, (hipStream_t)stream);
+  const int fk = nm ? fast_kind(x, nm->kind, nm->groups) : -1;
+  if (fk >= 0 && !addend_ptr && xdt == ydt && same_view(x, y)) {
+    es_fast_norm_fwd(x, fk, xdt, xp, yp, nm, ch, (hipStream_t)stream);
     ES_CHECK_LAUNCH();
     return ES_OK;
   }
@@ -527,7 +609,8 @@ extern "C" int64_t es_norm_bwd_ws_bytes(const es_view_t* x, int kind, int groups
   int cb, chunks; int64_t rows, per;
   colred_geometry(v, cb, chunks, rows, per);
   int64_t part = (int64_t)chunks * 3 * v.c * sizeof(float);
-  if (es_fast_dense_nhwc(x)) part = std::max<int64_t>(part, es_fast_part_floats(x) * (int64_t)sizeof(float));
+  const int fk = fast_kind(x, kind, groups);
+  if (fk >= 0) part = std::max<int64_t>(part, es_fast_part_floats(x, fk) * (int64_t)sizeof(float));
   const int64_t ng = kind == ES_NORM_NONE ? 0 : stats_groups(x, kind, groups);
   return part + 2 * ng * (int64_t)sizeof(float) + 256;
 }
@@ -553,21 +636,42 @@ extern "C" int es_norm_act_bwd(const es_view_t* x, es_dtype_t xdt, const void* x
   colred_geometry(b.x, cb, chunks, rows, per);
   float* part = (float*)ws;
   int64_t part_floats = (int64_t)chunks * 3 * x->c;
-  const bool fast = kind == ES_NORM_BN && !refp && beta == 0.f && xdt == dydt && dydt == dxdt &&
-                    es_fast_dense_nhwc(x) && same_view(x, dy) && same_view(x, dx);
-  if (es_fast_dense_nhwc(x)) part_floats = std::max<int64_t>(part_floats, es_fast_part_floats(x));
+  const int fk = fast_kind(x, kind, groups);
+  const bool fast = fk >= 0 && !refp && beta == 0.f && xdt == dydt && dydt == dxdt && same_view(x, dy) &&
+                    (dxp == nullptr || same_view(x, dx));
+  if (fk >= 0) part_floats = std::max<int64_t>(part_floats, es_fast_part_floats(x, fk));
   float* g1 = part + part_floats;
   const int64_t ng = kind == ES_NORM_NONE ? 0 : stats_groups(x, kind, groups);
   float* g2 = g1 + ng;
+  if (fast && fk > 0) {
+    const int fchunks = es_fast_norm_bwd_reduce(x, fk, xdt, xp, dyp, nm, ch, part, st);
+    hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3((unsigned)((ng + 255) / 256)), dim3(256), 0, st,
+                       (const float*)part, x->n, fchunks, x->c, groups, (float)((x->c / groups) * x->h * x->w),
+                       nm->gamma, g1, g2);
+    if (dgamma || dbeta) {
+      const int allc = x->n * fchunks;   // per-channel sums over every (n, chunk) partial
+      if (allc > 32)
+        hipLaunchKernelGGL(sums_finalize_block_kernel, dim3(x->c), dim3(256), 0, st, (const float*)part, allc,
+                           x->c, 1.f, nullptr, (float*)nullptr, (float*)nullptr, dbeta, dgamma, 1.f);
+      else
+        hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)part,
+                           allc, x->c, 1.f, nullptr, (float*)nullptr, (float*)nullptr, dgamma, dbeta);
+    }
+    if (dxp) fast_dsum_finalize(x->c, es_fast_norm_bwd_apply(x, fk, xdt, xp, dyp, dxp, nm, ch, g1, g2, dsum, part, st),
+                                part, dsum, st);
+    ES_CHECK_LAUNCH();
+    return ES_OK;
+  }
   if (fast) {
-    const int fchunks = es_fast_bn_bwd_reduce(x, xdt, xp, dyp, nm, ch, part, st);
+    const int fchunks = es_fast_norm_bwd_reduce(x, 0, xdt, xp, dyp, nm, ch, part, st);
     if (fchunks > 32)
       hipLaunchKernelGGL(sums_finalize_block_kernel, dim3(x->c), dim3(256), 0, st, (const float*)part, fchunks,
                          x->c, (float)rows, nm->gamma, g1, g2, dbeta, dgamma, 1.f);
     else
       hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)part,
                          fchunks, x->c, (float)rows, nm->gamma, g1, g2, dgamma, dbeta);
-    if (dxp) es_fast_bn_bwd_apply(x, xdt, xp, dyp, dxp, nm, ch, g1, g2, dsum, st);
+    if (dxp) fast_dsum_finalize(x->c, es_fast_norm_bwd_apply(x, 0, xdt, xp, dyp, dxp, nm, ch, g1, g2, dsum, part, st),
+                                part, dsum, st);
     ES_CHECK_LAUNCH();
     return ES_OK;
   }

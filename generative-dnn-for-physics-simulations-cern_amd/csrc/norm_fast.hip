@@ -1,8 +1,12 @@
-// Fast path of the BatchNorm + dropout + activation pipeline for dense channels-last tensors.
+// Fast path of the BatchNorm / GroupNorm + dropout + activation pipeline for dense channels-last
+// tensors.
 //
 // Covers every BatchNorm of the neutron generator and aux regressor (neutron/generator.py:13,19,
-// 26,31,35; neutron/aux_reg.py:15,23,31,39,47) when x, y / dy, dx are NHWC-dense ([rows][C],
-// rows = N*H*W) of one dtype and C % 8 == 0.  Layout of the work: a thread owns 8 consecutive
+// 26,31,35; neutron/aux_reg.py:15,23,31,39,47) and the GroupNorms of the discriminators and the
+// proton generator (neutron/discriminator.py:13,18; proton/generator.py:28,34,39) when x, y / dy,
+// dx are NHWC-dense ([rows][C], rows = N*H*W) of one dtype and C % 8 == 0.  GroupNorm runs the
+// same kernels with blockIdx.z = sample n: a block then covers the H*W rows of one sample, its
+// statistics are indexed (n, c / (C/G)), and per-(n, c) partials are merged per group.  Layout of the work: a thread owns 8 consecutive
 // channels (one 16-byte bf16 / 32-byte fp32 vector) of 4 consecutive rows, so
 //   * no per-element index division (one division per 4 rows),
 //   * 16-byte vector loads and stores,
@@ -40,6 +44,7 @@ template <> __device__ __forceinline__ void st8<float>(float* p, const float* f)
 struct FastArgs {
   const void* x; const void* dy; void* out;   // out: y (fwd) or dx (bwd apply)
   int rows, C, HW;
+  int G, cg, zrows;                           // GroupNorm: G groups of cg channels, zrows = HW; BN: G = 0
   const float *mean, *invstd, *gamma, *beta;
   const float *a1, *a2;                       // bwd apply: per-channel gamma*mean(dnorm), gamma*mean(dnorm*xhat)
   float* part;                                // [chunk][3][C] partials (stats / bwd sums)
@@ -116,9 +121,20 @@ __device__ __forceinline__ float chain_bwd(const FastArgs& a, float z, float dou
   return dout * a.drop.scale * dactf(a, z);
 }
 
+__device__ __forceinline__ int pow2_ceil(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
 struct Geo {
   int CV, TCV, RGB, cv, rg, c0;
+  int rbase, rlim;                            // rows of this block's z slice
   bool active;
+  // index of the statistics of channel c (per channel for BN, per (n, group) for GN)
+  __device__ __forceinline__ int sidx(const FastArgs& a, int c) const {
+    return a.G ? (int)blockIdx.z * a.G + c / a.cg : c;
+  }
 };
 __device__ __forceinline__ Geo geo(const FastArgs& a) {
   Geo g;
@@ -129,6 +145,8 @@ __device__ __forceinline__ Geo geo(const FastArgs& a) {
   g.rg = threadIdx.x / g.TCV;
   g.active = g.rg < g.RGB && g.cv < g.CV;
   g.c0 = g.cv * 8;
+  g.rbase = (int)blockIdx.z * a.zrows;
+  g.rlim = min(a.rows, g.rbase + a.zrows);
   return g;
 }
 
@@ -139,27 +157,29 @@ __global__ void __launch_bounds__(256) bn_fwd_fast(FastArgs a) {
   float sc[8], sh[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const int c = g.c0 + k;
-    const float s = (a.gamma ? a.gamma[c] : 1.f) * a.invstd[c];
+    const int c = g.c0 + k, si = g.sidx(a, c);
+    const float s = (a.gamma ? a.gamma[c] : 1.f) * a.invstd[si];
     sc[k] = s;
-    sh[k] = (a.beta ? a.beta[c] : 0.f) - a.mean[c] * s;
+    sh[k] = (a.beta ? a.beta[c] : 0.f) - a.mean[si] * s;
   }
-  const T* x = (const T*)a.x;
-  T* y = (T*)a.out;
-  const int ngroups = (a.rows + 3) >> 2;
+  const T* __restrict__ x = (const T*)a.x;
+  T* __restrict__ y = (T*)a.out;
+  const int ngroups = (g.rlim - g.rbase + 3) >> 2;
   for (int grp = blockIdx.y * g.RGB + g.rg; grp < ngroups; grp += gridDim.y * g.RGB) {
-    const int r0 = grp * 4;
+    const int r0 = g.rbase + grp * 4;
+    const int nr = min(4, g.rlim - r0);
+    float v[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)            // issue every load of the group before any store
+      if (j < nr) ld8<T>(x + (int64_t)(r0 + j) * a.C + g.c0, v[j]);
     uint32_t keep[4];
     keep_bits(a, r0, g.c0, keep);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int r = r0 + j;
-      if (r >= a.rows) break;
-      float v[8];
-      ld8<T>(x + (int64_t)r * a.C + g.c0, v);
+      if (j >= nr) break;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = chain_fwd(a, v[k] * sc[k] + sh[k], (keep[j] >> k) & 1u);
-      st8<T>(y + (int64_t)r * a.C + g.c0, v);
+      for (int k = 0; k < 8; ++k) v[j][k] = chain_fwd(a, v[j][k] * sc[k] + sh[k], (keep[j] >> k) & 1u);
+      st8<T>(y + (int64_t)(r0 + j) * a.C + g.c0, v[j]);
     }
   }
 }
@@ -175,24 +195,24 @@ __global__ void __launch_bounds__(256) bn_reduce_fast(FastArgs a) {
   if (g.active) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int c = g.c0 + k;
+      const int c = g.c0 + k, si = g.sidx(a, c);
       if (MODE == 1) {
-        mu[k] = a.mean[c]; is[k] = a.invstd[c];
+        mu[k] = a.mean[si]; is[k] = a.invstd[si];
         const float s = (a.gamma ? a.gamma[c] : 1.f) * is[k];
         sc[k] = s; sh[k] = (a.beta ? a.beta[c] : 0.f) - mu[k] * s;
       }
     }
-    const T* x = (const T*)a.x;
-    const T* dy = (const T*)a.dy;
-    const int ngroups = (a.rows + 3) >> 2;
+    const T* __restrict__ x = (const T*)a.x;
+    const T* __restrict__ dy = (const T*)a.dy;
+    const int ngroups = (g.rlim - g.rbase + 3) >> 2;
     for (int grp = blockIdx.y * g.RGB + g.rg; grp < ngroups; grp += gridDim.y * g.RGB) {
-      const int r0 = grp * 4;
+      const int r0 = g.rbase + grp * 4;
       uint32_t keep[4];
       if (MODE == 1) keep_bits(a, r0, g.c0, keep);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int r = r0 + j;
-        if (r >= a.rows) break;
+        if (r >= g.rlim) break;
         float v[8];
         ld8<T>(x + (int64_t)r * a.C + g.c0, v);
         if (MODE == 0) {
@@ -217,33 +237,38 @@ __global__ void __launch_bounds__(256) bn_reduce_fast(FastArgs a) {
       }
     }
   }
-  // block merge across row groups (same channels) through LDS
-  __shared__ float l0[256 * 8], l1[256 * 8], l2[256 * 8];
+  // tree merge across the row groups (same channels) through LDS, [k][thread] layout
+  __shared__ float l0[8 * 256], l1[8 * 256], l2[8 * 256];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    l0[threadIdx.x * 8 + k] = s0[k]; l1[threadIdx.x * 8 + k] = s1[k]; l2[threadIdx.x * 8 + k] = s2[k];
+    l0[k * 256 + threadIdx.x] = s0[k]; l1[k * 256 + threadIdx.x] = s1[k]; l2[k * 256 + threadIdx.x] = s2[k];
   }
   __syncthreads();
-  if (g.active && g.rg == 0) {
-    for (int r = 1; r < g.RGB; ++r) {
-      const int o = (r * g.TCV + (int)(threadIdx.x % g.TCV)) * 8;
+  for (int h = pow2_ceil(g.RGB) >> 1; h > 0; h >>= 1) {
+    if (g.active && g.rg < h && g.rg + h < g.RGB) {
+      const int o = threadIdx.x + h * g.TCV;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         if (MODE == 0) {
-          const float nb = l0[o + k];
-          if (nb == 0.f) continue;
-          const float mb = l1[o + k], Mb = l2[o + k];
-          const float nt = s0[k] + nb, dl = mb - s1[k];
-          s1[k] += dl * nb / nt;
-          s2[k] += Mb + dl * dl * s0[k] * nb / nt;
-          s0[k] = nt;
+          const float nb = l0[k * 256 + o];
+          if (nb > 0.f) {
+            const float mb = l1[k * 256 + o], Mb = l2[k * 256 + o];
+            const float nt = s0[k] + nb, dl = mb - s1[k], f = nb / nt;
+            s1[k] += dl * f;
+            s2[k] += Mb + dl * dl * s0[k] * f;
+            s0[k] = nt;
+          }
         } else {
-          s1[k] += l1[o + k];
-          s2[k] += l2[o + k];
+          s1[k] += l1[k * 256 + o];
+          s2[k] += l2[k * 256 + o];
         }
+        l0[k * 256 + threadIdx.x] = s0[k]; l1[k * 256 + threadIdx.x] = s1[k]; l2[k * 256 + threadIdx.x] = s2[k];
       }
     }
-    float* p = a.part + (int64_t)blockIdx.y * 3 * a.C;
+    __syncthreads();
+  }
+  if (g.active && g.rg == 0) {
+    float* p = a.part + ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * 3 * a.C;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       p[g.c0 + k] = s0[k]; p[a.C + g.c0 + k] = s1[k]; p[2 * a.C + g.c0 + k] = s2[k];
@@ -258,54 +283,67 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_fast(FastArgs a) {
 #pragma unroll
   for (int k = 0; k < 8; ++k) acc[k] = 0.f;
   if (g.active) {
-    float sc[8], sh[8], mu[8], is[8], ga[8], c1[8], c2[8];
+    float mu[8], is[8], ga[8], be[8], c1[8], c2[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int c = g.c0 + k;
-      mu[k] = a.mean[c]; is[k] = a.invstd[c];
+      const int c = g.c0 + k, si = g.sidx(a, c);
+      mu[k] = a.mean[si]; is[k] = a.invstd[si];
       ga[k] = a.gamma ? a.gamma[c] : 1.f;
-      sc[k] = ga[k] * is[k]; sh[k] = (a.beta ? a.beta[c] : 0.f) - mu[k] * sc[k];
-      c1[k] = a.a1[c]; c2[k] = a.a2[c];
+      be[k] = a.beta ? a.beta[c] : 0.f;
+      c1[k] = a.a1[si]; c2[k] = a.a2[si];
     }
-    const T* x = (const T*)a.x;
-    const T* dy = (const T*)a.dy;
-    T* dx = (T*)a.out;
-    const int ngroups = (a.rows + 3) >> 2;
+    const T* __restrict__ x = (const T*)a.x;
+    const T* __restrict__ dy = (const T*)a.dy;
+    T* __restrict__ dx = (T*)a.out;
+    const int ngroups = (g.rlim - g.rbase + 3) >> 2;
     for (int grp = blockIdx.y * g.RGB + g.rg; grp < ngroups; grp += gridDim.y * g.RGB) {
-      const int r0 = grp * 4;
+      const int r0 = g.rbase + grp * 4;
+      const int nr = min(4, g.rlim - r0);
+      float v[4][8], d[4][8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)          // issue every load of the group before any store
+        if (j < nr) {
+          ld8<T>(x + (int64_t)(r0 + j) * a.C + g.c0, v[j]);
+          ld8<T>(dy + (int64_t)(r0 + j) * a.C + g.c0, d[j]);
+        }
       uint32_t keep[4];
       keep_bits(a, r0, g.c0, keep);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int r = r0 + j;
-        if (r >= a.rows) break;
-        float v[8], d[8];
-        ld8<T>(x + (int64_t)r * a.C + g.c0, v);
-        ld8<T>(dy + (int64_t)r * a.C + g.c0, d);
+        if (j >= nr) break;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const float dn = chain_bwd(a, v[k] * sc[k] + sh[k], d[k], (keep[j] >> k) & 1u);
-          const float xh = (v[k] - mu[k]) * is[k];
-          d[k] = is[k] * (dn * ga[k] - c1[k] - xh * c2[k]);
-          acc[k] += d[k];
+          const float xh = (v[j][k] - mu[k]) * is[k];
+          const float dn = chain_bwd(a, xh * ga[k] + be[k], d[j][k], (keep[j] >> k) & 1u);
+          d[j][k] = is[k] * (dn * ga[k] - c1[k] - xh * c2[k]);
+          acc[k] += d[j][k];
         }
-        st8<T>(dx + (int64_t)r * a.C + g.c0, d);
+        st8<T>(dx + (int64_t)(r0 + j) * a.C + g.c0, d[j]);
       }
     }
   }
   if (a.dsum) {
-    __shared__ float l1[256 * 8];
+    // per-block channel sums of dx -> partials (s1 slot of [z][chunk][3][C]); the host merges
+    // them into dsum (no same-address atomics from every block)
+    __shared__ float l1[8 * 256];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) l1[threadIdx.x * 8 + k] = acc[k];
+    for (int k = 0; k < 8; ++k) l1[k * 256 + threadIdx.x] = acc[k];
     __syncthreads();
-    if (g.active && g.rg == 0) {
-      for (int r = 1; r < g.RGB; ++r) {
-        const int o = (r * g.TCV + (int)(threadIdx.x % g.TCV)) * 8;
+    for (int h = pow2_ceil(g.RGB) >> 1; h > 0; h >>= 1) {
+      if (g.active && g.rg < h && g.rg + h < g.RGB) {
+        const int o = threadIdx.x + h * g.TCV;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] += l1[o + k];
+        for (int k = 0; k < 8; ++k) {
+          acc[k] += l1[k * 256 + o];
+          l1[k * 256 + threadIdx.x] = acc[k];
+        }
       }
+      __syncthreads();
+    }
+    if (g.active && g.rg == 0) {
+      float* p = a.part + ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * 3 * a.C + a.C;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) atomicAdd(&a.dsum[g.c0 + k], acc[k]);
+      for (int k = 0; k < 8; ++k) p[g.c0 + k] = acc[k];
     }
   }
 }
@@ -319,61 +357,66 @@ bool es_fast_dense_nhwc(const es_view_t* v) {
   return v->c % 8 == 0 && v->s[1] == 1 && v->s[3] == C && v->s[2] == W * C && v->s[0] == H * W * C;
 }
 
-static void fast_geometry(const es_view_t* v, dim3& grid, int& chunks) {
+// G = 0: BatchNorm (one z slice over all rows); G > 0: GroupNorm (z = sample)
+static void fast_geometry(const es_view_t* v, int G, dim3& grid, int& chunks) {
   const int CV = v->c / 8;
   const int TCV = CV < 64 ? CV : 64;
   const int RGB = 256 / TCV;
   const int gx = (CV + TCV - 1) / TCV;
-  const int64_t rows = (int64_t)v->n * v->h * v->w;
-  const int64_t ngroups = (rows + 3) / 4;
-  int64_t gy = std::max<int64_t>(1, 2048 / gx);
+  const int gz = G ? v->n : 1;
+  const int64_t zrows = G ? (int64_t)v->h * v->w : (int64_t)v->n * v->h * v->w;
+  const int64_t ngroups = (zrows + 3) / 4;
+  int64_t gy = std::max<int64_t>(1, 2048 / ((int64_t)gx * gz));
   gy = std::min<int64_t>(gy, (ngroups + RGB - 1) / RGB);
-  grid = dim3(gx, (unsigned)gy);
+  grid = dim3(gx, (unsigned)gy, gz);
   chunks = (int)gy;
 }
 
-int64_t es_fast_part_floats(const es_view_t* v) {
+int64_t es_fast_part_floats(const es_view_t* v, int G) {
   dim3 g; int chunks;
-  fast_geometry(v, g, chunks);
-  return (int64_t)chunks * 3 * v->c;
+  fast_geometry(v, G, g, chunks);
+  return (int64_t)g.z * chunks * 3 * v->c;
 }
 
-static FastArgs mk(const es_view_t* v, const es_chain_t* ch) {
+static FastArgs mk(const es_view_t* v, const es_chain_t* ch, int G) {
   FastArgs a{};
   a.rows = v->n * v->h * v->w;
   a.C = v->c;
   a.HW = v->h * v->w;
+  a.G = G;
+  a.cg = G ? v->c / G : 1;
+  a.zrows = G ? a.HW : a.rows;
   if (ch) { a.drop = ch->drop; a.dfirst = ch->dropout_first; a.act = ch->act; a.slope = ch->slope; }
   return a;
 }
 
-// stats -> partials (caller runs the BN finalize); returns chunks
-int es_fast_bn_stats(const es_view_t* v, es_dtype_t dt, const void* xp, float* part, hipStream_t st) {
+// stats -> partials [z][chunk][3][C] (caller runs the finalize); returns chunks per z
+int es_fast_norm_stats(const es_view_t* v, int G, es_dtype_t dt, const void* xp, float* part, hipStream_t st) {
   dim3 grid; int chunks;
-  fast_geometry(v, grid, chunks);
-  FastArgs a = mk(v, nullptr);
+  fast_geometry(v, G, grid, chunks);
+  FastArgs a = mk(v, nullptr, G);
   a.x = xp; a.part = part;
   if (dt == ES_BF16) hipLaunchKernelGGL((bn_reduce_fast<bf16, 0>), grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((bn_reduce_fast<float, 0>), grid, dim3(256), 0, st, a);
   return chunks;
 }
 
-void es_fast_bn_fwd(const es_view_t* v, es_dtype_t dt, const void* xp, void* yp, const es_norm_t* nm,
-                    const es_chain_t* ch, hipStream_t st) {
+void es_fast_norm_fwd(const es_view_t* v, int G, es_dtype_t dt, const void* xp, void* yp, const es_norm_t* nm,
+                      const es_chain_t* ch, hipStream_t st) {
   dim3 grid; int chunks;
-  fast_geometry(v, grid, chunks);
-  FastArgs a = mk(v, ch);
+  fast_geometry(v, G, grid, chunks);
+  FastArgs a = mk(v, ch, G);
   a.x = xp; a.out = yp;
   a.mean = nm->mean; a.invstd = nm->invstd; a.gamma = nm->gamma; a.beta = nm->beta;
   if (dt == ES_BF16) hipLaunchKernelGGL(bn_fwd_fast<bf16>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(bn_fwd_fast<float>, grid, dim3(256), 0, st, a);
 }
 
-int es_fast_bn_bwd_reduce(const es_view_t* v, es_dtype_t dt, const void* xp, const void* dyp, const es_norm_t* nm,
-                          const es_chain_t* ch, float* part, hipStream_t st) {
+int es_fast_norm_bwd_reduce(const es_view_t* v, int G, es_dtype_t dt, const void* xp, const void* dyp,
+                            const es_norm_t* nm, const es_chain_t* ch, float* part, hipStream_t st) {
   dim3 grid; int chunks;
-  fast_geometry(v, grid, chunks);
-  FastArgs a = mk(v, ch);
+  fast_geometry(v, G, grid, chunks);
+  FastArgs a = mk(v, ch, G);
   a.x = xp; a.dy = dyp; a.part = part;
   a.mean = nm->mean; a.invstd = nm->invstd; a.gamma = nm->gamma; a.beta = nm->beta;
   if (dt == ES_BF16) hipLaunchKernelGGL((bn_reduce_fast<bf16, 1>), grid, dim3(256), 0, st, a);
@@ -381,14 +424,16 @@ int es_fast_bn_bwd_reduce(const es_view_t* v, es_dtype_t dt, const void* xp, con
   return chunks;
 }
 
-void es_fast_bn_bwd_apply(const es_view_t* v, es_dtype_t dt, const void* xp, const void* dyp, void* dxp,
-                          const es_norm_t* nm, const es_chain_t* ch, const float* a1, const float* a2,
-                          float* dsum, hipStream_t st) {
+// returns the number of dsum partials written to part (z slices x chunks), 0 without dsum
+int es_fast_norm_bwd_apply(const es_view_t* v, int G, es_dtype_t dt, const void* xp, const void* dyp, void* dxp,
+                           const es_norm_t* nm, const es_chain_t* ch, const float* a1, const float* a2,
+                           float* dsum, float* part, hipStream_t st) {
   dim3 grid; int chunks;
-  fast_geometry(v, grid, chunks);
-  FastArgs a = mk(v, ch);
-  a.x = xp; a.dy = dyp; a.out = dxp; a.a1 = a1; a.a2 = a2; a.dsum = dsum;
+  fast_geometry(v, G, grid, chunks);
+  FastArgs a = mk(v, ch, G);
+  a.x = xp; a.dy = dyp; a.out = dxp; a.a1 = a1; a.a2 = a2; a.dsum = dsum; a.part = part;
   a.mean = nm->mean; a.invstd = nm->invstd; a.gamma = nm->gamma; a.beta = nm->beta;
   if (dt == ES_BF16) hipLaunchKernelGGL(bn_bwd_apply_fast<bf16>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(bn_bwd_apply_fast<float>, grid, dim3(256), 0, st, a);
+  return dsum ? (int)(grid.z * grid.y) : 0;
 }

@@ -129,8 +129,9 @@ class GeneratorNeutron(ExpertModule):
         dh2 = o["bn2"].bwd(ctx["h2"], ctx["s2"], ch[1], dy2, dgamma=g("fc2.1", "weight"),
                            dbeta=g("fc2.1", "bias"), dsum=g("fc2.0", "bias"))
         o["fc2"].wgrad(dh2, ctx["y1"], g("fc2.0", "weight"), None)
-        dy1 = o["fc2"].dgrad(dh2, ctx["y1"])
-        dh1 = o["bn1"].bwd(ctx["h1"], ctx["s1"], ch[0], dy1, dgamma=g("fc1.1", "weight"),
+        # fp32 dense output: lets the K = 21632 GEMM split K across workgroups (8 output tiles)
+        dy1 = o["fc2"].dgrad(dh2, ctx["y1"], dx_dtype=torch.float32)
+        dh1 = o["bn1"].bwd(ctx["h1"], ctx["s1"], ch[0], dy1, dx_dtype=cdt, dgamma=g("fc1.1", "weight"),
                            dbeta=g("fc1.1", "bias"), dsum=g("fc1.0", "bias"))
         o["fc1"].wgrad(dh1, ctx["x0"], g("fc1.0", "weight"), None)
 

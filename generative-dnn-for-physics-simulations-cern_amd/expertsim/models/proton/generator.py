@@ -103,8 +103,8 @@ class Generator(ExpertModule):
         copy_act(dy2n, Act(dy2.t, (B, 512, 18, 10), (FEAT, 180, 10, 1)))
         dh2 = o["ln2"].bwd(c["h2"], c["s2"], lr, dy2, dgamma=g("fc2.1"), dbeta=g("fc2.1", "bias"), dsum=g("fc2.0", "bias"))
         o["fc2"].wgrad(dh2, c["y1"], g("fc2.0"), None)
-        dy1 = o["fc2"].dgrad(dh2, c["y1"])
-        dh1 = o["ln1"].bwd(c["h1"], c["s1"], lr, dy1, dgamma=g("fc1.1"), dbeta=g("fc1.1", "bias"), dsum=g("fc1.0", "bias"))
+        dy1 = o["fc2"].dgrad(dh2, c["y1"], dx_dtype=torch.float32)   # fp32: split-K over K = 92160
+        dh1 = o["ln1"].bwd(c["h1"], c["s1"], lr, dy1, dx_dtype=cdt, dgamma=g("fc1.1"), dbeta=g("fc1.1", "bias"), dsum=g("fc1.0", "bias"))
         o["fc1"].wgrad(dh1, c["x0"], g("fc1.0"), None)
 
     def forward(self, noise, cond):

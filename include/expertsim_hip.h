@@ -76,6 +76,11 @@ typedef struct {
 
 /* y[n,k,p,q] = bias[k] + sum_{c,r,s} xu[n,c,p*stride-pad+r,q*stride-pad+s] * W[k,c,r,s]
  * wk: packed weights [K][R][S][C] of dtype dt (es_pack_conv_weight, mode 0). bias may be NULL. */
+/* Select the bf16 FWD/DGRAD main loop: 1 = LDS-DMA staged kernel where eligible (default),
+ * 0 = register-staged kernel.  Both accumulate in the same order (bit-identical results); the
+ * switch exists for A/B measurement and tests.  Returns the previous setting. */
+int es_conv_set_glds(int on);
+
 int es_conv2d_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x, const int64_t xs[4],
                   const void* wk, const float* bias, void* y, es_dtype_t ydt, const int64_t ys[4],
                   es_stream_t stream);

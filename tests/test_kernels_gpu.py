@@ -45,7 +45,10 @@ CONV_CASES = [
     (2, 256, 24, 24, 128, 3, 1, 0, (2, 2)),       # neutron G conv_layers.5
     (3, 128, 46, 46, 64, 2, 1, 0, None),          # neutron G conv_layers.9
     (3, 64, 45, 45, 1, 2, 1, 0, None),            # neutron G conv_layers.13
-    (2, 1, 44, 44, 32, 3, 1, 0, None),            # D / A first conv (Cin = 1)
+    (2, 1, 44, 44, 32, 3, 1, 0, None),            # D / A first conv (Cin = 1, direct kernels)
+    (24, 1, 44, 44, 32, 3, 1, 0, None),           # same, many wgrad blocks
+    (2, 1, 20, 18, 16, 3, 2, 1, None),            # Cin = 1 direct path, stride 2, pad 1, K = 16
+    (2, 64, 55, 29, 1, 2, 1, 1, None),            # proton G conv_layers.11 (Cout = 1, pad 1)
     (2, 32, 21, 21, 16, 3, 1, 0, None),           # D conv_layers.4
     (2, 1, 56, 30, 32, 5, 2, 1, None),            # proton A conv1 (stride 2, pad 1)
     (2, 32, 26, 13, 32, 5, 2, 2, None),           # proton A res conv1
@@ -93,6 +96,47 @@ def test_conv_fwd_dgrad_wgrad(case, dtype):
     assert rel(db.cpu(), b.grad) < tol
 
 
+GLDS_CASES = [
+    # bf16 shapes that take the LDS-DMA main loop (one tap x 64 channels per K-step)
+    (6, 128, 13, 13, 256, 3, 1, 0, (2, 2)),       # G conv_layers.0: fwd + folded dgrad
+    (3, 256, 24, 24, 128, 3, 1, 0, (2, 2)),       # G conv_layers.5
+    (4, 128, 46, 46, 64, 2, 1, 0, None),          # G conv_layers.9 (Ng = 64 tile)
+    (3, 128, 17, 15, 64, 3, 2, 1, None),          # stride 2 + padding
+    (2, 512, 18, 10, 256, 4, 1, 1, (2, 2)),       # proton G conv_layers.1 (pad 1, up x2)
+]
+
+
+@pytest.mark.parametrize("case", GLDS_CASES)
+def test_conv_glds_matches_register_path(case):
+    """The LDS-DMA kernel and the register-staged kernel accumulate in the same order: the bf16
+    fwd and dgrad outputs must be bit-identical (and both close to torch fp32)."""
+    hip = _hip()
+    from expertsim.layers import ConvOp, Upsample
+    N, Cin, H, W, Cout, k, st, pad, up = case
+    torch.manual_seed(5)
+    x = torch.randn(N, Cin, H, W)
+    w = torch.randn(Cout, Cin, k, k) / np.sqrt(Cin * k * k)
+    b = torch.randn(Cout)
+    upsample = Upsample((H, W), scale=up) if up else None
+    op = ConvOp(torch.nn.Parameter(w.to(DEV)), torch.nn.Parameter(b.to(DEV)), stride=st, pad=pad, upsample=upsample)
+    xa = to_act(x, torch.bfloat16)
+    outs = []
+    try:
+        for on in (1, 0):
+            hip.lib().es_conv_set_glds(on)
+            ya = op.fwd(xa, out_dtype=torch.bfloat16)
+            dxa = op.dgrad(to_act(torch.randn(ya.dims, generator=torch.Generator().manual_seed(9)), torch.bfloat16),
+                           xa, dx_dtype=torch.bfloat16)
+            outs.append((ya.t.clone(), dxa.t.clone()))
+    finally:
+        hip.lib().es_conv_set_glds(1)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    xu = F.interpolate(x, scale_factor=up, mode="nearest") if up else x
+    y = F.conv2d(xu, w, b, st, pad)
+    assert rel(outs[0][0].float().cpu().view(y.shape[0], y.shape[2], y.shape[3], -1).permute(0, 3, 1, 2), y) < 3e-2
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_linear_as_conv(dtype):
     _hip()
@@ -132,7 +176,8 @@ def _chain_ref(y, p, mask, act, dropout_first):
     return lre(y) * (mask.float() * scale)
 
 
-@pytest.mark.parametrize("kind", ["bn2d", "bn1d", "gn", "ln", "bn2d_hw4", "bn1d_c8", "bn2d_bf16"])
+@pytest.mark.parametrize("kind", ["bn2d", "bn1d", "gn", "ln", "bn2d_hw4", "bn1d_c8", "bn2d_bf16",
+                                  "gn_hw4", "gn_c16_bf16", "gn_generic"])
 @pytest.mark.parametrize("drop", [False, True])
 def test_norm_chain(kind, drop):
     hip = _hip()
@@ -147,9 +192,16 @@ def test_norm_chain(kind, drop):
     elif kind == "bn1d_c8":
         x = torch.randn(7, 304) * 2 + 0.5               # linear BN1d, C % 8 == 0 (fast path)
     elif kind == "gn":
-        x = torch.randn(3, 32, 6, 5) * 2 - 1
+        x = torch.randn(3, 32, 6, 5) * 2 - 1            # fast GN path, H*W % 4 != 0
+    elif kind == "gn_hw4":
+        x = torch.randn(5, 32, 12, 11) * 2 - 1          # fast GN path, H*W % 4 == 0, cg = 4
+    elif kind == "gn_c16_bf16":
+        x = torch.randn(4, 16, 7, 9) * 2 + 0.3          # fast GN path, bf16, cg = 2
+    elif kind == "gn_generic":
+        x = torch.randn(3, 12, 5, 5) * 2 - 1            # C % 8 != 0: generic segment reduction
     else:
         x = torch.randn(6, 300) * 2 + 0.5
+    groups = 4 if kind == "gn_generic" else 8
     gamma = torch.rand(x.shape[1]) + 0.5
     beta = torch.randn(x.shape[1])
     p, seed, stream = 0.2, 1234, 77
@@ -162,8 +214,8 @@ def test_norm_chain(kind, drop):
     if kind.startswith("bn"):
         z = F.batch_norm(xr, rm, rv, g_, b_, True, 0.1, 1e-5)
         nk = hip.NORM_BN
-    elif kind == "gn":
-        z = F.group_norm(xr, 8, g_, b_, 1e-5)
+    elif kind.startswith("gn"):
+        z = F.group_norm(xr, groups, g_, b_, 1e-5)
         nk = hip.NORM_GN
     else:
         z = F.layer_norm(xr, (x.shape[1],), g_, b_, 1e-5)
@@ -177,7 +229,7 @@ def test_norm_chain(kind, drop):
     dg = torch.zeros_like(gamma, device=DEV)
     dbt = torch.zeros_like(beta, device=DEV)
     rmd, rvd = torch.zeros(x.shape[1], device=DEV), torch.ones(x.shape[1], device=DEV)
-    op = NormOp(nk, gamma.to(DEV), beta.to(DEV), groups=8, running_mean=rmd, running_var=rvd)
+    op = NormOp(nk, gamma.to(DEV), beta.to(DEV), groups=groups, running_mean=rmd, running_var=rvd)
     d = hip.dropout_struct(p, seed, stream, enabled=drop)
     ch = hip.chain_struct(hip.ACT_LRELU, 0.1, d, dropout_first=True)
     ya, stats = op.fwd(xa, ch)

@@ -1,0 +1,80 @@
+"""Micro-benchmark of the norm kernels on the bench's tensor shapes (GPU; HIP-event timing).
+
+usage: python tools/mb_norm.py"""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "generative-dnn-for-physics-simulations-cern_amd"))
+
+from expertsim import hip  # noqa: E402
+from expertsim.layers import Act, NormOp  # noqa: E402
+
+
+def timed(fn, reps=20):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps * 1e3   # us
+
+
+def case(name, kind, groups, N, C, H, W, dtype, drop):
+    dev = "cuda"
+    x = Act.nhwc(N, C, H, W, dtype, dev)
+    x.t.normal_()
+    dy = Act.nhwc(N, C, H, W, dtype, dev)
+    dy.t.normal_()
+    g = torch.rand(C, device=dev) + 0.5
+    b = torch.randn(C, device=dev)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    op = NormOp(kind, g, b, groups=groups, running_mean=rm, running_var=rv)
+    d = hip.dropout_struct(0.2, 1234, 7, enabled=drop)
+    ch = hip.chain_struct(hip.ACT_LRELU, 0.1, d, dropout_first=True)
+    nbytes = x.t.numel() * x.t.element_size()
+    stats = op.stats(x)
+    y = x.like_nhwc(dtype)
+    dg, db, ds = torch.zeros(C, device=dev), torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    t_stats = timed(lambda: op.stats(x))
+    t_fwd = timed(lambda: op.fwd(x, ch))
+    t_bwd = timed(lambda: op.bwd(x, stats, ch, dy, dgamma=dg, dbeta=db, dsum=ds))
+    t_copy = timed(lambda: y.t.copy_(x.t))
+    print(f"{name:28s} {nbytes / 1e6:8.1f} MB  stats {t_stats:7.1f} us ({nbytes / t_stats / 1e6:5.2f} TB/s)  "
+          f"fwd(stats+apply) {t_fwd:7.1f} us  bwd(reduce+apply) {t_bwd:7.1f} us ({5 * nbytes / t_bwd / 1e6:5.2f} TB/s)"
+          f"  copy {t_copy:6.1f} us ({2 * nbytes / t_copy / 1e6:5.2f} TB/s)", flush=True)
+
+
+def pool_case(name, N, C, H, W, k, dtype):
+    from expertsim.layers import MaxPool
+    x = Act.nhwc(N, C, H, W, dtype, "cuda")
+    x.t.normal_()
+    mp = MaxPool(k)
+    y, idx = mp.fwd(x)
+    dy = y.like_nhwc(dtype)
+    dy.t.normal_()
+    t_f = timed(lambda: mp.fwd(x))
+    t_b = timed(lambda: mp.bwd(dy, idx, x.dims, dtype))
+    nbytes = x.t.numel() * x.t.element_size()
+    print(f"{name:28s} {nbytes / 1e6:8.1f} MB  maxpool fwd {t_f:7.1f} us  bwd {t_b:7.1f} us", flush=True)
+
+
+def main():
+    hip.lib()
+    pool_case("D pool1 fp32 42x42x32", 512, 32, 42, 42, 2, torch.float32)
+    pool_case("A pool1 bf16 42x42x32", 512, 32, 42, 42, (2, 2), torch.bfloat16)
+    bf, f32 = torch.bfloat16, torch.float32
+    case("G c5 BN bf16 46x46x128", hip.NORM_BN, 1, 512, 128, 46, 46, bf, True)
+    case("G c9 BN bf16 45x45x64", hip.NORM_BN, 1, 512, 64, 45, 45, bf, True)
+    case("D GN1 fp32 42x42x32", hip.NORM_GN, 8, 512, 32, 42, 42, f32, False)
+    case("D GN2 fp32 19x19x16", hip.NORM_GN, 8, 512, 16, 19, 19, f32, False)
+    case("BN fp32 42x42x32 (as BN)", hip.NORM_BN, 1, 512, 32, 42, 42, f32, False)
+
+
+if __name__ == "__main__":
+    main()
