@@ -744,6 +744,116 @@ int launch_tile(const ConvArgs& a, bool avec, bool bvec, hipStream_t st, int spl
   return ES_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// bf16 WGRAD with LDS-DMA staging.  GEMM: dW[m = k][ng = (r,s,c)] = sum over pixels of
+// dy[pix][k] * x[pix + (r,s)][c]; a K-step is 64 pixels.  Both operands are contiguous along the
+// GEMM row (k / c), so each pixel contributes one 256-byte segment per operand per tile
+// (K % 128 == 0 and C % 128 == 0: the 128 columns of a tile are one tap).
+//   * LDS image [pixel][row] (256-byte k-rows, lane-linear DMA, 4 pixels per wave instruction),
+//     read with ds_read_b64_tr_b16.  The 16-byte chunk index of k-row kr is XORed with
+//     2*(kr & 3) | 8*((kr >> 3) & 1): the 8 k-rows one 32-lane half reads land on 8 disjoint
+//     32-byte bank groups (conflict-free without padding, which a DMA image cannot have).
+//   * Split-K over blockIdx.z with fp32 atomics (as the register-staged WGRAD).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int swz_tr(int k) { return ((k & 3) << 1) | (((k >> 3) & 1) << 3); }
+// byte offset of element (k-row k, row) in a [64][128] bf16 image with 256-byte k-rows
+__device__ __forceinline__ int trs_off(int k, int row) {
+  return k * 256 + ((((row >> 3) ^ swz_tr(k)) << 4) | ((row & 7) << 1));
+}
+
+__device__ __forceinline__ bf16x8 trs_frag(const char* img, int k0, int r0) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int ka = k0 + 8 * g + q;
+  const char* p0 = img + trs_off(ka, r0 + 4 * p);
+  const char* p1 = img + trs_off(ka + 4, r0 + 4 * p);
+  short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)p0);
+  short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)p1);
+  short8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__global__ void __launch_bounds__(NTHREADS) conv_wgrad_glds_kernel(ConvArgs a) {
+  constexpr int BM = 128, BN = 128, RM = 4, RN = 4;
+  constexpr int IMG = 64 * 256, STAGE = 2 * IMG;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const es_conv_desc_t& d = a.d;
+
+  // XCD-aware order: blocks of one K split (same pixels) are consecutive on one XCD
+  const int mt = gridDim.x, ntl = gridDim.y, tiles = mt * ntl;
+  const int nwg = tiles * gridDim.z;
+  const int orig = blockIdx.x + (blockIdx.y + blockIdx.z * ntl) * mt;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int tile = wgid % tiles, split = wgid / tiles;
+  const int m0 = (tile % mt) * BM, n0 = (tile / mt) * BN;
+  const int kbeg = split * a.k_per_split;
+  const int kend = min(a.Kd, kbeg + a.k_per_split);
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm0 = (wid >> 1) * (BM / 2), wn0 = (wid & 1) * (BN / 2);
+  const int lrow = lane >> 4, pc = lane & 15;          // pixel row within a piece, physical chunk
+  // the tile's tap and channel offset (C % 128 == 0: one tap per tile)
+  const int rs = fdiv(n0, a.fC), cb = n0 - rs * d.C;
+  const int tr = fdiv(rs, a.fS), ts = rs - tr * d.S;
+  const bf16* dy = (const bf16*)a.a_src;
+  const bf16* x = (const bf16*)a.b_src;
+  const char* zero = g_zero_row;
+
+  auto issue = [&](int k0, char* stage) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int kr = (wid * 4 + j) * 4 + lrow;          // pixel row of the K-step, 0..63
+      const int lc = pc ^ swz_tr(kr);
+      const int pix = k0 + kr;
+      const void* sa = zero;
+      const void* sb = zero;
+      if (pix < kend) {
+        const int np = fdiv(pix, a.fQ), qq = pix - np * d.Q;
+        const int n = fdiv(np, a.fP), pp = np - n * d.P;
+        sa = dy + (int64_t)n * a.as[0] + (int64_t)pp * a.as[2] + (int64_t)qq * a.as[3] + m0 + lc * 8;
+        const int hu = pp * d.stride - d.pad + tr, wu = qq * d.stride - d.pad + ts;
+        if (hu >= 0 && hu < d.Hu && wu >= 0 && wu < d.Wu)
+          sb = x + (int64_t)n * a.bs[0] + (int64_t)(d.up_h > 0 ? fdiv(hu, a.fUh) : hu) * a.bs[2] +
+               (int64_t)(d.up_w > 0 ? fdiv(wu, a.fUw) : wu) * a.bs[3] + cb + lc * 8;
+      }
+      glds16(sa, stage + (wid * 4 + j) * 1024);
+      glds16(sb, stage + IMG + (wid * 4 + j) * 1024);
+    }
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (kbeg < kend) {
+    const int nk = (kend - kbeg + 63) / 64;
+    issue(kbeg, smem);
+    for (int t = 0; t < nk; ++t) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const char* cur = smem + (t & 1) * STAGE;
+      if (t + 1 < nk) issue(kbeg + (t + 1) * 64, smem + ((t + 1) & 1) * STAGE);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[RM], bfr[RN];
+#pragma unroll
+        for (int i = 0; i < RM; ++i) af[i] = trs_frag(cur, kk * 32, wm0 + i * 16);
+#pragma unroll
+        for (int j = 0; j < RN; ++j) bfr[j] = trs_frag(cur + IMG, kk * 32, wn0 + j * 16);
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  conv_epilogue<bf16, MODE_WGRAD, BM, BN>(a, acc, m0, n0, wm0, wn0);
+}
+
 template <int MODE, int BM, int BN>
 int launch_glds(ConvArgs& a, hipStream_t st) {
   const int mt = (a.M + BM - 1) / BM;
@@ -761,7 +871,10 @@ int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
   if constexpr (sizeof(T) == 2 && MODE != MODE_WGRAD) {
     // LDS-DMA path: one tap x 64 channels per K-step, big enough to fill the chip without split-K
     const int nch = MODE == MODE_FWD ? a.d.C : a.d.K;
-    if (avec && bvec && nch % 64 == 0 && a.d.stride <= 2 && a.d.hmap == nullptr && a.M >= 128 && !g_no_glds) {
+    const int tiles = ((a.M + 127) / 128) * ((a.Ng + 127) / 128);
+    const bool splitk_better = a.dense_f32_out && tiles < 256 && a.Kd / 64 >= 16;   // see below
+    if (avec && bvec && nch % 64 == 0 && a.d.stride <= 2 && a.d.hmap == nullptr && a.M >= 128 && !splitk_better &&
+        !g_no_glds) {
       if (a.Ng > 64) return launch_glds<MODE, 128, 128>(a, st);
       return launch_glds<MODE, 128, 64>(a, st);
     }
@@ -769,6 +882,22 @@ int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
   // tile choice: 128x128 for big GEMMs, 64x64 when either side is small
   const bool big = a.M >= 128 && a.Ng >= 96;
   const int BM = big ? 128 : 64, BN = big ? 128 : 64;
+  if constexpr (sizeof(T) == 2 && MODE == MODE_WGRAD) {
+    if (avec && bvec && a.d.K % 128 == 0 && a.d.C % 128 == 0 && a.d.stride <= 2 && a.d.hmap == nullptr &&
+        !g_no_glds) {
+      const int t128 = (a.M / 128) * (a.Ng / 128);
+      const int ks = (a.Kd + 63) / 64;
+      int want = (2048 + t128 - 1) / t128;
+      want = max(1, min(want, ks / 4 > 0 ? ks / 4 : 1));
+      const int per = ((ks + want - 1) / want) * 64;
+      a.k_per_split = per;
+      a.splitk = 0;
+      dim3 grid(a.M / 128, a.Ng / 128, (a.Kd + per - 1) / per);
+      hipLaunchKernelGGL(conv_wgrad_glds_kernel, grid, dim3(NTHREADS), 2 * 2 * 64 * 256, st, a);
+      ES_CHECK_LAUNCH();
+      return ES_OK;
+    }
+  }
   int splits = 1;
   const int tiles = ((a.M + BM - 1) / BM) * ((a.Ng + BN - 1) / BN);
   const int ksteps = (a.Kd + BK - 1) / BK;

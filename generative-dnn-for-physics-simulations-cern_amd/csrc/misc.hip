@@ -111,6 +111,51 @@ __global__ void maxpool_bwd_kernel(View dy, const void* dyp, int bf, const uint8
   }
 }
 
+// Non-overlapping windows (kernel == stride) on dense NHWC views: every input position has at most
+// one window, so a thread owns VN channels of one input pixel, reads the window's gradient and
+// argmax bytes as vectors and writes the VN gradients with one 16-byte store.
+template <typename T>
+__global__ void __launch_bounds__(256) maxpool_bwd_nhwc(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                       int N, int C, int H, int W, int P, int Q, int kh, int kw,
+                                                       T* __restrict__ dx, float beta) {
+  constexpr int VN = 16 / sizeof(T);
+  const int cv = C / VN;
+  const uint32_t total = (uint32_t)N * H * W * cv;
+  for (uint32_t e = blockIdx.x * 256u + threadIdx.x; e < total; e += gridDim.x * 256u) {
+    const uint32_t pix = e / cv;
+    const int c0 = (int)(e - pix * cv) * VN;
+    const uint32_t nh = pix / W;
+    const int w = (int)(pix - nh * W);
+    const int n = (int)(nh / H), h = (int)(nh - (uint32_t)n * H);
+    const int oh = h / kh, ow = w / kw;
+    float g[VN];
+#pragma unroll
+    for (int v = 0; v < VN; ++v) g[v] = 0.f;
+    if (oh < P && ow < Q) {
+      const int64_t ye = (((int64_t)n * P + oh) * Q + ow) * C + c0;
+      const int want = (h - oh * kh) * kw + (w - ow * kw);
+      T gv[VN];
+      uint8_t iv[VN];
+      *(uint4*)gv = *(const uint4*)(dy + ye);
+      if constexpr (VN == 8) *(uint2*)iv = *(const uint2*)(idx + ye);
+      else *(uint32_t*)iv = *(const uint32_t*)(idx + ye);
+#pragma unroll
+      for (int v = 0; v < VN; ++v) g[v] = iv[v] == want ? to_f(gv[v]) : 0.f;
+    }
+    T* o = dx + (int64_t)pix * C + c0;
+    T ov[VN];
+    if (beta != 0.f) *(uint4*)ov = *(const uint4*)o;
+#pragma unroll
+    for (int v = 0; v < VN; ++v) ov[v] = from_f<T>(beta != 0.f ? g[v] + beta * to_f(ov[v]) : g[v]);
+    *(uint4*)o = *(const uint4*)ov;
+  }
+}
+
+bool dense_nhwc(const es_view_t* v) {
+  const int64_t C = v->c;
+  return v->s[1] == 1 && v->s[3] == C && v->s[2] == (int64_t)v->w * C && v->s[0] == (int64_t)v->h * v->w * C;
+}
+
 // ----------------------------------------------------------------------------- upsample bwd
 __global__ void upsample_bwd_kernel(View du, const void* dup, int ubf, const int32_t* hs, const int32_t* hc,
                                     const int32_t* ws, const int32_t* wc, View dx, void* dxp, int xbf, float beta) {
@@ -301,6 +346,20 @@ extern "C" int es_maxpool_bwd(const es_view_t* dy, es_dtype_t dt, const void* dy
                               int kw, int sh, int sw, const es_view_t* dx, void* dxp, float beta,
                               es_stream_t stream) {
   const int64_t total = (int64_t)dx->n * dx->c * dx->h * dx->w;
+  const int vn = dt == ES_BF16 ? 8 : 4;
+  if (kh == sh && kw == sw && dense_nhwc(dy) && dense_nhwc(dx) && dx->c % vn == 0 && dx->c > 1 &&
+      total < (1ll << 31)) {
+    const int64_t items = total / vn;
+    const unsigned grid = (unsigned)std::min<int64_t>((items + 255) / 256, 16384);
+    if (dt == ES_BF16)
+      hipLaunchKernelGGL(maxpool_bwd_nhwc<bf16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16*)dyp, idx,
+                         dx->n, dx->c, dx->h, dx->w, dy->h, dy->w, kh, kw, (bf16*)dxp, beta);
+    else
+      hipLaunchKernelGGL(maxpool_bwd_nhwc<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)dyp,
+                         idx, dx->n, dx->c, dx->h, dx->w, dy->h, dy->w, kh, kw, (float*)dxp, beta);
+    ES_CHECK_LAUNCH();
+    return ES_OK;
+  }
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
                      mkview(dy), dyp, dt == ES_BF16, idx, kh, kw, sh, sw, mkview(dx), dxp, beta);
   ES_CHECK_LAUNCH();

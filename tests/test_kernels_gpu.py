@@ -102,6 +102,7 @@ GLDS_CASES = [
     (3, 256, 24, 24, 128, 3, 1, 0, (2, 2)),       # G conv_layers.5
     (4, 128, 46, 46, 64, 2, 1, 0, None),          # G conv_layers.9 (Ng = 64 tile)
     (3, 128, 17, 15, 64, 3, 2, 1, None),          # stride 2 + padding
+    (3, 128, 17, 15, 128, 3, 2, 1, None),         # stride 2 + padding, WGRAD on the DMA path
     (2, 512, 18, 10, 256, 4, 1, 1, (2, 2)),       # proton G conv_layers.1 (pad 1, up x2)
 ]
 
@@ -121,17 +122,28 @@ def test_conv_glds_matches_register_path(case):
     op = ConvOp(torch.nn.Parameter(w.to(DEV)), torch.nn.Parameter(b.to(DEV)), stride=st, pad=pad, upsample=upsample)
     xa = to_act(x, torch.bfloat16)
     outs = []
+    gy = None
     try:
         for on in (1, 0):
             hip.lib().es_conv_set_glds(on)
             ya = op.fwd(xa, out_dtype=torch.bfloat16)
-            dxa = op.dgrad(to_act(torch.randn(ya.dims, generator=torch.Generator().manual_seed(9)), torch.bfloat16),
-                           xa, dx_dtype=torch.bfloat16)
-            outs.append((ya.t.clone(), dxa.t.clone()))
+            if gy is None:
+                gy = torch.randn(ya.dims, generator=torch.Generator().manual_seed(9))
+            gya = to_act(gy, torch.bfloat16)
+            dxa = op.dgrad(gya, xa, dx_dtype=torch.bfloat16)
+            dw = torch.zeros(Cout, Cin, k, k, device=DEV)
+            op.wgrad(gya, xa, dw, None, beta=1.0)
+            outs.append((ya.t.clone(), dxa.t.clone(), dw.cpu()))
     finally:
         hip.lib().es_conv_set_glds(1)
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+    # WGRAD: same per-split sums; only the order of the fp32 atomics across K splits differs
+    assert rel(outs[0][2], outs[1][2]) < 1e-5
+    wr = w.clone().requires_grad_(True)
+    xu_ = F.interpolate(x, scale_factor=up, mode="nearest") if up else x
+    F.conv2d(xu_, wr, b, st, pad).backward(gy.to(torch.bfloat16).float())
+    assert rel(outs[0][2], wr.grad) < 3e-2
     xu = F.interpolate(x, scale_factor=up, mode="nearest") if up else x
     y = F.conv2d(xu, w, b, st, pad)
     assert rel(outs[0][0].float().cpu().view(y.shape[0], y.shape[2], y.shape[3], -1).permute(0, 3, 1, 2), y) < 3e-2
