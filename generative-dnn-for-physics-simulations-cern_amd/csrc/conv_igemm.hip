@@ -879,8 +879,11 @@ int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
       return launch_glds<MODE, 128, 64>(a, st);
     }
   }
-  // tile choice: 128x128 for big GEMMs, 64x64 when either side is small
-  const bool big = a.M >= 128 && a.Ng >= 96;
+  // tile choice: 128x128 for big GEMMs, 64x64 when either side is small, or when the output is
+  // split over K anyway (few tiles, long K: more, smaller workgroups)
+  const int tiles128 = ((a.M + 127) / 128) * ((a.Ng + 127) / 128);
+  const bool splitk_case = MODE != MODE_WGRAD && a.dense_f32_out && tiles128 < 256 && (a.Kd + BK - 1) / BK >= 16;
+  const bool big = a.M >= 128 && a.Ng >= 96 && !splitk_case;
   const int BM = big ? 128 : 64, BN = big ? 128 : 64;
   if constexpr (sizeof(T) == 2 && MODE == MODE_WGRAD) {
     if (avec && bvec && a.d.K % 128 == 0 && a.d.C % 128 == 0 && a.d.stride <= 2 && a.d.hmap == nullptr &&
@@ -909,9 +912,10 @@ int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
     const int per = ((ksteps + want - 1) / want) * BK;
     a.k_per_split = per;
     splits = (a.Kd + per - 1) / per;
-  } else if (a.dense_f32_out && tiles < 256 && ksteps >= 16) {
-    // few output tiles and a long K (the linears at batch 512): split K over ~512 workgroups
-    int want = min((512 + tiles - 1) / tiles, ksteps / 8);
+  } else if (splitk_case) {
+    // few output tiles and a long K (the linears at batch 512): split K over ~1024 workgroups,
+    // at least 4 K-steps each
+    int want = min((1024 + tiles - 1) / tiles, ksteps / 4);
     if (want > 1) {
       const int per = ((ksteps + want - 1) / want) * BK;
       a.k_per_split = per;
@@ -1044,10 +1048,11 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, int K, int C, in
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     // i indexes the OUTPUT layout
     int k, c, r, s;
+    const uint32_t i32 = (uint32_t)i;   // n < 2^31 (host-checked): 32-bit index math
     if (mode == 0) {  // [K][R][S][C]
-      c = i % C; int64_t t = i / C; s = t % S; t /= S; r = t % R; k = t / R;
+      uint32_t t = i32 / C; c = i32 - t * C; s = t % S; t /= S; r = t % R; k = t / R;
     } else {          // [C][R][S][K]
-      k = i % K; int64_t t = i / K; s = t % S; t /= S; r = t % R; c = t / R;
+      uint32_t t = i32 / K; k = i32 - t * K; s = t % S; t /= S; r = t % R; c = t / R;
     }
     const int cs = col_perm ? col_perm[c] : c;
     out[i] = from_f<T>(w[(((int64_t)k * C + cs) * R + r) * S + s] * sc);
@@ -1059,7 +1064,9 @@ __global__ void unpack_grad_kernel(const float* __restrict__ dw, int K, int C, i
   const int64_t n = (int64_t)K * C * R * S;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     // i indexes dw layout [K][R][S][C]
-    const int c = i % C; int64_t t = i / C; const int s = t % S; t /= S; const int r = t % R; const int k = t / R;
+    uint32_t t = (uint32_t)i / C;
+    const int c = (int)((uint32_t)i - t * C);
+    const int s = t % S; t /= S; const int r = t % R; const int k = t / R;
     const int cs = col_perm ? col_perm[c] : c;
     float* g = grad + (((int64_t)k * C + cs) * R + r) * S + s;
     *g = (beta != 0.f ? beta * *g : 0.f) + dw[i];
@@ -1072,6 +1079,7 @@ extern "C" int es_pack_conv_weight(const float* w, int K, int C, int R, int S, i
                                    es_dtype_t dt, es_stream_t stream) {
   ES_CHECK_ARG(mode == 0 || mode == 1, "pack: bad mode");
   const int64_t n = (int64_t)K * C * R * S;
+  ES_CHECK_ARG(n < (1ll << 31), "pack: weight too large");
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
   if (dt == ES_F32)
     hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
@@ -1087,6 +1095,7 @@ extern "C" int es_unpack_conv_grad(const float* dw, int K, int C, int R, int S,
                                    const int32_t* col_perm, float* grad, float beta,
                                    es_stream_t stream) {
   const int64_t n = (int64_t)K * C * R * S;
+  ES_CHECK_ARG(n < (1ll << 31), "unpack: weight too large");
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(unpack_grad_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, dw, K, C,
                      R, S, col_perm, grad, beta);

@@ -267,6 +267,83 @@ __global__ void __launch_bounds__(1024) sn_power_kernel(const float* w, int h, i
   if (threadIdx.x == 0) sigma[0] = d;
 }
 
+// ---- multi-block power iteration for the large reshaped weights (discriminator fc1: 128 x 1305)
+// t = W^T u : block = 64 columns x 4 row groups, LDS reduction over the row groups
+__global__ void __launch_bounds__(256) sn_wtu_kernel(const float* __restrict__ w, int h, int wd,
+                                                     const float* __restrict__ u, float* __restrict__ vt) {
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + cl;
+  float t = 0.f;
+  if (j < wd)
+    for (int i = rg; i < h; i += 4) t += w[(int64_t)i * wd + j] * u[i];
+  __shared__ float sh[4][64];
+  sh[rg][cl] = t;
+  __syncthreads();
+  if (rg == 0 && j < wd) vt[j] = sh[0][cl] + sh[1][cl] + sh[2][cl] + sh[3][cl];
+}
+// wv = W (x * scale), one wave per row; scale = 1/||x|| when `normalize` (x = the new v, written
+// back normalised by block 0), else 1 (x = the stored v)
+__global__ void __launch_bounds__(256) sn_wv_kernel(const float* __restrict__ w, int h, int wd, const float* x,
+                                                    int normalize, float* v_out, float* __restrict__ wv) {
+  __shared__ float sh[8];
+  float sc = 1.f;
+  if (normalize) {
+    float ss = 0.f;
+    for (int j = threadIdx.x; j < wd; j += 256) ss += x[j] * x[j];
+    sc = 1.f / fmaxf(sqrtf(block_sum(ss, sh)), 1e-12f);
+    if (blockIdx.x == 0)
+      for (int j = threadIdx.x; j < wd; j += 256) v_out[j] = x[j] * sc;
+  }
+  const int lane = threadIdx.x & 63, i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= h) return;
+  float t = 0.f;
+  for (int j = lane; j < wd; j += 64) t += w[(int64_t)i * wd + j] * (x[j] * sc);
+  t = wave_sum(t);
+  if (lane == 0) wv[i] = t;
+}
+// u = wv / ||wv|| (update), sigma = u . wv
+__global__ void __launch_bounds__(256) sn_final_kernel(int h, const float* wv, float* u, int update, float* sigma) {
+  __shared__ float sh[8];
+  if (update) {
+    float ss = 0.f;
+    for (int i = threadIdx.x; i < h; i += 256) ss += wv[i] * wv[i];
+    const float nu = fmaxf(sqrtf(block_sum(ss, sh)), 1e-12f);
+    for (int i = threadIdx.x; i < h; i += 256) u[i] = wv[i] / nu;
+    __syncthreads();
+  }
+  float d = 0.f;
+  for (int i = threadIdx.x; i < h; i += 256) d += u[i] * wv[i];
+  d = block_sum(d, sh);
+  if (threadIdx.x == 0) sigma[0] = d;
+}
+
+// ---- multi-block backward: block partials of <G, W> (pass 1), then the elementwise update with
+// every block re-reducing the (<= 256) partials (pass 2)
+__global__ void __launch_bounds__(256) sn_dot_kernel(const float* __restrict__ g, const float* __restrict__ w,
+                                                     int n, float* part) {
+  __shared__ float sh[8];
+  float d = 0.f;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) d += g[i] * w[i];
+  d = block_sum(d, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = d;
+}
+__global__ void __launch_bounds__(256) sn_bwd_apply_kernel(const float* __restrict__ g, int h, int wd,
+                                                           const float* u, const float* v, const float* sigma,
+                                                           const float* part, int nparts, float* dw, float beta) {
+  __shared__ float sh[8];
+  float d = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += 256) d += part[i];
+  d = block_sum(d, sh);
+  const float s = sigma[0];
+  const float c = d / (s * s);
+  const int n = h * wd;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int r = i / wd, col = i - r * wd;
+    const float val = g[i] / s - c * u[r] * v[col];
+    dw[i] = (beta != 0.f ? beta * dw[i] : 0.f) + val;
+  }
+}
+
 // dW_orig = beta*dW + G/s - (<G,W>/s^2) u v^T
 __global__ void __launch_bounds__(1024) sn_bwd_kernel(const float* w, const float* g, int h, int wd,
                                                       const float* u, const float* v, const float* sigma,
@@ -419,16 +496,35 @@ extern "C" int es_gather_rows(const float* src, int64_t src_ld, const int32_t* i
 extern "C" int es_sn_power_iter(const float* w, int h, int wd, float* u, float* v, float* sigma, int update,
                                 es_stream_t stream) {
   // scratch lives after sigma[0] in the caller's buffer: sigma must have 1 + h + wd floats
-  hipLaunchKernelGGL(sn_power_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, w, h, wd, u, v, sigma, update,
-                     sigma + 1);
+  hipStream_t st = (hipStream_t)stream;
+  if ((int64_t)h * wd >= 16384) {   // large weights: spread the two mat-vecs over the chip
+    float* wv = sigma + 1;
+    float* vt = sigma + 1 + h;
+    if (update) hipLaunchKernelGGL(sn_wtu_kernel, dim3((wd + 63) / 64), dim3(256), 0, st, w, h, wd, u, vt);
+    hipLaunchKernelGGL(sn_wv_kernel, dim3((h + 3) / 4), dim3(256), 0, st, w, h, wd, update ? (const float*)vt : v,
+                       update, v, wv);
+    hipLaunchKernelGGL(sn_final_kernel, dim3(1), dim3(256), 0, st, h, (const float*)wv, u, update, sigma);
+  } else {
+    hipLaunchKernelGGL(sn_power_kernel, dim3(1), dim3(1024), 0, st, w, h, wd, u, v, sigma, update, sigma + 1);
+  }
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
 
 extern "C" int es_sn_bwd(const float* w, const float* g, int h, int wd, const float* u, const float* v,
                          const float* sigma, float* dw_orig, float beta, es_stream_t stream) {
-  hipLaunchKernelGGL(sn_bwd_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, w, g, h, wd, u, v, sigma,
-                     dw_orig, beta);
+  const int64_t n = (int64_t)h * wd;
+  if (n >= 16384 && h + wd >= 256) {
+    // partials go to the power iteration's scratch (sigma[1 .. h+wd]), free outside es_sn_power_iter
+    float* part = const_cast<float*>(sigma) + 1;
+    const int nb = (int)std::min<int64_t>(256, (n + 1023) / 1024);
+    hipLaunchKernelGGL(sn_dot_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, g, w, (int)n, part);
+    hipLaunchKernelGGL(sn_bwd_apply_kernel, dim3((unsigned)std::min<int64_t>(1024, (n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, g, h, wd, u, v, sigma, (const float*)part, nb, dw_orig, beta);
+  } else {
+    hipLaunchKernelGGL(sn_bwd_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, w, g, h, wd, u, v, sigma,
+                       dw_orig, beta);
+  }
   ES_CHECK_LAUNCH();
   return ES_OK;
 }

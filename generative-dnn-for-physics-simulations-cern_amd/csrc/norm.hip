@@ -37,9 +37,13 @@ static int fast_kind(const es_view_t* v, int kind, int groups) {
   return -1;
 }
 
+// same logical shape and the same element addresses (strides of size-1 dims are irrelevant)
 static bool same_view(const es_view_t* a, const es_view_t* b) {
-  return a->n == b->n && a->c == b->c && a->h == b->h && a->w == b->w && a->s[0] == b->s[0] &&
-         a->s[1] == b->s[1] && a->s[2] == b->s[2] && a->s[3] == b->s[3];
+  if (a->n != b->n || a->c != b->c || a->h != b->h || a->w != b->w) return false;
+  const int dims[4] = {a->n, a->c, a->h, a->w};
+  for (int i = 0; i < 4; ++i)
+    if (dims[i] > 1 && a->s[i] != b->s[i]) return false;
+  return true;
 }
 
 namespace {
@@ -387,6 +391,20 @@ void colred_geometry(const View& v, int& cblocks, int& chunks, int64_t& rows, in
   chunks = (int)((rows + per - 1) / per);
 }
 
+// single-channel sum: block partials into the s1 slot of [chunk][3][1]
+__global__ void __launch_bounds__(256) sum1_kernel(BwdIn b, int rows, float* part) {
+  const View& v = b.x;
+  __shared__ float sh[8];
+  float s = 0.f;
+  for (int r = blockIdx.x * 256 + threadIdx.x; r < rows; r += gridDim.x * 256) {
+    const uint32_t t = (uint32_t)r / (uint32_t)v.w;
+    const int w = r - (int)t * v.w, h = t % (uint32_t)v.h, n = t / (uint32_t)v.h;
+    s += ldf(b.xp, b.xbf, v.off(n, 0, h, w));
+  }
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) part[blockIdx.x * 3 + 1] = s;
+}
+
 // ============================================================================ segred
 // one block per stats group; RED_STATS writes mean/invstd, RED_BWD writes A1/A2 (means over group)
 template <int RED>
@@ -715,6 +733,15 @@ extern "C" int es_channel_sum(const es_view_t* x, es_dtype_t xdt, const void* xp
   BwdIn b = mk_bwdin(x, xdt, xp, nullptr, nullptr);
   int cb, chunks; int64_t rows, per;
   colred_geometry(b.x, cb, chunks, rows, per);
+  if (x->c == 1 && rows < (1ll << 31)) {
+    // one channel (bias of a 1-output conv): every thread of the colred geometry's chunks sums
+    // rows, instead of 63 of every 64 lanes idling
+    const int nb = std::min<int>(chunks, (int)((rows + 255) / 256));
+    hipLaunchKernelGGL(sum1_kernel, dim3(nb), dim3(256), 0, st, b, (int)rows, (float*)ws);
+    hipLaunchKernelGGL(sum_finalize_kernel, dim3(1), dim3(256), 0, st, (const float*)ws, nb, 1, out, beta);
+    ES_CHECK_LAUNCH();
+    return ES_OK;
+  }
   hipLaunchKernelGGL(colred_kernel<RED_SUM>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, (float*)ws);
   if (chunks > 32)
     hipLaunchKernelGGL(sums_finalize_block_kernel, dim3(x->c), dim3(256), 0, st, (const float*)ws, chunks, x->c,

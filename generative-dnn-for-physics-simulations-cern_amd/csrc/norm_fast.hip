@@ -92,6 +92,30 @@ __device__ __forceinline__ void keep_bits(const FastArgs& a, int r0, int c0, uin
                     ((uint32_t)((w.z >> 8) < thr) << 2) | ((uint32_t)((w.w >> 8) < thr) << 3)) << (4 * h);
       }
     }
+  } else if (r0 - (r0 / a.HW) * a.HW + 3 < a.HW && r0 + 3 < a.rows) {
+    // the 4 rows lie in one sample: their logical indices i0..i0+3 are consecutive and span at
+    // most two Philox counters per channel (2 calls instead of 4)
+    const int n = r0 / a.HW, hw0 = r0 - n * a.HW;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint64_t i0 = ((uint64_t)n * a.C + c0 + k) * (uint64_t)a.HW + hw0;
+      const uint64_t q = i0 >> 2;
+      const int off = (int)(i0 & 3);
+      const u32x4 w = philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), a.drop.stream, 0u, k0, k1);
+      uint32_t m = (uint32_t)((w.x >> 8) < thr) | ((uint32_t)((w.y >> 8) < thr) << 1) |
+                   ((uint32_t)((w.z >> 8) < thr) << 2) | ((uint32_t)((w.w >> 8) < thr) << 3);
+      if (off) {
+        const uint64_t q1 = q + 1;
+        const u32x4 v = philox4x32_10((uint32_t)q1, (uint32_t)(q1 >> 32), a.drop.stream, 0u, k0, k1);
+        m |= ((uint32_t)((v.x >> 8) < thr) << 4) | ((uint32_t)((v.y >> 8) < thr) << 5) |
+             ((uint32_t)((v.z >> 8) < thr) << 6) | ((uint32_t)((v.w >> 8) < thr) << 7);
+      }
+      m >>= off;
+      keep[0] |= (m & 1u) << k;
+      keep[1] |= ((m >> 1) & 1u) << k;
+      keep[2] |= ((m >> 2) & 1u) << k;
+      keep[3] |= ((m >> 3) & 1u) << k;
+    }
   } else {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -354,7 +378,8 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_fast(FastArgs a) {
 // Returns true when the fast path applies to these views (dense NHWC, same dtype, C % 8 == 0).
 bool es_fast_dense_nhwc(const es_view_t* v) {
   const int64_t C = v->c, W = v->w, H = v->h;
-  return v->c % 8 == 0 && v->s[1] == 1 && v->s[3] == C && v->s[2] == W * C && v->s[0] == H * W * C;
+  return v->c % 8 == 0 && v->s[1] == 1 && (W == 1 || v->s[3] == C) && (H == 1 || v->s[2] == W * C) &&
+         (v->n == 1 || v->s[0] == H * W * C);
 }
 
 // G = 0: BatchNorm (one z slice over all rows); G > 0: GroupNorm (z = sample)

@@ -199,7 +199,8 @@ int es_gather_rows(const float* src, int64_t src_ld, const int32_t* idx, int row
  * ---------------------------------------------------------------------------------------- */
 int es_sn_power_iter(const float* w, int h, int wd, float* u, float* v, float* sigma, int update,
                      es_stream_t stream);
-/* dW_orig = beta*dW_orig + G/sigma - (<G, W>/sigma^2) u v^T   (G = grad of W/sigma) */
+/* dW_orig = beta*dW_orig + G/sigma - (<G, W>/sigma^2) u v^T   (G = grad of W/sigma).
+ * sigma is the buffer es_sn_power_iter wrote (1 + h + wd floats); its tail is used as scratch. */
 int es_sn_bwd(const float* w, const float* g, int h, int wd, const float* u, const float* v,
               const float* sigma, float* dw_orig, float beta, es_stream_t stream);
 
