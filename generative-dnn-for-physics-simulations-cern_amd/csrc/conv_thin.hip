@@ -12,6 +12,7 @@
 // [C][R][S][K]) in the compute dtype, fp32 accumulation, wgrad accumulated into fp32 [K][R*S*C]
 // with atomics.  Stride 1 (Cin == 1 also stride 2), any zero padding, no upsample.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 
@@ -328,6 +329,53 @@ __global__ void __launch_bounds__(NT) k1_wgrad(Thin t, int LP) {
     atomicAdd(&dw[i], red[0][i] + red[1][i] + red[2][i] + red[3][i]);
 }
 
+// ============================================================ small fp32 convs (few channels)
+// The discriminator's conv_layers.4 (32 -> 16, 3x3, fp32: neutron/discriminator.py:16): as a GEMM
+// its N = 16 fills a quarter of every tile.  Direct forward: one thread per output pixel with KO
+// accumulators, weights in LDS.  (A direct dgrad measured slower than the GEMM; not used.)
+template <int KO>
+__global__ void __launch_bounds__(NT) small_fwd(Thin t) {
+  const es_conv_desc_t& d = t.d;
+  const int RS = d.R * d.S, C = d.C;
+  __shared__ float wf[9 * 64 * KO];                       // [rs][c][k]
+  __shared__ float bs[KO];
+  for (int i = threadIdx.x; i < KO * RS * C; i += NT) {   // packed wk = [k][rs][c]
+    const int k = i / (RS * C), rc = i - k * (RS * C);
+    wf[rc * KO + k] = ((const float*)t.w)[i];
+  }
+  if (threadIdx.x < KO) bs[threadIdx.x] = t.bias ? t.bias[threadIdx.x] : 0.f;
+  __syncthreads();
+  const int m = blockIdx.x * NT + threadIdx.x;
+  if (m >= t.M) return;
+  int n, p, q;
+  pix3(m, d.P, d.Q, n, p, q);
+  float acc[KO];
+#pragma unroll
+  for (int k = 0; k < KO; ++k) acc[k] = bs[k];
+  const float* x = (const float*)t.a + n * t.as[0];
+  for (int r = 0; r < d.R; ++r) {
+    const int hu = p - d.pad + r;
+    if (hu < 0 || hu >= d.H) continue;
+    for (int s_ = 0; s_ < d.S; ++s_) {
+      const int wu = q - d.pad + s_;
+      if (wu < 0 || wu >= d.W) continue;
+      const float* px = x + hu * t.as[2] + wu * t.as[3];
+      const float* wr = wf + (r * d.S + s_) * C * KO;
+      for (int c = 0; c < C; c += 4) {
+        const float4 xv = *(const float4*)(px + c);
+        const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int k = 0; k < KO; ++k) acc[k] += xs[e] * wr[(c + e) * KO + k];
+      }
+    }
+  }
+  float* y = (float*)t.out + n * t.os[0] + p * t.os[2] + q * t.os[3];
+#pragma unroll
+  for (int k = 0; k < KO; k += 4) *(float4*)(y + k) = make_float4(acc[k], acc[k + 1], acc[k + 2], acc[k + 3]);
+}
+
 bool plain(const es_conv_desc_t* d) {
   return d->hmap == nullptr && d->up_h <= 0 && d->Hu == d->H && d->Wu == d->W;
 }
@@ -393,6 +441,18 @@ void launch_wgrad(const Thin& t, int rs, int LP, hipStream_t st) {
 
 }  // namespace
 
+// fp32, stride 1, no upsample, K in {4, 8, 16}, C % 8 == 0, C <= 64, R*S <= 9, dense NHWC rows
+bool small_ok(const es_conv_desc_t* d, es_dtype_t dt) {
+  return dt == ES_F32 && plain(d) && d->stride == 1 && (d->K == 4 || d->K == 8 || d->K == 16) && d->C % 8 == 0 &&
+         d->C <= 64 && d->R * d->S <= 9 && d->C > 1;
+}
+template <typename F>
+void small_dispatch(int K, F&& f) {
+  if (K == 4) f(std::integral_constant<int, 4>{});
+  else if (K == 8) f(std::integral_constant<int, 8>{});
+  else f(std::integral_constant<int, 16>{});
+}
+
 // ------------------------------------------------------------------------------- entry points
 // Each returns 1 if it launched (caller checks the launch), 0 if the shape is not a thin conv.
 int es_thin_conv_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x, const int64_t xs[4], const void* wk,
@@ -400,6 +460,17 @@ int es_thin_conv_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x, cons
   const int rs = d->R * d->S, vn = dt == ES_BF16 ? 8 : 4;
   const bool c1 = c1_ok(d, rs) && ys[1] == 1 && aligned(ys, 8);
   const bool k1 = k1_ok(d, rs, vn) && xs[1] == 1 && xs[3] == d->C && aligned(xs, vn);
+  if (!c1 && !k1 && small_ok(d, dt) && ydt == ES_F32 && xs[1] == 1 && aligned(xs, 4) && ys[1] == 1 &&
+      aligned(ys, 4)) {
+    Thin t{};
+    t.d = *d; t.a = x; t.w = wk; t.bias = bias; t.out = y;
+    for (int i = 0; i < 4; ++i) { t.as[i] = xs[i]; t.os[i] = ys[i]; }
+    t.M = d->N * d->P * d->Q;
+    small_dispatch(d->K, [&](auto ko) {
+      hipLaunchKernelGGL((small_fwd<decltype(ko)::value>), dim3(blocks(t.M, NT)), dim3(NT), 0, st, t);
+    });
+    return 1;
+  }
   if (!c1 && !k1) return 0;
   Thin t{};
   t.d = *d; t.a = x; t.w = wk; t.bias = bias; t.out = y;

@@ -71,30 +71,43 @@ __global__ void expsum_bwd_kernel(View x, const void* xp, int bf, const float* c
   }
 }
 
-__global__ void __launch_bounds__(256) gen_losses_kernel(es_gen_loss_t p, const float* fo, const float* l1,
-                                                         const float* l2, const float* n1, const float* n2,
-                                                         const float* sd, const float* s, const float* inten,
-                                                         const float* coord, const float* pos, const float* wp,
-                                                         float* out, float* dfo, float* dl1, float* dl2,
-                                                         float* dcoord, float* coef) {
+// Generator losses in three passes (no host sync):
+//   A  one wave per sample: adl = mean|l1-l2| over the latent, adn = mean|n1-n2| over the noise,
+//      div_b = adl / (adn + 1e-5)   -> coef[b] = div_b, dfo[b] = adn (scratch, rewritten by B)
+//   B  one block: every batch sum, the metrics, and per-sample gradients (dfo, coef, dcoord) plus
+//      the SDI gradient factor g_b -> dl2[b * latent] (scratch, rewritten by C)
+//   C  one wave per sample: dl1 = g_b * sign(l1 - l2), dl2 = -dl1
+__global__ void __launch_bounds__(256) gen_losses_a(es_gen_loss_t p, const float* l1, const float* l2,
+                                                    const float* n1, const float* n2, float* div_out,
+                                                    float* adn_out) {
+  const int lane = threadIdx.x & 63, b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= p.n) return;
+  float adl = 0.f, adn = 0.f;
+  for (int k = lane; k < p.latent; k += 64) adl += fabsf(l1[b * p.latent + k] - l2[b * p.latent + k]);
+  for (int k = lane; k < p.noise; k += 64) adn += fabsf(n1[b * p.noise + k] - n2[b * p.noise + k]);
+  adl = wave_sum(adl) / (float)p.latent;
+  adn = wave_sum(adn) / (float)p.noise;
+  if (lane == 0) { div_out[b] = adl / (adn + 1e-5f); adn_out[b] = adn; }
+}
+
+__global__ void __launch_bounds__(256) gen_losses_b(es_gen_loss_t p, const float* fo, const float* sd,
+                                                    const float* s, const float* inten, const float* coord,
+                                                    const float* pos, const float* wp, float* out, float* dfo,
+                                                    float* coef, float* dcoord, float* dl2) {
   __shared__ float sh[8];
-  __shared__ float sdiv[4096];  // div_j (n <= 4096 checked on host)
+  __shared__ float sdiv[4096], sadn[4096];  // n <= 4096 checked on host
   const int n = p.n;
   const float w = wp[0];
   const float fn = (float)n;
-  // gen hinge + sums of std
-  float sfo = 0.f, sstd = 0.f, ss = 0.f, sl1 = 0.f, saux = 0.f;
+  for (int b = threadIdx.x; b < n; b += blockDim.x) { sdiv[b] = coef[b]; sadn[b] = dfo[b]; }
+  __syncthreads();
+  float sfo = 0.f, sstd = 0.f, ss = 0.f, sl1 = 0.f, saux = 0.f, sr = 0.f;
   for (int b = threadIdx.x; b < n; b += blockDim.x) {
     sfo += fo[b];
     sstd += sd[b];
     ss += s[b];
     sl1 += fabsf(s[b] - inten[b]);
-    float adl = 0.f, adn = 0.f;
-    for (int k = 0; k < p.latent; ++k) adl += fabsf(l1[b * p.latent + k] - l2[b * p.latent + k]);
-    for (int k = 0; k < p.noise; ++k) adn += fabsf(n1[b * p.noise + k] - n2[b * p.noise + k]);
-    adl /= (float)p.latent;
-    adn /= (float)p.noise;
-    sdiv[b] = adl / (adn + 1e-5f);
+    sr += 1.f / (sdiv[b] + 1e-5f);
     for (int k = 0; k < 2; ++k) {
       const float d = coord[b * 2 + k] - pos[b * 2 + k];
       const float z = -2.f * d;
@@ -107,8 +120,6 @@ __global__ void __launch_bounds__(256) gen_losses_kernel(es_gen_loss_t p, const 
   ss = block_sum(ss, sh);
   sl1 = block_sum(sl1, sh);
   saux = block_sum(saux, sh);
-  float sr = 0.f;
-  for (int b = threadIdx.x; b < n; b += blockDim.x) sr += 1.f / (sdiv[b] + 1e-5f);
   sr = block_sum(sr, sh);
   const float ms = sstd / fn;
   const float smean = ss / fn;
@@ -124,16 +135,8 @@ __global__ void __launch_bounds__(256) gen_losses_kernel(es_gen_loss_t p, const 
   for (int b = threadIdx.x; b < n; b += blockDim.x) {
     dfo[b] = -w / fn;
     coef[b] = w * p.in_strength / fn * signf_(s[b] - inten[b]);
-    float adn = 0.f;
-    for (int k = 0; k < p.noise; ++k) adn += fabsf(n1[b * p.noise + k] - n2[b * p.noise + k]);
-    adn /= (float)p.noise;
     const float e = sdiv[b] + 1e-5f;
-    const float g = kdiv / (e * e) / (adn + 1e-5f) / (float)p.latent;
-    for (int k = 0; k < p.latent; ++k) {
-      const float sg = signf_(l1[b * p.latent + k] - l2[b * p.latent + k]);
-      dl1[b * p.latent + k] = g * sg;
-      dl2[b * p.latent + k] = -g * sg;
-    }
+    dl2[b * p.latent] = kdiv / (e * e) / (sadn[b] + 1e-5f) / (float)p.latent;
     for (int k = 0; k < 2; ++k) {
       const float d = coord[b * 2 + k] - pos[b * 2 + k];
       const float z = -2.f * d;
@@ -150,6 +153,18 @@ __global__ void __launch_bounds__(256) gen_losses_kernel(es_gen_loss_t p, const 
     out[5] = n > 1 ? sqrtf(sq / (fn - 1.f)) : NAN;
     out[6] = smean;
     out[7] = w;
+  }
+}
+
+__global__ void __launch_bounds__(256) gen_losses_c(es_gen_loss_t p, const float* l1, const float* l2, float* dl1,
+                                                    float* dl2) {
+  const int lane = threadIdx.x & 63, b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= p.n) return;
+  const float g = dl2[b * p.latent];   // every lane's load precedes the wave's stores (data dependency)
+  for (int k = lane; k < p.latent; k += 64) {
+    const float sg = signf_(l1[b * p.latent + k] - l2[b * p.latent + k]);
+    dl1[b * p.latent + k] = g * sg;
+    dl2[b * p.latent + k] = -g * sg;
   }
 }
 
@@ -233,8 +248,13 @@ extern "C" int es_gen_losses(const es_gen_loss_t* p, const float* fo, const floa
                              float* out, float* dfo, float* dl1, float* dl2, float* dcoord, float* coef,
                              es_stream_t stream) {
   ES_CHECK_ARG(p->n > 0 && p->n <= 4096, "gen_losses: n=%d out of range (1..4096)", p->n);
-  hipLaunchKernelGGL(gen_losses_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, *p, fo, l1, l2, n1, n2, std_, s,
-                     intensity, coord, pos, w_ptr, out, dfo, dl1, dl2, dcoord, coef);
+  ES_CHECK_ARG(p->latent >= 1, "gen_losses: latent must be >= 1");
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 waves((p->n + 3) / 4);
+  hipLaunchKernelGGL(gen_losses_a, waves, dim3(256), 0, st, *p, l1, l2, n1, n2, coef, dfo);
+  hipLaunchKernelGGL(gen_losses_b, dim3(1), dim3(256), 0, st, *p, fo, std_, s, intensity, coord, pos, w_ptr, out,
+                     dfo, coef, dcoord, dl2);
+  hipLaunchKernelGGL(gen_losses_c, waves, dim3(256), 0, st, *p, l1, l2, dl1, dl2);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }

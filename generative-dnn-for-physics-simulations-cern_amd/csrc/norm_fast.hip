@@ -62,12 +62,17 @@ __device__ __forceinline__ float dactf(const FastArgs& a, float v) {
 }
 
 // keep bits for rows r0..r0+3 (bit k = channel c0+k)
+// KM (keep mode, chosen on the host): KM_NONE no dropout, KM_HW4 H*W % 4 == 0, KM_ROW H*W == 1 and
+// C % 4 == 0, KM_GEN anything else.  One instantiation per mode keeps each kernel's code small.
+enum { KM_NONE = 0, KM_HW4 = 1, KM_ROW = 2, KM_GEN = 3 };
+
+template <int KM>
 __device__ __forceinline__ void keep_bits(const FastArgs& a, int r0, int c0, uint32_t (&keep)[4]) {
-  if (!a.drop.enabled) { keep[0] = keep[1] = keep[2] = keep[3] = 0xFFu; return; }
+  if constexpr (KM == KM_NONE) { keep[0] = keep[1] = keep[2] = keep[3] = 0xFFu; return; }
   keep[0] = keep[1] = keep[2] = keep[3] = 0u;
   const uint32_t thr = a.drop.threshold;
   const uint32_t k0 = (uint32_t)a.drop.seed, k1 = (uint32_t)(a.drop.seed >> 32);
-  if ((a.HW & 3) == 0) {
+  if constexpr (KM == KM_HW4) {
     const int n = r0 / a.HW, hw0 = r0 - n * a.HW;     // r0 % 4 == 0 -> same n for the 4 rows
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -79,7 +84,7 @@ __device__ __forceinline__ void keep_bits(const FastArgs& a, int r0, int c0, uin
       keep[2] |= (uint32_t)((w.z >> 8) < thr) << k;
       keep[3] |= (uint32_t)((w.w >> 8) < thr) << k;
     }
-  } else if (a.HW == 1 && (a.C & 3) == 0) {
+  } else if constexpr (KM == KM_ROW) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int r = r0 + j;
@@ -92,7 +97,7 @@ __device__ __forceinline__ void keep_bits(const FastArgs& a, int r0, int c0, uin
                     ((uint32_t)((w.z >> 8) < thr) << 2) | ((uint32_t)((w.w >> 8) < thr) << 3)) << (4 * h);
       }
     }
-  } else if (r0 - (r0 / a.HW) * a.HW + 3 < a.HW && r0 + 3 < a.rows) {
+  } else if (r0 - (r0 / a.HW) * a.HW + 3 < a.HW && r0 + 3 < a.rows) {   // KM_GEN
     // the 4 rows lie in one sample: their logical indices i0..i0+3 are consecutive and span at
     // most two Philox counters per channel (2 calls instead of 4)
     const int n = r0 / a.HW, hw0 = r0 - n * a.HW;
@@ -174,7 +179,7 @@ __device__ __forceinline__ Geo geo(const FastArgs& a) {
   return g;
 }
 
-template <typename T>
+template <typename T, int KM>
 __global__ void __launch_bounds__(256) bn_fwd_fast(FastArgs a) {
   const Geo g = geo(a);
   if (!g.active) return;
@@ -197,7 +202,7 @@ __global__ void __launch_bounds__(256) bn_fwd_fast(FastArgs a) {
     for (int j = 0; j < 4; ++j)            // issue every load of the group before any store
       if (j < nr) ld8<T>(x + (int64_t)(r0 + j) * a.C + g.c0, v[j]);
     uint32_t keep[4];
-    keep_bits(a, r0, g.c0, keep);
+    keep_bits<KM>(a, r0, g.c0, keep);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (j >= nr) break;
@@ -209,7 +214,7 @@ __global__ void __launch_bounds__(256) bn_fwd_fast(FastArgs a) {
 }
 
 // MODE 0: Welford stats of x.  MODE 1: backward sums (sum dnorm, sum dnorm*xhat).
-template <typename T, int MODE>
+template <typename T, int MODE, int KM>
 __global__ void __launch_bounds__(256) bn_reduce_fast(FastArgs a) {
   const Geo g = geo(a);
   float s0[8], s1[8], s2[8];
@@ -232,7 +237,7 @@ __global__ void __launch_bounds__(256) bn_reduce_fast(FastArgs a) {
     for (int grp = blockIdx.y * g.RGB + g.rg; grp < ngroups; grp += gridDim.y * g.RGB) {
       const int r0 = g.rbase + grp * 4;
       uint32_t keep[4];
-      if (MODE == 1) keep_bits(a, r0, g.c0, keep);
+      if (MODE == 1) keep_bits<KM>(a, r0, g.c0, keep);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int r = r0 + j;
@@ -300,7 +305,7 @@ __global__ void __launch_bounds__(256) bn_reduce_fast(FastArgs a) {
   }
 }
 
-template <typename T>
+template <typename T, int KM>
 __global__ void __launch_bounds__(256) bn_bwd_apply_fast(FastArgs a) {
   const Geo g = geo(a);
   float acc[8];
@@ -331,7 +336,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_fast(FastArgs a) {
           ld8<T>(dy + (int64_t)(r0 + j) * a.C + g.c0, d[j]);
         }
       uint32_t keep[4];
-      keep_bits(a, r0, g.c0, keep);
+      keep_bits<KM>(a, r0, g.c0, keep);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if (j >= nr) break;
@@ -403,6 +408,45 @@ int64_t es_fast_part_floats(const es_view_t* v, int G) {
   return (int64_t)g.z * chunks * 3 * v->c;
 }
 
+static int keep_mode(const FastArgs& a) {
+  if (!a.drop.enabled) return KM_NONE;
+  if ((a.HW & 3) == 0) return KM_HW4;
+  if (a.HW == 1 && (a.C & 3) == 0) return KM_ROW;
+  return KM_GEN;
+}
+#define ES_KM_LAUNCH(K, T, KMV, grid, st, a) hipLaunchKernelGGL((K<T, KMV>), grid, dim3(256), 0, st, a)
+#define ES_KM_DISPATCH(a, K, dt, grid, st)                                                 \
+  do {                                                                                    \
+    const int km_ = keep_mode(a);                                                         \
+    if (dt == ES_BF16) {                                                                  \
+      if (km_ == KM_NONE) ES_KM_LAUNCH(K, bf16, KM_NONE, grid, st, a);                    \
+      else if (km_ == KM_HW4) ES_KM_LAUNCH(K, bf16, KM_HW4, grid, st, a);                 \
+      else if (km_ == KM_ROW) ES_KM_LAUNCH(K, bf16, KM_ROW, grid, st, a);                 \
+      else ES_KM_LAUNCH(K, bf16, KM_GEN, grid, st, a);                                    \
+    } else {                                                                              \
+      if (km_ == KM_NONE) ES_KM_LAUNCH(K, float, KM_NONE, grid, st, a);                   \
+      else if (km_ == KM_HW4) ES_KM_LAUNCH(K, float, KM_HW4, grid, st, a);                \
+      else if (km_ == KM_ROW) ES_KM_LAUNCH(K, float, KM_ROW, grid, st, a);                \
+      else ES_KM_LAUNCH(K, float, KM_GEN, grid, st, a);                                   \
+    }                                                                                     \
+  } while (0)
+#define ES_KM_LAUNCH1(K, T, KMV, grid, st, a) hipLaunchKernelGGL((K<T, 1, KMV>), grid, dim3(256), 0, st, a)
+#define ES_KM_DISPATCH1(a, K, dt, grid, st)                                                \
+  do {                                                                                    \
+    const int km_ = keep_mode(a);                                                         \
+    if (dt == ES_BF16) {                                                                  \
+      if (km_ == KM_NONE) ES_KM_LAUNCH1(K, bf16, KM_NONE, grid, st, a);                   \
+      else if (km_ == KM_HW4) ES_KM_LAUNCH1(K, bf16, KM_HW4, grid, st, a);                \
+      else if (km_ == KM_ROW) ES_KM_LAUNCH1(K, bf16, KM_ROW, grid, st, a);                \
+      else ES_KM_LAUNCH1(K, bf16, KM_GEN, grid, st, a);                                   \
+    } else {                                                                              \
+      if (km_ == KM_NONE) ES_KM_LAUNCH1(K, float, KM_NONE, grid, st, a);                  \
+      else if (km_ == KM_HW4) ES_KM_LAUNCH1(K, float, KM_HW4, grid, st, a);               \
+      else if (km_ == KM_ROW) ES_KM_LAUNCH1(K, float, KM_ROW, grid, st, a);               \
+      else ES_KM_LAUNCH1(K, float, KM_GEN, grid, st, a);                                  \
+    }                                                                                     \
+  } while (0)
+
 static FastArgs mk(const es_view_t* v, const es_chain_t* ch, int G) {
   FastArgs a{};
   a.rows = v->n * v->h * v->w;
@@ -421,8 +465,8 @@ int es_fast_norm_stats(const es_view_t* v, int G, es_dtype_t dt, const void* xp,
   fast_geometry(v, G, grid, chunks);
   FastArgs a = mk(v, nullptr, G);
   a.x = xp; a.part = part;
-  if (dt == ES_BF16) hipLaunchKernelGGL((bn_reduce_fast<bf16, 0>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((bn_reduce_fast<float, 0>), grid, dim3(256), 0, st, a);
+  if (dt == ES_BF16) hipLaunchKernelGGL((bn_reduce_fast<bf16, 0, KM_NONE>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((bn_reduce_fast<float, 0, KM_NONE>), grid, dim3(256), 0, st, a);
   return chunks;
 }
 
@@ -433,8 +477,7 @@ void es_fast_norm_fwd(const es_view_t* v, int G, es_dtype_t dt, const void* xp, 
   FastArgs a = mk(v, ch, G);
   a.x = xp; a.out = yp;
   a.mean = nm->mean; a.invstd = nm->invstd; a.gamma = nm->gamma; a.beta = nm->beta;
-  if (dt == ES_BF16) hipLaunchKernelGGL(bn_fwd_fast<bf16>, grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(bn_fwd_fast<float>, grid, dim3(256), 0, st, a);
+  ES_KM_DISPATCH(a, bn_fwd_fast, dt, grid, st);
 }
 
 int es_fast_norm_bwd_reduce(const es_view_t* v, int G, es_dtype_t dt, const void* xp, const void* dyp,
@@ -444,8 +487,7 @@ int es_fast_norm_bwd_reduce(const es_view_t* v, int G, es_dtype_t dt, const void
   FastArgs a = mk(v, ch, G);
   a.x = xp; a.dy = dyp; a.part = part;
   a.mean = nm->mean; a.invstd = nm->invstd; a.gamma = nm->gamma; a.beta = nm->beta;
-  if (dt == ES_BF16) hipLaunchKernelGGL((bn_reduce_fast<bf16, 1>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((bn_reduce_fast<float, 1>), grid, dim3(256), 0, st, a);
+  ES_KM_DISPATCH1(a, bn_reduce_fast, dt, grid, st);
   return chunks;
 }
 
@@ -458,7 +500,6 @@ int es_fast_norm_bwd_apply(const es_view_t* v, int G, es_dtype_t dt, const void*
   FastArgs a = mk(v, ch, G);
   a.x = xp; a.dy = dyp; a.out = dxp; a.a1 = a1; a.a2 = a2; a.dsum = dsum; a.part = part;
   a.mean = nm->mean; a.invstd = nm->invstd; a.gamma = nm->gamma; a.beta = nm->beta;
-  if (dt == ES_BF16) hipLaunchKernelGGL(bn_bwd_apply_fast<bf16>, grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(bn_bwd_apply_fast<float>, grid, dim3(256), 0, st, a);
+  ES_KM_DISPATCH(a, bn_bwd_apply_fast, dt, grid, st);
   return dsum ? (int)(grid.z * grid.y) : 0;
 }
