@@ -88,6 +88,8 @@ def main():
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the per-kernel HIP-event probe")
+    ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
+                    help="replay the step as a captured HIP graph (auto: single process, 1 expert)")
     args = ap.parse_args()
 
     import torch
@@ -112,13 +114,21 @@ def main():
     t = {k: torch.from_numpy(v).to(dev) for k, v in b.items()}
     real = t["real_images"].unsqueeze(1).contiguous()
 
-    def step():
-        moe.train_step(0, t["cond"], real, t["true_positions"], t["std"], t["intensity"], oa, og, od, orr, None, dev)
+    step_args = (0, t["cond"], real, t["true_positions"], t["std"], t["intensity"], oa, og, od, orr, None, dev)
 
+    def eager_step():
+        moe.train_step(*step_args)
+
+    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1 and args.experts == 1)
     for _ in range(args.warmup):
-        step()
+        eager_step()
+    step = eager_step
+    if use_graph:
+        from expertsim.graph import StepGraph
+        sg = StepGraph(moe, step_args, warmup=1)
+        step = sg.replay
     probe = None
-    if not args.no_probe:
+    if not args.no_probe and not use_graph:
         probe = layers.KernelProbe(["G0.c5.fwd", "G0.c5.dgrad", "G0.c5.wgrad"])
         layers.set_probe(probe)
     if world > 1:
@@ -132,6 +142,17 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     layers.set_probe(None)
+    if use_graph:
+        sg.sync_host_state([og[0], od[0], oa[0], orr])
+        if not args.no_probe:
+            # a graph replay cannot be split per kernel: the per-launch HIP events are taken on
+            # eager steps of the same model and batch right after the timed region
+            probe = layers.KernelProbe(["G0.c5.fwd", "G0.c5.dgrad", "G0.c5.wgrad"])
+            layers.set_probe(probe)
+            for _ in range(min(args.steps, 5)):
+                eager_step()
+            torch.cuda.synchronize()
+            layers.set_probe(None)
     if world > 1:
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -160,6 +181,7 @@ def main():
             "metric": "GAN-step images/sec (44x44 ZDC) at 1/2/4/8 MI355X; conv MFMA util %",
             "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+            "step_launch": "hip_graph" if use_graph else "eager",
             "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
             "config": {"workload": f"{args.arch} 44x44 MoE-GAN train_step, E={args.experts}, B={args.batch} per GPU "
                                    f"(BASELINE configs[1])", "arch": args.arch, "n_experts": args.experts,

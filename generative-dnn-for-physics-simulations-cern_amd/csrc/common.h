@@ -99,6 +99,10 @@ __device__ __forceinline__ uint32_t philox_word(uint64_t seed, uint32_t stream, 
   const uint32_t s = (uint32_t)(i & 3);
   return s == 0 ? r.x : (s == 1 ? r.y : (s == 2 ? r.z : r.w));
 }
+// stream + step * step_mul when the step lives on the device (captured train steps)
+__device__ __forceinline__ void resolve_stream(es_dropout_t& d) {
+  if (d.enabled && d.step_ptr) d.stream += (uint32_t)(d.step_ptr[0] * d.step_mul);
+}
 __device__ __forceinline__ bool dropout_keep(const es_dropout_t& d, uint64_t i) {
   return (philox_word(d.seed, d.stream, i) >> 8) < d.threshold;
 }

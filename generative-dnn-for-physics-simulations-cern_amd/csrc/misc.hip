@@ -379,8 +379,31 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   }
 }
 
+// step read on the device; bias corrections as torch computes them (double), per thread
+__global__ void adam_dev_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
+                                const int32_t* __restrict__ step_ptr, float gscale) {
+  const int step = step_ptr[0];
+  const double bc1 = 1.0 - pow((double)b1, (double)step);
+  const double bc2 = 1.0 - pow((double)b2, (double)step);
+  const float step_size = (float)((double)lr / bc1);
+  const float bc2_sqrt = (float)sqrt(bc2);
+  GRID_STRIDE(i, n) {
+    const float gi = g[i] * gscale;
+    float mi = m[i];
+    mi = mi + (1.f - b1) * (gi - mi);
+    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    p[i] = p[i] - step_size * (mi / (sqrtf(vi) / bc2_sqrt + eps));
+  }
+}
+__global__ void counter_add_kernel(int32_t* c, int32_t v) { c[0] += v; }
+
 // ------------------------------------------------------------------------------------ RNG
-__global__ void randn_kernel(float* out, int64_t n, uint64_t seed, uint32_t sid) {
+__global__ void randn_kernel(float* out, int64_t n, uint64_t seed, uint32_t sid, const int32_t* step_ptr,
+                             int32_t step_mul) {
+  if (step_ptr) sid += (uint32_t)(step_ptr[0] * step_mul);
   // Box-Muller on pairs: counter = pair index
   const int64_t pairs = (n + 1) / 2;
   GRID_STRIDE(i, pairs) {
@@ -395,7 +418,9 @@ __global__ void randn_kernel(float* out, int64_t n, uint64_t seed, uint32_t sid)
     if (2 * i + 1 < n) out[2 * i + 1] = rad * s;
   }
 }
-__global__ void rand_exp_kernel(float* out, int64_t n, uint64_t seed, uint32_t sid) {
+__global__ void rand_exp_kernel(float* out, int64_t n, uint64_t seed, uint32_t sid, const int32_t* step_ptr,
+                                int32_t step_mul) {
+  if (step_ptr) sid += (uint32_t)(step_ptr[0] * step_mul);
   GRID_STRIDE(i, n) {
     u32x4 r = philox4x32_10((uint32_t)i, (uint32_t)(i >> 32), sid, 0x5EED0002u, (uint32_t)seed,
                             (uint32_t)(seed >> 32));
@@ -404,6 +429,7 @@ __global__ void rand_exp_kernel(float* out, int64_t n, uint64_t seed, uint32_t s
   }
 }
 __global__ void dropout_mask_kernel(uint8_t* out, int64_t n, es_dropout_t d) {
+  resolve_stream(d);
   GRID_STRIDE(i, n) out[i] = dropout_keep(d, (uint64_t)i) ? 1 : 0;
 }
 }  // namespace
@@ -543,18 +569,42 @@ extern "C" int es_adam(float* p, const float* g, float* m, float* v, int64_t n, 
   return ES_OK;
 }
 
-extern "C" int es_randn(float* out, int64_t n, uint64_t seed, uint32_t stream_id, es_stream_t stream) {
+extern "C" int es_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                           float beta2, float eps, const int32_t* step_ptr, float grad_scale, es_stream_t stream) {
+  ES_CHECK_ARG(step_ptr != nullptr, "adam_dev: step_ptr is NULL");
   if (n == 0) return ES_OK;
-  hipLaunchKernelGGL(randn_kernel, dim3(grid_for((n + 1) / 2)), dim3(256), 0, (hipStream_t)stream, out, n, seed,
-                     stream_id);
+  hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr, beta1,
+                     beta2, eps, step_ptr, grad_scale);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
 
-extern "C" int es_rand_exponential(float* out, int64_t n, uint64_t seed, uint32_t stream_id, es_stream_t stream) {
+extern "C" int es_randn_dev(float* out, int64_t n, uint64_t seed, uint32_t stream_id, const int32_t* step_ptr,
+                            int32_t step_mul, es_stream_t stream) {
+  if (n == 0) return ES_OK;
+  hipLaunchKernelGGL(randn_kernel, dim3(grid_for((n + 1) / 2)), dim3(256), 0, (hipStream_t)stream, out, n, seed,
+                     stream_id, step_ptr, step_mul);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+extern "C" int es_randn(float* out, int64_t n, uint64_t seed, uint32_t stream_id, es_stream_t stream) {
+  return es_randn_dev(out, n, seed, stream_id, nullptr, 0, stream);
+}
+
+extern "C" int es_rand_exponential_dev(float* out, int64_t n, uint64_t seed, uint32_t stream_id,
+                                       const int32_t* step_ptr, int32_t step_mul, es_stream_t stream) {
   if (n == 0) return ES_OK;
   hipLaunchKernelGGL(rand_exp_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, out, n, seed,
-                     stream_id);
+                     stream_id, step_ptr, step_mul);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+extern "C" int es_rand_exponential(float* out, int64_t n, uint64_t seed, uint32_t stream_id, es_stream_t stream) {
+  return es_rand_exponential_dev(out, n, seed, stream_id, nullptr, 0, stream);
+}
+
+extern "C" int es_counter_add(int32_t* counter, int32_t v, es_stream_t stream) {
+  hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, counter, v);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }

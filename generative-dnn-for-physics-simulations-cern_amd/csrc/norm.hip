@@ -177,6 +177,7 @@ __device__ __forceinline__ void bwd_elem(const BwdIn& b, int n, int c, int h, in
 
 template <int RED>
 __global__ void __launch_bounds__(256) colred_kernel(BwdIn b, int64_t rows, int64_t rows_per_chunk, float* part) {
+  resolve_stream(b.ch.drop);
   // part layout: [chunk][3][C]
   const View& v = b.x;
   const int C = v.c;
@@ -409,6 +410,7 @@ __global__ void __launch_bounds__(256) sum1_kernel(BwdIn b, int rows, float* par
 // one block per stats group; RED_STATS writes mean/invstd, RED_BWD writes A1/A2 (means over group)
 template <int RED>
 __global__ void __launch_bounds__(256) segred_kernel(BwdIn b, float eps, float* o1, float* o2) {
+  resolve_stream(b.ch.drop);
   const View& v = b.x;
   const int G = b.nm.kind == ES_NORM_GN ? b.nm.groups : 1;
   const int cg = v.c / G;
@@ -460,6 +462,7 @@ struct FwdArgs {
 };
 
 __global__ void __launch_bounds__(256) norm_fwd_kernel(FwdArgs a) {
+  resolve_stream(a.ch.drop);
   const int64_t total = (int64_t)a.x.n * a.x.c * a.x.h * a.x.w;
   const bool cl = a.x.s[1] == 1 && a.x.c > 1;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
@@ -481,6 +484,7 @@ struct BwdApply {
 };
 
 __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(BwdApply a) {
+  resolve_stream(a.b.ch.drop);
   const View& v = a.b.x;
   const int64_t total = (int64_t)v.n * v.c * v.h * v.w;
   const bool cl = v.s[1] == 1 && v.c > 1;

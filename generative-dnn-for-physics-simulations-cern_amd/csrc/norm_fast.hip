@@ -181,6 +181,7 @@ __device__ __forceinline__ Geo geo(const FastArgs& a) {
 
 template <typename T, int KM>
 __global__ void __launch_bounds__(256) bn_fwd_fast(FastArgs a) {
+  resolve_stream(a.drop);
   const Geo g = geo(a);
   if (!g.active) return;
   float sc[8], sh[8];
@@ -216,6 +217,7 @@ __global__ void __launch_bounds__(256) bn_fwd_fast(FastArgs a) {
 // MODE 0: Welford stats of x.  MODE 1: backward sums (sum dnorm, sum dnorm*xhat).
 template <typename T, int MODE, int KM>
 __global__ void __launch_bounds__(256) bn_reduce_fast(FastArgs a) {
+  resolve_stream(a.drop);
   const Geo g = geo(a);
   float s0[8], s1[8], s2[8];
 #pragma unroll
@@ -307,6 +309,7 @@ __global__ void __launch_bounds__(256) bn_reduce_fast(FastArgs a) {
 
 template <typename T, int KM>
 __global__ void __launch_bounds__(256) bn_bwd_apply_fast(FastArgs a) {
+  resolve_stream(a.drop);
   const Geo g = geo(a);
   float acc[8];
 #pragma unroll

@@ -26,7 +26,7 @@ class View(C.Structure):
 
 class Dropout(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("stream", C.c_uint32), ("threshold", C.c_uint32),
-                ("scale", C.c_float), ("enabled", C.c_int)]
+                ("scale", C.c_float), ("enabled", C.c_int), ("step_ptr", C.c_void_p), ("step_mul", C.c_int32)]
 
 
 class ConvDesc(C.Structure):
@@ -88,8 +88,12 @@ _SIGS = {
     "es_router_alb": (C.c_int, [P, C.c_int, C.c_int, C.c_float, C.c_float, P, P, P]),
     "es_adam": (C.c_int, [P, P, P, P, I64, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int,
                           C.c_float, P]),
+    "es_adam_dev": (C.c_int, [P, P, P, P, I64, C.c_float, C.c_float, C.c_float, C.c_float, P, C.c_float, P]),
     "es_randn": (C.c_int, [P, I64, C.c_uint64, C.c_uint32, P]),
     "es_rand_exponential": (C.c_int, [P, I64, C.c_uint64, C.c_uint32, P]),
+    "es_randn_dev": (C.c_int, [P, I64, C.c_uint64, C.c_uint32, P, C.c_int32, P]),
+    "es_rand_exponential_dev": (C.c_int, [P, I64, C.c_uint64, C.c_uint32, P, C.c_int32, P]),
+    "es_counter_add": (C.c_int, [P, C.c_int32, P]),
     "es_dropout_mask": (C.c_int, [P, I64, P, P]),
 }
 
@@ -161,12 +165,28 @@ def make_view(dims, strides) -> View:
     return v
 
 
+# Device step counter of the running train step (see set_step_counter): dropout structs built while
+# it is set add step * STEP_STREAM_MUL to their stream ON THE DEVICE, so a captured graph of the
+# step draws the masks of the step it is replayed for.
+STEP_STREAM_MUL = 1024
+_STEP_COUNTER = None
+
+
+def set_step_counter(t):
+    """t: device int32 tensor [1] holding the current step, or None (streams used as given)."""
+    global _STEP_COUNTER
+    _STEP_COUNTER = t
+
+
 def dropout_struct(p: float = 0.0, seed: int = 0, stream: int = 0, enabled: bool = False) -> Dropout:
     d = Dropout()
     d.enabled = 1 if (enabled and p > 0.0) else 0
     if d.enabled:
         d.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         d.stream = int(stream) & 0xFFFFFFFF
+        if _STEP_COUNTER is not None:
+            d.step_ptr = _STEP_COUNTER.data_ptr()
+            d.step_mul = STEP_STREAM_MUL
         d.threshold = int((1.0 - float(p)) * 16777216.0)   # floor, = philox.keep_threshold
         d.scale = float(np.float32(1.0) / np.float32(1.0 - p))   # torch: bernoulli_(1-p).div_(1-p) in fp32
     return d

@@ -64,6 +64,7 @@ class MoEWrapper(nn.Module):
         self.ddp = None            # expertsim.train.ddp.DataParallel (set by the loop)
         self.rank = 0
         self.step_count = 0
+        self._dstep = None         # device int32 step counter: dropout / noise streams (graph replay)
         self.set_precision(cfg_get(cfg, "train.precision", "fp32"))
 
     def set_precision(self, precision: str):
@@ -102,6 +103,8 @@ class MoEWrapper(nn.Module):
         dev = torch.device(device) if not isinstance(device, torch.device) else device
         if dev.type != "cuda":
             raise hip.HipError("MoEWrapper.train_step runs on the HIP device only (no CPU fallback)")
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
         E = self.n_experts
         f32 = lambda t: t.to(device=dev, dtype=torch.float32).contiguous()
         cond, real_images, true_positions, std, intensity = map(f32, (cond, real_images, true_positions,
@@ -109,6 +112,23 @@ class MoEWrapper(nn.Module):
         if real_images.dim() == 3:
             real_images = real_images.unsqueeze(1)
         B = cond.shape[0]
+        step = self.step_count
+        rc = self.cfg.model.router
+        if self._dstep is None or self._dstep.device != dev:
+            self._dstep = torch.full((1,), step, dtype=torch.int32, device=dev)
+        # every step-dependent random stream is keyed on the device counter (captured graphs)
+        hip.set_step_counter(self._dstep)
+        self.rng.begin_step(self._dstep)
+        try:
+            return self._train_step(epoch, cond, real_images, true_positions, std, intensity, aux_reg_optimizers,
+                                    generator_optimizers, discriminator_optimizers, router_optimizer, dev, B)
+        finally:
+            hip.set_step_counter(None)
+            self.rng.end_step()
+
+    def _train_step(self, epoch, cond, real_images, true_positions, std, intensity, aux_reg_optimizers,
+                    generator_optimizers, discriminator_optimizers, router_optimizer, dev, B):
+        E = self.n_experts
         step = self.step_count
         rc = self.cfg.model.router
 
@@ -185,6 +205,7 @@ class MoEWrapper(nn.Module):
             gan = router_loss = ed = diff = ent = alb = zero
 
         self.step_count += 1
+        hip.call("es_counter_add", hip.ptr(self._dstep), 1, hip.stream_ptr())
         countsf = counts.to(torch.float32) if self.ddp is None else self.ddp.global_counts_tensor(dev)
         metrics = {
             "gen_loss": mbuf[:, 0].mean(), "disc_loss": mbuf[:, 8].mean(), "div_loss": mbuf[:, 2].mean(),
@@ -219,7 +240,8 @@ class MoEWrapper(nn.Module):
         w = float(np.float32(be) / np.float32(B))
         w_dev = torch.full((1,), w, dtype=torch.float32, device=dev)
         rank = self.rank
-        sb = lambda pid: philox.dropout_stream(step, e, pid, 0, rank)
+        # the step term (step * 1024) is added on the device from self._dstep
+        sb = lambda pid: philox.dropout_stream(0, e, pid, 0, rank)
 
         # ---- generator forward #1 (moe.py:144-145)
         n1 = self._noise(e, 0, (be, self.noise_dim), dev)

@@ -21,6 +21,7 @@ class FusedAdam(torch.optim.Optimizer):
         super().__init__(list(module.parameters()), dict(lr=lr, betas=betas, eps=eps, weight_decay=0.0))
         self._m = self._v = None
         self._step = 0
+        self._dstep = None   # device copy of the step (read by the kernel: graph-capturable)
 
     def _buffers(self):
         flat = self.module.flat_params
@@ -45,13 +46,26 @@ class FusedAdam(torch.optim.Optimizer):
         flat = self._buffers()
         if grad_scale is None:
             grad_scale = getattr(self.module, "_grad_scale", 1.0)
+        if self._dstep is None or self._dstep.device != flat.device:
+            self._dstep = torch.full((1,), self._step, dtype=torch.int32, device=flat.device)
         self._step += 1
         g = self.param_groups[0]
         b1, b2 = g["betas"]
-        hip.call("es_adam", hip.ptr(flat), hip.ptr(self.module.flat_grads), hip.ptr(self._m), hip.ptr(self._v),
-                 flat.numel(), float(g["lr"]), float(b1), float(b2), float(g["eps"]), self._step,
+        # step counter advanced and read on the device, so a captured step replays correctly
+        hip.call("es_counter_add", hip.ptr(self._dstep), 1, hip.stream_ptr())
+        hip.call("es_adam_dev", hip.ptr(flat), hip.ptr(self.module.flat_grads), hip.ptr(self._m), hip.ptr(self._v),
+                 flat.numel(), float(g["lr"]), float(b1), float(b2), float(g["eps"]), hip.ptr(self._dstep),
                  float(grad_scale), hip.stream_ptr())
         for p in self.module.parameters():
             self.state[p]["step"] = torch.tensor(float(self._step))
         self.module.invalidate()
         return None
+
+    def sync_step(self):
+        """Host step := device step (after replays of a captured train step)."""
+        if self._dstep is not None:
+            self._step = int(self._dstep.item())
+            for p in self.module.parameters():
+                if p in self.state:
+                    self.state[p]["step"] = torch.tensor(float(self._step))
+        return self._step

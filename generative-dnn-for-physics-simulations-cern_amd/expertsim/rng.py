@@ -1,31 +1,57 @@
 """Device random numbers (Philox4x32-10 counter streams) replacing torch.randn (moe.py:144,535)
 and the Exp(1) draws inside F.gumbel_softmax (router.py:23).  Each call consumes a fresh stream id,
-so no generator state lives on the device."""
+so no generator state lives on the device.
+
+Inside a train step (``begin_step(counter)``) the stream id of the i-th draw is
+``stream_base + i + counter[0] * 256``, the step term added on the device: a captured HIP graph
+of the step draws new numbers at every replay."""
 from __future__ import annotations
 
 import torch
 
 from . import hip
 
+STEP_MUL = 256   # draws per step stay below this
+
 
 class DeviceRNG:
     def __init__(self, seed: int = 1234, stream_base: int = 1 << 24):
         self.seed = int(seed)
+        self.stream_base = int(stream_base)
         self.counter = int(stream_base)
+        self.step_counter = None
+        self.calls = 0
+
+    def begin_step(self, step_counter: torch.Tensor):
+        """Key the following draws on a device step counter (int32 [1])."""
+        self.step_counter = step_counter
+        self.calls = 0
+
+    def end_step(self):
+        self.step_counter = None
 
     def _next(self):
         self.counter += 1
         return self.counter & 0xFFFFFFFF
 
-    def normal(self, out: torch.Tensor):
+    def _draw(self, name, out):
         hip.require_device(out)
-        hip.call("es_randn", hip.ptr(out), out.numel(), self.seed, self._next(), hip.stream_ptr())
+        if self.step_counter is not None:
+            if self.calls >= STEP_MUL:
+                raise RuntimeError("DeviceRNG: more than %d draws in one step" % STEP_MUL)
+            sid = (self.stream_base + self.calls) & 0xFFFFFFFF
+            self.calls += 1
+            hip.call(name + "_dev", hip.ptr(out), out.numel(), self.seed, sid, hip.ptr(self.step_counter), STEP_MUL,
+                     hip.stream_ptr())
+        else:
+            hip.call(name, hip.ptr(out), out.numel(), self.seed, self._next(), hip.stream_ptr())
         return out
 
+    def normal(self, out: torch.Tensor):
+        return self._draw("es_randn", out)
+
     def exponential(self, out: torch.Tensor):
-        hip.require_device(out)
-        hip.call("es_rand_exponential", hip.ptr(out), out.numel(), self.seed, self._next(), hip.stream_ptr())
-        return out
+        return self._draw("es_rand_exponential", out)
 
 
 _default = None

@@ -38,13 +38,17 @@ typedef struct {
 } es_view_t;
 
 /* Counter-based dropout (expertsim/utils/philox.py).  keep(i) = (philox(seed, stream, i) >> 8) <
- * threshold, i = NCHW-logical element index; kept values are multiplied by `scale` = 1/(1-p). */
+ * threshold, i = NCHW-logical element index; kept values are multiplied by `scale` = 1/(1-p).
+ * With step_ptr set, the stream used is stream + step_ptr[0] * step_mul, read on the device: a
+ * captured HIP graph then draws fresh masks at every replay (the train step's step counter). */
 typedef struct {
   uint64_t seed;
   uint32_t stream;
   uint32_t threshold;
   float scale;
   int enabled;
+  const int32_t* step_ptr; /* device int32 or NULL */
+  int32_t step_mul;
 } es_dropout_t;
 
 const char* es_last_error(void);
@@ -244,6 +248,10 @@ int es_router_alb(const float* gates, int B, int E, float tau, float coef, float
  * ---------------------------------------------------------------------------------------- */
 int es_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
             float beta2, float eps, int step, float grad_scale, es_stream_t stream);
+/* Same update with the (1-based) step read on the device from step_ptr[0]; bias corrections
+ * computed in the kernel (for captured train steps). */
+int es_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                float beta2, float eps, const int32_t* step_ptr, float grad_scale, es_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Random numbers (torch.randn at moe.py:144,535; exponential_ inside F.gumbel_softmax):
@@ -252,6 +260,13 @@ int es_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, f
 int es_randn(float* out, int64_t n, uint64_t seed, uint32_t stream_id, es_stream_t stream);
 int es_rand_exponential(float* out, int64_t n, uint64_t seed, uint32_t stream_id,
                         es_stream_t stream);
+/* Same draws with the stream id offset on the device: stream_id + step_ptr[0] * step_mul. */
+int es_randn_dev(float* out, int64_t n, uint64_t seed, uint32_t stream_id, const int32_t* step_ptr,
+                 int32_t step_mul, es_stream_t stream);
+int es_rand_exponential_dev(float* out, int64_t n, uint64_t seed, uint32_t stream_id,
+                            const int32_t* step_ptr, int32_t step_mul, es_stream_t stream);
+/* counter[0] += v on the device (step counters of a captured train step). */
+int es_counter_add(int32_t* counter, int32_t v, es_stream_t stream);
 /* dropout mask materialisation (tests): out[i] = keep(i) */
 int es_dropout_mask(uint8_t* out, int64_t n, const es_dropout_t* d, es_stream_t stream);
 

@@ -1,0 +1,64 @@
+"""A captured HIP graph of the train step (expertsim/graph.py) replays exactly the next steps.
+
+Model A runs 3 eager steps; model B (same initial state) runs 1 eager warm-up step, is captured,
+and replayed twice.  Everything step-dependent (dropout / noise streams, Adam bias corrections)
+is read from device counters, so both must land on the same parameters and metrics.  The only
+difference allowed is run-to-run rounding from the fp32 atomics of the split-K weight gradients,
+amplified by Adam (each step moves a parameter by ~lr whatever its gradient's magnitude):
+|p_A - p_B| <= 3 * 2 * lr elementwise, metrics within 1e-2 relative.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _build(seed=7):
+    from expertsim.config import inject_shared, load_config
+    from expertsim.models import build_model
+    from expertsim.models.moe import MoEWrapper
+    from expertsim.train.training_setup import setup_optimizers
+    cfg = inject_shared(load_config(overrides=["model.architecture=neutron", "model.n_experts=1",
+                                               "train.precision=bf16", f"train.rng_seed={seed}"]))
+    torch.manual_seed(seed)
+    parts = [build_model(f"neutron.{k}", getattr(cfg.model, k), DEV) for k in ("generator", "discriminator", "aux_reg")]
+    router = build_model("router_v1", cfg.model.router, DEV)
+    moe = MoEWrapper(*parts, router, 1, cfg, image_shape=(44, 44)).to(DEV)
+    return moe, setup_optimizers(moe, cfg), cfg
+
+
+def test_graph_replay_matches_eager_steps():
+    from expertsim.graph import StepGraph
+    from expertsim.utils.synthetic import make_batch
+    b = make_batch(64, "neutron", seed=3)
+    t = {k: torch.from_numpy(v).to(DEV) for k, v in b.items()}
+    real = t["real_images"].unsqueeze(1).contiguous()
+
+    runs = []
+    for mode in ("eager", "graph"):
+        moe, (og, od, oa, orr), cfg = _build()
+        args = (0, t["cond"], real, t["true_positions"], t["std"], t["intensity"], oa, og, od, orr, None, DEV)
+        if mode == "eager":
+            for _ in range(3):
+                m = moe.train_step(*args)
+        else:
+            sg = StepGraph(moe, args, warmup=1)
+            for _ in range(2):
+                m = sg.replay()
+            sg.sync_host_state([og[0], od[0], oa[0], orr])
+            assert og[0]._step == 3 and moe.step_count == 3
+        torch.cuda.synchronize()
+        runs.append(({k: float(v) for k, v in m.items()},
+                     {n: p.detach().clone() for n, p in moe.named_parameters()}, cfg))
+    (ma, pa, cfg), (mb, pb, _) = runs
+    lr = max(cfg.model.generator.lr_g, cfg.model.discriminator.lr_d, cfg.model.aux_reg.lr_a)
+    for n in pa:
+        d = float((pa[n] - pb[n]).abs().max())
+        assert d <= 6 * lr + 1e-7, (n, d)
+    for k in ("gen_loss", "disc_loss", "div_loss", "intensity_loss", "aux_reg_loss"):
+        assert abs(ma[k] - mb[k]) <= 1e-2 * max(abs(ma[k]), 1e-3), (k, ma[k], mb[k])
+    # and the replayed steps really trained: parameters moved away from the captured step's
+    moe0, _, _ = _build()
+    moved = sum(float((p0 - pb[n]).abs().max()) > 0 for n, p0 in moe0.named_parameters())
+    assert moved > 0
