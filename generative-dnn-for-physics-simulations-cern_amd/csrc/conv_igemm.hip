@@ -24,7 +24,7 @@
 //          k is unchanged; each MFMA is an exact fp32 FMA chain).
 #include <cstdlib>
 
-#include "common.h"
+#include "conv_common.h"
 
 // direct kernels for one-input-channel / one-output-channel convolutions (conv_thin.hip)
 int es_thin_conv_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x, const int64_t xs[4], const void* wk,
@@ -37,7 +37,6 @@ int es_thin_conv_wgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, c
 
 namespace {
 
-enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 
 // ES_NO_GLDS=1 (or es_conv_set_glds(0)) forces the register-staged kernels (A/B measurement)
 bool g_no_glds = [] { const char* e = getenv("ES_NO_GLDS"); return e && e[0] == '1'; }();
@@ -63,41 +62,6 @@ struct LdsImg {
   __device__ static __forceinline__ int tr_off(int k, int row) {   // byte offset of (k, row)
     return k * ROWB + ((row * 2) ^ (((k >> 3) & 1) * BROWS));
   }
-};
-
-// Unsigned division by a run-time constant (x < 2^31): q = (umulhi(x, m) + x) >> l.
-struct FastDiv {
-  uint32_t m;
-  int l;
-};
-inline FastDiv mkdiv(uint32_t d) {
-  FastDiv f;
-  f.l = 0;
-  while ((1ull << f.l) < d) ++f.l;
-  f.m = (uint32_t)(((1ull << 32) * ((1ull << f.l) - d)) / d + 1);
-  return f;
-}
-__device__ __forceinline__ int fdiv(int x, FastDiv f) {
-  return (int)((__umulhi((uint32_t)x, f.m) + (uint32_t)x) >> f.l);
-}
-
-struct ConvArgs {
-  FastDiv fC, fS, fK, fQ, fP, fWu, fHu, fUh, fUw, fRSK, fW, fH;
-  int fold;            // DGRAD with integer upsample folded (rows on the source grid)
-  es_conv_desc_t d;
-  const void* a_src;
-  const void* b_src;
-  int64_t as[4];      // FWD: x strides;  DGRAD/WGRAD: dy strides
-  int64_t bs[4];      // WGRAD: x strides
-  void* out;
-  int64_t os[4];      // FWD: y strides; DGRAD: dxu strides
-  const float* bias;
-  float beta;
-  int out_bf16;
-  int M, Ng, Kd;
-  int k_per_split;
-  int dense_f32_out;   // host: output is fp32, dense [M][Ng] and beta == 0 (split-K allowed)
-  int splitk;          // FWD / DGRAD split over blockIdx.z: fp32 atomics into a zeroed dense output
 };
 
 __device__ __forceinline__ int src_row(const int32_t* map, int u) { return map ? map[u] : u; }
@@ -875,6 +839,15 @@ int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
     const bool splitk_better = a.dense_f32_out && tiles < 256 && a.Kd / 64 >= 16;   // see below
     if (avec && bvec && nch % 64 == 0 && a.d.stride <= 2 && a.d.hmap == nullptr && a.M >= 128 && !splitk_better &&
         !g_no_glds) {
+      a.k_per_split = a.Kd;
+      a.splitk = 0;
+      if (a.Kd % 64 == 0) {
+        const int rc = es_conv_ring_launch(a, MODE, st);
+        if (rc) {
+          ES_CHECK_LAUNCH();
+          return ES_OK;
+        }
+      }
       if (a.Ng > 64) return launch_glds<MODE, 128, 128>(a, st);
       return launch_glds<MODE, 128, 64>(a, st);
     }
@@ -886,6 +859,10 @@ int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
   const bool big = a.M >= 128 && a.Ng >= 96 && !splitk_case;
   const int BM = big ? 128 : 64, BN = big ? 128 : 64;
   if constexpr (sizeof(T) == 2 && MODE == MODE_WGRAD) {
+    if (avec && bvec && !g_no_glds && es_conv_ring_launch(a, MODE, st)) {
+      ES_CHECK_LAUNCH();
+      return ES_OK;
+    }
     if (avec && bvec && a.d.K % 128 == 0 && a.d.C % 128 == 0 && a.d.stride <= 2 && a.d.hmap == nullptr &&
         !g_no_glds) {
       const int t128 = (a.M / 128) * (a.Ng / 128);

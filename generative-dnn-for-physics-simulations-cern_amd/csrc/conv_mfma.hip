@@ -1,0 +1,518 @@
+// 8-wave LDS-DMA ring kernels for the bf16 implicit-GEMM convolutions (the generator convs of
+// neutron/generator.py:24,29,33 and proton/generator.py:27,33,38 and the aux-regressor convs:
+// everything whose K-step is one filter tap over 64 contiguous channels).
+//
+// Same products as conv_igemm.hip (FWD: y = conv(x, W); DGRAD: dx with the integer upsample
+// folded; WGRAD: dW), re-tiled for gfx950:
+//   * 512 threads = 8 waves, one workgroup per CU (the 3-slot ring takes up to 144 KiB of the
+//     160 KiB LDS), two waves per SIMD, each wave a 64x64 (64x32 / 32x64) tile of
+//     v_mfma_f32_16x16x32_bf16;
+//   * block tiles 256x128 (FWD/DGRAD) and 128x256 / 256x128 (WGRAD): 48 KiB of operands per
+//     64-deep K-step for 4.2 MFLOP;
+//   * operands go global -> LDS by DMA (buffer_load_dwordx4 ... lds, 1 KiB per wave instruction,
+//     no register round trip) into a 3-slot ring: at step t a wave waits only for ITS pieces of
+//     slot t (s_waitcnt vmcnt(pieces per slot): slot t+1 stays in flight), one s_barrier, then it
+//     issues slot t+2 into the slot everyone finished reading at t-1 and runs the MFMAs of t;
+//   * IMAGE-MINOR ROW ORDER.  GEMM rows (FWD/DGRAD) and GEMM K (WGRAD) enumerate pixels as
+//     (image group g of 64 images, pixel, image within the group): m = (g*PQ + pix)*64 + nl.
+//     Each 8-row DMA piece (and each 64-deep WGRAD K-step) is then 8 (64) images at ONE pixel,
+//     so the im2col gather address of a piece is a per-lane constant (image nl) plus a
+//     WAVE-UNIFORM pixel/tap offset computed on the scalar unit: one VALU add per piece per
+//     K-step instead of a per-lane coordinate decode (which made the first version VALU-issue
+//     bound at ~4x the MFMA time).  Padding / out-of-image taps are uniform per piece and use an
+//     out-of-range buffer offset, which the buffer unit returns as zeros; images beyond N fall
+//     outside the buffer's num_records the same way;
+//   * workgroup ids are remapped so that consecutive tiles (same 64 images, neighbouring pixels)
+//     run on one XCD and share its L2.
+//
+// LDS images (per slot):
+//   FWD/DGRAD  [rows][128 B] per operand, 16-byte chunk c of row r stored at chunk
+//              c ^ ((r >> 1) & 7): the 16-row ds_read_b128 fragment reads are conflict-free.
+//   WGRAD      [64 images][rows] per operand (rows contiguous in global memory: channels), read
+//              with ds_read_b64_tr_b16; chunk c of k-row k stored at c ^ (2(k&3) | 8((k>>3)&1)).
+#include <cstdlib>
+#include <type_traits>
+
+#include "conv_common.h"
+
+namespace {
+
+constexpr int RT = 512;   // threads per workgroup (8 waves)
+constexpr int NSLOT = 3;  // ring depth
+constexpr uint32_t OOB = 0x80000000u;   // buffer offset past every num_records (< 2^31 bytes)
+
+// ES_NO_RING=1 (or es_conv_set_ring(0)) routes these shapes to the 4-wave kernels of
+// conv_igemm.hip (A/B measurement)
+bool g_ring_off = [] { const char* e = getenv("ES_NO_RING"); return e && e[0] == '1'; }();
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mkres(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
+}
+// 64 lanes x 16 bytes -> LDS at lds_wave_base + 16 * lane (M0-based, lane-linear)
+__device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, char* lds_wave_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_wave_base, 16, (int)voff, 0, 0, 0);
+}
+
+// s_barrier without __syncthreads()'s workgroup fence: that fence makes the compiler drain every
+// in-flight LDS-DMA (vmcnt(0)), which would serialise the ring.  The ring's own vmcnt wait before
+// the barrier is what publishes a wave's pieces; the asm memory clobber keeps the compiler from
+// moving LDS accesses across it.
+__device__ __forceinline__ void ring_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// bijective remap: consecutive ids land on one XCD (round-robin dispatch over 8 XCDs)
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+}
+
+// first argument type of a lambda's call operator (the fragment set of a ring's load lambda)
+template <typename F>
+struct lambda_arg : lambda_arg<decltype(&F::operator())> {};
+template <typename C, typename R, typename A0, typename... As>
+struct lambda_arg<R (C::*)(A0, As...) const> {
+  typedef A0 type;
+};
+
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+typedef short short4_t __attribute__((ext_vector_type(4)));
+typedef short short8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ int swz_tr(int k) { return ((k & 3) << 1) | (((k >> 3) & 1) << 3); }
+
+// byte offset of (k-row k, row) in a [64][BROWS] bf16 image
+template <int BROWS>
+__device__ __forceinline__ int tr_off(int k, int row) {
+  return k * (BROWS * 2) + ((((row >> 3) ^ swz_tr(k)) << 4) | ((row & 7) << 1));
+}
+
+// A/B fragment of v_mfma_f32_16x16x32_bf16 from a [k][rows] image: lane l gets row r0 + (l & 15),
+// k = k0 + 8 (l >> 4) + 0..7, as two ds_read_b64_tr_b16.
+template <int BROWS>
+__device__ __forceinline__ bf16x8 tr_frag(const char* img, int k0, int r0) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int ka = k0 + 8 * g + q;
+  const char* p0 = img + tr_off<BROWS>(ka, r0 + 4 * p);
+  const char* p1 = img + tr_off<BROWS>(ka + 4, r0 + 4 * p);
+  short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)p0);
+  short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)p1);
+  short8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// The ring main loop shared by the kernels.  Slot of K-step t = t % 3; two register fragment
+// sets: the kk = 1 half of step t is read from LDS while the MFMAs of the kk = 0 half run, and the
+// kk = 0 half of step t+1 while the kk = 1 MFMAs of step t run, so LDS latency hides behind MFMA
+// work.  Per step, one barrier (after this wave's reads of slot t have completed and its DMA
+// pieces of slot t+1 have landed): behind it every wave has finished slot t, which then takes the
+// DMA of step t+3, and slot t+1 is complete.
+template <int PW, typename Issue, typename Load, typename Mma>
+__device__ __forceinline__ void ring_loop(int nk, char* smem, int slot_bytes, Issue& issue, Load& load, Mma& mma) {
+  using Frag = typename std::remove_reference<typename lambda_arg<Load>::type>::type;
+  // issue() is called for steps 0, 1, 2, ... unconditionally; steps >= nk are all-OOB (zero-fill,
+  // no memory traffic), so every iteration keeps exactly two steps in flight and the loop body is
+  // one basic block (the compiler's LDS waits stay counted instead of draining at branch joins)
+  issue(smem);
+  issue(smem + slot_bytes);
+  wait_vmcnt<PW>();
+  ring_barrier();
+  issue(smem + 2 * slot_bytes);
+  Frag f0, f1;
+  load(f0, smem, 0);
+  int cur = 0;
+  for (int t = 0; t < nk - 1; ++t) {
+    load(f1, smem + cur * slot_bytes, 1);
+    mma(f0);
+    const int nxt = cur == 2 ? 0 : cur + 1;
+    wait_vmcnt<PW>();                                    // step t+1 landed (this wave's pieces)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of slot t are done
+    ring_barrier();
+    load(f0, smem + nxt * slot_bytes, 0);
+    issue(smem + cur * slot_bytes);                      // step t+3
+    mma(f1);
+    cur = nxt;
+  }
+  load(f1, smem + cur * slot_bytes, 1);
+  mma(f0);
+  mma(f1);
+  wait_vmcnt<0>();   // drain the zero-fill steps before the workgroup may exit
+}
+
+// Pixel grid of the GEMM rows: FWD output pixels, DGRAD input pixels (source grid when folded).
+struct RowGrid {
+  int h, w;
+};
+template <int MODE>
+__device__ __forceinline__ RowGrid row_grid(const ConvArgs& a) {
+  const es_conv_desc_t& d = a.d;
+  if constexpr (MODE == MODE_FWD) return {d.P, d.Q};
+  else return a.fold ? RowGrid{d.H, d.W} : RowGrid{d.Hu, d.Wu};
+}
+
+// ---------------------------------------------------------------------------------------------
+// FWD / DGRAD.  Rows m = (g*PQ + pix)*64 + nl (image n = 64 g + nl, pixel pix on the row grid),
+// columns = channels of the packed weight, K-step = one tap x 64 channels.
+// ---------------------------------------------------------------------------------------------
+template <int MODE, int BM, int BN>
+__global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
+  constexpr int WM = BM / 4, WN = BN / 2;       // 4 x 2 waves
+  constexpr int RM = WM / 16, RN = WN / 16;
+  constexpr int APW = BM / 64, BPW = BN / 64;   // 1 KiB pieces per wave per slot
+  constexpr int PW = APW + BPW;
+  constexpr int ABYTES = BM * 128, SLOT = (BM + BN) * 128;
+  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT];
+  const es_conv_desc_t& d = a.d;
+  const RowGrid rg = row_grid<MODE>(a);
+  const int PQ = rg.h * rg.w;
+  const int nblk = ((d.N + 63) >> 6) * PQ;      // 64-row blocks
+
+  // tile order: the column tiles of one row tile are consecutive (they share the gathered rows)
+  const int nt = gridDim.y;
+  const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * nt);
+  const int m0 = (wg / nt) * BM, n0 = (wg % nt) * BN;
+
+  const int lane = threadIdx.x & 63, wid = uni(threadIdx.x >> 6);
+  const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
+  const int lrow = lane >> 3, pc = lane & 7;
+
+  const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * 2));
+  const int ldb = (MODE == MODE_DGRAD && a.fold) ? d.R * d.S * d.K : a.Kd;
+  const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)(a.Ng * ldb * 2));
+  const int as2b = (int)a.as[2] * 2, as3b = (int)a.as[3] * 2;
+
+  // A pieces: per-lane constant (image, 16-byte chunk) + per-piece uniform pixel coordinates
+  uint32_t alane[APW];
+  int pc0[APW], pc1[APW];   // uniform: FWD p*st-pad, q*st-pad; DGRAD (folded) i*up+pad, j*up+pad
+  bool pval[APW];
+#pragma unroll
+  for (int j = 0; j < APW; ++j) {
+    const int pi = wid * APW + j;                 // piece of the tile (8 rows)
+    const int blk = (m0 >> 6) + (pi >> 3);        // 64-row block: (g, pix)
+    const int nl = ((pi & 7) << 3) + lrow;
+    const int rr = pi * 8 + lrow;                 // row within the tile (swizzle)
+    const int lc = pc ^ ((rr >> 1) & 7);
+    pval[j] = blk < nblk;
+    const int bb = pval[j] ? blk : 0;
+    const int g = bb / PQ, pix = bb - g * PQ;
+    const int y = pix / rg.w, x = pix - y * rg.w;
+    alane[j] = (uint32_t)((g * 64 + nl) * (int)a.as[0] * 2 + lc * 16);
+    if constexpr (MODE == MODE_FWD) {
+      pc0[j] = y * d.stride - d.pad;
+      pc1[j] = x * d.stride - d.pad;
+    } else if (a.fold) {
+      pc0[j] = y * d.up_h + d.pad;
+      pc1[j] = x * d.up_w + d.pad;
+    } else {
+      pc0[j] = y + d.pad;
+      pc1[j] = x + d.pad;
+    }
+  }
+  uint32_t blane[BPW];
+#pragma unroll
+  for (int j = 0; j < BPW; ++j) {
+    const int rr = (wid * BPW + j) * 8 + lrow;
+    // rows past Ng land past num_records (zeros)
+    blane[j] = (uint32_t)((n0 + rr) * ldb * 2 + ((pc ^ ((rr >> 1) & 7)) * 16));
+  }
+
+  // K-step cursor (uniform, advanced once per issued slot): FWD kk = ((r*S + s)*C + ch);
+  // DGRAD kk = (((ua*up_w + ub)*R + r)*S + s)*K + ch with weight column kb = kk mod R*S*K
+  int cr = 0, cs = 0, cch = 0, cua = 0, cub = 0, ckb = 0, cstep = 0;
+  const int nch = MODE == MODE_FWD ? d.C : d.K;
+  const int upw = d.up_w > 0 ? d.up_w : 1;
+  const int nk = a.Kd / 64;
+  auto issue = [&](char* slot) {
+    const bool live = cstep < nk;
+#pragma unroll
+    for (int j = 0; j < APW; ++j) {
+      uint32_t u;
+      if constexpr (MODE == MODE_FWD) {
+        const int hu = pc0[j] + cr, wu = pc1[j] + cs;
+        const bool ok = live && pval[j] && (unsigned)hu < (unsigned)d.Hu && (unsigned)wu < (unsigned)d.Wu;
+        // integer nearest upsample folded into the gather (factor 1 without upsample)
+        const int sh = fdiv(hu, a.fUh), sw = fdiv(wu, a.fUw);
+        u = ok ? (uint32_t)(sh * as2b + sw * as3b + cch * 2) : OOB;
+      } else {
+        const int ph = pc0[j] + cua - cr, pw = pc1[j] + cub - cs;
+        const int sp = d.stride == 2 ? 1 : 0;
+        const bool ok = live && pval[j] && ph >= 0 && pw >= 0 && !(((ph | pw) & sp)) &&
+                        (ph >> sp) < d.P && (pw >> sp) < d.Q;
+        u = ok ? (uint32_t)((ph >> sp) * as2b + (pw >> sp) * as3b + cch * 2) : OOB;
+      }
+      bdma16(ares, alane[j] + u, slot + (wid * APW + j) * 1024);
+    }
+    const int kb = MODE == MODE_FWD ? (cr * d.S + cs) * d.C + cch : ckb;
+    const uint32_t ub = live ? (uint32_t)(kb * 2) : OOB;
+#pragma unroll
+    for (int j = 0; j < BPW; ++j) bdma16(bres, blane[j] + ub, slot + ABYTES + (wid * BPW + j) * 1024);
+    // advance the cursor (selects, no branches)
+    ++cstep;
+    cch += 64;
+    ckb += 64;
+    const bool w1 = cch == nch;
+    cch = w1 ? 0 : cch;
+    cs += w1;
+    const bool w2 = cs == d.S;
+    cs = w2 ? 0 : cs;
+    cr += w2;
+    const bool w3 = cr == d.R;
+    cr = w3 ? 0 : cr;
+    ckb = w3 ? 0 : ckb;
+    cub += w3;
+    const bool w4 = cub == upw;
+    cub = w4 ? 0 : cub;
+    cua += w4;
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int r16 = lane & 15, g16 = lane >> 4;
+  struct Frag {
+    bf16x8 a[RM], b[RN];
+  };
+  auto load = [&](Frag& f, const char* slot, int kk) {
+    const int seg = kk * 4 + g16;
+#pragma unroll
+    for (int i = 0; i < RM; ++i) f.a[i] = *(const bf16x8*)(slot + swz(wm0 + i * 16 + r16, seg));
+#pragma unroll
+    for (int j = 0; j < RN; ++j) f.b[j] = *(const bf16x8*)(slot + ABYTES + swz(wn0 + j * 16 + r16, seg));
+  };
+  auto mma = [&](const Frag& f) {
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
+  };
+  ring_loop<PW>(nk, smem, SLOT, issue, load, mma);
+
+  // epilogue: the wave's WM (<= 64) rows lie in one 64-row block -> one pixel, images nl
+  const int mw = m0 + wm0;
+  const int blk = mw >> 6;
+  if (blk >= nblk) return;
+  const int g = blk / PQ, pix = blk - g * PQ;
+  const int y = pix / rg.w, x = pix - y * rg.w;
+  const int64_t pixoff = (int64_t)y * a.os[2] + (int64_t)x * a.os[3];
+  const int col16 = lane & 15, rq = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int n = g * 64 + (mw & 63) + i * 16 + rq + jj;
+      if (n >= d.N) continue;
+      const int64_t rowoff = (int64_t)n * a.os[0] + pixoff;
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int ng = n0 + wn0 + j * 16 + col16;
+        if (ng >= a.Ng) continue;
+        float v = acc[i][j][jj];
+        if constexpr (MODE == MODE_FWD) {
+          if (a.bias) v += a.bias[ng];
+        }
+        const int64_t o = rowoff + (int64_t)ng * a.os[1];
+        if (a.out_bf16) {
+          bf16* yp = (bf16*)a.out + o;
+          if (a.beta != 0.f) v += a.beta * (float)(*yp);
+          *yp = (bf16)v;
+        } else {
+          float* yp = (float*)a.out + o;
+          if (a.beta != 0.f) v += a.beta * (*yp);
+          *yp = v;
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// WGRAD: dW[m = k][ng = (r, s, c)] = sum over pixels of dy[pix][k] * xu[pix + (r, s)][c].
+// Block tile BM out-channels x BN in-channels of ONE tap (C % BN == 0).  K-step t = (output
+// pixel t / G, image group t % G): 64 images at one pixel.  Split over blockIdx.z with fp32
+// atomics into the zeroed dw.
+// ---------------------------------------------------------------------------------------------
+template <int BM, int BN>
+__global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
+  constexpr int WGM = BM / 64, WGN = 8 / WGM;   // waves along M / N
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int RM = WM / 16, RN = WN / 16;
+  constexpr int AIMG = 64 * BM * 2, SLOT = 64 * (BM + BN) * 2;
+  constexpr int APW = BM / 64, BPW = BN / 64;   // 1 KiB pieces per wave per slot
+  constexpr int PW = APW + BPW;
+  constexpr int ALPR = BM / 8, BLPR = BN / 8;   // lanes (16-byte chunks) per k-row
+  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT];
+  const es_conv_desc_t& d = a.d;
+  const int G = (d.N + 63) >> 6;
+
+  // blocks of one K split (same pixels) are consecutive on one XCD
+  const int mt = gridDim.x, ntl = gridDim.y, tiles = mt * ntl;
+  const int orig = blockIdx.x + (blockIdx.y + blockIdx.z * ntl) * mt;
+  const int wg = xcd_remap(orig, tiles * gridDim.z);
+  const int tile = wg % tiles, split = wg / tiles;
+  const int m0 = (tile % mt) * BM, n0 = (tile / mt) * BN;
+  const int tbeg = split * a.k_per_split;       // in K-steps
+  const int tend = min(d.P * d.Q * G, tbeg + a.k_per_split);
+
+  const int lane = threadIdx.x & 63, wid = uni(threadIdx.x >> 6);
+  const int wm0 = (wid / WGN) * WM, wn0 = (wid % WGN) * WN;
+  const int rs = n0 / d.C, cb = n0 - rs * d.C;
+  const int tr = rs / d.S, ts = rs - tr * d.S;
+  const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * 2));
+  const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)(d.N * a.bs[0] * 2));
+  const int as0b = (int)a.as[0] * 2, as2b = (int)a.as[2] * 2, as3b = (int)a.as[3] * 2;
+  const int bs0b = (int)a.bs[0] * 2, bs2b = (int)a.bs[2] * 2, bs3b = (int)a.bs[3] * 2;
+
+  uint32_t alane[APW], blane[BPW];
+#pragma unroll
+  for (int j = 0; j < APW; ++j) {
+    const int kr = (wid * APW + j) * (64 / ALPR) + lane / ALPR;   // image of the K-step
+    alane[j] = (uint32_t)(kr * as0b + (m0 + ((lane % ALPR) ^ swz_tr(kr)) * 8) * 2);
+  }
+#pragma unroll
+  for (int j = 0; j < BPW; ++j) {
+    const int kr = (wid * BPW + j) * (64 / BLPR) + lane / BLPR;
+    blane[j] = (uint32_t)(kr * bs0b + (cb + ((lane % BLPR) ^ swz_tr(kr)) * 8) * 2);
+  }
+
+  // K-step cursor (uniform): output pixel (p, q) and image group gi of step t = (p*Q + q)*G + gi
+  int cp, cq, cg, cstep = tbeg;
+  {
+    const int pix = tbeg / G;
+    cg = tbeg - pix * G;
+    cp = pix / d.Q;
+    cq = pix - cp * d.Q;
+  }
+  auto issue = [&](char* slot) {
+    const bool live = cstep < tend;
+    const uint32_t ua = live ? (uint32_t)(cg * 64 * as0b + cp * as2b + cq * as3b) : OOB;
+    const int hu = cp * d.stride - d.pad + tr, wu = cq * d.stride - d.pad + ts;
+    const bool ok = live && (unsigned)hu < (unsigned)d.Hu && (unsigned)wu < (unsigned)d.Wu;
+    const uint32_t ub = ok ? (uint32_t)(cg * 64 * bs0b + fdiv(hu, a.fUh) * bs2b + fdiv(wu, a.fUw) * bs3b) : OOB;
+#pragma unroll
+    for (int j = 0; j < APW; ++j) bdma16(ares, alane[j] + ua, slot + (wid * APW + j) * 1024);
+#pragma unroll
+    for (int j = 0; j < BPW; ++j) bdma16(bres, blane[j] + ub, slot + AIMG + (wid * BPW + j) * 1024);
+    ++cstep;
+    ++cg;
+    const bool w1 = cg == G;
+    cg = w1 ? 0 : cg;
+    cq += w1;
+    const bool w2 = cq == d.Q;
+    cq = w2 ? 0 : cq;
+    cp += w2;
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (tbeg >= tend) return;
+  struct Frag {
+    bf16x8 a[RM], b[RN];
+  };
+  auto load = [&](Frag& f, const char* slot, int kk) {
+#pragma unroll
+    for (int i = 0; i < RM; ++i) f.a[i] = tr_frag<BM>(slot, kk * 32, wm0 + i * 16);
+#pragma unroll
+    for (int j = 0; j < RN; ++j) f.b[j] = tr_frag<BN>(slot + AIMG, kk * 32, wn0 + j * 16);
+  };
+  auto mma = [&](const Frag& f) {
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
+  };
+  ring_loop<PW>(tend - tbeg, smem, SLOT, issue, load, mma);
+  const int col16 = lane & 15, rq = (lane >> 4) * 4;
+  float* out = (float*)a.out;
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int m = m0 + wm0 + i * 16 + rq + jj;
+#pragma unroll
+      for (int j = 0; j < RN; ++j) atomicAdd(out + (int64_t)m * a.Ng + n0 + wn0 + j * 16 + col16, acc[i][j][jj]);
+    }
+}
+
+template <int MODE, int BM, int BN>
+void launch_ring(const ConvArgs& a, int rows, hipStream_t st) {
+  dim3 grid((rows + BM - 1) / BM, (a.Ng + BN - 1) / BN, 1);
+  hipLaunchKernelGGL((conv_ring_kernel<MODE, BM, BN>), grid, dim3(RT), 0, st, a);
+}
+
+template <int BM, int BN>
+void launch_wgrad_ring(ConvArgs& a, hipStream_t st) {
+  const int tiles = (a.M / BM) * (a.Ng / BN);
+  const int ks = a.d.P * a.d.Q * ((a.d.N + 63) / 64);   // K-steps
+  // one workgroup per CU: aim at two full rounds of the 256 CUs, >= 8 K-steps per split
+  const int want = max(1, min(ks / 8, 512 / tiles));
+  const int per = (ks + want - 1) / want;
+  a.k_per_split = per;
+  dim3 grid(a.M / BM, a.Ng / BN, (ks + per - 1) / per);
+  hipLaunchKernelGGL((wgrad_ring_kernel<BM, BN>), grid, dim3(RT), 0, st, a);
+}
+
+// a dense NHWC image stack (n outermost, rows of c contiguous values) below 2 GiB in bytes
+bool dense_small(const int64_t s[4], int n, int c, int h, int w) {
+  return s[1] == 1 && s[3] == c && s[2] == (int64_t)w * c && s[0] == (int64_t)h * w * c &&
+         (int64_t)n * s[0] * 2 < (1ll << 30);
+}
+
+}  // namespace
+
+extern "C" int es_conv_set_ring(int on) {
+  const int old = !g_ring_off;
+  g_ring_off = !on;
+  return old;
+}
+
+int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
+  if (g_ring_off) return 0;
+  const es_conv_desc_t& d = a.d;
+  if (d.hmap != nullptr || d.stride > 2 || a.splitk) return 0;
+  if (mode == MODE_WGRAD) {
+    if (!dense_small(a.as, d.N, d.K, d.P, d.Q) || !dense_small(a.bs, d.N, d.C, d.H, d.W)) return 0;
+    if (d.K % 256 == 0 && d.C % 128 == 0) launch_wgrad_ring<256, 128>(a, st);
+    else if (d.K % 128 == 0 && d.C % 256 == 0) launch_wgrad_ring<128, 256>(a, st);
+    else if (d.K % 128 == 0 && d.C % 128 == 0) launch_wgrad_ring<128, 128>(a, st);
+    else return 0;
+    return 1;
+  }
+  // caller checked: bf16, channels % 64 == 0, K % 64 == 0 per step
+  int rows;
+  if (mode == MODE_FWD) {
+    if (!dense_small(a.as, d.N, d.C, d.H, d.W)) return 0;
+    rows = ((d.N + 63) / 64) * 64 * d.P * d.Q;
+  } else {
+    if (!dense_small(a.as, d.N, d.K, d.P, d.Q)) return 0;
+    rows = ((d.N + 63) / 64) * 64 * (a.fold ? d.H * d.W : d.Hu * d.Wu);
+  }
+  if ((int64_t)a.Ng * a.Kd * 2 >= (1ll << 30)) return 0;
+  const int nt128 = (a.Ng + 127) / 128;
+  const bool big_rows = ((rows + 255) / 256) * nt128 >= 768;   // >= 3 rounds of 256-row tiles
+  if (mode == MODE_FWD) {
+    if (a.Ng <= 64) big_rows ? launch_ring<MODE_FWD, 256, 64>(a, rows, st) : launch_ring<MODE_FWD, 128, 64>(a, rows, st);
+    else big_rows ? launch_ring<MODE_FWD, 256, 128>(a, rows, st) : launch_ring<MODE_FWD, 128, 128>(a, rows, st);
+  } else {
+    if (a.Ng <= 64) big_rows ? launch_ring<MODE_DGRAD, 256, 64>(a, rows, st) : launch_ring<MODE_DGRAD, 128, 64>(a, rows, st);
+    else big_rows ? launch_ring<MODE_DGRAD, 256, 128>(a, rows, st) : launch_ring<MODE_DGRAD, 128, 128>(a, rows, st);
+  }
+  return 1;
+}

@@ -57,6 +57,7 @@ _SIGS = {
     "es_version": (C.c_int, []),
     "es_device_sync": (C.c_int, []),
     "es_conv_set_glds": (C.c_int, [C.c_int]),
+    "es_conv_set_ring": (C.c_int, [C.c_int]),
     "es_conv2d_fwd": (C.c_int, [P, C.c_int, P, P, P, P, P, C.c_int, P, P]),
     "es_conv2d_dgrad": (C.c_int, [P, C.c_int, P, P, P, P, C.c_int, P, C.c_float, P]),
     "es_conv2d_wgrad": (C.c_int, [P, C.c_int, P, P, P, P, P, P]),

@@ -84,6 +84,9 @@ typedef struct {
  * 0 = register-staged kernel.  Both accumulate in the same order (bit-identical results); the
  * switch exists for A/B measurement and tests.  Returns the previous setting. */
 int es_conv_set_glds(int on);
+/* Select the 8-wave LDS-DMA ring kernels (conv_mfma.hip) for the bf16 convs whose K-step is one tap
+ * x 64 channels: 1 = on (default), 0 = use the 4-wave kernels.  Returns the previous setting. */
+int es_conv_set_ring(int on);
 
 int es_conv2d_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x, const int64_t xs[4],
                   const void* wk, const float* bias, void* y, es_dtype_t ydt, const int64_t ys[4],

@@ -316,3 +316,56 @@ def test_randn_moments():
     assert abs(out.mean().item()) < 5e-3 and abs(out.std().item() - 1) < 5e-3
     hip.call("es_rand_exponential", hip.ptr(out), out.numel(), 99, 4, hip.stream_ptr())
     assert abs(out.mean().item() - 1) < 5e-3 and out.min().item() > 0
+
+
+RING_CASES = [
+    # bf16 shapes on the 8-wave ring kernels (conv_mfma.hip); rows not a multiple of the tile
+    (3, 256, 24, 24, 128, 3, 1, 0, (2, 2)),       # G conv_layers.5: 256x128 FWD, folded DGRAD, WGRAD 128x256
+    (7, 128, 13, 13, 256, 3, 1, 0, (2, 2)),       # G conv_layers.0: WGRAD 256x128
+    (5, 128, 46, 46, 64, 2, 1, 0, None),          # G conv_layers.9: Ng = 64 tiles
+    (3, 128, 17, 15, 128, 3, 2, 1, None),         # stride 2 + padding, WGRAD 128x128
+    (2, 512, 18, 10, 256, 4, 1, 1, (2, 2)),       # proton G conv_layers.1 (pad 1, up x2)
+]
+
+
+@pytest.mark.parametrize("case", RING_CASES)
+def test_conv_ring_matches_4wave(case):
+    """The 8-wave ring kernels accumulate each output in the same K order as the 4-wave LDS-DMA
+    kernels: bf16 fwd / dgrad outputs bit-identical, wgrad equal up to the order of the split-K
+    fp32 atomics, and all close to torch fp32."""
+    hip = _hip()
+    from expertsim.layers import ConvOp, Upsample
+    N, Cin, H, W, Cout, k, st, pad, up = case
+    torch.manual_seed(11)
+    x = torch.randn(N, Cin, H, W)
+    w = torch.randn(Cout, Cin, k, k) / np.sqrt(Cin * k * k)
+    b = torch.randn(Cout)
+    upsample = Upsample((H, W), scale=up) if up else None
+    op = ConvOp(torch.nn.Parameter(w.to(DEV)), torch.nn.Parameter(b.to(DEV)), stride=st, pad=pad, upsample=upsample)
+    xa = to_act(x, torch.bfloat16)
+    outs = []
+    gy = None
+    try:
+        for on in (1, 0):
+            hip.lib().es_conv_set_ring(on)
+            ya = op.fwd(xa, out_dtype=torch.bfloat16)
+            if gy is None:
+                gy = torch.randn(ya.dims, generator=torch.Generator().manual_seed(3))
+            gya = to_act(gy, torch.bfloat16)
+            dxa = op.dgrad(gya, xa, dx_dtype=torch.bfloat16)
+            dw = torch.zeros(Cout, Cin, k, k, device=DEV)
+            op.wgrad(gya, xa, dw, None, beta=1.0)
+            torch.cuda.synchronize()
+            outs.append((ya.t.clone(), dxa.t.clone(), dw.cpu()))
+    finally:
+        hip.lib().es_conv_set_ring(1)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    assert rel(outs[0][2], outs[1][2]) < 1e-5
+    xu = F.interpolate(x, scale_factor=up, mode="nearest") if up else x
+    wr = w.clone().requires_grad_(True)
+    xr = xu.clone().requires_grad_(True)
+    y = F.conv2d(xr, wr, b, st, pad)
+    y.backward(gy.to(torch.bfloat16).float())
+    assert rel(outs[0][0].float().cpu().view(y.shape[0], y.shape[2], y.shape[3], -1).permute(0, 3, 1, 2), y) < 3e-2
+    assert rel(outs[0][2], wr.grad) < 3e-2

@@ -1,0 +1,78 @@
+"""Micro-benchmark of the bf16 conv kernels on the neutron generator's layer shapes (GPU; HIP-event
+timing on the current stream).  Each op runs with the 8-wave ring kernels (default) and with them
+disabled (es_conv_set_ring(0)); fwd/dgrad outputs of the two must be bit-identical.
+
+usage: python tools/mb_conv.py [batch]"""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "generative-dnn-for-physics-simulations-cern_amd"))
+
+from expertsim import hip  # noqa: E402
+from expertsim.layers import Act, ConvOp, Upsample  # noqa: E402
+
+
+def timed(fn, reps=10):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps * 1e3   # us
+
+
+def case(name, N, Cin, H, W, Cout, k, st, pad, up):
+    dev = "cuda"
+    w = torch.nn.Parameter(torch.randn(Cout, Cin, k, k, device=dev) / (Cin * k * k) ** 0.5)
+    b = torch.nn.Parameter(torch.randn(Cout, device=dev))
+    op = ConvOp(w, b, stride=st, pad=pad, upsample=Upsample((H, W), scale=up) if up else None)
+    x = Act.nhwc(N, Cin, H, W, torch.bfloat16, dev)
+    x.t.normal_()
+    y = op.fwd(x, out_dtype=torch.bfloat16)
+    dy = y.like_nhwc(torch.bfloat16)
+    dy.t.normal_()
+    P, Q = y.dims[2], y.dims[3]
+    flops = 2.0 * N * P * Q * Cout * Cin * k * k
+    dw = torch.zeros(Cout, Cin, k, k, device=dev)
+    res = {}
+    for on in (1, 0):
+        hip.lib().es_conv_set_ring(on)
+        yy = op.fwd(x, out_dtype=torch.bfloat16)
+        dx = op.dgrad(dy, x, dx_dtype=torch.bfloat16)
+        dw.zero_()
+        op.wgrad(dy, x, dw, None, beta=1.0)
+        torch.cuda.synchronize()
+        res[on] = (yy.t.clone(), dx.t.clone(), dw.clone(),
+                   timed(lambda: op.fwd(x, out_dtype=torch.bfloat16)),
+                   timed(lambda: op.dgrad(dy, x, dx_dtype=torch.bfloat16)),
+                   timed(lambda: op.wgrad(dy, x, None, None)))
+    hip.lib().es_conv_set_ring(1)
+    same_f = torch.equal(res[1][0], res[0][0])
+    same_d = torch.equal(res[1][1], res[0][1])
+    wrel = float((res[1][2] - res[0][2]).abs().max() / res[0][2].abs().max())
+    line = f"{name:34s} {flops / 1e9:7.1f} GF |"
+    for lab, i in (("fwd", 3), ("dgrad", 4), ("wgrad", 5)):
+        line += (f" {lab} ring {res[1][i]:7.1f} us {flops / res[1][i] / 1e6:6.1f} TF"
+                 f" / 4w {res[0][i]:7.1f} us {flops / res[0][i] / 1e6:6.1f} TF |")
+    line += f" fwd==:{same_f} dgrad==:{same_d} wgrad rel {wrel:.1e}"
+    print(line, flush=True)
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+    hip.lib()
+    case("G c0 128->256 k3 up2 13->24", B, 128, 13, 13, 256, 3, 1, 0, (2, 2))
+    case("G c5 256->128 k3 up2 24->46", B, 256, 24, 24, 128, 3, 1, 0, (2, 2))
+    case("G c9 128->64 k2 46->45", B, 128, 46, 46, 64, 2, 1, 0, None)
+    case("A conv3 64->128 k3 9x19", B, 64, 9, 19, 128, 3, 1, 0, None)
+    case("A conv4 128->256 k3 3x17", B, 128, 3, 17, 256, 3, 1, 0, None)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,59 @@
+"""Run ONE conv op of the neutron generator a few times (for rocprofv3 --pmc passes).
+
+usage: python tools/mb_one.py <c0|c5|c9> <fwd|dgrad|wgrad> [ring 1|0] [reps]"""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "generative-dnn-for-physics-simulations-cern_amd"))
+
+from expertsim import hip  # noqa: E402
+from expertsim.layers import Act, ConvOp, Upsample  # noqa: E402
+
+SHAPES = {"c0": (512, 128, 13, 13, 256, 3, 1, 0, (2, 2)), "c5": (512, 256, 24, 24, 128, 3, 1, 0, (2, 2)),
+          "c9": (512, 128, 46, 46, 64, 2, 1, 0, None)}
+
+
+def main():
+    layer, mode = sys.argv[1], sys.argv[2]
+    ring = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+    reps = int(sys.argv[4]) if len(sys.argv) > 4 else 5
+    N, Cin, H, W, Cout, k, st, pad, up = SHAPES[layer]
+    dev = "cuda"
+    hip.lib().es_conv_set_ring(ring)
+    w = torch.nn.Parameter(torch.randn(Cout, Cin, k, k, device=dev) / (Cin * k * k) ** 0.5)
+    b = torch.nn.Parameter(torch.randn(Cout, device=dev))
+    op = ConvOp(w, b, stride=st, pad=pad, upsample=Upsample((H, W), scale=up) if up else None)
+    x = Act.nhwc(N, Cin, H, W, torch.bfloat16, dev)
+    x.t.normal_()
+    y = op.fwd(x, out_dtype=torch.bfloat16)
+    dy = y.like_nhwc(torch.bfloat16)
+    dy.t.normal_()
+    op.packed(torch.bfloat16, 1)
+    torch.cuda.synchronize()
+
+    def run():
+        if mode == "fwd":
+            op.fwd(x, out_dtype=torch.bfloat16)
+        elif mode == "dgrad":
+            op.dgrad(dy, x, dx_dtype=torch.bfloat16)
+        else:
+            op.wgrad(dy, x, None, None)
+    run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / reps * 1e3
+    flops = 2.0 * N * y.dims[2] * y.dims[3] * Cout * Cin * k * k
+    print(f"{layer} {mode} ring={ring} dbg={os.environ.get('ES_RING_DBG', '0')}: {us:.1f} us "
+          f"{flops / us / 1e6:.1f} TF", flush=True)
+
+
+if __name__ == "__main__":
+    main()
