@@ -22,6 +22,22 @@ __device__ __forceinline__ int fdiv(int x, FastDiv f) {
   return (int)((__umulhi((uint32_t)x, f.m) + (uint32_t)x) >> f.l);
 }
 
+// Sub-pixel decomposition of a stride-1 conv over a x2 nearest-upsampled input (conv_mfma.hip).
+// Output pixels split into 4 parity classes c = 2a + b, (p - pad) mod 2 = a, (q - pad) mod 2 = b.
+// Class c covers output rows p = p0[c] + 2u (u < ph[c]) and is a plain dh[c] x dw[c] conv on the
+// SOURCE grid: y[p0 + 2u][q0 + 2v] = sum_{d,e} x[u + oh + d][v + ow + e] * W'_c[d][e] with
+// W'_c[d][e] = sum of W[r][s] over r in {2d - a, 2d - a + 1}, s in {2e - b, 2e - b + 1} (in range).
+struct SubPixel {
+  int on;
+  int ph[4], pw[4];      // class grid
+  int p0[4], q0[4];      // first output row / column of the class
+  int oh[4], ow[4];      // source row of (u, d) = u + oh + d
+  int dh[4], dw[4];      // combined taps
+  int tap0[5];           // prefix sums of dh*dw (packed weight blocks)
+  int tile0[5];          // FWD: prefix sums of the classes' row tiles
+};
+void es_make_subpixel(const es_conv_desc_t& d, int row_tile, SubPixel& sp);
+
 struct ConvArgs {
   FastDiv fC, fS, fK, fQ, fP, fWu, fHu, fUh, fUw, fRSK, fW, fH;
   int fold;            // DGRAD with integer upsample folded (rows on the source grid)
@@ -39,6 +55,7 @@ struct ConvArgs {
   int k_per_split;
   int dense_f32_out;   // host: output is fp32, dense [M][Ng] and beta == 0 (split-K allowed)
   int splitk;          // FWD / DGRAD split over blockIdx.z: fp32 atomics into a zeroed dense output
+  SubPixel sp;         // ring kernels: sub-pixel class geometry (sp.on)
 };
 
 

@@ -943,6 +943,20 @@ int check_desc(const es_conv_desc_t* d) {
   return ES_OK;
 }
 
+// sub-pixel FWD / DGRAD: only the ring kernels read mode 2 / 3 packed weights
+int ring_direct(ConvArgs& a, int mode, hipStream_t st) {
+  a.fC = mkdiv(a.d.C); a.fS = mkdiv(a.d.S); a.fK = mkdiv(a.d.K); a.fQ = mkdiv(a.d.Q);
+  a.fP = mkdiv(a.d.P); a.fWu = mkdiv(a.d.Wu); a.fHu = mkdiv(a.d.Hu);
+  a.fUh = mkdiv(2); a.fUw = mkdiv(2);
+  a.fRSK = mkdiv(a.d.R * a.d.S * a.d.K); a.fW = mkdiv(a.d.W); a.fH = mkdiv(a.d.H);
+  a.k_per_split = a.Kd;
+  a.splitk = 0;
+  const int rc = es_conv_ring_launch(a, mode, st);
+  ES_CHECK_ARG(rc > 0, "conv: sub-pixel operands not dense NHWC (ring kernels required)");
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
 }  // namespace
 
 extern "C" int es_conv_set_glds(int on) {
@@ -955,6 +969,7 @@ extern "C" int es_conv2d_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void*
                              const int64_t xs[4], const void* wk, const float* bias, void* y,
                              es_dtype_t ydt, const int64_t ys[4], es_stream_t stream) {
   if (int e = check_desc(d)) return e;
+  if (d->subpixel) ES_CHECK_ARG(es_conv_subpixel_ok(d, dt), "conv fwd: sub-pixel weights for a conv the sub-pixel path cannot run");
   if (es_thin_conv_fwd(d, dt, x, xs, wk, bias, y, ydt, ys, (hipStream_t)stream)) {
     ES_CHECK_LAUNCH();
     return ES_OK;
@@ -968,6 +983,7 @@ extern "C" int es_conv2d_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void*
   const int vn = dt == ES_BF16 ? 8 : 4;
   const bool avec = xs[1] == 1 && d->C % vn == 0;
   const bool bvec = a.Kd % vn == 0;
+  if (d->subpixel) return ring_direct(a, MODE_FWD, (hipStream_t)stream);
   return dispatch<MODE_FWD>(a, dt, avec, bvec, (hipStream_t)stream);
 }
 
@@ -975,6 +991,7 @@ extern "C" int es_conv2d_dgrad(const es_conv_desc_t* d, es_dtype_t dt, const voi
                                const int64_t ys[4], const void* wd, void* dxu, es_dtype_t dxdt,
                                const int64_t dxs[4], float beta, es_stream_t stream) {
   if (int e = check_desc(d)) return e;
+  if (d->subpixel) ES_CHECK_ARG(es_conv_subpixel_ok(d, dt), "conv dgrad: sub-pixel weights for a conv the sub-pixel path cannot run");
   if (es_thin_conv_dgrad(d, dt, dy, ys, wd, dxu, dxdt, dxs, beta, (hipStream_t)stream)) {
     ES_CHECK_LAUNCH();
     return ES_OK;
@@ -994,6 +1011,7 @@ extern "C" int es_conv2d_dgrad(const es_conv_desc_t* d, es_dtype_t dt, const voi
   const int vn = dt == ES_BF16 ? 8 : 4;
   const bool avec = ys[1] == 1 && d->K % vn == 0;
   const bool bvec = a.Kd % vn == 0;
+  if (d->subpixel) return ring_direct(a, MODE_DGRAD, (hipStream_t)stream);
   return dispatch<MODE_DGRAD>(a, dt, avec, bvec, (hipStream_t)stream);
 }
 
@@ -1017,6 +1035,57 @@ extern "C" int es_conv2d_wgrad(const es_conv_desc_t* d, es_dtype_t dt, const voi
 
 // ------------------------------------------------------------------------- weight (un)packing
 namespace {
+// sub-pixel combined weight W'_t[d][e] (t = 2a + b) at (k, c): sum over the covered taps
+__device__ __forceinline__ float subpixel_weight(const float* __restrict__ w, int k, int c, int C, int R, int S,
+                                                 int t, int dd, int ee) {
+  const int a = t >> 1, b = t & 1;
+  const int r0 = max(0, 2 * dd - a), r1 = min(R - 1, 2 * dd - a + 1);
+  const int s0 = max(0, 2 * ee - b), s1 = min(S - 1, 2 * ee - b + 1);
+  float v = 0.f;
+  for (int r = r0; r <= r1; ++r)
+    for (int s = s0; s <= s1; ++s) v += w[(((int64_t)k * C + c) * R + r) * S + s];
+  return v;
+}
+
+// taps of class t: dh = ((a + R - 1) >> 1) + 1, dw likewise
+__device__ __forceinline__ int sp_dh(int t, int R) { return (((t >> 1) + R - 1) >> 1) + 1; }
+__device__ __forceinline__ int sp_dw(int t, int S) { return (((t & 1) + S - 1) >> 1) + 1; }
+
+template <typename T>
+__global__ void pack_subpixel_kernel(const float* __restrict__ w, int K, int C, int R, int S, int mode,
+                                     const float* inv_scale, T* out) {
+  int tap0[5];
+  tap0[0] = 0;
+  for (int t = 0; t < 4; ++t) tap0[t + 1] = tap0[t] + sp_dh(t, R) * sp_dw(t, S);
+  const int taps = tap0[4];
+  const int64_t n = (int64_t)K * C * taps;
+  const float sc = inv_scale ? 1.f / inv_scale[0] : 1.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int k, c, tap;
+    if (mode == 2) {   // class blocks [K][d][e][C]
+      const int64_t kc = (int64_t)K * C;
+      tap = 0;
+      int t = (i >= tap0[1] * kc) + (i >= tap0[2] * kc) + (i >= tap0[3] * kc);
+      const int64_t rem = i - tap0[t] * kc;
+      const int nde = sp_dh(t, R) * sp_dw(t, S);
+      k = (int)(rem / ((int64_t)nde * C));
+      const int r2 = (int)(rem - (int64_t)k * nde * C);
+      const int de = r2 / C;
+      c = r2 - de * C;
+      tap = tap0[t] + de;
+    } else {           // [C][tap][K]
+      c = (int)(i / ((int64_t)taps * K));
+      const int r2 = (int)(i - (int64_t)c * taps * K);
+      tap = r2 / K;
+      k = r2 - tap * K;
+    }
+    const int t = (tap >= tap0[1]) + (tap >= tap0[2]) + (tap >= tap0[3]);
+    const int de = tap - tap0[t], dw = sp_dw(t, S);
+    const int dd = de / dw, ee = de - dd * dw;
+    out[i] = from_f<T>(subpixel_weight(w, k, c, C, R, S, t, dd, ee) * sc);
+  }
+}
+
 template <typename T>
 __global__ void pack_weight_kernel(const float* __restrict__ w, int K, int C, int R, int S, int mode,
                                    const float* inv_scale, const int32_t* col_perm, T* out) {
@@ -1054,7 +1123,21 @@ __global__ void unpack_grad_kernel(const float* __restrict__ dw, int K, int C, i
 extern "C" int es_pack_conv_weight(const float* w, int K, int C, int R, int S, int mode,
                                    const float* inv_scale, const int32_t* col_perm, void* out,
                                    es_dtype_t dt, es_stream_t stream) {
-  ES_CHECK_ARG(mode == 0 || mode == 1, "pack: bad mode");
+  ES_CHECK_ARG(mode >= 0 && mode <= 3, "pack: bad mode");
+  if (mode >= 2) {
+    ES_CHECK_ARG(col_perm == nullptr, "pack: sub-pixel modes take no column permutation");
+    const int64_t n = (int64_t)K * C * es_subpixel_taps(R, S);
+    ES_CHECK_ARG(n < (1ll << 31), "pack: weight too large");
+    const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+    if (dt == ES_F32)
+      hipLaunchKernelGGL(pack_subpixel_kernel<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                         w, K, C, R, S, mode, inv_scale, (float*)out);
+    else
+      hipLaunchKernelGGL(pack_subpixel_kernel<bf16>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                         w, K, C, R, S, mode, inv_scale, (bf16*)out);
+    ES_CHECK_LAUNCH();
+    return ES_OK;
+  }
   const int64_t n = (int64_t)K * C * R * S;
   ES_CHECK_ARG(n < (1ll << 31), "pack: weight too large");
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);

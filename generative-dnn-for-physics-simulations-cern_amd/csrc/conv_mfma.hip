@@ -148,22 +148,18 @@ __device__ __forceinline__ void ring_loop(int nk, char* smem, int slot_bytes, Is
   wait_vmcnt<0>();   // drain the zero-fill steps before the workgroup may exit
 }
 
-// Pixel grid of the GEMM rows: FWD output pixels, DGRAD input pixels (source grid when folded).
-struct RowGrid {
-  int h, w;
-};
-template <int MODE>
-__device__ __forceinline__ RowGrid row_grid(const ConvArgs& a) {
-  const es_conv_desc_t& d = a.d;
-  if constexpr (MODE == MODE_FWD) return {d.P, d.Q};
-  else return a.fold ? RowGrid{d.H, d.W} : RowGrid{d.Hu, d.Wu};
-}
-
 // ---------------------------------------------------------------------------------------------
 // FWD / DGRAD.  Rows m = (g*PQ + pix)*64 + nl (image n = 64 g + nl, pixel pix on the row grid),
 // columns = channels of the packed weight, K-step = one tap x 64 channels.
+//
+// SP (sub-pixel decomposition of a conv over a x2 nearest-upsampled input, SubPixel in
+// conv_common.h): FWD row tiles belong to one parity class of output pixels and run the class's
+// dh x dw conv on the SOURCE grid with combined weights (packed by es_pack_conv_weight mode 2);
+// DGRAD rows are source pixels and the K-steps run over (class, d, e, channels) against the
+// mode-3 packing.  3x3 taps on the upsampled grid become 4 taps on the source grid: 2.25x fewer
+// MACs and gathered bytes for the same result (up to the rounding of the combined weights).
 // ---------------------------------------------------------------------------------------------
-template <int MODE, int BM, int BN>
+template <int MODE, int BM, int BN, bool SP>
 __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   constexpr int WM = BM / 4, WN = BN / 2;       // 4 x 2 waves
   constexpr int RM = WM / 16, RN = WN / 16;
@@ -172,27 +168,55 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   constexpr int ABYTES = BM * 128, SLOT = (BM + BN) * 128;
   __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT];
   const es_conv_desc_t& d = a.d;
-  const RowGrid rg = row_grid<MODE>(a);
-  const int PQ = rg.h * rg.w;
-  const int nblk = ((d.N + 63) >> 6) * PQ;      // 64-row blocks
+  const SubPixel& sp = a.sp;
+  const int G = (d.N + 63) >> 6;
 
   // tile order: the column tiles of one row tile are consecutive (they share the gathered rows)
   const int nt = gridDim.y;
   const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * nt);
-  const int m0 = (wg / nt) * BM, n0 = (wg % nt) * BN;
+  const int tl = wg / nt, n0 = (wg % nt) * BN;
+  // row grid: FWD output pixels (SP: the class's output pixels), DGRAD input pixels (source grid
+  // when the upsample is folded)
+  int cls = 0, m0 = tl * BM, gh, gw;
+  if constexpr (MODE == MODE_FWD && SP) {
+    cls = (tl >= sp.tile0[1]) + (tl >= sp.tile0[2]) + (tl >= sp.tile0[3]);
+    m0 = (tl - sp.tile0[cls]) * BM;
+    gh = sp.ph[cls];
+    gw = sp.pw[cls];
+  } else if constexpr (MODE == MODE_FWD) {
+    gh = d.P;
+    gw = d.Q;
+  } else {
+    gh = a.fold ? d.H : d.Hu;
+    gw = a.fold ? d.W : d.Wu;
+  }
+  const int PQ = gh * gw;
+  const int nblk = G * PQ;                      // 64-row blocks
 
   const int lane = threadIdx.x & 63, wid = uni(threadIdx.x >> 6);
   const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
   const int lrow = lane >> 3, pc = lane & 7;
 
   const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * 2));
-  const int ldb = (MODE == MODE_DGRAD && a.fold) ? d.R * d.S * d.K : a.Kd;
-  const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)(a.Ng * ldb * 2));
+  // packed weights: row stride ldb (elements) and the class's block offset
+  int ldb, bbase = 0, bbytes;
+  if constexpr (SP && MODE == MODE_FWD) {
+    ldb = sp.dh[cls] * sp.dw[cls] * d.C;
+    bbase = sp.tap0[cls] * a.Ng * d.C;
+    bbytes = sp.tap0[4] * a.Ng * d.C * 2;
+  } else if constexpr (SP) {
+    ldb = sp.tap0[4] * d.K;
+    bbytes = a.Ng * ldb * 2;
+  } else {
+    ldb = (MODE == MODE_DGRAD && a.fold) ? d.R * d.S * d.K : a.Kd;
+    bbytes = a.Ng * ldb * 2;
+  }
+  const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)bbytes);
   const int as2b = (int)a.as[2] * 2, as3b = (int)a.as[3] * 2;
 
   // A pieces: per-lane constant (image, 16-byte chunk) + per-piece uniform pixel coordinates
   uint32_t alane[APW];
-  int pc0[APW], pc1[APW];   // uniform: FWD p*st-pad, q*st-pad; DGRAD (folded) i*up+pad, j*up+pad
+  int pc0[APW], pc1[APW];
   bool pval[APW];
 #pragma unroll
   for (int j = 0; j < APW; ++j) {
@@ -204,11 +228,17 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
     pval[j] = blk < nblk;
     const int bb = pval[j] ? blk : 0;
     const int g = bb / PQ, pix = bb - g * PQ;
-    const int y = pix / rg.w, x = pix - y * rg.w;
+    const int y = pix / gw, x = pix - y * gw;
     alane[j] = (uint32_t)((g * 64 + nl) * (int)a.as[0] * 2 + lc * 16);
-    if constexpr (MODE == MODE_FWD) {
+    if constexpr (MODE == MODE_FWD && SP) {       // source row = u + oh + d
+      pc0[j] = y + sp.oh[cls];
+      pc1[j] = x + sp.ow[cls];
+    } else if constexpr (MODE == MODE_FWD) {
       pc0[j] = y * d.stride - d.pad;
       pc1[j] = x * d.stride - d.pad;
+    } else if constexpr (SP) {                    // source pixel (i, j)
+      pc0[j] = y;
+      pc1[j] = x;
     } else if (a.fold) {
       pc0[j] = y * d.up_h + d.pad;
       pc1[j] = x * d.up_w + d.pad;
@@ -221,37 +251,56 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
 #pragma unroll
   for (int j = 0; j < BPW; ++j) {
     const int rr = (wid * BPW + j) * 8 + lrow;
-    // rows past Ng land past num_records (zeros)
-    blane[j] = (uint32_t)((n0 + rr) * ldb * 2 + ((pc ^ ((rr >> 1) & 7)) * 16));
+    // rows past Ng read garbage columns that the epilogue drops (or zeros past num_records)
+    blane[j] = (uint32_t)((bbase + (n0 + rr) * ldb) * 2 + ((pc ^ ((rr >> 1) & 7)) * 16));
   }
 
-  // K-step cursor (uniform, advanced once per issued slot): FWD kk = ((r*S + s)*C + ch);
-  // DGRAD kk = (((ua*up_w + ub)*R + r)*S + s)*K + ch with weight column kb = kk mod R*S*K
-  int cr = 0, cs = 0, cch = 0, cua = 0, cub = 0, ckb = 0, cstep = 0;
+  // K-step cursor (uniform, advanced once per issued slot).
+  //   FWD      kk = ((r*S + s)*C + ch)                      (SP: taps d < dh, e < dw of the class)
+  //   DGRAD    kk = (((ua*up_w + ub)*R + r)*S + s)*K + ch  with weight column kb = kk mod R*S*K
+  //   DGRAD SP kk = ((class, d, e), ch)                    with column (tap0[class] + d*dw + e)*K + ch
+  int cr = 0, cs = 0, cch = 0, cua = 0, cub = 0, ckb = 0, ccls = 0, cstep = 0;
   const int nch = MODE == MODE_FWD ? d.C : d.K;
   const int upw = d.up_w > 0 ? d.up_w : 1;
-  const int nk = a.Kd / 64;
+  int nk;
+  if constexpr (SP && MODE == MODE_FWD) nk = ldb / 64;
+  else if constexpr (SP) nk = ldb / 64;
+  else nk = a.Kd / 64;
+  int kh = SP ? sp.dh[cls] : d.R, kw = SP ? sp.dw[cls] : d.S;   // taps of the cursor's class
   auto issue = [&](char* slot) {
     const bool live = cstep < nk;
 #pragma unroll
     for (int j = 0; j < APW; ++j) {
       uint32_t u;
-      if constexpr (MODE == MODE_FWD) {
+      if constexpr (MODE == MODE_FWD && SP) {
+        const int hs = pc0[j] + cr, ws = pc1[j] + cs;
+        const bool ok = live && pval[j] && (unsigned)hs < (unsigned)d.H && (unsigned)ws < (unsigned)d.W;
+        u = ok ? (uint32_t)(hs * as2b + ws * as3b + cch * 2) : OOB;
+      } else if constexpr (MODE == MODE_FWD) {
         const int hu = pc0[j] + cr, wu = pc1[j] + cs;
         const bool ok = live && pval[j] && (unsigned)hu < (unsigned)d.Hu && (unsigned)wu < (unsigned)d.Wu;
         // integer nearest upsample folded into the gather (factor 1 without upsample)
         const int sh = fdiv(hu, a.fUh), sw = fdiv(wu, a.fUw);
         u = ok ? (uint32_t)(sh * as2b + sw * as3b + cch * 2) : OOB;
+      } else if constexpr (SP) {
+        // output pixel (p0 + 2u, q0 + 2v) of class ccls feeds source pixel u + oh + d
+        const int uu = pc0[j] - cr - sp.oh[ccls], vv = pc1[j] - cs - sp.ow[ccls];
+        const bool ok = live && pval[j] && (unsigned)uu < (unsigned)sp.ph[ccls] &&
+                        (unsigned)vv < (unsigned)sp.pw[ccls];
+        u = ok ? (uint32_t)((sp.p0[ccls] + 2 * uu) * as2b + (sp.q0[ccls] + 2 * vv) * as3b + cch * 2) : OOB;
       } else {
         const int ph = pc0[j] + cua - cr, pw = pc1[j] + cub - cs;
-        const int sp = d.stride == 2 ? 1 : 0;
-        const bool ok = live && pval[j] && ph >= 0 && pw >= 0 && !(((ph | pw) & sp)) &&
-                        (ph >> sp) < d.P && (pw >> sp) < d.Q;
-        u = ok ? (uint32_t)((ph >> sp) * as2b + (pw >> sp) * as3b + cch * 2) : OOB;
+        const int sh = d.stride == 2 ? 1 : 0;
+        const bool ok = live && pval[j] && ph >= 0 && pw >= 0 && !(((ph | pw) & sh)) &&
+                        (ph >> sh) < d.P && (pw >> sh) < d.Q;
+        u = ok ? (uint32_t)((ph >> sh) * as2b + (pw >> sh) * as3b + cch * 2) : OOB;
       }
       bdma16(ares, alane[j] + u, slot + (wid * APW + j) * 1024);
     }
-    const int kb = MODE == MODE_FWD ? (cr * d.S + cs) * d.C + cch : ckb;
+    int kb;
+    if constexpr (MODE == MODE_FWD) kb = (cr * kw + cs) * d.C + cch;
+    else if constexpr (SP) kb = (sp.tap0[ccls] + cr * kw + cs) * d.K + cch;
+    else kb = ckb;
     const uint32_t ub = live ? (uint32_t)(kb * 2) : OOB;
 #pragma unroll
     for (int j = 0; j < BPW; ++j) bdma16(bres, blane[j] + ub, slot + ABYTES + (wid * BPW + j) * 1024);
@@ -262,16 +311,22 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
     const bool w1 = cch == nch;
     cch = w1 ? 0 : cch;
     cs += w1;
-    const bool w2 = cs == d.S;
+    const bool w2 = cs == kw;
     cs = w2 ? 0 : cs;
     cr += w2;
-    const bool w3 = cr == d.R;
+    const bool w3 = cr == kh;
     cr = w3 ? 0 : cr;
     ckb = w3 ? 0 : ckb;
     cub += w3;
     const bool w4 = cub == upw;
     cub = w4 ? 0 : cub;
     cua += w4;
+    if constexpr (SP && MODE == MODE_DGRAD) {
+      ccls += w3;
+      const int cn = ccls < 4 ? ccls : 3;
+      kh = sp.dh[cn];
+      kw = sp.dw[cn];
+    }
   };
 
   f32x4 acc[RM][RN];
@@ -305,7 +360,11 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   const int blk = mw >> 6;
   if (blk >= nblk) return;
   const int g = blk / PQ, pix = blk - g * PQ;
-  const int y = pix / rg.w, x = pix - y * rg.w;
+  int y = pix / gw, x = pix - y * gw;
+  if constexpr (SP && MODE == MODE_FWD) {
+    y = sp.p0[cls] + 2 * y;
+    x = sp.q0[cls] + 2 * x;
+  }
   const int64_t pixoff = (int64_t)y * a.os[2] + (int64_t)x * a.os[3];
   const int col16 = lane & 15, rq = (lane >> 4) * 4;
 #pragma unroll
@@ -343,8 +402,11 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
 // Block tile BM out-channels x BN in-channels of ONE tap (C % BN == 0).  K-step t = (output
 // pixel t / G, image group t % G): 64 images at one pixel.  Split over blockIdx.z with fp32
 // atomics into the zeroed dw.
+// SP: the tile's tap is a (class, d, e) tap of the sub-pixel decomposition; its K runs over the
+// class's output pixels, and the epilogue adds the tile into every original tap (r, s) the
+// combined tap covers (r in {2d - a, 2d - a + 1} within [0, R), likewise s).
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN>
+template <int BM, int BN, bool SP>
 __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
   constexpr int WGM = BM / 64, WGN = 8 / WGM;   // waves along M / N
   constexpr int WM = BM / WGM, WN = BN / WGN;
@@ -355,6 +417,7 @@ __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
   constexpr int ALPR = BM / 8, BLPR = BN / 8;   // lanes (16-byte chunks) per k-row
   __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT];
   const es_conv_desc_t& d = a.d;
+  const SubPixel& sp = a.sp;
   const int G = (d.N + 63) >> 6;
 
   // blocks of one K split (same pixels) are consecutive on one XCD
@@ -363,13 +426,28 @@ __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
   const int wg = xcd_remap(orig, tiles * gridDim.z);
   const int tile = wg % tiles, split = wg / tiles;
   const int m0 = (tile % mt) * BM, n0 = (tile / mt) * BN;
+  const int rs = n0 / d.C, cb = n0 - rs * d.C;   // tap of the tile, channel base
+  // the tile's tap and the pixel grid its K runs over
+  int cls = 0, tr, ts, gq, npix;
+  if constexpr (SP) {
+    cls = (rs >= sp.tap0[1]) + (rs >= sp.tap0[2]) + (rs >= sp.tap0[3]);
+    const int de = rs - sp.tap0[cls];
+    tr = de / sp.dw[cls];
+    ts = de - tr * sp.dw[cls];
+    gq = sp.pw[cls];
+    npix = sp.ph[cls] * gq;
+  } else {
+    tr = rs / d.S;
+    ts = rs - tr * d.S;
+    gq = d.Q;
+    npix = d.P * d.Q;
+  }
   const int tbeg = split * a.k_per_split;       // in K-steps
-  const int tend = min(d.P * d.Q * G, tbeg + a.k_per_split);
+  const int tend = min(npix * G, tbeg + a.k_per_split);
+  if (tbeg >= tend) return;
 
   const int lane = threadIdx.x & 63, wid = uni(threadIdx.x >> 6);
   const int wm0 = (wid / WGN) * WM, wn0 = (wid % WGN) * WN;
-  const int rs = n0 / d.C, cb = n0 - rs * d.C;
-  const int tr = rs / d.S, ts = rs - tr * d.S;
   const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * 2));
   const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)(d.N * a.bs[0] * 2));
   const int as0b = (int)a.as[0] * 2, as2b = (int)a.as[2] * 2, as3b = (int)a.as[3] * 2;
@@ -387,20 +465,28 @@ __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
     blane[j] = (uint32_t)(kr * bs0b + (cb + ((lane % BLPR) ^ swz_tr(kr)) * 8) * 2);
   }
 
-  // K-step cursor (uniform): output pixel (p, q) and image group gi of step t = (p*Q + q)*G + gi
+  // K-step cursor (uniform): pixel (p, q) of the grid and image group gi of step t = (p*gq + q)*G + gi
   int cp, cq, cg, cstep = tbeg;
   {
     const int pix = tbeg / G;
     cg = tbeg - pix * G;
-    cp = pix / d.Q;
-    cq = pix - cp * d.Q;
+    cp = pix / gq;
+    cq = pix - cp * gq;
   }
   auto issue = [&](char* slot) {
     const bool live = cstep < tend;
-    const uint32_t ua = live ? (uint32_t)(cg * 64 * as0b + cp * as2b + cq * as3b) : OOB;
-    const int hu = cp * d.stride - d.pad + tr, wu = cq * d.stride - d.pad + ts;
-    const bool ok = live && (unsigned)hu < (unsigned)d.Hu && (unsigned)wu < (unsigned)d.Wu;
-    const uint32_t ub = ok ? (uint32_t)(cg * 64 * bs0b + fdiv(hu, a.fUh) * bs2b + fdiv(wu, a.fUw) * bs3b) : OOB;
+    uint32_t ua, ub;
+    if constexpr (SP) {   // dy at output pixel (p0 + 2p, q0 + 2q), x at source (p + oh + d, q + ow + e)
+      ua = live ? (uint32_t)(cg * 64 * as0b + (sp.p0[cls] + 2 * cp) * as2b + (sp.q0[cls] + 2 * cq) * as3b) : OOB;
+      const int hs = cp + sp.oh[cls] + tr, ws = cq + sp.ow[cls] + ts;
+      const bool ok = live && (unsigned)hs < (unsigned)d.H && (unsigned)ws < (unsigned)d.W;
+      ub = ok ? (uint32_t)(cg * 64 * bs0b + hs * bs2b + ws * bs3b) : OOB;
+    } else {
+      ua = live ? (uint32_t)(cg * 64 * as0b + cp * as2b + cq * as3b) : OOB;
+      const int hu = cp * d.stride - d.pad + tr, wu = cq * d.stride - d.pad + ts;
+      const bool ok = live && (unsigned)hu < (unsigned)d.Hu && (unsigned)wu < (unsigned)d.Wu;
+      ub = ok ? (uint32_t)(cg * 64 * bs0b + fdiv(hu, a.fUh) * bs2b + fdiv(wu, a.fUw) * bs3b) : OOB;
+    }
 #pragma unroll
     for (int j = 0; j < APW; ++j) bdma16(ares, alane[j] + ua, slot + (wid * APW + j) * 1024);
 #pragma unroll
@@ -410,7 +496,7 @@ __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
     const bool w1 = cg == G;
     cg = w1 ? 0 : cg;
     cq += w1;
-    const bool w2 = cq == d.Q;
+    const bool w2 = cq == gq;
     cq = w2 ? 0 : cq;
     cp += w2;
   };
@@ -421,7 +507,6 @@ __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (tbeg >= tend) return;
   struct Frag {
     bf16x8 a[RM], b[RN];
   };
@@ -439,43 +524,98 @@ __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
   };
   ring_loop<PW>(tend - tbeg, smem, SLOT, issue, load, mma);
+
   const int col16 = lane & 15, rq = (lane >> 4) * 4;
   float* out = (float*)a.out;
+  // original taps this tile's tap feeds: one (no SP) or up to 2 x 2 (SP)
+  int r0 = tr, r1 = tr, s0 = ts, s1 = ts;
+  if constexpr (SP) {
+    const int ca = cls >> 1, cbb = cls & 1;
+    r0 = max(0, 2 * tr - ca);
+    r1 = min(d.R - 1, 2 * tr - ca + 1);
+    s0 = max(0, 2 * ts - cbb);
+    s1 = min(d.S - 1, 2 * ts - cbb + 1);
+  }
+  const int ldo = d.R * d.S * d.C;
+  for (int r = r0; r <= r1; ++r)
+    for (int s_ = s0; s_ <= s1; ++s_) {
+      float* o = out + (r * d.S + s_) * d.C + cb + wn0 + col16;
 #pragma unroll
-  for (int i = 0; i < RM; ++i)
+      for (int i = 0; i < RM; ++i)
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int m = m0 + wm0 + i * 16 + rq + jj;
+        for (int jj = 0; jj < 4; ++jj) {
+          const int m = m0 + wm0 + i * 16 + rq + jj;
 #pragma unroll
-      for (int j = 0; j < RN; ++j) atomicAdd(out + (int64_t)m * a.Ng + n0 + wn0 + j * 16 + col16, acc[i][j][jj]);
+          for (int j = 0; j < RN; ++j) atomicAdd(o + (int64_t)m * ldo + j * 16, acc[i][j][jj]);
+        }
     }
 }
 
-template <int MODE, int BM, int BN>
-void launch_ring(const ConvArgs& a, int rows, hipStream_t st) {
-  dim3 grid((rows + BM - 1) / BM, (a.Ng + BN - 1) / BN, 1);
-  hipLaunchKernelGGL((conv_ring_kernel<MODE, BM, BN>), grid, dim3(RT), 0, st, a);
+template <int MODE, int BM, int BN, bool SP>
+void launch_ring(const ConvArgs& a, int row_tiles, hipStream_t st) {
+  dim3 grid(row_tiles, (a.Ng + BN - 1) / BN, 1);
+  hipLaunchKernelGGL((conv_ring_kernel<MODE, BM, BN, SP>), grid, dim3(RT), 0, st, a);
 }
 
-template <int BM, int BN>
+template <int BM, int BN, bool SP>
 void launch_wgrad_ring(ConvArgs& a, hipStream_t st) {
-  const int tiles = (a.M / BM) * (a.Ng / BN);
-  const int ks = a.d.P * a.d.Q * ((a.d.N + 63) / 64);   // K-steps
+  const int taps = SP ? a.sp.tap0[4] : a.d.R * a.d.S;
+  const int tiles = (a.M / BM) * (taps * a.d.C / BN);
+  int npix = a.d.P * a.d.Q;
+  if (SP)
+    for (int c = 0; c < 4; ++c) npix = c == 0 ? a.sp.ph[0] * a.sp.pw[0] : max(npix, a.sp.ph[c] * a.sp.pw[c]);
+  const int ks = npix * ((a.d.N + 63) / 64);   // K-steps (the largest class)
   // one workgroup per CU: aim at two full rounds of the 256 CUs, >= 8 K-steps per split
   const int want = max(1, min(ks / 8, 512 / tiles));
   const int per = (ks + want - 1) / want;
   a.k_per_split = per;
-  dim3 grid(a.M / BM, a.Ng / BN, (ks + per - 1) / per);
-  hipLaunchKernelGGL((wgrad_ring_kernel<BM, BN>), grid, dim3(RT), 0, st, a);
+  dim3 grid(a.M / BM, taps * a.d.C / BN, (ks + per - 1) / per);
+  hipLaunchKernelGGL((wgrad_ring_kernel<BM, BN, SP>), grid, dim3(RT), 0, st, a);
 }
 
-// a dense NHWC image stack (n outermost, rows of c contiguous values) below 2 GiB in bytes
+// a dense NHWC image stack (n outermost, rows of c contiguous values) below 1 GiB in bytes
 bool dense_small(const int64_t s[4], int n, int c, int h, int w) {
   return s[1] == 1 && s[3] == c && s[2] == (int64_t)w * c && s[0] == (int64_t)h * w * c &&
          (int64_t)n * s[0] * 2 < (1ll << 30);
 }
 
+bool g_subpixel_off = [] { const char* e = getenv("ES_NO_SUBPIXEL"); return e && e[0] == '1'; }();
+
 }  // namespace
+
+// Class geometry of the sub-pixel decomposition (see SubPixel): output row p belongs to class
+// a = (p - pad) mod 2, p = p0 + 2u, source row of combined tap d = u + oh + d, dh = taps.
+void es_make_subpixel(const es_conv_desc_t& d, int row_tile, SubPixel& sp) {
+  int dhv[2], dwv[2], p0v[2], q0v[2], phv[2], pwv[2], ohv[2], owv[2];
+  for (int a = 0; a < 2; ++a) {
+    dhv[a] = ((a + d.R - 1) >> 1) + 1;
+    dwv[a] = ((a + d.S - 1) >> 1) + 1;
+    p0v[a] = (a + d.pad) & 1;
+    q0v[a] = (a + d.pad) & 1;
+    phv[a] = d.P > p0v[a] ? (d.P - p0v[a] + 1) / 2 : 0;
+    pwv[a] = d.Q > q0v[a] ? (d.Q - q0v[a] + 1) / 2 : 0;
+    ohv[a] = (p0v[a] - d.pad - a) / 2;
+    owv[a] = (q0v[a] - d.pad - a) / 2;
+  }
+  sp.on = 1;
+  sp.tap0[0] = 0;
+  sp.tile0[0] = 0;
+  const int G = (d.N + 63) / 64;
+  for (int c = 0; c < 4; ++c) {
+    const int a = c >> 1, b = c & 1;
+    sp.ph[c] = phv[a];
+    sp.pw[c] = pwv[b];
+    sp.p0[c] = p0v[a];
+    sp.q0[c] = q0v[b];
+    sp.oh[c] = ohv[a];
+    sp.ow[c] = owv[b];
+    sp.dh[c] = dhv[a];
+    sp.dw[c] = dwv[b];
+    sp.tap0[c + 1] = sp.tap0[c] + dhv[a] * dwv[b];
+    const int rows = G * 64 * phv[a] * pwv[b];
+    sp.tile0[c + 1] = sp.tile0[c] + (row_tile > 0 ? (rows + row_tile - 1) / row_tile : 0);
+  }
+}
 
 extern "C" int es_conv_set_ring(int on) {
   const int old = !g_ring_off;
@@ -483,36 +623,74 @@ extern "C" int es_conv_set_ring(int on) {
   return old;
 }
 
+extern "C" int es_conv_set_subpixel(int on) {
+  const int old = !g_subpixel_off;
+  g_subpixel_off = !on;
+  return old;
+}
+
+extern "C" int es_subpixel_taps(int R, int S) {
+  return (((R - 1) >> 1) + 1 + (R >> 1) + 1) * (((S - 1) >> 1) + 1 + (S >> 1) + 1);
+}
+
+// Whether es_conv2d_fwd / es_conv2d_dgrad take the sub-pixel path for this conv (then the weights
+// must be packed with es_pack_conv_weight mode 2 / 3 and d->subpixel set): bf16, x2 integer
+// upsample, stride 1, channels % 64 == 0, below the ring's size limits.  The activations must be
+// dense NHWC at call time.
+extern "C" int es_conv_subpixel_ok(const es_conv_desc_t* d, es_dtype_t dt) {
+  if (g_ring_off || g_subpixel_off || !d || dt != ES_BF16) return 0;
+  if (d->up_h != 2 || d->up_w != 2 || d->hmap || d->stride != 1) return 0;
+  if (d->C % 64 || d->K % 64) return 0;
+  const int64_t xbytes = (int64_t)d->N * d->H * d->W * d->C * 2, ybytes = (int64_t)d->N * d->P * d->Q * d->K * 2;
+  const int64_t wbytes = (int64_t)d->K * d->C * es_subpixel_taps(d->R, d->S) * 2;
+  return xbytes < (1ll << 30) && ybytes < (1ll << 30) && wbytes < (1ll << 30);
+}
+
 int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
-  if (g_ring_off) return 0;
   const es_conv_desc_t& d = a.d;
-  if (d.hmap != nullptr || d.stride > 2 || a.splitk) return 0;
+  const bool sp_weights = d.subpixel != 0;   // FWD / DGRAD operands packed for the sub-pixel path
+  if (g_ring_off && !sp_weights) return 0;
+  if (d.hmap != nullptr || d.stride > 2 || a.splitk) return sp_weights ? -1 : 0;
   if (mode == MODE_WGRAD) {
     if (!dense_small(a.as, d.N, d.K, d.P, d.Q) || !dense_small(a.bs, d.N, d.C, d.H, d.W)) return 0;
-    if (d.K % 256 == 0 && d.C % 128 == 0) launch_wgrad_ring<256, 128>(a, st);
-    else if (d.K % 128 == 0 && d.C % 256 == 0) launch_wgrad_ring<128, 256>(a, st);
-    else if (d.K % 128 == 0 && d.C % 128 == 0) launch_wgrad_ring<128, 128>(a, st);
+    const bool sp = !g_subpixel_off && d.up_h == 2 && d.up_w == 2 && d.stride == 1;
+    if (sp) es_make_subpixel(d, 0, a.sp);
+#define ES_WG(BM, BN) (sp ? launch_wgrad_ring<BM, BN, true>(a, st) : launch_wgrad_ring<BM, BN, false>(a, st))
+    if (d.K % 256 == 0 && d.C % 128 == 0) ES_WG(256, 128);
+    else if (d.K % 128 == 0 && d.C % 256 == 0) ES_WG(128, 256);
+    else if (d.K % 128 == 0 && d.C % 128 == 0) ES_WG(128, 128);
     else return 0;
+#undef ES_WG
     return 1;
   }
   // caller checked: bf16, channels % 64 == 0, K % 64 == 0 per step
   int rows;
   if (mode == MODE_FWD) {
-    if (!dense_small(a.as, d.N, d.C, d.H, d.W)) return 0;
+    if (!dense_small(a.as, d.N, d.C, d.H, d.W)) return sp_weights ? -1 : 0;
     rows = ((d.N + 63) / 64) * 64 * d.P * d.Q;
   } else {
-    if (!dense_small(a.as, d.N, d.K, d.P, d.Q)) return 0;
+    if (!dense_small(a.as, d.N, d.K, d.P, d.Q)) return sp_weights ? -1 : 0;
     rows = ((d.N + 63) / 64) * 64 * (a.fold ? d.H * d.W : d.Hu * d.Wu);
   }
-  if ((int64_t)a.Ng * a.Kd * 2 >= (1ll << 30)) return 0;
+  if ((int64_t)a.Ng * a.Kd * 2 * (sp_weights ? 2 : 1) >= (1ll << 30)) return sp_weights ? -1 : 0;
   const int nt128 = (a.Ng + 127) / 128;
-  const bool big_rows = ((rows + 255) / 256) * nt128 >= 768;   // >= 3 rounds of 256-row tiles
-  if (mode == MODE_FWD) {
-    if (a.Ng <= 64) big_rows ? launch_ring<MODE_FWD, 256, 64>(a, rows, st) : launch_ring<MODE_FWD, 128, 64>(a, rows, st);
-    else big_rows ? launch_ring<MODE_FWD, 256, 128>(a, rows, st) : launch_ring<MODE_FWD, 128, 128>(a, rows, st);
-  } else {
-    if (a.Ng <= 64) big_rows ? launch_ring<MODE_DGRAD, 256, 64>(a, rows, st) : launch_ring<MODE_DGRAD, 128, 64>(a, rows, st);
-    else big_rows ? launch_ring<MODE_DGRAD, 256, 128>(a, rows, st) : launch_ring<MODE_DGRAD, 128, 128>(a, rows, st);
+  const bool big = ((rows + 255) / 256) * nt128 >= 768;   // >= 3 rounds of 256-row tiles
+  const int BM = big ? 256 : 128;
+  int row_tiles = (rows + BM - 1) / BM;
+  if (sp_weights) {
+    es_make_subpixel(d, BM, a.sp);
+    if (mode == MODE_FWD) row_tiles = a.sp.tile0[4];
   }
+#define ES_RING(MD, BMV, BNV)                                                                  \
+  (sp_weights ? launch_ring<MD, BMV, BNV, true>(a, row_tiles, st)                              \
+              : launch_ring<MD, BMV, BNV, false>(a, row_tiles, st))
+  if (mode == MODE_FWD) {
+    if (a.Ng <= 64) big ? ES_RING(MODE_FWD, 256, 64) : ES_RING(MODE_FWD, 128, 64);
+    else big ? ES_RING(MODE_FWD, 256, 128) : ES_RING(MODE_FWD, 128, 128);
+  } else {
+    if (a.Ng <= 64) big ? ES_RING(MODE_DGRAD, 256, 64) : ES_RING(MODE_DGRAD, 128, 64);
+    else big ? ES_RING(MODE_DGRAD, 256, 128) : ES_RING(MODE_DGRAD, 128, 128);
+  }
+#undef ES_RING
   return 1;
 }

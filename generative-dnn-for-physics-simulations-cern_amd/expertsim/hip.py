@@ -33,7 +33,7 @@ class ConvDesc(C.Structure):
     _fields_ = [("N", C.c_int), ("C", C.c_int), ("H", C.c_int), ("W", C.c_int), ("Hu", C.c_int),
                 ("Wu", C.c_int), ("K", C.c_int), ("P", C.c_int), ("Q", C.c_int), ("R", C.c_int),
                 ("S", C.c_int), ("stride", C.c_int), ("pad", C.c_int), ("hmap", C.c_void_p),
-                ("wmap", C.c_void_p), ("up_h", C.c_int), ("up_w", C.c_int)]
+                ("wmap", C.c_void_p), ("up_h", C.c_int), ("up_w", C.c_int), ("subpixel", C.c_int)]
 
 
 class Norm(C.Structure):
@@ -58,6 +58,9 @@ _SIGS = {
     "es_device_sync": (C.c_int, []),
     "es_conv_set_glds": (C.c_int, [C.c_int]),
     "es_conv_set_ring": (C.c_int, [C.c_int]),
+    "es_conv_set_subpixel": (C.c_int, [C.c_int]),
+    "es_conv_subpixel_ok": (C.c_int, [P, C.c_int]),
+    "es_subpixel_taps": (C.c_int, [C.c_int, C.c_int]),
     "es_conv2d_fwd": (C.c_int, [P, C.c_int, P, P, P, P, P, C.c_int, P, P]),
     "es_conv2d_dgrad": (C.c_int, [P, C.c_int, P, P, P, P, C.c_int, P, C.c_float, P]),
     "es_conv2d_wgrad": (C.c_int, [P, C.c_int, P, P, P, P, P, P]),
@@ -149,6 +152,14 @@ def dt_of(t: torch.Tensor) -> int:
     if t.dtype == torch.bfloat16:
         return ES_BF16
     raise HipError(f"unsupported dtype {t.dtype}")
+
+
+def dt_of_dtype(dtype) -> int:
+    if dtype == torch.float32:
+        return ES_F32
+    if dtype == torch.bfloat16:
+        return ES_BF16
+    raise HipError(f"unsupported dtype {dtype}")
 
 
 def strides4(s):

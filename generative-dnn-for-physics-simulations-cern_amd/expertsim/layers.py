@@ -222,7 +222,8 @@ class ConvOp:
         if inv_scale is None and key in self._packed:
             return self._packed[key]
         w = self.weight
-        out = torch.empty(w.numel(), dtype=dtype, device=w.device)
+        n = w.numel() if mode < 2 else self.K * self.C * hip.lib().es_subpixel_taps(self.R, self.S)
+        out = torch.empty(n, dtype=dtype, device=w.device)
         hip.call("es_pack_conv_weight", hip.ptr(w), self.K, self.C, self.R, self.S, mode,
                  hip.ptr(inv_scale), None, hip.ptr(out), hip.dt_of(out), hip.stream_ptr())
         if inv_scale is None:
@@ -253,10 +254,21 @@ class ConvOp:
         d.Q = (d.Wu + 2 * self.pad - self.S) // self.stride + 1
         return d
 
+    def subpixel(self, d, dtype) -> bool:
+        """Run this x2-upsample conv as 4 parity-class convs on the source grid (bf16 ring path,
+        conv_mfma.hip): es_conv_subpixel_ok decides, the weights are packed in modes 2 / 3."""
+        if self.up is None or self.up.factor != (2, 2) or dtype != torch.bfloat16:
+            return False
+        return bool(hip.lib().es_conv_subpixel_ok(C.byref(d), hip.dt_of_dtype(dtype)))
+
     def fwd(self, x: Act, out_dtype=None, inv_scale=None, out: Act = None, with_bias=True) -> Act:
         d = self.desc(x)
         cdt = x.t.dtype
-        wk = self.packed(cdt, 0, inv_scale)
+        if self.subpixel(d, cdt):
+            d.subpixel = 1
+            wk = self.packed(cdt, 2, inv_scale)
+        else:
+            wk = self.packed(cdt, 0, inv_scale)
         if out is None:
             out = Act.nhwc(d.N, d.K, d.P, d.Q, out_dtype or cdt, x.t.device)
         bias = self.bias if (with_bias and self.bias is not None) else None
@@ -269,7 +281,11 @@ class ConvOp:
         """Gradient w.r.t. the conv input x (folded through the upsample when present)."""
         d = self.desc(x)
         cdt = dy.t.dtype
-        wd = self.packed(cdt, 1, inv_scale)
+        if self.subpixel(d, cdt):
+            d.subpixel = 1
+            wd = self.packed(cdt, 3, inv_scale)
+        else:
+            wd = self.packed(cdt, 1, inv_scale)
         N, Cc, H, W = x.dims
         ddt = dx_dtype or cdt
         if self.up is None or self.up.factor is not None:   # no upsample, or folded in the GEMM

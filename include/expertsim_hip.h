@@ -76,6 +76,9 @@ typedef struct {
   int up_h, up_w;      /* integer nearest-upsample factors (Hu = H*up_h), or 0 to use the maps.
                           With factors set, es_conv2d_dgrad folds the upsample backward: it
                           writes dx on the SOURCE grid (H x W) with dxs strides.               */
+  int subpixel;        /* 1: the packed weights are the sub-pixel combination of a x2 upsample
+                          conv (es_pack_conv_weight mode 2 for fwd, 3 for dgrad) and the conv runs
+                          as 4 parity-class convs on the source grid (es_conv_subpixel_ok).      */
 } es_conv_desc_t;
 
 /* y[n,k,p,q] = bias[k] + sum_{c,r,s} xu[n,c,p*stride-pad+r,q*stride-pad+s] * W[k,c,r,s]
@@ -87,6 +90,16 @@ int es_conv_set_glds(int on);
 /* Select the 8-wave LDS-DMA ring kernels (conv_mfma.hip) for the bf16 convs whose K-step is one tap
  * x 64 channels: 1 = on (default), 0 = use the 4-wave kernels.  Returns the previous setting. */
 int es_conv_set_ring(int on);
+/* Sub-pixel decomposition of stride-1 convs over a x2 nearest upsample (conv_mfma.hip): 1 = on
+ * (default; wgrad uses it internally, fwd/dgrad when the caller packs mode 2/3 weights and sets
+ * desc->subpixel), 0 = off.  Returns the previous setting. */
+int es_conv_set_subpixel(int on);
+/* 1 if es_conv2d_fwd / es_conv2d_dgrad can run this conv on the sub-pixel path (bf16, x2 integer
+ * upsample, stride 1, channels % 64 == 0, tensors below 1 GiB, dense NHWC activations). */
+int es_conv_subpixel_ok(const es_conv_desc_t* d, es_dtype_t dt);
+/* Number of combined taps of the sub-pixel packing (16 for 3x3, 25 for 4x4): the packed weight
+ * of mode 2 / 3 holds K * C * es_subpixel_taps(R, S) elements. */
+int es_subpixel_taps(int R, int S);
 
 int es_conv2d_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x, const int64_t xs[4],
                   const void* wk, const float* bias, void* y, es_dtype_t ydt, const int64_t ys[4],
@@ -106,6 +119,10 @@ int es_conv2d_wgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, cons
 
 /* Weight packing for the implicit GEMM (fp32 master [K][C][R][S] -> dt).
  * mode 0: out[k][r][s][c] = w*scale ; mode 1: out[c][r][s][k] = w*scale.
+ * mode 2 / 3 (sub-pixel, x2 upsample): for each parity class t = 2a + b the combined weights
+ * W'_t[d][e] = sum of w[.][.][r][s] over r in {2d-a, 2d-a+1}, s in {2e-b, 2e-b+1} (within range),
+ * d < ((a+R-1)>>1)+1, e < ((b+S-1)>>1)+1; mode 2: class blocks [K][d][e][C] one after another,
+ * mode 3: out[c][tap][k] with tap = the classes' (d, e) taps in order.  col_perm must be NULL.
  * scale = (inv_scale ? 1/inv_scale[0] : 1)  — the spectral-norm division W/sigma
  * (torch.nn.utils.spectral_norm compute_weight) is folded here.
  * col_perm (optional, device [C*R*S] for R=S=1 linears): input column index permutation. */

@@ -345,6 +345,7 @@ def test_conv_ring_matches_4wave(case):
     xa = to_act(x, torch.bfloat16)
     outs = []
     gy = None
+    sp_old = hip.lib().es_conv_set_subpixel(0)   # bit-exact comparison: same taps on both sides
     try:
         for on in (1, 0):
             hip.lib().es_conv_set_ring(on)
@@ -359,6 +360,7 @@ def test_conv_ring_matches_4wave(case):
             outs.append((ya.t.clone(), dxa.t.clone(), dw.cpu()))
     finally:
         hip.lib().es_conv_set_ring(1)
+        hip.lib().es_conv_set_subpixel(sp_old)
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
     assert rel(outs[0][2], outs[1][2]) < 1e-5
@@ -369,3 +371,51 @@ def test_conv_ring_matches_4wave(case):
     y.backward(gy.to(torch.bfloat16).float())
     assert rel(outs[0][0].float().cpu().view(y.shape[0], y.shape[2], y.shape[3], -1).permute(0, 3, 1, 2), y) < 3e-2
     assert rel(outs[0][2], wr.grad) < 3e-2
+
+
+SUBPIXEL_CASES = [
+    # x2-upsample convs on the sub-pixel path (4 parity-class convs on the source grid)
+    (3, 256, 24, 24, 128, 3, 0),      # neutron G conv_layers.5 (3x3 -> 2x2 taps per class)
+    (7, 128, 13, 13, 256, 3, 0),      # neutron G conv_layers.0
+    (2, 512, 18, 10, 256, 4, 1),      # proton G conv_layers.1 (4x4, pad 1: 2/3 taps per class)
+    (70, 64, 5, 7, 64, 3, 1),         # pad 1, N not a multiple of 64, odd grids
+]
+
+
+@pytest.mark.parametrize("case", SUBPIXEL_CASES)
+def test_conv_subpixel(case):
+    """Sub-pixel fwd / dgrad / wgrad (bf16) against torch fp32 of the upsample + conv, and the
+    wgrad against the non-sub-pixel ring kernel."""
+    hip = _hip()
+    from expertsim.layers import ConvOp, Upsample
+    N, Cin, H, W, Cout, k, pad = case
+    torch.manual_seed(21)
+    x = torch.randn(N, Cin, H, W).to(torch.bfloat16).float()
+    w = torch.randn(Cout, Cin, k, k) / np.sqrt(Cin * k * k)
+    b = torch.randn(Cout)
+    op = ConvOp(torch.nn.Parameter(w.to(DEV)), torch.nn.Parameter(b.to(DEV)), stride=1, pad=pad,
+                upsample=Upsample((H, W), scale=(2, 2)))
+    xa = to_act(x, torch.bfloat16)
+    assert op.subpixel(op.desc(xa), torch.bfloat16)
+    ya = op.fwd(xa, out_dtype=torch.float32)
+    xr = F.interpolate(x, scale_factor=(2, 2), mode="nearest").requires_grad_(True)
+    xs = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    y = F.conv2d(F.interpolate(xs, scale_factor=(2, 2), mode="nearest"), wr, b, 1, pad)
+    assert ya.dims == tuple(y.shape)
+    assert rel(from_act(ya), y.detach()) < 2e-2
+    gy = torch.randn(y.shape).to(torch.bfloat16).float()
+    y.backward(gy)
+    gya = to_act(gy, torch.bfloat16)
+    dxa = op.dgrad(gya, xa, dx_dtype=torch.float32)
+    assert rel(from_act(dxa), xs.grad) < 2e-2
+    dw = torch.zeros(Cout, Cin, k, k, device=DEV)
+    op.wgrad(gya, xa, dw, None, beta=1.0)
+    assert rel(dw.cpu(), wr.grad) < 2e-2
+    old = hip.lib().es_conv_set_subpixel(0)
+    try:
+        dw0 = torch.zeros(Cout, Cin, k, k, device=DEV)
+        op.wgrad(gya, xa, dw0, None, beta=1.0)
+    finally:
+        hip.lib().es_conv_set_subpixel(old)
+    assert rel(dw.cpu(), dw0.cpu()) < 1e-4   # same products, fp32 sums in another order

@@ -41,8 +41,9 @@ def case(name, N, Cin, H, W, Cout, k, st, pad, up):
     flops = 2.0 * N * P * Q * Cout * Cin * k * k
     dw = torch.zeros(Cout, Cin, k, k, device=dev)
     res = {}
-    for on in (1, 0):
-        hip.lib().es_conv_set_ring(on)
+    for on in (2, 1, 0):   # 2: ring + sub-pixel, 1: ring, 0: 4-wave kernels
+        hip.lib().es_conv_set_ring(1 if on else 0)
+        hip.lib().es_conv_set_subpixel(1 if on == 2 else 0)
         yy = op.fwd(x, out_dtype=torch.bfloat16)
         dx = op.dgrad(dy, x, dx_dtype=torch.bfloat16)
         dw.zero_()
@@ -53,14 +54,16 @@ def case(name, N, Cin, H, W, Cout, k, st, pad, up):
                    timed(lambda: op.dgrad(dy, x, dx_dtype=torch.bfloat16)),
                    timed(lambda: op.wgrad(dy, x, None, None)))
     hip.lib().es_conv_set_ring(1)
+    hip.lib().es_conv_set_subpixel(1)
     same_f = torch.equal(res[1][0], res[0][0])
     same_d = torch.equal(res[1][1], res[0][1])
-    wrel = float((res[1][2] - res[0][2]).abs().max() / res[0][2].abs().max())
-    line = f"{name:34s} {flops / 1e9:7.1f} GF |"
+    r = lambda u, v: float((u.float() - v.float()).abs().max() / v.float().abs().max())
+    line = f"{name:30s} {flops / 1e9:6.1f} GF |"
     for lab, i in (("fwd", 3), ("dgrad", 4), ("wgrad", 5)):
-        line += (f" {lab} ring {res[1][i]:7.1f} us {flops / res[1][i] / 1e6:6.1f} TF"
-                 f" / 4w {res[0][i]:7.1f} us {flops / res[0][i] / 1e6:6.1f} TF |")
-    line += f" fwd==:{same_f} dgrad==:{same_d} wgrad rel {wrel:.1e}"
+        line += (f" {lab} sp {res[2][i]:6.1f} us {flops / res[2][i] / 1e6:6.1f} TF"
+                 f" ring {res[1][i]:6.1f} us {flops / res[1][i] / 1e6:6.1f} TF / 4w {res[0][i]:6.1f} us |")
+    line += (f" ring==4w fwd:{same_f} dgrad:{same_d} | sp-vs-ring rel fwd {r(res[2][0], res[1][0]):.1e}"
+             f" dgrad {r(res[2][1], res[1][1]):.1e} wgrad {r(res[2][2], res[1][2]):.1e}")
     print(line, flush=True)
 
 
