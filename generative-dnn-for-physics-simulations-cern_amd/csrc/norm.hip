@@ -19,6 +19,7 @@
 
 // fast path for dense channels-last BatchNorm / GroupNorm (norm_fast.hip); G = 0 means BN
 bool es_fast_dense_nhwc(const es_view_t* v);
+void es_fast_keep_bits(const es_view_t* v, const es_chain_t* ch, hipStream_t st);
 int64_t es_fast_part_floats(const es_view_t* v, int G);
 int es_fast_norm_stats(const es_view_t* v, int G, es_dtype_t dt, const void* xp, float* part, hipStream_t st);
 void es_fast_norm_fwd(const es_view_t* v, int G, es_dtype_t dt, const void* xp, void* yp, const es_norm_t* nm,
@@ -604,11 +605,14 @@ extern "C" int es_norm_act_fwd(const es_view_t* x, es_dtype_t xdt, const es_norm
                                es_dtype_t ydt, void* yp, es_stream_t stream) {
   ES_CHECK_ARG(x->n == y->n && x->c == y->c && x->h == y->h && x->w == y->w, "norm_act_fwd: shape");
   const int fk = nm ? fast_kind(x, nm->kind, nm->groups) : -1;
+  const bool bits = ch && ch->keep && ch->drop.enabled;
+  ES_CHECK_ARG(!bits || x->c % 8 == 0, "norm_act_fwd: dropout keep bits need C %% 8 == 0");
   if (fk >= 0 && !addend_ptr && xdt == ydt && same_view(x, y)) {
     es_fast_norm_fwd(x, fk, xdt, xp, yp, nm, ch, (hipStream_t)stream);
     ES_CHECK_LAUNCH();
     return ES_OK;
   }
+  if (bits) es_fast_keep_bits(x, ch, (hipStream_t)stream);   // the generic kernel draws the same mask
   FwdArgs a{};
   a.x = mkview(x); a.xp = xp; a.xbf = xdt == ES_BF16;
   a.y = mkview(y); a.yp = yp; a.ybf = ydt == ES_BF16;

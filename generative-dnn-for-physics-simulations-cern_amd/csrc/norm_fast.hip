@@ -52,6 +52,7 @@ struct FastArgs {
   es_dropout_t drop;
   int dfirst, act;
   float slope;
+  uint8_t* keep;                              // dropout keep bits [rows][C/8] (written fwd, read bwd)
 };
 
 __device__ __forceinline__ float actf(const FastArgs& a, float v) {
@@ -64,11 +65,18 @@ __device__ __forceinline__ float dactf(const FastArgs& a, float v) {
 // keep bits for rows r0..r0+3 (bit k = channel c0+k)
 // KM (keep mode, chosen on the host): KM_NONE no dropout, KM_HW4 H*W % 4 == 0, KM_ROW H*W == 1 and
 // C % 4 == 0, KM_GEN anything else.  One instantiation per mode keeps each kernel's code small.
-enum { KM_NONE = 0, KM_HW4 = 1, KM_ROW = 2, KM_GEN = 3 };
+// KM_BITS: read the bits a forward pass stored in a.keep (no Philox).
+enum { KM_NONE = 0, KM_HW4 = 1, KM_ROW = 2, KM_GEN = 3, KM_BITS = 4 };
 
 template <int KM>
 __device__ __forceinline__ void keep_bits(const FastArgs& a, int r0, int c0, uint32_t (&keep)[4]) {
   if constexpr (KM == KM_NONE) { keep[0] = keep[1] = keep[2] = keep[3] = 0xFFu; return; }
+  if constexpr (KM == KM_BITS) {
+    const int cb = a.C >> 3, cv = c0 >> 3;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) keep[j] = r0 + j < a.rows ? a.keep[(int64_t)(r0 + j) * cb + cv] : 0u;
+    return;
+  }
   keep[0] = keep[1] = keep[2] = keep[3] = 0u;
   const uint32_t thr = a.drop.threshold;
   const uint32_t k0 = (uint32_t)a.drop.seed, k1 = (uint32_t)(a.drop.seed >> 32);
@@ -204,6 +212,11 @@ __global__ void __launch_bounds__(256) bn_fwd_fast(FastArgs a) {
       if (j < nr) ld8<T>(x + (int64_t)(r0 + j) * a.C + g.c0, v[j]);
     uint32_t keep[4];
     keep_bits<KM>(a, r0, g.c0, keep);
+    if (KM != KM_NONE && KM != KM_BITS && a.keep) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (j < nr) a.keep[(int64_t)(r0 + j) * (a.C >> 3) + g.cv] = (uint8_t)keep[j];
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (j >= nr) break;
@@ -411,23 +424,26 @@ int64_t es_fast_part_floats(const es_view_t* v, int G) {
   return (int64_t)g.z * chunks * 3 * v->c;
 }
 
-static int keep_mode(const FastArgs& a) {
+static int keep_mode(const FastArgs& a, bool read_bits = false) {
   if (!a.drop.enabled) return KM_NONE;
+  if (read_bits && a.keep) return KM_BITS;
   if ((a.HW & 3) == 0) return KM_HW4;
   if (a.HW == 1 && (a.C & 3) == 0) return KM_ROW;
   return KM_GEN;
 }
 #define ES_KM_LAUNCH(K, T, KMV, grid, st, a) hipLaunchKernelGGL((K<T, KMV>), grid, dim3(256), 0, st, a)
-#define ES_KM_DISPATCH(a, K, dt, grid, st)                                                 \
+#define ES_KM_DISPATCH(a, K, dt, grid, st, RB)                                             \
   do {                                                                                    \
-    const int km_ = keep_mode(a);                                                         \
+    const int km_ = keep_mode(a, RB);                                                     \
     if (dt == ES_BF16) {                                                                  \
       if (km_ == KM_NONE) ES_KM_LAUNCH(K, bf16, KM_NONE, grid, st, a);                    \
+      else if (km_ == KM_BITS) ES_KM_LAUNCH(K, bf16, KM_BITS, grid, st, a);               \
       else if (km_ == KM_HW4) ES_KM_LAUNCH(K, bf16, KM_HW4, grid, st, a);                 \
       else if (km_ == KM_ROW) ES_KM_LAUNCH(K, bf16, KM_ROW, grid, st, a);                 \
       else ES_KM_LAUNCH(K, bf16, KM_GEN, grid, st, a);                                    \
     } else {                                                                              \
       if (km_ == KM_NONE) ES_KM_LAUNCH(K, float, KM_NONE, grid, st, a);                   \
+      else if (km_ == KM_BITS) ES_KM_LAUNCH(K, float, KM_BITS, grid, st, a);              \
       else if (km_ == KM_HW4) ES_KM_LAUNCH(K, float, KM_HW4, grid, st, a);                \
       else if (km_ == KM_ROW) ES_KM_LAUNCH(K, float, KM_ROW, grid, st, a);                \
       else ES_KM_LAUNCH(K, float, KM_GEN, grid, st, a);                                   \
@@ -436,14 +452,16 @@ static int keep_mode(const FastArgs& a) {
 #define ES_KM_LAUNCH1(K, T, KMV, grid, st, a) hipLaunchKernelGGL((K<T, 1, KMV>), grid, dim3(256), 0, st, a)
 #define ES_KM_DISPATCH1(a, K, dt, grid, st)                                                \
   do {                                                                                    \
-    const int km_ = keep_mode(a);                                                         \
+    const int km_ = keep_mode(a, true);                                                   \
     if (dt == ES_BF16) {                                                                  \
       if (km_ == KM_NONE) ES_KM_LAUNCH1(K, bf16, KM_NONE, grid, st, a);                   \
+      else if (km_ == KM_BITS) ES_KM_LAUNCH1(K, bf16, KM_BITS, grid, st, a);              \
       else if (km_ == KM_HW4) ES_KM_LAUNCH1(K, bf16, KM_HW4, grid, st, a);                \
       else if (km_ == KM_ROW) ES_KM_LAUNCH1(K, bf16, KM_ROW, grid, st, a);                \
       else ES_KM_LAUNCH1(K, bf16, KM_GEN, grid, st, a);                                   \
     } else {                                                                              \
       if (km_ == KM_NONE) ES_KM_LAUNCH1(K, float, KM_NONE, grid, st, a);                  \
+      else if (km_ == KM_BITS) ES_KM_LAUNCH1(K, float, KM_BITS, grid, st, a);             \
       else if (km_ == KM_HW4) ES_KM_LAUNCH1(K, float, KM_HW4, grid, st, a);               \
       else if (km_ == KM_ROW) ES_KM_LAUNCH1(K, float, KM_ROW, grid, st, a);               \
       else ES_KM_LAUNCH1(K, float, KM_GEN, grid, st, a);                                  \
@@ -458,7 +476,10 @@ static FastArgs mk(const es_view_t* v, const es_chain_t* ch, int G) {
   a.G = G;
   a.cg = G ? v->c / G : 1;
   a.zrows = G ? a.HW : a.rows;
-  if (ch) { a.drop = ch->drop; a.dfirst = ch->dropout_first; a.act = ch->act; a.slope = ch->slope; }
+  if (ch) {
+    a.drop = ch->drop; a.dfirst = ch->dropout_first; a.act = ch->act; a.slope = ch->slope;
+    a.keep = ch->drop.enabled ? ch->keep : nullptr;
+  }
   return a;
 }
 
@@ -480,7 +501,38 @@ void es_fast_norm_fwd(const es_view_t* v, int G, es_dtype_t dt, const void* xp, 
   FastArgs a = mk(v, ch, G);
   a.x = xp; a.out = yp;
   a.mean = nm->mean; a.invstd = nm->invstd; a.gamma = nm->gamma; a.beta = nm->beta;
-  ES_KM_DISPATCH(a, bn_fwd_fast, dt, grid, st);
+  ES_KM_DISPATCH(a, bn_fwd_fast, dt, grid, st, false);
+}
+
+// dropout keep bits alone (for a forward that did not run the fast kernels): same bits as
+// bn_fwd_fast would store
+template <int KM>
+__global__ void __launch_bounds__(256) keep_bits_kernel(FastArgs a) {
+  resolve_stream(a.drop);
+  const Geo g = geo(a);
+  if (!g.active) return;
+  const int ngroups = (g.rlim - g.rbase + 3) >> 2;
+  for (int grp = blockIdx.y * g.RGB + g.rg; grp < ngroups; grp += gridDim.y * g.RGB) {
+    const int r0 = g.rbase + grp * 4;
+    const int nr = min(4, g.rlim - r0);
+    uint32_t keep[4];
+    keep_bits<KM>(a, r0, g.c0, keep);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j < nr) a.keep[(int64_t)(r0 + j) * (a.C >> 3) + g.cv] = (uint8_t)keep[j];
+  }
+}
+
+void es_fast_keep_bits(const es_view_t* v, const es_chain_t* ch, hipStream_t st) {
+  es_view_t d = *v;   // logical rows (n, h, w) x C: the geometry of a dense view of the same shape
+  dim3 grid; int chunks;
+  fast_geometry(&d, 0, grid, chunks);
+  FastArgs a = mk(&d, ch, 0);
+  switch (keep_mode(a)) {
+    case KM_HW4: hipLaunchKernelGGL((keep_bits_kernel<KM_HW4>), grid, dim3(256), 0, st, a); break;
+    case KM_ROW: hipLaunchKernelGGL((keep_bits_kernel<KM_ROW>), grid, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL((keep_bits_kernel<KM_GEN>), grid, dim3(256), 0, st, a); break;
+  }
 }
 
 int es_fast_norm_bwd_reduce(const es_view_t* v, int G, es_dtype_t dt, const void* xp, const void* dyp,
@@ -503,6 +555,6 @@ int es_fast_norm_bwd_apply(const es_view_t* v, int G, es_dtype_t dt, const void*
   FastArgs a = mk(v, ch, G);
   a.x = xp; a.dy = dyp; a.out = dxp; a.a1 = a1; a.a2 = a2; a.dsum = dsum; a.part = part;
   a.mean = nm->mean; a.invstd = nm->invstd; a.gamma = nm->gamma; a.beta = nm->beta;
-  ES_KM_DISPATCH(a, bn_bwd_apply_fast, dt, grid, st);
+  ES_KM_DISPATCH(a, bn_bwd_apply_fast, dt, grid, st, true);
   return dsum ? (int)(grid.z * grid.y) : 0;
 }

@@ -42,7 +42,8 @@ class Norm(C.Structure):
 
 
 class Chain(C.Structure):
-    _fields_ = [("drop", Dropout), ("dropout_first", C.c_int), ("act", C.c_int), ("slope", C.c_float)]
+    _fields_ = [("drop", Dropout), ("dropout_first", C.c_int), ("act", C.c_int), ("slope", C.c_float),
+                ("keep", C.c_void_p)]
 
 
 class GenLoss(C.Structure):
@@ -212,3 +213,15 @@ def chain_struct(act=ACT_NONE, slope=0.1, drop: Dropout | None = None, dropout_f
     if drop is not None:
         ch.drop = drop
     return ch
+
+
+def attach_keep(chain: Chain, rows: int, channels: int, device):
+    """Give a dropout chain a device keep-bit buffer [rows][channels/8] (es_chain_t.keep): the
+    forward norm pass stores the mask it draws and the backward passes read it instead of re-running
+    Philox.  Returns the buffer (the caller keeps it alive until the backward), or None when the
+    chain has no dropout or channels % 8 != 0."""
+    if not chain.drop.enabled or channels % 8:
+        return None
+    buf = torch.empty(rows * (channels // 8), dtype=torch.uint8, device=device)
+    chain.keep = buf.data_ptr()
+    return buf

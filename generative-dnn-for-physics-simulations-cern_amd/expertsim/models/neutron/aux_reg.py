@@ -80,17 +80,22 @@ class AuxRegNeutron(ExpertModule):
             copy_act(img, x)
         ch = [self._chain(seed, stream_base, i, train) for i in range(4)] + [self._chain(0, 0, None, train)]
         c = {"x": x, "ch": ch}
+        keep = c["keep"] = []   # dropout keep bits: drawn in the forward norm pass, re-read backward
+
+        def bn(name, h, chain):
+            keep.append(hip.attach_keep(chain, h.dims[0] * h.dims[2] * h.dims[3], h.dims[1], h.t.device))
+            return o[name].fwd(h, chain, train=train)
         c["h1"] = o["c1"].fwd(x)
-        c["y1"], c["s1"] = o["b1"].fwd(c["h1"], ch[0], train=train)
+        c["y1"], c["s1"] = bn("b1", c["h1"], ch[0])
         c["q1"], c["i1"] = o["p1"].fwd(c["y1"])
         c["h2"] = o["c2"].fwd(c["q1"])
-        c["y2"], c["s2"] = o["b2"].fwd(c["h2"], ch[1], train=train)
+        c["y2"], c["s2"] = bn("b2", c["h2"], ch[1])
         c["q2"], c["i2"] = o["p2"].fwd(c["y2"])
         c["h3"] = o["c3"].fwd(c["q2"])
-        c["y3"], c["s3"] = o["b3"].fwd(c["h3"], ch[2], train=train)
+        c["y3"], c["s3"] = bn("b3", c["h3"], ch[2])
         c["q3"], c["i3"] = o["p3"].fwd(c["y3"])
         c["h4"] = o["c4"].fwd(c["q3"])
-        c["y4"], c["s4"] = o["b4"].fwd(c["h4"], ch[3], train=train)
+        c["y4"], c["s4"] = bn("b4", c["h4"], ch[3])
         c["h5"] = o["r"].fwd(c["y4"])
         c["y5"], c["s5"] = o["rb"].fwd(c["h5"], ch[4], train=train)
         c["f"] = avgpool_fwd(c["y5"])                                   # [B,64] fp32

@@ -82,6 +82,9 @@ class GeneratorNeutron(ExpertModule):
         copy_act(Act.of(noise), Act.of(x0m[:, :self.noise_dim]))
         copy_act(Act.of(cond), Act.of(x0m[:, self.noise_dim:]))
         ch = [self._chain(seed, stream_base, i, train) for i in range(5)]
+        # dropout keep bits, drawn once in the forward norm pass and re-read by the backward
+        keep = [hip.attach_keep(ch[i], B * r, c, dev)
+                for i, (r, c) in enumerate(((1, 256), (1, 21632), (576, 256), (2116, 128), (2025, 64)))]
         h1 = o["fc1"].fwd(x0)
         y1, s1 = o["bn1"].fwd(h1, ch[0], train=train)
         h2 = o["fc2"].fwd(y1)
@@ -98,7 +101,7 @@ class GeneratorNeutron(ExpertModule):
         h6 = o["c13"].fwd(y5, out_dtype=torch.float32)
         img = act_fwd(h6, hip.chain_struct(hip.ACT_RELU))
         ctx = dict(x0=x0, h1=h1, y1=y1, s1=s1, h2=h2, y2=y2, s2=s2, y2n=y2n, h3=h3, y3=y3, s3=s3,
-                   h4=h4, y4=y4, s4=s4, h5=h5, y5=y5, s5=s5, h6=h6, ch=ch)
+                   h4=h4, y4=y4, s4=s4, h5=h5, y5=y5, s5=s5, h6=h6, ch=ch, keep=keep)
         return img, ctx
 
     # --------------------------------------------------------------------------- backward

@@ -154,6 +154,9 @@ typedef struct {
   int dropout_first; /* 1: act(drop(norm(x)))  [generator.py:13-15]; 0: drop(act(norm(x))) [aux_reg.py:15-17] */
   int act;           /* ES_ACT_*                                                          */
   float slope;       /* LeakyReLU negative slope (0.1 everywhere in the reference)        */
+  uint8_t* keep;     /* optional device dropout keep bits, layout [n*h*w][c/8] (bit c%8 of byte
+                        (row, c/8)), c % 8 == 0 required: es_norm_act_fwd writes the mask it draws,
+                        es_norm_act_bwd then reads it instead of re-running Philox (same mask)   */
 } es_chain_t;
 
 /* Batch statistics of x (train-mode BN / GN / LN), written to mean/invstd per stats group.

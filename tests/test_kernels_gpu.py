@@ -260,6 +260,27 @@ def test_norm_chain(kind, drop):
     assert rel(dbt.cpu(), b_.grad) < btol
     red = (0, 2, 3) if x.dim() == 4 else (0,)
     assert float((dsum.cpu() - xr.grad.sum(red)).abs().max()) < 1e-3 * max(1.0, float(xr.grad.abs().max()))
+    if drop and x.shape[1] % 8 == 0:
+        # keep bits (es_chain_t.keep): the forward stores the mask it draws (bit-exact against the
+        # host Philox), the backward reads it and reproduces the regenerating backward exactly
+        ck = hip.chain_struct(hip.ACT_LRELU, 0.1, hip.dropout_struct(p, seed, stream, enabled=True),
+                              dropout_first=True)
+        C_ = x.shape[1]
+        rows = x.numel() // C_
+        kb = hip.attach_keep(ck, rows, C_, DEV)
+        op2 = NormOp(nk, gamma.to(DEV), beta.to(DEV), groups=groups,
+                     running_mean=torch.zeros(C_, device=DEV), running_var=torch.ones(C_, device=DEV))
+        yk, sk = op2.fwd(xa, ck)
+        assert torch.equal(yk.t, ya.t)
+        bits = kb.cpu().numpy().reshape(rows, C_ // 8)
+        keep = np.unpackbits(bits, axis=1, bitorder="little").astype(bool)     # [rows][C]
+        m = mask.numpy()
+        m_rows = m.transpose(0, 2, 3, 1).reshape(rows, C_) if x.dim() == 4 else m.reshape(rows, C_)
+        assert np.array_equal(keep, m_rows.astype(bool))
+        dg2, db2, ds2 = torch.zeros_like(dg), torch.zeros_like(dbt), torch.zeros_like(dsum)
+        dxk = op2.bwd(xa, sk, ck, gya, dgamma=dg2, dbeta=db2, dsum=ds2)
+        assert torch.equal(dxk.t, dxa.t)
+        assert torch.equal(dg2, dg) and torch.equal(db2, dbt)
 
 
 def test_dropout_mask_bit_exact():

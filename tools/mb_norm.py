@@ -70,6 +70,8 @@ def main():
     pool_case("A pool1 bf16 42x42x32", 512, 32, 42, 42, (2, 2), torch.bfloat16)
     bf, f32 = torch.bfloat16, torch.float32
     case("G c5 BN bf16 46x46x128", hip.NORM_BN, 1, 512, 128, 46, 46, bf, True)
+    case("G c5 BN bf16 no dropout", hip.NORM_BN, 1, 512, 128, 46, 46, bf, False)
+    case("G c0 BN bf16 24x24x256", hip.NORM_BN, 1, 512, 256, 24, 24, bf, True)
     case("G c9 BN bf16 45x45x64", hip.NORM_BN, 1, 512, 64, 45, 45, bf, True)
     case("D GN1 fp32 42x42x32", hip.NORM_GN, 8, 512, 32, 42, 42, f32, False)
     case("D GN2 fp32 19x19x16", hip.NORM_GN, 8, 512, 16, 19, 19, f32, False)
