@@ -56,8 +56,19 @@ struct ConvArgs {
   int dense_f32_out;   // host: output is fp32, dense [M][Ng] and beta == 0 (split-K allowed)
   int splitk;          // FWD / DGRAD split over blockIdx.z: fp32 atomics into a zeroed dense output
   SubPixel sp;         // ring kernels: sub-pixel class geometry (sp.on)
+  int vec_out;         // ring FWD/DGRAD: output rows channel-contiguous, 16-byte aligned, beta == 0
+  float* stats_part;   // ring FWD: per-row-tile BatchNorm partials [tile][3][Ng] (count, mean, M2)
 };
 
+
+// es_conv2d_fwd_stats: the caller's request for fused BatchNorm partials (host, per thread); the
+// ring FWD launch sets chunks when it writes them.
+struct StatsRequest {
+  float* part;
+  int64_t floats;
+  int chunks;
+};
+extern thread_local StatsRequest g_stats_req;
 
 // 8-wave LDS-DMA ring kernels (conv_mfma.hip).  Return 1 when the call was launched, 0 when the
 // shape is not eligible (the caller falls back to the kernels of conv_igemm.hip), <0 on error.

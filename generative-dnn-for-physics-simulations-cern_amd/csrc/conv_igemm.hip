@@ -987,6 +987,17 @@ extern "C" int es_conv2d_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void*
   return dispatch<MODE_FWD>(a, dt, avec, bvec, (hipStream_t)stream);
 }
 
+extern "C" int es_conv2d_fwd_stats(const es_conv_desc_t* d, es_dtype_t dt, const void* x, const int64_t xs[4],
+                                   const void* wk, const float* bias, void* y, es_dtype_t ydt, const int64_t ys[4],
+                                   float* part, int64_t part_floats, int* chunks, es_stream_t stream) {
+  ES_CHECK_ARG(part && chunks, "conv fwd stats: part / chunks NULL");
+  g_stats_req = StatsRequest{part, part_floats, 0};
+  const int rc = es_conv2d_fwd(d, dt, x, xs, wk, bias, y, ydt, ys, stream);
+  *chunks = g_stats_req.chunks;
+  g_stats_req = StatsRequest{nullptr, 0, 0};
+  return rc;
+}
+
 extern "C" int es_conv2d_dgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy,
                                const int64_t ys[4], const void* wd, void* dxu, es_dtype_t dxdt,
                                const int64_t dxs[4], float beta, es_stream_t stream) {

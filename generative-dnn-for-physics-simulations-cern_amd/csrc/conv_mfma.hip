@@ -358,20 +358,137 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   // epilogue: the wave's WM (<= 64) rows lie in one 64-row block -> one pixel, images nl
   const int mw = m0 + wm0;
   const int blk = mw >> 6;
-  if (blk >= nblk) return;
-  const int g = blk / PQ, pix = blk - g * PQ;
-  int y = pix / gw, x = pix - y * gw;
-  if constexpr (SP && MODE == MODE_FWD) {
-    y = sp.p0[cls] + 2 * y;
-    x = sp.q0[cls] + 2 * x;
+  const bool wave_live = blk < nblk;
+  int g = 0, y = 0, x = 0;
+  if (wave_live) {
+    g = blk / PQ;
+    const int pix = blk - g * PQ;
+    y = pix / gw;
+    x = pix - y * gw;
+    if constexpr (SP && MODE == MODE_FWD) {
+      y = sp.p0[cls] + 2 * y;
+      x = sp.q0[cls] + 2 * x;
+    }
   }
   const int64_t pixoff = (int64_t)y * a.os[2] + (int64_t)x * a.os[3];
   const int col16 = lane & 15, rq = (lane >> 4) * 4;
+  const int nbase = g * 64 + (mw & 63);   // image of the wave's row 0
+  // final values (bias added, rounded to the output dtype) back into acc
+#pragma unroll
+  for (int j = 0; j < RN; ++j) {
+    const int ng = n0 + wn0 + j * 16 + col16;
+    float bv = 0.f;
+    if constexpr (MODE == MODE_FWD) bv = (a.bias && ng < a.Ng) ? a.bias[ng] : 0.f;
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const float v = acc[i][j][jj] + bv;
+        acc[i][j][jj] = a.out_bf16 ? (float)(bf16)v : v;
+      }
+  }
+  if (a.vec_out) {
+    // BatchNorm statistics of the stored values (conv -> BatchNorm fusion): per column, count /
+    // mean / M2 over the wave's valid rows (lanes own 16 rows, Chan-merged across the 4 row
+    // groups by shuffles), then across the 4 row waves in LDS -> one [3][Ng] partial per row tile
+    float* part = a.stats_part;
+    __shared__ float st_n[4][BN], st_m[4][BN], st_q[4][BN];
+    if (part) {
+      const int wmi = wid >> 1;
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        float cnt = 0.f, s = 0.f;
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj)
+            if (wave_live && nbase + i * 16 + rq + jj < d.N) { cnt += 1.f; s += acc[i][j][jj]; }
+        const float mu = cnt > 0.f ? s / cnt : 0.f;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj)
+            if (wave_live && nbase + i * 16 + rq + jj < d.N) { const float e = acc[i][j][jj] - mu; q += e * e; }
+        float n_ = cnt, m_ = mu;
+#pragma unroll
+        for (int o = 16; o <= 32; o <<= 1) {
+          const float nb = __shfl_xor(n_, o, 64), mb = __shfl_xor(m_, o, 64), qb = __shfl_xor(q, o, 64);
+          const float nt = n_ + nb;
+          if (nt > 0.f) {
+            const float dl = mb - m_, f = nb / nt;
+            m_ += dl * f;
+            q += qb + dl * dl * n_ * f;
+          }
+          n_ = nt;
+        }
+        if (lane < 16) {
+          st_n[wmi][wn0 + j * 16 + col16] = n_;
+          st_m[wmi][wn0 + j * 16 + col16] = m_;
+          st_q[wmi][wn0 + j * 16 + col16] = q;
+        }
+      }
+    }
+    // stage the wave's tile in LDS (rows of WN values), then 16-byte row-contiguous stores
+    constexpr int ESZ_MAX = 4;
+    constexpr int PITCH = WN * ESZ_MAX + 16;
+    const int esz = a.out_bf16 ? 2 : 4;
+    const int pitch = WN * esz + 16;
+    __syncthreads();   // every wave is done with the ring slots
+    char* stg = smem + wid * (WM * PITCH);
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          char* p = stg + (i * 16 + rq + jj) * pitch + (j * 16 + col16) * esz;
+          if (a.out_bf16) *(bf16*)p = (bf16)acc[i][j][jj];
+          else *(float*)p = acc[i][j][jj];
+        }
+    __syncthreads();
+    const int cpr = WN * esz / 16;          // 16-byte chunks per row
+    const int rpi = 64 / cpr;               // rows per wave instruction
+    const int lr = lane / cpr, lch = lane % cpr;
+    if (wave_live) {
+      char* obase = (char*)a.out + (pixoff + n0 + wn0) * esz + lch * 16;
+      for (int r = lr; r < WM; r += rpi) {
+        const int n = nbase + r;
+        if (n >= d.N) break;
+        if (n0 + wn0 + lch * 16 / esz >= a.Ng) continue;
+        *(uint4*)(obase + (int64_t)n * a.os[0] * esz) = *(const uint4*)(stg + r * pitch + lch * 16);
+      }
+    }
+    if (part && wid < 2) {   // the wave pair of row block 0 merges the 4 row waves of its columns
+      for (int c = lane; c < WN; c += 64) {
+        const int col = wn0 + c;
+        float n_ = st_n[0][col], m_ = st_m[0][col], q = st_q[0][col];
+        for (int w = 1; w < 4; ++w) {
+          const float nb = st_n[w][col];
+          if (nb > 0.f) {
+            const float mb = st_m[w][col], nt = n_ + nb, dl = mb - m_, f = nb / nt;
+            m_ += dl * f;
+            q += st_q[w][col] + dl * dl * n_ * f;
+            n_ = nt;
+          }
+        }
+        if (n0 + col < a.Ng) {
+          float* pp = part + (int64_t)tl * 3 * a.Ng;   // one partial per row tile
+          pp[n0 + col] = n_;
+          pp[a.Ng + n0 + col] = m_;
+          pp[2 * a.Ng + n0 + col] = q;
+        }
+      }
+    }
+    (void)ESZ_MAX;
+    return;
+  }
+  if (!wave_live) return;
 #pragma unroll
   for (int i = 0; i < RM; ++i) {
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
-      const int n = g * 64 + (mw & 63) + i * 16 + rq + jj;
+      const int n = nbase + i * 16 + rq + jj;
       if (n >= d.N) continue;
       const int64_t rowoff = (int64_t)n * a.os[0] + pixoff;
 #pragma unroll
@@ -379,9 +496,6 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
         const int ng = n0 + wn0 + j * 16 + col16;
         if (ng >= a.Ng) continue;
         float v = acc[i][j][jj];
-        if constexpr (MODE == MODE_FWD) {
-          if (a.bias) v += a.bias[ng];
-        }
         const int64_t o = rowoff + (int64_t)ng * a.os[1];
         if (a.out_bf16) {
           bf16* yp = (bf16*)a.out + o;
@@ -583,6 +697,8 @@ bool g_subpixel_off = [] { const char* e = getenv("ES_NO_SUBPIXEL"); return e &&
 
 }  // namespace
 
+thread_local StatsRequest g_stats_req;
+
 // Class geometry of the sub-pixel decomposition (see SubPixel): output row p belongs to class
 // a = (p - pad) mod 2, p = p0 + 2u, source row of combined tap d = u + oh + d, dh = taps.
 void es_make_subpixel(const es_conv_desc_t& d, int row_tile, SubPixel& sp) {
@@ -680,6 +796,16 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
   if (sp_weights) {
     es_make_subpixel(d, BM, a.sp);
     if (mode == MODE_FWD) row_tiles = a.sp.tile0[4];
+  }
+  // staged 16-byte row stores: channel-contiguous rows, 16-byte aligned, no beta
+  const int vel = a.out_bf16 ? 8 : 4;
+  a.vec_out = a.os[1] == 1 && a.beta == 0.f && a.os[0] % vel == 0 && a.os[2] % vel == 0 && a.os[3] % vel == 0 &&
+              a.Ng % vel == 0 && ((uintptr_t)a.out & 15) == 0;
+  // fused BatchNorm statistics (es_conv2d_fwd_stats): one [3][Ng] partial per row tile
+  a.stats_part = nullptr;
+  if (mode == MODE_FWD && g_stats_req.part && a.vec_out && (int64_t)row_tiles * 3 * a.Ng <= g_stats_req.floats) {
+    a.stats_part = g_stats_req.part;
+    g_stats_req.chunks = row_tiles;
   }
 #define ES_RING(MD, BMV, BNV)                                                                  \
   (sp_weights ? launch_ring<MD, BMV, BNV, true>(a, row_tiles, st)                              \

@@ -599,6 +599,20 @@ extern "C" int es_norm_stats(const es_view_t* x, es_dtype_t xdt, const void* xp,
   return ES_OK;
 }
 
+extern "C" int es_norm_stats_finalize(const float* part, int chunks, int C, float eps, float* mean, float* invstd,
+                                      float* running_mean, float* running_var, float momentum, es_stream_t stream) {
+  ES_CHECK_ARG(part && chunks > 0 && C > 0, "norm_stats_finalize: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  if (chunks > 32)
+    hipLaunchKernelGGL(bn_finalize_block_kernel, dim3(C), dim3(256), 0, st, part, chunks, C, eps, mean, invstd,
+                       running_mean, running_var, momentum);
+  else
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, chunks, C, eps, mean,
+                       invstd, running_mean, running_var, momentum);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
 extern "C" int es_norm_act_fwd(const es_view_t* x, es_dtype_t xdt, const es_norm_t* nm,
                                const es_chain_t* ch, const es_view_t* addend, es_dtype_t adt,
                                const void* addend_ptr, const void* xp, const es_view_t* y,

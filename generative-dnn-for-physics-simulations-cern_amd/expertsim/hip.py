@@ -63,6 +63,7 @@ _SIGS = {
     "es_conv_subpixel_ok": (C.c_int, [P, C.c_int]),
     "es_subpixel_taps": (C.c_int, [C.c_int, C.c_int]),
     "es_conv2d_fwd": (C.c_int, [P, C.c_int, P, P, P, P, P, C.c_int, P, P]),
+    "es_conv2d_fwd_stats": (C.c_int, [P, C.c_int, P, P, P, P, P, C.c_int, P, P, I64, P, P]),
     "es_conv2d_dgrad": (C.c_int, [P, C.c_int, P, P, P, P, C.c_int, P, C.c_float, P]),
     "es_conv2d_wgrad": (C.c_int, [P, C.c_int, P, P, P, P, P, P]),
     "es_pack_conv_weight": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, C.c_int, P]),
@@ -70,6 +71,7 @@ _SIGS = {
     "es_norm_stats_ws_bytes": (I64, [P, C.c_int, C.c_int]),
     "es_norm_stats": (C.c_int, [P, C.c_int, P, C.c_int, C.c_int, C.c_float, P, P, P, P, C.c_float, P, P]),
     "es_norm_act_fwd": (C.c_int, [P, C.c_int, P, P, P, C.c_int, P, P, P, C.c_int, P, P]),
+    "es_norm_stats_finalize": (C.c_int, [P, C.c_int, C.c_int, C.c_float, P, P, P, P, C.c_float, P]),
     "es_norm_bwd_ws_bytes": (I64, [P, C.c_int, C.c_int]),
     "es_norm_act_bwd": (C.c_int, [P, C.c_int, P, P, P, P, C.c_int, P, P, C.c_int, P, P, C.c_int, P,
                                   C.c_float, P, P, P, P, P]),

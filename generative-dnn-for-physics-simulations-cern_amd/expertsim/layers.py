@@ -19,9 +19,10 @@ from . import hip
 class Act:
     """Logical (N, C, H, W) tensor over a flat device buffer with explicit element strides."""
 
-    __slots__ = ("t", "dims", "strides")
+    __slots__ = ("t", "dims", "strides", "bn_part")
 
     def __init__(self, t: torch.Tensor, dims, strides):
+        self.bn_part = None       # (partials, chunks) of fused BatchNorm statistics (ConvOp.fwd)
         self.t = t
         self.dims = tuple(int(d) for d in dims)
         self.strides = tuple(int(s) for s in strides)
@@ -261,7 +262,11 @@ class ConvOp:
             return False
         return bool(hip.lib().es_conv_subpixel_ok(C.byref(d), hip.dt_of_dtype(dtype)))
 
-    def fwd(self, x: Act, out_dtype=None, inv_scale=None, out: Act = None, with_bias=True) -> Act:
+    def fwd(self, x: Act, out_dtype=None, inv_scale=None, out: Act = None, with_bias=True,
+            bn_stats=False) -> Act:
+        """bn_stats: also ask for the BatchNorm partials of the output (es_conv2d_fwd_stats); when
+        the kernel provides them, out.bn_part = (part, chunks) and NormOp.stats merges those instead
+        of re-reading the output."""
         d = self.desc(x)
         cdt = x.t.dtype
         if self.subpixel(d, cdt):
@@ -273,8 +278,19 @@ class ConvOp:
             out = Act.nhwc(d.N, d.K, d.P, d.Q, out_dtype or cdt, x.t.device)
         bias = self.bias if (with_bias and self.bias is not None) else None
         with _probed(self.label and self.label + ".fwd"):
-          hip.call("es_conv2d_fwd", C.byref(d), x.dt, x.ptr, hip.strides4(x.strides), hip.ptr(wk),
-                 hip.ptr(bias), out.ptr, out.dt, hip.strides4(out.strides), hip.stream_ptr())
+            if bn_stats:
+                rows = ((d.N + 63) // 64) * 64 * d.P * d.Q
+                floats = ((rows + 127) // 128 + 8) * 3 * d.K
+                part = torch.empty(floats, dtype=torch.float32, device=x.t.device)
+                chunks = C.c_int(0)
+                hip.call("es_conv2d_fwd_stats", C.byref(d), x.dt, x.ptr, hip.strides4(x.strides), hip.ptr(wk),
+                         hip.ptr(bias), out.ptr, out.dt, hip.strides4(out.strides), hip.ptr(part), floats,
+                         C.byref(chunks), hip.stream_ptr())
+                if chunks.value > 0:
+                    out.bn_part = (part, chunks.value)
+            else:
+                hip.call("es_conv2d_fwd", C.byref(d), x.dt, x.ptr, hip.strides4(x.strides), hip.ptr(wk),
+                         hip.ptr(bias), out.ptr, out.dt, hip.strides4(out.strides), hip.stream_ptr())
         return out
 
     def dgrad(self, dy: Act, x: Act, dx_dtype=None, inv_scale=None, dx: Act = None, beta=0.0) -> Act:
@@ -353,6 +369,15 @@ class NormOp:
                     hip.NORM_LN: x.dims[0]}[self.kind]
         mean = torch.empty(n_groups, dtype=torch.float32, device=dev)
         invstd = torch.empty(n_groups, dtype=torch.float32, device=dev)
+        bn_part = getattr(x, "bn_part", None)
+        if self.kind == hip.NORM_BN and train and bn_part is not None:
+            # partials from the producing conv's epilogue (ConvOp.fwd(bn_stats=True))
+            part, chunks = bn_part
+            hip.call("es_norm_stats_finalize", hip.ptr(part), chunks, x.dims[1], float(self.eps), hip.ptr(mean),
+                     hip.ptr(invstd), hip.ptr(self.rm), hip.ptr(self.rv), float(self.momentum), hip.stream_ptr())
+            if self.nbt is not None:
+                self.nbt.add_(1)
+            return mean, invstd
         wsb = ws(hip.lib().es_norm_stats_ws_bytes(C.byref(x.view), self.kind, self.groups), dev)
         upd = self.kind == hip.NORM_BN and train
         hip.call("es_norm_stats", C.byref(x.view), x.dt, x.ptr, self.kind, self.groups, float(self.eps),

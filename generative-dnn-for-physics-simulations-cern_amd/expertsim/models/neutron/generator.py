@@ -92,11 +92,11 @@ class GeneratorNeutron(ExpertModule):
         # [B, 21632] rows are NCHW [B,128,13,13]; re-layout to NHWC for the vector gather
         y2n = Act.nhwc(B, 128, 13, 13, cdt, dev)
         copy_act(Act(y2.t, (B, 128, 13, 13), (21632, 169, 13, 1)), y2n)
-        h3 = o["c0"].fwd(y2n)
+        h3 = o["c0"].fwd(y2n, bn_stats=train)         # BatchNorm statistics from the conv epilogue
         y3, s3 = o["bn3"].fwd(h3, ch[2], train=train)
-        h4 = o["c5"].fwd(y3)
+        h4 = o["c5"].fwd(y3, bn_stats=train)
         y4, s4 = o["bn4"].fwd(h4, ch[3], train=train)
-        h5 = o["c9"].fwd(y4)
+        h5 = o["c9"].fwd(y4, bn_stats=train)
         y5, s5 = o["bn5"].fwd(h5, ch[4], train=train)
         h6 = o["c13"].fwd(y5, out_dtype=torch.float32)
         img = act_fwd(h6, hip.chain_struct(hip.ACT_RELU))

@@ -104,6 +104,14 @@ int es_subpixel_taps(int R, int S);
 int es_conv2d_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x, const int64_t xs[4],
                   const void* wk, const float* bias, void* y, es_dtype_t ydt, const int64_t ys[4],
                   es_stream_t stream);
+/* es_conv2d_fwd fused with the BatchNorm statistics of the stored y (torch batch_norm train mode,
+ * neutron/generator.py:26,31,35): when the 8-wave ring kernel runs this conv, its epilogue also
+ * writes per row tile and channel (count, mean, M2) partials to part [chunks][3][K] (part_floats
+ * available) and *chunks > 0; es_norm_stats_finalize then merges them.  *chunks == 0 means y was
+ * computed but no partials were written (use es_norm_stats). */
+int es_conv2d_fwd_stats(const es_conv_desc_t* d, es_dtype_t dt, const void* x, const int64_t xs[4],
+                        const void* wk, const float* bias, void* y, es_dtype_t ydt, const int64_t ys[4],
+                        float* part, int64_t part_floats, int* chunks, es_stream_t stream);
 /* dxu[n,c,hu,wu] = sum_{k,r,s} dy[n,k,p,q] * W[k,c,r,s] over (hu+pad-r) = p*stride, ...
  * (gradient w.r.t. the UPSAMPLED input; es_upsample_bwd folds it to the source grid).  With
  * integer factors d->up_h/up_w the fold happens inside the GEMM (K grows by up_h*up_w) and the
@@ -167,6 +175,10 @@ int es_norm_stats(const es_view_t* x, es_dtype_t xdt, const void* xp, int kind, 
                   float eps, float* mean, float* invstd, float* running_mean, float* running_var,
                   float momentum, void* ws, es_stream_t stream);
 /* y = chain(norm(x) [+ addend]) ; addend may be NULL (residual add of proton/aux_reg.py:130) */
+/* Merge BatchNorm partials [chunks][3][C] (count, mean, M2; es_conv2d_fwd_stats) into mean /
+ * invstd and the running statistics (momentum, unbiased variance), as es_norm_stats does. */
+int es_norm_stats_finalize(const float* part, int chunks, int C, float eps, float* mean, float* invstd,
+                           float* running_mean, float* running_var, float momentum, es_stream_t stream);
 int es_norm_act_fwd(const es_view_t* x, es_dtype_t xdt, const es_norm_t* nm, const es_chain_t* ch,
                     const es_view_t* addend, es_dtype_t adt, const void* addend_ptr, const void* xp,
                     const es_view_t* y, es_dtype_t ydt, void* yp, es_stream_t stream);

@@ -440,3 +440,32 @@ def test_conv_subpixel(case):
     finally:
         hip.lib().es_conv_set_subpixel(old)
     assert rel(dw.cpu(), dw0.cpu()) < 1e-4   # same products, fp32 sums in another order
+
+
+@pytest.mark.parametrize("case", [(3, 256, 24, 24, 128, 3, (2, 2)), (70, 128, 13, 13, 256, 3, (2, 2)),
+                                  (5, 128, 46, 46, 64, 2, None)])
+def test_conv_fused_bn_stats(case):
+    """es_conv2d_fwd_stats + es_norm_stats_finalize give the BatchNorm statistics of the stored
+    bf16 output (count / mean / M2 partials from the ring epilogue) = es_norm_stats over it."""
+    hip = _hip()
+    from expertsim.layers import ConvOp, NormOp, Upsample
+    N, Cin, H, W, Cout, k, up = case
+    torch.manual_seed(4)
+    x = torch.randn(N, Cin, H, W)
+    w = torch.randn(Cout, Cin, k, k) / np.sqrt(Cin * k * k)
+    b = torch.randn(Cout) + 2.0
+    op = ConvOp(torch.nn.Parameter(w.to(DEV)), torch.nn.Parameter(b.to(DEV)),
+                upsample=Upsample((H, W), scale=up) if up else None)
+    xa = to_act(x, torch.bfloat16)
+    y1 = op.fwd(xa, bn_stats=True)
+    assert y1.bn_part is not None and y1.bn_part[1] > 0
+    y0 = op.fwd(xa)
+    assert torch.equal(y1.t, y0.t)
+    mk = lambda: NormOp(hip.NORM_BN, torch.ones(Cout, device=DEV), torch.zeros(Cout, device=DEV),
+                        running_mean=torch.zeros(Cout, device=DEV), running_var=torch.ones(Cout, device=DEV))
+    n1, n0 = mk(), mk()
+    m1, i1 = n1.stats(y1)
+    m0, i0 = n0.stats(y0)
+    assert rel(m1.cpu(), m0.cpu()) < 1e-5
+    assert rel(i1.cpu(), i0.cpu()) < 1e-5
+    assert rel(n1.rv.cpu(), n0.rv.cpu()) < 1e-5 and rel(n1.rm.cpu(), n0.rm.cpu()) < 1e-5
