@@ -34,7 +34,7 @@ struct SubPixel {
   int oh[4], ow[4];      // source row of (u, d) = u + oh + d
   int dh[4], dw[4];      // combined taps
   int tap0[5];           // prefix sums of dh*dw (packed weight blocks)
-  int tile0[5];          // FWD: prefix sums of the classes' row tiles
+  int tile0[5];          // FWD: prefix sums of the classes' row tiles (per 8-image group)
 };
 void es_make_subpixel(const es_conv_desc_t& d, int row_tile, SubPixel& sp);
 
@@ -56,6 +56,7 @@ struct ConvArgs {
   int dense_f32_out;   // host: output is fp32, dense [M][Ng] and beta == 0 (split-K allowed)
   int splitk;          // FWD / DGRAD split over blockIdx.z: fp32 atomics into a zeroed dense output
   SubPixel sp;         // ring kernels: sub-pixel class geometry (sp.on)
+  int ng;              // ring FWD/DGRAD: images per group of the row order (8, 16, 32 or 64)
   int vec_out;         // ring FWD/DGRAD: output rows channel-contiguous, 16-byte aligned, beta == 0
   float* stats_part;   // ring FWD: per-row-tile BatchNorm partials [tile][3][Ng] (count, mean, M2)
 };

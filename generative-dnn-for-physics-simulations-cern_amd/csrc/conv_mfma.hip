@@ -169,29 +169,40 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT];
   const es_conv_desc_t& d = a.d;
   const SubPixel& sp = a.sp;
-  const int G = (d.N + 63) >> 6;
 
   // tile order: the column tiles of one row tile are consecutive (they share the gathered rows)
   const int nt = gridDim.y;
   const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * nt);
   const int tl = wg / nt, n0 = (wg % nt) * BN;
-  // row grid: FWD output pixels (SP: the class's output pixels), DGRAD input pixels (source grid
-  // when the upsample is folded)
-  int cls = 0, m0 = tl * BM, gh, gw;
+  // Row order: image groups g of NG = a.ng images (8..64); inside a group, per class (SP FWD: 4
+  // parity classes, else one) the class's pixels in tiles of NB = BM/NG pixels (each class
+  // segment padded to whole tiles); a tile is NG images x NB pixels, a DMA piece (8 rows) is 8
+  // images at one pixel.  Consecutive tiles (one XCD) stay on the same images, so their sources
+  // share the L2; the host picks NG per operand (small groups keep a forward gather's source
+  // footprint inside one XCD's L2).
+  const int NG = a.ng, PPG = NG >> 3;                    // pieces per pixel
+  const int NB = BM / NG;
+  int cls = 0, gh, gw, TT, seg0 = 0;
   if constexpr (MODE == MODE_FWD && SP) {
-    cls = (tl >= sp.tile0[1]) + (tl >= sp.tile0[2]) + (tl >= sp.tile0[3]);
-    m0 = (tl - sp.tile0[cls]) * BM;
+    TT = sp.tile0[4];
+    const int r = tl % TT;
+    cls = (r >= sp.tile0[1]) + (r >= sp.tile0[2]) + (r >= sp.tile0[3]);
+    seg0 = sp.tile0[cls];
     gh = sp.ph[cls];
     gw = sp.pw[cls];
-  } else if constexpr (MODE == MODE_FWD) {
-    gh = d.P;
-    gw = d.Q;
   } else {
-    gh = a.fold ? d.H : d.Hu;
-    gw = a.fold ? d.W : d.Wu;
+    if constexpr (MODE == MODE_FWD) {
+      gh = d.P;
+      gw = d.Q;
+    } else {
+      gh = a.fold ? d.H : d.Hu;
+      gw = a.fold ? d.W : d.Wu;
+    }
+    TT = (gh * gw + NB - 1) / NB;
   }
   const int PQ = gh * gw;
-  const int nblk = G * PQ;                      // 64-row blocks
+  const int gi = tl / TT;                                // image group: images NG gi ..
+  const int pix0 = (tl - gi * TT - seg0) * NB;           // first pixel of the tile
 
   const int lane = threadIdx.x & 63, wid = uni(threadIdx.x >> 6);
   const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
@@ -220,16 +231,16 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   bool pval[APW];
 #pragma unroll
   for (int j = 0; j < APW; ++j) {
-    const int pi = wid * APW + j;                 // piece of the tile (8 rows)
-    const int blk = (m0 >> 6) + (pi >> 3);        // 64-row block: (g, pix)
-    const int nl = ((pi & 7) << 3) + lrow;
+    const int pi = wid * APW + j;                 // piece of the tile: pixel pix0 + pi / PPG
     const int rr = pi * 8 + lrow;                 // row within the tile (swizzle)
     const int lc = pc ^ ((rr >> 1) & 7);
-    pval[j] = blk < nblk;
-    const int bb = pval[j] ? blk : 0;
-    const int g = bb / PQ, pix = bb - g * PQ;
-    const int y = pix / gw, x = pix - y * gw;
-    alane[j] = (uint32_t)((g * 64 + nl) * (int)a.as[0] * 2 + lc * 16);
+    const int ppix = pi / PPG;
+    const int pix = pix0 + ppix;
+    pval[j] = pix < PQ;
+    const int pp = pval[j] ? pix : 0;
+    const int y = pp / gw, x = pp - y * gw;
+    const int img = gi * NG + (pi - ppix * PPG) * 8 + lrow;
+    alane[j] = (uint32_t)(img * (int)a.as[0] * 2 + lc * 16);   // images >= N: past num_records
     if constexpr (MODE == MODE_FWD && SP) {       // source row = u + oh + d
       pc0[j] = y + sp.oh[cls];
       pc1[j] = x + sp.ow[cls];
@@ -355,24 +366,21 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   };
   ring_loop<PW>(nk, smem, SLOT, issue, load, mma);
 
-  // epilogue: the wave's WM (<= 64) rows lie in one 64-row block -> one pixel, images nl
-  const int mw = m0 + wm0;
-  const int blk = mw >> 6;
-  const bool wave_live = blk < nblk;
-  int g = 0, y = 0, x = 0;
-  if (wave_live) {
-    g = blk / PQ;
-    const int pix = blk - g * PQ;
-    y = pix / gw;
-    x = pix - y * gw;
+  // epilogue.  Wave row r (0..WM-1) = tile row t = wm0 + r: pixel pix0 + t / NG, image
+  // NG gi + t % NG.
+  const int col16 = lane & 15, rq = (lane >> 4) * 4;
+  auto row_pix = [&](int r) { return pix0 + (wm0 + r) / NG; };
+  auto row_img = [&](int r) { return gi * NG + (wm0 + r) % NG; };
+  auto row_off = [&](int r) -> int64_t {   // element offset of the wave row's output pixel
+    const int pix = row_pix(r);
+    int y = pix / gw, x = pix - y * gw;
     if constexpr (SP && MODE == MODE_FWD) {
       y = sp.p0[cls] + 2 * y;
       x = sp.q0[cls] + 2 * x;
     }
-  }
-  const int64_t pixoff = (int64_t)y * a.os[2] + (int64_t)x * a.os[3];
-  const int col16 = lane & 15, rq = (lane >> 4) * 4;
-  const int nbase = g * 64 + (mw & 63);   // image of the wave's row 0
+    return (int64_t)row_img(r) * a.os[0] + (int64_t)y * a.os[2] + (int64_t)x * a.os[3];
+  };
+  auto row_ok = [&](int r) { return row_pix(r) < PQ && row_img(r) < d.N; };
   // final values (bias added, rounded to the output dtype) back into acc
 #pragma unroll
   for (int j = 0; j < RN; ++j) {
@@ -395,6 +403,11 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
     __shared__ float st_n[4][BN], st_m[4][BN], st_q[4][BN];
     if (part) {
       const int wmi = wid >> 1;
+      bool okr[RM][4];
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) okr[i][jj] = row_ok(i * 16 + rq + jj);
 #pragma unroll
       for (int j = 0; j < RN; ++j) {
         float cnt = 0.f, s = 0.f;
@@ -402,14 +415,14 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
         for (int i = 0; i < RM; ++i)
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj)
-            if (wave_live && nbase + i * 16 + rq + jj < d.N) { cnt += 1.f; s += acc[i][j][jj]; }
+            if (okr[i][jj]) { cnt += 1.f; s += acc[i][j][jj]; }
         const float mu = cnt > 0.f ? s / cnt : 0.f;
         float q = 0.f;
 #pragma unroll
         for (int i = 0; i < RM; ++i)
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj)
-            if (wave_live && nbase + i * 16 + rq + jj < d.N) { const float e = acc[i][j][jj] - mu; q += e * e; }
+            if (okr[i][jj]) { const float e = acc[i][j][jj] - mu; q += e * e; }
         float n_ = cnt, m_ = mu;
 #pragma unroll
         for (int o = 16; o <= 32; o <<= 1) {
@@ -430,8 +443,7 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
       }
     }
     // stage the wave's tile in LDS (rows of WN values), then 16-byte row-contiguous stores
-    constexpr int ESZ_MAX = 4;
-    constexpr int PITCH = WN * ESZ_MAX + 16;
+    constexpr int PITCH = WN * 4 + 16;
     const int esz = a.out_bf16 ? 2 : 4;
     const int pitch = WN * esz + 16;
     __syncthreads();   // every wave is done with the ring slots
@@ -450,14 +462,10 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
     const int cpr = WN * esz / 16;          // 16-byte chunks per row
     const int rpi = 64 / cpr;               // rows per wave instruction
     const int lr = lane / cpr, lch = lane % cpr;
-    if (wave_live) {
-      char* obase = (char*)a.out + (pixoff + n0 + wn0) * esz + lch * 16;
-      for (int r = lr; r < WM; r += rpi) {
-        const int n = nbase + r;
-        if (n >= d.N) break;
-        if (n0 + wn0 + lch * 16 / esz >= a.Ng) continue;
-        *(uint4*)(obase + (int64_t)n * a.os[0] * esz) = *(const uint4*)(stg + r * pitch + lch * 16);
-      }
+    if (n0 + wn0 + lch * 16 / esz < a.Ng) {
+      char* obase = (char*)a.out + (int64_t)(n0 + wn0) * esz + lch * 16;
+      for (int r = lr; r < WM; r += rpi)
+        if (row_ok(r)) *(uint4*)(obase + row_off(r) * esz) = *(const uint4*)(stg + r * pitch + lch * 16);
     }
     if (part && wid < 2) {   // the wave pair of row block 0 merges the 4 row waves of its columns
       for (int c = lane; c < WN; c += 64) {
@@ -480,17 +488,15 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
         }
       }
     }
-    (void)ESZ_MAX;
     return;
   }
-  if (!wave_live) return;
 #pragma unroll
   for (int i = 0; i < RM; ++i) {
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
-      const int n = nbase + i * 16 + rq + jj;
-      if (n >= d.N) continue;
-      const int64_t rowoff = (int64_t)n * a.os[0] + pixoff;
+      const int r = i * 16 + rq + jj;
+      if (!row_ok(r)) continue;
+      const int64_t rowoff = row_off(r);
 #pragma unroll
       for (int j = 0; j < RN; ++j) {
         const int ng = n0 + wn0 + j * 16 + col16;
@@ -693,6 +699,7 @@ bool dense_small(const int64_t s[4], int n, int c, int h, int w) {
          (int64_t)n * s[0] * 2 < (1ll << 30);
 }
 
+int g_ring_ng = [] { const char* e = getenv("ES_RING_NG"); return e ? atoi(e) : 0; }();
 bool g_subpixel_off = [] { const char* e = getenv("ES_NO_SUBPIXEL"); return e && e[0] == '1'; }();
 
 }  // namespace
@@ -701,6 +708,7 @@ thread_local StatsRequest g_stats_req;
 
 // Class geometry of the sub-pixel decomposition (see SubPixel): output row p belongs to class
 // a = (p - pad) mod 2, p = p0 + 2u, source row of combined tap d = u + oh + d, dh = taps.
+// tile0: prefix over the classes of ceil(class pixels / row_tile) (row_tile = pixels per FWD tile).
 void es_make_subpixel(const es_conv_desc_t& d, int row_tile, SubPixel& sp) {
   int dhv[2], dwv[2], p0v[2], q0v[2], phv[2], pwv[2], ohv[2], owv[2];
   for (int a = 0; a < 2; ++a) {
@@ -716,7 +724,6 @@ void es_make_subpixel(const es_conv_desc_t& d, int row_tile, SubPixel& sp) {
   sp.on = 1;
   sp.tap0[0] = 0;
   sp.tile0[0] = 0;
-  const int G = (d.N + 63) / 64;
   for (int c = 0; c < 4; ++c) {
     const int a = c >> 1, b = c & 1;
     sp.ph[c] = phv[a];
@@ -728,8 +735,8 @@ void es_make_subpixel(const es_conv_desc_t& d, int row_tile, SubPixel& sp) {
     sp.dh[c] = dhv[a];
     sp.dw[c] = dwv[b];
     sp.tap0[c + 1] = sp.tap0[c] + dhv[a] * dwv[b];
-    const int rows = G * 64 * phv[a] * pwv[b];
-    sp.tile0[c + 1] = sp.tile0[c] + (row_tile > 0 ? (rows + row_tile - 1) / row_tile : 0);
+    const int pix = phv[a] * pwv[b];
+    sp.tile0[c + 1] = sp.tile0[c] + (row_tile > 0 ? (pix + row_tile - 1) / row_tile : 0);
   }
 }
 
@@ -780,22 +787,27 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
     return 1;
   }
   // caller checked: bf16, channels % 64 == 0, K % 64 == 0 per step
-  int rows;
+  int PQ;
   if (mode == MODE_FWD) {
     if (!dense_small(a.as, d.N, d.C, d.H, d.W)) return sp_weights ? -1 : 0;
-    rows = ((d.N + 63) / 64) * 64 * d.P * d.Q;
+    PQ = d.P * d.Q;
   } else {
     if (!dense_small(a.as, d.N, d.K, d.P, d.Q)) return sp_weights ? -1 : 0;
-    rows = ((d.N + 63) / 64) * 64 * (a.fold ? d.H * d.W : d.Hu * d.Wu);
+    PQ = a.fold ? d.H * d.W : d.Hu * d.Wu;
   }
   if ((int64_t)a.Ng * a.Kd * 2 * (sp_weights ? 2 : 1) >= (1ll << 30)) return sp_weights ? -1 : 0;
+  // image group size of the row order (see conv_ring_kernel).  Measured on the whole train step
+  // (tools/gpu_ab.sh, one box): 64 > 16 > 8 for both FWD and DGRAD, although an isolated FWD
+  // prefers 8 (less MALL traffic).  ES_RING_NG overrides it (measurement).
+  a.ng = g_ring_ng > 0 ? g_ring_ng : 64;
+  const int NGI = (d.N + a.ng - 1) / a.ng;
   const int nt128 = (a.Ng + 127) / 128;
-  const bool big = ((rows + 255) / 256) * nt128 >= 768;   // >= 3 rounds of 256-row tiles
-  const int BM = big ? 256 : 128;
-  int row_tiles = (rows + BM - 1) / BM;
+  const bool big = (int64_t)NGI * a.ng * PQ / 256 * nt128 >= 768;   // >= 3 rounds of 256-row tiles
+  const int BM = big ? 256 : 128, NB = BM / a.ng;
+  int row_tiles = NGI * ((PQ + NB - 1) / NB);
   if (sp_weights) {
-    es_make_subpixel(d, BM, a.sp);
-    if (mode == MODE_FWD) row_tiles = a.sp.tile0[4];
+    es_make_subpixel(d, NB, a.sp);   // FWD: tile0 = per-class tile prefix of one image group
+    if (mode == MODE_FWD) row_tiles = NGI * a.sp.tile0[4];
   }
   // staged 16-byte row stores: channel-contiguous rows, 16-byte aligned, no beta
   const int vel = a.out_bf16 ? 8 : 4;

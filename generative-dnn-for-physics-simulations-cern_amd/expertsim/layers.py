@@ -279,8 +279,8 @@ class ConvOp:
         bias = self.bias if (with_bias and self.bias is not None) else None
         with _probed(self.label and self.label + ".fwd"):
             if bn_stats:
-                rows = ((d.N + 63) // 64) * 64 * d.P * d.Q
-                floats = ((rows + 127) // 128 + 8) * 3 * d.K
+                tiles = ((d.N + 7) // 8) * (d.P * d.Q // 16 + 8)   # >= the ring's row tiles
+                floats = tiles * 3 * d.K
                 part = torch.empty(floats, dtype=torch.float32, device=x.t.device)
                 chunks = C.c_int(0)
                 hip.call("es_conv2d_fwd_stats", C.byref(d), x.dt, x.ptr, hip.strides4(x.strides), hip.ptr(wk),
