@@ -87,12 +87,20 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((ch
 typedef short short4_t __attribute__((ext_vector_type(4)));
 typedef short short8_t __attribute__((ext_vector_type(8)));
 
-__device__ __forceinline__ int swz_tr(int k) { return ((k & 3) << 1) | (((k >> 3) & 1) << 3); }
+// 16-byte chunk swizzle of k-row k in a [64][BROWS] image: the 8 k-rows one half-wave reads with
+// ds_read_b64_tr_b16 (k0 + {0..3, 8..11}) must hit 8 distinct 32-byte bank groups.
+//   BROWS >= 128 (k-rows of >= 256 B, every k-row starts at bank 0): XOR 2(k&3) | 8((k>>3)&1)
+//   BROWS == 64  (128-B k-rows, odd rows start at bank 32): XOR 2((k>>1)&1) | 4((k>>3)&1)
+template <int BROWS>
+__device__ __forceinline__ int swz_tr(int k) {
+  if constexpr (BROWS >= 128) return ((k & 3) << 1) | (((k >> 3) & 1) << 3);
+  else return (((k >> 1) & 1) << 1) | (((k >> 3) & 1) << 2);
+}
 
 // byte offset of (k-row k, row) in a [64][BROWS] bf16 image
 template <int BROWS>
 __device__ __forceinline__ int tr_off(int k, int row) {
-  return k * (BROWS * 2) + ((((row >> 3) ^ swz_tr(k)) << 4) | ((row & 7) << 1));
+  return k * (BROWS * 2) + ((((row >> 3) ^ swz_tr<BROWS>(k)) << 4) | ((row & 7) << 1));
 }
 
 // A/B fragment of v_mfma_f32_16x16x32_bf16 from a [k][rows] image: lane l gets row r0 + (l & 15),
@@ -528,7 +536,7 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
 // ---------------------------------------------------------------------------------------------
 template <int BM, int BN, bool SP>
 __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
-  constexpr int WGM = BM / 64, WGN = 8 / WGM;   // waves along M / N
+  constexpr int WGM = BM >= 64 ? BM / 64 : 1, WGN = 8 / WGM;   // waves along M / N
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int RM = WM / 16, RN = WN / 16;
   constexpr int AIMG = 64 * BM * 2, SLOT = 64 * (BM + BN) * 2;
@@ -577,12 +585,12 @@ __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
 #pragma unroll
   for (int j = 0; j < APW; ++j) {
     const int kr = (wid * APW + j) * (64 / ALPR) + lane / ALPR;   // image of the K-step
-    alane[j] = (uint32_t)(kr * as0b + (m0 + ((lane % ALPR) ^ swz_tr(kr)) * 8) * 2);
+    alane[j] = (uint32_t)(kr * as0b + (m0 + ((lane % ALPR) ^ swz_tr<BM>(kr)) * 8) * 2);
   }
 #pragma unroll
   for (int j = 0; j < BPW; ++j) {
     const int kr = (wid * BPW + j) * (64 / BLPR) + lane / BLPR;
-    blane[j] = (uint32_t)(kr * bs0b + (cb + ((lane % BLPR) ^ swz_tr(kr)) * 8) * 2);
+    blane[j] = (uint32_t)(kr * bs0b + (cb + ((lane % BLPR) ^ swz_tr<BN>(kr)) * 8) * 2);
   }
 
   // K-step cursor (uniform): pixel (p, q) of the grid and image group gi of step t = (p*gq + q)*G + gi
@@ -782,6 +790,7 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
     if (d.K % 256 == 0 && d.C % 128 == 0) ES_WG(256, 128);
     else if (d.K % 128 == 0 && d.C % 256 == 0) ES_WG(128, 256);
     else if (d.K % 128 == 0 && d.C % 128 == 0) ES_WG(128, 128);
+    else if (d.K == 64 && d.C % 128 == 0) ES_WG(64, 128);   // neutron G conv_layers.9 (128 -> 64)
     else return 0;
 #undef ES_WG
     return 1;

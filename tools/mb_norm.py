@@ -25,7 +25,7 @@ def timed(fn, reps=20):
     return a.elapsed_time(b) / reps * 1e3   # us
 
 
-def case(name, kind, groups, N, C, H, W, dtype, drop):
+def case(name, kind, groups, N, C, H, W, dtype, drop, bits=False):
     dev = "cuda"
     x = Act.nhwc(N, C, H, W, dtype, dev)
     x.t.normal_()
@@ -37,6 +37,7 @@ def case(name, kind, groups, N, C, H, W, dtype, drop):
     op = NormOp(kind, g, b, groups=groups, running_mean=rm, running_var=rv)
     d = hip.dropout_struct(0.2, 1234, 7, enabled=drop)
     ch = hip.chain_struct(hip.ACT_LRELU, 0.1, d, dropout_first=True)
+    keep = hip.attach_keep(ch, N * H * W, C, dev) if bits else None   # noqa: F841 (kept alive)
     nbytes = x.t.numel() * x.t.element_size()
     stats = op.stats(x)
     y = x.like_nhwc(dtype)
@@ -71,6 +72,7 @@ def main():
     bf, f32 = torch.bfloat16, torch.float32
     case("G c5 BN bf16 46x46x128", hip.NORM_BN, 1, 512, 128, 46, 46, bf, True)
     case("G c5 BN bf16 no dropout", hip.NORM_BN, 1, 512, 128, 46, 46, bf, False)
+    case("G c5 BN bf16 keep bits", hip.NORM_BN, 1, 512, 128, 46, 46, bf, True, True)
     case("G c0 BN bf16 24x24x256", hip.NORM_BN, 1, 512, 256, 24, 24, bf, True)
     case("G c9 BN bf16 45x45x64", hip.NORM_BN, 1, 512, 64, 45, 45, bf, True)
     case("D GN1 fp32 42x42x32", hip.NORM_GN, 8, 512, 32, 42, 42, f32, False)
