@@ -707,6 +707,7 @@ bool dense_small(const int64_t s[4], int n, int c, int h, int w) {
          (int64_t)n * s[0] * 2 < (1ll << 30);
 }
 
+bool g_ring_shortk = [] { const char* e = getenv("ES_RING_SHORTK"); return !(e && e[0] == '0'); }();
 int g_ring_ng = [] { const char* e = getenv("ES_RING_NG"); return e ? atoi(e) : 0; }();
 bool g_subpixel_off = [] { const char* e = getenv("ES_NO_SUBPIXEL"); return e && e[0] == '1'; }();
 
@@ -811,7 +812,11 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
   a.ng = g_ring_ng > 0 ? g_ring_ng : 64;
   const int NGI = (d.N + a.ng - 1) / a.ng;
   const int nt128 = (a.Ng + 127) / 128;
-  const bool big = (int64_t)NGI * a.ng * PQ / 256 * nt128 >= 768;   // >= 3 rounds of 256-row tiles
+  // short-K FWD (<= 8 K-steps, e.g. conv_layers.9: 2x2 taps x 128 channels): 128 x 64 tiles (72 KiB
+  // of LDS, two workgroups per CU) so one tile's fill and epilogue overlap another's MFMAs
+  // (measured 201 -> 177 us; the same rule on the DGRAD of that conv was slower)
+  const bool shortk = g_ring_shortk && mode == MODE_FWD && !sp_weights && a.Kd / 64 <= 8;
+  const bool big = !shortk && (int64_t)NGI * a.ng * PQ / 256 * nt128 >= 768;   // >= 3 rounds of 256-row tiles
   const int BM = big ? 256 : 128, NB = BM / a.ng;
   int row_tiles = NGI * ((PQ + NB - 1) / NB);
   if (sp_weights) {
@@ -832,10 +837,10 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
   (sp_weights ? launch_ring<MD, BMV, BNV, true>(a, row_tiles, st)                              \
               : launch_ring<MD, BMV, BNV, false>(a, row_tiles, st))
   if (mode == MODE_FWD) {
-    if (a.Ng <= 64) big ? ES_RING(MODE_FWD, 256, 64) : ES_RING(MODE_FWD, 128, 64);
+    if (a.Ng <= 64 || shortk) big ? ES_RING(MODE_FWD, 256, 64) : ES_RING(MODE_FWD, 128, 64);
     else big ? ES_RING(MODE_FWD, 256, 128) : ES_RING(MODE_FWD, 128, 128);
   } else {
-    if (a.Ng <= 64) big ? ES_RING(MODE_DGRAD, 256, 64) : ES_RING(MODE_DGRAD, 128, 64);
+    if (a.Ng <= 64 || shortk) big ? ES_RING(MODE_DGRAD, 256, 64) : ES_RING(MODE_DGRAD, 128, 64);
     else big ? ES_RING(MODE_DGRAD, 256, 128) : ES_RING(MODE_DGRAD, 128, 128);
   }
 #undef ES_RING
