@@ -810,6 +810,7 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
   // (tools/gpu_ab.sh, one box): 64 > 16 > 8 for both FWD and DGRAD, although an isolated FWD
   // prefers 8 (less MALL traffic).  ES_RING_NG overrides it (measurement).
   a.ng = g_ring_ng > 0 ? g_ring_ng : 64;
+  while (a.ng > 8 && a.ng / 2 >= d.N) a.ng /= 2;   // small batches (per-expert shards): no empty rows
   const int NGI = (d.N + a.ng - 1) / a.ng;
   const int nt128 = (a.Ng + 127) / 128;
   // short-K FWD (<= 8 K-steps, e.g. conv_layers.9: 2x2 taps x 128 channels): 128 x 64 tiles (72 KiB

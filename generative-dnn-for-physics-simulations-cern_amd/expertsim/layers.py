@@ -279,7 +279,8 @@ class ConvOp:
         bias = self.bias if (with_bias and self.bias is not None) else None
         with _probed(self.label and self.label + ".fwd"):
             if bn_stats:
-                tiles = ((d.N + 7) // 8) * (d.P * d.Q // 16 + 8)   # >= the ring's row tiles
+                # >= the ring's row tiles for every image-group size it may pick (8..64)
+                tiles = ((d.N + 7) // 8) * (d.P * d.Q // 16 + 8) + ((d.N + 63) // 64) * (d.P * d.Q // 2 + 8)
                 floats = tiles * 3 * d.K
                 part = torch.empty(floats, dtype=torch.float32, device=x.t.device)
                 chunks = C.c_int(0)
