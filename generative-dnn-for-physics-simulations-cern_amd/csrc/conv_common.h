@@ -59,6 +59,8 @@ struct ConvArgs {
   int ng;              // ring FWD/DGRAD: images per group of the row order (8, 16, 32 or 64)
   int vec_out;         // ring FWD/DGRAD: output rows channel-contiguous, 16-byte aligned, beta == 0
   float* stats_part;   // ring FWD: per-row-tile BatchNorm partials [tile][3][Ng] (count, mean, M2)
+  int sp_tpc;          // ring SP FWD: 0 = class-major tile order; else class-interleaved with this
+                       // many tiles per class (the 4 classes of the same source pixels adjacent)
 };
 
 

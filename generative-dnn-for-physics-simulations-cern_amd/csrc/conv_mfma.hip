@@ -30,6 +30,7 @@
 //              c ^ ((r >> 1) & 7): the 16-row ds_read_b128 fragment reads are conflict-free.
 //   WGRAD      [64 images][rows] per operand (rows contiguous in global memory: channels), read
 //              with ds_read_b64_tr_b16; chunk c of k-row k stored at c ^ (2(k&3) | 8((k>>3)&1)).
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -190,12 +191,29 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   // footprint inside one XCD's L2).
   const int NG = a.ng, PPG = NG >> 3;                    // pieces per pixel
   const int NB = BM / NG;
-  int cls = 0, gh, gw, TT, seg0 = 0;
+  int cls = 0, gh, gw, TT, jt;
   if constexpr (MODE == MODE_FWD && SP) {
-    TT = sp.tile0[4];
-    const int r = tl % TT;
-    cls = (r >= sp.tile0[1]) + (r >= sp.tile0[2]) + (r >= sp.tile0[3]);
-    seg0 = sp.tile0[cls];
+    if (a.sp_tpc > 0) {
+      // class-interleaved: tile r = 4 jt + class, so the 4 class tiles of the same source
+      // pixels run back to back (one XCD, shared L2); classes with fewer tiles skip the tail
+      TT = 4 * a.sp_tpc;
+      const int r = tl % TT;
+      cls = r & 3;
+      jt = r >> 2;
+      if (jt >= sp.tile0[cls + 1] - sp.tile0[cls]) {
+        if (a.stats_part) {   // empty partial (count 0) for this tile
+          float* pp = a.stats_part + (int64_t)tl * 3 * a.Ng;
+          for (int c = threadIdx.x; c < BN; c += RT)
+            if (n0 + c < a.Ng) pp[n0 + c] = 0.f;
+        }
+        return;
+      }
+    } else {
+      TT = sp.tile0[4];
+      const int r = tl % TT;
+      cls = (r >= sp.tile0[1]) + (r >= sp.tile0[2]) + (r >= sp.tile0[3]);
+      jt = r - sp.tile0[cls];
+    }
     gh = sp.ph[cls];
     gw = sp.pw[cls];
   } else {
@@ -207,10 +225,11 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
       gw = a.fold ? d.W : d.Wu;
     }
     TT = (gh * gw + NB - 1) / NB;
+    jt = tl % TT;
   }
   const int PQ = gh * gw;
   const int gi = tl / TT;                                // image group: images NG gi ..
-  const int pix0 = (tl - gi * TT - seg0) * NB;           // first pixel of the tile
+  const int pix0 = jt * NB;                              // first pixel of the tile
 
   const int lane = threadIdx.x & 63, wid = uni(threadIdx.x >> 6);
   const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
@@ -710,6 +729,11 @@ bool dense_small(const int64_t s[4], int n, int c, int h, int w) {
 bool g_ring_shortk = [] { const char* e = getenv("ES_RING_SHORTK"); return !(e && e[0] == '0'); }();
 int g_ring_ng = [] { const char* e = getenv("ES_RING_NG"); return e ? atoi(e) : 0; }();
 bool g_subpixel_off = [] { const char* e = getenv("ES_NO_SUBPIXEL"); return e && e[0] == '1'; }();
+// Sub-pixel FWD knobs: class-interleaved tile order (default; ES_SP_ILV=0 class-major: measured
+// 14.45 -> 14.33 ms per step); ES_SP_SHORTK=n: 128 x 64 tiles when a class has <= n K-steps (n = 16
+// measured slower: 14.59 ms)
+int g_sp_ilv = [] { const char* e = getenv("ES_SP_ILV"); return e ? atoi(e) : 1; }();
+int g_sp_shortk = [] { const char* e = getenv("ES_SP_SHORTK"); return e ? atoi(e) : 0; }();
 
 }  // namespace
 
@@ -816,13 +840,22 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
   // short-K FWD (<= 8 K-steps, e.g. conv_layers.9: 2x2 taps x 128 channels): 128 x 64 tiles (72 KiB
   // of LDS, two workgroups per CU) so one tile's fill and epilogue overlap another's MFMAs
   // (measured 201 -> 177 us; the same rule on the DGRAD of that conv was slower)
-  const bool shortk = g_ring_shortk && mode == MODE_FWD && !sp_weights && a.Kd / 64 <= 8;
+  bool shortk = g_ring_shortk && mode == MODE_FWD && !sp_weights && a.Kd / 64 <= 8;
+  if (sp_weights && mode == MODE_FWD && g_sp_shortk > 0) {
+    const int cls_steps = ((d.R + 1) / 2) * ((d.S + 1) / 2) * d.C / 64;   // K-steps of the largest class
+    shortk = cls_steps <= g_sp_shortk;
+  }
   const bool big = !shortk && (int64_t)NGI * a.ng * PQ / 256 * nt128 >= 768;   // >= 3 rounds of 256-row tiles
   const int BM = big ? 256 : 128, NB = BM / a.ng;
   int row_tiles = NGI * ((PQ + NB - 1) / NB);
   if (sp_weights) {
     es_make_subpixel(d, NB, a.sp);   // FWD: tile0 = per-class tile prefix of one image group
     if (mode == MODE_FWD) row_tiles = NGI * a.sp.tile0[4];
+  }
+  a.sp_tpc = 0;
+  if (sp_weights && mode == MODE_FWD && g_sp_ilv) {
+    for (int c = 0; c < 4; ++c) a.sp_tpc = std::max(a.sp_tpc, a.sp.tile0[c + 1] - a.sp.tile0[c]);
+    row_tiles = NGI * 4 * a.sp_tpc;
   }
   // staged 16-byte row stores: channel-contiguous rows, 16-byte aligned, no beta
   const int vel = a.out_bf16 ? 8 : 4;

@@ -80,7 +80,12 @@ _SIGS = {
     "es_channel_sum": (C.c_int, [P, C.c_int, P, P, C.c_float, P, P]),
     "es_maxpool_fwd": (C.c_int, [P, C.c_int, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P]),
     "es_maxpool_bwd": (C.c_int, [P, C.c_int, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, C.c_float, P]),
-    "es_upsample_bwd": (C.c_int, [P, C.c_int, P, P, P, P, P, P, C.c_int, P, C.c_float, P]),
+    "es_dfront_fwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, P, P, P, P, C.c_float, C.c_float, P, P, P, P,
+                                P]),
+    "es_dfront_part_floats": (I64, [C.c_int]),
+    "es_dfront_bwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, P, P, P, P, C.c_float, C.c_float, P, P, P, P,
+                                P, P, P, P, P, P, P, P]),
+    "es_upsample_bwd":(C.c_int, [P, C.c_int, P, P, P, P, P, P, C.c_int, P, C.c_float, P]),
     "es_copy": (C.c_int, [P, C.c_int, P, P, C.c_int, P, C.c_float, C.c_float, P]),
     "es_avgpool_fwd": (C.c_int, [P, C.c_int, P, P, P, P]),
     "es_avgpool_bwd": (C.c_int, [P, P, P, C.c_int, P, C.c_float, P]),

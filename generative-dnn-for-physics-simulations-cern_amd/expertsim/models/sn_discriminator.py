@@ -14,6 +14,8 @@ Program:
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 from torch.nn.utils import spectral_norm
@@ -65,6 +67,55 @@ class SNDiscriminator(ExpertModule):
         ops["pool2"] = MaxPool(self.pool2)
         return ops
 
+    # ------------------------------------------------------------------ fused front (d_front.hip)
+    # conv_layers.0..3 as the per-image fused kernels (ES_NO_DFRONT=1: separate kernels, A/B)
+    fuse_front = os.environ.get("ES_NO_DFRONT") != "1"
+
+    def front_fused(self, x: Act) -> bool:
+        """SNconv 1->32 + GN + LReLU + pool as es_dfront_*: fp32, even 3x3-conv output grid (the 2x2
+        pool then covers every conv output), image <= 2048 pixels (staged in LDS)."""
+        N, Cc, H, W = x.dims
+        return (self.fuse_front and x.t.dtype == torch.float32 and Cc == 1 and H >= 4 and W >= 4
+                and (H - 2) % 2 == 0 and (W - 2) % 2 == 0 and H * W <= 2048 and (H - 2) * (W - 2) <= 1792)
+
+    def _front_params(self, sigma):
+        c0, gn = get_module(self, "conv_layers.0"), get_module(self, "conv_layers.1")
+        return (hip.ptr(c0.weight_orig), hip.ptr(sigma), hip.ptr(c0.bias), hip.ptr(gn.weight), hip.ptr(gn.bias),
+                float(gn.eps), SLOPE)
+
+    def front_fwd(self, x: Act, sigma):
+        """-> pooled Act [B,32,Hp,Wp] fp32 NHWC, pool argmax bytes, GN (mean, invstd) [B*8]."""
+        B, _, H, W = x.dims
+        dev = x.t.device
+        p1 = Act.nhwc(B, 32, (H - 2) // 2, (W - 2) // 2, torch.float32, dev)
+        i1 = torch.empty(p1.numel, dtype=torch.uint8, device=dev)
+        mean = torch.empty(B * 8, dtype=torch.float32, device=dev)
+        invstd = torch.empty_like(mean)
+        hip.call("es_dfront_fwd", x.ptr, hip.strides4(x.strides), B, H, W, *self._front_params(sigma),
+                 hip.ptr(mean), hip.ptr(invstd), p1.ptr, hip.ptr(i1), hip.stream_ptr())
+        return p1, i1, (mean, invstd)
+
+    def front_bwd(self, ctx, dp1: Act, weight_grads, input_grad):
+        """Backward of the fused front from d(pooled); returns the image gradient (fp32) or None."""
+        x = ctx["x"]
+        B, _, H, W = x.dims
+        dev = x.t.device
+        assert dp1.strides == ctx["p1"].strides, (dp1.strides, ctx["p1"].strides)
+        c0, gn = get_module(self, "conv_layers.0"), get_module(self, "conv_layers.1")
+        sig = ctx["sig"]["conv_layers.0"]
+        mean, invstd = ctx["s1"]
+        dx = Act.nhwc(B, 1, H, W, torch.float32, dev) if input_grad else None
+        g_sn = torch.empty_like(c0.weight_orig) if weight_grads else None
+        part = torch.empty(hip.lib().es_dfront_part_floats(B), dtype=torch.float32, device=dev)
+        grad = (lambda t: hip.ptr(t.grad)) if weight_grads else (lambda t: None)
+        hip.call("es_dfront_bwd", x.ptr, hip.strides4(x.strides), B, H, W, *self._front_params(sig[0]),
+                 hip.ptr(mean), hip.ptr(invstd), hip.ptr(ctx["i1"]), dp1.ptr,
+                 dx.ptr if dx is not None else None, hip.strides4(dx.strides) if dx is not None else None,
+                 hip.ptr(part), hip.ptr(g_sn), grad(c0.bias), grad(gn.weight), grad(gn.bias), hip.stream_ptr())
+        if weight_grads:
+            self.ops()["sn:conv_layers.0"].bwd(g_sn, sig, c0.weight_orig.grad, beta=1.0)
+        return dx
+
     # --------------------------------------------------------------------------- forward
     def fwd(self, img: Act, cond: torch.Tensor, train=True):
         """img Act [B,1,H,W] (any dtype), cond [B,9] fp32 -> (out [B,1] fp32, latent [B,64] fp32, ctx)."""
@@ -79,9 +130,14 @@ class SNDiscriminator(ExpertModule):
             copy_act(img, x)
         sig = {n: o["sn:" + n].sigma(update=train) for n in LAYERS}
         inv = lambda n: sig[n][0]
-        h1 = o["conv_layers.0"].fwd(x, inv_scale=inv("conv_layers.0"))
-        y1, s1 = o["gn1"].fwd(h1, lr)
-        p1, i1 = o["pool1"].fwd(y1)
+        front = self.front_fused(x)
+        if front:
+            p1, i1, s1 = self.front_fwd(x, inv("conv_layers.0"))
+            h1 = y1 = None
+        else:
+            h1 = o["conv_layers.0"].fwd(x, inv_scale=inv("conv_layers.0"))
+            y1, s1 = o["gn1"].fwd(h1, lr)
+            p1, i1 = o["pool1"].fwd(y1)
         h2 = o["conv_layers.4"].fwd(p1, inv_scale=inv("conv_layers.4"))
         y2, s2 = o["gn2"].fwd(h2, lr)
         F = self.flat_dim + self.cond_dim
@@ -100,7 +156,7 @@ class SNDiscriminator(ExpertModule):
             lat_c = lat.like_nhwc(cdt)
             copy_act(lat, lat_c)
         out = o["fc3"].fwd(lat_c, inv_scale=inv("fc3"), out_dtype=torch.float32)
-        ctx = dict(x=x, sig=sig, h1=h1, y1=y1, s1=s1, p1=p1, i1=i1, h2=h2, y2=y2, s2=s2, i2=i2, X=X,
+        ctx = dict(x=x, sig=sig, front=front, h1=h1, y1=y1, s1=s1, p1=p1, i1=i1, h2=h2, y2=y2, s2=s2, i2=i2, X=X,
                    feat_dims=(B, 16, fh, fw), h3=h3, y3=y3, s3=s3, h4=h4, s4=s4, lat=lat_c)
         return out, lat, ctx
 
@@ -159,7 +215,9 @@ class SNDiscriminator(ExpertModule):
                            dsum=bias_g("conv_layers.4"))
         wgrad("conv_layers.4", dh2, ctx["p1"])
         dp1 = o["conv_layers.4"].dgrad(dh2, ctx["p1"], inv_scale=sig["conv_layers.4"][0])
-        dy1 = o["pool1"].bwd(dp1, ctx["i1"], ctx["y1"].dims, cdt)
+        if ctx["front"]:
+            return self.front_bwd(ctx, dp1, weight_grads, input_grad)
+        dy1 =o["pool1"].bwd(dp1, ctx["i1"], ctx["y1"].dims, cdt)
         dh1 = o["gn1"].bwd(ctx["h1"], ctx["s1"], lr, dy1,
                            dgamma=m("conv_layers.1").weight.grad if weight_grads else None,
                            dbeta=m("conv_layers.1").bias.grad if weight_grads else None,

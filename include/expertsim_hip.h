@@ -214,6 +214,24 @@ int es_maxpool_fwd(const es_view_t* x, es_dtype_t dt, const void* xp, int kh, in
 int es_maxpool_bwd(const es_view_t* dy, es_dtype_t dt, const void* dyp, const uint8_t* idx, int kh,
                    int kw, int sh, int sw, const es_view_t* dx, void* dxp, float beta,
                    es_stream_t stream);
+/* Fused discriminator front (neutron/discriminator.py:11-15, proton/discriminator.py:121-125):
+ * SNconv3x3 1->32 (+bias, weight w * 1/sigma[0]) -> GroupNorm(8, 32) -> LeakyReLU(slope) ->
+ * MaxPool 2x2, one workgroup per image, the 32-channel conv map recomputed from the image in LDS
+ * instead of stored.  img: fp32 [N][1][H][W] (element strides is[4]); H-2 and W-2 even,
+ * H*W <= 2048.  Forward writes pooled [N][(H-2)/2][(W-2)/2][32] fp32 (dense NHWC), idx (same
+ * shape, uint8 window argmax as es_maxpool_fwd) and the GN mean / invstd [N][8]. */
+int es_dfront_fwd(const float* img, const int64_t is[4], int N, int H, int W, const float* w,
+                  const float* sigma, const float* bias, const float* gamma, const float* beta, float eps,
+                  float slope, float* mean, float* invstd, float* pooled, uint8_t* idx, es_stream_t stream);
+/* Backward from dpooled (dense NHWC like pooled).  dx (optional, fp32 [N][1][H][W], strides dxs):
+ * image gradient, written.  part: workspace of es_dfront_part_floats(N) floats.  dw (gradient of
+ * W/sigma, [32][1][3][3]) is written; dbias / dgamma / dbeta are accumulated; each may be NULL. */
+int64_t es_dfront_part_floats(int N);
+int es_dfront_bwd(const float* img, const int64_t is[4], int N, int H, int W, const float* w,
+                  const float* sigma, const float* bias, const float* gamma, const float* beta, float eps,
+                  float slope, const float* mean, const float* invstd, const uint8_t* idx,
+                  const float* dpooled, float* dx, const int64_t dxs[4], float* part, float* dw,
+                  float* dbias, float* dgamma, float* dbeta, es_stream_t stream);
 /* dx[n,c,h,w] = beta*dx + sum over upsampled positions mapping to (h,w).  hstart/hcount (device
  * [H]) and wstart/wcount (device [W]) describe the contiguous preimage of each source row/col. */
 int es_upsample_bwd(const es_view_t* dxu, es_dtype_t dt, const void* dxup, const int32_t* hstart,

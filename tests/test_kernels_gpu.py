@@ -469,3 +469,59 @@ def test_conv_fused_bn_stats(case):
     assert rel(m1.cpu(), m0.cpu()) < 1e-5
     assert rel(i1.cpu(), i0.cpu()) < 1e-5
     assert rel(n1.rv.cpu(), n0.rv.cpu()) < 1e-5 and rel(n1.rm.cpu(), n0.rm.cpu()) < 1e-5
+
+
+@pytest.mark.parametrize("N,H,W", [(5, 44, 44), (3, 56, 30), (4, 10, 8)])
+def test_dfront_fused(N, H, W):
+    """es_dfront_fwd / es_dfront_bwd (fused SNconv 1->32 + GroupNorm(8) + LeakyReLU + maxpool 2x2,
+    d_front.hip) against torch fp32 autograd of the same block: pooled output, GN statistics, pool
+    argmax, image gradient and the gradients of W/sigma, bias, gamma, beta."""
+    hip = _hip()
+    from expertsim.layers import Act
+    torch.manual_seed(17)
+    x = torch.randn(N, 1, H, W)
+    w = torch.randn(32, 1, 3, 3) / 3
+    b, gm, bt = 0.1 * torch.randn(32), 1 + 0.1 * torch.randn(32), 0.1 * torch.randn(32)
+    sigma = torch.tensor([1.7])
+    xr = x.clone().requires_grad_(True)
+    weff = (w * (1.0 / sigma)).requires_grad_(True)
+    br, gmr, btr = (t.clone().requires_grad_(True) for t in (b, gm, bt))
+    h = F.conv2d(xr, weff, br)
+    y = F.leaky_relu(F.group_norm(h, 8, gmr, btr, 1e-5), 0.1)
+    p, pidx = F.max_pool2d(y, 2, return_indices=True)
+    gp = torch.randn_like(p)
+    p.backward(gp)
+
+    xd = x.to(DEV)
+    dev_params = [w.to(DEV), sigma.to(DEV), b.to(DEV), gm.to(DEV), bt.to(DEV)]
+    args = (hip.ptr(xd), hip.strides4(xd.stride()), N, H, W) + tuple(hip.ptr(t) for t in dev_params) + (1e-5, 0.1)
+    Hp, Wp = (H - 2) // 2, (W - 2) // 2
+    pooled = Act.nhwc(N, 32, Hp, Wp, torch.float32, DEV)
+    idx = torch.empty(pooled.numel, dtype=torch.uint8, device=DEV)
+    mean = torch.empty(N * 8, device=DEV)
+    invstd = torch.empty(N * 8, device=DEV)
+    hip.call("es_dfront_fwd", *args, hip.ptr(mean), hip.ptr(invstd), pooled.ptr, hip.ptr(idx), hip.stream_ptr())
+    assert rel(from_act(pooled), p.detach()) < 1e-5
+    hg = h.detach().view(N, 8, -1)
+    assert rel(mean.cpu(), hg.mean(-1).reshape(-1)) < 1e-5
+    assert rel(invstd.cpu(), torch.rsqrt(hg.var(-1, unbiased=False) + 1e-5).reshape(-1)) < 1e-4
+    # argmax byte (window row-major) vs torch's flat index
+    pi = torch.arange(Hp).view(1, 1, Hp, 1) * 2
+    pj = torch.arange(Wp).view(1, 1, 1, Wp) * 2
+    ref_bytes = (pidx // (W - 2) - pi) * 2 + (pidx % (W - 2) - pj)
+    got = idx.cpu().view(N, Hp, Wp, 32).permute(0, 3, 1, 2).long()
+    assert torch.equal(got, ref_bytes)
+
+    dpooled = to_act(gp)
+    dx = torch.empty(N, 1, H, W, device=DEV)
+    part = torch.empty(hip.lib().es_dfront_part_floats(N), device=DEV)
+    dw = torch.empty(32 * 9, device=DEV)
+    db, dg, dbt = (torch.full((32,), 0.5, device=DEV) for _ in range(3))   # accumulated into
+    hip.call("es_dfront_bwd", *args, hip.ptr(mean), hip.ptr(invstd), hip.ptr(idx), dpooled.ptr, hip.ptr(dx),
+             hip.strides4(dx.stride()), hip.ptr(part), hip.ptr(dw), hip.ptr(db), hip.ptr(dg), hip.ptr(dbt),
+             hip.stream_ptr())
+    assert rel(dx.cpu(), xr.grad) < 1e-4
+    assert rel(dw.cpu().view(32, 1, 3, 3), weff.grad) < 1e-4
+    assert rel(db.cpu() - 0.5, br.grad) < 1e-4
+    assert rel(dg.cpu() - 0.5, gmr.grad) < 1e-4
+    assert rel(dbt.cpu() - 0.5, btr.grad) < 1e-4
