@@ -175,7 +175,10 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   constexpr int APW = BM / 64, BPW = BN / 64;   // 1 KiB pieces per wave per slot
   constexpr int PW = APW + BPW;
   constexpr int ABYTES = BM * 128, SLOT = (BM + BN) * 128;
-  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT];
+  // ONE __shared__ object (a second one beside the DMA ring makes hipcc wait vmcnt(0) before
+  // every ds_read of the loop): the ring slots, then the fused-stats scratch [3][4][BN] floats,
+  // which no DMA targets
+  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT + 12 * BN * 4];
   const es_conv_desc_t& d = a.d;
   const SubPixel& sp = a.sp;
 
@@ -427,7 +430,9 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
     // mean / M2 over the wave's valid rows (lanes own 16 rows, Chan-merged across the 4 row
     // groups by shuffles), then across the 4 row waves in LDS -> one [3][Ng] partial per row tile
     float* part = a.stats_part;
-    __shared__ float st_n[4][BN], st_m[4][BN], st_q[4][BN];
+    float (*st_n)[BN] = (float (*)[BN])(smem + NSLOT * SLOT);
+    float (*st_m)[BN] = st_n + 4;
+    float (*st_q)[BN] = st_n + 8;
     if (part) {
       const int wmi = wid >> 1;
       bool okr[RM][4];
