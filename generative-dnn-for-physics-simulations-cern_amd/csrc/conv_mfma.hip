@@ -83,6 +83,20 @@ struct lambda_arg<R (C::*)(A0, As...) const> {
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Per-class sub-pixel values in registers: 4 x int16 packed in one 64-bit scalar, read with a
+// shift.  Indexing the kernel-argument arrays with a runtime class makes hipcc reload them
+// (s_load + lgkmcnt(0), which also drains the ds_reads) after every ring barrier, and a select
+// chain over 4 copies becomes branches inside the loop.
+struct ClsReg {
+  uint64_t v;
+  __device__ __forceinline__ void init(const int* src) {
+    uint32_t lo = ((uint32_t)(uint16_t)src[0]) | ((uint32_t)(uint16_t)src[1] << 16);
+    uint32_t hi = ((uint32_t)(uint16_t)src[2]) | ((uint32_t)(uint16_t)src[3] << 16);
+    v = ((uint64_t)(uint32_t)uni((int)hi) << 32) | (uint32_t)uni((int)lo);
+  }
+  __device__ __forceinline__ int operator()(int c) const { return (int)(short)(uint16_t)(v >> (16 * c)); }
+};
+
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
 
 typedef short short4_t __attribute__((ext_vector_type(4)));
@@ -119,15 +133,56 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* img, int k0, int r0) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// The same fragment read as inline asm.  hipcc cannot tell which LDS-DMA a
+// __builtin_amdgcn_ds_read_tr16_b64 may alias, so it drains every DMA in flight (vmcnt(0)) before
+// the first one of each K-step, which serialises the ring; as asm the reads are invisible to its
+// wait insertion and ring_loop orders them itself (lgkmcnt + an operand fence before the MFMAs).
+typedef int int2v __attribute__((ext_vector_type(2)));
+typedef int int4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ int2v ds_tr16(uint32_t addr) {
+  int2v r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+template <int BROWS>
+__device__ __forceinline__ bf16x8 tr_frag_asm(uint32_t img, int k0, int r0) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int ka = k0 + 8 * g + q;
+  const int2v lo = ds_tr16(img + tr_off<BROWS>(ka, r0 + 4 * p));
+  const int2v hi = ds_tr16(img + tr_off<BROWS>(ka + 4, r0 + 4 * p));
+  const int4v v = {lo[0], lo[1], hi[0], hi[1]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+// make x depend on the preceding (volatile) wait: MFMAs reading x cannot move above it
+__device__ __forceinline__ void fence_frag(bf16x8& x) {
+  int4v v = __builtin_bit_cast(int4v, x);
+  asm volatile("" : "+v"(v));
+  x = __builtin_bit_cast(bf16x8, v);
+}
+template <int N>
+__device__ __forceinline__ void wait_lgkmcnt() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // The ring main loop shared by the kernels.  Slot of K-step t = t % 3; two register fragment
 // sets: the kk = 1 half of step t is read from LDS while the MFMAs of the kk = 0 half run, and the
 // kk = 0 half of step t+1 while the kk = 1 MFMAs of step t run, so LDS latency hides behind MFMA
 // work.  Per step, one barrier (after this wave's reads of slot t have completed and its DMA
 // pieces of slot t+1 have landed): behind it every wave has finished slot t, which then takes the
 // DMA of step t+3, and slot t+1 is complete.
-template <int PW, typename Issue, typename Load, typename Mma>
-__device__ __forceinline__ void ring_loop(int nk, char* smem, int slot_bytes, Issue& issue, Load& load, Mma& mma) {
+//
+// NLDS > 0: load() issues its LDS reads as inline asm (NLDS per call), invisible to hipcc's wait
+// insertion; then before each mma the loop waits lgkmcnt(reads issued since) and fences the
+// fragment (fence(f)) so the MFMAs cannot be scheduled above the wait.
+template <int PW, int NLDS, typename Issue, typename Load, typename Mma, typename Fence>
+__device__ __forceinline__ void ring_loop(int nk, char* smem, int slot_bytes, Issue& issue, Load& load, Mma& mma,
+                                          Fence& fence) {
   using Frag = typename std::remove_reference<typename lambda_arg<Load>::type>::type;
+  constexpr int LATER = NLDS > 15 ? 15 : NLDS;   // lgkmcnt is a 4-bit count
   // issue() is called for steps 0, 1, 2, ... unconditionally; steps >= nk are all-OOB (zero-fill,
   // no memory traffic), so every iteration keeps exactly two steps in flight and the loop body is
   // one basic block (the compiler's LDS waits stay counted instead of draining at branch joins)
@@ -141,10 +196,15 @@ __device__ __forceinline__ void ring_loop(int nk, char* smem, int slot_bytes, Is
   int cur = 0;
   for (int t = 0; t < nk - 1; ++t) {
     load(f1, smem + cur * slot_bytes, 1);
+    if constexpr (NLDS > 0) {                            // f0's reads done, f1's may be in flight
+      wait_lgkmcnt<LATER>();
+      fence(f0);
+    }
     mma(f0);
     const int nxt = cur == 2 ? 0 : cur + 1;
     wait_vmcnt<PW>();                                    // step t+1 landed (this wave's pieces)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of slot t are done
+    if constexpr (NLDS > 0) fence(f1);
     ring_barrier();
     load(f0, smem + nxt * slot_bytes, 0);
     issue(smem + cur * slot_bytes);                      // step t+3
@@ -152,7 +212,15 @@ __device__ __forceinline__ void ring_loop(int nk, char* smem, int slot_bytes, Is
     cur = nxt;
   }
   load(f1, smem + cur * slot_bytes, 1);
+  if constexpr (NLDS > 0) {
+    wait_lgkmcnt<LATER>();
+    fence(f0);
+  }
   mma(f0);
+  if constexpr (NLDS > 0) {
+    wait_lgkmcnt<0>();
+    fence(f1);
+  }
   mma(f1);
   wait_vmcnt<0>();   // drain the zero-fill steps before the workgroup may exit
 }
@@ -307,7 +375,12 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   if constexpr (SP && MODE == MODE_FWD) nk = ldb / 64;
   else if constexpr (SP) nk = ldb / 64;
   else nk = a.Kd / 64;
-  int kh = SP ? sp.dh[cls] : d.R, kw = SP ? sp.dw[cls] : d.S;   // taps of the cursor's class
+  ClsReg Roh, Row, Rph, Rpw, Rp0, Rq0, Rtap0, Rdh, Rdw;
+  if constexpr (SP && MODE == MODE_DGRAD) {
+    Roh.init(sp.oh); Row.init(sp.ow); Rph.init(sp.ph); Rpw.init(sp.pw); Rp0.init(sp.p0); Rq0.init(sp.q0);
+    Rtap0.init(sp.tap0); Rdh.init(sp.dh); Rdw.init(sp.dw);
+  }
+  int kh = SP ? uni(sp.dh[cls]) : d.R, kw = SP ? uni(sp.dw[cls]) : d.S;   // taps of the cursor's class
   auto issue = [&](char* slot) {
     const bool live = cstep < nk;
 #pragma unroll
@@ -325,10 +398,10 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
         u = ok ? (uint32_t)(sh * as2b + sw * as3b + cch * 2) : OOB;
       } else if constexpr (SP) {
         // output pixel (p0 + 2u, q0 + 2v) of class ccls feeds source pixel u + oh + d
-        const int uu = pc0[j] - cr - sp.oh[ccls], vv = pc1[j] - cs - sp.ow[ccls];
-        const bool ok = live && pval[j] && (unsigned)uu < (unsigned)sp.ph[ccls] &&
-                        (unsigned)vv < (unsigned)sp.pw[ccls];
-        u = ok ? (uint32_t)((sp.p0[ccls] + 2 * uu) * as2b + (sp.q0[ccls] + 2 * vv) * as3b + cch * 2) : OOB;
+        const int uu = pc0[j] - cr - Roh(ccls), vv = pc1[j] - cs - Row(ccls);
+        const bool ok = live && pval[j] && (unsigned)uu < (unsigned)Rph(ccls) &&
+                        (unsigned)vv < (unsigned)Rpw(ccls);
+        u = ok ? (uint32_t)((Rp0(ccls) + 2 * uu) * as2b + (Rq0(ccls) + 2 * vv) * as3b + cch * 2) : OOB;
       } else {
         const int ph = pc0[j] + cua - cr, pw = pc1[j] + cub - cs;
         const int sh = d.stride == 2 ? 1 : 0;
@@ -340,7 +413,7 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
     }
     int kb;
     if constexpr (MODE == MODE_FWD) kb = (cr * kw + cs) * d.C + cch;
-    else if constexpr (SP) kb = (sp.tap0[ccls] + cr * kw + cs) * d.K + cch;
+    else if constexpr (SP) kb = (Rtap0(ccls) + cr * kw + cs) * d.K + cch;
     else kb = ckb;
     const uint32_t ub = live ? (uint32_t)(kb * 2) : OOB;
 #pragma unroll
@@ -365,8 +438,8 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
     if constexpr (SP && MODE == MODE_DGRAD) {
       ccls += w3;
       const int cn = ccls < 4 ? ccls : 3;
-      kh = sp.dh[cn];
-      kw = sp.dw[cn];
+      kh = Rdh(cn);
+      kw = Rdw(cn);
     }
   };
 
@@ -394,7 +467,8 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
       for (int j = 0; j < RN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
   };
-  ring_loop<PW>(nk, smem, SLOT, issue, load, mma);
+  auto nofence = [](Frag&) {};
+  ring_loop<PW, 0>(nk, smem, SLOT, issue, load, mma, nofence);
 
   // epilogue.  Wave row r (0..WM-1) = tile row t = wm0 + r: pixel pix0 + t / NG, image
   // NG gi + t % NG.
@@ -625,12 +699,15 @@ __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
     cp = pix / gq;
     cq = pix - cp * gq;
   }
+  // the tile's class values as register copies (no kernel-argument reloads inside the loop)
+  const int cp0 = SP ? uni(sp.p0[cls]) : 0, cq0 = SP ? uni(sp.q0[cls]) : 0;
+  const int coh = SP ? uni(sp.oh[cls]) : 0, cow = SP ? uni(sp.ow[cls]) : 0;
   auto issue = [&](char* slot) {
     const bool live = cstep < tend;
     uint32_t ua, ub;
     if constexpr (SP) {   // dy at output pixel (p0 + 2p, q0 + 2q), x at source (p + oh + d, q + ow + e)
-      ua = live ? (uint32_t)(cg * 64 * as0b + (sp.p0[cls] + 2 * cp) * as2b + (sp.q0[cls] + 2 * cq) * as3b) : OOB;
-      const int hs = cp + sp.oh[cls] + tr, ws = cq + sp.ow[cls] + ts;
+      ua = live ? (uint32_t)(cg * 64 * as0b + (cp0 + 2 * cp) * as2b + (cq0 + 2 * cq) * as3b) : OOB;
+      const int hs = cp + coh + tr, ws = cq + cow + ts;
       const bool ok = live && (unsigned)hs < (unsigned)d.H && (unsigned)ws < (unsigned)d.W;
       ub = ok ? (uint32_t)(cg * 64 * bs0b + hs * bs2b + ws * bs3b) : OOB;
     } else {
@@ -663,10 +740,17 @@ __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
     bf16x8 a[RM], b[RN];
   };
   auto load = [&](Frag& f, const char* slot, int kk) {
+    const uint32_t base = lds_u32(slot);
 #pragma unroll
-    for (int i = 0; i < RM; ++i) f.a[i] = tr_frag<BM>(slot, kk * 32, wm0 + i * 16);
+    for (int i = 0; i < RM; ++i) f.a[i] = tr_frag_asm<BM>(base, kk * 32, wm0 + i * 16);
 #pragma unroll
-    for (int j = 0; j < RN; ++j) f.b[j] = tr_frag<BN>(slot + AIMG, kk * 32, wn0 + j * 16);
+    for (int j = 0; j < RN; ++j) f.b[j] = tr_frag_asm<BN>(base + AIMG, kk * 32, wn0 + j * 16);
+  };
+  auto fence = [&](Frag& f) {
+#pragma unroll
+    for (int i = 0; i < RM; ++i) fence_frag(f.a[i]);
+#pragma unroll
+    for (int j = 0; j < RN; ++j) fence_frag(f.b[j]);
   };
   auto mma = [&](const Frag& f) {
 #pragma unroll
@@ -675,7 +759,7 @@ __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
       for (int j = 0; j < RN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
   };
-  ring_loop<PW>(tend - tbeg, smem, SLOT, issue, load, mma);
+  ring_loop<PW, 2 * (RM + RN)>(tend - tbeg, smem, SLOT, issue, load, mma, fence);
 
   const int col16 = lane & 15, rq = (lane >> 4) * 4;
   float* out = (float*)a.out;
