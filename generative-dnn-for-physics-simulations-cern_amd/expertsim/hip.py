@@ -12,7 +12,9 @@ import os
 import numpy as np
 import torch
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libexpertsim_hip.so")
+# ES_LIB: load another build of the library (same-box A/B of two builds, tools/gpu_ab.sh)
+_LIB_PATH = os.environ.get("ES_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
+                                                     "libexpertsim_hip.so")
 _lib = None
 
 ES_F32, ES_BF16 = 0, 1
@@ -85,7 +87,7 @@ _SIGS = {
     "es_dfront_part_floats": (I64, [C.c_int]),
     "es_dfront_bwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, P, P, P, P, C.c_float, C.c_float, P, P, P, P,
                                 P, P, P, P, P, P, P, P]),
-    "es_upsample_bwd":(C.c_int, [P, C.c_int, P, P, P, P, P, P, C.c_int, P, C.c_float, P]),
+    "es_upsample_bwd": (C.c_int, [P, C.c_int, P, P, P, P, P, P, C.c_int, P, C.c_float, P]),
     "es_copy": (C.c_int, [P, C.c_int, P, P, C.c_int, P, C.c_float, C.c_float, P]),
     "es_avgpool_fwd": (C.c_int, [P, C.c_int, P, P, P, P]),
     "es_avgpool_bwd": (C.c_int, [P, P, P, C.c_int, P, C.c_float, P]),
