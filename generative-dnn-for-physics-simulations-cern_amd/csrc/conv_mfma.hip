@@ -39,6 +39,9 @@
 namespace {
 
 constexpr int RT = 512;   // threads per workgroup (8 waves)
+#ifndef ES_RING_LEAN
+#define ES_RING_LEAN 0   // 256 x 256 tiles: 1 = single fragment set per step (ring_loop_lean)
+#endif
 constexpr int NSLOT = 3;  // ring depth
 constexpr uint32_t OOB = 0x80000000u;   // buffer offset past every num_records (< 2^31 bytes)
 
@@ -97,7 +100,18 @@ struct ClsReg {
   __device__ __forceinline__ int operator()(int c) const { return (int)(short)(uint16_t)(v >> (16 * c)); }
 };
 
-__device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+// byte offset of 16-byte chunk `chunk` of row `row` in a [rows][BK] bf16 slot image:
+//   BK = 64 (128-byte rows): chunk ^ ((row >> 1) & 7)
+//   BK = 32 (64-byte rows):  chunk ^ f(row / 4 mod 4), f = {0, 2, 3, 1}
+// so that each of ds_read_b128's four 16-lane bank groups ({0-3, 12-15, 20-27}, {4-11, 16-19,
+// 28-31}, and the same + 32; MI355X_MICROARCH.md §LDS) hits 16 distinct 16-byte bank slots when
+// lane l reads row r0 + (l & 15), chunk l >> 4 (a plain ((row >> 2) & 3) leaves 2-way conflicts)
+template <int BK = 64>
+__device__ __forceinline__ int swz_x(int row) {
+  return BK == 64 ? ((row >> 1) & 7) : ((0x78 >> (2 * ((row >> 2) & 3))) & 3);
+}
+template <int BK = 64>
+__device__ __forceinline__ int swz(int row, int chunk) { return row * (BK * 2) + ((chunk ^ swz_x<BK>(row)) << 4); }
 
 typedef short short4_t __attribute__((ext_vector_type(4)));
 typedef short short8_t __attribute__((ext_vector_type(8)));
@@ -178,19 +192,20 @@ __device__ __forceinline__ void wait_lgkmcnt() {
 // NLDS > 0: load() issues its LDS reads as inline asm (NLDS per call), invisible to hipcc's wait
 // insertion; then before each mma the loop waits lgkmcnt(reads issued since) and fences the
 // fragment (fence(f)) so the MFMAs cannot be scheduled above the wait.
-template <int PW, int NLDS, typename Issue, typename Load, typename Mma, typename Fence>
+// NS slots (3 or 4): NS - 1 steps in flight behind the one being computed.
+template <int PW, int NLDS, int NS = 3, typename Issue, typename Load, typename Mma, typename Fence>
 __device__ __forceinline__ void ring_loop(int nk, char* smem, int slot_bytes, Issue& issue, Load& load, Mma& mma,
                                           Fence& fence) {
   using Frag = typename std::remove_reference<typename lambda_arg<Load>::type>::type;
   constexpr int LATER = NLDS > 15 ? 15 : NLDS;   // lgkmcnt is a 4-bit count
   // issue() is called for steps 0, 1, 2, ... unconditionally; steps >= nk are all-OOB (zero-fill,
-  // no memory traffic), so every iteration keeps exactly two steps in flight and the loop body is
-  // one basic block (the compiler's LDS waits stay counted instead of draining at branch joins)
-  issue(smem);
-  issue(smem + slot_bytes);
-  wait_vmcnt<PW>();
+  // no memory traffic), so every iteration keeps exactly NS - 1 steps in flight and the loop body
+  // is one basic block (the compiler's LDS waits stay counted instead of draining at branch joins)
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i) issue(smem + i * slot_bytes);
+  wait_vmcnt<(NS - 2) * PW>();
   ring_barrier();
-  issue(smem + 2 * slot_bytes);
+  issue(smem + (NS - 1) * slot_bytes);
   Frag f0, f1;
   load(f0, smem, 0);
   int cur = 0;
@@ -201,13 +216,13 @@ __device__ __forceinline__ void ring_loop(int nk, char* smem, int slot_bytes, Is
       fence(f0);
     }
     mma(f0);
-    const int nxt = cur == 2 ? 0 : cur + 1;
-    wait_vmcnt<PW>();                                    // step t+1 landed (this wave's pieces)
+    const int nxt = cur == NS - 1 ? 0 : cur + 1;
+    wait_vmcnt<(NS - 2) * PW>();                         // step t+1 landed (this wave's pieces)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of slot t are done
     if constexpr (NLDS > 0) fence(f1);
     ring_barrier();
     load(f0, smem + nxt * slot_bytes, 0);
-    issue(smem + cur * slot_bytes);                      // step t+3
+    issue(smem + cur * slot_bytes);                      // step t + NS
     mma(f1);
     cur = nxt;
   }
@@ -225,6 +240,32 @@ __device__ __forceinline__ void ring_loop(int nk, char* smem, int slot_bytes, Is
   wait_vmcnt<0>();   // drain the zero-fill steps before the workgroup may exit
 }
 
+// Single fragment set variant (register-lean, for the 256 x 256 tiles): per step one barrier,
+// then both fragment halves are read and multiplied in turn; the LDS latency is covered by the
+// other wave of the SIMD.  Same slot / vmcnt discipline as ring_loop.
+template <int PW, int NS, typename Issue, typename Load, typename Mma>
+__device__ __forceinline__ void ring_loop_lean(int nk, char* smem, int slot_bytes, Issue& issue, Load& load,
+                                               Mma& mma) {
+  using Frag = typename std::remove_reference<typename lambda_arg<Load>::type>::type;
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i) issue(smem + i * slot_bytes);
+  int cur = 0, prv = NS - 1;
+  for (int t = 0; t < nk; ++t) {
+    wait_vmcnt<(NS - 2) * PW>();                         // step t landed (this wave's pieces)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of step t-1 are done
+    ring_barrier();
+    issue(smem + prv * slot_bytes);                      // step t + NS - 1 into step t-1's slot
+    Frag f;
+    load(f, smem + cur * slot_bytes, 0);
+    mma(f);
+    load(f, smem + cur * slot_bytes, 1);
+    mma(f);
+    prv = cur;
+    cur = cur == NS - 1 ? 0 : cur + 1;
+  }
+  wait_vmcnt<0>();   // drain the zero-fill steps before the workgroup may exit
+}
+
 // ---------------------------------------------------------------------------------------------
 // FWD / DGRAD.  Rows m = (g*PQ + pix)*64 + nl (image n = 64 g + nl, pixel pix on the row grid),
 // columns = channels of the packed weight, K-step = one tap x 64 channels.
@@ -236,17 +277,31 @@ __device__ __forceinline__ void ring_loop(int nk, char* smem, int slot_bytes, Is
 // mode-3 packing.  3x3 taps on the upsampled grid become 4 taps on the source grid: 2.25x fewer
 // MACs and gathered bytes for the same result (up to the rounding of the combined weights).
 // ---------------------------------------------------------------------------------------------
-template <int MODE, int BM, int BN, bool SP>
+//
+// BK = 64: K-steps of 64 channels (128-byte slot rows), 3 slots, 4 x 2 waves.
+// BK = 32 (256 x 256 tiles): K-steps of 32 channels (64-byte rows), 4 slots (three steps in flight),
+// 2 x 4 waves of 128 x 64; per step 32 KiB of operands for 4.2 MFLOP (the 256 x 128 BK = 64 tile
+// moves 48 KiB for the same work), and an A row tile is gathered once for 256 output channels.
+template <int MODE, int BM, int BN, bool SP, int BK = 64>
 __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
-  constexpr int WM = BM / 4, WN = BN / 2;       // 4 x 2 waves
+  constexpr int WGM = BK == 32 ? 2 : 4, WGN = 8 / WGM;   // waves along M / N
+  constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int RM = WM / 16, RN = WN / 16;
-  constexpr int APW = BM / 64, BPW = BN / 64;   // 1 KiB pieces per wave per slot
+  constexpr int ROWB = BK * 2, PROWS = 1024 / ROWB;      // slot row bytes, rows per 1 KiB piece
+  constexpr int CPR = ROWB / 16;                         // 16-byte chunks per row
+  constexpr int APW = BM / PROWS / 8, BPW = BN / PROWS / 8;   // pieces per wave per slot
   constexpr int PW = APW + BPW;
-  constexpr int ABYTES = BM * 128, SLOT = (BM + BN) * 128;
+  constexpr int NS = BK == 32 ? 4 : NSLOT;
+  constexpr int ABYTES = BM * ROWB, SLOT = (BM + BN) * ROWB;
+  constexpr int KH = BK == 64 ? 2 : 1;                   // MFMA K-halves per step
+  constexpr int RMF = RM / (3 - KH);                     // A tiles per fragment set
+  constexpr int SROWS = WM < 64 ? WM : 64;               // epilogue staging rows per pass
+  constexpr int STAGE = 8 * SROWS * (WN * 4 + 16);
+  constexpr int RING = NS * SLOT > STAGE ? NS * SLOT : STAGE;
   // ONE __shared__ object (a second one beside the DMA ring makes hipcc wait vmcnt(0) before
-  // every ds_read of the loop): the ring slots, then the fused-stats scratch [3][4][BN] floats,
-  // which no DMA targets
-  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT + 12 * BN * 4];
+  // every ds_read of the loop): the ring slots (also the epilogue staging), then the fused-stats
+  // scratch [3][WGM][BN] floats, which no DMA targets
+  __shared__ __attribute__((aligned(16))) char smem[RING + 3 * WGM * BN * 4];
   const es_conv_desc_t& d = a.d;
   const SubPixel& sp = a.sp;
 
@@ -260,7 +315,7 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   // images at one pixel.  Consecutive tiles (one XCD) stay on the same images, so their sources
   // share the L2; the host picks NG per operand (small groups keep a forward gather's source
   // footprint inside one XCD's L2).
-  const int NG = a.ng, PPG = NG >> 3;                    // pieces per pixel
+  const int NG = a.ng, PPG = NG / PROWS;                 // pieces per pixel
   const int NB = BM / NG;
   int cls = 0, gh, gw, TT, jt;
   if constexpr (MODE == MODE_FWD && SP) {
@@ -303,8 +358,8 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   const int pix0 = jt * NB;                              // first pixel of the tile
 
   const int lane = threadIdx.x & 63, wid = uni(threadIdx.x >> 6);
-  const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
-  const int lrow = lane >> 3, pc = lane & 7;
+  const int wm0 = (wid / WGN) * WM, wn0 = (wid % WGN) * WN;
+  const int lrow = lane / CPR, pc = lane % CPR;
 
   const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * 2));
   // packed weights: row stride ldb (elements) and the class's block offset
@@ -330,14 +385,14 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
 #pragma unroll
   for (int j = 0; j < APW; ++j) {
     const int pi = wid * APW + j;                 // piece of the tile: pixel pix0 + pi / PPG
-    const int rr = pi * 8 + lrow;                 // row within the tile (swizzle)
-    const int lc = pc ^ ((rr >> 1) & 7);
+    const int rr = pi * PROWS + lrow;             // row within the tile (swizzle)
+    const int lc = pc ^ swz_x<BK>(rr);
     const int ppix = pi / PPG;
     const int pix = pix0 + ppix;
     pval[j] = pix < PQ;
     const int pp = pval[j] ? pix : 0;
     const int y = pp / gw, x = pp - y * gw;
-    const int img = gi * NG + (pi - ppix * PPG) * 8 + lrow;
+    const int img = gi * NG + (pi - ppix * PPG) * PROWS + lrow;
     alane[j] = (uint32_t)(img * (int)a.as[0] * 2 + lc * 16);   // images >= N: past num_records
     if constexpr (MODE == MODE_FWD && SP) {       // source row = u + oh + d
       pc0[j] = y + sp.oh[cls];
@@ -359,9 +414,9 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   uint32_t blane[BPW];
 #pragma unroll
   for (int j = 0; j < BPW; ++j) {
-    const int rr = (wid * BPW + j) * 8 + lrow;
+    const int rr = (wid * BPW + j) * PROWS + lrow;
     // rows past Ng read garbage columns that the epilogue drops (or zeros past num_records)
-    blane[j] = (uint32_t)((bbase + (n0 + rr) * ldb) * 2 + ((pc ^ ((rr >> 1) & 7)) * 16));
+    blane[j] = (uint32_t)((bbase + (n0 + rr) * ldb) * 2 + ((pc ^ swz_x<BK>(rr)) * 16));
   }
 
   // K-step cursor (uniform, advanced once per issued slot).
@@ -372,74 +427,87 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   const int nch = MODE == MODE_FWD ? d.C : d.K;
   const int upw = d.up_w > 0 ? d.up_w : 1;
   int nk;
-  if constexpr (SP && MODE == MODE_FWD) nk = ldb / 64;
-  else if constexpr (SP) nk = ldb / 64;
-  else nk = a.Kd / 64;
+  if constexpr (SP && MODE == MODE_FWD) nk = ldb / BK;
+  else if constexpr (SP) nk = ldb / BK;
+  else nk = a.Kd / BK;
   ClsReg Roh, Row, Rph, Rpw, Rp0, Rq0, Rtap0, Rdh, Rdw;
   if constexpr (SP && MODE == MODE_DGRAD) {
     Roh.init(sp.oh); Row.init(sp.ow); Rph.init(sp.ph); Rpw.init(sp.pw); Rp0.init(sp.p0); Rq0.init(sp.q0);
     Rtap0.init(sp.tap0); Rdh.init(sp.dh); Rdw.init(sp.dw);
   }
   int kh = SP ? uni(sp.dh[cls]) : d.R, kw = SP ? uni(sp.dw[cls]) : d.S;   // taps of the cursor's class
+  // Per-tap cache: the pieces' offsets only change when the cursor enters a new tap (every
+  // nch / BK steps); inside a tap a step adds BK channels.  Recomputing them every step cost
+  // ~100 scalar instructions per K-step, which made the loop issue-bound (the CU's scalar unit
+  // is shared by its 8 waves).
+  uint32_t ua_t[APW], ub_t = 0;
+#pragma unroll
+  for (int j = 0; j < APW; ++j) ua_t[j] = OOB;
   auto issue = [&](char* slot) {
-    const bool live = cstep < nk;
+    if (cch == 0) {   // first step of a tap (wave-uniform branch, scalar work only)
+      const bool live = cstep < nk;
 #pragma unroll
-    for (int j = 0; j < APW; ++j) {
-      uint32_t u;
-      if constexpr (MODE == MODE_FWD && SP) {
-        const int hs = pc0[j] + cr, ws = pc1[j] + cs;
-        const bool ok = live && pval[j] && (unsigned)hs < (unsigned)d.H && (unsigned)ws < (unsigned)d.W;
-        u = ok ? (uint32_t)(hs * as2b + ws * as3b + cch * 2) : OOB;
-      } else if constexpr (MODE == MODE_FWD) {
-        const int hu = pc0[j] + cr, wu = pc1[j] + cs;
-        const bool ok = live && pval[j] && (unsigned)hu < (unsigned)d.Hu && (unsigned)wu < (unsigned)d.Wu;
-        // integer nearest upsample folded into the gather (factor 1 without upsample)
-        const int sh = fdiv(hu, a.fUh), sw = fdiv(wu, a.fUw);
-        u = ok ? (uint32_t)(sh * as2b + sw * as3b + cch * 2) : OOB;
-      } else if constexpr (SP) {
-        // output pixel (p0 + 2u, q0 + 2v) of class ccls feeds source pixel u + oh + d
-        const int uu = pc0[j] - cr - Roh(ccls), vv = pc1[j] - cs - Row(ccls);
-        const bool ok = live && pval[j] && (unsigned)uu < (unsigned)Rph(ccls) &&
-                        (unsigned)vv < (unsigned)Rpw(ccls);
-        u = ok ? (uint32_t)((Rp0(ccls) + 2 * uu) * as2b + (Rq0(ccls) + 2 * vv) * as3b + cch * 2) : OOB;
-      } else {
-        const int ph = pc0[j] + cua - cr, pw = pc1[j] + cub - cs;
-        const int sh = d.stride == 2 ? 1 : 0;
-        const bool ok = live && pval[j] && ph >= 0 && pw >= 0 && !(((ph | pw) & sh)) &&
-                        (ph >> sh) < d.P && (pw >> sh) < d.Q;
-        u = ok ? (uint32_t)((ph >> sh) * as2b + (pw >> sh) * as3b + cch * 2) : OOB;
+      for (int j = 0; j < APW; ++j) {
+        uint32_t u;
+        if constexpr (MODE == MODE_FWD && SP) {
+          const int hs = pc0[j] + cr, ws = pc1[j] + cs;
+          const bool ok = live && pval[j] && (unsigned)hs < (unsigned)d.H && (unsigned)ws < (unsigned)d.W;
+          u = ok ? (uint32_t)(hs * as2b + ws * as3b) : OOB;
+        } else if constexpr (MODE == MODE_FWD) {
+          const int hu = pc0[j] + cr, wu = pc1[j] + cs;
+          const bool ok = live && pval[j] && (unsigned)hu < (unsigned)d.Hu && (unsigned)wu < (unsigned)d.Wu;
+          // integer nearest upsample folded into the gather (factor 1 without upsample)
+          const int sh = fdiv(hu, a.fUh), sw = fdiv(wu, a.fUw);
+          u = ok ? (uint32_t)(sh * as2b + sw * as3b) : OOB;
+        } else if constexpr (SP) {
+          // output pixel (p0 + 2u, q0 + 2v) of class ccls feeds source pixel u + oh + d
+          const int uu = pc0[j] - cr - Roh(ccls), vv = pc1[j] - cs - Row(ccls);
+          const bool ok = live && pval[j] && (unsigned)uu < (unsigned)Rph(ccls) &&
+                          (unsigned)vv < (unsigned)Rpw(ccls);
+          u = ok ? (uint32_t)((Rp0(ccls) + 2 * uu) * as2b + (Rq0(ccls) + 2 * vv) * as3b) : OOB;
+        } else {
+          const int ph = pc0[j] + cua - cr, pw = pc1[j] + cub - cs;
+          const int sh = d.stride == 2 ? 1 : 0;
+          const bool ok = live && pval[j] && ph >= 0 && pw >= 0 && !(((ph | pw) & sh)) &&
+                          (ph >> sh) < d.P && (pw >> sh) < d.Q;
+          u = ok ? (uint32_t)((ph >> sh) * as2b + (pw >> sh) * as3b) : OOB;
+        }
+        ua_t[j] = u;
       }
-      bdma16(ares, alane[j] + u, slot + (wid * APW + j) * 1024);
+      int kb;
+      if constexpr (MODE == MODE_FWD) kb = (cr * kw + cs) * d.C;
+      else if constexpr (SP) kb = (Rtap0(ccls) + cr * kw + cs) * d.K;
+      else kb = ckb;
+      ub_t = live ? (uint32_t)(kb * 2) : OOB;
     }
-    int kb;
-    if constexpr (MODE == MODE_FWD) kb = (cr * kw + cs) * d.C + cch;
-    else if constexpr (SP) kb = (Rtap0(ccls) + cr * kw + cs) * d.K + cch;
-    else kb = ckb;
-    const uint32_t ub = live ? (uint32_t)(kb * 2) : OOB;
+    // (OOB + a channel offset stays past every num_records: offsets are < 1 GiB)
+    const uint32_t co = (uint32_t)(cch * 2);
 #pragma unroll
-    for (int j = 0; j < BPW; ++j) bdma16(bres, blane[j] + ub, slot + ABYTES + (wid * BPW + j) * 1024);
-    // advance the cursor (selects, no branches)
+    for (int j = 0; j < APW; ++j) bdma16(ares, alane[j] + (ua_t[j] + co), slot + (wid * APW + j) * 1024);
+#pragma unroll
+    for (int j = 0; j < BPW; ++j) bdma16(bres, blane[j] + (ub_t + co), slot + ABYTES + (wid * BPW + j) * 1024);
     ++cstep;
-    cch += 64;
-    ckb += 64;
-    const bool w1 = cch == nch;
-    cch = w1 ? 0 : cch;
-    cs += w1;
-    const bool w2 = cs == kw;
-    cs = w2 ? 0 : cs;
-    cr += w2;
-    const bool w3 = cr == kh;
-    cr = w3 ? 0 : cr;
-    ckb = w3 ? 0 : ckb;
-    cub += w3;
-    const bool w4 = cub == upw;
-    cub = w4 ? 0 : cub;
-    cua += w4;
-    if constexpr (SP && MODE == MODE_DGRAD) {
-      ccls += w3;
-      const int cn = ccls < 4 ? ccls : 3;
-      kh = Rdh(cn);
-      kw = Rdw(cn);
+    cch += BK;
+    if (cch == nch) {   // tap done: advance the tap cursor (wave-uniform branch)
+      cch = 0;
+      ckb += nch;
+      ++cs;
+      const bool w2 = cs == kw;
+      cs = w2 ? 0 : cs;
+      cr += w2;
+      const bool w3 = cr == kh;
+      cr = w3 ? 0 : cr;
+      ckb = w3 ? 0 : ckb;
+      cub += w3;
+      const bool w4 = cub == upw;
+      cub = w4 ? 0 : cub;
+      cua += w4;
+      if constexpr (SP && MODE == MODE_DGRAD) {
+        ccls += w3;
+        const int cn = ccls < 4 ? ccls : 3;
+        kh = Rdh(cn);
+        kw = Rdw(cn);
+      }
     }
   };
 
@@ -449,26 +517,36 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // fragment set kk: BK = 64 -> K half kk (all RM x RN tiles); BK = 32 -> the step's 32 channels
+  // for A tiles kk*RM/2 .. (the wave's row half kk) and all RN B tiles
   const int r16 = lane & 15, g16 = lane >> 4;
   struct Frag {
-    bf16x8 a[RM], b[RN];
+    bf16x8 a[RMF], b[RN];
+    int h;
   };
   auto load = [&](Frag& f, const char* slot, int kk) {
-    const int seg = kk * 4 + g16;
+    const int seg = KH == 2 ? kk * 4 + g16 : g16;
+    const int i0 = KH == 2 ? 0 : kk * RMF;
+    f.h = kk;
 #pragma unroll
-    for (int i = 0; i < RM; ++i) f.a[i] = *(const bf16x8*)(slot + swz(wm0 + i * 16 + r16, seg));
+    for (int i = 0; i < RMF; ++i) f.a[i] = *(const bf16x8*)(slot + swz<BK>(wm0 + (i0 + i) * 16 + r16, seg));
 #pragma unroll
-    for (int j = 0; j < RN; ++j) f.b[j] = *(const bf16x8*)(slot + ABYTES + swz(wn0 + j * 16 + r16, seg));
+    for (int j = 0; j < RN; ++j) f.b[j] = *(const bf16x8*)(slot + ABYTES + swz<BK>(wn0 + j * 16 + r16, seg));
   };
   auto mma = [&](const Frag& f) {
+    const int i0 = KH == 2 ? 0 : f.h * RMF;
 #pragma unroll
-    for (int i = 0; i < RM; ++i)
+    for (int i = 0; i < RMF; ++i)
 #pragma unroll
       for (int j = 0; j < RN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
+        acc[i0 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[j], acc[i0 + i][j], 0, 0, 0);
   };
-  auto nofence = [](Frag&) {};
-  ring_loop<PW, 0>(nk, smem, SLOT, issue, load, mma, nofence);
+  if constexpr (BK == 32 && ES_RING_LEAN) {
+    ring_loop_lean<PW, NS>(nk, smem, SLOT, issue, load, mma);
+  } else {
+    auto nofence = [](Frag&) {};
+    ring_loop<PW, 0, NS>(nk, smem, SLOT, issue, load, mma, nofence);
+  }
 
   // epilogue.  Wave row r (0..WM-1) = tile row t = wm0 + r: pixel pix0 + t / NG, image
   // NG gi + t % NG.
@@ -499,16 +577,16 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
         acc[i][j][jj] = a.out_bf16 ? (float)(bf16)v : v;
       }
   }
-  if (a.vec_out) {
+  if (BK == 32 || a.vec_out) {   // (the host runs BK = 32 only with vec_out)
     // BatchNorm statistics of the stored values (conv -> BatchNorm fusion): per column, count /
     // mean / M2 over the wave's valid rows (lanes own 16 rows, Chan-merged across the 4 row
     // groups by shuffles), then across the 4 row waves in LDS -> one [3][Ng] partial per row tile
-    float* part = a.stats_part;
-    float (*st_n)[BN] = (float (*)[BN])(smem + NSLOT * SLOT);
-    float (*st_m)[BN] = st_n + 4;
-    float (*st_q)[BN] = st_n + 8;
+    float* part = MODE == MODE_FWD ? a.stats_part : nullptr;   // (FWD only: compiled out of DGRAD)
+    float (*st_n)[BN] = (float (*)[BN])(smem + RING);
+    float (*st_m)[BN] = st_n + WGM;
+    float (*st_q)[BN] = st_n + 2 * WGM;
     if (part) {
-      const int wmi = wid >> 1;
+      const int wmi = wid / WGN;
       bool okr[RM][4];
 #pragma unroll
       for (int i = 0; i < RM; ++i)
@@ -548,36 +626,42 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
         }
       }
     }
-    // stage the wave's tile in LDS (rows of WN values), then 16-byte row-contiguous stores
+    // stage the wave's tile in LDS (rows of WN values; passes of SROWS rows), then 16-byte
+    // row-contiguous stores
     constexpr int PITCH = WN * 4 + 16;
     const int esz = a.out_bf16 ? 2 : 4;
     const int pitch = WN * esz + 16;
-    __syncthreads();   // every wave is done with the ring slots
-    char* stg = smem + wid * (WM * PITCH);
-#pragma unroll
-    for (int i = 0; i < RM; ++i)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-        for (int j = 0; j < RN; ++j) {
-          char* p = stg + (i * 16 + rq + jj) * pitch + (j * 16 + col16) * esz;
-          if (a.out_bf16) *(bf16*)p = (bf16)acc[i][j][jj];
-          else *(float*)p = acc[i][j][jj];
-        }
-    __syncthreads();
+    char* stg = smem + wid * (SROWS * PITCH);
     const int cpr = WN * esz / 16;          // 16-byte chunks per row
     const int rpi = 64 / cpr;               // rows per wave instruction
     const int lr = lane / cpr, lch = lane % cpr;
-    if (n0 + wn0 + lch * 16 / esz < a.Ng) {
-      char* obase = (char*)a.out + (int64_t)(n0 + wn0) * esz + lch * 16;
-      for (int r = lr; r < WM; r += rpi)
-        if (row_ok(r)) *(uint4*)(obase + row_off(r) * esz) = *(const uint4*)(stg + r * pitch + lch * 16);
+#pragma unroll
+    for (int ps = 0; ps < WM / SROWS; ++ps) {
+      __syncthreads();   // every wave is done with the ring slots / the previous pass
+#pragma unroll
+      for (int i = 0; i < SROWS / 16; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+          for (int j = 0; j < RN; ++j) {
+            char* p = stg + (i * 16 + rq + jj) * pitch + (j * 16 + col16) * esz;
+            const float v = acc[ps * (SROWS / 16) + i][j][jj];
+            if (a.out_bf16) *(bf16*)p = (bf16)v;
+            else *(float*)p = v;
+          }
+      __syncthreads();
+      if (n0 + wn0 + lch * 16 / esz < a.Ng) {
+        char* obase = (char*)a.out + (int64_t)(n0 + wn0) * esz + lch * 16;
+        for (int r = lr; r < SROWS; r += rpi)
+          if (row_ok(ps * SROWS + r))
+            *(uint4*)(obase + row_off(ps * SROWS + r) * esz) = *(const uint4*)(stg + r * pitch + lch * 16);
+      }
     }
-    if (part && wid < 2) {   // the wave pair of row block 0 merges the 4 row waves of its columns
+    if (part && wid < WGN) {   // the waves of row block 0 merge the WGM row waves of their columns
       for (int c = lane; c < WN; c += 64) {
         const int col = wn0 + c;
         float n_ = st_n[0][col], m_ = st_m[0][col], q = st_q[0][col];
-        for (int w = 1; w < 4; ++w) {
+        for (int w = 1; w < WGM; ++w) {
           const float nb = st_n[w][col];
           if (nb > 0.f) {
             const float mb = st_m[w][col], nt = n_ + nb, dl = mb - m_, f = nb / nt;
@@ -787,10 +871,10 @@ __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
     }
 }
 
-template <int MODE, int BM, int BN, bool SP>
+template <int MODE, int BM, int BN, bool SP, int BK = 64>
 void launch_ring(const ConvArgs& a, int row_tiles, hipStream_t st) {
   dim3 grid(row_tiles, (a.Ng + BN - 1) / BN, 1);
-  hipLaunchKernelGGL((conv_ring_kernel<MODE, BM, BN, SP>), grid, dim3(RT), 0, st, a);
+  hipLaunchKernelGGL((conv_ring_kernel<MODE, BM, BN, SP, BK>), grid, dim3(RT), 0, st, a);
 }
 
 template <int BM, int BN, bool SP>
@@ -823,6 +907,9 @@ bool g_subpixel_off = [] { const char* e = getenv("ES_NO_SUBPIXEL"); return e &&
 // measured slower: 14.59 ms)
 int g_sp_ilv = [] { const char* e = getenv("ES_SP_ILV"); return e ? atoi(e) : 1; }();
 int g_sp_shortk = [] { const char* e = getenv("ES_SP_SHORTK"); return e ? atoi(e) : 0; }();
+// 256 x 256 tiles with 32-deep K-steps (conv_ring_kernel BK = 32) for FWD / DGRAD with >= 256 output
+// columns; ES_RING256=0 keeps 256 x 128 (A/B)
+bool g_ring256 = [] { const char* e = getenv("ES_RING256"); return !(e && e[0] == '0'); }();
 
 }  // namespace
 
@@ -865,6 +952,12 @@ void es_make_subpixel(const es_conv_desc_t& d, int row_tile, SubPixel& sp) {
 extern "C" int es_conv_set_ring(int on) {
   const int old = !g_ring_off;
   g_ring_off = !on;
+  return old;
+}
+
+extern "C" int es_conv_set_ring256(int on) {
+  const int old = g_ring256;
+  g_ring256 = on != 0;
   return old;
 }
 
@@ -959,6 +1052,18 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
 #define ES_RING(MD, BMV, BNV)                                                                  \
   (sp_weights ? launch_ring<MD, BMV, BNV, true>(a, row_tiles, st)                              \
               : launch_ring<MD, BMV, BNV, false>(a, row_tiles, st))
+  const bool wide = g_ring256 && big && !shortk && a.Ng >= 256 && a.ng >= 16 && a.vec_out &&
+                    (sp_weights || mode == MODE_DGRAD);   // (plain FWD: register spills at 256 x 256)
+  if (wide) {
+    if (mode == MODE_FWD) {
+      if (sp_weights) launch_ring<MODE_FWD, 256, 256, true, 32>(a, row_tiles, st);
+      else launch_ring<MODE_FWD, 256, 256, false, 32>(a, row_tiles, st);
+    } else {
+      if (sp_weights) launch_ring<MODE_DGRAD, 256, 256, true, 32>(a, row_tiles, st);
+      else launch_ring<MODE_DGRAD, 256, 256, false, 32>(a, row_tiles, st);
+    }
+    return 1;
+  }
   if (mode == MODE_FWD) {
     if (a.Ng <= 64 || shortk) big ? ES_RING(MODE_FWD, 256, 64) : ES_RING(MODE_FWD, 128, 64);
     else big ? ES_RING(MODE_FWD, 256, 128) : ES_RING(MODE_FWD, 128, 128);

@@ -90,6 +90,10 @@ int es_conv_set_glds(int on);
 /* Select the 8-wave LDS-DMA ring kernels (conv_mfma.hip) for the bf16 convs whose K-step is one tap
  * x 64 channels: 1 = on (default), 0 = use the 4-wave kernels.  Returns the previous setting. */
 int es_conv_set_ring(int on);
+/* 256 x 256 ring tiles with 32-deep K-steps for sub-pixel FWD and DGRAD with >= 256 output channels:
+ * 1 = on (default), 0 = 256 x 128 tiles (same accumulation order: bit-identical results).
+ * Returns the previous setting. */
+int es_conv_set_ring256(int on);
 /* Sub-pixel decomposition of stride-1 convs over a x2 nearest upsample (conv_mfma.hip): 1 = on
  * (default; wgrad uses it internally, fwd/dgrad when the caller packs mode 2/3 weights and sets
  * desc->subpixel), 0 = off.  Returns the previous setting. */

@@ -525,3 +525,39 @@ def test_dfront_fused(N, H, W):
     assert rel(db.cpu() - 0.5, br.grad) < 1e-4
     assert rel(dg.cpu() - 0.5, gmr.grad) < 1e-4
     assert rel(dbt.cpu() - 0.5, btr.grad) < 1e-4
+
+
+@pytest.mark.parametrize("case", [(200, 256, 24, 24, 128, 3), (200, 128, 13, 13, 256, 3)])
+def test_conv_ring256_matches_ring128(case):
+    """256 x 256 ring tiles with 32-deep K-steps (sub-pixel FWD with 256 output channels, DGRAD
+    with 256 input channels) accumulate in the same K order as the 256 x 128 tiles: bf16 outputs
+    bit-identical; fused BatchNorm statistics equal up to the merge order."""
+    hip = _hip()
+    from expertsim.layers import ConvOp, NormOp, Upsample
+    N, Cin, H, W, Cout, k = case
+    torch.manual_seed(5)
+    w = torch.randn(Cout, Cin, k, k, device=DEV) / np.sqrt(Cin * k * k)
+    b = torch.randn(Cout, device=DEV)
+    op = ConvOp(torch.nn.Parameter(w), torch.nn.Parameter(b), upsample=Upsample((H, W), scale=(2, 2)))
+    from expertsim.layers import Act
+    xa = Act.nhwc(N, Cin, H, W, torch.bfloat16, DEV)
+    xa.t.normal_()
+    outs = []
+    old = hip.lib().es_conv_set_ring256(1)
+    try:
+        for on in (1, 0):
+            hip.lib().es_conv_set_ring256(on)
+            ya = op.fwd(xa, out_dtype=torch.bfloat16, bn_stats=True)
+            gy = ya.like_nhwc(torch.bfloat16)
+            gy.t.copy_(torch.randn(gy.t.shape, generator=torch.Generator().manual_seed(2)).to(DEV))
+            dxa = op.dgrad(gy, xa, dx_dtype=torch.bfloat16)
+            nm = NormOp(hip.NORM_BN, torch.ones(Cout, device=DEV), torch.zeros(Cout, device=DEV),
+                        running_mean=torch.zeros(Cout, device=DEV), running_var=torch.ones(Cout, device=DEV))
+            m, istd = nm.stats(ya)
+            torch.cuda.synchronize()
+            outs.append((ya.t.clone(), dxa.t.clone(), m.cpu(), istd.cpu()))
+    finally:
+        hip.lib().es_conv_set_ring256(old)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    assert rel(outs[0][2], outs[1][2]) < 1e-5 and rel(outs[0][3], outs[1][3]) < 1e-5
