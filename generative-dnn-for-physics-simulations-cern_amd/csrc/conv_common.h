@@ -61,6 +61,8 @@ struct ConvArgs {
   float* stats_part;   // ring FWD: per-row-tile BatchNorm partials [tile][3][Ng] (count, mean, M2)
   int sp_tpc;          // ring SP FWD: 0 = class-major tile order; else class-interleaved with this
                        // many tiles per class (the 4 classes of the same source pixels adjacent)
+  int sp_merge;        // ring SP FWD with 4 identical class geometries: ONE GEMM whose columns are
+                       // (class, out-channel) (4*Ng columns; the classes share the source gather)
 };
 
 

@@ -319,7 +319,12 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   const int NB = BM / NG;
   int cls = 0, gh, gw, TT, jt;
   if constexpr (MODE == MODE_FWD && SP) {
-    if (a.sp_tpc > 0) {
+    if (a.sp_merge) {
+      // merged classes: the rows are the (shared) source pixels of class 0's geometry, the
+      // columns (class, channel); the class is resolved per wave in the epilogue
+      TT = sp.tile0[1];
+      jt = tl % TT;
+    } else if (a.sp_tpc > 0) {
       // class-interleaved: tile r = 4 jt + class, so the 4 class tiles of the same source
       // pixels run back to back (one XCD, shared L2); classes with fewer tiles skip the tail
       TT = 4 * a.sp_tpc;
@@ -553,12 +558,21 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   const int col16 = lane & 15, rq = (lane >> 4) * 4;
   auto row_pix = [&](int r) { return pix0 + (wm0 + r) / NG; };
   auto row_img = [&](int r) { return gi * NG + (wm0 + r) % NG; };
+  // the wave's output columns: class ecls (merged sub-pixel FWD: column block / Ng), first
+  // output channel kc0 (a wave's WN columns never straddle a class: Ng % 64 == 0)
+  int ecls = cls, kc0 = n0 + wn0;
+  if constexpr (SP && MODE == MODE_FWD) {
+    if (a.sp_merge) {
+      ecls = kc0 / a.Ng;
+      kc0 -= ecls * a.Ng;
+    }
+  }
   auto row_off = [&](int r) -> int64_t {   // element offset of the wave row's output pixel
     const int pix = row_pix(r);
     int y = pix / gw, x = pix - y * gw;
     if constexpr (SP && MODE == MODE_FWD) {
-      y = sp.p0[cls] + 2 * y;
-      x = sp.q0[cls] + 2 * x;
+      y = sp.p0[ecls] + 2 * y;
+      x = sp.q0[ecls] + 2 * x;
     }
     return (int64_t)row_img(r) * a.os[0] + (int64_t)y * a.os[2] + (int64_t)x * a.os[3];
   };
@@ -566,7 +580,7 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   // final values (bias added, rounded to the output dtype) back into acc
 #pragma unroll
   for (int j = 0; j < RN; ++j) {
-    const int ng = n0 + wn0 + j * 16 + col16;
+    const int ng = kc0 + j * 16 + col16;
     float bv = 0.f;
     if constexpr (MODE == MODE_FWD) bv = (a.bias && ng < a.Ng) ? a.bias[ng] : 0.f;
 #pragma unroll
@@ -650,8 +664,8 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
             else *(float*)p = v;
           }
       __syncthreads();
-      if (n0 + wn0 + lch * 16 / esz < a.Ng) {
-        char* obase = (char*)a.out + (int64_t)(n0 + wn0) * esz + lch * 16;
+      if (kc0 + lch * 16 / esz < a.Ng) {
+        char* obase = (char*)a.out + (int64_t)kc0 * esz + lch * 16;
         for (int r = lr; r < SROWS; r += rpi)
           if (row_ok(ps * SROWS + r))
             *(uint4*)(obase + row_off(ps * SROWS + r) * esz) = *(const uint4*)(stg + r * pitch + lch * 16);
@@ -670,11 +684,13 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
             n_ = nt;
           }
         }
-        if (n0 + col < a.Ng) {
-          float* pp = part + (int64_t)tl * 3 * a.Ng;   // one partial per row tile
-          pp[n0 + col] = n_;
-          pp[a.Ng + n0 + col] = m_;
-          pp[2 * a.Ng + n0 + col] = q;
+        const int kc = kc0 + c;
+        if (kc < a.Ng) {
+          // one partial per row tile (merged sub-pixel FWD: per row tile and class)
+          float* pp = part + (int64_t)(a.sp_merge ? tl * 4 + ecls : tl) * 3 * a.Ng;
+          pp[kc] = n_;
+          pp[a.Ng + kc] = m_;
+          pp[2 * a.Ng + kc] = q;
         }
       }
     }
@@ -910,6 +926,10 @@ int g_sp_shortk = [] { const char* e = getenv("ES_SP_SHORTK"); return e ? atoi(e
 // 256 x 256 tiles with 32-deep K-steps (conv_ring_kernel BK = 32) for FWD / DGRAD with >= 256 output
 // columns; ES_RING256=0 keeps 256 x 128 (A/B)
 bool g_ring256 = [] { const char* e = getenv("ES_RING256"); return !(e && e[0] == '0'); }();
+// sub-pixel FWD whose 4 parity classes have the same geometry (e.g. 3x3 pad 0: every class reads
+// the 2x2 source window at (u, v)): one 256 x 256 GEMM over (class, channel) columns; ES_SP_MERGE=0
+// runs the classes as separate row tiles (A/B)
+bool g_sp_merge = [] { const char* e = getenv("ES_SP_MERGE"); return !(e && e[0] == '0'); }();
 
 }  // namespace
 
@@ -1034,20 +1054,38 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
     es_make_subpixel(d, NB, a.sp);   // FWD: tile0 = per-class tile prefix of one image group
     if (mode == MODE_FWD) row_tiles = NGI * a.sp.tile0[4];
   }
-  a.sp_tpc = 0;
-  if (sp_weights && mode == MODE_FWD && g_sp_ilv) {
-    for (int c = 0; c < 4; ++c) a.sp_tpc = std::max(a.sp_tpc, a.sp.tile0[c + 1] - a.sp.tile0[c]);
-    row_tiles = NGI * 4 * a.sp_tpc;
-  }
   // staged 16-byte row stores: channel-contiguous rows, 16-byte aligned, no beta
   const int vel = a.out_bf16 ? 8 : 4;
   a.vec_out = a.os[1] == 1 && a.beta == 0.f && a.os[0] % vel == 0 && a.os[2] % vel == 0 && a.os[3] % vel == 0 &&
               a.Ng % vel == 0 && ((uintptr_t)a.out & 15) == 0;
+  a.sp_tpc = 0;
+  a.sp_merge = 0;
+  if (sp_weights && mode == MODE_FWD && g_sp_merge && g_ring256 && big && a.vec_out && a.ng >= 16 &&
+      a.Ng % 64 == 0) {
+    bool same = true;
+    for (int c = 1; c < 4; ++c)
+      same = same && a.sp.dh[c] == a.sp.dh[0] && a.sp.dw[c] == a.sp.dw[0] && a.sp.ph[c] == a.sp.ph[0] &&
+             a.sp.pw[c] == a.sp.pw[0] && a.sp.oh[c] == a.sp.oh[0] && a.sp.ow[c] == a.sp.ow[0];
+    if (same) {
+      a.sp_merge = 1;
+      row_tiles = NGI * a.sp.tile0[1];
+    }
+  }
+  if (sp_weights && mode == MODE_FWD && g_sp_ilv && !a.sp_merge) {
+    for (int c = 0; c < 4; ++c) a.sp_tpc = std::max(a.sp_tpc, a.sp.tile0[c + 1] - a.sp.tile0[c]);
+    row_tiles = NGI * 4 * a.sp_tpc;
+  }
   // fused BatchNorm statistics (es_conv2d_fwd_stats): one [3][Ng] partial per row tile
   a.stats_part = nullptr;
-  if (mode == MODE_FWD && g_stats_req.part && a.vec_out && (int64_t)row_tiles * 3 * a.Ng <= g_stats_req.floats) {
+  const int chunks = a.sp_merge ? 4 * row_tiles : row_tiles;
+  if (mode == MODE_FWD && g_stats_req.part && a.vec_out && (int64_t)chunks * 3 * a.Ng <= g_stats_req.floats) {
     a.stats_part = g_stats_req.part;
-    g_stats_req.chunks = row_tiles;
+    g_stats_req.chunks = chunks;
+  }
+  if (a.sp_merge) {   // (vec_out: the merged epilogue is the staged one)
+    dim3 grid(row_tiles, (4 * a.Ng + 255) / 256, 1);
+    hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 256, true, 32>), grid, dim3(RT), 0, st, a);
+    return 1;
   }
 #define ES_RING(MD, BMV, BNV)                                                                  \
   (sp_weights ? launch_ring<MD, BMV, BNV, true>(a, row_tiles, st)                              \
