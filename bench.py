@@ -30,6 +30,9 @@ sys.path.insert(0, ROOT)
 # reference): neutron 10.573 GFLOP, proton 28.566 GFLOP
 STEP_FLOP_PER_IMAGE = {"neutron": 10.573e9, "proton": 28.566e9}
 PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
+# HBM traffic of the roofline kernel from committed PMC passes (tools/gpu_traffic.sh ->
+# tools/traffic_json.py): FETCH_SIZE (x2, gfx950) + WRITE_SIZE per launch of G0.c5.fwd
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01_s2h_c5_fwd_traffic.json")
 
 
 def conv_flops_per_image(arch):
@@ -169,9 +172,15 @@ def main():
             avg_ms = stats[dom]["avg_ms"]
             achieved = flops / (avg_ms * 1e-3) / 1e12
             peak = PEAK_TFLOPS[args.precision]
-            roof = {"bound": "mfma", "kernel": f"conv_igemm {dom} (generator conv_layers.5)",
+            traffic, tnote = None, None
+            if dom == "G0.c5.fwd" and args.arch == "neutron" and os.path.exists(TRAFFIC_JSON):
+                tj = json.load(open(TRAFFIC_JSON))
+                traffic = tj["traffic_bytes"]
+                tnote = (f"bytes per launch: FETCH_SIZE x2 {tj['fetch_bytes']} + WRITE_SIZE {tj['write_bytes']} "
+                         f"(algorithmic {tj['algorithmic_bytes']}), {os.path.relpath(TRAFFIC_JSON, ROOT)}")
+            roof = {"bound": "mfma", "kernel": f"conv_ring {dom} (generator conv_layers.5)",
                     "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                    "frac": round(achieved / peak, 4), "traffic": None,
+                    "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_note": tnote,
                     "avg_ms": round(avg_ms, 4), "launches": stats[dom]["count"],
                     "all_probed": {k: {"avg_ms": round(v["avg_ms"], 4),
                                        "tflops": round(flops / (v["avg_ms"] * 1e-3) / 1e12, 2)}
