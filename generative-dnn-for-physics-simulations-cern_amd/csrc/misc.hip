@@ -188,6 +188,55 @@ __global__ void copy_kernel(View x, const void* xp, int xbf, View y, void* yp, i
   }
 }
 
+// Dense NCHW <-> NHWC re-layout (the neutron generator's fc2 rows [B][128*13*13] <-> the NHWC conv
+// input, neutron/generator.py:18-20): per sample a [R][S] -> [S][R] transpose through a 64 x 64
+// LDS tile, both sides read / written along contiguous rows (the generic element-wise copy above
+// divides per element and ran at ~1 TB/s).
+template <typename T>
+__global__ void __launch_bounds__(256) transpose_kernel(const T* __restrict__ x, T* __restrict__ y, int R, int S) {
+  __shared__ T tile[64][65];
+  const int n = blockIdx.z, r0 = blockIdx.y * 64, s0 = blockIdx.x * 64;
+  const T* xs = x + (int64_t)n * R * S;
+  T* ys = y + (int64_t)n * R * S;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 64; i += 4) {
+    const int r = r0 + ty + i, c = s0 + tx;
+    if (r < R && c < S) tile[ty + i][tx] = xs[(int64_t)r * S + c];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 64; i += 4) {
+    const int c = s0 + ty + i, r = r0 + tx;
+    if (r < R && c < S) ys[(int64_t)c * R + r] = tile[tx][ty + i];
+  }
+}
+
+// x / y dense NCHW and dense NHWC of one shape (either direction): launch the transpose and
+// return true
+bool try_transpose(const es_view_t* x, es_dtype_t xdt, const void* xp, const es_view_t* y, es_dtype_t ydt, void* yp,
+                   hipStream_t st) {
+  if (xdt != ydt || x->c <= 1) return false;
+  const int64_t C = x->c, HW = (int64_t)x->h * x->w;
+  auto nchw = [&](const es_view_t* v) {
+    return v->s[3] == 1 && v->s[2] == v->w && v->s[1] == HW && v->s[0] == C * HW;
+  };
+  auto nhwc = [&](const es_view_t* v) {
+    return v->s[1] == 1 && v->s[3] == C && v->s[2] == (int64_t)v->w * C && v->s[0] == C * HW;
+  };
+  int64_t R, S;
+  if (nchw(x) && nhwc(y)) { R = C; S = HW; }
+  else if (nhwc(x) && nchw(y)) { R = HW; S = C; }
+  else return false;
+  if (R * S * x->n * 4 >= (1ll << 31) || x->n > 65535) return false;
+  const dim3 grid((unsigned)((S + 63) / 64), (unsigned)((R + 63) / 64), (unsigned)x->n);
+  if (xdt == ES_BF16)
+    hipLaunchKernelGGL(transpose_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)xp, (bf16*)yp, (int)R, (int)S);
+  else
+    hipLaunchKernelGGL(transpose_kernel<float>, grid, dim3(256), 0, st, (const float*)xp, (float*)yp, (int)R, (int)S);
+  return true;
+}
+
 // ------------------------------------------------------------------------------- avg pool
 __global__ void avgpool_fwd_kernel(View x, const void* xp, int bf, View y, void* yp) {
   // one wave per (n, c)
@@ -485,6 +534,10 @@ extern "C" int es_copy(const es_view_t* x, es_dtype_t xdt, const void* xp, const
   ES_CHECK_ARG(x->n == y->n && x->c == y->c && x->h == y->h && x->w == y->w, "copy: shape mismatch");
   const int64_t total = (int64_t)x->n * x->c * x->h * x->w;
   if (total == 0) return ES_OK;
+  if (alpha == 1.f && beta == 0.f && try_transpose(x, xdt, xp, y, ydt, yp, (hipStream_t)stream)) {
+    ES_CHECK_LAUNCH();
+    return ES_OK;
+  }
   hipLaunchKernelGGL(copy_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, mkview(x), xp,
                      xdt == ES_BF16, mkview(y), yp, ydt == ES_BF16, alpha, beta);
   ES_CHECK_LAUNCH();

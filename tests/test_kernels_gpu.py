@@ -561,3 +561,20 @@ def test_conv_ring256_matches_ring128(case):
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
     assert rel(outs[0][2], outs[1][2]) < 1e-5 and rel(outs[0][3], outs[1][3]) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [(5, 128, 13, 13), (3, 70, 9, 7), (2, 3, 5, 4)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_copy_relayout(shape, dtype):
+    """es_copy between dense NCHW and dense NHWC views (the LDS-tiled transpose path) is exact."""
+    hip = _hip()
+    from expertsim.layers import Act, copy_act
+    N, Cc, H, W = shape
+    x = torch.randn(shape).to(dtype).to(DEV)
+    nchw = Act(x.reshape(-1), shape, (Cc * H * W, H * W, W, 1))
+    nhwc = Act.nhwc(N, Cc, H, W, dtype, DEV)
+    copy_act(nchw, nhwc)
+    assert torch.equal(nhwc.torch_nchw().contiguous(), x)
+    back = Act(torch.empty_like(x).reshape(-1), shape, (Cc * H * W, H * W, W, 1))
+    copy_act(nhwc, back)
+    assert torch.equal(back.t.view(shape), x)
