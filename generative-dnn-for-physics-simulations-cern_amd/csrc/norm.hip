@@ -760,7 +760,11 @@ extern "C" int es_channel_sum(const es_view_t* x, es_dtype_t xdt, const void* xp
     // rows, instead of 63 of every 64 lanes idling
     const int nb = std::min<int>(chunks, (int)((rows + 255) / 256));
     hipLaunchKernelGGL(sum1_kernel, dim3(nb), dim3(256), 0, st, b, (int)rows, (float*)ws);
-    hipLaunchKernelGGL(sum_finalize_kernel, dim3(1), dim3(256), 0, st, (const float*)ws, nb, 1, out, beta);
+    if (nb > 32)   // (a single thread summing thousands of partials took ~75 us)
+      hipLaunchKernelGGL(sums_finalize_block_kernel, dim3(1), dim3(256), 0, st, (const float*)ws, nb, 1, 1.f,
+                         nullptr, (float*)nullptr, (float*)nullptr, out, (float*)nullptr, beta);
+    else
+      hipLaunchKernelGGL(sum_finalize_kernel, dim3(1), dim3(256), 0, st, (const float*)ws, nb, 1, out, beta);
     ES_CHECK_LAUNCH();
     return ES_OK;
   }
