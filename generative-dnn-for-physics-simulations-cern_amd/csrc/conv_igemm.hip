@@ -82,10 +82,26 @@ template <> struct Vec16<bf16> { typedef uint4 type; static constexpr int N = 8;
 // ---------------------------------------------------------------------------------------------
 // Element gathers (scalar); used by the generic path and by the vector path for the base address
 // ---------------------------------------------------------------------------------------------
+// a Linear as a 1x1 conv of 1x1 images: rows m = sample, kk = feature (the generic decomposition
+// below costs 8 integer divisions per element, ~30 us per launch for the small linears)
+__device__ __forceinline__ bool is_linear(const ConvArgs& a) {
+  const es_conv_desc_t& d = a.d;
+  return d.R == 1 && d.S == 1 && d.P == 1 && d.Q == 1 && d.Hu == 1 && d.Wu == 1 && d.stride == 1 && d.pad == 0 &&
+         !a.fold && d.hmap == nullptr;
+}
+
 template <typename T, int MODE>
 __device__ __forceinline__ float gather_a(const ConvArgs& a, int m, int kk) {
   const es_conv_desc_t& d = a.d;
   const T* src = (const T*)a.a_src;
+  if (is_linear(a)) {   // branch-free: clamped index + select (the loads of a chunk issue together)
+    const bool ok = m < a.M && kk < a.Kd;
+    int64_t i;
+    if constexpr (MODE == MODE_WGRAD) i = (int64_t)kk * a.as[0] + (int64_t)m * a.as[1];
+    else i = (int64_t)m * a.as[0] + (int64_t)kk * a.as[1];
+    const float v = to_f(src[ok ? i : 0]);
+    return ok ? v : 0.f;
+  }
   if (m >= a.M || kk >= a.Kd) return 0.f;
   if constexpr (MODE == MODE_FWD) {
     const int c = kk % d.C; const int rs = kk / d.C; const int s = rs % d.S; const int r = rs / d.S;
@@ -120,6 +136,14 @@ template <typename T, int MODE>
 __device__ __forceinline__ float gather_b(const ConvArgs& a, int ng, int kk) {
   const es_conv_desc_t& d = a.d;
   const T* src = (const T*)a.b_src;
+  if (is_linear(a)) {
+    const bool ok = ng < a.Ng && kk < a.Kd;
+    int64_t i;
+    if constexpr (MODE == MODE_WGRAD) i = (int64_t)kk * a.bs[0] + (int64_t)ng * a.bs[1];
+    else i = (int64_t)ng * a.Kd + kk;   // packed weights (no upsample fold for a linear)
+    const float v = to_f(src[ok ? i : 0]);
+    return ok ? v : 0.f;
+  }
   if (ng >= a.Ng || kk >= a.Kd) return 0.f;
   if constexpr (MODE == MODE_FWD) {
     return to_f(src[(int64_t)ng * a.Kd + kk]);
@@ -856,7 +880,9 @@ int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
   // split over K anyway (few tiles, long K: more, smaller workgroups)
   const int tiles128 = ((a.M + 127) / 128) * ((a.Ng + 127) / 128);
   const bool splitk_case = MODE != MODE_WGRAD && a.dense_f32_out && tiles128 < 256 && (a.Kd + BK - 1) / BK >= 16;
-  const bool big = a.M >= 128 && a.Ng >= 96 && !splitk_case;
+  // 128 x 128 only with enough tiles to fill the chip: a small GEMM (the discriminator / router /
+  // aux linears at batch 512) is latency-bound per K-step, so more, smaller workgroups finish sooner
+  const bool big = a.M >= 128 && a.Ng >= 96 && !splitk_case && tiles128 >= 128;
   const int BM = big ? 128 : 64, BN = big ? 128 : 64;
   if constexpr (sizeof(T) == 2 && MODE == MODE_WGRAD) {
     if (avec && bvec && !g_no_glds && es_conv_ring_launch(a, MODE, st)) {
