@@ -314,6 +314,10 @@ __global__ void __launch_bounds__(1024) sn_power_kernel(const float* w, int h, i
   for (int i = threadIdx.x; i < h; i += blockDim.x) d += u[i] * wv[i];
   d = block_sum(d, sh);
   if (threadIdx.x == 0) sigma[0] = d;
+  // snapshot of the u, v this call used (for the backward; the next call updates them in place)
+  float* snap = scratch + h + wd;
+  for (int i = threadIdx.x; i < h; i += blockDim.x) snap[i] = u[i];
+  for (int j = threadIdx.x; j < wd; j += blockDim.x) snap[h + j] = v[j];
 }
 
 // ---- multi-block power iteration for the large reshaped weights (discriminator fc1: 128 x 1305)
@@ -351,7 +355,8 @@ __global__ void __launch_bounds__(256) sn_wv_kernel(const float* __restrict__ w,
   if (lane == 0) wv[i] = t;
 }
 // u = wv / ||wv|| (update), sigma = u . wv
-__global__ void __launch_bounds__(256) sn_final_kernel(int h, const float* wv, float* u, int update, float* sigma) {
+__global__ void __launch_bounds__(256) sn_final_kernel(int h, int wd, const float* wv, float* u, const float* v,
+                                                       int update, float* sigma, float* snap) {
   __shared__ float sh[8];
   if (update) {
     float ss = 0.f;
@@ -364,6 +369,8 @@ __global__ void __launch_bounds__(256) sn_final_kernel(int h, const float* wv, f
   for (int i = threadIdx.x; i < h; i += 256) d += u[i] * wv[i];
   d = block_sum(d, sh);
   if (threadIdx.x == 0) sigma[0] = d;
+  for (int i = threadIdx.x; i < h; i += 256) snap[i] = u[i];
+  for (int j = threadIdx.x; j < wd; j += 256) snap[h + j] = v[j];
 }
 
 // ---- multi-block backward: block partials of <G, W> (pass 1), then the elementwise update with
@@ -574,7 +581,8 @@ extern "C" int es_gather_rows(const float* src, int64_t src_ld, const int32_t* i
 
 extern "C" int es_sn_power_iter(const float* w, int h, int wd, float* u, float* v, float* sigma, int update,
                                 es_stream_t stream) {
-  // scratch lives after sigma[0] in the caller's buffer: sigma must have 1 + h + wd floats
+  // the caller's buffer: sigma[0], scratch [h + wd], then the snapshot of the u, v used [h + wd]
+  // (1 + 2 (h + wd) floats)
   hipStream_t st = (hipStream_t)stream;
   if ((int64_t)h * wd >= 16384) {   // large weights: spread the two mat-vecs over the chip
     float* wv = sigma + 1;
@@ -582,7 +590,8 @@ extern "C" int es_sn_power_iter(const float* w, int h, int wd, float* u, float* 
     if (update) hipLaunchKernelGGL(sn_wtu_kernel, dim3((wd + 63) / 64), dim3(256), 0, st, w, h, wd, u, vt);
     hipLaunchKernelGGL(sn_wv_kernel, dim3((h + 3) / 4), dim3(256), 0, st, w, h, wd, update ? (const float*)vt : v,
                        update, v, wv);
-    hipLaunchKernelGGL(sn_final_kernel, dim3(1), dim3(256), 0, st, h, (const float*)wv, u, update, sigma);
+    hipLaunchKernelGGL(sn_final_kernel, dim3(1), dim3(256), 0, st, h, wd, (const float*)wv, u, (const float*)v, update,
+                       sigma, sigma + 1 + h + wd);
   } else {
     hipLaunchKernelGGL(sn_power_kernel, dim3(1), dim3(1024), 0, st, w, h, wd, u, v, sigma, update, sigma + 1);
   }

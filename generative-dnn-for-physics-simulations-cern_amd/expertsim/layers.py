@@ -502,11 +502,13 @@ class SpectralNorm:
 
     def sigma(self, update=True):
         """One power iteration (train mode) -> device tensor holding sigma (no host sync)."""
-        buf = torch.empty(1 + self.h + self.wd, dtype=torch.float32, device=self.w.device)
-        hip.call("es_sn_power_iter", hip.ptr(self.w), self.h, self.wd, hip.ptr(self.u), hip.ptr(self.v),
+        h, wd = self.h, self.wd
+        buf = torch.empty(1 + 2 * (h + wd), dtype=torch.float32, device=self.w.device)
+        hip.call("es_sn_power_iter", hip.ptr(self.w), h, wd, hip.ptr(self.u), hip.ptr(self.v),
                  hip.ptr(buf), 1 if update else 0, hip.stream_ptr())
-        # snapshot u, v used by this call (the next call updates them in place)
-        return buf[:1], self.u.clone(), self.v.clone()
+        # the kernel snapshots the u, v it used after the scratch (the next call updates them in place)
+        o = 1 + h + wd
+        return buf[:1], buf[o:o + h], buf[o + h:o + h + wd]
 
     def bwd(self, g_sn: torch.Tensor, sig, dw_orig: torch.Tensor, beta=1.0):
         sigma, u, v = sig

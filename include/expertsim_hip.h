@@ -257,6 +257,8 @@ int es_gather_rows(const float* src, int64_t src_ld, const int32_t* idx, int row
  * Spectral norm (torch.nn.utils.spectral_norm, n_power_iterations=1, eps=1e-12) for every
  * discriminator layer (neutron/discriminator.py:12,17,27,33,39; proton/discriminator.py:122,
  * 127,134,140,146).  One power iteration updates u,v in place and writes sigma = u.(W v).
+ * sigma points to 1 + 2*(h + wd) floats: sigma[0], scratch, then a snapshot of the u [h] and
+ * v [wd] this call used (what es_sn_bwd needs once the next call has updated u, v in place).
  * ---------------------------------------------------------------------------------------- */
 int es_sn_power_iter(const float* w, int h, int wd, float* u, float* v, float* sigma, int update,
                      es_stream_t stream);
