@@ -556,8 +556,18 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   // epilogue.  Wave row r (0..WM-1) = tile row t = wm0 + r: pixel pix0 + t / NG, image
   // NG gi + t % NG.
   const int col16 = lane & 15, rq = (lane >> 4) * 4;
-  auto row_pix = [&](int r) { return pix0 + (wm0 + r) / NG; };
-  auto row_img = [&](int r) { return gi * NG + (wm0 + r) % NG; };
+  // (no integer divisions per row: NG is a power of two and gw is divided by magic numbers; the
+  // generic divides cost ~100 VALU per stored row, a third of the whole epilogue)
+  const int lgNG = uni(31 - __builtin_clz(NG));
+  FastDiv fgw;
+  {
+    uint32_t l = 0;
+    while ((1u << l) < (uint32_t)gw) ++l;
+    fgw.l = uni((int)l);
+    fgw.m = (uint32_t)uni((int)(uint32_t)(((1ull << 32) * ((1ull << l) - (uint32_t)gw)) / (uint32_t)gw + 1));
+  }
+  auto row_pix = [&](int r) { return pix0 + ((wm0 + r) >> lgNG); };
+  auto row_img = [&](int r) { return gi * NG + ((wm0 + r) & (NG - 1)); };
   // the wave's output columns: class ecls (merged sub-pixel FWD: column block / Ng), first
   // output channel kc0 (a wave's WN columns never straddle a class: Ng % 64 == 0)
   int ecls = cls, kc0 = n0 + wn0;
@@ -569,7 +579,7 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   }
   auto row_off = [&](int r) -> int64_t {   // element offset of the wave row's output pixel
     const int pix = row_pix(r);
-    int y = pix / gw, x = pix - y * gw;
+    int y = fdiv(pix, fgw), x = pix - y * gw;
     if constexpr (SP && MODE == MODE_FWD) {
       y = sp.p0[ecls] + 2 * y;
       x = sp.q0[ecls] + 2 * x;
