@@ -74,7 +74,11 @@ __device__ __forceinline__ void keep_bits(const FastArgs& a, int r0, int c0, uin
   if constexpr (KM == KM_BITS) {
     const int cb = a.C >> 3, cv = c0 >> 3;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) keep[j] = r0 + j < a.rows ? a.keep[(int64_t)(r0 + j) * cb + cv] : 0u;
+    for (int j = 0; j < 4; ++j) {   // clamped row, unconditional load (the 4 loads issue together)
+      const bool in = r0 + j < a.rows;
+      const uint32_t b = a.keep[(int64_t)(in ? r0 + j : r0) * cb + cv];
+      keep[j] = in ? b : 0u;
+    }
     return;
   }
   keep[0] = keep[1] = keep[2] = keep[3] = 0u;
@@ -209,7 +213,7 @@ __global__ void __launch_bounds__(256) bn_fwd_fast(FastArgs a) {
     float v[4][8];
 #pragma unroll
     for (int j = 0; j < 4; ++j)            // issue every load of the group before any store
-      if (j < nr) ld8<T>(x + (int64_t)(r0 + j) * a.C + g.c0, v[j]);
+      ld8<T>(x + (int64_t)(r0 + (j < nr ? j : 0)) * a.C + g.c0, v[j]);   // clamped: no branch per row
     uint32_t keep[4];
     keep_bits<KM>(a, r0, g.c0, keep);
     if (KM != KM_NONE && KM != KM_BITS && a.keep) {
@@ -253,12 +257,20 @@ __global__ void __launch_bounds__(256) bn_reduce_fast(FastArgs a) {
       const int r0 = g.rbase + grp * 4;
       uint32_t keep[4];
       if (MODE == 1) keep_bits<KM>(a, r0, g.c0, keep);
+      // every load of the group first (clamped rows; rows past the end are masked below): the
+      // per-row guarded loads were serialised by a wait per row (~4 TB/s -> 5+)
+      const int nr = min(4, g.rlim - r0);
+      float vv[4][8], dd[4][8];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int r = r0 + j;
-        if (r >= g.rlim) break;
-        float v[8];
-        ld8<T>(x + (int64_t)r * a.C + g.c0, v);
+        const int rr = r0 + (j < nr ? j : 0);
+        ld8<T>(x + (int64_t)rr * a.C + g.c0, vv[j]);
+        if (MODE == 1) ld8<T>(dy + (int64_t)rr * a.C + g.c0, dd[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j >= nr) break;
+        const float* v = vv[j];
         if (MODE == 0) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
@@ -268,8 +280,7 @@ __global__ void __launch_bounds__(256) bn_reduce_fast(FastArgs a) {
             s2[k] += d * (v[k] - s1[k]);
           }
         } else {
-          float d[8];
-          ld8<T>(dy + (int64_t)r * a.C + g.c0, d);
+          const float* d = dd[j];
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
             const float dn = chain_bwd(a, v[k] * sc[k] + sh[k], d[k], (keep[j] >> k) & 1u);
@@ -346,11 +357,11 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_fast(FastArgs a) {
       const int nr = min(4, g.rlim - r0);
       float v[4][8], d[4][8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)          // issue every load of the group before any store
-        if (j < nr) {
-          ld8<T>(x + (int64_t)(r0 + j) * a.C + g.c0, v[j]);
-          ld8<T>(dy + (int64_t)(r0 + j) * a.C + g.c0, d[j]);
-        }
+      for (int j = 0; j < 4; ++j) {        // every load of the group, unconditionally (clamped rows)
+        const int rr = r0 + (j < nr ? j : 0);
+        ld8<T>(x + (int64_t)rr * a.C + g.c0, v[j]);
+        ld8<T>(dy + (int64_t)rr * a.C + g.c0, d[j]);
+      }
       uint32_t keep[4];
       keep_bits<KM>(a, r0, g.c0, keep);
 #pragma unroll
