@@ -83,7 +83,9 @@ __global__ void __launch_bounds__(NT) c1_fwd(Thin t) {
 #pragma unroll
   for (int j = 0; j < RS; ++j) {
     const int hu = p * d.stride - d.pad + j / d.S, wu = q * d.stride - d.pad + j % d.S;
-    xv[j] = (hu >= 0 && hu < d.H && wu >= 0 && wu < d.W) ? to_f(x[hu * t.as[2] + wu * t.as[3]]) : 0.f;
+    const bool ok = hu >= 0 && hu < d.H && wu >= 0 && wu < d.W;
+    const float v = to_f(x[ok ? hu * t.as[2] + wu * t.as[3] : 0]);   // clamped: loads issue together
+    xv[j] = ok ? v : 0.f;
   }
   float o[8];
 #pragma unroll
@@ -117,22 +119,23 @@ __global__ void __launch_bounds__(NT) c1_dgrad(Thin t) {
 #pragma unroll
   for (int j = 0; j < RS; ++j) {
     int ph = h + d.pad - j / d.S, pw = w + d.pad - j % d.S;
-    if (!live || ph < 0 || pw < 0) continue;
+    bool ok = live && ph >= 0 && pw >= 0;
     if (d.stride == 2) {
-      if ((ph | pw) & 1) continue;
+      ok = ok && !((ph | pw) & 1);
       ph >>= 1; pw >>= 1;
     }
-    if (ph >= d.P || pw >= d.Q) continue;
-    const T* row = dy + ph * t.as[2] + pw * t.as[3];
+    ok = ok && ph < d.P && pw < d.Q;
+    // clamped tap (row 0) and a select instead of a branch: the taps' loads issue together
+    const T* row = dy + (ok ? ph * t.as[2] + pw * t.as[3] : 0);
     const float* wr = wf + j * d.K + l * VN;
     if constexpr (VN == 8) {
       float v[8];
       ld8<T>(row, v);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc += v[e] * wr[e];
+      for (int e = 0; e < 8; ++e) acc += (ok ? v[e] : 0.f) * wr[e];
     } else {
       const float4 v = *(const float4*)row;
-      acc += v.x * wr[0] + v.y * wr[1] + v.z * wr[2] + v.w * wr[3];
+      if (ok) acc += v.x * wr[0] + v.y * wr[1] + v.z * wr[2] + v.w * wr[3];
     }
   }
   for (int o = LP >> 1; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
@@ -209,17 +212,17 @@ __global__ void __launch_bounds__(NT) k1_fwd(Thin t, int LP) {
 #pragma unroll
   for (int j = 0; j < RS; ++j) {
     const int hu = p - d.pad + j / d.S, wu = q - d.pad + j % d.S;
-    if (!live || hu < 0 || hu >= d.H || wu < 0 || wu >= d.W) continue;
-    const T* px = x + hu * t.as[2] + wu * t.as[3];
+    const bool ok = live && hu >= 0 && hu < d.H && wu >= 0 && wu < d.W;
+    const T* px = x + (ok ? hu * t.as[2] + wu * t.as[3] : 0);   // clamped: the taps' loads issue together
     const float* pw = wf + j * d.C + l * VN;
     if constexpr (VN == 8) {
       float v[8];
       ld8<T>(px, v);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s += v[e] * pw[e];
+      for (int e = 0; e < 8; ++e) s += (ok ? v[e] : 0.f) * pw[e];
     } else {
       const float4 v = *(const float4*)px;
-      s += v.x * pw[0] + v.y * pw[1] + v.z * pw[2] + v.w * pw[3];
+      if (ok) s += v.x * pw[0] + v.y * pw[1] + v.z * pw[2] + v.w * pw[3];
     }
   }
   for (int o = LP >> 1; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
@@ -252,8 +255,9 @@ __global__ void __launch_bounds__(NT) k1_dgrad(Thin t, int LP) {
 #pragma unroll
   for (int j = 0; j < RS; ++j) {
     const int ph = h + d.pad - j / d.S, pw = w + d.pad - j % d.S;
-    if (ph < 0 || pw < 0 || ph >= d.P || pw >= d.Q) continue;
-    const float g = to_f(dy[ph * t.as[2] + pw * t.as[3]]);
+    const bool ok = ph >= 0 && pw >= 0 && ph < d.P && pw < d.Q;
+    const float gv = to_f(dy[ok ? ph * t.as[2] + pw * t.as[3] : 0]);   // clamped, then select
+    const float g = ok ? gv : 0.f;
     const float* wr = wf + j * d.C + l * VN;
 #pragma unroll
     for (int e = 0; e < VN; ++e) acc[e] += g * wr[e];
@@ -297,16 +301,17 @@ __global__ void __launch_bounds__(NT) k1_wgrad(Thin t, int LP) {
 #pragma unroll
     for (int j = 0; j < RS; ++j) {
       const int hu = p - d.pad + j / d.S, wu = q - d.pad + j % d.S;
-      if (hu < 0 || hu >= d.H || wu < 0 || wu >= d.W) continue;
-      const T* px = x + hu * t.bs[2] + wu * t.bs[3];
+      const bool ok = hu >= 0 && hu < d.H && wu >= 0 && wu < d.W;
+      const T* px = x + (ok ? hu * t.bs[2] + wu * t.bs[3] : 0);   // clamped: loads issue together
+      const float gj = ok ? g : 0.f;
       if constexpr (VN == 8) {
         float v[8];
         ld8<T>(px, v);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[j][e] += g * v[e];
+        for (int e = 0; e < 8; ++e) acc[j][e] += gj * v[e];
       } else {
         const float4 v = *(const float4*)px;
-        acc[j][0] += g * v.x; acc[j][1] += g * v.y; acc[j][2] += g * v.z; acc[j][3] += g * v.w;
+        acc[j][0] += gj * v.x; acc[j][1] += gj * v.y; acc[j][2] += gj * v.z; acc[j][3] += gj * v.w;
       }
     }
   }
