@@ -97,6 +97,7 @@ _SIGS = {
     "es_sn_bwd": (C.c_int, [P, P, C.c_int, C.c_int, P, P, P, P, C.c_float, P]),
     "es_hinge_d": (C.c_int, [P, P, C.c_int, P, P, P, P, P]),
     "es_image_expsum": (C.c_int, [P, C.c_int, P, P, P]),
+    "es_channel_sums": (C.c_int, [P, C.c_int, P, C.c_int, P, P]),
     "es_gen_losses": (C.c_int, [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "es_image_expsum_bwd": (C.c_int, [P, C.c_int, P, P, P, P, C.c_float, P]),
     "es_router_gumbel": (C.c_int, [P, P, C.c_int, C.c_int, C.c_float, P, P, P, P]),

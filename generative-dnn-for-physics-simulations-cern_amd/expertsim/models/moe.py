@@ -294,10 +294,38 @@ class MoEWrapper(nn.Module):
         opt_a.step()
 
     # ---------------------------------------------------------------------------- evaluation
+    # generator batch of the evaluation (the reference uses 64, train/utils.py:118; eval-mode
+    # outputs are per-sample, so the batch only sets how many images one HIP program covers)
+    eval_batch_size = 1024
+
     @torch.no_grad()
     def evaluate(self, epoch, y_test, x_test, true_positions, std, intensity, cfg, device):
-        from ..train.evaluation import evaluate_moe
-        return evaluate_moe(self, epoch, y_test, x_test, cfg, device)
+        """Wasserstein metrics of one test batch — reference moe.py:644-692.
+
+        Real 5-channel sums: expm1 + masked sums of x_test on the device (es_channel_sums, one pass).
+        Routing: the router with its stochastic Gumbel at tau=1 (moe.py:650), argmax.
+        Generated sums: each expert's generator in eval mode over its routed conditions, images kept
+        in HBM and reduced by the same kernel; WS distances on the host (train/utils.py:117-176).
+        Returns {'ws_mean', 'ws_std', 'ws_mean_i', 'ws_std_i', 'epoch'}."""
+        from ..train.utils import calculate_joint_ws_across_experts, channel_sums
+        shape = tuple(cfg.dataset.input_image_shape)
+        x = x_test if isinstance(x_test, torch.Tensor) else torch.as_tensor(np.asarray(x_test))
+        x = x.reshape(-1, *shape)
+        ch_org_dev = channel_sums(x.to(device, dtype=torch.float32), log_domain=True)
+        y = y_test.to(device) if isinstance(y_test, torch.Tensor) else torch.as_tensor(y_test, device=device)
+        soft_gates, _ = self.router(y.float())
+        pred = torch.argmax(soft_gates, 1).cpu().numpy()
+        ch_org = ch_org_dev.cpu().numpy()
+        idx = [np.where(pred == i)[0] for i in range(self.n_experts)]
+        ch_org_experts = [ch_org[ix] if len(ix) else np.zeros((0, 5)) for ix in idx]
+        idx_dev = [torch.as_tensor(ix, device=device, dtype=torch.long) for ix in idx]
+        ws_mean, ws_std, ws_mean_exp, ws_std_exp = calculate_joint_ws_across_experts(
+            min(epoch // 5 + 1, 5), [x[ix] for ix in idx], [y[ix] for ix in idx_dev], list(self.generators),
+            ch_org, ch_org_experts, self.noise_dim, device, batch_size=self.eval_batch_size,
+            n_experts=self.n_experts, shape_images=shape)
+        log = {"ws_mean": ws_mean, **{f"ws_mean_{i}": ws_mean_exp[i] for i in range(self.n_experts)},
+               "ws_std": ws_std, **{f"ws_std_{i}": ws_std_exp[i] for i in range(self.n_experts)}, "epoch": epoch}
+        return log
 
     def get_expert_assignment_counts(self, expert_assignments: torch.Tensor) -> torch.Tensor:
         counts = torch.bincount(expert_assignments.long(), minlength=self.n_experts).float()

@@ -4,8 +4,8 @@ Same entry points (``train``, ``train_epoch``, ``train_step``, ``setup_moe_syste
 step is ``MoEWrapper.train_step`` on the HIP path.  Metrics are fetched to the host once per batch
 (the reference does ``.cpu().item()`` per key, loop.py:136-148).  With WORLD_SIZE > 1 (torchrun),
 every rank trains on its own shard and gradients are all-reduced over RCCL (expertsim/train/ddp.py).
-Evaluation (Wasserstein metrics), plotting, W&B and checkpoint callbacks are outside the hot-path
-scope of this build; ``evaluate_epoch`` is skipped when no test loader is given.
+``evaluate_epoch`` (loop.py:185-256) produces the Wasserstein metrics of MoEWrapper.evaluate on the
+HIP path; plotting, W&B and checkpoint callbacks stay out of scope.
 """
 from __future__ import annotations
 
@@ -66,6 +66,23 @@ def train_epoch(moe, train_loader, gen_optims, disc_optims, aux_reg_optims, rout
     return out
 
 
+@torch.no_grad()
+def evaluate_epoch(moe, test_loader, epoch: int, cfg, device, max_batches=None) -> Dict:
+    """Reference loop.py:185-256 without the plots: per-batch MoEWrapper.evaluate, averaged."""
+    moe.eval()
+    keys = ["ws_mean", *[f"ws_mean_{i}" for i in range(moe.n_experts)],
+            "ws_std", *[f"ws_std_{i}" for i in range(moe.n_experts)]]
+    acc: Dict[str, List[float]] = {k: [] for k in keys}
+    for b, batch in enumerate(test_loader):
+        if max_batches is not None and b >= max_batches:
+            break
+        real_images, _, cond, std, intensity, true_positions = batch
+        m = moe.evaluate(epoch, cond.to(device), real_images, true_positions, std, intensity, cfg, device)
+        for k in keys:
+            acc[k].append(float(m[k]))
+    return {k: (sum(v) / len(v) if v else 0.0) for k, v in acc.items()}
+
+
 def train(cfg, train_loader, test_loader=None, max_steps_per_epoch=None) -> List[Dict]:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -90,6 +107,8 @@ def train(cfg, train_loader, test_loader=None, max_steps_per_epoch=None) -> List
         t0 = time.time()
         metrics = train_epoch(moe, train_loader, gen_optims, disc_optims, aux_optims, router_optim, cfg, device,
                               epoch, None, max_steps=max_steps_per_epoch)
+        if test_loader is not None:
+            metrics.update(evaluate_epoch(moe, test_loader, epoch, cfg, device))
         metrics["epoch_time"] = time.time() - t0
         metrics["epoch"] = epoch
         history.append(metrics)

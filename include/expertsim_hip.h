@@ -329,6 +329,15 @@ int es_counter_add(int32_t* counter, int32_t v, es_stream_t stream);
 /* dropout mask materialisation (tests): out[i] = keep(i) */
 int es_dropout_mask(uint8_t* out, int64_t n, const es_dropout_t* d, es_stream_t stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Evaluation (moe.py:644-692).
+ * ---------------------------------------------------------------------------------------- */
+/* 5-channel photon sums of x [n,1,h,w] (any strides): out[b*5 + k] (fp64) = sum over mask k+1 of
+ * get_channel_masks (train/utils.py:18-59) as sum_channels_parallel (train/utils.py:62-78)
+ * computes it; log_domain != 0 applies expm1 first (moe.py:646, train/utils.py:198). */
+int es_channel_sums(const es_view_t* x, es_dtype_t dt, const void* xp, int log_domain, double* out,
+                    es_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -16,6 +16,9 @@ What it restates (reference file:line, /root/reference):
     generator_train_step (529-571), sdi_gan_regularization (573-588),
     intensity_regularization (590-642) and the router losses of train/utils.py:372-419,623-642
   * torch.optim.Adam single-tensor update (training_setup.py:12-41 creates them)
+  * evaluation: channel masks / 5-channel sums (train/utils.py:18-78),
+    the 1-D Wasserstein distance scipy computes (scipy.stats.wasserstein_distance, restated in
+    numpy) and the joint-WS aggregation (train/utils.py:117-176); pinned by tests/golden/eval_*.npz
 Gradients come from torch autograd on these functional graphs.
 
 Randomness is injected: generator noise and Gumbel exponentials are passed in; dropout masks
@@ -555,3 +558,66 @@ DEFAULT_CFG = dict(noise_dim=10, cond_dim=9, lr_g=1e-4, lr_d=1e-5, lr_a=1e-4, lr
                    gan_strength=0.1, diff_strength=1e-6, util_strength=0.0, alb_strength=1e-5,
                    stop_router_training_epoch=40, alpha=60, min_weight=0.2, tau_start=1.2,
                    tau_min=0.8, tau_decay=0.985)
+
+
+# --------------------------------------------------------------------------------------------
+# evaluation
+# --------------------------------------------------------------------------------------------
+def channel_masks(h, w):
+    """train/utils.py:18-59, as loops over the pattern [[0,1],[1,0]] and the four quadrants."""
+    mask = np.zeros((h, w), dtype=np.float64)
+    for i in range(h):
+        for j in range(w):
+            mask[i, j] = (0, 1)[j % 2] if i % 2 == 0 else (1, 0)[j % 2]
+    mask5 = 1.0 - mask
+    mr, mc = h // 2, w // 2
+    m1, m2, m3, m4 = mask.copy(), mask.copy(), mask.copy(), mask.copy()
+    m4[mr:, :] = 0
+    m4[:, :mc] = 0
+    m2[:, :mc] = 0
+    m2[:mr, :] = 0
+    m3[mr:, :] = 0
+    m3[:, mc:] = 0
+    m1[:, mc:] = 0
+    m1[:mr, :] = 0
+    return m1, m2, m3, m4, mask5
+
+
+def channel_sums(images):
+    """train/utils.py:62-78 in float64: [N,H,W] -> [N,5]."""
+    x = np.asarray(images, dtype=np.float64)
+    ms = channel_masks(x.shape[1], x.shape[2])
+    return np.stack([(x * m).sum(axis=(1, 2)) for m in ms], axis=1)
+
+
+def wasserstein_1d(u, v):
+    """First Wasserstein distance of two 1-D empirical distributions, as scipy.stats computes it
+    (_cdf_distance with p=1): integral of |F_u - F_v| over the merged sorted support."""
+    u = np.asarray(u, dtype=np.float64)
+    v = np.asarray(v, dtype=np.float64)
+    us, vs = np.sort(u), np.sort(v)
+    allv = np.sort(np.concatenate([u, v]))
+    d = np.diff(allv)
+    cu = np.searchsorted(us, allv[:-1], "right") / u.size
+    cv = np.searchsorted(vs, allv[:-1], "right") / v.size
+    return float(np.sum(np.abs(cu - cv) * d))
+
+
+def joint_ws(ch_org, ch_org_exp, ch_gen_runs):
+    """train/utils.py:117-176 aggregation.  ch_gen_runs[j][e] = [n_e,5] generated sums of expert e
+    in repetition j (empty for an expert with no samples)."""
+    n_calc, E = len(ch_gen_runs), len(ch_gen_runs[0])
+    ws = np.zeros((n_calc, 5))
+    ws_exp = np.zeros((n_calc, E, 5))
+    for j in range(n_calc):
+        live = [g for g in ch_gen_runs[j] if len(g)]
+        allg = np.concatenate(live) if live else np.zeros((0, 5))
+        for i in range(5):
+            ws[j, i] = wasserstein_1d(ch_org[:, i], allg[:, i])
+            for e in range(E):
+                if len(ch_gen_runs[j][e]) == 0 or len(ch_org_exp[e]) == 0:
+                    continue
+                ws_exp[j, e, i] = wasserstein_1d(ch_org_exp[e][:, i], ch_gen_runs[j][e][:, i])
+    r = ws.mean(axis=1)
+    re = ws_exp.mean(axis=2)
+    return r.mean(), r.std(), re.mean(axis=0), re.std(axis=0)
