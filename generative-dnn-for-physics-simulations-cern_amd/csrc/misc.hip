@@ -456,6 +456,26 @@ __global__ void adam_dev_kernel(float* __restrict__ p, const float* __restrict__
 }
 __global__ void counter_add_kernel(int32_t* c, int32_t v) { c[0] += v; }
 
+// EMA of a flat parameter buffer (EMAHelper.update, loop.py:392-400): s = decay*s + (1-decay)*p with
+// the reference's two roundings and one add (contraction off: no FMA), float4 when aligned.
+__global__ void ema_kernel(float* __restrict__ s, const float* __restrict__ p, int64_t n, float d, float omd) {
+#pragma clang fp contract(off)
+  const int64_t n4 = ((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(p)) & 15) ? 0 : n / 4;
+  GRID_STRIDE(i, n4) {
+    float4 a = reinterpret_cast<const float4*>(s)[i];
+    const float4 b = reinterpret_cast<const float4*>(p)[i];
+    a.x = d * a.x + omd * b.x;
+    a.y = d * a.y + omd * b.y;
+    a.z = d * a.z + omd * b.z;
+    a.w = d * a.w + omd * b.w;
+    reinterpret_cast<float4*>(s)[i] = a;
+  }
+  GRID_STRIDE(j, n - 4 * n4) {
+    const int64_t i = 4 * n4 + j;
+    s[i] = d * s[i] + omd * p[i];
+  }
+}
+
 // ------------------------------------------------------------------------------------ RNG
 __global__ void randn_kernel(float* out, int64_t n, uint64_t seed, uint32_t sid, const int32_t* step_ptr,
                              int32_t step_mul) {
@@ -637,6 +657,16 @@ extern "C" int es_adam_dev(float* p, const float* g, float* m, float* v, int64_t
   if (n == 0) return ES_OK;
   hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr, beta1,
                      beta2, eps, step_ptr, grad_scale);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_ema_update(float* shadow, const float* p, int64_t n, float decay, float one_minus_decay,
+                             es_stream_t stream) {
+  ES_CHECK_ARG(n >= 0, "ema_update: n < 0");
+  if (n == 0) return ES_OK;
+  hipLaunchKernelGGL(ema_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, shadow, p, n, decay,
+                     one_minus_decay);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }

@@ -105,6 +105,7 @@ _SIGS = {
     "es_adam": (C.c_int, [P, P, P, P, I64, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int,
                           C.c_float, P]),
     "es_adam_dev": (C.c_int, [P, P, P, P, I64, C.c_float, C.c_float, C.c_float, C.c_float, P, C.c_float, P]),
+    "es_ema_update": (C.c_int, [P, P, I64, C.c_float, C.c_float, P]),
     "es_randn": (C.c_int, [P, I64, C.c_uint64, C.c_uint32, P]),
     "es_rand_exponential": (C.c_int, [P, I64, C.c_uint64, C.c_uint32, P]),
     "es_randn_dev": (C.c_int, [P, I64, C.c_uint64, C.c_uint32, P, C.c_int32, P]),

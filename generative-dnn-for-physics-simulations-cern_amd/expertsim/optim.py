@@ -61,6 +61,31 @@ class FusedAdam(torch.optim.Optimizer):
         self.module.invalidate()
         return None
 
+    # ------------------------------------------------------------------ checkpointing
+    def state_dict(self):
+        """Flat form: {'step', 'exp_avg' [P], 'exp_avg_sq' [P], 'param_groups'} (host copies); loadable
+        with torch.load(weights_only=True)."""
+        self.sync_step()
+        flat = self._buffers()
+        return {"step": int(self._step), "numel": int(flat.numel()),
+                "exp_avg": self._m.detach().cpu().clone(), "exp_avg_sq": self._v.detach().cpu().clone(),
+                "param_groups": [{k: (list(v) if isinstance(v, tuple) else v) for k, v in g.items() if k != "params"}
+                                 for g in self.param_groups]}
+
+    def load_state_dict(self, sd):
+        flat = self._buffers()
+        if int(sd["numel"]) != flat.numel():
+            raise ValueError(f"FusedAdam.load_state_dict: {sd['numel']} moments for {flat.numel()} parameters")
+        self._m.copy_(sd["exp_avg"].to(flat.device))
+        self._v.copy_(sd["exp_avg_sq"].to(flat.device))
+        for g, src in zip(self.param_groups, sd["param_groups"]):
+            g.update({k: (tuple(v) if k == "betas" else v) for k, v in src.items()})
+        self._step = int(sd["step"])
+        if self._dstep is not None:          # keep the pointer a captured graph reads
+            self._dstep.fill_(self._step)
+        for p in self.module.parameters():
+            self.state[p]["step"] = torch.tensor(float(self._step))
+
     def sync_step(self):
         """Host step := device step (after replays of a captured train step)."""
         if self._dstep is not None:

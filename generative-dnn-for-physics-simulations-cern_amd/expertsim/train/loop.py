@@ -5,7 +5,9 @@ step is ``MoEWrapper.train_step`` on the HIP path.  Metrics are fetched to the h
 (the reference does ``.cpu().item()`` per key, loop.py:136-148).  With WORLD_SIZE > 1 (torchrun),
 every rank trains on its own shard and gradients are all-reduced over RCCL (expertsim/train/ddp.py).
 ``evaluate_epoch`` (loop.py:185-256) produces the Wasserstein metrics of MoEWrapper.evaluate on the
-HIP path; plotting, W&B and checkpoint callbacks stay out of scope.
+HIP path.  Checkpoints (hooks.CheckpointSaver, training_utils) and the
+EMAHelper (ema.py) follow loop.py:36-107,357-418; resume restores weights, optimizer moments and
+the step counters.  Plotting and W&B stay out of scope.
 """
 from __future__ import annotations
 
@@ -19,7 +21,10 @@ import torch
 
 from ..models import build_model
 from ..models.moe import MoEWrapper
+from .ema import EMAHelper
+from .hooks import CheckpointSaver
 from .training_setup import setup_optimizers
+from .training_utils import load_checkpoint
 
 logger = logging.getLogger(__name__)
 
@@ -45,6 +50,27 @@ def train_step(batch, moe, gen_optims, disc_optims, aux_reg_optim, router_optim,
                           router_optim, ema_helper, device)
 
 
+def setup_callbacks(cfg, moe, ema_helper=None) -> List:
+    """loop.py:357-375 (the W&B logger is out of scope)."""
+    callbacks = []
+    cfg.generator_name = getattr(moe.generators[0], "name", "generator")
+    cfg.discriminator_name = getattr(moe.discriminators[0], "name", "discriminator")
+    cfg.router_name = getattr(moe.router, "name", "router")
+    if cfg.train.get("save_experiment_data", False):
+        callbacks.append(CheckpointSaver(dir_path=_dir_models(cfg), monitor="ws_mean",
+                                         ws_threshold=cfg.train.ws_threshold_model_save, ema_helper=ema_helper))
+    return callbacks
+
+
+def _dir_models(cfg):
+    d = cfg.train.get("dir_models")
+    if d is None:
+        exp = cfg.get_path("config.experiment_dir") or os.path.join(cfg.train.get("save_experiments_dir") or "",
+                                                                     cfg.config.get("run_name", "experiment"))
+        d = cfg.train.dir_models = f"{exp}/models/"
+    return d
+
+
 def train_epoch(moe, train_loader, gen_optims, disc_optims, aux_reg_optims, router_optim, cfg, device, epoch,
                 ema_helper, max_steps=None) -> Dict:
     moe.train()
@@ -54,6 +80,8 @@ def train_epoch(moe, train_loader, gen_optims, disc_optims, aux_reg_optims, rout
             break
         m = train_step(batch, moe, gen_optims, disc_optims, aux_reg_optims, router_optim, cfg, device, epoch,
                        ema_helper)
+        if ema_helper is not None and cfg.train.get("ema_update", False):
+            ema_helper.update(moe, range(moe.n_experts))     # build extension: the reference never updates
         keys = list(m)
         vals = torch.stack([torch.as_tensor(m[k], dtype=torch.float32, device=device).reshape(())
                             for k in keys]).cpu().numpy()   # ONE device->host copy per batch
@@ -101,14 +129,26 @@ def train(cfg, train_loader, test_loader=None, max_steps_per_epoch=None) -> List
         moe.ddp = DataParallel()
         moe.rank = dist.get_rank()
     gen_optims, disc_optims, aux_optims, router_optim = setup_optimizers(moe, cfg)
+    ema_helper = EMAHelper(moe, decay=0.99)                 # loop.py:44
     history = []
-    start = 0 if cfg.train.get("epoch_to_load") is None else int(cfg.train.epoch_to_load)
+    start = 0
+    ckpt_dir, ckpt_epoch = cfg.train.get("checkpoint_experiment_dir"), cfg.train.get("epoch_to_load")
+    if (ckpt_dir is None) != (ckpt_epoch is None):
+        raise ValueError("You should set both checkpoint_experiment_dir and epoch_to_load parameters!")
+    if ckpt_dir is not None:
+        load_checkpoint(os.path.join(ckpt_dir, "models"), int(ckpt_epoch), moe, gen_optims, disc_optims, aux_optims,
+                        router_optim, ema_helper, device)
+        start = int(ckpt_epoch) + 1
+    callbacks = setup_callbacks(cfg, moe, ema_helper if cfg.train.get("ema_update", False) else None)
     for epoch in range(start, int(cfg.train.epochs)):
         t0 = time.time()
         metrics = train_epoch(moe, train_loader, gen_optims, disc_optims, aux_optims, router_optim, cfg, device,
-                              epoch, None, max_steps=max_steps_per_epoch)
+                              epoch, ema_helper, max_steps=max_steps_per_epoch)
         if test_loader is not None:
             metrics.update(evaluate_epoch(moe, test_loader, epoch, cfg, device))
+        for cb in callbacks:
+            if moe.rank == 0:
+                cb.on_epoch_end(epoch, metrics, moe, gen_optims, disc_optims, aux_optims, router_optim)
         metrics["epoch_time"] = time.time() - t0
         metrics["epoch"] = epoch
         history.append(metrics)

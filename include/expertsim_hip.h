@@ -326,6 +326,10 @@ int es_rand_exponential_dev(float* out, int64_t n, uint64_t seed, uint32_t strea
                             const int32_t* step_ptr, int32_t step_mul, es_stream_t stream);
 /* counter[0] += v on the device (step counters of a captured train step). */
 int es_counter_add(int32_t* counter, int32_t v, es_stream_t stream);
+/* EMA of a flat parameter buffer — replaces EMAHelper.update (expertsim/train/loop.py:392-400):
+ * shadow[i] = decay*shadow[i] + one_minus_decay*p[i], each product rounded, then one add. */
+int es_ema_update(float* shadow, const float* p, int64_t n, float decay, float one_minus_decay,
+                  es_stream_t stream);
 /* dropout mask materialisation (tests): out[i] = keep(i) */
 int es_dropout_mask(uint8_t* out, int64_t n, const es_dropout_t* d, es_stream_t stream);
 
