@@ -29,11 +29,18 @@ class DataParallel:
         self.rank = rank if rank is not None else dist.get_rank(group)
         self._counts = None
         self.local_batch = None
+        self._counts_dev = {}
 
     # ---------------------------------------------------------------- routing bookkeeping
     def global_groups(self, groups, B_local):
         """All-reduce the per-expert counts (one small collective) and keep local groups."""
         E = len(groups)
+        self.local_batch = B_local
+        if E == 1:
+            # one expert holds every sample: its global count is the global batch (equal shards,
+            # as DistributedSampler(drop_last=True) and bench.py give) -- no collective, no host sync
+            self._counts = np.array([B_local * self.world], dtype=np.int64)
+            return groups
         local = torch.tensor([g[2] for g in groups], dtype=torch.int64)
         dev = "cuda" if dist.get_backend(self.group) == "nccl" else "cpu"
         t = local.to(dev)
@@ -50,7 +57,11 @@ class DataParallel:
         return self.local_batch * self.world
 
     def global_counts_tensor(self, device):
-        return torch.from_numpy(self._counts.astype(np.float32)).to(device)
+        # cached per value: no host->device copy inside a captured step
+        key = (str(device), tuple(int(c) for c in self._counts))
+        if key not in self._counts_dev:
+            self._counts_dev[key] = torch.from_numpy(self._counts.astype(np.float32)).to(device)
+        return self._counts_dev[key]
 
     # ---------------------------------------------------------------- gradients
     def allreduce_grads(self, module):
