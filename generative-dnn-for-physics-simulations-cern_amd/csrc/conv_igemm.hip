@@ -40,6 +40,8 @@ namespace {
 
 // ES_NO_GLDS=1 (or es_conv_set_glds(0)) forces the register-staged kernels (A/B measurement)
 bool g_no_glds = [] { const char* e = getenv("ES_NO_GLDS"); return e && e[0] == '1'; }();
+// ES_NARROW_TILES=0 restores 64 x 64 tiles for the narrow fp32 GEMMs (A/B switch)
+bool g_narrow_tiles = [] { const char* e = getenv("ES_NARROW_TILES"); return !(e && e[0] == '0'); }();
 
 constexpr int KSTEP_BYTES = 128;               // operand bytes per row per K-step
 constexpr int ROW_BYTES = KSTEP_BYTES + 16;    // padded LDS row
@@ -883,7 +885,13 @@ int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
   // 128 x 128 only with enough tiles to fill the chip: a small GEMM (the discriminator / router /
   // aux linears at batch 512) is latency-bound per K-step, so more, smaller workgroups finish sooner
   const bool big = a.M >= 128 && a.Ng >= 96 && !splitk_case && tiles128 >= 128;
-  const int BM = big ? 128 : 64, BN = big ? 128 : 64;
+  // narrow fp32 GEMMs (the discriminator's 32->16 conv: FWD / DGRAD with N <= 32, WGRAD with
+  // M = 16 output channels): a 64 x 64 tile wastes half or 3/4 of every MFMA; 128 x 32 and
+  // 32 x 128 tiles keep the 2 x 2 wave grid with one 16-row (column) fragment per wave
+  const bool narrow_n = sizeof(T) == 4 && g_narrow_tiles && MODE != MODE_WGRAD && a.Ng <= 32 && !splitk_case;
+  const bool narrow_m = sizeof(T) == 4 && g_narrow_tiles && MODE == MODE_WGRAD && a.M <= 32 && !big;
+  const int BM = big ? 128 : (narrow_n ? 128 : (narrow_m ? 32 : 64));
+  const int BN = big ? 128 : (narrow_n ? 32 : (narrow_m ? 128 : 64));
   if constexpr (sizeof(T) == 2 && MODE == MODE_WGRAD) {
     if (avec && bvec && !g_no_glds && es_conv_ring_launch(a, MODE, st)) {
       ES_CHECK_LAUNCH();
@@ -931,6 +939,13 @@ int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
     }
   }
   if (big) return launch_tile<T, MODE, 128, 128>(a, avec, bvec, st, splits);
+  if constexpr (sizeof(T) == 4) {
+    if constexpr (MODE != MODE_WGRAD) {
+      if (narrow_n) return launch_tile<T, MODE, 128, 32>(a, avec, bvec, st, splits);
+    } else {
+      if (narrow_m) return launch_tile<T, MODE, 32, 128>(a, avec, bvec, st, splits);
+    }
+  }
   return launch_tile<T, MODE, 64, 64>(a, avec, bvec, st, splits);
 }
 

@@ -20,6 +20,8 @@ gradients of every optimizer phase are all-reduced (RCCL) before the fused Adam.
 """
 from __future__ import annotations
 
+import os
+
 import copy
 import ctypes as C
 from itertools import combinations
@@ -79,8 +81,9 @@ class MoEWrapper(nn.Module):
             m.compute_dtype = low
         for m in self.aux_regs:
             m.compute_dtype = low
+        d_low = low if os.environ.get("ES_D_BF16", "0") == "1" else torch.float32
         for m in self.discriminators:
-            m.compute_dtype = torch.float32
+            m.compute_dtype = d_low
 
     # ---------------------------------------------------------------------------- helpers
     def _noise(self, expert, which, shape, device):

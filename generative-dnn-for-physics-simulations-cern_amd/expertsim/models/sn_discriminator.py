@@ -125,14 +125,18 @@ class SNDiscriminator(ExpertModule):
         B = img.dims[0]
         lr = hip.chain_struct(hip.ACT_LRELU, SLOPE)
         x = img
-        if img.t.dtype != cdt:
+        front = self.front_fused(img)               # the fused front reads the fp32 image directly
+        if img.t.dtype != cdt and not front:
             x = img.like_nhwc(cdt)
             copy_act(img, x)
         sig = {n: o["sn:" + n].sigma(update=train) for n in LAYERS}
         inv = lambda n: sig[n][0]
-        front = self.front_fused(x)
         if front:
             p1, i1, s1 = self.front_fwd(x, inv("conv_layers.0"))
+            if p1.t.dtype != cdt:                   # bf16 mode: the GEMM layers after the front
+                p1c = p1.like_nhwc(cdt)
+                copy_act(p1, p1c)
+                p1 = p1c
             h1 = y1 = None
         else:
             h1 = o["conv_layers.0"].fwd(x, inv_scale=inv("conv_layers.0"))
@@ -214,7 +218,8 @@ class SNDiscriminator(ExpertModule):
                            dbeta=m("conv_layers.5").bias.grad if weight_grads else None,
                            dsum=bias_g("conv_layers.4"))
         wgrad("conv_layers.4", dh2, ctx["p1"])
-        dp1 = o["conv_layers.4"].dgrad(dh2, ctx["p1"], inv_scale=sig["conv_layers.4"][0])
+        dp1 = o["conv_layers.4"].dgrad(dh2, ctx["p1"], inv_scale=sig["conv_layers.4"][0],
+                                       dx_dtype=torch.float32 if ctx["front"] else None)
         if ctx["front"]:
             return self.front_bwd(ctx, dp1, weight_grads, input_grad)
         dy1 =o["pool1"].bwd(dp1, ctx["i1"], ctx["y1"].dims, cdt)

@@ -50,6 +50,8 @@ CONV_CASES = [
     (2, 1, 20, 18, 16, 3, 2, 1, None),            # Cin = 1 direct path, stride 2, pad 1, K = 16
     (2, 64, 55, 29, 1, 2, 1, 1, None),            # proton G conv_layers.11 (Cout = 1, pad 1)
     (2, 32, 21, 21, 16, 3, 1, 0, None),           # D conv_layers.4
+    (37, 32, 21, 21, 16, 3, 1, 0, None),          # same, many 128x32 / 32x128 tiles and K splits
+    (5, 24, 11, 9, 8, 3, 1, 1, None),             # narrow tiles with ragged M / N / K
     (2, 1, 56, 30, 32, 5, 2, 1, None),            # proton A conv1 (stride 2, pad 1)
     (2, 32, 26, 13, 32, 5, 2, 2, None),           # proton A res conv1
     (2, 32, 26, 13, 64, 1, 2, 0, None),           # proton A downsample 1x1 s2
