@@ -338,10 +338,13 @@ __global__ void __launch_bounds__(NT) k1_wgrad(Thin t, int LP) {
 // The discriminator's conv_layers.4 (32 -> 16, 3x3, fp32: neutron/discriminator.py:16): as a GEMM
 // its N = 16 fills a quarter of every tile.  Direct forward: one thread per output pixel with KO
 // accumulators, weights in LDS.  (A direct dgrad measured slower than the GEMM; not used.)
-template <int KO>
+// CC > 0: the channel count is a compile-time constant, so each tap's CC/4 float4 loads are issued
+// together before its FMAs (the runtime-C loop waited on one load per 4 channels: 72 dependent
+// global round trips per thread, 69 us per call at B = 512; latency-bound, not FMA-bound).
+template <int KO, int CC>
 __global__ void __launch_bounds__(NT) small_fwd(Thin t) {
   const es_conv_desc_t& d = t.d;
-  const int RS = d.R * d.S, C = d.C;
+  const int RS = d.R * d.S, C = CC > 0 ? CC : d.C;
   __shared__ float wf[9 * 64 * KO];                       // [rs][c][k]
   __shared__ float bs[KO];
   for (int i = threadIdx.x; i < KO * RS * C; i += NT) {   // packed wk = [k][rs][c]
@@ -366,13 +369,27 @@ __global__ void __launch_bounds__(NT) small_fwd(Thin t) {
       if (wu < 0 || wu >= d.W) continue;
       const float* px = x + hu * t.as[2] + wu * t.as[3];
       const float* wr = wf + (r * d.S + s_) * C * KO;
-      for (int c = 0; c < C; c += 4) {
-        const float4 xv = *(const float4*)(px + c);
-        const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+      if constexpr (CC > 0) {
+        float4 xv[CC / 4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
+        for (int c4 = 0; c4 < CC / 4; ++c4) xv[c4] = *(const float4*)(px + 4 * c4);
 #pragma unroll
-          for (int k = 0; k < KO; ++k) acc[k] += xs[e] * wr[(c + e) * KO + k];
+        for (int c4 = 0; c4 < CC / 4; ++c4) {
+          const float xs[4] = {xv[c4].x, xv[c4].y, xv[c4].z, xv[c4].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int k = 0; k < KO; ++k) acc[k] += xs[e] * wr[(4 * c4 + e) * KO + k];
+        }
+      } else {
+        for (int c = 0; c < C; c += 4) {
+          const float4 xv = *(const float4*)(px + c);
+          const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int k = 0; k < KO; ++k) acc[k] += xs[e] * wr[(c + e) * KO + k];
+        }
       }
     }
   }
@@ -472,7 +489,11 @@ int es_thin_conv_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x, cons
     for (int i = 0; i < 4; ++i) { t.as[i] = xs[i]; t.os[i] = ys[i]; }
     t.M = d->N * d->P * d->Q;
     small_dispatch(d->K, [&](auto ko) {
-      hipLaunchKernelGGL((small_fwd<decltype(ko)::value>), dim3(blocks(t.M, NT)), dim3(NT), 0, st, t);
+      constexpr int KO = decltype(ko)::value;
+      if (d->C == 32)
+        hipLaunchKernelGGL((small_fwd<KO, 32>), dim3(blocks(t.M, NT)), dim3(NT), 0, st, t);
+      else
+        hipLaunchKernelGGL((small_fwd<KO, 0>), dim3(blocks(t.M, NT)), dim3(NT), 0, st, t);
     });
     return 1;
   }
