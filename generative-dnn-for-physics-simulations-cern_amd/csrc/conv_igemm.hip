@@ -42,6 +42,8 @@ namespace {
 bool g_no_glds = [] { const char* e = getenv("ES_NO_GLDS"); return e && e[0] == '1'; }();
 // ES_NARROW_TILES=0 restores 64 x 64 tiles for the narrow fp32 GEMMs (A/B switch)
 bool g_narrow_tiles = [] { const char* e = getenv("ES_NARROW_TILES"); return !(e && e[0] == '0'); }();
+// cap on the K splits of a narrow fp32 WGRAD (every split atomically adds the same M x N outputs)
+int g_narrow_wgrad_splits = [] { const char* e = getenv("ES_NARROW_WGRAD_SPLITS"); return e ? atoi(e) : 0; }();
 
 constexpr int KSTEP_BYTES = 128;               // operand bytes per row per K-step
 constexpr int ROW_BYTES = KSTEP_BYTES + 16;    // padded LDS row
@@ -919,6 +921,7 @@ int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
   a.splitk = 0;
   if (MODE == MODE_WGRAD) {
     int want = (2048 + tiles - 1) / tiles;            // ~2048 workgroups
+    if (narrow_m && g_narrow_wgrad_splits > 0) want = min(want, g_narrow_wgrad_splits);
     want = max(1, min(want, ksteps / 4 > 0 ? ksteps / 4 : 1));  // >= 4 K-steps per split
     const int per = ((ksteps + want - 1) / want) * BK;
     a.k_per_split = per;
