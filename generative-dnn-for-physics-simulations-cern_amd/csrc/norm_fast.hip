@@ -175,6 +175,37 @@ __device__ __forceinline__ float chain_bwd(const FastArgs& a, float z, float dou
   return dout * a.drop.scale * dactf(a, z);
 }
 
+// Chain specialised at compile time (CH, from the launch's KM template argument): the generic
+// chain branches on a.act / a.dfirst / a.drop.enabled per element, which left the Philox forward
+// with ~1100 basic blocks; the specialised forms are the same expressions without the branches.
+enum { CH_GEN = 0, CH_LRELU_DFIRST = 1, CH_LRELU_DLAST = 2 };
+template <int CH, bool DROP>
+__device__ __forceinline__ float chain_fwd_t(const FastArgs& a, float z, bool keep) {
+  if constexpr (CH == CH_GEN) {
+    return chain_fwd(a, z, keep);
+  } else if constexpr (!DROP) {
+    return lrelu(z, a.slope);
+  } else if constexpr (CH == CH_LRELU_DFIRST) {
+    return lrelu(keep ? z * a.drop.scale : 0.f, a.slope);
+  } else {
+    return keep ? lrelu(z, a.slope) * a.drop.scale : 0.f;
+  }
+}
+template <int CH, bool DROP>
+__device__ __forceinline__ float chain_bwd_t(const FastArgs& a, float z, float dout, bool keep) {
+  if constexpr (CH == CH_GEN) {
+    return chain_bwd(a, z, dout, keep);
+  } else if constexpr (!DROP) {
+    return dout * (z > 0.f ? 1.f : a.slope);
+  } else if constexpr (CH == CH_LRELU_DFIRST) {
+    if (!keep) return 0.f;
+    return dout * (z * a.drop.scale > 0.f ? 1.f : a.slope) * a.drop.scale;
+  } else {
+    if (!keep) return 0.f;
+    return dout * a.drop.scale * (z > 0.f ? 1.f : a.slope);
+  }
+}
+
 __device__ __forceinline__ int pow2_ceil(int v) {
   int p = 1;
   while (p < v) p <<= 1;
@@ -204,8 +235,9 @@ __device__ __forceinline__ Geo geo(const FastArgs& a) {
   return g;
 }
 
-template <typename T, int KM>
+template <typename T, int KMC>
 __global__ void __launch_bounds__(256) bn_fwd_fast(FastArgs a) {
+  constexpr int KM = KMC & 15, CH = KMC >> 4;
   resolve_stream(a.drop);
   const Geo g = geo(a);
   if (!g.active) return;
@@ -238,15 +270,17 @@ __global__ void __launch_bounds__(256) bn_fwd_fast(FastArgs a) {
     for (int j = 0; j < 4; ++j) {
       if (j >= nr) break;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[j][k] = chain_fwd(a, v[j][k] * sc[k] + sh[k], (keep[j] >> k) & 1u);
+      for (int k = 0; k < 8; ++k)
+        v[j][k] = chain_fwd_t<CH, KM != KM_NONE>(a, v[j][k] * sc[k] + sh[k], (keep[j] >> k) & 1u);
       st8<T>(y + (int64_t)(r0 + j) * a.C + g.c0, v[j]);
     }
   }
 }
 
 // MODE 0: Welford stats of x.  MODE 1: backward sums (sum dnorm, sum dnorm*xhat).
-template <typename T, int MODE, int KM>
+template <typename T, int MODE, int KMC>
 __global__ void __launch_bounds__(256) bn_reduce_fast(FastArgs a) {
+  constexpr int KM = KMC & 15, CH = KMC >> 4;
   resolve_stream(a.drop);
   const Geo g = geo(a);
   float s0[8], s1[8], s2[8];
@@ -300,7 +334,7 @@ __global__ void __launch_bounds__(256) bn_reduce_fast(FastArgs a) {
           const float* d = dd[j];
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
-            const float dn = chain_bwd(a, v[k] * sc[k] + sh[k], d[k], (keep[j] >> k) & 1u);
+            const float dn = chain_bwd_t<CH, KM != KM_NONE>(a, v[k] * sc[k] + sh[k], d[k], (keep[j] >> k) & 1u);
             const float xh = (v[k] - mu[k]) * is[k];
             s1[k] += dn;
             s2[k] += dn * xh;
@@ -348,8 +382,9 @@ __global__ void __launch_bounds__(256) bn_reduce_fast(FastArgs a) {
   }
 }
 
-template <typename T, int KM>
+template <typename T, int KMC>
 __global__ void __launch_bounds__(256) bn_bwd_apply_fast(FastArgs a) {
+  constexpr int KM = KMC & 15, CH = KMC >> 4;
   resolve_stream(a.drop);
   const Geo g = geo(a);
   float acc[8];
@@ -387,7 +422,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_fast(FastArgs a) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const float xh = (v[j][k] - mu[k]) * is[k];
-          const float dn = chain_bwd(a, xh * ga[k] + be[k], d[j][k], (keep[j] >> k) & 1u);
+          const float dn = chain_bwd_t<CH, KM != KM_NONE>(a, xh * ga[k] + be[k], d[j][k], (keep[j] >> k) & 1u);
           d[j][k] = is[k] * (dn * ga[k] - c1[k] - xh * c2[k]);
           acc[k] += d[j][k];
         }
@@ -459,7 +494,17 @@ static int keep_mode(const FastArgs& a, bool read_bits = false) {
   if (a.HW == 1 && (a.C & 3) == 0) return KM_ROW;
   return KM_GEN;
 }
-#define ES_KM_LAUNCH(K, T, KMV, grid, st, a) hipLaunchKernelGGL((K<T, KMV>), grid, dim3(256), 0, st, a)
+static int chain_kind(const FastArgs& a) {
+  if (a.act != ES_ACT_LRELU) return CH_GEN;
+  return a.dfirst ? CH_LRELU_DFIRST : CH_LRELU_DLAST;
+}
+#define ES_KM_LAUNCH(K, T, KMV, grid, st, a)                                                   \
+  do {                                                                                      \
+    const int ch_ = chain_kind(a);                                                          \
+    if (ch_ == CH_LRELU_DFIRST) hipLaunchKernelGGL((K<T, (KMV) | (CH_LRELU_DFIRST << 4)>), grid, dim3(256), 0, st, a); \
+    else if (ch_ == CH_LRELU_DLAST) hipLaunchKernelGGL((K<T, (KMV) | (CH_LRELU_DLAST << 4)>), grid, dim3(256), 0, st, a); \
+    else hipLaunchKernelGGL((K<T, KMV>), grid, dim3(256), 0, st, a);                        \
+  } while (0)
 #define ES_KM_DISPATCH(a, K, dt, grid, st, RB)                                             \
   do {                                                                                    \
     const int km_ = keep_mode(a, RB);                                                     \
@@ -477,7 +522,13 @@ static int keep_mode(const FastArgs& a, bool read_bits = false) {
       else ES_KM_LAUNCH(K, float, KM_GEN, grid, st, a);                                   \
     }                                                                                     \
   } while (0)
-#define ES_KM_LAUNCH1(K, T, KMV, grid, st, a) hipLaunchKernelGGL((K<T, 1, KMV>), grid, dim3(256), 0, st, a)
+#define ES_KM_LAUNCH1(K, T, KMV, grid, st, a)                                                  \
+  do {                                                                                      \
+    const int ch_ = chain_kind(a);                                                          \
+    if (ch_ == CH_LRELU_DFIRST) hipLaunchKernelGGL((K<T, 1, (KMV) | (CH_LRELU_DFIRST << 4)>), grid, dim3(256), 0, st, a); \
+    else if (ch_ == CH_LRELU_DLAST) hipLaunchKernelGGL((K<T, 1, (KMV) | (CH_LRELU_DLAST << 4)>), grid, dim3(256), 0, st, a); \
+    else hipLaunchKernelGGL((K<T, 1, KMV>), grid, dim3(256), 0, st, a);                     \
+  } while (0)
 #define ES_KM_DISPATCH1(a, K, dt, grid, st)                                                \
   do {                                                                                    \
     const int km_ = keep_mode(a, true);                                                   \
