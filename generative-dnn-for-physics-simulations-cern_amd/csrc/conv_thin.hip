@@ -203,7 +203,11 @@ __global__ void __launch_bounds__(NT) k1_fwd(Thin t, int LP) {
   for (int i = threadIdx.x; i < RS * d.C; i += NT) wf[i] = to_f(((const T*)t.w)[i]);   // [R][S][C]
   __syncthreads();
   const int PPB = NT / LP;
-  const int m = blockIdx.x * PPB + threadIdx.x / LP, l = threadIdx.x % LP;
+  const int l = threadIdx.x % LP;
+  // block-uniform grid-stride loop (the weights are staged once per block; the LP lanes of a
+  // pixel stay in step for the shuffle reduction)
+  for (int mb = blockIdx.x * PPB; mb < t.M; mb += gridDim.x * PPB) {
+  const int m = mb + threadIdx.x / LP;
   const bool live = m < t.M;
   int n, p, q;
   pix3(live ? m : 0, d.P, d.Q, n, p, q);
@@ -230,6 +234,7 @@ __global__ void __launch_bounds__(NT) k1_fwd(Thin t, int LP) {
     TO* y = (TO*)t.out + n * t.os[0] + p * t.os[2] + q * t.os[3];
     *y = from_f<TO>(s + (t.bias ? t.bias[0] : 0.f));
   }
+  }
 }
 
 // dgrad: dx[n,h,w,c] = sum over taps of dy[n, h+pad-r, w+pad-s] * w[c][r][s]   (wd = [C][R][S])
@@ -244,8 +249,8 @@ __global__ void __launch_bounds__(NT) k1_dgrad(Thin t, int LP) {
   }
   __syncthreads();
   const int PPB = NT / LP;
-  const int m = blockIdx.x * PPB + threadIdx.x / LP, l = threadIdx.x % LP;
-  if (m >= t.M) return;
+  const int l = threadIdx.x % LP;
+  for (int m = blockIdx.x * PPB + threadIdx.x / LP; m < t.M; m += gridDim.x * PPB) {
   int n, h, w;
   pix3(m, d.H, d.W, n, h, w);
   const T* dy = (const T*)t.a + n * t.as[0];
@@ -278,6 +283,7 @@ __global__ void __launch_bounds__(NT) k1_dgrad(Thin t, int LP) {
       if (t.beta != 0.f) v += t.beta * to_f(o[e]);
       o[e] = from_f<TO>(v);
     }
+  }
   }
 }
 
@@ -417,6 +423,11 @@ bool k1_ok(const es_conv_desc_t* d, int rs, int vn) {
 }
 
 unsigned blocks(int64_t items, int per) { return (unsigned)((items + per - 1) / per); }
+// grid caps of the grid-stride thin kernels (A/B switches; 0 = one block per PPB pixels)
+int env_int(const char* k, int dflt) { const char* e = getenv(k); return e ? atoi(e) : dflt; }
+const int g_k1_grid = env_int("ES_K1_GRID", 2048);
+const int g_thin_wgrid = env_int("ES_THIN_WGRID", 1024);
+unsigned capped(unsigned b, int cap) { return cap > 0 ? std::min<unsigned>(b, (unsigned)cap) : b; }
 
 template <typename T, typename TO>
 void launch_fwd(const Thin& t, int rs, int LP, hipStream_t st) {
@@ -426,7 +437,7 @@ void launch_fwd(const Thin& t, int rs, int LP, hipStream_t st) {
     if (rs == 4) hipLaunchKernelGGL((c1_fwd<T, TO, 4>), grid, dim3(NT), 0, st, t);
     else hipLaunchKernelGGL((c1_fwd<T, TO, 9>), grid, dim3(NT), 0, st, t);
   } else {
-    const dim3 grid(blocks(t.M, NT / LP));
+    const dim3 grid(capped(blocks(t.M, NT / LP), g_k1_grid));
     if (rs == 4) hipLaunchKernelGGL((k1_fwd<T, TO, 4>), grid, dim3(NT), 0, st, t, LP);
     else hipLaunchKernelGGL((k1_fwd<T, TO, 9>), grid, dim3(NT), 0, st, t, LP);
   }
@@ -440,7 +451,7 @@ void launch_dgrad(const Thin& t, int rs, int LP, hipStream_t st) {
     if (rs == 4) hipLaunchKernelGGL((c1_dgrad<T, TO, 4>), grid, dim3(NT), 0, st, t);
     else hipLaunchKernelGGL((c1_dgrad<T, TO, 9>), grid, dim3(NT), 0, st, t);
   } else {
-    const dim3 grid(blocks(t.M, NT / LP));
+    const dim3 grid(capped(blocks(t.M, NT / LP), g_k1_grid));
     if (rs == 4) hipLaunchKernelGGL((k1_dgrad<T, TO, 4>), grid, dim3(NT), 0, st, t, LP);
     else hipLaunchKernelGGL((k1_dgrad<T, TO, 9>), grid, dim3(NT), 0, st, t, LP);
   }
@@ -451,7 +462,7 @@ void launch_wgrad(const Thin& t, int rs, int LP, hipStream_t st) {
   const es_conv_desc_t& d = t.d;
   // ~4 blocks per CU, each reducing a strided slice of the pixels
   const int per = d.C == 1 ? NT / (d.K / 8) : NT / LP;
-  const dim3 grid(std::min<unsigned>(1024u, blocks(t.M, per)));
+  const dim3 grid(capped(blocks(t.M, per), g_thin_wgrid));
   if (d.C == 1) {
     if (rs == 4) hipLaunchKernelGGL((c1_wgrad<T, 4>), grid, dim3(NT), 0, st, t);
     else hipLaunchKernelGGL((c1_wgrad<T, 9>), grid, dim3(NT), 0, st, t);
