@@ -158,19 +158,33 @@ __global__ void __launch_bounds__(NT) c1_wgrad(Thin t) {
   for (int kk = 0; kk < 8; ++kk)
 #pragma unroll
     for (int j = 0; j < RS; ++j) acc[kk][j] = 0.f;
-  for (int m = blockIdx.x * PL + pl; m < t.M; m += gridDim.x * PL) {
-    int n, p, q;
-    pix3(m, d.P, d.Q, n, p, q);
-    float g[8];
-    ld8<T>((const T*)t.a + n * t.as[0] + p * t.as[2] + q * t.as[3] + ko * 8, g);
-    const T* x = (const T*)t.b + n * t.bs[0];
+  // two pixels per trip, every load clamped and issued before the FMAs (the guarded per-tap
+  // loads of one pixel at a time left each trip waiting on one round of global latency)
+  const int stride = gridDim.x * PL;
+  for (int m0 = blockIdx.x * PL + pl; m0 < t.M; m0 += 2 * stride) {
+    float g[2][8], xv[2][RS];
 #pragma unroll
-    for (int j = 0; j < RS; ++j) {
-      const int hu = p * d.stride - d.pad + j / d.S, wu = q * d.stride - d.pad + j % d.S;
-      const float xv = (hu >= 0 && hu < d.H && wu >= 0 && wu < d.W) ? to_f(x[hu * t.bs[2] + wu * t.bs[3]]) : 0.f;
+    for (int u = 0; u < 2; ++u) {
+      const int mu = m0 + u * stride;
+      const bool live = mu < t.M;
+      int n, p, q;
+      pix3(live ? mu : m0, d.P, d.Q, n, p, q);
+      ld8<T>((const T*)t.a + n * t.as[0] + p * t.as[2] + q * t.as[3] + ko * 8, g[u]);
+      const T* x = (const T*)t.b + n * t.bs[0];
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) acc[kk][j] += g[kk] * xv;
+      for (int j = 0; j < RS; ++j) {
+        const int hu = p * d.stride - d.pad + j / d.S, wu = q * d.stride - d.pad + j % d.S;
+        const bool ok = live && hu >= 0 && hu < d.H && wu >= 0 && wu < d.W;
+        const float v = to_f(x[ok ? hu * t.bs[2] + wu * t.bs[3] : 0]);
+        xv[u][j] = ok ? v : 0.f;
+      }
     }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int j = 0; j < RS; ++j)
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) acc[kk][j] += g[u][kk] * xv[u][j];
   }
   // lanes l and l ^ (KO * 2^i) share the channel group inside a wave
 #pragma unroll
@@ -299,27 +313,39 @@ __global__ void __launch_bounds__(NT) k1_wgrad(Thin t, int LP) {
   for (int j = 0; j < RS; ++j)
 #pragma unroll
     for (int e = 0; e < VN; ++e) acc[j][e] = 0.f;
-  for (int m = blockIdx.x * PPB + threadIdx.x / LP; m < t.M; m += gridDim.x * PPB) {
-    int n, p, q;
-    pix3(m, d.P, d.Q, n, p, q);
-    const float g = to_f(((const T*)t.a)[n * t.as[0] + p * t.as[2] + q * t.as[3]]);
-    const T* x = (const T*)t.b + n * t.bs[0] + l * VN;
+  // two pixels per trip: both pixels' tap loads are issued before the FMAs
+  const int stride = gridDim.x * PPB;
+  for (int m0 = blockIdx.x * PPB + threadIdx.x / LP; m0 < t.M; m0 += 2 * stride) {
+    float gj[2][RS];
+    float v[2][RS][VN];
 #pragma unroll
-    for (int j = 0; j < RS; ++j) {
-      const int hu = p - d.pad + j / d.S, wu = q - d.pad + j % d.S;
-      const bool ok = hu >= 0 && hu < d.H && wu >= 0 && wu < d.W;
-      const T* px = x + (ok ? hu * t.bs[2] + wu * t.bs[3] : 0);   // clamped: loads issue together
-      const float gj = ok ? g : 0.f;
-      if constexpr (VN == 8) {
-        float v[8];
-        ld8<T>(px, v);
+    for (int u = 0; u < 2; ++u) {
+      const int mu = m0 + u * stride;
+      const bool live = mu < t.M;
+      int n, p, q;
+      pix3(live ? mu : m0, d.P, d.Q, n, p, q);
+      const float g = to_f(((const T*)t.a)[n * t.as[0] + p * t.as[2] + q * t.as[3]]);
+      const T* x = (const T*)t.b + n * t.bs[0] + l * VN;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[j][e] += gj * v[e];
-      } else {
-        const float4 v = *(const float4*)px;
-        acc[j][0] += gj * v.x; acc[j][1] += gj * v.y; acc[j][2] += gj * v.z; acc[j][3] += gj * v.w;
+      for (int j = 0; j < RS; ++j) {
+        const int hu = p - d.pad + j / d.S, wu = q - d.pad + j % d.S;
+        const bool ok = live && hu >= 0 && hu < d.H && wu >= 0 && wu < d.W;
+        const T* px = x + (ok ? hu * t.bs[2] + wu * t.bs[3] : 0);   // clamped: loads issue together
+        gj[u][j] = ok ? g : 0.f;
+        if constexpr (VN == 8) {
+          ld8<T>(px, v[u][j]);
+        } else {
+          const float4 w4 = *(const float4*)px;
+          v[u][j][0] = w4.x; v[u][j][1] = w4.y; v[u][j][2] = w4.z; v[u][j][3] = w4.w;
+        }
       }
     }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int j = 0; j < RS; ++j)
+#pragma unroll
+        for (int e = 0; e < VN; ++e) acc[j][e] += gj[u][j] * v[u][j][e];
   }
 #pragma unroll
   for (int j = 0; j < RS; ++j)
