@@ -184,6 +184,8 @@ __global__ void __launch_bounds__(FT) dfront_fwd_kernel(FrontArgs a) {
   }
 }
 
+// WANT_DX is compile-time: without the image gradient (the D step) the e_rs sums are not computed
+template <bool WANT_DX>
 __global__ void __launch_bounds__(FT) dfront_bwd_kernel(FrontArgs a) {
   __shared__ float im[MAXPIX];
   __shared__ float ep[TAPS * MAXOUT];      // e_rs planes; also the reduction scratch
@@ -243,7 +245,7 @@ __global__ void __launch_bounds__(FT) dfront_bwd_kernel(FrontArgs a) {
   float acc[CPG * TAPS + CPG];
 #pragma unroll
   for (int i = 0; i < CPG * TAPS + CPG; ++i) acc[i] = 0.f;
-  const bool want_dx = a.dx != nullptr;
+  constexpr bool want_dx = WANT_DX;
   for (int pp = u; pp < NP; pp += FT / 8) {
     const int pi = pp / a.Wp, pj = pp - pi * a.Wp;
     float x[4][4], v[4][CPG];
@@ -269,11 +271,11 @@ __global__ void __launch_bounds__(FT) dfront_bwd_kernel(FrontArgs a) {
 #pragma unroll
         for (int t = 0; t < TAPS; ++t) {
           acc[c * TAPS + t] = fmaf(dh, x[(pos >> 1) + t / 3][(pos & 1) + t % 3], acc[c * TAPS + t]);
-          e[pos][t] = fmaf(dh, q.w[c][t], e[pos][t]);
+          if constexpr (WANT_DX) e[pos][t] = fmaf(dh, q.w[c][t], e[pos][t]);
         }
       }
     }
-    if (want_dx) {                         // kernel-uniform
+    if constexpr (want_dx) {
       // sum e over the window's 8 lanes (all 32 channels), then lane g stores entries g, g+8, ...
 #pragma unroll
       for (int pos = 0; pos < 4; ++pos)
@@ -295,7 +297,7 @@ __global__ void __launch_bounds__(FT) dfront_bwd_kernel(FrontArgs a) {
       }
     }
   }
-  if (want_dx) {
+  if constexpr (want_dx) {
     __syncthreads();
     // pass 3: image gradient, dx[i][j] = sum over taps (r, s) of e_rs[i - r][j - s]
     float* dx = a.dx + n * a.dxs[0];
@@ -388,7 +390,8 @@ extern "C" int es_dfront_bwd(const float* img, const int64_t is[4], int N, int H
   a.dpooled = dpooled; a.dx = dx; a.part = part;
   if (dx)
     for (int i = 0; i < 4; ++i) a.dxs[i] = dxs[i];
-  hipLaunchKernelGGL(dfront_bwd_kernel, dim3(N), dim3(FT), 0, (hipStream_t)stream, a);
+  if (a.dx) hipLaunchKernelGGL(dfront_bwd_kernel<true>, dim3(N), dim3(FT), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(dfront_bwd_kernel<false>, dim3(N), dim3(FT), 0, (hipStream_t)stream, a);
   ES_CHECK_LAUNCH();
   if (dw || dbias || dgamma || dbeta) {
     hipLaunchKernelGGL(dfront_part_reduce, dim3((NPART + 63) / 64), dim3(1024), 0, (hipStream_t)stream, part, N,
