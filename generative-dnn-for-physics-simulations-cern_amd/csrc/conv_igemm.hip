@@ -1196,6 +1196,21 @@ __global__ void unpack_grad_kernel(const float* __restrict__ dw, int K, int C, i
     *g = (beta != 0.f ? beta * *g : 0.f) + dw[i];
   }
 }
+// same, and the packed accumulator is left zeroed for the next weight gradient (each element is
+// read and cleared by the one thread that owns it): no zero-fill launch per weight gradient
+__global__ void unpack_grad_clear_kernel(float* __restrict__ dw, int K, int C, int R, int S, float* grad,
+                                         float beta) {
+  const int64_t n = (int64_t)K * C * R * S;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t t = (uint32_t)i / C;
+    const int c = (int)((uint32_t)i - t * C);
+    const int s = t % S; t /= S; const int r = t % R; const int k = t / R;
+    float* g = grad + (((int64_t)k * C + c) * R + r) * S + s;
+    const float v = dw[i];
+    dw[i] = 0.f;
+    *g = (beta != 0.f ? beta * *g : 0.f) + v;
+  }
+}
 }  // namespace
 
 extern "C" int es_pack_conv_weight(const float* w, int K, int C, int R, int S, int mode,
@@ -1237,6 +1252,17 @@ extern "C" int es_pack_conv_weight(const float* w, int K, int C, int R, int S, i
   else
     hipLaunchKernelGGL(pack_weight_kernel<bf16>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
                        w, K, C, R, S, mode, inv_scale, col_perm, (bf16*)out);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_unpack_conv_grad_clear(float* dw, int K, int C, int R, int S, float* grad, float beta,
+                                         es_stream_t stream) {
+  const int64_t n = (int64_t)K * C * R * S;
+  ES_CHECK_ARG(n < (1ll << 31), "unpack: weight too large");
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(unpack_grad_clear_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, dw, K, C, R, S,
+                     grad, beta);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }

@@ -71,6 +71,7 @@ _SIGS = {
     "es_conv2d_wgrad": (C.c_int, [P, C.c_int, P, P, P, P, P, P]),
     "es_pack_conv_weight": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, C.c_int, P]),
     "es_unpack_conv_grad": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, C.c_float, P]),
+    "es_unpack_conv_grad_clear": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_float, P]),
     "es_norm_stats_ws_bytes": (I64, [P, C.c_int, C.c_int]),
     "es_norm_stats": (C.c_int, [P, C.c_int, P, C.c_int, C.c_int, C.c_float, P, P, P, P, C.c_float, P, P]),
     "es_norm_act_fwd": (C.c_int, [P, C.c_int, P, P, P, C.c_int, P, P, P, C.c_int, P, P]),

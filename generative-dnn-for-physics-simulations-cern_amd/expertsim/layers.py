@@ -8,6 +8,7 @@ conv activations live channels-last (NHWC) while linear activations are plain [r
 from __future__ import annotations
 
 import ctypes as C
+import os
 import math
 
 import numpy as np
@@ -329,13 +330,30 @@ class ConvOp:
         """dW (torch layout, fp32) accumulated into dw_out (beta=1) or written (beta=0)."""
         d = self.desc(x)
         dev = dy.t.device
-        dwk = torch.zeros(self.weight.numel(), dtype=torch.float32, device=dev)
         assert dy.t.dtype == x.t.dtype, (dy.t.dtype, x.t.dtype)
+        # every wgrad kernel ACCUMULATES into its packed [K][R][S][C] output, so:
+        #  * packed == torch layout (1x1 / linear, or Cin = 1) and beta = 1: accumulate straight
+        #    into the parameter's gradient (no scratch, no unpack);
+        #  * otherwise a persistent packed scratch that the unpack leaves zeroed (no zero fill).
+        legacy = os.environ.get("ES_WGRAD_SCRATCH", "1") == "0"         # A/B switch
+        direct = (not legacy and dw_out is not None and float(beta) == 1.0 and (self.R * self.S == 1 or self.C == 1)
+                  and dw_out.is_contiguous() and dw_out.dtype == torch.float32)
+        if direct:
+            dwk = dw_out
+        elif dw_out is not None and not legacy:
+            dwk = getattr(self, "_dwk", None)
+            if dwk is None or dwk.device != dev:
+                dwk = self._dwk = torch.zeros(self.weight.numel(), dtype=torch.float32, device=dev)
+        else:
+            dwk = torch.zeros(self.weight.numel(), dtype=torch.float32, device=dev)
         with _probed(self.label and self.label + ".wgrad"):
           hip.call("es_conv2d_wgrad", C.byref(d), dy.dt, dy.ptr, hip.strides4(dy.strides), x.ptr,
                  hip.strides4(x.strides), hip.ptr(dwk), hip.stream_ptr())
-        if dw_out is not None:
+        if dw_out is not None and legacy:
             hip.call("es_unpack_conv_grad", hip.ptr(dwk), self.K, self.C, self.R, self.S, None,
+                     hip.ptr(dw_out), float(beta), hip.stream_ptr())
+        elif dw_out is not None and not direct:
+            hip.call("es_unpack_conv_grad_clear", hip.ptr(dwk), self.K, self.C, self.R, self.S,
                      hip.ptr(dw_out), float(beta), hip.stream_ptr())
         if db_out is not None:
             channel_sum(dy, db_out, beta)

@@ -144,6 +144,10 @@ int es_pack_conv_weight(const float* w, int K, int C, int R, int S, int mode,
 /* grad[k][c][r][s] = beta*grad + dw[k][r][s][c] * (inv_scale ? 1/inv_scale[0] : 1) */
 int es_unpack_conv_grad(const float* dw, int K, int C, int R, int S, const int32_t* col_perm,
                         float* grad, float beta, es_stream_t stream);
+/* as es_unpack_conv_grad (no permutation), then dw[] = 0: a persistent packed accumulator needs no
+ * zero fill before the next es_conv2d_wgrad */
+int es_unpack_conv_grad_clear(float* dw, int K, int C, int R, int S, float* grad, float beta,
+                              es_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Normalisation + dropout + activation (aten::native_batch_norm / native_group_norm /
