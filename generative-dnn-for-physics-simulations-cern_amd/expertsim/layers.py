@@ -367,6 +367,40 @@ def channel_sum(x: Act, out: torch.Tensor, beta=1.0):
 
 
 # ------------------------------------------------------------------------------ norm + act
+# BatchNorm num_batches_tracked increments: one torch kernel per train-mode BN forward (15 per
+# neutron step).  Inside MoEWrapper.train_step they are counted on the host and applied at the end
+# as one multi-tensor add per distinct count (same final values).
+_NBT_PENDING = None
+
+
+class defer_num_batches:
+    def __enter__(self):
+        global _NBT_PENDING
+        on = os.environ.get("ES_DEFER_NBT", "1") != "0"                 # A/B switch
+        self.prev, _NBT_PENDING = _NBT_PENDING, ({} if on else None)
+        return self
+
+    def __exit__(self, *exc):
+        global _NBT_PENDING
+        pending, _NBT_PENDING = _NBT_PENDING, self.prev
+        if pending is None:
+            return False
+        by_count = {}
+        for t, k in pending.values():
+            by_count.setdefault(k, []).append(t)
+        for k, ts in by_count.items():
+            torch._foreach_add_(ts, k)
+        return False
+
+
+def _count_batch(nbt):
+    if _NBT_PENDING is None:
+        nbt.add_(1)
+    else:
+        t, k = _NBT_PENDING.get(id(nbt), (nbt, 0))
+        _NBT_PENDING[id(nbt)] = (t, k + 1)
+
+
 class NormOp:
     """BatchNorm (train: batch stats + running update), GroupNorm or LayerNorm, fused with the
     dropout / activation chain that follows it in the reference's nn.Sequential."""
@@ -395,7 +429,7 @@ class NormOp:
             hip.call("es_norm_stats_finalize", hip.ptr(part), chunks, x.dims[1], float(self.eps), hip.ptr(mean),
                      hip.ptr(invstd), hip.ptr(self.rm), hip.ptr(self.rv), float(self.momentum), hip.stream_ptr())
             if self.nbt is not None:
-                self.nbt.add_(1)
+                _count_batch(self.nbt)
             return mean, invstd
         wsb = ws(hip.lib().es_norm_stats_ws_bytes(C.byref(x.view), self.kind, self.groups), dev)
         upd = self.kind == hip.NORM_BN and train
@@ -403,7 +437,7 @@ class NormOp:
                  hip.ptr(mean), hip.ptr(invstd), hip.ptr(self.rm) if upd else None,
                  hip.ptr(self.rv) if upd else None, float(self.momentum), hip.ptr(wsb), hip.stream_ptr())
         if upd and self.nbt is not None:
-            self.nbt.add_(1)
+            _count_batch(self.nbt)
         return mean, invstd
 
     def norm_struct(self, mean, invstd):

@@ -32,7 +32,7 @@ from torch import nn
 
 from .. import hip
 from ..config import cfg_get
-from ..layers import Act, copy_act
+from ..layers import Act, copy_act, defer_num_batches
 from ..rng import DeviceRNG
 from ..utils import philox
 
@@ -123,8 +123,10 @@ class MoEWrapper(nn.Module):
         hip.set_step_counter(self._dstep)
         self.rng.begin_step(self._dstep)
         try:
-            return self._train_step(epoch, cond, real_images, true_positions, std, intensity, aux_reg_optimizers,
-                                    generator_optimizers, discriminator_optimizers, router_optimizer, dev, B)
+            with defer_num_batches():
+                return self._train_step(epoch, cond, real_images, true_positions, std, intensity,
+                                        aux_reg_optimizers, generator_optimizers, discriminator_optimizers,
+                                        router_optimizer, dev, B)
         finally:
             hip.set_step_counter(None)
             self.rng.end_step()
