@@ -284,36 +284,35 @@ __global__ void sum_finalize_kernel(const float* part, int chunks, int C, float*
 __global__ void __launch_bounds__(256) bn_finalize_block_kernel(const float* part, int chunks, int C, float eps,
                                                                 float* mean, float* invstd, float* rmean,
                                                                 float* rvar, float mom) {
+  // Plain fp64 sums n, sum n_b*m_b, sum (M_b + n_b*m_b^2) instead of a Welford merge per chunk: the
+  // merge's fp64 division made every thread's loop one dependent chain (17 us per call at 2048
+  // chunks); sums let the strided partial loads issue back to back.  fp64 keeps the
+  // S2 - n*mean^2 subtraction exact far beyond fp32 resolution for activation statistics.
   const int c = blockIdx.x;
-  double n_ = 0.0, mu = 0.0, M = 0.0;
+  double n_ = 0.0, s1 = 0.0, s2 = 0.0;
+#pragma unroll 4
   for (int k = threadIdx.x; k < chunks; k += blockDim.x) {
     const float* p = part + (int64_t)k * 3 * C;
-    const double nb = p[c];
-    if (nb == 0.0) continue;
-    const double mb = p[C + c], Mb = p[2 * C + c];
-    const double nt = n_ + nb, dl = mb - mu;
-    mu += dl * nb / nt;
-    M += Mb + dl * dl * n_ * nb / nt;
-    n_ = nt;
+    const double nb = p[c], mb = p[C + c], Mb = p[2 * C + c];
+    const bool has = nb > 0.0;             // an empty chunk's mean / M2 may be 0/0: skip it
+    n_ += nb;
+    s1 += has ? nb * mb : 0.0;
+    s2 += has ? Mb + nb * mb * mb : 0.0;
   }
   __shared__ double sn[256], sm[256], sM[256];
-  sn[threadIdx.x] = n_; sm[threadIdx.x] = mu; sM[threadIdx.x] = M;
+  sn[threadIdx.x] = n_; sm[threadIdx.x] = s1; sM[threadIdx.x] = s2;
   __syncthreads();
   for (int off = 128; off > 0; off >>= 1) {
     if (threadIdx.x < off) {
-      const double na = sn[threadIdx.x], nb = sn[threadIdx.x + off];
-      if (nb > 0.0) {
-        const double ma = sm[threadIdx.x], mb = sm[threadIdx.x + off];
-        const double nt = na + nb, dl = mb - ma;
-        sm[threadIdx.x] = ma + dl * nb / nt;
-        sM[threadIdx.x] = sM[threadIdx.x] + sM[threadIdx.x + off] + dl * dl * na * nb / nt;
-        sn[threadIdx.x] = nt;
-      }
+      sn[threadIdx.x] += sn[threadIdx.x + off];
+      sm[threadIdx.x] += sm[threadIdx.x + off];
+      sM[threadIdx.x] += sM[threadIdx.x + off];
     }
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    const double nt = sn[0], mt = sm[0], Mt = sM[0];
+    const double nt = sn[0], mt = sm[0] / nt;
+    const double Mt = fmax(sM[0] - nt * mt * mt, 0.0);
     const double var = Mt / nt;
     mean[c] = (float)mt;
     invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
