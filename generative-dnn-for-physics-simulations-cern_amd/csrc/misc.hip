@@ -276,9 +276,32 @@ __global__ void gather_rows_kernel(const float* src, int64_t sld, const int32_t*
 // --------------------------------------------------------------------------- spectral norm
 // One block.  v = normalize(W^T u); u = normalize(W v); sigma = u . (W v)
 // (torch.nn.utils.spectral_norm.SpectralNorm.compute_weight, eps = 1e-12)
+__device__ __forceinline__ void sn_power_body(const float* w, int h, int wd, float* u, float* v, float* sigma,
+                                              int update, float* scratch, float* sh);
+
 __global__ void __launch_bounds__(1024) sn_power_kernel(const float* w, int h, int wd, float* u, float* v,
                                                         float* sigma, int update, float* scratch) {
   __shared__ float sh[16];
+  sn_power_body(w, h, wd, u, v, sigma, update, scratch, sh);
+}
+
+// several small layers' power iterations in one launch (one block per layer): the discriminator's
+// conv_layers.0 / .4, fc2 and fc3 (neutron/discriminator.py:12-24) issue one launch instead of four
+struct SnJobs {
+  const float* w[ES_SN_BATCH_MAX];
+  float* u[ES_SN_BATCH_MAX];
+  float* v[ES_SN_BATCH_MAX];
+  float* buf[ES_SN_BATCH_MAX];
+  int h[ES_SN_BATCH_MAX], wd[ES_SN_BATCH_MAX];
+};
+__global__ void __launch_bounds__(1024) sn_power_batch_kernel(SnJobs j, int update) {
+  __shared__ float sh[16];
+  const int b = blockIdx.x;
+  sn_power_body(j.w[b], j.h[b], j.wd[b], j.u[b], j.v[b], j.buf[b], update, j.buf[b] + 1, sh);
+}
+
+__device__ __forceinline__ void sn_power_body(const float* w, int h, int wd, float* u, float* v, float* sigma,
+                                              int update, float* scratch, float* sh) {
   float* wv = scratch;       // [h]
   float* vt = scratch + h;   // [wd]
   if (update) {
@@ -615,6 +638,19 @@ extern "C" int es_sn_power_iter(const float* w, int h, int wd, float* u, float* 
   } else {
     hipLaunchKernelGGL(sn_power_kernel, dim3(1), dim3(1024), 0, st, w, h, wd, u, v, sigma, update, sigma + 1);
   }
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_sn_power_iter_batch(int n, const float* const* w, const int* h, const int* wd, float* const* u,
+                                      float* const* v, float* const* buf, int update, es_stream_t stream) {
+  ES_CHECK_ARG(n >= 1 && n <= ES_SN_BATCH_MAX, "sn_power_iter_batch: 1 <= n <= ES_SN_BATCH_MAX");
+  SnJobs j{};
+  for (int i = 0; i < n; ++i) {
+    ES_CHECK_ARG((int64_t)h[i] * wd[i] < 16384, "sn_power_iter_batch: layer too large for one block");
+    j.w[i] = w[i]; j.u[i] = u[i]; j.v[i] = v[i]; j.buf[i] = buf[i]; j.h[i] = h[i]; j.wd[i] = wd[i];
+  }
+  hipLaunchKernelGGL(sn_power_batch_kernel, dim3(n), dim3(1024), 0, (hipStream_t)stream, j, update);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }

@@ -562,6 +562,32 @@ class SpectralNorm:
         o = 1 + h + wd
         return buf[:1], buf[o:o + h], buf[o + h:o + h + wd]
 
+    @staticmethod
+    def sigma_many(sns, update=True):
+        """sigma() of several layers: the small ones (h*wd < 16384) share one launch."""
+        out = [None] * len(sns)
+        small = [i for i, sn in enumerate(sns) if sn.h * sn.wd < 16384]
+        if len(small) < 2 or os.environ.get("ES_SN_BATCH", "1") == "0":
+            small = []
+        for i, sn in enumerate(sns):
+            if i not in small:
+                out[i] = sn.sigma(update)
+        for c0 in range(0, len(small), 8):
+            idx = small[c0:c0 + 8]
+            n = len(idx)
+            bufs = [torch.empty(1 + 2 * (sns[i].h + sns[i].wd), dtype=torch.float32, device=sns[i].w.device)
+                    for i in idx]
+            arr = lambda vals: (C.c_void_p * n)(*vals)
+            hip.call("es_sn_power_iter_batch", n, arr([sns[i].w.data_ptr() for i in idx]),
+                     (C.c_int * n)(*[sns[i].h for i in idx]), (C.c_int * n)(*[sns[i].wd for i in idx]),
+                     arr([sns[i].u.data_ptr() for i in idx]), arr([sns[i].v.data_ptr() for i in idx]),
+                     arr([b.data_ptr() for b in bufs]), 1 if update else 0, hip.stream_ptr())
+            for i, b in zip(idx, bufs):
+                h, wd = sns[i].h, sns[i].wd
+                o = 1 + h + wd
+                out[i] = (b[:1], b[o:o + h], b[o + h:o + h + wd])
+        return out
+
     def bwd(self, g_sn: torch.Tensor, sig, dw_orig: torch.Tensor, beta=1.0):
         sigma, u, v = sig
         hip.call("es_sn_bwd", hip.ptr(self.w), hip.ptr(g_sn), self.h, self.wd, hip.ptr(u), hip.ptr(v),

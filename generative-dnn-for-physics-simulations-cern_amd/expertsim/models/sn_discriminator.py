@@ -129,7 +129,7 @@ class SNDiscriminator(ExpertModule):
         if img.t.dtype != cdt and not front:
             x = img.like_nhwc(cdt)
             copy_act(img, x)
-        sig = {n: o["sn:" + n].sigma(update=train) for n in LAYERS}
+        sig = dict(zip(LAYERS, SpectralNorm.sigma_many([o["sn:" + n] for n in LAYERS], update=train)))
         inv = lambda n: sig[n][0]
         if front:
             p1, i1, s1 = self.front_fwd(x, inv("conv_layers.0"))

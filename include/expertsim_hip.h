@@ -266,6 +266,11 @@ int es_gather_rows(const float* src, int64_t src_ld, const int32_t* idx, int row
  * ---------------------------------------------------------------------------------------- */
 int es_sn_power_iter(const float* w, int h, int wd, float* u, float* v, float* sigma, int update,
                      es_stream_t stream);
+/* es_sn_power_iter for n <= ES_SN_BATCH_MAX small layers (h*wd < 16384 each) in ONE launch; the
+ * arrays are host arrays of device pointers / sizes, buf[i] as es_sn_power_iter's sigma buffer. */
+#define ES_SN_BATCH_MAX 8
+int es_sn_power_iter_batch(int n, const float* const* w, const int* h, const int* wd, float* const* u,
+                           float* const* v, float* const* buf, int update, es_stream_t stream);
 /* dW_orig = beta*dW_orig + G/sigma - (<G, W>/sigma^2) u v^T   (G = grad of W/sigma).
  * sigma is the buffer es_sn_power_iter wrote (1 + h + wd floats); its tail is used as scratch. */
 int es_sn_bwd(const float* w, const float* g, int h, int wd, const float* u, const float* v,
