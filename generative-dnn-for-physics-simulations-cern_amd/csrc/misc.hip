@@ -424,10 +424,31 @@ __global__ void __launch_bounds__(256) sn_bwd_apply_kernel(const float* __restri
 }
 
 // dW_orig = beta*dW + G/s - (<G,W>/s^2) u v^T
+__device__ __forceinline__ void sn_bwd_body(const float* w, const float* g, int h, int wd, const float* u,
+                                            const float* v, const float* sigma, float* dw, float beta, float* sh);
 __global__ void __launch_bounds__(1024) sn_bwd_kernel(const float* w, const float* g, int h, int wd,
                                                       const float* u, const float* v, const float* sigma,
                                                       float* dw, float beta) {
   __shared__ float sh[16];
+  sn_bwd_body(w, g, h, wd, u, v, sigma, dw, beta, sh);
+}
+// several small layers' weight_orig gradients in one launch (one block per layer)
+struct SnBwdJobs {
+  const float* w[ES_SN_BATCH_MAX];
+  const float* g[ES_SN_BATCH_MAX];
+  const float* u[ES_SN_BATCH_MAX];
+  const float* v[ES_SN_BATCH_MAX];
+  const float* sigma[ES_SN_BATCH_MAX];
+  float* dw[ES_SN_BATCH_MAX];
+  int h[ES_SN_BATCH_MAX], wd[ES_SN_BATCH_MAX];
+};
+__global__ void __launch_bounds__(1024) sn_bwd_batch_kernel(SnBwdJobs j, float beta) {
+  __shared__ float sh[16];
+  const int b = blockIdx.x;
+  sn_bwd_body(j.w[b], j.g[b], j.h[b], j.wd[b], j.u[b], j.v[b], j.sigma[b], j.dw[b], beta, sh);
+}
+__device__ __forceinline__ void sn_bwd_body(const float* w, const float* g, int h, int wd, const float* u,
+                                            const float* v, const float* sigma, float* dw, float beta, float* sh) {
   const int64_t n = (int64_t)h * wd;
   float d = 0.f;
   for (int64_t i = threadIdx.x; i < n; i += blockDim.x) d += g[i] * w[i];
@@ -651,6 +672,22 @@ extern "C" int es_sn_power_iter_batch(int n, const float* const* w, const int* h
     j.w[i] = w[i]; j.u[i] = u[i]; j.v[i] = v[i]; j.buf[i] = buf[i]; j.h[i] = h[i]; j.wd[i] = wd[i];
   }
   hipLaunchKernelGGL(sn_power_batch_kernel, dim3(n), dim3(1024), 0, (hipStream_t)stream, j, update);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_sn_bwd_batch(int n, const float* const* w, const float* const* g, const int* h, const int* wd,
+                               const float* const* u, const float* const* v, const float* const* sigma,
+                               float* const* dw, float beta, es_stream_t stream) {
+  ES_CHECK_ARG(n >= 1 && n <= ES_SN_BATCH_MAX, "sn_bwd_batch: 1 <= n <= ES_SN_BATCH_MAX");
+  SnBwdJobs j{};
+  for (int i = 0; i < n; ++i) {
+    const int64_t e = (int64_t)h[i] * wd[i];
+    ES_CHECK_ARG(!(e >= 16384 && h[i] + wd[i] >= 256), "sn_bwd_batch: layer too large for one block");
+    j.w[i] = w[i]; j.g[i] = g[i]; j.u[i] = u[i]; j.v[i] = v[i]; j.sigma[i] = sigma[i]; j.dw[i] = dw[i];
+    j.h[i] = h[i]; j.wd[i] = wd[i];
+  }
+  hipLaunchKernelGGL(sn_bwd_batch_kernel, dim3(n), dim3(1024), 0, (hipStream_t)stream, j, beta);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }

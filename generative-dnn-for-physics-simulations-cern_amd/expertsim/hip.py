@@ -96,6 +96,7 @@ _SIGS = {
     "es_gather_rows": (C.c_int, [P, I64, P, C.c_int, C.c_int, P, I64, P]),
     "es_sn_power_iter": (C.c_int, [P, C.c_int, C.c_int, P, P, P, C.c_int, P]),
     "es_sn_power_iter_batch": (C.c_int, [C.c_int, P, P, P, P, P, P, C.c_int, P]),
+    "es_sn_bwd_batch": (C.c_int, [C.c_int, P, P, P, P, P, P, P, P, C.c_float, P]),
     "es_sn_bwd": (C.c_int, [P, P, C.c_int, C.c_int, P, P, P, P, C.c_float, P]),
     "es_hinge_d": (C.c_int, [P, P, C.c_int, P, P, P, P, P]),
     "es_image_expsum": (C.c_int, [P, C.c_int, P, P, P]),

@@ -588,6 +588,26 @@ class SpectralNorm:
                 out[i] = (b[:1], b[o:o + h], b[o + h:o + h + wd])
         return out
 
+    @staticmethod
+    def bwd_many(jobs, beta=1.0):
+        """bwd() of several layers, jobs = [(sn, g_sn, sig, dw_orig)]: the small ones share a launch."""
+        small = [j for j in jobs if not (j[0].h * j[0].wd >= 16384 and j[0].h + j[0].wd >= 256)]
+        if len(small) < 2 or os.environ.get("ES_SN_BATCH", "1") == "0":
+            small = []
+        for j in jobs:
+            if not any(j is k for k in small):
+                j[0].bwd(j[1], j[2], j[3], beta)
+        for c0 in range(0, len(small), 8):
+            part = small[c0:c0 + 8]
+            n = len(part)
+            arr = lambda vals: (C.c_void_p * n)(*vals)
+            hip.call("es_sn_bwd_batch", n, arr([sn.w.data_ptr() for sn, _, _, _ in part]),
+                     arr([g.data_ptr() for _, g, _, _ in part]),
+                     (C.c_int * n)(*[sn.h for sn, _, _, _ in part]), (C.c_int * n)(*[sn.wd for sn, _, _, _ in part]),
+                     arr([sig[1].data_ptr() for _, _, sig, _ in part]), arr([sig[2].data_ptr() for _, _, sig, _ in part]),
+                     arr([sig[0].data_ptr() for _, _, sig, _ in part]), arr([d.data_ptr() for _, _, _, d in part]),
+                     float(beta), hip.stream_ptr())
+
     def bwd(self, g_sn: torch.Tensor, sig, dw_orig: torch.Tensor, beta=1.0):
         sigma, u, v = sig
         hip.call("es_sn_bwd", hip.ptr(self.w), hip.ptr(g_sn), self.h, self.wd, hip.ptr(u), hip.ptr(v),

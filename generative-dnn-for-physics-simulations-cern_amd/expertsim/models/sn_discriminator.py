@@ -166,7 +166,17 @@ class SNDiscriminator(ExpertModule):
 
     # --------------------------------------------------------------------------- backward
     def bwd(self, ctx, dout: Act = None, dlat: Act = None, weight_grads=True, input_grad=True):
-        """dout [B,1] fp32 (or None), dlat [B,64] fp32 (or None).  Returns d image (fp32 Act) or None."""
+        """dout [B,1] fp32 (or None), dlat [B,64] fp32 (or None).  Returns d image (fp32 Act) or None.
+        The spectral-norm weight_orig gradients of the layers are issued together at the end
+        (SpectralNorm.bwd_many: the small layers share one launch)."""
+        sn_jobs = []
+        try:
+            return self._bwd(ctx, dout, dlat, weight_grads, input_grad, sn_jobs)
+        finally:
+            if sn_jobs:
+                SpectralNorm.bwd_many(sn_jobs, beta=1.0)
+
+    def _bwd(self, ctx, dout, dlat, weight_grads, input_grad, sn_jobs):
         o = self.ops()
         cdt = self.compute_dtype
         dev = ctx["X"].t.device
@@ -184,7 +194,7 @@ class SNDiscriminator(ExpertModule):
             op.wgrad(dy, x, g_sn, None, beta=0.0)          # grad of W/sigma
             if not bias_done:                               # bias is not normalised
                 channel_sum(dy, mod.bias.grad, beta=1.0)
-            o["sn:" + name].bwd(g_sn, sig[name], mod.weight_orig.grad, beta=1.0)
+            sn_jobs.append((o["sn:" + name], g_sn, sig[name], mod.weight_orig.grad))
 
         bias_g = (lambda n: m(n).bias.grad) if weight_grads else (lambda n: None)
 

@@ -271,6 +271,10 @@ int es_sn_power_iter(const float* w, int h, int wd, float* u, float* v, float* s
 #define ES_SN_BATCH_MAX 8
 int es_sn_power_iter_batch(int n, const float* const* w, const int* h, const int* wd, float* const* u,
                            float* const* v, float* const* buf, int update, es_stream_t stream);
+/* es_sn_bwd for n <= ES_SN_BATCH_MAX small layers in ONE launch (host arrays of device pointers). */
+int es_sn_bwd_batch(int n, const float* const* w, const float* const* g, const int* h, const int* wd,
+                    const float* const* u, const float* const* v, const float* const* sigma, float* const* dw,
+                    float beta, es_stream_t stream);
 /* dW_orig = beta*dW_orig + G/sigma - (<G, W>/sigma^2) u v^T   (G = grad of W/sigma).
  * sigma is the buffer es_sn_power_iter wrote (1 + h + wd floats); its tail is used as scratch. */
 int es_sn_bwd(const float* w, const float* g, int h, int wd, const float* u, const float* v,
