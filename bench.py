@@ -1,23 +1,27 @@
 #!/usr/bin/env python
-"""Benchmark of the expertsim GAN training step on MI355X (BASELINE.json metric, configs[1]).
+"""Benchmark of the expertsim GAN training step on MI355X (BASELINE.json metric).
 
-Workload: neutron 44x44 ZDC MoE-GAN, 1 expert, batch 512 per GPU, bf16 GEMM operands (fp32
-accumulation / statistics / optimizer), synthetic data resident in HBM.  One "step" =
-``MoEWrapper.train_step`` (router, G fwd x2, D fwd x4 + bwd x4, aux regressor fwd/bwd, losses,
-four fused Adam updates; with N > 1 also the RCCL gradient all-reduces).
+Default workload = BASELINE configs[2]: neutron 44x44 ZDC GAN with SDI diversity + auxiliary coord
+regressor (always on in the reference), 1 expert, batch 1024 per GPU, bf16 GEMM operands (fp32
+accumulation / statistics / parameters / optimizer), synthetic data resident in HBM.  One "step" =
+``MoEWrapper.train_step`` (router, G fwd x2 + bwd x2, D fwd x4 + bwd x4, aux regressor fwd/bwd,
+losses, four fused Adam updates; with N > 1 also the RCCL gradient all-reduces).  Beside the bf16
+line it measures the same step in fp32 parity mode (exact fp32 MFMA, the precision the parity
+tests pin against the reference) as ``parity_fp32``.
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W --batch B --experts E --arch neutron|proton]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 Prints ONE JSON line (rank 0) with the metric, a live-measured roofline of the dominant kernel
-(HIP events around its launches inside the timed region) and the CPU baseline (the oracle, a CPU
-fp32 restatement of the same step, timed on this host's cores on a bounded sample).
+(HIP events on its launch stream inside eager steps of the same model) and the CPU baseline (the
+oracle, a CPU fp32 restatement of the same step, timed on this host's cores on a bounded sample).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -30,9 +34,30 @@ sys.path.insert(0, ROOT)
 # reference): neutron 10.573 GFLOP, proton 28.566 GFLOP
 STEP_FLOP_PER_IMAGE = {"neutron": 10.573e9, "proton": 28.566e9}
 PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
-# HBM traffic of the roofline kernel from committed PMC passes (tools/gpu_traffic.sh ->
-# tools/traffic_json.py): FETCH_SIZE (x2, gfx950) + WRITE_SIZE per launch of G0.c5.fwd
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01_s2h_c5_fwd_traffic.json")
+IMAGE = {"neutron": "44x44", "proton": "56x30"}
+
+
+def traffic_json(arch, batch):
+    """Committed PMC passes of the roofline kernel (tools/gpu_traffic.sh -> tools/traffic_json.py)."""
+    p = os.path.join(ROOT, "profiles", f"traffic_{arch}_c5_fwd_b{batch}.json")
+    return p if os.path.exists(p) else None
+
+
+def workload_label(arch, E, batch, world):
+    """Which BASELINE.json config the flags reproduce (configs[0] is the CPU plumbing run)."""
+    gb = batch * world
+    if arch == "neutron" and E == 1 and gb == 512 and world == 1:
+        k = "configs[1]"
+    elif arch == "neutron" and E == 1 and gb == 1024 and world == 1:
+        k = "configs[2]"
+    elif arch == "neutron" and E == 4 and gb == 2048:
+        k = "configs[3]"
+    elif E == 1 and batch in (512, 1024) and world > 1:
+        k = f"configs[{1 if batch == 512 else 2}] per GPU, weak-scaled over {world} GPUs"
+    else:
+        k = "not a BASELINE config"
+    return (f"{arch} {IMAGE[arch]} MoE-GAN train_step (hinge + SDI + intensity + aux regressor), "
+            f"E={E}, B={batch} per GPU, global {gb} ({k})")
 
 
 def conv_flops_per_image(arch):
@@ -49,8 +74,11 @@ def build(arch, E, precision, seed, device):
     from expertsim.models import build_model
     from expertsim.models.moe import MoEWrapper
     from expertsim.train.training_setup import setup_optimizers
-    cfg = inject_shared(load_config(overrides=[f"model.architecture={arch}", f"model.n_experts={E}",
-                                               f"train.precision={precision}", f"train.rng_seed={seed}"]))
+    ov = [f"model.architecture={arch}", f"model.n_experts={E}", f"train.precision={precision}",
+          f"train.rng_seed={seed}"]
+    if E > 1:
+        ov.append("model.router.diff_strength=1e-6")     # default.yaml '1-6' 
+    cfg = inject_shared(load_config(overrides=ov))
     torch.manual_seed(seed)
     parts = [build_model(f"{arch}.{k}", getattr(cfg.model, k), device) for k in ("generator", "discriminator", "aux_reg")]
     router = build_model("router_v1", cfg.model.router, device)
@@ -58,7 +86,21 @@ def build(arch, E, precision, seed, device):
     return moe, setup_optimizers(moe, cfg), cfg
 
 
-def cpu_baseline(arch, batch=64, steps=2):
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(arch, batch=64, max_steps=20, budget_s=25.0):
+    """The oracle (torch CPU fp32 restatement of the same step, pinned to the reference's goldens)
+    timed on this host: median of up to ``max_steps`` steps within ``budget_s`` after one warm-up.
+    B=64 keeps the sample bounded: the reference's CPU throughput is flat in B (22.4 / 22.3 /
+    21.6 img/s at B = 64 / 512 / 1024 on 8 threads)."""
     import torch
     from oracle import expertsim_oracle as O
     from expertsim.utils.synthetic import make_batch
@@ -69,30 +111,136 @@ def cpu_baseline(arch, batch=64, steps=2):
     t = {k: torch.from_numpy(v) for k, v in b.items()}
     noise_fn = lambda e, w, shape: torch.randn(shape, generator=g)
     times = []
-    for i in range(steps + 1):
+    t_start = time.perf_counter()
+    for i in range(max_steps + 1):
         t0 = time.perf_counter()
         m.train_step(0, t["cond"], t["real_images"].unsqueeze(1), t["true_positions"], t["std"], t["intensity"],
                      noise_fn, torch.empty(batch, 1).exponential_(generator=g))
         times.append(time.perf_counter() - t0)
-    dt = sum(times[1:]) / steps
+        if time.perf_counter() - t_start > budget_s and len(times) >= 4:
+            break
+    steps = times[1:]
+    dt = statistics.median(steps)
     return {"value": round(batch / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{arch} E=1 B={batch}: {steps} timed train steps after 1 warm-up, "
-                      f"oracle/expertsim_oracle.py (torch CPU fp32, {threads} threads)"}
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+            "sample": f"{arch} E=1 B={batch}: median of {len(steps)} train steps after 1 warm-up "
+                      f"({sum(steps):.1f} s), oracle/expertsim_oracle.py (torch CPU fp32, {threads} threads)"}
+
+
+def timed(step, steps, world):
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def make_step(moe, step_args, use_graph):
+    def eager_step():
+        moe.train_step(*step_args)
+    if not use_graph:
+        return eager_step, None
+    from expertsim.graph import StepGraph
+    sg = StepGraph(moe, step_args, warmup=1)
+    return sg.replay, sg
+
+
+def probe_dominant(moe, eager_step, steps, arch, batch, precision):
+    """Per-launch HIP events around the dominant conv's launches (on its launch stream) over
+    eager steps of the same model and batch -> the roofline object."""
+    import torch
+    from expertsim import layers
+    probe = layers.KernelProbe(["G0.c5.fwd", "G0.c5.dgrad", "G0.c5.wgrad"])
+    layers.set_probe(probe)
+    for _ in range(steps):
+        eager_step()
+    torch.cuda.synchronize()
+    layers.set_probe(None)
+    stats = probe.summary()
+    flops = conv_flops_per_image(arch) * batch
+    dom = max(stats, key=lambda k: stats[k]["total_ms"])
+    avg_ms = stats[dom]["avg_ms"]
+    achieved = flops / (avg_ms * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[precision]
+    traffic, tnote, mfma_busy = None, None, None
+    tj_path = traffic_json(arch, batch) if (dom == "G0.c5.fwd" and precision == "bf16") else None
+    if tj_path:
+        tj = json.load(open(tj_path))
+        traffic = tj["traffic_bytes"]
+        mfma_busy = tj.get("mfma_busy_frac")
+        tnote = (f"HBM bytes per launch: FETCH_SIZE x2 {tj['fetch_bytes']} + WRITE_SIZE {tj['write_bytes']} "
+                 f"(algorithmic {tj['algorithmic_bytes']}), {os.path.relpath(tj_path, ROOT)}")
+    return {"bound": "mfma", "kernel": f"{dom} (generator conv_layers.5, "
+                                       f"{'conv_ring bf16' if precision == 'bf16' else 'conv_igemm fp32'})",
+            "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_note": tnote,
+            "mfma_busy_pmc": mfma_busy,
+            "flop_per_launch": flops, "avg_ms": round(avg_ms, 4), "launches": stats[dom]["count"],
+            "all_probed": {k: {"avg_ms": round(v["avg_ms"], 4),
+                               "tflops": round(flops / (v["avg_ms"] * 1e-3) / 1e12, 2)}
+                           for k, v in stats.items()}}
+
+
+def run_mode(args, precision, steps, warmup, dev, rank, world, ddp, probe_steps):
+    """Build a model in ``precision``, warm up, time ``steps`` steps; returns (value, dt, roof, launch)."""
+    import torch
+    import torch.distributed as dist
+    from expertsim.train.ddp import DataParallel
+    from expertsim.utils.synthetic import make_batch
+    moe, (og, od, oa, orr), cfg = build(args.arch, args.experts, precision, 1234, dev)
+    if ddp:
+        moe.ddp = DataParallel()
+        moe.rank = rank
+    b = make_batch(args.batch, args.arch, seed=1000 + rank)
+    t = {k: torch.from_numpy(v).to(dev) for k, v in b.items()}
+    real = t["real_images"].unsqueeze(1).contiguous()
+    step_args = (0, t["cond"], real, t["true_positions"], t["std"], t["intensity"], oa, og, od, orr, None, dev)
+    use_graph = args.graph == "on" or (args.graph == "auto" and not ddp)
+    if use_graph and args.experts > 1:
+        from expertsim.graph import graph_supported
+        use_graph = graph_supported(moe)
+    eager = lambda: moe.train_step(*step_args)
+    for _ in range(warmup):
+        eager()
+    step, sg = make_step(moe, step_args, use_graph)
+    dt = timed(step, steps, world)
+    if sg is not None:
+        sg.sync_host_state([*og, *od, *oa, orr])
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    roof = None
+    if probe_steps and rank == 0:
+        roof = probe_dominant(moe, eager, probe_steps, args.arch, args.batch, precision)
+    value = args.batch * world * steps / dt
+    del moe, og, od, oa, orr, step, sg, t, real, step_args
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return value, dt, roof, ("hip_graph" if use_graph else "eager")
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=512, help="images per GPU")
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=1024, help="images per GPU")
     ap.add_argument("--arch", default="neutron")
     ap.add_argument("--experts", type=int, default=1)
     ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--fp32-steps", type=int, default=30, help="timed steps of the fp32 parity-mode line (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the per-kernel HIP-event probe")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
-                    help="replay the step as a captured HIP graph (auto: single process, 1 expert)")
+                    help="replay the step as a captured HIP graph (auto: single process)")
     ap.add_argument("--ddp", action="store_true",
                     help="run the data-parallel code path even on one process (1-rank RCCL group)")
     args = ap.parse_args()
@@ -110,102 +258,38 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29533")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
-    from expertsim import layers
-    from expertsim.train.ddp import DataParallel
-    from expertsim.utils.synthetic import make_batch
-    moe, (og, od, oa, orr), cfg = build(args.arch, args.experts, args.precision, 1234, dev)
-    if ddp:
-        moe.ddp = DataParallel()
-        moe.rank = rank
-    b = make_batch(args.batch, args.arch, seed=1000 + rank)
-    t = {k: torch.from_numpy(v).to(dev) for k, v in b.items()}
-    real = t["real_images"].unsqueeze(1).contiguous()
-
-    step_args = (0, t["cond"], real, t["true_positions"], t["std"], t["intensity"], oa, og, od, orr, None, dev)
-
-    def eager_step():
-        moe.train_step(*step_args)
-
-    # DDP stays eager: its eager step issues as fast as the graph replays (1-rank DDP 41.9k vs graph
-    # 42.0k img/s on one MI355X), and capturing around the RCCL calls is not needed for that
-    use_graph = args.graph == "on" or (args.graph == "auto" and not ddp and args.experts == 1)
-    for _ in range(args.warmup):
-        eager_step()
-    step = eager_step
-    if use_graph:
-        from expertsim.graph import StepGraph
-        sg = StepGraph(moe, step_args, warmup=1)
-        step = sg.replay
-    probe = None
-    if not args.no_probe and not use_graph:
-        probe = layers.KernelProbe(["G0.c5.fwd", "G0.c5.dgrad", "G0.c5.wgrad"])
-        layers.set_probe(probe)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    layers.set_probe(None)
-    if use_graph:
-        sg.sync_host_state([og[0], od[0], oa[0], orr])
-        if not args.no_probe:
-            # a graph replay cannot be split per kernel: the per-launch HIP events are taken on
-            # eager steps of the same model and batch right after the timed region
-            probe = layers.KernelProbe(["G0.c5.fwd", "G0.c5.dgrad", "G0.c5.wgrad"])
-            layers.set_probe(probe)
-            for _ in range(min(args.steps, 5)):
-                eager_step()
-            torch.cuda.synchronize()
-            layers.set_probe(None)
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-    images = args.batch * world * args.steps
-    value = images / dt
+    probe_steps = 0 if args.no_probe else 5
+    value, dt, roof, launch = run_mode(args, args.precision, args.steps, args.warmup, dev, rank, world, ddp,
+                                       probe_steps)
+    parity = None
+    if args.fp32_steps > 0 and args.precision != "fp32" and world == 1:
+        v32, dt32, roof32, launch32 = run_mode(args, "fp32", args.fp32_steps, 3, dev, rank, world, ddp,
+                                               2 if probe_steps else 0)
+        parity = {"dtype": "fp32", "value": round(v32, 2), "unit": "images/s", "steps": args.fp32_steps,
+                  "ms_per_step": round(dt32 / args.fp32_steps * 1e3, 3), "step_launch": launch32,
+                  "step_mfma_frac": round(STEP_FLOP_PER_IMAGE[args.arch] * v32 / 1e12 / PEAK_TFLOPS["fp32"], 4),
+                  "roofline": roof32,
+                  "note": "exact fp32 MFMA (v_mfma_f32_16x16x4_f32), the mode tests/test_train_step_gpu.py "
+                          "pins to the reference within 1e-4"}
 
     if rank == 0:
-        roof = None
-        if probe is not None:
-            stats = probe.summary()
-            flops = conv_flops_per_image(args.arch) * args.batch
-            dom = max(stats, key=lambda k: stats[k]["total_ms"])
-            avg_ms = stats[dom]["avg_ms"]
-            achieved = flops / (avg_ms * 1e-3) / 1e12
-            peak = PEAK_TFLOPS[args.precision]
-            traffic, tnote = None, None
-            if dom == "G0.c5.fwd" and args.arch == "neutron" and os.path.exists(TRAFFIC_JSON):
-                tj = json.load(open(TRAFFIC_JSON))
-                traffic = tj["traffic_bytes"]
-                tnote = (f"bytes per launch: FETCH_SIZE x2 {tj['fetch_bytes']} + WRITE_SIZE {tj['write_bytes']} "
-                         f"(algorithmic {tj['algorithmic_bytes']}), {os.path.relpath(TRAFFIC_JSON, ROOT)}")
-            roof = {"bound": "mfma", "kernel": f"conv_ring {dom} (generator conv_layers.5)",
-                    "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                    "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_note": tnote,
-                    "avg_ms": round(avg_ms, 4), "launches": stats[dom]["count"],
-                    "all_probed": {k: {"avg_ms": round(v["avg_ms"], 4),
-                                       "tflops": round(flops / (v["avg_ms"] * 1e-3) / 1e12, 2)}
-                                   for k, v in stats.items()}}
         step_flops = STEP_FLOP_PER_IMAGE[args.arch] * value
         out = {
             "metric": "GAN-step images/sec (44x44 ZDC) at 1/2/4/8 MI355X; conv MFMA util %",
             "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
-            "step_launch": "hip_graph" if use_graph else "eager",
+            "step_launch": launch,
             "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
-            "config": {"workload": f"{args.arch} 44x44 MoE-GAN train_step, E={args.experts}, B={args.batch} per GPU "
-                                   f"(BASELINE configs[1])", "arch": args.arch, "n_experts": args.experts,
-                       "global_batch": args.batch * world, "image": "44x44" if args.arch == "neutron" else "56x30",
+            "config": {"workload": workload_label(args.arch, args.experts, args.batch, world),
+                       "arch": args.arch, "n_experts": args.experts, "batch_per_gpu": args.batch,
+                       "global_batch": args.batch * world, "image": IMAGE[args.arch],
                        "parallelism": f"dp{world}"},
             "step_tflops": round(step_flops / 1e12, 2),
             "step_mfma_frac": round(step_flops / 1e12 / PEAK_TFLOPS[args.precision], 4),
             "roofline": roof,
         }
+        if parity is not None:
+            out["parity_fp32"] = parity
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.arch)
         print(json.dumps(out), flush=True)

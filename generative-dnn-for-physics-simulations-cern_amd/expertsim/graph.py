@@ -18,9 +18,14 @@ from __future__ import annotations
 import torch
 
 
+def graph_supported(moe) -> bool:
+    """True when ``moe.train_step`` issues no host synchronisation and can be captured."""
+    return moe.n_experts == 1 and moe.ddp is None
+
+
 class StepGraph:
     def __init__(self, moe, step_args, warmup: int = 2):
-        if moe.n_experts != 1 or moe.ddp is not None:
+        if not graph_supported(moe):
             raise ValueError("StepGraph captures single-process, single-expert train steps only")
         self.moe = moe
         self.args = tuple(step_args)

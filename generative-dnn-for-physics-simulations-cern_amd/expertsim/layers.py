@@ -380,11 +380,11 @@ class defer_num_batches:
         self.prev, _NBT_PENDING = _NBT_PENDING, ({} if on else None)
         return self
 
-    def __exit__(self, *exc):
+    def __exit__(self, exc_type, exc, tb):
         global _NBT_PENDING
         pending, _NBT_PENDING = _NBT_PENDING, self.prev
-        if pending is None:
-            return False
+        if pending is None or exc_type is not None:
+            return False     # a failed step applies none of its BatchNorm batch counts
         by_count = {}
         for t, k in pending.values():
             by_count.setdefault(k, []).append(t)

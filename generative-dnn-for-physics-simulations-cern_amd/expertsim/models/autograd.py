@@ -5,7 +5,9 @@ Forward/backward run the explicit HIP programs; parameter gradients are accumula
 into each module's flat gradient buffer (its ``p.grad`` views), which is where the fused Adam of
 expertsim.optim reads them.  Gradients w.r.t. noise / cond are not produced (the reference never
 needs them).  Dropout streams for module calls outside MoEWrapper.train_step come from a
-per-module call counter."""
+per-module call counter, or — to replay a given run's masks, e.g. the reference goldens — from
+``module.dropout_keys``, a list of (seed, stream_base) pairs consumed one per forward call
+(stream_base = expertsim.utils.philox.dropout_stream(step, expert, pass, 0))."""
 from __future__ import annotations
 
 import torch
@@ -17,12 +19,21 @@ def _img_tensor(act: Act):
     return act.torch_nchw()
 
 
+def _dropout_key(module, pass_offset):
+    keys = getattr(module, "dropout_keys", None)
+    if keys:
+        seed, base = keys.pop(0)
+        return int(seed), int(base)
+    module._calls = getattr(module, "_calls", 0) + 1
+    return torch.initial_seed(), (1 << 30) + module._calls * 8 + pass_offset
+
+
 class _GenFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, noise, cond, flat, module):
-        module._calls = getattr(module, "_calls", 0) + 1
-        img, c = module.fwd(noise.contiguous(), cond.contiguous(), seed=torch.initial_seed(),
-                            stream_base=(1 << 30) + module._calls * 8, train=module.training)
+        seed, base = _dropout_key(module, 0)
+        img, c = module.fwd(noise.contiguous().float(), cond.contiguous().float(), seed=seed, stream_base=base,
+                            train=module.training)
         ctx.module, ctx.c = module, c
         return _img_tensor(img).clone()
 
@@ -52,9 +63,8 @@ class _DiscFn(torch.autograd.Function):
 class _AuxFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, img, flat, module):
-        module._calls = getattr(module, "_calls", 0) + 1
-        out, c = module.fwd(Act.of(img.contiguous().float()), seed=torch.initial_seed(),
-                            stream_base=(1 << 30) + module._calls * 8 + 2, train=module.training)
+        seed, base = _dropout_key(module, 2)
+        out, c = module.fwd(Act.of(img.contiguous().float()), seed=seed, stream_base=base, train=module.training)
         ctx.module, ctx.c = module, c
         ctx.need_img = img.requires_grad
         return out.rows2d().clone()

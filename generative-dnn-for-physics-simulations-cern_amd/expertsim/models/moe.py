@@ -13,7 +13,8 @@ on the device; the only host synchronisation is the expert-size read when n_expe
 
 Randomness: noise / Gumbel draws come from device Philox streams unless ``noise_fn`` /
 ``gumbel_fn`` inject them (parity tests); dropout masks are Philox streams keyed by
-(step, rank, expert, pass, layer) — expertsim/utils/philox.py.
+(step, expert, pass, layer), with the data-parallel rank in the Philox key (``philox.rank_seed``)
+so ranks draw independent noise, Gumbel and dropout — expertsim/utils/philox.py.
 
 Data parallel (expertsim/train/ddp.py): with ``self.ddp`` set, each rank routes its own shard,
 gradients of every optimizer phase are all-reduced (RCCL) before the fused Adam.
@@ -60,14 +61,28 @@ class MoEWrapper(nn.Module):
         self.g_steps = [0 for _ in range(n_experts)]
         self.d_steps = [0 for _ in range(n_experts)]
         self.rng_seed = int(cfg_get(cfg, "train.rng_seed", 1234))
+        self._rank = 0
         self.rng = DeviceRNG(self.rng_seed)
         self.noise_fn = None       # optional injection: fn(expert, which, shape) -> tensor
         self.gumbel_fn = None      # optional injection: fn(shape) -> Exp(1) tensor
         self.ddp = None            # expertsim.train.ddp.DataParallel (set by the loop)
-        self.rank = 0
         self.step_count = 0
         self._dstep = None         # device int32 step counter: dropout / noise streams (graph replay)
         self.set_precision(cfg_get(cfg, "train.precision", "fp32"))
+
+    @property
+    def rank(self) -> int:
+        return self._rank
+
+    @rank.setter
+    def rank(self, r: int):
+        """Data-parallel rank: re-keys the noise / Gumbel / dropout Philox streams of this rank."""
+        self._rank = int(r)
+        self.rng = DeviceRNG(philox.rank_seed(self.rng_seed, self._rank))
+
+    @property
+    def dropout_seed(self) -> int:
+        return philox.rank_seed(self.rng_seed, self._rank)
 
     def set_precision(self, precision: str):
         """fp32: every GEMM on fp32 MFMA (parity mode).  bf16: generator and aux-regressor GEMM
@@ -244,13 +259,13 @@ class MoEWrapper(nn.Module):
         # (DDP: local weight B_e^r / B_r; the all-reduce averages, see expertsim/train/ddp.py)
         w = float(np.float32(be) / np.float32(B))
         w_dev = torch.full((1,), w, dtype=torch.float32, device=dev)
-        rank = self.rank
         # the step term (step * 1024) is added on the device from self._dstep
-        sb = lambda pid: philox.dropout_stream(0, e, pid, 0, rank)
+        sb = lambda pid: philox.dropout_stream(0, e, pid, 0)
+        seed = self.dropout_seed
 
         # ---- generator forward #1 (moe.py:144-145)
         n1 = self._noise(e, 0, (be, self.noise_dim), dev)
-        fake1, gctx1 = G.fwd(n1, sc, seed=self.rng_seed, stream_base=sb(philox.PASS_G1))
+        fake1, gctx1 = G.fwd(n1, sc, seed=seed, stream_base=sb(philox.PASS_G1))
 
         # ---- discriminator step (moe.py:506-527)
         ro, _, dctx_r = D.fwd(Act.of(sr), sc)
@@ -266,12 +281,12 @@ class MoEWrapper(nn.Module):
 
         # ---- generator step (moe.py:529-571)
         n2 = self._noise(e, 1, (be, self.noise_dim), dev)
-        fake2, gctx2 = G.fwd(n2, sc, seed=self.rng_seed, stream_base=sb(philox.PASS_G2))
+        fake2, gctx2 = G.fwd(n2, sc, seed=seed, stream_base=sb(philox.PASS_G2))
         fo1, fl1, dctx1 = D.fwd(fake1, sc)
         _, fl2, dctx2 = D.fwd(fake2, sc)
         s = torch.empty(be, dtype=torch.float32, device=dev)
         hip.call("es_image_expsum", C.byref(fake1.view), fake1.dt, fake1.ptr, hip.ptr(s), hip.stream_ptr())
-        coords, actx = A.fwd(fake1, seed=self.rng_seed, stream_base=sb(philox.PASS_AUX))
+        coords, actx = A.fwd(fake1, seed=seed, stream_base=sb(philox.PASS_AUX))
         L = fl1.dims[1]
         p = hip.GenLoss()
         p.n, p.latent, p.noise = be, L, self.noise_dim

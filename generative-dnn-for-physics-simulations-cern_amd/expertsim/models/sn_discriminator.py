@@ -170,11 +170,11 @@ class SNDiscriminator(ExpertModule):
         The spectral-norm weight_orig gradients of the layers are issued together at the end
         (SpectralNorm.bwd_many: the small layers share one launch)."""
         sn_jobs = []
-        try:
-            return self._bwd(ctx, dout, dlat, weight_grads, input_grad, sn_jobs)
-        finally:
-            if sn_jobs:
-                SpectralNorm.bwd_many(sn_jobs, beta=1.0)
+        dimg = self._bwd(ctx, dout, dlat, weight_grads, input_grad, sn_jobs)
+        # only on the normal return path: a failed _bwd leaves no half-issued gradient launch
+        if sn_jobs:
+            SpectralNorm.bwd_many(sn_jobs, beta=1.0)
+        return dimg
 
     def _bwd(self, ctx, dout, dlat, weight_grads, input_grad, sn_jobs):
         o = self.ops()

@@ -49,7 +49,7 @@ def save_models_and_architectures(filepath_models, n_experts, aux_regs, aux_reg_
 
 def save_training_state(filepath_models, epoch, moe, ema_helper=None):
     state = {"epoch": int(epoch), "step_count": _device_step(moe), "g_steps": list(moe.g_steps),
-             "d_steps": list(moe.d_steps), "rng_counter": int(moe.rng.counter), "rng_seed": int(moe.rng.seed)}
+             "d_steps": list(moe.d_steps), "rng_counter": int(moe.rng.counter), "rng_seed": int(moe.rng_seed)}
     if ema_helper is not None:
         state["ema"] = ema_helper.state_dict()
     torch.save(state, _path(filepath_models, "train_state", epoch))
@@ -103,8 +103,9 @@ def load_checkpoint(checkpoint_dir, epoch, moe, gen_optims, disc_optims, aux_reg
     if getattr(moe, "_dstep", None) is not None:
         moe._dstep.fill_(moe.step_count)
     moe.g_steps, moe.d_steps = list(st["g_steps"]), list(st["d_steps"])
+    moe.rng_seed = int(st["rng_seed"])     # base Philox key of dropout / noise / Gumbel draws
+    moe.rank = moe.rank                    # re-key this rank's device RNG from the base seed
     moe.rng.counter = int(st["rng_counter"])
-    moe.rng_seed = moe.rng.seed = int(st["rng_seed"])      # dropout / noise / Gumbel Philox key
     if ema_helper is not None and "ema" in st:
         ema_helper.load_state_dict(st["ema"])
     return st

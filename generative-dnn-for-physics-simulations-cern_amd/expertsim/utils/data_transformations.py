@@ -292,5 +292,7 @@ def get_train_test_data_loaders(cfg, rank: int = 0, world: int = 1, device=None)
     resident = bool(cfg.dataset.get("resident", True)) and torch.cuda.is_available()
     if device is None and resident:
         device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
-    return (_make_loader(train, bs, True, resident, device),
+    # the reference's DataLoader keeps the last partial batch (data_transformations.py:275,298);
+    # data-parallel ranks drop it so every rank runs the same number of equal-sized steps
+    return (_make_loader(train, bs, world > 1, resident, device),
             _make_loader(test, bs, False, resident, device))

@@ -14,9 +14,16 @@ The golden-capture script feeds exactly these masks to the reference, so masks a
 across reference, oracle and HIP kernels.
 
 Stream ids (one per dropout call site, see ``dropout_stream``) are:
-    stream = step * 1024 + rank * 512 + expert * 32 + pass_id * 8 + layer
+    stream = step * 1024 + expert * 32 + pass_id * 8 + layer        (expert < 32, layer < 8)
 with pass_id 0 = generator forward #1 (moe.py:145), 1 = generator forward #2 (moe.py:538),
-2 = auxiliary regressor forward (moe.py:557).
+2 = auxiliary regressor forward (moe.py:557).  Counter word 3 is 0 for dropout; the device noise
+and Gumbel draws (csrc/misc.hip randn / rand_exp) use 0x5EED0001 / 0x5EED0002 there, so the three
+families never share a Philox block whatever their stream ids.
+
+Data parallelism: the rank lives in the key, not in the stream id — every rank keys its dropout,
+noise and Gumbel draws with ``rank_seed(seed, rank)`` (rank in the key's high word; rank 0 keeps
+the plain seed, so single-device runs and the goldens are unchanged).  Ranks therefore draw
+independent masks and noise at every (step, expert, pass, layer).
 """
 from __future__ import annotations
 
@@ -31,8 +38,15 @@ MASK32 = np.uint64(0xFFFFFFFF)
 PASS_G1, PASS_G2, PASS_AUX = 0, 1, 2
 
 
-def dropout_stream(step: int, expert: int, pass_id: int, layer: int, rank: int = 0) -> int:
-    return int(step) * 1024 + int(rank) * 512 + int(expert) * 32 + int(pass_id) * 8 + int(layer)
+def dropout_stream(step: int, expert: int, pass_id: int, layer: int) -> int:
+    if not (0 <= expert < 32 and 0 <= pass_id < 4 and 0 <= layer < 8):
+        raise ValueError(f"dropout_stream: expert {expert} / pass {pass_id} / layer {layer} out of range")
+    return int(step) * 1024 + int(expert) * 32 + int(pass_id) * 8 + int(layer)
+
+
+def rank_seed(seed: int, rank: int) -> int:
+    """Philox key of a data-parallel rank: the rank is added to the key's high word."""
+    return (int(seed) + (int(rank) << 32)) & 0xFFFFFFFFFFFFFFFF
 
 
 def keep_threshold(p: float) -> int:

@@ -194,11 +194,12 @@ class Dropper:
     """Counter-based dropout for one module pass (layer index advances per call)."""
 
     def __init__(self, seed, step, expert, pass_id, rank=0):
-        self.seed, self.step, self.expert, self.pass_id, self.rank = seed, step, expert, pass_id, rank
+        # data-parallel ranks key their masks with the rank in the key (philox.rank_seed)
+        self.seed, self.step, self.expert, self.pass_id = philox.rank_seed(seed, rank), step, expert, pass_id
         self.layer = 0
 
     def __call__(self, x, p):
-        stream = philox.dropout_stream(self.step, self.expert, self.pass_id, self.layer, self.rank)
+        stream = philox.dropout_stream(self.step, self.expert, self.pass_id, self.layer)
         self.layer += 1
         mask = torch.from_numpy(philox.dropout_mask(tuple(x.shape), p, self.seed, stream))
         noise = mask.to(x.dtype)

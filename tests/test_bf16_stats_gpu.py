@@ -1,0 +1,104 @@
+"""Statistical parity of the bf16 performance mode (last row).
+
+bf16 GEMM operands / activations are not elementwise-comparable with the reference's fp32, so the
+bench's mode is validated on what the training run produces.  Three runs of the same neutron 44x44
+E=1 train loop, B=64, 20 steps, identical seeds, data batches and injected noise:
+  * ORC — the oracle (torch CPU fp32 restatement pinned bit-exactly to the reference's goldens);
+  * F32 — the HIP path in fp32 parity mode;
+  * B16 — the HIP path in bf16 mode (what bench.py measures).
+
+Checked (tolerances from the measured spread):
+  1. loss trajectories: for each of gen / disc / div / intensity / aux losses,
+     max_step |run_s - ORC_s| / mean_step |ORC_s|  <=  TRAJ_TOL[run];
+  2. generated photon-sum / 5-channel-sum distributions after training (eval-mode generators, 1024
+     fixed conditions and noise, expm1 -> the reference's channel sums, train/utils.py:62-78):
+     the per-channel Wasserstein distance between a run and ORC, relative to ORC's channel mean,
+     <= WS_TOL[run]; for scale, the natural spread is the same distance between two ORC
+     generations with independent noise (printed).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+B, STEPS, N_EVAL = 64, 20, 1024
+KEYS = ("gen_loss", "disc_loss", "div_loss", "intensity_loss", "aux_reg_loss")
+TRAJ_TOL = {"fp32": 0.02, "bf16": 0.10}
+WS_TOL = {"fp32": 0.02, "bf16": 0.10}
+
+
+def _inputs():
+    from expertsim.utils.synthetic import make_batch
+    gen = torch.Generator().manual_seed(11)
+    steps = []
+    for s in range(STEPS):
+        b = {k: torch.from_numpy(v) for k, v in make_batch(B, "neutron", seed=500 + s).items()}
+        noise = {(0, w): torch.randn(B, 10, generator=gen) for w in (0, 1)}
+        gum = torch.empty(B, 1).exponential_(generator=gen)
+        steps.append((b, noise, gum))
+    ev = make_batch(N_EVAL, "neutron", seed=900)
+    eval_cond = torch.from_numpy(ev["cond"])
+    eval_noise = [torch.randn(N_EVAL, 10, generator=gen) for _ in range(2)]
+    return steps, eval_cond, eval_noise
+
+
+def _hip_run(precision, steps, eval_cond, eval_noise):
+    import bench
+    moe, (og, od, oa, orr), cfg = bench.build("neutron", 1, precision, 1234, torch.device(DEV))
+    traj = []
+    for b, noise, gum in steps:
+        moe.noise_fn = lambda e, w, shape, _n=noise: _n[(e, w)]
+        moe.gumbel_fn = lambda shape, _g=gum: _g
+        t = lambda k: b[k].to(DEV)
+        m = moe.train_step(0, t("cond"), t("real_images").unsqueeze(1), t("true_positions"), t("std"),
+                           t("intensity"), oa, og, od, orr, None, DEV)
+        traj.append({k: float(m[k]) for k in KEYS})
+    with torch.no_grad():
+        img, _ = moe.generators[0].fwd(eval_noise[0].to(DEV), eval_cond.to(DEV), train=False)
+        x = img.torch_nchw().float().cpu().numpy()[:, 0]
+    return traj, x
+
+
+def _oracle_run(steps, eval_cond, eval_noise):
+    from oracle import expertsim_oracle as O
+    m = O.OracleMoE("neutron", 1, dict(O.DEFAULT_CFG), seed=1234)
+    traj = []
+    for b, noise, gum in steps:
+        met, _ = m.train_step(0, b["cond"], b["real_images"].unsqueeze(1), b["true_positions"], b["std"],
+                              b["intensity"], lambda e, w, shape, _n=noise: _n[(e, w)], gum)
+        traj.append({k: met[k] for k in KEYS})
+    with torch.no_grad():
+        P = m.state["G"][0]
+        xs = [O.generator_forward("neutron", P, n, eval_cond, training=False)[:, 0].numpy() for n in eval_noise]
+    return traj, xs
+
+
+def _ws_rel(x, ref):
+    from oracle import expertsim_oracle as O
+    a, r = O.channel_sums(np.expm1(x.astype(np.float64))), O.channel_sums(np.expm1(ref.astype(np.float64)))
+    return max(O.wasserstein_1d(a[:, i], r[:, i]) / max(abs(r[:, i].mean()), 1e-9) for i in range(5))
+
+
+@pytest.mark.timeout(400)
+def test_bf16_training_statistics_match_fp32_and_oracle():
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    steps, eval_cond, eval_noise = _inputs()
+    orc, orc_x = _oracle_run(steps, eval_cond, eval_noise)
+    runs = {p: _hip_run(p, steps, eval_cond, eval_noise) for p in ("fp32", "bf16")}
+    natural = _ws_rel(orc_x[1], orc_x[0])
+    report = {}
+    for p, (traj, x) in runs.items():
+        dev = {}
+        for k in KEYS:
+            ref = np.array([s[k] for s in orc])
+            mine = np.array([s[k] for s in traj])
+            dev[k] = float(np.max(np.abs(mine - ref)) / max(np.mean(np.abs(ref)), 1e-12))
+        ws = _ws_rel(x, orc_x[0])
+        report[p] = (dev, ws)
+        print(f"{p}: trajectory max-dev / mean|ref| {dev}; WS(run, ORC)/mean {ws:.4g}; "
+              f"natural WS(ORC noise a, b)/mean {natural:.4g}")
+    for p, (dev, ws) in report.items():
+        for k, d in dev.items():
+            assert d <= TRAJ_TOL[p], (p, k, d)
+        assert ws <= WS_TOL[p], (p, ws, natural)

@@ -1,0 +1,168 @@
+"""Gradients of the HIP train step against the reference's recorded gradients.
+
+The goldens (tests/golden/make_goldens.py:220-233) hold, for every optimizer step of the reference,
+a checksum of each parameter's gradient as it enters ``Adam.step`` (sum, |.|-sum, L2 norm and 64
+strided samples).  Here the HIP path's gradients are captured at the same point (the flat
+gradient buffer each FusedAdam reads) and compared with SURVEY.md §8(c)'s contract:
+
+  * norm-relative error <= 1e-2 (neutron, BatchNorm after every conv + dropout) / 1e-3 (proton),
+    on the 64 sampled elements (||g_s - g_s,ref|| / ||g_s,ref||) and on the full L2 norm;
+  * the noise-only set — biases that feed a normalisation with per-channel statistics, whose
+    analytic gradient is exactly zero (neutron G fc1.0 / fc2.0 / conv_layers.{0,5,9} biases, the
+    neutron aux regressor's BN-fed conv biases, the proton aux regressor's GroupNorm(C, C)-fed
+    residual biases) — is checked absolutely: ||g|| <= 1e-5;
+  * step 0 is the contract step.  At step 1 every parameter has moved by +-lr through Adam's
+    first step whatever its gradient's size (SURVEY.md §8(c) hard part (c)), so rounding-level
+    sign flips of tiny step-0 gradients change the step-1 gradients; they are held to the
+    STEP1_TOL norm-relative bound (the reference's own sensitivity, see test_train_step_gpu.py).
+
+A second test drives the same step through the reference's nn.Module API — ``G(noise, cond)``,
+``D(img, cond)``, ``A(img)``, losses in torch, ``loss.backward()``, ``opt.step()`` — i.e. the
+drop-in path of INTEGRATION.md, and holds its outputs and gradients to the same goldens.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from golden_utils import CASES, Golden, checksum
+from test_train_step_gpu import _build
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL = {"neutron": 1e-2, "proton": 1e-3}
+STEP1_TOL = {"neutron": 0.25, "proton": 0.25}
+NOISE_ONLY = {
+    "neutron": {"G": {"fc1.0.bias", "fc2.0.bias", "conv_layers.0.bias", "conv_layers.5.bias",
+                      "conv_layers.9.bias"},
+                "A": {"feature_extractor.conv1.bias", "feature_extractor.conv2.bias",
+                      "feature_extractor.conv3.bias", "feature_extractor.conv4.bias"}},
+    "proton": {"A": {"feature_extractor.res1.conv1.0.bias", "feature_extractor.res1.conv2.0.bias",
+                     "feature_extractor.res1.downsample.0.bias"}},
+}
+
+
+def _capture(opts_by_label, store):
+    """Wrap each FusedAdam.step: snapshot the module's parameter gradients before the update."""
+    for label, (opt, module) in opts_by_label.items():
+        orig = opt.step
+
+        def step(*a, _orig=orig, _label=label, _module=module, **k):
+            store[_label] = {n: p.grad.detach().double().cpu().numpy().copy()
+                             for n, p in _module.named_parameters()}
+            return _orig(*a, **k)
+        opt.step = step
+
+
+def grad_errors(g: Golden, s, label, grads, arch, comp):
+    """[(name, kind, err)] for every parameter of one optimizer step."""
+    out = []
+    noise = NOISE_ONLY.get(arch, {}).get(comp, set())
+    for n, gm in grads.items():
+        key = f"s{s}/{label}/grad/{n}"
+        assert g.has(key), key
+        ref = g[key]
+        c = checksum(gm)
+        if n in noise or ref[2] == 0.0:
+            out.append((n, "abs", float(c[2])))
+            continue
+        samp = float(np.linalg.norm(c[3:] - ref[3:]) / max(np.linalg.norm(ref[3:]), 1e-30))
+        l2 = float(abs(c[2] - ref[2]) / ref[2])
+        out.append((n, "rel", max(samp, l2)))
+    return out
+
+
+def _check(errs, tol, what):
+    worst = max((e for e in errs if e[1] == "rel"), key=lambda e: e[2], default=None)
+    print(what, "worst rel:", worst, "worst abs:",
+          max((e for e in errs if e[1] == "abs"), key=lambda e: e[2], default=None))
+    for n, kind, e in errs:
+        if kind == "abs":
+            assert e <= 1e-5, (what, n, e)
+        else:
+            assert e <= tol, (what, n, e)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_step_gradients_match_reference(case):
+    g = Golden(case)
+    moe, (og, od, oa, orr), cfg = _build(g)
+    store = {}
+    labels = {}
+    for e in range(g.E):
+        labels[f"optG{e}"] = (og[e], moe.generators[e])
+        labels[f"optD{e}"] = (od[e], moe.discriminators[e])
+        labels[f"optA{e}"] = (oa[e], moe.aux_regs[e])
+    labels["optR"] = (orr, moe.router)
+    _capture(labels, store)
+    for s in range(g.steps):
+        store.clear()
+        inp = g.inputs(s)
+        nz = g.noise(s)
+        moe.noise_fn = lambda e, w, shape: torch.from_numpy(nz[(e, w)])
+        gum = torch.from_numpy(g.gumbel(s))
+        moe.gumbel_fn = lambda shape: gum
+        t = lambda k: torch.from_numpy(inp[k]).to(DEV)
+        moe.train_step(g.epoch, t("cond"), t("real_images").unsqueeze(1), t("true_positions"), t("std"),
+                       t("intensity"), oa, og, od, orr, None, DEV)
+        torch.cuda.synchronize()
+        want = {k.split("/")[1] for k in g.keys(f"s{s}/") if "/grad/" in k}
+        assert set(store) == want, (s, sorted(store), sorted(want))
+        tol = TOL[g.arch] if s == 0 else STEP1_TOL[g.arch]
+        for label, grads in store.items():
+            comp = label[3]
+            _check(grad_errors(g, s, label, grads, g.arch, comp), tol, (case, s, label))
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if "_e1_" in c])
+def test_module_api_backward_matches_reference(case):
+    """The reference's call pattern (moe.py:506-571) through the nn.Module API + loss.backward()."""
+    from oracle import expertsim_oracle as O
+    g = Golden(case)
+    moe, (og, od, oa, orr), cfg = _build(g)
+    G, D, A = moe.generators[0], moe.discriminators[0], moe.aux_regs[0]
+    store = {}
+    _capture({"optG0": (og[0], G), "optD0": (od[0], D), "optA0": (oa[0], A)}, store)
+    inp = g.inputs(0)
+    nz = g.noise(0)
+    t = lambda k: torch.from_numpy(inp[k]).to(DEV)
+    cond, real, pos, std, inten = t("cond"), t("real_images").unsqueeze(1), t("true_positions"), t("std"), \
+        t("intensity")
+    n1, n2 = (torch.from_numpy(nz[(0, w)]).to(DEV) for w in (0, 1))
+    # the reference's step-0 dropout masks: (seed, dropout_stream(0, expert 0, pass, 0))
+    G.dropout_keys = [(g.seed, 0), (g.seed, 8)]
+    A.dropout_keys = [(g.seed, 16)]
+    for o in (og[0], od[0], oa[0]):
+        o.zero_grad(set_to_none=True)
+    w = 1.0                                           # class_counts_adjusted with one expert
+
+    fake = G(n1, cond)                                # moe.py:145
+    ro, _ = D(real, cond)                             # discriminator_train_step, moe.py:513-527
+    fo, _ = D(fake.detach(), cond)
+    d_loss = (F.relu(1.0 - ro).mean() + F.relu(1.0 + fo).mean()) * w
+    d_loss.backward()
+    od[0].step()
+
+    fake2 = G(n2, cond)                               # generator_train_step, moe.py:535-566
+    fo1, fl1 = D(fake, cond)
+    _, fl2 = D(fake2, cond)
+    gen = -fo1.mean()
+    div = O.sdi_gan_regularization(fl1, fl2, n1, n2, std, G.di_strength)
+    il = O.intensity_regularization(fake, inten, G.in_strength)[0]
+    coords = A(fake)
+    aux = A.regressor_loss(pos, coords) * cfg.model.aux_reg.strength
+    g_loss = (gen + div + il + aux) * w
+    g_loss.backward()
+    og[0].step()
+    oa[0].step()
+    torch.cuda.synchronize()
+
+    rel = lambda a, b: float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-6))
+    assert rel(fake.detach().cpu().numpy(), g["s0/G0/call0/out0"]) <= 1e-4
+    assert rel(fake2.detach().cpu().numpy(), g["s0/G0/call1/out0"]) <= 1e-4
+    assert rel(coords.detach().cpu().numpy(), g["s0/A0/call0/out0"]) <= 1e-4
+    gm = g.metrics(0)
+    assert abs(float(d_loss) - gm["disc_loss"]) <= 1e-4 * max(abs(gm["disc_loss"]), 1e-3)
+    assert abs(float(g_loss) - gm["gen_loss"]) <= 1e-4 * max(abs(gm["gen_loss"]), 1e-3)
+    for label, grads in store.items():
+        _check(grad_errors(g, 0, label, grads, g.arch, label[3]), TOL[g.arch], (case, "module-api", label))

@@ -1,6 +1,7 @@
 """Run ONE conv op of the neutron generator a few times (for rocprofv3 --pmc passes).
 
-usage: python tools/mb_one.py <c0|c5|c9> <fwd|dgrad|wgrad> [ring 1|0] [reps]"""
+usage: python tools/mb_one.py <c0|c5|c9> <fwd|dgrad|wgrad> [ring 1|0] [reps]
+(ES_MB_BATCH=<images> overrides the batch of 512)"""
 import os
 import sys
 
@@ -21,6 +22,7 @@ def main():
     ring = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     reps = int(sys.argv[4]) if len(sys.argv) > 4 else 5
     N, Cin, H, W, Cout, k, st, pad, up = SHAPES[layer]
+    N = int(os.environ.get("ES_MB_BATCH", N))
     dev = "cuda"
     hip.lib().es_conv_set_ring(ring)
     w = torch.nn.Parameter(torch.randn(Cout, Cin, k, k, device=dev) / (Cin * k * k) ** 0.5)
