@@ -31,10 +31,11 @@ sys.path.insert(0, PKG_DIR)
 sys.path.insert(0, ROOT)
 
 # algorithmic FLOPs per image per train_step (torch FlopCounterMode on the
-# reference): neutron 10.573 GFLOP, proton 28.566 GFLOP
-STEP_FLOP_PER_IMAGE = {"neutron": 10.573e9, "proton": 28.566e9}
+# reference): neutron 10.573 GFLOP, proton 28.566 GFLOP; the declared 56x56 extension (configs[4],
+# no reference model) 16.868 GFLOP = 6*2746.3 + 12*8.05 + 3*97.9 MFLOP (same counter on the oracle)
+STEP_FLOP_PER_IMAGE = {"neutron": 10.573e9, "proton": 28.566e9, "neutron56": 16.868e9}
 PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
-IMAGE = {"neutron": "44x44", "proton": "56x30"}
+IMAGE = {"neutron": "44x44", "proton": "56x30", "neutron56": "56x56"}
 
 
 def traffic_json(arch, batch):
@@ -52,6 +53,8 @@ def workload_label(arch, E, batch, world):
         k = "configs[2]"
     elif arch == "neutron" and E == 4 and gb == 2048:
         k = "configs[3]"
+    elif arch == "neutron56" and E == 8 and gb == 4096:
+        k = "configs[4], declared 56x56 extension, parity unpinned"
     elif E == 1 and batch in (512, 1024) and world > 1:
         k = f"configs[{1 if batch == 512 else 2}] per GPU, weak-scaled over {world} GPUs"
     else:
@@ -65,6 +68,8 @@ def conv_flops_per_image(arch):
     each of its fwd / dgrad / wgrad launches, as torch's flop counter does)."""
     if arch == "neutron":   # conv_layers.5: 256x48x48 -> 128x46x46, k3
         return 2 * 46 * 46 * 128 * (256 * 9)
+    if arch == "neutron56":  # conv_layers.5: 256x60x60 -> 128x58x58, k3
+        return 2 * 58 * 58 * 128 * (256 * 9)
     return 2 * 55 * 29 * 128 * (256 * 16)   # proton conv_layers.5: 256x56x30 -> 128x55x29, k4 p1
 
 
@@ -233,7 +238,7 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=1024, help="images per GPU")
-    ap.add_argument("--arch", default="neutron")
+    ap.add_argument("--arch", default="neutron", choices=["neutron", "proton", "neutron56"])
     ap.add_argument("--experts", type=int, default=1)
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--fp32-steps", type=int, default=30, help="timed steps of the fp32 parity-mode line (0: skip)")

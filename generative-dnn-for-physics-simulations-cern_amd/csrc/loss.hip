@@ -216,6 +216,84 @@ __global__ void __launch_bounds__(256) router_alb_kernel(const float* gates, int
     for (int e = 0; e < E; ++e) dlogits[b * E + e] = gates[b * E + e] * (gS[e] - dot) / tau;
   }
 }
+// Expert-distribution (ED) pair sums, train/utils.py:372-395 with gating = the straight-through
+// one-hot gates (moe.py:103,264): T[a,e] = sum_{b: idx_b = e} |f_a - f_b| (cdist p=2 of the [B,1]
+// per-sample photon sums).  One thread per (a, e); f / idx staged through LDS in 1024-row tiles.
+__global__ void __launch_bounds__(256) router_ed_pairs_kernel(const float* feat, const int32_t* idx, int B, int E,
+                                                              float* T) {
+  __shared__ float fs[1024];
+  __shared__ int32_t is[1024];
+  const int a = blockIdx.x * blockDim.x + threadIdx.x, e = blockIdx.y;
+  const float fa = a < B ? feat[a] : 0.f;
+  float acc = 0.f;
+  for (int b0 = 0; b0 < B; b0 += 1024) {
+    const int nb = min(1024, B - b0);
+    __syncthreads();
+    for (int j = threadIdx.x; j < nb; j += blockDim.x) {
+      fs[j] = feat[b0 + j];
+      is[j] = idx[b0 + j];
+    }
+    __syncthreads();
+    for (int j = 0; j < nb; ++j) acc += is[j] == e ? fabsf(fa - fs[j]) : 0.f;
+  }
+  if (a < B) T[a * E + e] = acc;
+}
+
+// Router loss terms with gradient into the router (moe.py:258-268,407-434; train/utils.py:372-419,
+// 623-642) and d loss / d logits through the Gumbel softmax (gates = softmax(z / tau)):
+//   ALB  = alb_coef * mean_e exp(1 / (S_e + 1e-6)),      S_e = sum_b gates[b,e]
+//   ENT  = util * sum_e avg_e log(avg_e + 1e-9),          avg_e = S_e / B  (= -entropy * util)
+//   ED   = 0.1 * ed / B * sum_a T[a, idx_a]               (T from router_ed_pairs_kernel, or none)
+// d/dgates[b,e] = alb_coef/E exp(inv_e)(-inv_e^2) + util/B (log(avg_e+1e-9) + avg_e/(avg_e+1e-9))
+//               + 0.2 * ed / B * T[b,e];   dlogits = gates * (dG - <gates, dG>) / tau.
+// out[0] = ALB, out[1] = ENT, out[2] = ED.  T aliases dlogits (each row is read before written).
+__global__ void __launch_bounds__(1024) router_loss_kernel(const float* gates, const int32_t* idx, int B, int E,
+                                                           float tau, float alb_coef, float util, float ed,
+                                                           float* out, float* dlogits) {
+  __shared__ float sh[16];
+  __shared__ float gS[64];
+  float L = 0.f, ent = 0.f;
+  for (int e = 0; e < E; ++e) {
+    float s = 0.f;
+    for (int b = threadIdx.x; b < B; b += blockDim.x) s += gates[b * E + e];
+    s = block_sum(s, sh);
+    const float inv = 1.f / (s + 1e-6f);
+    const float ex = expf(inv);
+    L += ex;
+    const float avg = s / (float)B;
+    const float lg = logf(avg + 1e-9f);
+    ent += avg * lg;
+    if (threadIdx.x == 0)
+      gS[e] = alb_coef / (float)E * ex * (-inv * inv) + util / (float)B * (lg + avg / (avg + 1e-9f));
+  }
+  float edsum = 0.f;
+  if (ed != 0.f) {
+    for (int b = threadIdx.x; b < B; b += blockDim.x) edsum += dlogits[b * E + idx[b]];
+    edsum = block_sum(edsum, sh);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out[0] = alb_coef * (L / (float)E);
+    out[1] = util * ent;
+    out[2] = 0.1f * (edsum / (float)B) * ed;
+  }
+  const float ked = 0.2f * ed / (float)B;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    float dg[64];
+    float dot = 0.f;
+    for (int e = 0; e < E; ++e) {
+      dg[e] = gS[e] + (ed != 0.f ? ked * dlogits[b * E + e] : 0.f);
+      dot += gates[b * E + e] * dg[e];
+    }
+    for (int e = 0; e < E; ++e) dlogits[b * E + e] = gates[b * E + e] * (dg[e] - dot) / tau;
+  }
+}
+
+// mean_intensities_in_batch_expert[mask] = s (moe.py:196-198): dst[rows[i]] = src[i]
+__global__ void scatter_rows_kernel(const float* src, const int32_t* rows, int n, float* dst) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[rows ? rows[i] : i] = src[i];
+}
 }  // namespace
 
 extern "C" int es_hinge_d(const float* ro, const float* fo, int n, const float* w_ptr, float* out, float* dro,
@@ -272,6 +350,27 @@ extern "C" int es_router_alb(const float* gates, int B, int E, float tau, float 
   ES_CHECK_ARG(E <= 64, "router_alb: E <= 64");
   hipLaunchKernelGGL(router_alb_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, gates, B, E, tau, coef, out,
                      dlogits);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_router_loss(const float* gates, const int32_t* idx, const float* feat, int B, int E, float tau,
+                              float alb_coef, float util_strength, float ed_strength, float* out, float* dlogits,
+                              es_stream_t stream) {
+  ES_CHECK_ARG(B > 0 && E >= 1 && E <= 64, "router_loss: B=%d E=%d (E <= 64)", B, E);
+  ES_CHECK_ARG(ed_strength == 0.f || (feat && idx), "router_loss: ED needs feat and idx");
+  hipStream_t st = (hipStream_t)stream;
+  if (ed_strength != 0.f)
+    hipLaunchKernelGGL(router_ed_pairs_kernel, dim3((B + 255) / 256, E), dim3(256), 0, st, feat, idx, B, E, dlogits);
+  hipLaunchKernelGGL(router_loss_kernel, dim3(1), dim3(1024), 0, st, gates, idx, B, E, tau, alb_coef, util_strength,
+                     ed_strength, out, dlogits);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_scatter_rows(const float* src, const int32_t* rows, int n, float* dst, es_stream_t stream) {
+  if (n <= 0) return ES_OK;
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, src, rows, n, dst);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }

@@ -105,6 +105,9 @@ _SIGS = {
     "es_image_expsum_bwd": (C.c_int, [P, C.c_int, P, P, P, P, C.c_float, P]),
     "es_router_gumbel": (C.c_int, [P, P, C.c_int, C.c_int, C.c_float, P, P, P, P]),
     "es_router_alb": (C.c_int, [P, C.c_int, C.c_int, C.c_float, C.c_float, P, P, P]),
+    "es_router_loss": (C.c_int, [P, P, P, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, P, P,
+                                 P]),
+    "es_scatter_rows": (C.c_int, [P, P, C.c_int, P, P]),
     "es_adam": (C.c_int, [P, P, P, P, I64, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int,
                           C.c_float, P]),
     "es_adam_dev": (C.c_int, [P, P, P, P, I64, C.c_float, C.c_float, C.c_float, C.c_float, P, C.c_float, P]),

@@ -67,6 +67,7 @@ class MoEWrapper(nn.Module):
         self.gumbel_fn = None      # optional injection: fn(shape) -> Exp(1) tensor
         self.ddp = None            # expertsim.train.ddp.DataParallel (set by the loop)
         self.step_count = 0
+        self._ed_feat = None       # [B] per-sample photon sums for the router's ED term
         self._dstep = None         # device int32 step counter: dropout / noise streams (graph replay)
         self.set_precision(cfg_get(cfg, "train.precision", "fp32"))
 
@@ -176,6 +177,9 @@ class MoEWrapper(nn.Module):
 
         # metrics buffer: per expert [total, gen, div, int, aux, std_int, mean_int, w, disc]
         mbuf = torch.zeros(E, 9, dtype=torch.float32, device=dev)
+        # mean_intensities_in_batch_expert (moe.py:196-198): the ED router term's per-sample features
+        self._ed_feat = (torch.zeros(B, dtype=torch.float32, device=dev)
+                         if E > 1 and float(rc.ed_strength) != 0.0 else None)
         for e, rows, be in groups:
             be_global = be if self.ddp is None else self.ddp.global_count(e)
             if be_global <= 1:                                                   # moe.py:126-135
@@ -193,9 +197,6 @@ class MoEWrapper(nn.Module):
         # ---- router (moe.py:213-449)
         zero = torch.zeros((), dtype=torch.float32, device=dev)
         if E > 1:
-            if rc.util_strength != 0 or rc.ed_strength != 0:
-                raise NotImplementedError("util_strength / ed_strength != 0: not on the HIP path "
-                                          "(reference default is 0)")
             gan = mbuf[:, 0].mean() * rc.gan_strength
             if rc.diff_strength != 0:
                 dli = sum((mbuf[a, 6] - mbuf[b, 6]).abs() for a, b in combinations(range(E), 2)) * rc.diff_strength
@@ -204,23 +205,24 @@ class MoEWrapper(nn.Module):
             diff = -dli * rc.diff_strength
             alpha = min(max(epoch / rc.alpha, 0.0), 1.0)
             dec_w = rc.min_weight + (1.0 - rc.min_weight) * alpha
-            alb_out = torch.zeros(1, dtype=torch.float32, device=dev)
+            # ALB, utilisation entropy and expert-distribution terms + d/dlogits in one program
+            rl = torch.zeros(3, dtype=torch.float32, device=dev)
             dlogits = torch.empty(B, E, dtype=torch.float32, device=dev)
-            if rc.alb_strength != 0:
-                hip.call("es_router_alb", hip.ptr(gates), B, E, float(tau), float(rc.alb_strength * dec_w),
-                         hip.ptr(alb_out), hip.ptr(dlogits), hip.stream_ptr())
-                alb = alb_out[0] / dec_w
-            else:
-                dlogits.zero_()
-                alb = zero
-            router_loss = gan + diff + dec_w * alb
+            ed_on = float(rc.ed_strength) != 0.0
+            hip.call("es_router_loss", hip.ptr(gates), hip.ptr(idx) if ed_on else None,
+                     hip.ptr(self._ed_feat) if ed_on else None, B, E, float(tau),
+                     float(rc.alb_strength * dec_w), float(rc.util_strength), float(rc.ed_strength),
+                     hip.ptr(rl), hip.ptr(dlogits), hip.stream_ptr())
+            alb = rl[0] / dec_w if rc.alb_strength != 0 else zero
+            ent = rl[1] if rc.util_strength != 0 else zero
+            ed = rl[2] if ed_on else zero
+            router_loss = ed + gan + diff + ent + dec_w * alb
             if epoch < rc.stop_router_training_epoch:
                 self.router.bwd(rctx, dlogits)
                 self._allreduce(self.router)
                 router_optimizer.step()
             else:
                 router_loss = zero
-            ed = ent = zero
         else:
             gan = router_loss = ed = diff = ent = alb = zero
 
@@ -248,6 +250,7 @@ class MoEWrapper(nn.Module):
     def _expert_step(self, e, rows, be, B, cond, real, pos, std, intensity, opt_g, opt_d, opt_a, mbuf, step, dev):
         G, D, A = self.generators[e], self.discriminators[e], self.aux_regs[e]
         H, W = real.shape[2], real.shape[3]
+        ridx = None
         if rows is None:
             sc, sr, sp, ss, si = cond, real, pos, std, intensity
         else:
@@ -286,6 +289,9 @@ class MoEWrapper(nn.Module):
         _, fl2, dctx2 = D.fwd(fake2, sc)
         s = torch.empty(be, dtype=torch.float32, device=dev)
         hip.call("es_image_expsum", C.byref(fake1.view), fake1.dt, fake1.ptr, hip.ptr(s), hip.stream_ptr())
+        if self._ed_feat is not None:
+            hip.call("es_scatter_rows", hip.ptr(s), hip.ptr(ridx) if rows is not None else None, be,
+                     hip.ptr(self._ed_feat), hip.stream_ptr())
         coords, actx = A.fwd(fake1, seed=seed, stream_base=sb(philox.PASS_AUX))
         L = fl1.dims[1]
         p = hip.GenLoss()

@@ -10,6 +10,10 @@ Program (train mode), every step a HIP kernel:
   conv2 128->64 -> BN2d -> Dropout -> LReLU
   conv2 64->1 -> ReLU                                  -> image [B,1,44,44] fp32
 Dropout masks come from Philox streams (expertsim/utils/philox.py), layer index 0..4.
+
+``GeneratorNeutron56`` is the declared 56x56 shape extension of BASELINE configs[4] (SURVEY.md
+§8(d) C5; no reference model exists, parity unpinned): the same program with fc2 -> 128x16x16,
+16 -> up 32 -> conv 30 -> up 60 -> conv 58 -> conv 57 -> conv 56.
 """
 from __future__ import annotations
 
@@ -26,18 +30,22 @@ P_DROP = 0.2
 
 
 class GeneratorNeutron(ExpertModule):
+    base = 13          # fc2 reshapes to 128 x base x base; the image is (4*base - 8)^2
+
     def __init__(self, noise_dim, cond_dim, di_strength, in_strength, **kwargs):
         super().__init__()
         self.name = "Generator-neutron-1-original-architecture"
         self.di_strength = di_strength
         self.in_strength = in_strength
         self.noise_dim, self.cond_dim = int(noise_dim), int(cond_dim)
-        self.image_shape = (44, 44)
+        k = self.base
+        self.image_shape = (4 * k - 8, 4 * k - 8)
+        self.fc2_features = 128 * k * k
         build_tree(self, [
             ("fc1.0", lambda: nn.Linear(self.noise_dim + self.cond_dim, 256)),
             ("fc1.1", lambda: nn.BatchNorm1d(256)),
-            ("fc2.0", lambda: nn.Linear(256, 128 * 13 * 13)),
-            ("fc2.1", lambda: nn.BatchNorm1d(128 * 13 * 13)),
+            ("fc2.0", lambda: nn.Linear(256, self.fc2_features)),
+            ("fc2.1", lambda: nn.BatchNorm1d(self.fc2_features)),
             ("conv_layers.0", lambda: nn.Conv2d(128, 256, kernel_size=(3, 3))),
             ("conv_layers.1", lambda: nn.BatchNorm2d(256)),
             ("conv_layers.5", lambda: nn.Conv2d(256, 128, kernel_size=(3, 3))),
@@ -57,11 +65,12 @@ class GeneratorNeutron(ExpertModule):
             return NormOp(hip.NORM_BN, b.weight, b.bias, running_mean=b.running_mean,
                           running_var=b.running_var, momentum=b.momentum, eps=b.eps,
                           num_batches=b.num_batches_tracked)
+        k = self.base
         return {
             "fc1": conv("fc1.0"), "bn1": bn("fc1.1"),
             "fc2": conv("fc2.0"), "bn2": bn("fc2.1"),
-            "c0": conv("conv_layers.0", Upsample((13, 13), scale=(2, 2))), "bn3": bn("conv_layers.1"),
-            "c5": conv("conv_layers.5", Upsample((24, 24), scale=(2, 2))), "bn4": bn("conv_layers.6"),
+            "c0": conv("conv_layers.0", Upsample((k, k), scale=(2, 2))), "bn3": bn("conv_layers.1"),
+            "c5": conv("conv_layers.5", Upsample((2 * k - 2, 2 * k - 2), scale=(2, 2))), "bn4": bn("conv_layers.6"),
             "c9": conv("conv_layers.9"), "bn5": bn("conv_layers.10"),
             "c13": conv("conv_layers.13"),
         }
@@ -74,6 +83,7 @@ class GeneratorNeutron(ExpertModule):
     def fwd(self, noise: torch.Tensor, cond: torch.Tensor, seed=0, stream_base=0, train=True):
         """noise [B,10] fp32, cond [B,9] fp32 (device) -> (image Act [B,1,44,44] fp32 NHWC, ctx)."""
         o = self.ops()
+        k, F2 = self.base, self.fc2_features
         cdt = self.compute_dtype
         dev = noise.device
         B = noise.shape[0]
@@ -84,14 +94,15 @@ class GeneratorNeutron(ExpertModule):
         ch = [self._chain(seed, stream_base, i, train) for i in range(5)]
         # dropout keep bits, drawn once in the forward norm pass and re-read by the backward
         keep = [hip.attach_keep(ch[i], B * r, c, dev)
-                for i, (r, c) in enumerate(((1, 256), (1, 21632), (576, 256), (2116, 128), (2025, 64)))]
+                for i, (r, c) in enumerate(((1, 256), (1, F2), ((2 * k - 2) ** 2, 256), ((4 * k - 6) ** 2, 128),
+                                            ((4 * k - 7) ** 2, 64)))]
         h1 = o["fc1"].fwd(x0)
         y1, s1 = o["bn1"].fwd(h1, ch[0], train=train)
         h2 = o["fc2"].fwd(y1)
         y2, s2 = o["bn2"].fwd(h2, ch[1], train=train)
         # [B, 21632] rows are NCHW [B,128,13,13]; re-layout to NHWC for the vector gather
-        y2n = Act.nhwc(B, 128, 13, 13, cdt, dev)
-        copy_act(Act(y2.t, (B, 128, 13, 13), (21632, 169, 13, 1)), y2n)
+        y2n = Act.nhwc(B, 128, k, k, cdt, dev)
+        copy_act(Act(y2.t, (B, 128, k, k), (F2, k * k, k, 1)), y2n)
         h3 = o["c0"].fwd(y2n, bn_stats=train)         # BatchNorm statistics from the conv epilogue
         y3, s3 = o["bn3"].fwd(h3, ch[2], train=train)
         h4 = o["c5"].fwd(y3, bn_stats=train)
@@ -126,9 +137,9 @@ class GeneratorNeutron(ExpertModule):
                            dbeta=g("conv_layers.1", "bias"), dsum=g("conv_layers.0", "bias"))
         o["c0"].wgrad(dh3, ctx["y2n"], g("conv_layers.0", "weight"), None)
         dy2n = o["c0"].dgrad(dh3, ctx["y2n"])
-        B = dy2n.dims[0]
-        dy2 = Act.rows(B, 21632, cdt, dy2n.t.device)
-        copy_act(dy2n, Act(dy2.t, (B, 128, 13, 13), (21632, 169, 13, 1)))
+        B, k, F2 = dy2n.dims[0], self.base, self.fc2_features
+        dy2 = Act.rows(B, F2, cdt, dy2n.t.device)
+        copy_act(dy2n, Act(dy2.t, (B, 128, k, k), (F2, k * k, k, 1)))
         dh2 = o["bn2"].bwd(ctx["h2"], ctx["s2"], ch[1], dy2, dgamma=g("fc2.1", "weight"),
                            dbeta=g("fc2.1", "bias"), dsum=g("fc2.0", "bias"))
         o["fc2"].wgrad(dh2, ctx["y1"], g("fc2.0", "weight"), None)
@@ -143,3 +154,12 @@ class GeneratorNeutron(ExpertModule):
         """Reference signature (generator.py:42): image [B,1,44,44]."""
         from ..autograd import generator_apply
         return generator_apply(self, noise, cond)
+
+
+class GeneratorNeutron56(GeneratorNeutron):
+    """Declared 56x56 extension (BASELINE configs[4]) -- parity unpinned."""
+    base = 16
+
+    def __init__(self, noise_dim, cond_dim, di_strength, in_strength, **kwargs):
+        super().__init__(noise_dim, cond_dim, di_strength, in_strength, **kwargs)
+        self.name = "Generator-neutron56-declared-extension"

@@ -18,9 +18,11 @@ from __future__ import annotations
 
 import numpy as np
 
-_SHAPES = {"neutron": (44, 44), "proton": (56, 30)}
-_RHO = {"neutron": 0.039, "proton": 0.011}
-_CLIP = {"neutron": 591.0, "proton": 765.0}
+# "neutron56": BASELINE configs[4]'s padded 56x56 extension: a 44x44 ZN
+# response zero-padded to 56x56 keeps its photons, so the hit density scales by 44^2 / 56^2
+_SHAPES = {"neutron": (44, 44), "proton": (56, 30), "neutron56": (56, 56)}
+_RHO = {"neutron": 0.039, "proton": 0.011, "neutron56": 0.039 * 44 * 44 / (56 * 56)}
+_CLIP = {"neutron": 591.0, "proton": 765.0, "neutron56": 765.0}
 
 
 def image_shape(architecture: str) -> tuple:

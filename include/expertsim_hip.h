@@ -313,6 +313,18 @@ int es_router_gumbel(const float* logits, const float* expo, int B, int E, float
  * and the loss value: out[0] = coef*mean_e exp(1/(S_e+1e-6)), S_e = sum_b gates[b,e]. */
 int es_router_alb(const float* gates, int B, int E, float tau, float coef, float* out,
                   float* dlogits, es_stream_t stream);
+/* All router-loss terms that carry gradient (moe.py:258-268,407-434; train/utils.py:372-395
+ * calculate_expert_distribution_loss, 398-419 calculate_expert_utilization_entropy, 623-642 ALB):
+ * out[0] = alb_coef*mean_e exp(1/(S_e+1e-6)); out[1] = util*sum_e avg_e*log(avg_e+1e-9)
+ * (= -entropy*util); out[2] = 0.1*ed/B*sum_{a,b: idx_a=idx_b} |feat_a - feat_b| (cdist of the
+ * [B,1] per-sample photon sums, gated by the straight-through one-hot gates); dlogits = d(sum of
+ * the three)/d logits through the Gumbel softmax.  feat / idx may be NULL when ed_strength == 0. */
+int es_router_loss(const float* gates, const int32_t* idx, const float* feat, int B, int E, float tau,
+                   float alb_coef, float util_strength, float ed_strength, float* out, float* dlogits,
+                   es_stream_t stream);
+/* dst[rows[i]] = src[i] for i < n (rows NULL: identity) -- moe.py:196-198 scatter of the
+ * per-sample photon sums into the batch-ordered ED features. */
+int es_scatter_rows(const float* src, const int32_t* rows, int n, float* dst, es_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Optimizer (torch.optim.Adam, created at train/training_setup.py:20-40, stepped at

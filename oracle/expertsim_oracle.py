@@ -46,6 +46,15 @@ philox = importlib.util.module_from_spec(_spec)
 _spec.loader.exec_module(philox)
 
 SLOPE = 0.1
+# "neutron56": the declared 56x56 shape extension of BASELINE configs[4] --
+# the neutron family with fc2 -> 128x16x16 (16->32->30->60->58->57->56) and D flatten 16*12*12.
+# No reference model exists for it: its parity is UNPINNED; the oracle runs it through
+# the same functions whose 44x44 instance is pinned to the reference's goldens.
+NEUTRON_BASE = {"neutron": 13, "neutron56": 16}
+
+
+def _family(arch):
+    return "neutron" if arch in NEUTRON_BASE else arch
 
 
 # --------------------------------------------------------------------------------------------
@@ -114,9 +123,10 @@ def _gn_groups(c, groups=32):
 
 def build_generator(arch, noise_dim=10, cond_dim=9):
     b = _Builder()
-    if arch == "neutron":              # neutron/generator.py:10-40
+    if arch in NEUTRON_BASE:           # neutron/generator.py:10-40
+        k = NEUTRON_BASE[arch]
         b.linear("fc1.0", noise_dim + cond_dim, 256); b.bn("fc1.1", 256)
-        b.linear("fc2.0", 256, 128 * 13 * 13); b.bn("fc2.1", 128 * 13 * 13)
+        b.linear("fc2.0", 256, 128 * k * k); b.bn("fc2.1", 128 * k * k)
         b.conv("conv_layers.0", 128, 256, 3); b.bn("conv_layers.1", 256)
         b.conv("conv_layers.5", 256, 128, 3); b.bn("conv_layers.6", 128)
         b.conv("conv_layers.9", 128, 64, 2); b.bn("conv_layers.10", 64)
@@ -135,7 +145,7 @@ def build_discriminator(arch, cond_dim=9):
     b = _Builder()                     # neutron/discriminator.py:10-39, proton/discriminator.py:120-146
     b.conv("conv_layers.0", 1, 32, 3, sn=True); b.affine("conv_layers.1", 32)
     b.conv("conv_layers.4", 32, 16, 3, sn=True); b.affine("conv_layers.5", 16)
-    flat = 9 * 12 * 12 if arch == "neutron" else 16 * 12 * 12
+    flat = 9 * 12 * 12 if arch == "neutron" else 16 * 12 * 12       # neutron56: 16*12*12 too
     b.linear("fc1.0", flat + cond_dim, 128, sn=True); b.affine("fc1.1", 128)
     b.linear("fc2.0", 128, 64, sn=True); b.affine("fc2.1", 64)
     b.linear("fc3", 64, 1, sn=True)
@@ -144,7 +154,7 @@ def build_discriminator(arch, cond_dim=9):
 
 def build_aux_reg(arch):
     b = _Builder()
-    if arch == "neutron":              # neutron/aux_reg.py:9-68
+    if _family(arch) == "neutron":              # neutron/aux_reg.py:9-68
         p = "feature_extractor."
         b.conv(p + "conv1", 1, 32, 3); b.bn(p + "conv1_bd.0", 32)
         b.conv(p + "conv2", 32, 64, 3); b.bn(p + "conv2_bd.0", 64)
@@ -246,12 +256,13 @@ def generator_forward(arch, P, noise, cond, drop=None, training=True):
     """neutron/generator.py:42-49, proton/generator.py:46-52."""
     x = torch.cat((noise, cond), dim=1)
     lrelu = lambda t: F.leaky_relu(t, SLOPE)
-    if arch == "neutron":
+    if arch in NEUTRON_BASE:
+        k = NEUTRON_BASE[arch]
         bn = _bn_train if training else _bn_eval
         dp = (lambda t: drop(t, 0.2)) if training else (lambda t: t)
         x = lrelu(dp(bn(_lin(x, P, "fc1.0"), P, "fc1.1")))
         x = lrelu(dp(bn(_lin(x, P, "fc2.0"), P, "fc2.1")))
-        x = x.view(-1, 128, 13, 13)
+        x = x.view(-1, 128, k, k)
         x = F.interpolate(x, scale_factor=(2, 2), mode="nearest")
         x = lrelu(dp(bn(_conv(x, P, "conv_layers.0"), P, "conv_layers.1")))
         x = F.interpolate(x, scale_factor=(2, 2), mode="nearest")
@@ -279,7 +290,7 @@ def discriminator_forward(arch, P, img, cond, training=True):
     x = F.max_pool2d(x, (2, 2))
     x = F.conv2d(x, _sn_weight(P, "conv_layers.4", training), P["conv_layers.4.bias"])
     x = lrelu(F.group_norm(x, 8, P["conv_layers.5.weight"], P["conv_layers.5.bias"], 1e-5))
-    x = F.max_pool2d(x, (2, 2) if arch == "neutron" else (2, 1))
+    x = F.max_pool2d(x, (2, 2) if _family(arch) == "neutron" else (2, 1))
     x = torch.cat((x.reshape(x.shape[0], -1), cond), dim=1)
     x = F.linear(x, _sn_weight(P, "fc1.0", training), P["fc1.0.bias"])
     x = lrelu(F.layer_norm(x, (128,), P["fc1.1.weight"], P["fc1.1.bias"], 1e-5))
@@ -295,7 +306,7 @@ def aux_forward(arch, P, x, drop=None, training=True):
         x = x.unsqueeze(1)
     p = "feature_extractor."
     lrelu = lambda t: F.leaky_relu(t, SLOPE)
-    if arch == "neutron":
+    if arch in NEUTRON_BASE:
         bn = _bn_train if training else _bn_eval
         dp = (lambda t: drop(t, 0.2)) if training else (lambda t: t)
         x = F.max_pool2d(dp(lrelu(bn(_conv(x, P, p + "conv1"), P, p + "conv1_bd.0"))), (2, 2))

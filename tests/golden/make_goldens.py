@@ -313,6 +313,11 @@ CASES = {
     "neutron_e3_b12": dict(arch="neutron", n_experts=3, batch=12, steps=2),
     "proton_e1_b8": dict(arch="proton", n_experts=1, batch=8, steps=2),
     "proton_e3_b12": dict(arch="proton", n_experts=3, batch=12, steps=2),
+    # the router terms that are 0 in default.yaml: expert-distribution loss (ed_strength, the
+    # value default.yaml:25 comments out) and utilisation entropy, at epoch 3 (tau / alpha ramps)
+    "neutron_e3_b12_router": dict(arch="neutron", n_experts=3, batch=12, steps=2, epoch=3,
+                                  overrides={"model.router.ed_strength": 0.01,
+                                             "model.router.util_strength": 0.1}),
 }
 
 

@@ -7,7 +7,7 @@ import os
 import numpy as np
 
 GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-CASES = ["neutron_e1_b8", "neutron_e3_b12", "proton_e1_b8", "proton_e3_b12"]
+CASES = ["neutron_e1_b8", "neutron_e3_b12", "proton_e1_b8", "proton_e3_b12", "neutron_e3_b12_router"]
 
 
 class Golden:
@@ -21,6 +21,20 @@ class Golden:
         self.steps = self.meta["steps"]
         self.seed = self.meta["seed"]
         self.epoch = self.meta["epoch"]
+
+    def overrides(self):
+        """The case's config overrides as load_config strings (``model.router.x=v``)."""
+        return [f"{k}={v}" for k, v in self.meta.get("overrides", {}).items()
+                if k not in ("model.architecture", "model.n_experts", "train.batch_size")]
+
+    def oracle_cfg(self, base):
+        """Flat oracle config (oracle.DEFAULT_CFG keys) with the case's router overrides applied."""
+        cfg = dict(base)
+        for k, v in self.meta.get("overrides", {}).items():
+            leaf = k.split(".")[-1]
+            if k.startswith("model.router.") and leaf in cfg:
+                cfg[leaf] = float(v)
+        return cfg
 
     def __getitem__(self, k):
         return self.z[k]

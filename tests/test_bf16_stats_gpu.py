@@ -24,8 +24,10 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 B, STEPS, N_EVAL = 64, 20, 1024
 KEYS = ("gen_loss", "disc_loss", "div_loss", "intensity_loss", "aux_reg_loss")
-TRAJ_TOL = {"fp32": 0.02, "bf16": 0.10}
-WS_TOL = {"fp32": 0.02, "bf16": 0.10}
+# measured on MI355X (r02): trajectory max-dev fp32 0.0082 / bf16 0.039 (gen_loss, the largest);
+# WS/mean fp32 0.013 / bf16 0.030, natural spread of two oracle noise draws 0.0082
+TRAJ_TOL = {"fp32": 0.02, "bf16": 0.08}
+WS_TOL = {"fp32": 0.03, "bf16": 0.06}
 
 
 def _inputs():

@@ -5,6 +5,7 @@ test_train_step_gpu.py / test_grads_gpu.py; bf16 statistical parity is test_bf16
   configs[1]  neutron 44x44, E=1, B=512
   configs[2]  neutron 44x44, E=1, B=1024 (the bench headline)
   configs[3]  neutron 44x44, E=4, B=512 per GPU (the per-rank shard of the 4-GPU B=2048 run)
+  configs[4]  neutron56 56x56 (declared extension, parity unpinned), E=8, B=512 per GPU
   + proton 56x30, E=1, B=512 (the reference's other model family)
 
 Each runs 3 train steps: every metric is finite and the metric-key set is the reference's
@@ -20,7 +21,8 @@ import torch
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
-CONFIGS = [("neutron", 1, 512), ("neutron", 1, 1024), ("neutron", 4, 512), ("proton", 1, 512)]
+CONFIGS = [("neutron", 1, 512), ("neutron", 1, 1024), ("neutron", 4, 512), ("neutron56", 8, 512),
+           ("proton", 1, 512)]
 
 
 def _keys(E):
@@ -44,7 +46,6 @@ def test_config_steps(arch, E, B):
     real = t["real_images"].unsqueeze(1).contiguous()
     args = (0, t["cond"], real, t["true_positions"], t["std"], t["intensity"], oa, og, od, orr, None, DEV)
     p0 = {n: p.detach().clone() for n, p in moe.named_parameters()}
-    imgs = []
     for s in range(3):
         m = moe.train_step(*args)
         torch.cuda.synchronize()

