@@ -4,7 +4,9 @@ No reference model accepts 56x56, so this row's parity is UNPINNED a
 reference.  What is checked: the HIP path (fp32 mode) against the oracle's same restatement of
 the neutron family at base 16 (oracle.NEUTRON_BASE; its 44x44 instance is the one pinned
 bit-exactly to the reference's goldens) on one train step with injected noise / Gumbel draws:
-metrics and generated images <= 1e-4 relative, as the pinned 44x44 cases at step 0.
+metrics and generated images <= 1e-4 relative, as the pinned 44x44 cases at step 0 (losses that
+are small differences of O(0.1) terms, e.g. gen_loss = -mean D + div + intensity + aux, compared
+relative to 1e-2).
 """
 import numpy as np
 import pytest
@@ -49,7 +51,7 @@ def test_neutron56_step_matches_oracle_restatement(E, B):
     ref, tr = om.train_step(0, tb["cond"], tb["real_images"].unsqueeze(1), tb["true_positions"], tb["std"],
                             tb["intensity"], noise_fn, gum)
     for k, v in ref.items():
-        assert abs(float(met[k]) - v) <= 1e-4 * max(abs(v), 1e-3), (k, float(met[k]), v)
+        assert abs(float(met[k]) - v) <= 1e-4 * max(abs(v), 1e-2), (k, float(met[k]), v)
     if "G0/0" in tr:
         want = tr["G0/0"].numpy()
         assert imgs and np.max(np.abs(imgs[0] - want)) <= 1e-4 * max(np.max(np.abs(want)), 1e-6)
