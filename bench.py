@@ -201,7 +201,7 @@ def run_mode(args, precision, steps, warmup, dev, rank, world, ddp, probe_steps)
     from expertsim.utils.synthetic import make_batch
     moe, (og, od, oa, orr), cfg = build(args.arch, args.experts, precision, 1234, dev)
     if ddp:
-        moe.ddp = DataParallel()
+        moe.ddp = DataParallel(sync_bn=args.sync_bn)
         moe.rank = rank
     b = make_batch(args.batch, args.arch, seed=1000 + rank)
     t = {k: torch.from_numpy(v).to(dev) for k, v in b.items()}
@@ -246,6 +246,8 @@ def main():
     ap.add_argument("--no-probe", action="store_true", help="skip the per-kernel HIP-event probe")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="replay the step as a captured HIP graph (auto: single process)")
+    ap.add_argument("--sync-bn", action="store_true",
+                    help="data parallel: global BatchNorm / SDI / router statistics (single-device semantics)")
     ap.add_argument("--ddp", action="store_true",
                     help="run the data-parallel code path even on one process (1-rank RCCL group)")
     args = ap.parse_args()

@@ -104,7 +104,7 @@ __device__ __forceinline__ void resolve_stream(es_dropout_t& d) {
   if (d.enabled && d.step_ptr) d.stream += (uint32_t)(d.step_ptr[0] * d.step_mul);
 }
 __device__ __forceinline__ bool dropout_keep(const es_dropout_t& d, uint64_t i) {
-  return (philox_word(d.seed, d.stream, i) >> 8) < d.threshold;
+  return (philox_word(d.seed, d.stream, i + d.index_offset) >> 8) < d.threshold;
 }
 
 // ---------------------------------------------------------------- logical 4-D index helpers

@@ -121,13 +121,13 @@ __global__ void __launch_bounds__(256) gen_losses_b(es_gen_loss_t p, const float
   sl1 = block_sum(sl1, sh);
   saux = block_sum(saux, sh);
   sr = block_sum(sr, sh);
-  const float ms = sstd / fn;
+  const float ms = p.std_mean ? p.std_mean[0] : sstd / fn;   // data parallel: the expert's global mean
   const float smean = ss / fn;
   float sq = 0.f;
   for (int b = threadIdx.x; b < n; b += blockDim.x) { const float d = s[b] - smean; sq += d * d; }
   sq = block_sum(sq, sh);
   const float gen = -sfo / fn;
-  const float div = ms * (sstd * sr / (fn * fn)) * p.di_strength;
+  const float div = ms * ((p.std_mean ? ms * fn : sstd) * sr / (fn * fn)) * p.di_strength;
   const float inl = sl1 / fn * p.in_strength;
   const float aux = saux / (2.f * fn) * p.aux_strength;
   // gradients (all scaled by w)
@@ -219,24 +219,36 @@ __global__ void __launch_bounds__(256) router_alb_kernel(const float* gates, int
 // Expert-distribution (ED) pair sums, train/utils.py:372-395 with gating = the straight-through
 // one-hot gates (moe.py:103,264): T[a,e] = sum_{b: idx_b = e} |f_a - f_b| (cdist p=2 of the [B,1]
 // per-sample photon sums).  One thread per (a, e); f / idx staged through LDS in 1024-row tiles.
-__global__ void __launch_bounds__(256) router_ed_pairs_kernel(const float* feat, const int32_t* idx, int B, int E,
-                                                              float* T) {
+// a: the B local rows; b: the Ball rows of the (all-gathered) global batch.
+__global__ void __launch_bounds__(256) router_ed_pairs_kernel(const float* feat, int B, const float* feat_all,
+                                                              const int32_t* idx_all, int Ball, int E, float* T) {
   __shared__ float fs[1024];
   __shared__ int32_t is[1024];
   const int a = blockIdx.x * blockDim.x + threadIdx.x, e = blockIdx.y;
   const float fa = a < B ? feat[a] : 0.f;
   float acc = 0.f;
-  for (int b0 = 0; b0 < B; b0 += 1024) {
-    const int nb = min(1024, B - b0);
+  for (int b0 = 0; b0 < Ball; b0 += 1024) {
+    const int nb = min(1024, Ball - b0);
     __syncthreads();
     for (int j = threadIdx.x; j < nb; j += blockDim.x) {
-      fs[j] = feat[b0 + j];
-      is[j] = idx[b0 + j];
+      fs[j] = feat_all[b0 + j];
+      is[j] = idx_all[b0 + j];
     }
     __syncthreads();
     for (int j = 0; j < nb; ++j) acc += is[j] == e ? fabsf(fa - fs[j]) : 0.f;
   }
   if (a < B) T[a * E + e] = acc;
+}
+
+// S_e = sum_b gates[b, e] (a rank's share of the router's global gate sums)
+__global__ void __launch_bounds__(256) router_colsum_kernel(const float* gates, int B, int E, float* out) {
+  __shared__ float sh[8];
+  for (int e = 0; e < E; ++e) {
+    float s = 0.f;
+    for (int b = threadIdx.x; b < B; b += blockDim.x) s += gates[b * E + e];
+    s = block_sum(s, sh);
+    if (threadIdx.x == 0) out[e] = s;
+  }
 }
 
 // Router loss terms with gradient into the router (moe.py:258-268,407-434; train/utils.py:372-419,
@@ -249,22 +261,27 @@ __global__ void __launch_bounds__(256) router_ed_pairs_kernel(const float* feat,
 // out[0] = ALB, out[1] = ENT, out[2] = ED.  T aliases dlogits (each row is read before written).
 __global__ void __launch_bounds__(1024) router_loss_kernel(const float* gates, const int32_t* idx, int B, int E,
                                                            float tau, float alb_coef, float util, float ed,
-                                                           float* out, float* dlogits) {
+                                                           const float* colsum, float Btot, float* out,
+                                                           float* dlogits) {
   __shared__ float sh[16];
   __shared__ float gS[64];
   float L = 0.f, ent = 0.f;
   for (int e = 0; e < E; ++e) {
     float s = 0.f;
-    for (int b = threadIdx.x; b < B; b += blockDim.x) s += gates[b * E + e];
-    s = block_sum(s, sh);
+    if (colsum) {
+      s = colsum[e];                       // data parallel: the all-reduced global sums
+    } else {
+      for (int b = threadIdx.x; b < B; b += blockDim.x) s += gates[b * E + e];
+      s = block_sum(s, sh);
+    }
     const float inv = 1.f / (s + 1e-6f);
     const float ex = expf(inv);
     L += ex;
-    const float avg = s / (float)B;
+    const float avg = s / Btot;
     const float lg = logf(avg + 1e-9f);
     ent += avg * lg;
     if (threadIdx.x == 0)
-      gS[e] = alb_coef / (float)E * ex * (-inv * inv) + util / (float)B * (lg + avg / (avg + 1e-9f));
+      gS[e] = alb_coef / (float)E * ex * (-inv * inv) + util / Btot * (lg + avg / (avg + 1e-9f));
   }
   float edsum = 0.f;
   if (ed != 0.f) {
@@ -275,9 +292,9 @@ __global__ void __launch_bounds__(1024) router_loss_kernel(const float* gates, c
   if (threadIdx.x == 0) {
     out[0] = alb_coef * (L / (float)E);
     out[1] = util * ent;
-    out[2] = 0.1f * (edsum / (float)B) * ed;
+    out[2] = 0.1f * (edsum / Btot) * ed;
   }
-  const float ked = 0.2f * ed / (float)B;
+  const float ked = 0.2f * ed / Btot;
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
     float dg[64];
     float dot = 0.f;
@@ -287,6 +304,32 @@ __global__ void __launch_bounds__(1024) router_loss_kernel(const float* gates, c
     }
     for (int e = 0; e < E; ++e) dlogits[b * E + e] = gates[b * E + e] * (dg[e] - dot) / tau;
   }
+}
+
+// Data-parallel metric merge: rows [world][E][10] = the ranks' per-expert metric rows (total, gen,
+// div, int, aux, std_int, mean_int, w, disc) + the local sample count (0 when the rank did not run
+// the expert).  Totals / w / disc (local-count-weighted losses) average over ranks; per-sample means
+// (gen, div, int, aux, mean_int) are count-weighted; std_int merges (n, mean, M2) (Chan).
+__global__ void dp_metrics_merge_kernel(const float* rows, int world, int E, float* out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  double N = 0.0, tot = 0.0, wsum = 0.0, disc = 0.0, c[4] = {0.0, 0.0, 0.0, 0.0}, mean = 0.0, M2 = 0.0;
+  for (int r = 0; r < world; ++r) {
+    const float* q = rows + ((int64_t)r * E + e) * 10;
+    tot += q[0]; wsum += q[7]; disc += q[8];
+    const double n = q[9];
+    if (n <= 0.0) continue;
+    for (int k = 0; k < 4; ++k) c[k] += n * q[1 + k];
+    const double nt = N + n, dl = (double)q[6] - mean;
+    M2 += (n - 1.0) * (double)q[5] * (double)q[5] + dl * dl * N * n / nt;
+    mean += dl * n / nt;
+    N = nt;
+  }
+  float* o = out + (int64_t)e * 9;
+  o[0] = (float)(tot / world); o[7] = (float)(wsum / world); o[8] = (float)(disc / world);
+  for (int k = 0; k < 4; ++k) o[1 + k] = N > 0.0 ? (float)(c[k] / N) : 0.f;
+  o[6] = N > 0.0 ? (float)mean : 0.f;
+  o[5] = N > 1.0 ? (float)sqrt(M2 / (N - 1.0)) : 0.f;
 }
 
 // mean_intensities_in_batch_expert[mask] = s (moe.py:196-198): dst[rows[i]] = src[i]
@@ -355,15 +398,34 @@ extern "C" int es_router_alb(const float* gates, int B, int E, float tau, float 
 }
 
 extern "C" int es_router_loss(const float* gates, const int32_t* idx, const float* feat, int B, int E, float tau,
-                              float alb_coef, float util_strength, float ed_strength, float* out, float* dlogits,
-                              es_stream_t stream) {
+                              float alb_coef, float util_strength, float ed_strength, const float* colsum,
+                              int B_total, const float* feat_all, const int32_t* idx_all, int B_all, float* out,
+                              float* dlogits, es_stream_t stream) {
   ES_CHECK_ARG(B > 0 && E >= 1 && E <= 64, "router_loss: B=%d E=%d (E <= 64)", B, E);
   ES_CHECK_ARG(ed_strength == 0.f || (feat && idx), "router_loss: ED needs feat and idx");
   hipStream_t st = (hipStream_t)stream;
+  if (B_total <= 0) B_total = B;
+  if (!feat_all) { feat_all = feat; idx_all = idx; B_all = B; }
   if (ed_strength != 0.f)
-    hipLaunchKernelGGL(router_ed_pairs_kernel, dim3((B + 255) / 256, E), dim3(256), 0, st, feat, idx, B, E, dlogits);
+    hipLaunchKernelGGL(router_ed_pairs_kernel, dim3((B + 255) / 256, E), dim3(256), 0, st, feat, B, feat_all,
+                       idx_all, B_all, E, dlogits);
   hipLaunchKernelGGL(router_loss_kernel, dim3(1), dim3(1024), 0, st, gates, idx, B, E, tau, alb_coef, util_strength,
-                     ed_strength, out, dlogits);
+                     ed_strength, colsum, (float)B_total, out, dlogits);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_router_colsum(const float* gates, int B, int E, float* out, es_stream_t stream) {
+  ES_CHECK_ARG(B > 0 && E >= 1, "router_colsum: B=%d E=%d", B, E);
+  hipLaunchKernelGGL(router_colsum_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, gates, B, E, out);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_dp_metrics_merge(const float* rows, int world, int E, float* out, es_stream_t stream) {
+  ES_CHECK_ARG(world >= 1 && E >= 1, "dp_metrics_merge: world=%d E=%d", world, E);
+  hipLaunchKernelGGL(dp_metrics_merge_kernel, dim3((E + 63) / 64), dim3(64), 0, (hipStream_t)stream, rows, world, E,
+                     out);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }

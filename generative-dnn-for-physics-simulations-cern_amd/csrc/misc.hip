@@ -522,12 +522,13 @@ __global__ void ema_kernel(float* __restrict__ s, const float* __restrict__ p, i
 
 // ------------------------------------------------------------------------------------ RNG
 __global__ void randn_kernel(float* out, int64_t n, uint64_t seed, uint32_t sid, const int32_t* step_ptr,
-                             int32_t step_mul) {
+                             int32_t step_mul, int64_t pair0) {
   if (step_ptr) sid += (uint32_t)(step_ptr[0] * step_mul);
-  // Box-Muller on pairs: counter = pair index
+  // Box-Muller on pairs: counter = global pair index (pair0 = offset / 2)
   const int64_t pairs = (n + 1) / 2;
   GRID_STRIDE(i, pairs) {
-    u32x4 r = philox4x32_10((uint32_t)i, (uint32_t)(i >> 32), sid, 0x5EED0001u, (uint32_t)seed,
+    const int64_t q = i + pair0;
+    u32x4 r = philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), sid, 0x5EED0001u, (uint32_t)seed,
                             (uint32_t)(seed >> 32));
     const float u1 = ((r.x >> 8) + 1) * (1.f / 16777217.f);   // (0, 1]
     const float u2 = (r.y >> 8) * (1.f / 16777216.f);
@@ -539,10 +540,11 @@ __global__ void randn_kernel(float* out, int64_t n, uint64_t seed, uint32_t sid,
   }
 }
 __global__ void rand_exp_kernel(float* out, int64_t n, uint64_t seed, uint32_t sid, const int32_t* step_ptr,
-                                int32_t step_mul) {
+                                int32_t step_mul, int64_t off) {
   if (step_ptr) sid += (uint32_t)(step_ptr[0] * step_mul);
   GRID_STRIDE(i, n) {
-    u32x4 r = philox4x32_10((uint32_t)i, (uint32_t)(i >> 32), sid, 0x5EED0002u, (uint32_t)seed,
+    const int64_t q = i + off;
+    u32x4 r = philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), sid, 0x5EED0002u, (uint32_t)seed,
                             (uint32_t)(seed >> 32));
     const float u = ((r.x >> 8) + 1) * (1.f / 16777217.f);
     out[i] = -logf(u);
@@ -745,27 +747,30 @@ extern "C" int es_ema_update(float* shadow, const float* p, int64_t n, float dec
 }
 
 extern "C" int es_randn_dev(float* out, int64_t n, uint64_t seed, uint32_t stream_id, const int32_t* step_ptr,
-                            int32_t step_mul, es_stream_t stream) {
+                            int32_t step_mul, int64_t offset, es_stream_t stream) {
   if (n == 0) return ES_OK;
+  ES_CHECK_ARG(offset >= 0 && offset % 2 == 0, "randn: offset %lld must be even and >= 0", (long long)offset);
   hipLaunchKernelGGL(randn_kernel, dim3(grid_for((n + 1) / 2)), dim3(256), 0, (hipStream_t)stream, out, n, seed,
-                     stream_id, step_ptr, step_mul);
+                     stream_id, step_ptr, step_mul, offset / 2);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
 extern "C" int es_randn(float* out, int64_t n, uint64_t seed, uint32_t stream_id, es_stream_t stream) {
-  return es_randn_dev(out, n, seed, stream_id, nullptr, 0, stream);
+  return es_randn_dev(out, n, seed, stream_id, nullptr, 0, 0, stream);
 }
 
 extern "C" int es_rand_exponential_dev(float* out, int64_t n, uint64_t seed, uint32_t stream_id,
-                                       const int32_t* step_ptr, int32_t step_mul, es_stream_t stream) {
+                                       const int32_t* step_ptr, int32_t step_mul, int64_t offset,
+                                       es_stream_t stream) {
   if (n == 0) return ES_OK;
+  ES_CHECK_ARG(offset >= 0, "rand_exponential: offset must be >= 0");
   hipLaunchKernelGGL(rand_exp_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, out, n, seed,
-                     stream_id, step_ptr, step_mul);
+                     stream_id, step_ptr, step_mul, offset);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
 extern "C" int es_rand_exponential(float* out, int64_t n, uint64_t seed, uint32_t stream_id, es_stream_t stream) {
-  return es_rand_exponential_dev(out, n, seed, stream_id, nullptr, 0, stream);
+  return es_rand_exponential_dev(out, n, seed, stream_id, nullptr, 0, 0, stream);
 }
 
 extern "C" int es_counter_add(int32_t* counter, int32_t v, es_stream_t stream) {

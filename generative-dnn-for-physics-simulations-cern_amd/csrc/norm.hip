@@ -544,6 +544,49 @@ int64_t stats_groups(const es_view_t* x, int kind, int groups) {
   return x->n;
 }
 
+// ---- data-parallel (SyncBN) helpers
+// merge [chunks][3][C] (count, mean, M2) partials into one [3][C] partial (fp64 sums, as
+// bn_finalize_block_kernel): a rank's local BatchNorm statistics, all-gathered across ranks and
+// finalized with es_norm_stats_finalize(world partials)
+__global__ void __launch_bounds__(256) stats_merge_kernel(const float* part, int chunks, int C, float* out) {
+  const int c = blockIdx.x;
+  double n_ = 0.0, s1 = 0.0, s2 = 0.0;
+  for (int k = threadIdx.x; k < chunks; k += blockDim.x) {
+    const float* p = part + (int64_t)k * 3 * C;
+    const double nb = p[c], mb = p[C + c], Mb = p[2 * C + c];
+    const bool has = nb > 0.0;
+    n_ += nb;
+    s1 += has ? nb * mb : 0.0;
+    s2 += has ? Mb + nb * mb * mb : 0.0;
+  }
+  __shared__ double sn[256], sm[256], sM[256];
+  sn[threadIdx.x] = n_; sm[threadIdx.x] = s1; sM[threadIdx.x] = s2;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) {
+      sn[threadIdx.x] += sn[threadIdx.x + off];
+      sm[threadIdx.x] += sm[threadIdx.x + off];
+      sM[threadIdx.x] += sM[threadIdx.x + off];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double nt = sn[0], mt = nt > 0.0 ? sm[0] / nt : 0.0;
+    out[c] = (float)nt;
+    out[C + c] = (float)mt;
+    out[2 * C + c] = (float)fmax(sM[0] - nt * mt * mt, 0.0);
+  }
+}
+
+// a1 = gamma*s1/cnt, a2 = gamma*s2/cnt from (all-reduced) raw backward sums [2][C]
+__global__ void bn_scale_sums_kernel(const float* sums, int C, float cnt, const float* gamma, float* a1, float* a2) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float g = gamma ? gamma[c] : 1.f;
+  a1[c] = g * sums[c] / cnt;
+  a2[c] = g * sums[C + c] / cnt;
+}
+
 }  // namespace
 
 // ================================================================================ C ABI
@@ -774,6 +817,85 @@ extern "C" int es_channel_sum(const es_view_t* x, es_dtype_t xdt, const void* xp
   else
     hipLaunchKernelGGL(sum_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)ws,
                        chunks, x->c, out, beta);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+// ------------------------------------------------------------------------ data-parallel BatchNorm
+extern "C" int es_norm_stats_merge(const float* part, int chunks, int C, float* out, es_stream_t stream) {
+  ES_CHECK_ARG(part && out && chunks > 0 && C > 0, "norm_stats_merge: bad arguments");
+  hipLaunchKernelGGL(stats_merge_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, part, chunks, C, out);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_norm_stats_local(const es_view_t* x, es_dtype_t xdt, const void* xp, void* ws, float* out,
+                                   es_stream_t stream) {
+  hipStream_t st = (hipStream_t)stream;
+  ES_CHECK_ARG(ws != nullptr && out != nullptr, "norm_stats_local: workspace / out");
+  es_norm_t nm{ES_NORM_BN, 1, nullptr, nullptr, nullptr, nullptr};
+  BwdIn b = mk_bwdin(x, xdt, xp, &nm, nullptr);
+  const int fk = fast_kind(x, ES_NORM_BN, 1);
+  int cb, chunks; int64_t rows, per;
+  colred_geometry(b.x, cb, chunks, rows, per);
+  if (fk == 0)
+    chunks = es_fast_norm_stats(x, 0, xdt, xp, (float*)ws, st);
+  else
+    hipLaunchKernelGGL(colred_kernel<RED_STATS>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, (float*)ws);
+  hipLaunchKernelGGL(stats_merge_kernel, dim3(x->c), dim3(256), 0, st, (const float*)ws, chunks, x->c, out);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_norm_bwd_sync(int phase, const es_view_t* x, es_dtype_t xdt, const void* xp, const es_norm_t* nm,
+                                const es_chain_t* ch, const es_view_t* dy, es_dtype_t dydt, const void* dyp,
+                                const es_view_t* dx, es_dtype_t dxdt, void* dxp, float* sums, float cnt,
+                                float* dgamma, float* dbeta, float* dsum, void* ws, es_stream_t stream) {
+  hipStream_t st = (hipStream_t)stream;
+  ES_CHECK_ARG(nm && nm->kind == ES_NORM_BN, "norm_bwd_sync: BatchNorm only");
+  ES_CHECK_ARG(phase == 0 || phase == 1, "norm_bwd_sync: phase 0 (sums) or 1 (apply)");
+  ES_CHECK_ARG(sums && ws, "norm_bwd_sync: sums / workspace");
+  ES_CHECK_ARG(dsum == nullptr || x->c <= 1024, "norm_bwd_sync: dsum needs C <= 1024");
+  BwdIn b = mk_bwdin(x, xdt, xp, nm, ch);
+  b.dy = mkview(dy); b.dyp = dyp; b.dybf = dydt == ES_BF16;
+  int cb, chunks; int64_t rows, per;
+  colred_geometry(b.x, cb, chunks, rows, per);
+  float* part = (float*)ws;
+  int64_t part_floats = (int64_t)chunks * 3 * x->c;
+  const int fk = fast_kind(x, ES_NORM_BN, 1);
+  const bool fast = fk == 0 && xdt == dydt && dydt == dxdt && same_view(x, dy) && (dxp == nullptr || same_view(x, dx));
+  if (fk >= 0) part_floats = std::max<int64_t>(part_floats, es_fast_part_floats(x, fk));
+  float* g1 = part + part_floats;
+  float* g2 = g1 + x->c;
+  if (phase == 0) {
+    int nchunks = chunks;
+    if (fast)
+      nchunks = es_fast_norm_bwd_reduce(x, 0, xdt, xp, dyp, nm, ch, part, st);
+    else
+      hipLaunchKernelGGL(colred_kernel<RED_BWD>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, part);
+    // raw per-channel sums s1 = sum dnorm, s2 = sum dnorm*xhat (+ the local dbeta / dgamma)
+    if (nchunks > 32)
+      hipLaunchKernelGGL(sums_finalize_block_kernel, dim3(x->c), dim3(256), 0, st, (const float*)part, nchunks,
+                         x->c, 1.f, nullptr, sums, sums + x->c, dbeta, dgamma, 1.f);
+    else
+      hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)part,
+                         nchunks, x->c, 1.f, nullptr, sums, sums + x->c, dgamma, dbeta);
+    ES_CHECK_LAUNCH();
+    return ES_OK;
+  }
+  ES_CHECK_ARG(cnt > 0.f && dxp != nullptr, "norm_bwd_sync: apply needs cnt > 0 and dx");
+  hipLaunchKernelGGL(bn_scale_sums_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)sums, x->c,
+                     cnt, nm->gamma, g1, g2);
+  if (fast) {
+    fast_dsum_finalize(x->c, es_fast_norm_bwd_apply(x, 0, xdt, xp, dyp, dxp, nm, ch, g1, g2, dsum, part, st),
+                       part, dsum, st);
+  } else {
+    BwdApply ap{};
+    ap.b = b; ap.dx = mkview(dx); ap.dxp = dxp; ap.dxbf = dxdt == ES_BF16; ap.beta = 0.f; ap.csum = dsum;
+    ap.a1 = g1; ap.a2 = g2;
+    const int64_t total = (int64_t)x->n * x->c * x->h * x->w;
+    hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(grid_for(total)), dim3(256), 0, st, ap);
+  }
   ES_CHECK_LAUNCH();
   return ES_OK;
 }

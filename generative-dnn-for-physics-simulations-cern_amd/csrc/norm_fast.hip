@@ -101,7 +101,7 @@ __device__ __forceinline__ void keep_bits(const FastArgs& a, int r0, int c0, uin
     const int n = r0 / a.HW, hw0 = r0 - n * a.HW;     // r0 % 4 == 0 -> same n for the 4 rows
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const uint64_t base = ((uint64_t)n * a.C + c0 + k) * (uint64_t)a.HW + hw0;
+      const uint64_t base = ((uint64_t)n * a.C + c0 + k) * (uint64_t)a.HW + hw0 + a.drop.index_offset;
       const uint64_t q = base >> 2;
       const u32x4 w = philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), a.drop.stream, 0u, k0, k1);
       keep[0] |= (uint32_t)((w.x >> 8) < thr) << k;
@@ -116,7 +116,7 @@ __device__ __forceinline__ void keep_bits(const FastArgs& a, int r0, int c0, uin
       if (r >= a.rows) break;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const uint64_t q = ((uint64_t)r * a.C + c0 + 4 * h) >> 2;
+        const uint64_t q = ((uint64_t)r * a.C + c0 + 4 * h + a.drop.index_offset) >> 2;
         const u32x4 w = philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), a.drop.stream, 0u, k0, k1);
         keep[j] |= ((uint32_t)((w.x >> 8) < thr) | ((uint32_t)((w.y >> 8) < thr) << 1) |
                     ((uint32_t)((w.z >> 8) < thr) << 2) | ((uint32_t)((w.w >> 8) < thr) << 3)) << (4 * h);
@@ -128,7 +128,7 @@ __device__ __forceinline__ void keep_bits(const FastArgs& a, int r0, int c0, uin
     const int n = r0 / a.HW, hw0 = r0 - n * a.HW;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const uint64_t i0 = ((uint64_t)n * a.C + c0 + k) * (uint64_t)a.HW + hw0;
+      const uint64_t i0 = ((uint64_t)n * a.C + c0 + k) * (uint64_t)a.HW + hw0 + a.drop.index_offset;
       const uint64_t q = i0 >> 2;
       const int off = (int)(i0 & 3);
       const u32x4 w = philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), a.drop.stream, 0u, k0, k1);
@@ -155,7 +155,7 @@ __device__ __forceinline__ void keep_bits(const FastArgs& a, int r0, int c0, uin
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const uint64_t i = ((uint64_t)n * a.C + c0 + k) * (uint64_t)a.HW + hw;
-        keep[j] |= (uint32_t)((philox_word(a.drop.seed, a.drop.stream, i) >> 8) < thr) << k;
+        keep[j] |= (uint32_t)((philox_word(a.drop.seed, a.drop.stream, i + a.drop.index_offset) >> 8) < thr) << k;
       }
     }
   }
@@ -490,8 +490,9 @@ int64_t es_fast_part_floats(const es_view_t* v, int G) {
 static int keep_mode(const FastArgs& a, bool read_bits = false) {
   if (!a.drop.enabled) return KM_NONE;
   if (read_bits && a.keep) return KM_BITS;
-  if ((a.HW & 3) == 0) return KM_HW4;
-  if (a.HW == 1 && (a.C & 3) == 0) return KM_ROW;
+  const bool al4 = (a.drop.index_offset & 3) == 0;   // both fast modes need 4-aligned global indices
+  if ((a.HW & 3) == 0 && al4) return KM_HW4;
+  if (a.HW == 1 && (a.C & 3) == 0 && al4) return KM_ROW;
   return KM_GEN;
 }
 static int chain_kind(const FastArgs& a) {

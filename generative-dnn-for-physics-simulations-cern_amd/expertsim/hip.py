@@ -28,7 +28,8 @@ class View(C.Structure):
 
 class Dropout(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("stream", C.c_uint32), ("threshold", C.c_uint32),
-                ("scale", C.c_float), ("enabled", C.c_int), ("step_ptr", C.c_void_p), ("step_mul", C.c_int32)]
+                ("scale", C.c_float), ("enabled", C.c_int), ("step_ptr", C.c_void_p), ("step_mul", C.c_int32),
+                ("index_offset", C.c_uint64)]
 
 
 class ConvDesc(C.Structure):
@@ -50,7 +51,7 @@ class Chain(C.Structure):
 
 class GenLoss(C.Structure):
     _fields_ = [("n", C.c_int), ("latent", C.c_int), ("noise", C.c_int), ("di_strength", C.c_float),
-                ("in_strength", C.c_float), ("aux_strength", C.c_float)]
+                ("in_strength", C.c_float), ("aux_strength", C.c_float), ("std_mean", C.c_void_p)]
 
 
 P = C.c_void_p
@@ -79,6 +80,10 @@ _SIGS = {
     "es_norm_bwd_ws_bytes": (I64, [P, C.c_int, C.c_int]),
     "es_norm_act_bwd": (C.c_int, [P, C.c_int, P, P, P, P, C.c_int, P, P, C.c_int, P, P, C.c_int, P,
                                   C.c_float, P, P, P, P, P]),
+    "es_norm_stats_merge": (C.c_int, [P, C.c_int, C.c_int, P, P]),
+    "es_norm_stats_local": (C.c_int, [P, C.c_int, P, P, P, P]),
+    "es_norm_bwd_sync": (C.c_int, [C.c_int, P, C.c_int, P, P, P, P, C.c_int, P, P, C.c_int, P, P, C.c_float, P, P,
+                                   P, P, P]),
     "es_act_fwd": (C.c_int, [P, C.c_int, P, P, P, C.c_int, P, P]),
     "es_channel_sum_ws_bytes": (I64, [P]),
     "es_channel_sum": (C.c_int, [P, C.c_int, P, P, C.c_float, P, P]),
@@ -105,8 +110,10 @@ _SIGS = {
     "es_image_expsum_bwd": (C.c_int, [P, C.c_int, P, P, P, P, C.c_float, P]),
     "es_router_gumbel": (C.c_int, [P, P, C.c_int, C.c_int, C.c_float, P, P, P, P]),
     "es_router_alb": (C.c_int, [P, C.c_int, C.c_int, C.c_float, C.c_float, P, P, P]),
-    "es_router_loss": (C.c_int, [P, P, P, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, P, P,
-                                 P]),
+    "es_router_loss": (C.c_int, [P, P, P, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, P,
+                                 C.c_int, P, P, C.c_int, P, P, P]),
+    "es_router_colsum": (C.c_int, [P, C.c_int, C.c_int, P, P]),
+    "es_dp_metrics_merge": (C.c_int, [P, C.c_int, C.c_int, P, P]),
     "es_scatter_rows": (C.c_int, [P, P, C.c_int, P, P]),
     "es_adam": (C.c_int, [P, P, P, P, I64, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int,
                           C.c_float, P]),
@@ -114,8 +121,8 @@ _SIGS = {
     "es_ema_update": (C.c_int, [P, P, I64, C.c_float, C.c_float, P]),
     "es_randn": (C.c_int, [P, I64, C.c_uint64, C.c_uint32, P]),
     "es_rand_exponential": (C.c_int, [P, I64, C.c_uint64, C.c_uint32, P]),
-    "es_randn_dev": (C.c_int, [P, I64, C.c_uint64, C.c_uint32, P, C.c_int32, P]),
-    "es_rand_exponential_dev": (C.c_int, [P, I64, C.c_uint64, C.c_uint32, P, C.c_int32, P]),
+    "es_randn_dev": (C.c_int, [P, I64, C.c_uint64, C.c_uint32, P, C.c_int32, I64, P]),
+    "es_rand_exponential_dev": (C.c_int, [P, I64, C.c_uint64, C.c_uint32, P, C.c_int32, I64, P]),
     "es_counter_add": (C.c_int, [P, C.c_int32, P]),
     "es_dropout_mask": (C.c_int, [P, I64, P, P]),
 }
@@ -209,12 +216,16 @@ def set_step_counter(t):
     _STEP_COUNTER = t
 
 
-def dropout_struct(p: float = 0.0, seed: int = 0, stream: int = 0, enabled: bool = False) -> Dropout:
+def dropout_struct(p: float = 0.0, seed: int = 0, stream: int = 0, enabled: bool = False,
+                   index_offset: int = 0) -> Dropout:
+    """index_offset: logical element index of the tensor's first element in the global batch
+    (data-parallel ranks: first sample of the rank's rows x elements per sample)."""
     d = Dropout()
     d.enabled = 1 if (enabled and p > 0.0) else 0
     if d.enabled:
         d.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         d.stream = int(stream) & 0xFFFFFFFF
+        d.index_offset = int(index_offset)
         if _STEP_COUNTER is not None:
             d.step_ptr = _STEP_COUNTER.data_ptr()
             d.step_mul = STEP_STREAM_MUL

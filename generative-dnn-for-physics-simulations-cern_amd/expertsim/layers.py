@@ -401,6 +401,16 @@ def _count_batch(nbt):
         _NBT_PENDING[id(nbt)] = (t, k + 1)
 
 
+# Data-parallel SyncBN (expertsim/train/ddp.py): while set, train-mode BatchNorm statistics are
+# all-gathered and backward sums all-reduced across ranks (set around an expert's step by MoEWrapper)
+_NORM_SYNC = None
+
+
+def set_norm_sync(ddp):
+    global _NORM_SYNC
+    _NORM_SYNC = ddp
+
+
 class NormOp:
     """BatchNorm (train: batch stats + running update), GroupNorm or LayerNorm, fused with the
     dropout / activation chain that follows it in the reference's nn.Sequential."""
@@ -423,6 +433,24 @@ class NormOp:
         mean = torch.empty(n_groups, dtype=torch.float32, device=dev)
         invstd = torch.empty(n_groups, dtype=torch.float32, device=dev)
         bn_part = getattr(x, "bn_part", None)
+        sync = _NORM_SYNC
+        if self.kind == hip.NORM_BN and train and sync is not None:
+            # SyncBN: the rank's (count, mean, M2) per channel, all-gathered, merged over the ranks
+            Cc = x.dims[1]
+            local = torch.empty(3, Cc, dtype=torch.float32, device=dev)
+            if bn_part is not None:
+                part, chunks = bn_part
+                hip.call("es_norm_stats_merge", hip.ptr(part), chunks, Cc, hip.ptr(local), hip.stream_ptr())
+            else:
+                wsb = ws(hip.lib().es_norm_stats_ws_bytes(C.byref(x.view), self.kind, 1), dev)
+                hip.call("es_norm_stats_local", C.byref(x.view), x.dt, x.ptr, hip.ptr(wsb), hip.ptr(local),
+                         hip.stream_ptr())
+            allp = sync.all_gather(local)
+            hip.call("es_norm_stats_finalize", hip.ptr(allp), sync.world, Cc, float(self.eps), hip.ptr(mean),
+                     hip.ptr(invstd), hip.ptr(self.rm), hip.ptr(self.rv), float(self.momentum), hip.stream_ptr())
+            if self.nbt is not None:
+                _count_batch(self.nbt)
+            return mean, invstd
         if self.kind == hip.NORM_BN and train and bn_part is not None:
             # partials from the producing conv's epilogue (ConvOp.fwd(bn_stats=True))
             part, chunks = bn_part
@@ -468,6 +496,25 @@ class NormOp:
             dx = x.like_nhwc(dx_dtype or dy.t.dtype)
         wsb = ws(hip.lib().es_norm_bwd_ws_bytes(C.byref(x.view), self.kind, self.groups), x.t.device)
         assert addend is None, "residual addend handled through act_ref"
+        sync = _NORM_SYNC
+        if self.kind == hip.NORM_BN and sync is not None:
+            # SyncBN backward: the rank's sums of dnorm and dnorm*xhat, all-reduced, applied with the
+            # global row count (dgamma / dbeta stay local: parameter gradients are all-reduced later)
+            assert act_ref is None and beta == 0.0, "SyncBN backward: no act_ref / accumulation"
+            Cc = x.dims[1]
+            sums = torch.empty(2, Cc, dtype=torch.float32, device=x.t.device)
+            args = lambda ph, cnt, dsm: (ph, C.byref(x.view), x.dt, x.ptr, C.byref(nm), C.byref(chain),
+                                         C.byref(dy.view), dy.dt, dy.ptr, C.byref(dx.view), dx.dt, dx.ptr,
+                                         hip.ptr(sums), float(cnt), hip.ptr(dgamma) if ph == 0 else None,
+                                         hip.ptr(dbeta) if ph == 0 else None, dsm, hip.ptr(wsb), hip.stream_ptr())
+            hip.call("es_norm_bwd_sync", *args(0, 0.0, None))
+            sync.all_reduce_(sums)
+            rows = x.dims[0] * x.dims[2] * x.dims[3]
+            hip.call("es_norm_bwd_sync", *args(1, sync.bn_rows(rows, x.dims[0]),
+                                                hip.ptr(dsum) if (dsum is not None and Cc <= 1024) else None))
+            if dsum is not None and Cc > 1024:
+                channel_sum(dx, dsum, 1.0)
+            return dx
         hip.call("es_norm_act_bwd", C.byref(x.view), x.dt, x.ptr, C.byref(nm), C.byref(chain),
                  C.byref(dy.view), dy.dt, dy.ptr,
                  C.byref(act_ref.view) if act_ref is not None else None,

@@ -13,11 +13,13 @@ on the device; the only host synchronisation is the expert-size read when n_expe
 
 Randomness: noise / Gumbel draws come from device Philox streams unless ``noise_fn`` /
 ``gumbel_fn`` inject them (parity tests); dropout masks are Philox streams keyed by
-(step, expert, pass, layer), with the data-parallel rank in the Philox key (``philox.rank_seed``)
-so ranks draw independent noise, Gumbel and dropout — expertsim/utils/philox.py.
+(step, expert, pass, layer) at the GLOBAL element index (data-parallel ranks draw their rows of the
+single-device draws) — expertsim/utils/philox.py.
 
 Data parallel (expertsim/train/ddp.py): with ``self.ddp`` set, each rank routes its own shard,
-gradients of every optimizer phase are all-reduced (RCCL) before the fused Adam.
+gradients of every optimizer phase are all-reduced (RCCL) before the fused Adam; with
+``ddp.sync_bn`` the batch-coupled statistics are global and the step equals the single-device
+step of the global batch.
 """
 from __future__ import annotations
 
@@ -33,7 +35,7 @@ from torch import nn
 
 from .. import hip
 from ..config import cfg_get
-from ..layers import Act, copy_act, defer_num_batches
+from ..layers import Act, copy_act, defer_num_batches, set_norm_sync
 from ..rng import DeviceRNG
 from ..utils import philox
 
@@ -61,7 +63,7 @@ class MoEWrapper(nn.Module):
         self.g_steps = [0 for _ in range(n_experts)]
         self.d_steps = [0 for _ in range(n_experts)]
         self.rng_seed = int(cfg_get(cfg, "train.rng_seed", 1234))
-        self._rank = 0
+        self.rank = 0
         self.rng = DeviceRNG(self.rng_seed)
         self.noise_fn = None       # optional injection: fn(expert, which, shape) -> tensor
         self.gumbel_fn = None      # optional injection: fn(shape) -> Exp(1) tensor
@@ -70,20 +72,6 @@ class MoEWrapper(nn.Module):
         self._ed_feat = None       # [B] per-sample photon sums for the router's ED term
         self._dstep = None         # device int32 step counter: dropout / noise streams (graph replay)
         self.set_precision(cfg_get(cfg, "train.precision", "fp32"))
-
-    @property
-    def rank(self) -> int:
-        return self._rank
-
-    @rank.setter
-    def rank(self, r: int):
-        """Data-parallel rank: re-keys the noise / Gumbel / dropout Philox streams of this rank."""
-        self._rank = int(r)
-        self.rng = DeviceRNG(philox.rank_seed(self.rng_seed, self._rank))
-
-    @property
-    def dropout_seed(self) -> int:
-        return philox.rank_seed(self.rng_seed, self._rank)
 
     def set_precision(self, precision: str):
         """fp32: every GEMM on fp32 MFMA (parity mode).  bf16: generator and aux-regressor GEMM
@@ -102,19 +90,20 @@ class MoEWrapper(nn.Module):
             m.compute_dtype = d_low
 
     # ---------------------------------------------------------------------------- helpers
-    def _noise(self, expert, which, shape, device):
+    def _noise(self, expert, which, shape, device, row0=0):
+        """row0: the rows' first index in the expert's global batch (data parallel)."""
         if self.noise_fn is not None:
             return self.noise_fn(expert, which, shape).to(device=device, dtype=torch.float32).contiguous()
-        return self.rng.normal(torch.empty(shape, dtype=torch.float32, device=device))
+        return self.rng.normal(torch.empty(shape, dtype=torch.float32, device=device), offset=row0 * shape[1])
 
-    def _gumbel(self, shape, device):
+    def _gumbel(self, shape, device, row0=0):
         if self.gumbel_fn is not None:
             return self.gumbel_fn(shape).to(device=device, dtype=torch.float32).contiguous()
-        return self.rng.exponential(torch.empty(shape, dtype=torch.float32, device=device))
+        return self.rng.exponential(torch.empty(shape, dtype=torch.float32, device=device), offset=row0 * shape[1])
 
-    def _allreduce(self, module):
+    def _allreduce(self, module, average=True):
         if self.ddp is not None:
-            self.ddp.allreduce_grads(module)
+            self.ddp.allreduce_grads(module, average)
 
     # ---------------------------------------------------------------------------- the step
     def train_step(self, epoch, cond, real_images, true_positions, std, intensity, aux_reg_optimizers,
@@ -153,8 +142,9 @@ class MoEWrapper(nn.Module):
         step = self.step_count
         rc = self.cfg.model.router
 
+        ddp = self.ddp
         tau = max(rc.tau_min, rc.tau_start * (rc.tau_decay ** epoch))          # moe.py:62-74
-        expo = self._gumbel((B, E), dev)
+        expo = self._gumbel((B, E), dev, row0=(ddp.rank * B if ddp is not None else 0))
         gates, logits, idx, counts, rctx = self.router.fwd(cond, expo, tau)
 
         for i in range(E):                                                       # moe.py:115-119
@@ -172,8 +162,12 @@ class MoEWrapper(nn.Module):
             for e in range(E):
                 rows = np.nonzero(idx_h == e)[0].astype(np.int32)
                 groups.append((e, rows, rows.size))
-        if self.ddp is not None:
-            groups = self.ddp.global_groups(groups, B)
+        if ddp is not None:
+            groups = ddp.global_groups(groups, B)
+            if ddp.sync_bn and any(ddp.global_count(e) > 1 and ddp._local[e] == 0 for e in range(E)):
+                # every rank sees the same count matrix, so every rank raises here together
+                raise RuntimeError("sync_bn: a rank holds no sample of an active expert (its SyncBN "
+                                   "collectives could not be matched); use larger shards or sync_bn=False")
 
         # metrics buffer: per expert [total, gen, div, int, aux, std_int, mean_int, w, disc]
         mbuf = torch.zeros(E, 9, dtype=torch.float32, device=dev)
@@ -181,18 +175,25 @@ class MoEWrapper(nn.Module):
         self._ed_feat = (torch.zeros(B, dtype=torch.float32, device=dev)
                          if E > 1 and float(rc.ed_strength) != 0.0 else None)
         for e, rows, be in groups:
-            be_global = be if self.ddp is None else self.ddp.global_count(e)
+            be_global = be if ddp is None else ddp.global_count(e)
             if be_global <= 1:                                                   # moe.py:126-135
                 continue
             og, od, oa = generator_optimizers[e], discriminator_optimizers[e], aux_reg_optimizers[e]
-            if be > 1:
+            # SyncBN: global batch statistics, so even one local sample runs
+            if be > 1 or (ddp is not None and ddp.sync_bn and be >= 1):
                 self._expert_step(e, rows, be, B, cond, real_images, true_positions, std, intensity,
                                   og, od, oa, mbuf, step, dev)
             else:
                 # DDP: expert active globally but (almost) absent from this shard -> zero local
-                # gradients, but join the same collectives and optimizer steps as the other ranks
+                # gradients, but join the same collectives and optimizer steps as the other ranks;
+                # the two noise draws' stream ids are consumed so later draws stay aligned
+                if self.noise_fn is None and self.rng.step_counter is not None:
+                    self.rng.calls += 2
                 self._allreduce(self.discriminators[e]); od.step()
                 self._allreduce(self.generators[e]); self._allreduce(self.aux_regs[e]); og.step(); oa.step()
+
+        if ddp is not None:
+            ddp.merge_metrics(mbuf)          # the global batch's per-expert metrics on every rank
 
         # ---- router (moe.py:213-449)
         zero = torch.zeros((), dtype=torch.float32, device=dev)
@@ -209,17 +210,31 @@ class MoEWrapper(nn.Module):
             rl = torch.zeros(3, dtype=torch.float32, device=dev)
             dlogits = torch.empty(B, E, dtype=torch.float32, device=dev)
             ed_on = float(rc.ed_strength) != 0.0
+            colsum = feat_all = idx_all = None
+            B_tot, B_all = B, B
+            if ddp is not None:
+                # the ALB / entropy terms see the global gate sums, the ED term the global batch
+                colsum = torch.empty(E, dtype=torch.float32, device=dev)
+                hip.call("es_router_colsum", hip.ptr(gates), B, E, hip.ptr(colsum), hip.stream_ptr())
+                ddp.all_reduce_(colsum)
+                B_tot = B * ddp.world
+                if ed_on:
+                    feat_all, idx_all, B_all = ddp.all_gather(self._ed_feat), ddp.all_gather(idx), B_tot
             hip.call("es_router_loss", hip.ptr(gates), hip.ptr(idx) if ed_on else None,
                      hip.ptr(self._ed_feat) if ed_on else None, B, E, float(tau),
                      float(rc.alb_strength * dec_w), float(rc.util_strength), float(rc.ed_strength),
+                     hip.ptr(colsum), B_tot, hip.ptr(feat_all), hip.ptr(idx_all), B_all,
                      hip.ptr(rl), hip.ptr(dlogits), hip.stream_ptr())
+            if ddp is not None and ed_on:
+                ddp.all_reduce_(rl[2:3])       # the ED sum over every rank's rows
             alb = rl[0] / dec_w if rc.alb_strength != 0 else zero
             ent = rl[1] if rc.util_strength != 0 else zero
             ed = rl[2] if ed_on else zero
             router_loss = ed + gan + diff + ent + dec_w * alb
             if epoch < rc.stop_router_training_epoch:
                 self.router.bwd(rctx, dlogits)
-                self._allreduce(self.router)
+                # summed, not averaged: the router terms are functions of global sums
+                self._allreduce(self.router, average=False)
                 router_optimizer.step()
             else:
                 router_loss = zero
@@ -264,11 +279,26 @@ class MoEWrapper(nn.Module):
         w_dev = torch.full((1,), w, dtype=torch.float32, device=dev)
         # the step term (step * 1024) is added on the device from self._dstep
         sb = lambda pid: philox.dropout_stream(0, e, pid, 0)
-        seed = self.dropout_seed
+        seed = self.rng_seed
+        ddp = self.ddp
+        n0 = ddp.sample_offset(e) if ddp is not None else 0     # first global sample index
+        sync = ddp is not None and ddp.sync_bn
+        if sync:
+            ddp.expert = e
+            set_norm_sync(ddp)
+        try:
+            self._expert_program(e, be, B, G, D, A, sc, sr, sp, ss, si, opt_g, opt_d, opt_a, mbuf, dev, w_dev,
+                                 sb, seed, n0, sync, rows, ridx)
+        finally:
+            set_norm_sync(None)
+
+    def _expert_program(self, e, be, B, G, D, A, sc, sr, sp, ss, si, opt_g, opt_d, opt_a, mbuf, dev, w_dev, sb,
+                        seed, n0, sync, rows, ridx):
+        ddp = self.ddp
 
         # ---- generator forward #1 (moe.py:144-145)
-        n1 = self._noise(e, 0, (be, self.noise_dim), dev)
-        fake1, gctx1 = G.fwd(n1, sc, seed=seed, stream_base=sb(philox.PASS_G1))
+        n1 = self._noise(e, 0, (be, self.noise_dim), dev, row0=n0)
+        fake1, gctx1 = G.fwd(n1, sc, seed=seed, stream_base=sb(philox.PASS_G1), n_offset=n0)
 
         # ---- discriminator step (moe.py:506-527)
         ro, _, dctx_r = D.fwd(Act.of(sr), sc)
@@ -283,8 +313,8 @@ class MoEWrapper(nn.Module):
         opt_d.step()
 
         # ---- generator step (moe.py:529-571)
-        n2 = self._noise(e, 1, (be, self.noise_dim), dev)
-        fake2, gctx2 = G.fwd(n2, sc, seed=seed, stream_base=sb(philox.PASS_G2))
+        n2 = self._noise(e, 1, (be, self.noise_dim), dev, row0=n0)
+        fake2, gctx2 = G.fwd(n2, sc, seed=seed, stream_base=sb(philox.PASS_G2), n_offset=n0)
         fo1, fl1, dctx1 = D.fwd(fake1, sc)
         _, fl2, dctx2 = D.fwd(fake2, sc)
         s = torch.empty(be, dtype=torch.float32, device=dev)
@@ -292,12 +322,19 @@ class MoEWrapper(nn.Module):
         if self._ed_feat is not None:
             hip.call("es_scatter_rows", hip.ptr(s), hip.ptr(ridx) if rows is not None else None, be,
                      hip.ptr(self._ed_feat), hip.stream_ptr())
-        coords, actx = A.fwd(fake1, seed=seed, stream_base=sb(philox.PASS_AUX))
+        coords, actx = A.fwd(fake1, seed=seed, stream_base=sb(philox.PASS_AUX), n_offset=n0)
         L = fl1.dims[1]
         p = hip.GenLoss()
         p.n, p.latent, p.noise = be, L, self.noise_dim
         p.di_strength, p.in_strength = float(G.di_strength), float(G.in_strength)
         p.aux_strength = float(self.cfg.model.aux_reg.strength)
+        if sync:
+            # SDI prefactor mean(std)^2 over the expert's global batch (moe.py:573-588)
+            std_mean = torch.empty(1, dtype=torch.float32, device=dev)
+            hip.call("es_router_colsum", hip.ptr(ss), be, 1, hip.ptr(std_mean), hip.stream_ptr())
+            ddp.all_reduce_(std_mean)
+            copy_act(Act.of(std_mean.view(1, 1)), Act.of(std_mean.view(1, 1)), 1.0 / ddp.global_count(e), 0.0)
+            p.std_mean = std_mean.data_ptr()
         dfo1 = torch.empty(be, 1, dtype=torch.float32, device=dev)
         dl1 = torch.empty(be, L, dtype=torch.float32, device=dev)
         dl2 = torch.empty(be, L, dtype=torch.float32, device=dev)

@@ -71,7 +71,8 @@ class AuxRegNeutron(ExpertModule):
         d = hip.dropout_struct(P_DROP, seed, stream_base + layer, enabled=train)
         return hip.chain_struct(hip.ACT_LRELU, SLOPE, d, dropout_first=False)
 
-    def fwd(self, img: Act, seed=0, stream_base=0, train=True):
+    def fwd(self, img: Act, seed=0, stream_base=0, train=True, n_offset=0):
+        """n_offset: first sample's index in the expert's global batch (dropout index offset)."""
         o = self.ops()
         cdt = self.compute_dtype
         x = img
@@ -83,6 +84,7 @@ class AuxRegNeutron(ExpertModule):
         keep = c["keep"] = []   # dropout keep bits: drawn in the forward norm pass, re-read backward
 
         def bn(name, h, chain):
+            chain.drop.index_offset = int(n_offset) * h.dims[1] * h.dims[2] * h.dims[3]
             keep.append(hip.attach_keep(chain, h.dims[0] * h.dims[2] * h.dims[3], h.dims[1], h.t.device))
             return o[name].fwd(h, chain, train=train)
         c["h1"] = o["c1"].fwd(x)

@@ -80,8 +80,10 @@ class GeneratorNeutron(ExpertModule):
         return hip.chain_struct(hip.ACT_LRELU, SLOPE, d, dropout_first=True)
 
     # --------------------------------------------------------------------------- forward
-    def fwd(self, noise: torch.Tensor, cond: torch.Tensor, seed=0, stream_base=0, train=True):
-        """noise [B,10] fp32, cond [B,9] fp32 (device) -> (image Act [B,1,44,44] fp32 NHWC, ctx)."""
+    def fwd(self, noise: torch.Tensor, cond: torch.Tensor, seed=0, stream_base=0, train=True, n_offset=0):
+        """noise [B,10] fp32, cond [B,9] fp32 (device) -> (image Act [B,1,44,44] fp32 NHWC, ctx).
+        n_offset: index of the first sample in the expert's global batch (data parallel: dropout
+        masks are drawn at the global sample index, expertsim/utils/philox.py)."""
         o = self.ops()
         k, F2 = self.base, self.fc2_features
         cdt = self.compute_dtype
@@ -93,9 +95,10 @@ class GeneratorNeutron(ExpertModule):
         copy_act(Act.of(cond), Act.of(x0m[:, self.noise_dim:]))
         ch = [self._chain(seed, stream_base, i, train) for i in range(5)]
         # dropout keep bits, drawn once in the forward norm pass and re-read by the backward
-        keep = [hip.attach_keep(ch[i], B * r, c, dev)
-                for i, (r, c) in enumerate(((1, 256), (1, F2), ((2 * k - 2) ** 2, 256), ((4 * k - 6) ** 2, 128),
-                                            ((4 * k - 7) ** 2, 64)))]
+        per_sample = ((1, 256), (1, F2), ((2 * k - 2) ** 2, 256), ((4 * k - 6) ** 2, 128), ((4 * k - 7) ** 2, 64))
+        keep = [hip.attach_keep(ch[i], B * r, c, dev) for i, (r, c) in enumerate(per_sample)]
+        for i, (r, c) in enumerate(per_sample):
+            ch[i].drop.index_offset = int(n_offset) * r * c
         h1 = o["fc1"].fwd(x0)
         y1, s1 = o["bn1"].fwd(h1, ch[0], train=train)
         h2 = o["fc2"].fwd(y1)

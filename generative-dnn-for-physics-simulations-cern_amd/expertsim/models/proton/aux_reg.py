@@ -76,7 +76,7 @@ class AuxReg(ExpertModule):
         ops["l8"] = conv("regressor.8")
         return ops
 
-    def fwd(self, img: Act, seed=0, stream_base=0, train=True):
+    def fwd(self, img: Act, seed=0, stream_base=0, train=True, n_offset=0):
         o = self.ops()
         cdt = self.compute_dtype
         x = img
@@ -113,8 +113,8 @@ class AuxReg(ExpertModule):
             fc = c["f"].like_nhwc(cdt)
             copy_act(c["f"], fc)
         c["fc"] = fc
-        d0 = hip.dropout_struct(P_DROP, seed, stream_base + 0, enabled=train)
-        d1 = hip.dropout_struct(P_DROP, seed, stream_base + 1, enabled=train)
+        d0 = hip.dropout_struct(P_DROP, seed, stream_base + 0, enabled=train, index_offset=int(n_offset) * 128)
+        d1 = hip.dropout_struct(P_DROP, seed, stream_base + 1, enabled=train, index_offset=int(n_offset) * 64)
         c["ch0"] = hip.chain_struct(hip.ACT_LRELU, SLOPE, d0, dropout_first=False)
         c["ch1"] = hip.chain_struct(hip.ACT_LRELU, SLOPE, d1, dropout_first=False)
         c["r0"] = o["l0"].fwd(fc)

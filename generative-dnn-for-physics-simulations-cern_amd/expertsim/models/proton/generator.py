@@ -54,7 +54,7 @@ class Generator(ExpertModule):
             "c11": conv("conv_layers.11"),
         }
 
-    def fwd(self, noise, cond, seed=0, stream_base=0, train=True):
+    def fwd(self, noise, cond, seed=0, stream_base=0, train=True, n_offset=0):
         o = self.ops()
         cdt = self.compute_dtype
         dev = noise.device

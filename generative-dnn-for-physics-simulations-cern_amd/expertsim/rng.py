@@ -4,7 +4,8 @@ so no generator state lives on the device.
 
 Inside a train step (``begin_step(counter)``) the stream id of the i-th draw is
 ``stream_base + i + counter[0] * 256``, the step term added on the device: a captured HIP graph
-of the step draws new numbers at every replay."""
+of the step draws new numbers at every replay.  Every rank of a data-parallel run issues the same
+sequence of draws (same stream ids) and takes its own rows of each through the element offset."""
 from __future__ import annotations
 
 import torch
@@ -34,7 +35,7 @@ class DeviceRNG:
         self.counter += 1
         return self.counter & 0xFFFFFFFF
 
-    def _draw(self, name, out):
+    def _draw(self, name, out, offset=0):
         hip.require_device(out)
         if self.step_counter is not None:
             if self.calls >= STEP_MUL:
@@ -42,16 +43,19 @@ class DeviceRNG:
             sid = (self.stream_base + self.calls) & 0xFFFFFFFF
             self.calls += 1
             hip.call(name + "_dev", hip.ptr(out), out.numel(), self.seed, sid, hip.ptr(self.step_counter), STEP_MUL,
-                     hip.stream_ptr())
+                     int(offset), hip.stream_ptr())
         else:
-            hip.call(name, hip.ptr(out), out.numel(), self.seed, self._next(), hip.stream_ptr())
+            hip.call(name + "_dev", hip.ptr(out), out.numel(), self.seed, self._next(), None, 0, int(offset),
+                     hip.stream_ptr())
         return out
 
-    def normal(self, out: torch.Tensor):
-        return self._draw("es_randn", out)
+    def normal(self, out: torch.Tensor, offset: int = 0):
+        """out[i] = draw number offset + i of this call's stream (offset even): a data-parallel rank
+        passes its first global row x row length and draws exactly its rows of the global draw."""
+        return self._draw("es_randn", out, offset)
 
-    def exponential(self, out: torch.Tensor):
-        return self._draw("es_rand_exponential", out)
+    def exponential(self, out: torch.Tensor, offset: int = 0):
+        return self._draw("es_rand_exponential", out, offset)
 
 
 _default = None

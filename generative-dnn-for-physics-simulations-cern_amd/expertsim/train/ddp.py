@@ -1,17 +1,33 @@
-"""Data parallelism for the training step: one process per GPU, RCCL (backend "nccl") all-reduce.
+"""Data parallelism for the training step: one process per GPU, RCCL (backend "nccl") collectives.
 
 The reference is single-device (expertsim/train/loop.py:39); north_star asks for the batch sharded
-data-parallel over a node's GPUs.  Semantics chosen:
-  * every rank routes and trains on its own shard of B_local samples;
-  * per-expert loss weights use the LOCAL counts (B_e^r / B_r) and gradients are AVERAGED over
-    ranks, which reproduces the single-device gradient exactly for every per-sample-mean term
-    (hinge, generator hinge, intensity L1, log-cosh): (1/R) sum_r (1/B_r) sum_{b in r} g_b
-    = (1/B) sum_b g_b;
-  * batch-coupled statistics (BatchNorm batch stats, the SDI mean(std)^2 product) stay per rank,
-    as torch DDP without SyncBatchNorm does;
+data-parallel over a node's GPUs.  Semantics:
+
+  * the global batch is the ranks' equal shards in rank order; every rank routes its own shard;
+  * randomness is drawn at GLOBAL sample indices: a rank holding samples [n0, n0 + n) of an
+    expert's global batch draws exactly those rows of the single-device noise / Gumbel draws and
+    dropout masks (expertsim/utils/philox.py), n0 = the lower ranks' counts for that expert
+    (``sample_offset``);
+  * per-expert loss weights use the LOCAL counts (B_e^r / B_r) and the gradients of the generator,
+    discriminator and aux regressor are AVERAGED over ranks, which reproduces the single-device
+    gradient exactly for every per-sample-mean term (hinge, generator hinge, intensity L1,
+    log-cosh): (1/R) sum_r (1/B_r) sum_{b in r} g_b = (1/B) sum_b g_b;
+  * batch-coupled statistics:
+      - ``sync_bn=True``: BatchNorm batch statistics and backward sums of the neutron generator and
+        aux regressor are all-gathered / all-reduced per layer (SyncBN), the SDI prefactor
+        mean(std)^2 uses the expert's global mean, the router's ALB / entropy terms the global
+        gate sums S_e and its ED term the all-gathered per-sample features -- with equal shards the
+        data-parallel step then equals the single-device step of the global batch (tests:
+        tests/test_ddp_gpu.py on the HIP path, tests/test_ddp_cpu.py on the oracle);
+      - ``sync_bn=False`` (default, torch-DDP-without-SyncBatchNorm behaviour, no collective inside
+        the forward / backward): those statistics stay per rank (tests/test_ddp_cpu.py measures the
+        deviation from the global-batch step);
+  * the router's gradient is SUMMED over ranks (its ALB / entropy / ED terms are functions of
+    global sums, not per-sample means);
   * an expert is trained iff its GLOBAL count is > 1 (the reference's skip rule, moe.py:126, on
-    the global batch); a rank whose local count is <= 1 contributes zero gradients but still joins
-    every collective, so the collective sequence is identical on all ranks;
+    the global batch); a rank with too few local samples contributes zero gradients but joins every
+    collective, so the collective sequence is identical on all ranks;
+  * metrics are merged across ranks on the device (one all-gather of the [E, 10] metric rows);
   * one flat all-reduce per model per optimizer phase (D; G and A; router) — the flat parameter
     buffers make each model a single bucket.
 """
@@ -21,36 +37,77 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from .. import hip
+
 
 class DataParallel:
-    def __init__(self, world_size=None, rank=None, group=None):
+    def __init__(self, world_size=None, rank=None, group=None, sync_bn=False):
         self.group = group
         self.world = world_size if world_size is not None else dist.get_world_size(group)
         self.rank = rank if rank is not None else dist.get_rank(group)
-        self._counts = None
+        self.sync_bn = bool(sync_bn)
+        self.gloo = dist.get_backend(group) != "nccl"
+        self._counts = None        # global count per expert
+        self._offsets = None       # this rank's first global sample index per expert
+        self._local = None         # local count per expert
         self.local_batch = None
         self._counts_dev = {}
+        self.expert = None         # expert whose step is running (global count for SyncBN)
+
+    # ---------------------------------------------------------------- collectives on device tensors
+    def all_reduce_(self, t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
+        if self.gloo and t.is_cuda:        # gloo (CPU tests / single-GPU rehearsals): via the host
+            h = t.cpu()
+            dist.all_reduce(h, op=op, group=self.group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=op, group=self.group)
+        return t
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """[world, *t.shape] (rank order), contiguous."""
+        t = t.contiguous()
+        if self.gloo:
+            src = t.cpu() if t.is_cuda else t
+            parts = [torch.empty_like(src) for _ in range(self.world)]
+            dist.all_gather(parts, src, group=self.group)
+            return torch.stack(parts).to(t.device)
+        out = torch.empty((self.world, *t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t, group=self.group)
+        return out
 
     # ---------------------------------------------------------------- routing bookkeeping
     def global_groups(self, groups, B_local):
-        """All-reduce the per-expert counts (one small collective) and keep local groups."""
+        """Global per-expert counts and this rank's sample offsets (one small all-gather for E > 1)."""
         E = len(groups)
         self.local_batch = B_local
         if E == 1:
-            # one expert holds every sample: its global count is the global batch (equal shards,
-            # as DistributedSampler(drop_last=True) and bench.py give) -- no collective, no host sync
+            # one expert holds every sample: equal shards (DistributedSampler(drop_last=True) and
+            # bench.py give them) -- no collective, no host sync
             self._counts = np.array([B_local * self.world], dtype=np.int64)
+            self._offsets = np.array([B_local * self.rank], dtype=np.int64)
+            self._local = np.array([B_local], dtype=np.int64)
             return groups
         local = torch.tensor([g[2] for g in groups], dtype=torch.int64)
-        dev = "cuda" if dist.get_backend(self.group) == "nccl" else "cpu"
-        t = local.to(dev)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
-        self._counts = t.cpu().numpy()
-        self.local_batch = B_local
+        if not self.gloo:
+            local = local.to(torch.device("cuda", torch.cuda.current_device()))
+        allc = self.all_gather(local).cpu().numpy()     # [world, E] (the routing host sync)
+        self._local = allc[self.rank]
+        self._counts = allc.sum(0)
+        self._offsets = allc[:self.rank].sum(0) if self.rank else np.zeros(E, dtype=np.int64)
         return groups
 
     def global_count(self, e):
         return int(self._counts[e])
+
+    def sample_offset(self, e):
+        """Index of this rank's first sample in expert e's global batch."""
+        return int(self._offsets[e])
+
+    @property
+    def batch_offset(self):
+        """Index of this rank's first sample in the global batch (equal shards)."""
+        return self.local_batch * self.rank
 
     @property
     def global_batch(self):
@@ -63,10 +120,29 @@ class DataParallel:
             self._counts_dev[key] = torch.from_numpy(self._counts.astype(np.float32)).to(device)
         return self._counts_dev[key]
 
+    # ---------------------------------------------------------------- SyncBN hooks (layers.NormOp)
+    def bn_rows(self, local_rows, local_n):
+        """Global row count of a BatchNorm input of the running expert: rows per sample x global n."""
+        return (local_rows // max(local_n, 1)) * self.global_count(self.expert)
+
     # ---------------------------------------------------------------- gradients
-    def allreduce_grads(self, module):
+    def allreduce_grads(self, module, average=True):
         """SUM-all-reduce the flat gradient buffer; the 1/world average is folded into the fused
         Adam's grad_scale (module._grad_scale), so no extra pass over the gradients."""
         g = module.flat_grads
-        dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group)
-        module._grad_scale = 1.0 / self.world
+        self.all_reduce_(g)
+        module._grad_scale = 1.0 / self.world if average else 1.0
+
+    # ---------------------------------------------------------------- metrics
+    def merge_metrics(self, mbuf: torch.Tensor):
+        """mbuf [E, 9] (per expert: total, gen, div, int, aux, std_int, mean_int, w, disc) -> the
+        global-batch values, in place (es_dp_metrics_merge over the all-gathered rows)."""
+        E = mbuf.shape[0]
+        rows = torch.empty(E, 10, dtype=torch.float32, device=mbuf.device)
+        rows[:, :9].copy_(mbuf)
+        ran = self._local >= (1 if self.sync_bn else 2)        # the ranks that ran the expert's step
+        n = torch.from_numpy(np.where(ran, self._local, 0).astype(np.float32))
+        rows[:, 9].copy_(n)
+        allr = self.all_gather(rows)
+        hip.call("es_dp_metrics_merge", hip.ptr(allr), self.world, E, hip.ptr(mbuf), hip.stream_ptr())
+        return mbuf

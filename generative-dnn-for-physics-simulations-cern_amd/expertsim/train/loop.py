@@ -126,7 +126,7 @@ def train(cfg, train_loader, test_loader=None, max_steps_per_epoch=None) -> List
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             dist.init_process_group("nccl", device_id=device)
-        moe.ddp = DataParallel()
+        moe.ddp = DataParallel(sync_bn=bool(cfg.train.get("sync_bn", False)))
         moe.rank = dist.get_rank()
     gen_optims, disc_optims, aux_optims, router_optim = setup_optimizers(moe, cfg)
     ema_helper = EMAHelper(moe, decay=0.99)                 # loop.py:44

@@ -103,8 +103,7 @@ def load_checkpoint(checkpoint_dir, epoch, moe, gen_optims, disc_optims, aux_reg
     if getattr(moe, "_dstep", None) is not None:
         moe._dstep.fill_(moe.step_count)
     moe.g_steps, moe.d_steps = list(st["g_steps"]), list(st["d_steps"])
-    moe.rng_seed = int(st["rng_seed"])     # base Philox key of dropout / noise / Gumbel draws
-    moe.rank = moe.rank                    # re-key this rank's device RNG from the base seed
+    moe.rng_seed = moe.rng.seed = int(st["rng_seed"])      # dropout / noise / Gumbel Philox key
     moe.rng.counter = int(st["rng_counter"])
     if ema_helper is not None and "ema" in st:
         ema_helper.load_state_dict(st["ema"])

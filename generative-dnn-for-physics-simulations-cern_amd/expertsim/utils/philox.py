@@ -20,10 +20,12 @@ with pass_id 0 = generator forward #1 (moe.py:145), 1 = generator forward #2 (mo
 and Gumbel draws (csrc/misc.hip randn / rand_exp) use 0x5EED0001 / 0x5EED0002 there, so the three
 families never share a Philox block whatever their stream ids.
 
-Data parallelism: the rank lives in the key, not in the stream id — every rank keys its dropout,
-noise and Gumbel draws with ``rank_seed(seed, rank)`` (rank in the key's high word; rank 0 keeps
-the plain seed, so single-device runs and the goldens are unchanged).  Ranks therefore draw
-independent masks and noise at every (step, expert, pass, layer).
+Data parallelism: the rank lives in neither the key nor the stream id but in the element index —
+a rank holding samples [n0, n0 + n) of an expert's global batch (the global batch is the rank
+shards in rank order, so n0 = the sum of the lower ranks' counts for that expert) draws elements
+n0 * (elements per sample) onwards of the single-device draw, for dropout masks as for noise and
+Gumbel draws (es_dropout_t.index_offset, es_randn_dev / es_rand_exponential_dev ``offset``).  Ranks
+therefore draw independent masks and noise, and together exactly the single-device ones.
 """
 from __future__ import annotations
 
@@ -42,11 +44,6 @@ def dropout_stream(step: int, expert: int, pass_id: int, layer: int) -> int:
     if not (0 <= expert < 32 and 0 <= pass_id < 4 and 0 <= layer < 8):
         raise ValueError(f"dropout_stream: expert {expert} / pass {pass_id} / layer {layer} out of range")
     return int(step) * 1024 + int(expert) * 32 + int(pass_id) * 8 + int(layer)
-
-
-def rank_seed(seed: int, rank: int) -> int:
-    """Philox key of a data-parallel rank: the rank is added to the key's high word."""
-    return (int(seed) + (int(rank) << 32)) & 0xFFFFFFFFFFFFFFFF
 
 
 def keep_threshold(p: float) -> int:
@@ -75,16 +72,20 @@ def philox4x32(ctr0, ctr1, ctr2, ctr3, key0: int, key1: int):
             c3.astype(np.uint32))
 
 
-def random_bits(n: int, seed: int, stream: int) -> np.ndarray:
-    """uint32 word for each logical element index 0..n-1."""
-    q = np.arange((n + 3) // 4, dtype=np.uint64)
+def random_bits(n: int, seed: int, stream: int, offset: int = 0) -> np.ndarray:
+    """uint32 word for each logical element index offset .. offset+n-1."""
+    q = np.arange(offset // 4, (offset + n + 3) // 4, dtype=np.uint64)
     words = philox4x32(q & MASK32, q >> np.uint64(32), np.uint64(stream & 0xFFFFFFFF), 0,
                        seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
-    return np.stack(words, axis=1).reshape(-1)[:n]   # element i = word (i & 3) of counter i >> 2
+    flat = np.stack(words, axis=1).reshape(-1)       # element i = word (i & 3) of counter i >> 2
+    s = offset % 4
+    return flat[s:s + n]
 
 
-def dropout_mask(shape, p: float, seed: int, stream: int) -> np.ndarray:
-    """Boolean keep-mask of ``shape`` (logical row-major element order)."""
+def dropout_mask(shape, p: float, seed: int, stream: int, n_offset: int = 0) -> np.ndarray:
+    """Boolean keep-mask of ``shape`` (logical row-major element order); ``n_offset``: index of the
+    tensor's first sample in the global batch (rows n_offset.. of the mask of the whole batch)."""
     n = int(np.prod(shape))
-    x = random_bits(n, seed, stream)
+    per = n // shape[0] if shape[0] else 0
+    x = random_bits(n, seed, stream, int(n_offset) * per)
     return ((x >> np.uint32(8)) < np.uint32(keep_threshold(p))).reshape(shape)

@@ -37,10 +37,14 @@ typedef struct {
   int64_t s[4];
 } es_view_t;
 
-/* Counter-based dropout (expertsim/utils/philox.py).  keep(i) = (philox(seed, stream, i) >> 8) <
- * threshold, i = NCHW-logical element index; kept values are multiplied by `scale` = 1/(1-p).
+/* Counter-based dropout (expertsim/utils/philox.py).  keep(i) = (philox(seed, stream, i + index_offset)
+ * >> 8) < threshold, i = NCHW-logical element index; kept values are multiplied by `scale` = 1/(1-p).
  * With step_ptr set, the stream used is stream + step_ptr[0] * step_mul, read on the device: a
- * captured HIP graph then draws fresh masks at every replay (the train step's step counter). */
+ * captured HIP graph then draws fresh masks at every replay (the train step's step counter).
+ * index_offset: logical index of this tensor's first element within the global batch (data-parallel
+ * rank r holding samples [n0, n0 + n) of an expert's batch passes n0 * C*H*W), so every rank draws
+ * exactly the single-device masks of its samples.  Must keep i + index_offset 4-aligned wherever i is
+ * (a multiple of 8 for C % 8 == 0 layers). */
 typedef struct {
   uint64_t seed;
   uint32_t stream;
@@ -49,6 +53,7 @@ typedef struct {
   int enabled;
   const int32_t* step_ptr; /* device int32 or NULL */
   int32_t step_mul;
+  uint64_t index_offset;
 } es_dropout_t;
 
 const char* es_last_error(void);
@@ -201,6 +206,25 @@ int es_norm_act_bwd(const es_view_t* x, es_dtype_t xdt, const void* xp, const es
                     const es_view_t* dx, es_dtype_t dxdt, void* dxp, float beta, float* dgamma,
                     float* dbeta, float* dsum, void* ws, es_stream_t stream);
 
+/* Data-parallel (synchronised) BatchNorm: the batch statistics of the neutron generator's and aux
+ * regressor's BatchNorms (neutron/generator.py:13,19,26,31,35; neutron/aux_reg.py:15-47) over the
+ * GLOBAL batch, as one device computes them for the reference.
+ *   es_norm_stats_merge: [chunks][3][C] (count, mean, M2) partials -> one [3][C] partial;
+ *   es_norm_stats_local: the rank's [3][C] partial straight from x (ws: es_norm_stats_ws_bytes);
+ * the caller all-gathers the ranks' [3][C] partials and finalizes them with es_norm_stats_finalize
+ * (world partials -> mean / invstd / running stats).
+ *   es_norm_bwd_sync phase 0: raw per-channel sums [2][C] (sum dnorm, sum dnorm*xhat) of the rank
+ *   into `sums`, and the rank's dgamma / dbeta accumulation; the caller all-reduces `sums`;
+ *   phase 1: dx from the global sums and the global row count `cnt` (+ dsum as es_norm_act_bwd).
+ * ws: es_norm_bwd_ws_bytes(x, ES_NORM_BN, 1). */
+int es_norm_stats_merge(const float* part, int chunks, int C, float* out, es_stream_t stream);
+int es_norm_stats_local(const es_view_t* x, es_dtype_t xdt, const void* xp, void* ws, float* out,
+                        es_stream_t stream);
+int es_norm_bwd_sync(int phase, const es_view_t* x, es_dtype_t xdt, const void* xp, const es_norm_t* nm,
+                     const es_chain_t* ch, const es_view_t* dy, es_dtype_t dydt, const void* dyp,
+                     const es_view_t* dx, es_dtype_t dxdt, void* dxp, float* sums, float cnt,
+                     float* dgamma, float* dbeta, float* dsum, void* ws, es_stream_t stream);
+
 /* Plain elementwise chain without normalisation (router LeakyReLU, final ReLU, casts):
  * y = chain(x). And its backward dx = beta*dx + dchain(dy) evaluated at x (or act_ref). */
 int es_act_fwd(const es_view_t* x, es_dtype_t xdt, const void* xp, const es_chain_t* ch,
@@ -295,6 +319,8 @@ int es_image_expsum(const es_view_t* x, es_dtype_t dt, const void* xp, float* s,
 typedef struct {
   int n, latent, noise;
   float di_strength, in_strength, aux_strength;
+  const float* std_mean; /* optional device scalar: mean(std) over the expert's GLOBAL batch (data
+                            parallel, SDI prefactor); NULL: the mean over these n samples */
 } es_gen_loss_t;
 int es_gen_losses(const es_gen_loss_t* p, const float* fo, const float* l1, const float* l2,
                   const float* n1, const float* n2, const float* std_, const float* s,
@@ -316,12 +342,21 @@ int es_router_alb(const float* gates, int B, int E, float tau, float coef, float
 /* All router-loss terms that carry gradient (moe.py:258-268,407-434; train/utils.py:372-395
  * calculate_expert_distribution_loss, 398-419 calculate_expert_utilization_entropy, 623-642 ALB):
  * out[0] = alb_coef*mean_e exp(1/(S_e+1e-6)); out[1] = util*sum_e avg_e*log(avg_e+1e-9)
- * (= -entropy*util); out[2] = 0.1*ed/B*sum_{a,b: idx_a=idx_b} |feat_a - feat_b| (cdist of the
- * [B,1] per-sample photon sums, gated by the straight-through one-hot gates); dlogits = d(sum of
- * the three)/d logits through the Gumbel softmax.  feat / idx may be NULL when ed_strength == 0. */
+ * (= -entropy*util, avg = S/B_total); out[2] = 0.1*ed/B_total*sum_{a,b: idx_a=idx_b} |feat_a - feat_b|
+ * (cdist of the [B,1] per-sample photon sums, gated by the straight-through one-hot gates);
+ * dlogits = d(sum of the three)/d logits through the Gumbel softmax, for the B rows of `gates`.
+ * Data parallel: colsum = the all-reduced S_e (NULL: this call's rows), B_total = the global batch
+ * (<= 0: B), feat_all / idx_all [B_all] = the all-gathered ED features (NULL: this call's rows); out
+ * then holds this rank's share of the ED sum.  feat / idx may be NULL when ed_strength == 0. */
 int es_router_loss(const float* gates, const int32_t* idx, const float* feat, int B, int E, float tau,
-                   float alb_coef, float util_strength, float ed_strength, float* out, float* dlogits,
+                   float alb_coef, float util_strength, float ed_strength, const float* colsum, int B_total,
+                   const float* feat_all, const int32_t* idx_all, int B_all, float* out, float* dlogits,
                    es_stream_t stream);
+/* out[e] = sum_b gates[b, e] (the rank's share of the router's gate sums). */
+int es_router_colsum(const float* gates, int B, int E, float* out, es_stream_t stream);
+/* Data-parallel merge of the per-expert metric rows: rows [world][E][10] (the 9 metric columns of
+ * MoEWrapper's buffer + the rank's sample count, 0 = not run) -> out [E][9], global-batch values. */
+int es_dp_metrics_merge(const float* rows, int world, int E, float* out, es_stream_t stream);
 /* dst[rows[i]] = src[i] for i < n (rows NULL: identity) -- moe.py:196-198 scatter of the
  * per-sample photon sums into the batch-ordered ED features. */
 int es_scatter_rows(const float* src, const int32_t* rows, int n, float* dst, es_stream_t stream);
@@ -344,11 +379,13 @@ int es_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, float l
 int es_randn(float* out, int64_t n, uint64_t seed, uint32_t stream_id, es_stream_t stream);
 int es_rand_exponential(float* out, int64_t n, uint64_t seed, uint32_t stream_id,
                         es_stream_t stream);
-/* Same draws with the stream id offset on the device: stream_id + step_ptr[0] * step_mul. */
+/* Same draws with the stream id offset on the device: stream_id + step_ptr[0] * step_mul, and the
+ * element counter starting at `offset` (out[i] = draw number offset + i; randn: offset even), so a
+ * data-parallel rank draws exactly its rows of the single-device draw. */
 int es_randn_dev(float* out, int64_t n, uint64_t seed, uint32_t stream_id, const int32_t* step_ptr,
-                 int32_t step_mul, es_stream_t stream);
+                 int32_t step_mul, int64_t offset, es_stream_t stream);
 int es_rand_exponential_dev(float* out, int64_t n, uint64_t seed, uint32_t stream_id,
-                            const int32_t* step_ptr, int32_t step_mul, es_stream_t stream);
+                            const int32_t* step_ptr, int32_t step_mul, int64_t offset, es_stream_t stream);
 /* counter[0] += v on the device (step counters of a captured train step). */
 int es_counter_add(int32_t* counter, int32_t v, es_stream_t stream);
 /* EMA of a flat parameter buffer — replaces EMAHelper.update (expertsim/train/loop.py:392-400):

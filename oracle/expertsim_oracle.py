@@ -203,15 +203,16 @@ def build_all(arch, n_experts, seed, noise_dim=10, cond_dim=9):
 class Dropper:
     """Counter-based dropout for one module pass (layer index advances per call)."""
 
-    def __init__(self, seed, step, expert, pass_id, rank=0):
-        # data-parallel ranks key their masks with the rank in the key (philox.rank_seed)
-        self.seed, self.step, self.expert, self.pass_id = philox.rank_seed(seed, rank), step, expert, pass_id
+    def __init__(self, seed, step, expert, pass_id, n_offset=0):
+        # n_offset: first sample's index in the expert's global batch (a data-parallel rank draws
+        # its rows of the single-device masks, expertsim/utils/philox.py)
+        self.seed, self.step, self.expert, self.pass_id, self.n_offset = seed, step, expert, pass_id, n_offset
         self.layer = 0
 
     def __call__(self, x, p):
         stream = philox.dropout_stream(self.step, self.expert, self.pass_id, self.layer)
         self.layer += 1
-        mask = torch.from_numpy(philox.dropout_mask(tuple(x.shape), p, self.seed, stream))
+        mask = torch.from_numpy(philox.dropout_mask(tuple(x.shape), p, self.seed, stream, self.n_offset))
         noise = mask.to(x.dtype)
         noise.div_(1 - p)
         return x * noise
@@ -428,8 +429,12 @@ class OracleMoE:
         for k in list(sd):
             sd[k] = sd[k].detach()
 
-    def train_step(self, epoch, cond, real, pos, std, intensity, noise_fn, gumbel_exp, trace=None):
-        """``noise_fn(expert, which, shape)`` supplies noise_1 (which=0) / noise_2 (which=1)."""
+    def train_step(self, epoch, cond, real, pos, std, intensity, noise_fn, gumbel_exp, trace=None, dp=None):
+        """``noise_fn(expert, which, shape)`` supplies noise_1 (which=0) / noise_2 (which=1).
+
+        ``dp`` (data-parallel restatement, tests/test_ddp_cpu.py; not part of the reference): an
+        object with ``offset(expert)`` (the rank's first sample in the expert's global batch, for the
+        dropout masks) and ``reduce(grads)`` (all-reduce-average of a gradient dict before Adam)."""
         c = self.cfg
         E, B, step = self.E, cond.shape[0], self.step_count
         trace = trace if trace is not None else {}
@@ -447,7 +452,7 @@ class OracleMoE:
         gen_losses, disc_losses = [], []
         div_l, aux_l, int_l = np.zeros(E), np.zeros(E), np.zeros(E)
         mean_int, std_int = [], []
-        mean_in_batch = torch.zeros((B, 1))
+        mean_in_batch = torch.zeros((B, 1), dtype=real.dtype)
         for i in range(E):
             mask = (idx == i).nonzero(as_tuple=True)[0]
             be = mask.numel()
@@ -460,7 +465,9 @@ class OracleMoE:
             w = float(counts_adj[i])
             n1 = noise_fn(i, 0, (be, c["noise_dim"]))
             gl = self._grad_leaves(G)
-            fake = generator_forward(self.arch, G, n1, sc, Dropper(self.seed, step, i, philox.PASS_G1))
+            n0 = dp.offset(i) if dp is not None else 0
+            red = dp.reduce if dp is not None else (lambda g: g)
+            fake = generator_forward(self.arch, G, n1, sc, Dropper(self.seed, step, i, philox.PASS_G1, n0))
             trace[f"G{i}/0"] = fake.detach().clone()
             # ---- discriminator step (moe.py:506-527)
             dl = self._grad_leaves(D)
@@ -470,14 +477,14 @@ class OracleMoE:
             trace[f"D{i}/1"] = (fo.detach().clone(), fl.detach().clone())
             d_loss = (F.relu(1.0 - ro).mean() + F.relu(1.0 + fo).mean()) * w
             grads = torch.autograd.grad(d_loss, list(dl.values()), allow_unused=True)
-            gd = dict(zip(dl.keys(), grads))
+            gd = red(dict(zip(dl.keys(), grads)))
             trace[f"optD{i}/grad"] = {k: v.detach().clone() for k, v in gd.items()}
             self._release(D)
             with torch.no_grad():
                 self.opt_d[i].step(D, gd)
             # ---- generator step (moe.py:529-571); D weights frozen (their grads are discarded)
             n2 = noise_fn(i, 1, (be, c["noise_dim"]))
-            fake2 = generator_forward(self.arch, G, n2, sc, Dropper(self.seed, step, i, philox.PASS_G2))
+            fake2 = generator_forward(self.arch, G, n2, sc, Dropper(self.seed, step, i, philox.PASS_G2, n0))
             trace[f"G{i}/1"] = fake2.detach().clone()
             fo1, fl1 = discriminator_forward(self.arch, D, fake, sc)
             fo2, fl2 = discriminator_forward(self.arch, D, fake2, sc)
@@ -488,15 +495,15 @@ class OracleMoE:
             il, sums, s_std, s_mean = intensity_regularization(fake, si, c["in_strength"])
             g_loss = g_loss + div + il
             al_leaves = self._grad_leaves(A)
-            coords = aux_forward(self.arch, A, fake, Dropper(self.seed, step, i, philox.PASS_AUX))
+            coords = aux_forward(self.arch, A, fake, Dropper(self.seed, step, i, philox.PASS_AUX, n0))
             trace[f"A{i}/0"] = coords.detach().clone()
             aux = regressor_loss(sp, coords) * c["aux_strength"]
             g_loss = (g_loss + aux) * w
             keys = list(gl.keys()) + list(al_leaves.keys())
             grads = torch.autograd.grad(g_loss, list(gl.values()) + list(al_leaves.values()),
                                         allow_unused=True)
-            gg = dict(zip(keys[:len(gl)], grads[:len(gl)]))
-            ga = dict(zip(keys[len(gl):], grads[len(gl):]))
+            gg = red(dict(zip(keys[:len(gl)], grads[:len(gl)])))
+            ga = red(dict(zip(keys[len(gl):], grads[len(gl):])))
             trace[f"optG{i}/grad"] = {k: v.detach().clone() for k, v in gg.items() if v is not None}
             trace[f"optA{i}/grad"] = {k: v.detach().clone() for k, v in ga.items() if v is not None}
             self._release(G); self._release(A)

@@ -1,0 +1,117 @@
+"""Data parallelism on the HIP path (expertsim/train/ddp.py) against the single-device step.
+
+Two ranks share the one GPU of the test box (gloo process group: the collectives go through the
+host; RCCL needs distinct devices).  Each rank trains on its half of a global batch of 96 with
+``sync_bn=True`` — randomness at global sample indices, SyncBN, global SDI / router statistics,
+averaged gradients, merged metrics — and the result is compared with ONE process running the
+same seeds on the whole batch (fp32 parity mode, device RNG, no injection):
+
+  * step 0: every metric <= 1e-4 relative (as the golden tests); parameters after the step
+    |dp - p| <= 2 lr (Adam's first step turns rounding-level sign flips of tiny gradients into
+    +-lr moves);
+  * step 1: metrics <= 2e-2 relative (the reference's own step-1 sensitivity, see
+    test_train_step_gpu.py); parameters <= 4 lr;
+  * E = 1 and E = 3 (the router: global gate sums, summed router gradient, per-expert global
+    sample offsets);
+  * the per-rank-statistics mode (``sync_bn=False``, the default) runs and is reported.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+B_GLOBAL, STEPS, WORLD = 96, 2, 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(E, B, rank=0, ddp=None):
+    import bench
+    from expertsim.utils.synthetic import make_batch
+    dev = torch.device("cuda", 0)
+    moe, (og, od, oa, orr), cfg = bench.build("neutron", E, "fp32", 1234, dev)
+    if ddp is not None:
+        moe.ddp = ddp
+        moe.rank = ddp.rank
+    out = []
+    for s in range(STEPS):
+        b = make_batch(B_GLOBAL, "neutron", seed=70 + s)
+        rows = slice(rank * B, (rank + 1) * B)
+        t = {k: torch.from_numpy(v[rows].copy()).to(dev) for k, v in b.items()}
+        m = moe.train_step(0, t["cond"], t["real_images"].unsqueeze(1), t["true_positions"], t["std"],
+                           t["intensity"], oa, og, od, orr, None, dev)
+        torch.cuda.synchronize()
+        params = {n: p.detach().double().cpu().numpy().copy() for n, p in moe.named_parameters()}
+        out.append(({k: float(v) for k, v in m.items()}, params))
+    lr = {"generators": cfg.model.generator.lr_g, "discriminators": cfg.model.discriminator.lr_d,
+          "aux_regs": cfg.model.aux_reg.lr_a, "router": cfg.model.router.lr_r}
+    return out, lr
+
+
+def _worker(rank, world, port, q, E, sync):
+    import sys
+    from conftest import PKG_DIR, REPO
+    for p in (PKG_DIR, REPO):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from expertsim.train.ddp import DataParallel
+    try:
+        res, _ = _run(E, B_GLOBAL // world, rank, DataParallel(sync_bn=sync))
+        q.put((rank, res, None))
+    except Exception as e:         # report instead of hanging the parent
+        q.put((rank, None, repr(e)))
+    dist.destroy_process_group()
+
+
+def _spawn(E, sync):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q, E, sync)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=240) for _ in range(WORLD)), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    for rank, r, err in res:
+        assert err is None, (rank, err)
+    return [r for _, r, _ in res]
+
+
+def _deviation(single, dp, lr):
+    out = []
+    for s, ((ms, ps), (md, pd)) in enumerate(zip(single, dp)):
+        mdev = max(abs(md[k] - v) / max(abs(v), 1e-3) for k, v in ms.items())
+        pdev = max(float(np.max(np.abs(pd[n] - a))) / lr[n.split(".")[0]] for n, a in ps.items())
+        out.append((mdev, pdev))
+    return out
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("E", [1, 3])
+def test_ddp_sync_bn_matches_single_device(E):
+    single, lr = _run(E, B_GLOBAL)
+    dp = _spawn(E, True)
+    for (m0, p0), (m1, p1) in zip(dp[0], dp[1]):            # ranks agree on metrics and parameters
+        assert m0 == m1
+        assert all(np.array_equal(p0[n], p1[n]) for n in p0)
+    dev = _deviation(single, dp[0], lr)
+    local = _deviation(single, _spawn(E, False)[0], lr)
+    print(f"E={E}: DP(sync-BN) vs single (metric rel, param / lr): {dev}; DP(per-rank BN): {local}")
+    assert dev[0][0] <= 1e-4 and dev[0][1] <= 2.0 + 1e-3
+    assert dev[1][0] <= 2e-2 and dev[1][1] <= 4.0 + 1e-3
