@@ -332,6 +332,46 @@ __global__ void dp_metrics_merge_kernel(const float* rows, int world, int E, flo
   o[5] = N > 1.0 ? (float)sqrt(M2 / (N - 1.0)) : 0.f;
 }
 
+// Expert dispatch as a stable counting sort (moe.py:121-123: per expert, the rows with idx == e in
+// batch order): perm = [rows of expert 0 | rows of expert 1 | ...], offs[e] = first position of
+// expert e, offs[E] = B.  One block; per expert a block-wide exclusive scan over 1024-row tiles.
+__global__ void __launch_bounds__(1024) router_dispatch_kernel(const int32_t* idx, int B, int E, int32_t* perm,
+                                                               int32_t* offs) {
+  __shared__ int wsum[16];
+  __shared__ int base;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
+  for (int e = 0; e < E; ++e) {
+    if (threadIdx.x == 0) offs[e] = base;
+    for (int t0 = 0; t0 < B; t0 += 1024) {
+      const int b = t0 + threadIdx.x;
+      const int f = (b < B && idx[b] == e) ? 1 : 0;
+      // inclusive scan within the wave
+      int v = f;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(v, o, 64);
+        if (lane >= o) v += u;
+      }
+      if (lane == 63) wsum[wid] = v;
+      __syncthreads();
+      int before = 0;
+      for (int w = 0; w < wid; ++w) before += wsum[w];
+      const int pos = base + before + v - f;
+      if (f) perm[pos] = b;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < 16; ++w) tot += wsum[w];
+        base += tot;
+      }
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x == 0) offs[E] = base;
+}
+
 // mean_intensities_in_batch_expert[mask] = s (moe.py:196-198): dst[rows[i]] = src[i]
 __global__ void scatter_rows_kernel(const float* src, const int32_t* rows, int n, float* dst) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -433,6 +473,14 @@ extern "C" int es_dp_metrics_merge(const float* rows, int world, int E, float* o
 extern "C" int es_scatter_rows(const float* src, const int32_t* rows, int n, float* dst, es_stream_t stream) {
   if (n <= 0) return ES_OK;
   hipLaunchKernelGGL(scatter_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, src, rows, n, dst);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_router_dispatch(const int32_t* idx, int B, int E, int32_t* perm, int32_t* offs,
+                                  es_stream_t stream) {
+  ES_CHECK_ARG(B > 0 && E >= 1, "router_dispatch: B=%d E=%d", B, E);
+  hipLaunchKernelGGL(router_dispatch_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, idx, B, E, perm, offs);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }

@@ -50,15 +50,20 @@ class ExpertModule(nn.Module):
         super().__init__()
         self._flat = None
         self._ops = None
+        self._flat_ok = False      # flat storage verified since the last device move / reload
+        self._offs = None
 
     # ----------------------------------------------------------------- flat parameter storage
     def flatten(self):
+        if self._flat_ok and self._flat is not None:
+            return
         params = [p for p in self.parameters()]
         dev = params[0].device
         total = sum(p.numel() for p in params)
         if self._flat is not None and self._flat[0].device == dev and self._flat[0].numel() == total \
                 and all(p.data.data_ptr() == self._flat[0][o:o + p.numel()].data_ptr()
                         for p, o in zip(params, self._offsets())):
+            self._flat_ok = True
             return
         flat_p = torch.empty(total, dtype=torch.float32, device=dev)
         flat_g = torch.zeros(total, dtype=torch.float32, device=dev)
@@ -71,13 +76,16 @@ class ExpertModule(nn.Module):
             o += n
         self._flat = (flat_p, flat_g)
         self._ops = None
+        self._flat_ok = True
 
     def _offsets(self):
-        o, out = 0, []
-        for p in self.parameters():
-            out.append(o)
-            o += p.numel()
-        return out
+        if self._offs is None:
+            o, out = 0, []
+            for p in self.parameters():
+                out.append(o)
+                o += p.numel()
+            self._offs = out
+        return self._offs
 
     @property
     def flat_params(self):
@@ -92,8 +100,13 @@ class ExpertModule(nn.Module):
     def zero_grads(self):
         self.flatten()
         self._flat[1].zero_()
+        g = self._flat[1]
+        base = g.data_ptr()
         for p, o in zip(self.parameters(), self._offsets()):
-            p.grad = self._flat[1][o:o + p.numel()].view_as(p)
+            pg = p.grad
+            # re-point only a gradient someone replaced (set_to_none elsewhere, autograd accumulate)
+            if pg is None or pg.data_ptr() != base + 4 * o or pg.shape != p.shape:
+                p.grad = g[o:o + p.numel()].view_as(p)
 
     def ops(self):
         """Layer ops bound to the flat parameter storage (rebuilt after device moves)."""
@@ -117,7 +130,12 @@ class ExpertModule(nn.Module):
         out = super()._apply(fn, *args, **kwargs)
         self._flat = None
         self._ops = None
+        self._flat_ok = False
         return out
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        super()._load_from_state_dict(*args, **kwargs)
+        self._flat_ok = False       # re-verify: loading copies in place, but a module may be rebuilt
 
     def __deepcopy__(self, memo):
         # deep copies (moe.py:29-31) must not share flat storage
@@ -126,8 +144,10 @@ class ExpertModule(nn.Module):
         memo[id(self)] = new
         import copy as _copy
         for k, v in self.__dict__.items():
-            if k in ("_flat", "_ops"):
+            if k in ("_flat", "_ops", "_offs"):
                 setattr(new, k, None)
+            elif k == "_flat_ok":
+                setattr(new, k, False)
             else:
                 setattr(new, k, _copy.deepcopy(v, memo))
         for p in new.parameters():

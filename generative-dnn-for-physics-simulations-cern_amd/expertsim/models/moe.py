@@ -153,15 +153,21 @@ class MoEWrapper(nn.Module):
             discriminator_optimizers[i].zero_grad(set_to_none=True)
         router_optimizer.zero_grad(set_to_none=True)
 
-        # expert dispatch (moe.py:97-99,123): E == 1 needs no routing sync
+        # expert dispatch (moe.py:97-99,121-123): E == 1 needs no routing at all; otherwise the
+        # rows are grouped per expert on the device (es_router_dispatch) and only the E counts
+        # cross to the host (the reference's B_e <= 1 skip rule and the per-expert launch sizes)
         if E == 1:
             groups = [(0, None, B)]
         else:
-            idx_h = idx.cpu().numpy()
-            groups = []
+            perm = torch.empty(B, dtype=torch.int32, device=dev)
+            offs = torch.empty(E + 1, dtype=torch.int32, device=dev)
+            hip.call("es_router_dispatch", hip.ptr(idx), B, E, hip.ptr(perm), hip.ptr(offs), hip.stream_ptr())
+            counts_h = counts.cpu().numpy()
+            groups, o = [], 0
             for e in range(E):
-                rows = np.nonzero(idx_h == e)[0].astype(np.int32)
-                groups.append((e, rows, rows.size))
+                be = int(counts_h[e])
+                groups.append((e, perm[o:o + be], be))
+                o += be
         if ddp is not None:
             groups = ddp.global_groups(groups, B)
             if ddp.sync_bn and any(ddp.global_count(e) > 1 and ddp._local[e] == 0 for e in range(E)):
@@ -269,7 +275,7 @@ class MoEWrapper(nn.Module):
         if rows is None:
             sc, sr, sp, ss, si = cond, real, pos, std, intensity
         else:
-            ridx = torch.from_numpy(rows).to(dev)
+            ridx = rows                      # device int32 row indices (es_router_dispatch)
             gather = lambda t, cols: _gather_rows(t, ridx, cols)
             sc, sp, ss, si = gather(cond, cond.shape[1]), gather(pos, 2), gather(std, 1), gather(intensity, 1)
             sr = gather(real.reshape(B, -1), H * W).view(be, 1, H, W)

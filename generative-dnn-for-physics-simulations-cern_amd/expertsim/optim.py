@@ -21,6 +21,7 @@ class FusedAdam(torch.optim.Optimizer):
         super().__init__(list(module.parameters()), dict(lr=lr, betas=betas, eps=eps, weight_decay=0.0))
         self._m = self._v = None
         self._step = 0
+        self._step_t = torch.tensor(0.0)   # one host tensor shared by every parameter's state['step']
         self._dstep = None   # device copy of the step (read by the kernel: graph-capturable)
 
     def _buffers(self):
@@ -31,7 +32,7 @@ class FusedAdam(torch.optim.Optimizer):
             o = 0
             for p in self.module.parameters():
                 n = p.numel()
-                self.state[p] = {"step": torch.tensor(float(self._step)),
+                self.state[p] = {"step": self._step_t,
                                  "exp_avg": self._m[o:o + n].view_as(p),
                                  "exp_avg_sq": self._v[o:o + n].view_as(p)}
                 o += n
@@ -56,8 +57,7 @@ class FusedAdam(torch.optim.Optimizer):
         hip.call("es_adam_dev", hip.ptr(flat), hip.ptr(self.module.flat_grads), hip.ptr(self._m), hip.ptr(self._v),
                  flat.numel(), float(g["lr"]), float(b1), float(b2), float(g["eps"]), hip.ptr(self._dstep),
                  float(grad_scale), hip.stream_ptr())
-        for p in self.module.parameters():
-            self.state[p]["step"] = torch.tensor(float(self._step))
+        self._step_t.fill_(float(self._step))
         self.module.invalidate()
         return None
 
@@ -83,14 +83,11 @@ class FusedAdam(torch.optim.Optimizer):
         self._step = int(sd["step"])
         if self._dstep is not None:          # keep the pointer a captured graph reads
             self._dstep.fill_(self._step)
-        for p in self.module.parameters():
-            self.state[p]["step"] = torch.tensor(float(self._step))
+        self._step_t.fill_(float(self._step))
 
     def sync_step(self):
         """Host step := device step (after replays of a captured train step)."""
         if self._dstep is not None:
             self._step = int(self._dstep.item())
-            for p in self.module.parameters():
-                if p in self.state:
-                    self.state[p]["step"] = torch.tensor(float(self._step))
+            self._step_t.fill_(float(self._step))
         return self._step

@@ -352,6 +352,10 @@ int es_router_loss(const float* gates, const int32_t* idx, const float* feat, in
                    float alb_coef, float util_strength, float ed_strength, const float* colsum, int B_total,
                    const float* feat_all, const int32_t* idx_all, int B_all, float* out, float* dlogits,
                    es_stream_t stream);
+/* Device-side expert dispatch (moe.py:121-123 `(idx == i).nonzero()` per expert, without the host
+ * round trip): perm[B] = the batch rows grouped by expert, each group in batch order;
+ * offs[E+1] = start of each group (offs[E] = B). */
+int es_router_dispatch(const int32_t* idx, int B, int E, int32_t* perm, int32_t* offs, es_stream_t stream);
 /* out[e] = sum_b gates[b, e] (the rank's share of the router's gate sums). */
 int es_router_colsum(const float* gates, int B, int E, float* out, es_stream_t stream);
 /* Data-parallel merge of the per-expert metric rows: rows [world][E][10] (the 9 metric columns of

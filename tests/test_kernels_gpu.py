@@ -607,3 +607,20 @@ def test_gn_backward_proton_shapes(shape):
     dxa = op.bwd(xa, stats, ch, to_act(gy, torch.float32), dgamma=dg, dbeta=dbt, dsum=dsum)
     assert rel(from_act(dxa), xr.grad) < 1e-4
     assert rel(dg.cpu(), g_.grad) < 1e-4 and rel(dbt.cpu(), b_.grad) < 1e-4
+
+
+@pytest.mark.parametrize("B,E", [(12, 3), (1000, 5), (4096, 8), (3000, 1)])
+def test_router_dispatch_is_stable_grouping(B, E):
+    """es_router_dispatch == per expert (idx == e).nonzero() in batch order (moe.py:121-123)."""
+    hip = _hip()
+    g = torch.Generator().manual_seed(B + E)
+    idx = torch.randint(0, E, (B,), generator=g, dtype=torch.int32)
+    if E > 2:
+        idx[idx == 1] = 0                            # an empty expert
+    perm = torch.empty(B, dtype=torch.int32, device=DEV)
+    offs = torch.empty(E + 1, dtype=torch.int32, device=DEV)
+    hip.call("es_router_dispatch", hip.ptr(idx.to(DEV)), B, E, hip.ptr(perm), hip.ptr(offs), hip.stream_ptr())
+    want = np.concatenate([np.nonzero(idx.numpy() == e)[0] for e in range(E)])
+    counts = np.bincount(idx.numpy(), minlength=E)
+    assert np.array_equal(perm.cpu().numpy(), want)
+    assert np.array_equal(offs.cpu().numpy(), np.concatenate([[0], np.cumsum(counts)]))
