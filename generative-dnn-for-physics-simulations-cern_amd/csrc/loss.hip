@@ -372,6 +372,42 @@ __global__ void __launch_bounds__(1024) router_dispatch_kernel(const int32_t* id
   if (threadIdx.x == 0) offs[E] = base;
 }
 
+// The step's metric dict (moe.py:480-502) from the per-expert rows and the router terms, in one
+// launch.  out = [gen, disc, div, intensity, aux, router, ED, differentiation, entropy, ALB, gan,
+// then per expert: gen_i, disc_i, div_i, int_i, aux_i, std_int_i, mean_int_i, n_i].
+__global__ void step_metrics_kernel(const float* mbuf, int E, const float* rl, const int32_t* counts,
+                                    const float* countsf, float gan_strength, float diff_strength, float dec_w,
+                                    int flags, float* out) {
+  if (threadIdx.x != 0) return;
+  const bool router = flags & 1, trained = flags & 2, alb_on = flags & 4, util_on = flags & 8, ed_on = flags & 16;
+  float s[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  const int col[5] = {0, 8, 2, 3, 4};
+  for (int e = 0; e < E; ++e)
+    for (int k = 0; k < 5; ++k) s[k] += mbuf[e * 9 + col[k]];
+  for (int k = 0; k < 5; ++k) out[k] = s[k] / (float)E;
+  float gan = 0.f, diff = 0.f, ent = 0.f, alb = 0.f, ed = 0.f, rloss = 0.f;
+  if (router) {
+    gan = out[0] * gan_strength;                                  // moe.py:255
+    if (diff_strength != 0.f) {                                   // moe.py:395-405
+      float dli = 0.f;
+      for (int a = 0; a < E; ++a)
+        for (int b = a + 1; b < E; ++b) dli += fabsf(mbuf[a * 9 + 6] - mbuf[b * 9 + 6]);
+      diff = -(dli * diff_strength) * diff_strength;
+    }
+    alb = alb_on ? rl[0] / dec_w : 0.f;
+    ent = util_on ? rl[1] : 0.f;
+    ed = ed_on ? rl[2] : 0.f;
+    rloss = trained ? ed + gan + diff + ent + dec_w * alb : 0.f;   // moe.py:424-442
+  }
+  out[5] = rloss; out[6] = ed; out[7] = diff; out[8] = ent; out[9] = alb; out[10] = gan;
+  for (int e = 0; e < E; ++e) {
+    float* o = out + 11 + 8 * e;
+    const float* m = mbuf + e * 9;
+    o[0] = m[0]; o[1] = m[8]; o[2] = m[2]; o[3] = m[3]; o[4] = m[4]; o[5] = m[5]; o[6] = m[6];
+    o[7] = countsf ? countsf[e] : (float)counts[e];
+  }
+}
+
 // mean_intensities_in_batch_expert[mask] = s (moe.py:196-198): dst[rows[i]] = src[i]
 __global__ void scatter_rows_kernel(const float* src, const int32_t* rows, int n, float* dst) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -481,6 +517,17 @@ extern "C" int es_router_dispatch(const int32_t* idx, int B, int E, int32_t* per
                                   es_stream_t stream) {
   ES_CHECK_ARG(B > 0 && E >= 1, "router_dispatch: B=%d E=%d", B, E);
   hipLaunchKernelGGL(router_dispatch_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, idx, B, E, perm, offs);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_step_metrics(const float* mbuf, int E, const float* rl, const int32_t* counts, const float* countsf,
+                               float gan_strength, float diff_strength, float dec_w, int flags, float* out,
+                               es_stream_t stream) {
+  ES_CHECK_ARG(E >= 1 && (counts || countsf), "step_metrics: E=%d, counts", E);
+  ES_CHECK_ARG(!(flags & 1) || rl, "step_metrics: router terms need rl");
+  hipLaunchKernelGGL(step_metrics_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, mbuf, E, rl, counts, countsf,
+                     gan_strength, diff_strength, dec_w, flags, out);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }

@@ -115,6 +115,7 @@ _SIGS = {
     "es_router_colsum": (C.c_int, [P, C.c_int, C.c_int, P, P]),
     "es_router_dispatch": (C.c_int, [P, C.c_int, C.c_int, P, P, P]),
     "es_dp_metrics_merge": (C.c_int, [P, C.c_int, C.c_int, P, P]),
+    "es_step_metrics": (C.c_int, [P, C.c_int, P, P, P, C.c_float, C.c_float, C.c_float, C.c_int, P, P]),
     "es_scatter_rows": (C.c_int, [P, P, C.c_int, P, P]),
     "es_adam": (C.c_int, [P, P, P, P, I64, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int,
                           C.c_float, P]),

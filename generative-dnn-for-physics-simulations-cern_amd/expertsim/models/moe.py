@@ -27,7 +27,6 @@ import os
 
 import copy
 import ctypes as C
-from itertools import combinations
 
 import numpy as np
 import torch
@@ -70,6 +69,7 @@ class MoEWrapper(nn.Module):
         self.ddp = None            # expertsim.train.ddp.DataParallel (set by the loop)
         self.step_count = 0
         self._ed_feat = None       # [B] per-sample photon sums for the router's ED term
+        self._w_cache = {}         # class_counts_adjusted device scalars
         self._dstep = None         # device int32 step counter: dropout / noise streams (graph replay)
         self.set_precision(cfg_get(cfg, "train.precision", "fp32"))
 
@@ -202,14 +202,9 @@ class MoEWrapper(nn.Module):
             ddp.merge_metrics(mbuf)          # the global batch's per-expert metrics on every rank
 
         # ---- router (moe.py:213-449)
-        zero = torch.zeros((), dtype=torch.float32, device=dev)
+        rl = None
+        flags, dec_w = 0, 1.0
         if E > 1:
-            gan = mbuf[:, 0].mean() * rc.gan_strength
-            if rc.diff_strength != 0:
-                dli = sum((mbuf[a, 6] - mbuf[b, 6]).abs() for a, b in combinations(range(E), 2)) * rc.diff_strength
-            else:
-                dli = zero
-            diff = -dli * rc.diff_strength
             alpha = min(max(epoch / rc.alpha, 0.0), 1.0)
             dec_w = rc.min_weight + (1.0 - rc.min_weight) * alpha
             # ALB, utilisation entropy and expert-distribution terms + d/dlogits in one program
@@ -233,39 +228,31 @@ class MoEWrapper(nn.Module):
                      hip.ptr(rl), hip.ptr(dlogits), hip.stream_ptr())
             if ddp is not None and ed_on:
                 ddp.all_reduce_(rl[2:3])       # the ED sum over every rank's rows
-            alb = rl[0] / dec_w if rc.alb_strength != 0 else zero
-            ent = rl[1] if rc.util_strength != 0 else zero
-            ed = rl[2] if ed_on else zero
-            router_loss = ed + gan + diff + ent + dec_w * alb
-            if epoch < rc.stop_router_training_epoch:
+            trained = epoch < rc.stop_router_training_epoch
+            if trained:
                 self.router.bwd(rctx, dlogits)
                 # summed, not averaged: the router terms are functions of global sums
                 self._allreduce(self.router, average=False)
                 router_optimizer.step()
-            else:
-                router_loss = zero
-        else:
-            gan = router_loss = ed = diff = ent = alb = zero
+            flags = (1 | (2 if trained else 0) | (4 if rc.alb_strength != 0 else 0)
+                     | (8 if rc.util_strength != 0 else 0) | (16 if ed_on else 0))
 
         self.step_count += 1
         hip.call("es_counter_add", hip.ptr(self._dstep), 1, hip.stream_ptr())
-        countsf = counts.to(torch.float32) if self.ddp is None else self.ddp.global_counts_tensor(dev)
-        metrics = {
-            "gen_loss": mbuf[:, 0].mean(), "disc_loss": mbuf[:, 8].mean(), "div_loss": mbuf[:, 2].mean(),
-            "intensity_loss": mbuf[:, 3].mean(), "aux_reg_loss": mbuf[:, 4].mean(),
-            "router_loss": router_loss, "expert_distribution_loss": ed, "differentiation_loss": diff,
-            "expert_entropy_loss": ent, "adaptive_load_balancing_loss": alb, "gan_loss": gan,
-        }
+        # the metric dict (moe.py:480-502): one kernel over the expert rows and router terms
+        countsf = None if self.ddp is None else self.ddp.global_counts_tensor(dev)
+        mvec = torch.empty(11 + 8 * E, dtype=torch.float32, device=dev)
+        hip.call("es_step_metrics", hip.ptr(mbuf), E, hip.ptr(rl), hip.ptr(counts) if countsf is None else None,
+                 hip.ptr(countsf), float(rc.gan_strength), float(rc.diff_strength), float(dec_w), flags,
+                 hip.ptr(mvec), hip.stream_ptr())
+        names = ["gen_loss", "disc_loss", "div_loss", "intensity_loss", "aux_reg_loss", "router_loss",
+                 "expert_distribution_loss", "differentiation_loss", "expert_entropy_loss",
+                 "adaptive_load_balancing_loss", "gan_loss"]
         for i in range(E):
-            metrics[f"gen_loss_{i}"] = mbuf[i, 0]
-            metrics[f"disc_loss_{i}"] = mbuf[i, 8]
-            metrics[f"div_loss_experts_{i}"] = mbuf[i, 2]
-            metrics[f"intensity_loss_experts_{i}"] = mbuf[i, 3]
-            metrics[f"aux_reg_loss_experts_{i}"] = mbuf[i, 4]
-            metrics[f"std_intensities_experts_{i}"] = mbuf[i, 5]
-            metrics[f"mean_intensities_experts_{i}"] = mbuf[i, 6]
-            metrics[f"n_choosen_experts_mean_epoch_{i}"] = countsf[i]
-        return metrics
+            names += [f"gen_loss_{i}", f"disc_loss_{i}", f"div_loss_experts_{i}", f"intensity_loss_experts_{i}",
+                      f"aux_reg_loss_experts_{i}", f"std_intensities_experts_{i}", f"mean_intensities_experts_{i}",
+                      f"n_choosen_experts_mean_epoch_{i}"]
+        return {k: mvec[j] for j, k in enumerate(names)}
 
     # ---------------------------------------------------------------------------- one expert
     def _expert_step(self, e, rows, be, B, cond, real, pos, std, intensity, opt_g, opt_d, opt_a, mbuf, step, dev):
@@ -282,7 +269,9 @@ class MoEWrapper(nn.Module):
         # class_counts_adjusted[i] as float32 (moe.py:99-100,522,562)
         # (DDP: local weight B_e^r / B_r; the all-reduce averages, see expertsim/train/ddp.py)
         w = float(np.float32(be) / np.float32(B))
-        w_dev = torch.full((1,), w, dtype=torch.float32, device=dev)
+        w_dev = self._w_cache.get((w, dev))
+        if w_dev is None:      # one device scalar per distinct weight (no fill launch per step)
+            w_dev = self._w_cache[(w, dev)] = torch.full((1,), w, dtype=torch.float32, device=dev)
         # the step term (step * 1024) is added on the device from self._dstep
         sb = lambda pid: philox.dropout_stream(0, e, pid, 0)
         seed = self.rng_seed

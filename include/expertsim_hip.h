@@ -358,6 +358,15 @@ int es_router_loss(const float* gates, const int32_t* idx, const float* feat, in
 int es_router_dispatch(const int32_t* idx, int B, int E, int32_t* perm, int32_t* offs, es_stream_t stream);
 /* out[e] = sum_b gates[b, e] (the rank's share of the router's gate sums). */
 int es_router_colsum(const float* gates, int B, int E, float* out, es_stream_t stream);
+/* The train step's metric dict (moe.py:480-502) in one launch: out[11 + 8E] = gen, disc, div,
+ * intensity, aux (means over the experts of mbuf [E][9] = per expert total, gen, div, int, aux,
+ * std_int, mean_int, w, disc), router, ED, differentiation, entropy, ALB, gan (moe.py:255-434 from
+ * rl = [ALB*dec_w, entropy, ED]), then per expert gen_i, disc_i, div_i, int_i, aux_i, std_int_i,
+ * mean_int_i, n_i (counts int32 or countsf float).  flags: 1 router (E > 1), 2 router trained this
+ * epoch, 4 ALB on, 8 entropy on, 16 ED on. */
+int es_step_metrics(const float* mbuf, int E, const float* rl, const int32_t* counts, const float* countsf,
+                    float gan_strength, float diff_strength, float dec_w, int flags, float* out,
+                    es_stream_t stream);
 /* Data-parallel merge of the per-expert metric rows: rows [world][E][10] (the 9 metric columns of
  * MoEWrapper's buffer + the rank's sample count, 0 = not run) -> out [E][9], global-batch values. */
 int es_dp_metrics_merge(const float* rows, int world, int E, float* out, es_stream_t stream);
