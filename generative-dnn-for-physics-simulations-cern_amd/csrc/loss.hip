@@ -409,8 +409,9 @@ __global__ void step_metrics_kernel(const float* mbuf, int E, const float* rl, c
 }
 
 // mean_intensities_in_batch_expert[mask] = s (moe.py:196-198): dst[rows[i]] = src[i]
-__global__ void scatter_rows_kernel(const float* src, const int32_t* rows, int n, float* dst) {
+__global__ void scatter_rows_kernel(const float* src, const int32_t* rows, const int32_t* start, int n, float* dst) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (start) rows += start[0];
   if (i < n) dst[rows ? rows[i] : i] = src[i];
 }
 }  // namespace
@@ -508,7 +509,8 @@ extern "C" int es_dp_metrics_merge(const float* rows, int world, int E, float* o
 
 extern "C" int es_scatter_rows(const float* src, const int32_t* rows, int n, float* dst, es_stream_t stream) {
   if (n <= 0) return ES_OK;
-  hipLaunchKernelGGL(scatter_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, src, rows, n, dst);
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, src, rows,
+                     (const int32_t*)nullptr, n, dst);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
@@ -528,6 +530,16 @@ extern "C" int es_step_metrics(const float* mbuf, int E, const float* rl, const 
   ES_CHECK_ARG(!(flags & 1) || rl, "step_metrics: router terms need rl");
   hipLaunchKernelGGL(step_metrics_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, mbuf, E, rl, counts, countsf,
                      gan_strength, diff_strength, dec_w, flags, out);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_scatter_rows_at(const float* src, const int32_t* perm, const int32_t* start, int n, float* dst,
+                                  es_stream_t stream) {
+  if (n <= 0) return ES_OK;
+  ES_CHECK_ARG(perm && start, "scatter_rows_at: perm / start");
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, src, perm, start,
+                     n, dst);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }

@@ -263,9 +263,10 @@ __global__ void avgpool_bwd_kernel(View dy, const float* dyp, View dx, void* dxp
   }
 }
 
-__global__ void gather_rows_kernel(const float* src, int64_t sld, const int32_t* idx, int rows, int cols,
-                                   float* dst, int64_t dld) {
+__global__ void gather_rows_kernel(const float* src, int64_t sld, const int32_t* idx, const int32_t* start,
+                                   int rows, int cols, float* dst, int64_t dld) {
   const int64_t total = (int64_t)rows * cols;
+  if (start) idx += start[0];   // the expert's first position in the dispatch permutation (device)
   GRID_STRIDE(e, total) {
     const int r = e / cols, c = e % cols;
     const int sr = idx ? idx[r] : r;
@@ -640,7 +641,18 @@ extern "C" int es_gather_rows(const float* src, int64_t src_ld, const int32_t* i
   const int64_t total = (int64_t)rows * cols;
   if (total == 0) return ES_OK;
   hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, src, src_ld,
-                     idx, rows, cols, dst, dst_ld);
+                     idx, (const int32_t*)nullptr, rows, cols, dst, dst_ld);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_gather_rows_at(const float* src, int64_t src_ld, const int32_t* perm, const int32_t* start,
+                                 int rows, int cols, float* dst, int64_t dst_ld, es_stream_t stream) {
+  const int64_t total = (int64_t)rows * cols;
+  if (total == 0) return ES_OK;
+  ES_CHECK_ARG(perm && start, "gather_rows_at: perm / start");
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, src, src_ld,
+                     perm, start, rows, cols, dst, dst_ld);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }

@@ -99,6 +99,8 @@ _SIGS = {
     "es_avgpool_fwd": (C.c_int, [P, C.c_int, P, P, P, P]),
     "es_avgpool_bwd": (C.c_int, [P, P, P, C.c_int, P, C.c_float, P]),
     "es_gather_rows": (C.c_int, [P, I64, P, C.c_int, C.c_int, P, I64, P]),
+    "es_gather_rows_at": (C.c_int, [P, I64, P, P, C.c_int, C.c_int, P, I64, P]),
+    "es_scatter_rows_at": (C.c_int, [P, P, P, C.c_int, P, P]),
     "es_sn_power_iter": (C.c_int, [P, C.c_int, C.c_int, P, P, P, C.c_int, P]),
     "es_sn_power_iter_batch": (C.c_int, [C.c_int, P, P, P, P, P, P, C.c_int, P]),
     "es_sn_bwd_batch": (C.c_int, [C.c_int, P, P, P, P, P, P, P, P, C.c_float, P]),

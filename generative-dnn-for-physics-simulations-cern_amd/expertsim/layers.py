@@ -393,6 +393,25 @@ class defer_num_batches:
         return False
 
 
+def nbt_snapshot():
+    """The pending BatchNorm batch counts of the running step (for graph captures to record)."""
+    return {} if _NBT_PENDING is None else {k: (t, n) for k, (t, n) in _NBT_PENDING.items()}
+
+
+def nbt_added(before):
+    """[(counter tensor, increments)] added since ``before`` (nbt_snapshot)."""
+    if _NBT_PENDING is None:
+        return []
+    return [(t, n - before.get(k, (t, 0))[1]) for k, (t, n) in _NBT_PENDING.items()
+            if n != before.get(k, (t, 0))[1]]
+
+
+def count_batches(nbt, k):
+    """k increments of one counter (a replayed graph's BatchNorm batches)."""
+    for _ in range(k):
+        _count_batch(nbt)
+
+
 def _count_batch(nbt):
     if _NBT_PENDING is None:
         nbt.add_(1)

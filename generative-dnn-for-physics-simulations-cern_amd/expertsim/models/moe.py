@@ -70,6 +70,12 @@ class MoEWrapper(nn.Module):
         self.step_count = 0
         self._ed_feat = None       # [B] per-sample photon sums for the router's ED term
         self._w_cache = {}         # class_counts_adjusted device scalars
+        self.expert_graphs = bool(cfg_get(cfg, "train.expert_graphs", True))
+        self._egraphs = None       # ExpertGraphs (n_experts > 1, single process)
+        self._graphs = None
+        self._static = None
+        self._bufs = {}
+        self._eager_steps = 0
         self._dstep = None         # device int32 step counter: dropout / noise streams (graph replay)
         self.set_precision(cfg_get(cfg, "train.precision", "fp32"))
 
@@ -90,16 +96,56 @@ class MoEWrapper(nn.Module):
             m.compute_dtype = d_low
 
     # ---------------------------------------------------------------------------- helpers
+    # stream indices of the step's draws: Gumbel 0, expert e's noise_1 / noise_2 1 + 2e / 2 + 2e
+    # (fixed per call site: a captured per-expert graph draws the same streams in every step)
     def _noise(self, expert, which, shape, device, row0=0):
         """row0: the rows' first index in the expert's global batch (data parallel)."""
         if self.noise_fn is not None:
             return self.noise_fn(expert, which, shape).to(device=device, dtype=torch.float32).contiguous()
-        return self.rng.normal(torch.empty(shape, dtype=torch.float32, device=device), offset=row0 * shape[1])
+        return self.rng.normal_at(torch.empty(shape, dtype=torch.float32, device=device), 1 + 2 * expert + which,
+                                  offset=row0 * shape[1])
 
     def _gumbel(self, shape, device, row0=0):
         if self.gumbel_fn is not None:
             return self.gumbel_fn(shape).to(device=device, dtype=torch.float32).contiguous()
-        return self.rng.exponential(torch.empty(shape, dtype=torch.float32, device=device), offset=row0 * shape[1])
+        return self.rng.exponential_at(torch.empty(shape, dtype=torch.float32, device=device), 0,
+                                       offset=row0 * shape[1])
+
+    def _expert_graphs_on(self, E):
+        """Per-expert graph replay: multi-expert, single process, device randomness, and after one
+        eager step (optimizer moments, packed weights and step counters exist outside any graph)."""
+        return (self.expert_graphs and E > 1 and self.ddp is None and self.noise_fn is None
+                and self.gumbel_fn is None and self._eager_steps >= 1 and not torch.cuda.is_current_stream_capturing())
+
+    def _weight_scalar(self, be, B, dev):
+        """class_counts_adjusted as a device scalar, one per distinct value (created outside any
+        graph capture, no fill launch per step)."""
+        w = float(np.float32(be) / np.float32(B))
+        t = self._w_cache.get((w, dev))
+        if t is None:
+            t = self._w_cache[(w, dev)] = torch.full((1,), w, dtype=torch.float32, device=dev)
+        return t
+
+    def _buf(self, name, shape, dtype, dev):
+        """A persistent device buffer (same storage every step)."""
+        t = self._bufs.get(name)
+        if t is None or tuple(t.shape) != tuple(shape) or t.device != dev or t.dtype != dtype:
+            t = self._bufs[name] = torch.empty(shape, dtype=dtype, device=dev)
+            if self._egraphs is not None:
+                self._egraphs.clear()        # graphs captured against the old buffer
+        return t
+
+    def _static_inputs(self, dev, *ts):
+        shapes = tuple(tuple(t.shape) for t in ts)
+        if self._static is None or self._static[0] != shapes:
+            self._static = (shapes, [torch.empty_like(t) for t in ts])
+            if self._egraphs is not None:
+                self._egraphs.clear()
+        out = self._static[1]
+        for d, t in zip(out, ts):
+            if d.data_ptr() != t.data_ptr():
+                d.copy_(t)
+        return out
 
     def _allreduce(self, module, average=True):
         if self.ddp is not None:
@@ -121,6 +167,14 @@ class MoEWrapper(nn.Module):
             real_images = real_images.unsqueeze(1)
         B = cond.shape[0]
         step = self.step_count
+        self._graphs = None
+        if self._expert_graphs_on(E):
+            # per-expert HIP graphs (ExpertGraphs): the batch lives in static buffers the graphs read
+            cond, real_images, true_positions, std, intensity = self._static_inputs(
+                dev, cond, real_images, true_positions, std, intensity)
+            if self._egraphs is None:
+                self._egraphs = ExpertGraphs()
+            self._graphs = self._egraphs
         rc = self.cfg.model.router
         if self._dstep is None or self._dstep.device != dev:
             self._dstep = torch.full((1,), step, dtype=torch.int32, device=dev)
@@ -159,15 +213,11 @@ class MoEWrapper(nn.Module):
         if E == 1:
             groups = [(0, None, B)]
         else:
-            perm = torch.empty(B, dtype=torch.int32, device=dev)
-            offs = torch.empty(E + 1, dtype=torch.int32, device=dev)
+            perm = self._buf("perm", (B,), torch.int32, dev)
+            offs = self._buf("offs", (E + 1,), torch.int32, dev)
             hip.call("es_router_dispatch", hip.ptr(idx), B, E, hip.ptr(perm), hip.ptr(offs), hip.stream_ptr())
             counts_h = counts.cpu().numpy()
-            groups, o = [], 0
-            for e in range(E):
-                be = int(counts_h[e])
-                groups.append((e, perm[o:o + be], be))
-                o += be
+            groups = [(e, (perm, offs), int(counts_h[e])) for e in range(E)]
         if ddp is not None:
             groups = ddp.global_groups(groups, B)
             if ddp.sync_bn and any(ddp.global_count(e) > 1 and ddp._local[e] == 0 for e in range(E)):
@@ -176,10 +226,13 @@ class MoEWrapper(nn.Module):
                                    "collectives could not be matched); use larger shards or sync_bn=False")
 
         # metrics buffer: per expert [total, gen, div, int, aux, std_int, mean_int, w, disc]
-        mbuf = torch.zeros(E, 9, dtype=torch.float32, device=dev)
+        # (persistent buffers: captured expert graphs write into them)
+        mbuf = self._buf("mbuf", (E, 9), torch.float32, dev).zero_()
         # mean_intensities_in_batch_expert (moe.py:196-198): the ED router term's per-sample features
-        self._ed_feat = (torch.zeros(B, dtype=torch.float32, device=dev)
+        self._ed_feat = (self._buf("ed_feat", (B,), torch.float32, dev).zero_()
                          if E > 1 and float(rc.ed_strength) != 0.0 else None)
+        if self._graphs is not None:
+            self._graphs.begin()
         for e, rows, be in groups:
             be_global = be if ddp is None else ddp.global_count(e)
             if be_global <= 1:                                                   # moe.py:126-135
@@ -187,17 +240,21 @@ class MoEWrapper(nn.Module):
             og, od, oa = generator_optimizers[e], discriminator_optimizers[e], aux_reg_optimizers[e]
             # SyncBN: global batch statistics, so even one local sample runs
             if be > 1 or (ddp is not None and ddp.sync_bn and be >= 1):
-                self._expert_step(e, rows, be, B, cond, real_images, true_positions, std, intensity,
-                                  og, od, oa, mbuf, step, dev)
+                run = lambda: self._expert_step(e, rows, be, B, cond, real_images, true_positions, std, intensity,
+                                                og, od, oa, mbuf, step, dev)
+                if self._graphs is not None:
+                    self._weight_scalar(be, B, dev)
+                    self._graphs.run((e, be, B), run)
+                else:
+                    run()
             else:
                 # DDP: expert active globally but (almost) absent from this shard -> zero local
-                # gradients, but join the same collectives and optimizer steps as the other ranks;
-                # the two noise draws' stream ids are consumed so later draws stay aligned
-                if self.noise_fn is None and self.rng.step_counter is not None:
-                    self.rng.calls += 2
+                # gradients, but join the same collectives and optimizer steps as the other ranks
                 self._allreduce(self.discriminators[e]); od.step()
                 self._allreduce(self.generators[e]); self._allreduce(self.aux_regs[e]); og.step(); oa.step()
 
+        if self._graphs is not None:
+            self._graphs.join()
         if ddp is not None:
             ddp.merge_metrics(mbuf)          # the global batch's per-expert metrics on every rank
 
@@ -238,6 +295,7 @@ class MoEWrapper(nn.Module):
                      | (8 if rc.util_strength != 0 else 0) | (16 if ed_on else 0))
 
         self.step_count += 1
+        self._eager_steps += 1
         hip.call("es_counter_add", hip.ptr(self._dstep), 1, hip.stream_ptr())
         # the metric dict (moe.py:480-502): one kernel over the expert rows and router terms
         countsf = None if self.ddp is None else self.ddp.global_counts_tensor(dev)
@@ -262,16 +320,15 @@ class MoEWrapper(nn.Module):
         if rows is None:
             sc, sr, sp, ss, si = cond, real, pos, std, intensity
         else:
-            ridx = rows                      # device int32 row indices (es_router_dispatch)
-            gather = lambda t, cols: _gather_rows(t, ridx, cols)
+            # expert e's rows: perm[offs[e] : offs[e] + be] of the device dispatch, read at run time
+            perm, offs = rows
+            ridx = (perm, offs[e:e + 1])
+            gather = lambda t, cols: _gather_rows(t, ridx, be, cols)
             sc, sp, ss, si = gather(cond, cond.shape[1]), gather(pos, 2), gather(std, 1), gather(intensity, 1)
             sr = gather(real.reshape(B, -1), H * W).view(be, 1, H, W)
         # class_counts_adjusted[i] as float32 (moe.py:99-100,522,562)
         # (DDP: local weight B_e^r / B_r; the all-reduce averages, see expertsim/train/ddp.py)
-        w = float(np.float32(be) / np.float32(B))
-        w_dev = self._w_cache.get((w, dev))
-        if w_dev is None:      # one device scalar per distinct weight (no fill launch per step)
-            w_dev = self._w_cache[(w, dev)] = torch.full((1,), w, dtype=torch.float32, device=dev)
+        w_dev = self._weight_scalar(be, B, dev)
         # the step term (step * 1024) is added on the device from self._dstep
         sb = lambda pid: philox.dropout_stream(0, e, pid, 0)
         seed = self.rng_seed
@@ -315,8 +372,11 @@ class MoEWrapper(nn.Module):
         s = torch.empty(be, dtype=torch.float32, device=dev)
         hip.call("es_image_expsum", C.byref(fake1.view), fake1.dt, fake1.ptr, hip.ptr(s), hip.stream_ptr())
         if self._ed_feat is not None:
-            hip.call("es_scatter_rows", hip.ptr(s), hip.ptr(ridx) if rows is not None else None, be,
-                     hip.ptr(self._ed_feat), hip.stream_ptr())
+            if rows is None:
+                hip.call("es_scatter_rows", hip.ptr(s), None, be, hip.ptr(self._ed_feat), hip.stream_ptr())
+            else:
+                hip.call("es_scatter_rows_at", hip.ptr(s), hip.ptr(ridx[0]), hip.ptr(ridx[1]), be,
+                         hip.ptr(self._ed_feat), hip.stream_ptr())
         coords, actx = A.fwd(fake1, seed=seed, stream_base=sb(philox.PASS_AUX), n_offset=n0)
         L = fl1.dims[1]
         p = hip.GenLoss()
@@ -390,10 +450,84 @@ class MoEWrapper(nn.Module):
         return counts / expert_assignments.size(0)
 
 
-def _gather_rows(t: torch.Tensor, ridx: torch.Tensor, cols: int) -> torch.Tensor:
-    rows = ridx.numel()
+def _gather_rows(t: torch.Tensor, ridx, rows: int, cols: int) -> torch.Tensor:
+    """ridx = (dispatch permutation, device start position): rows perm[start : start + rows]."""
+    perm, start = ridx
     out = torch.empty(rows, cols, dtype=torch.float32, device=t.device)
     src = t.reshape(t.shape[0], -1)
-    hip.call("es_gather_rows", hip.ptr(src), src.stride(0), hip.ptr(ridx), rows, cols, hip.ptr(out), cols,
-             hip.stream_ptr())
+    hip.call("es_gather_rows_at", hip.ptr(src), src.stride(0), hip.ptr(perm), hip.ptr(start), rows, cols,
+             hip.ptr(out), cols, hip.stream_ptr())
     return out
+
+
+class ExpertGraphs:
+    """HIP graphs of whole expert steps (gather, G fwd, D step + Adam, G step + Adam), one per
+    (expert, expert batch size, batch size).  A multi-expert step then issues ~40 launches from the
+    host (router, dispatch, router loss + Adam, metrics) plus one graph replay per active expert,
+    instead of ~450 launches per expert, and the experts' graphs run CONCURRENTLY, one HIP stream
+    per expert: experts share no parameters and write disjoint rows of the step's buffers, and a
+    quarter-batch expert alone leaves most of the chip idle.  Each expert has its own memory pool
+    (its graphs replay one after another, so they may share temporaries; different experts'
+    graphs may not).  Everything that changes between steps is read on the device: the step
+    counters (dropout / noise streams, Adam bias corrections), the expert's rows (dispatch
+    permutation + device start), the batch (static input buffers).  The first occurrence of a key
+    is captured and then replayed; BatchNorm batch counts recorded at capture are re-applied on
+    every replay."""
+
+    def __init__(self, max_graphs: int = 512):
+        self.pools, self.streams = {}, {}
+        self.graphs = {}
+        self.max_graphs = max_graphs
+        self.captures = 0
+        self.replays = 0
+        self._used = []
+        self._ready = None
+
+    def clear(self):
+        self.graphs = {}
+
+    def begin(self):
+        """Mark the point on the current stream the experts' graphs start after."""
+        self._ready = torch.cuda.Event()
+        self._ready.record()
+        self._used = []
+
+    def run(self, key, fn):
+        from ..layers import count_batches, nbt_added, nbt_snapshot
+        e = key[0]
+        if e not in self.streams:
+            self.streams[e] = torch.cuda.Stream()
+            self.pools[e] = torch.cuda.graph_pool_handle()
+        st = self.streams[e]
+        st.wait_event(self._ready)
+        entry = self.graphs.get(key)
+        if entry is None:
+            if len(self.graphs) >= self.max_graphs:
+                self.graphs = {}
+            before = nbt_snapshot()
+            g = torch.cuda.CUDAGraph()
+            # capture on the expert's own stream (torch.cuda.graph's gc.collect + empty_cache per
+            # capture cost ~10 ms; the experts' captures do not need them)
+            with torch.cuda.stream(st):
+                g.capture_begin(pool=self.pools[e])
+                try:
+                    fn()
+                finally:
+                    g.capture_end()
+            # the capture recorded the host-side batch counts once; replays re-apply them
+            entry = self.graphs[key] = (g, nbt_added(before))
+            self.captures += 1
+        else:
+            self.replays += 1
+            for t, k in entry[1]:
+                count_batches(t, k)
+        with torch.cuda.stream(st):
+            entry[0].replay()
+        self._used.append(st)
+
+    def join(self):
+        """The current stream waits for every expert graph of this step."""
+        cur = torch.cuda.current_stream()
+        for st in self._used:
+            cur.wait_stream(st)
+        self._used = []

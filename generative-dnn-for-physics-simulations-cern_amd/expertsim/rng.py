@@ -49,6 +49,24 @@ class DeviceRNG:
                      hip.stream_ptr())
         return out
 
+    def _draw_at(self, name, out, index, offset=0):
+        """Draw on the step's stream ``stream_base + index`` (a fixed id per call site, so a captured
+        per-expert graph draws the same stream whatever other experts ran)."""
+        hip.require_device(out)
+        if self.step_counter is None:
+            return self._draw(name, out, offset)
+        if not 0 <= index < STEP_MUL:
+            raise RuntimeError("DeviceRNG: stream index %d outside [0, %d)" % (index, STEP_MUL))
+        hip.call(name + "_dev", hip.ptr(out), out.numel(), self.seed, (self.stream_base + index) & 0xFFFFFFFF,
+                 hip.ptr(self.step_counter), STEP_MUL, int(offset), hip.stream_ptr())
+        return out
+
+    def normal_at(self, out: torch.Tensor, index: int, offset: int = 0):
+        return self._draw_at("es_randn", out, index, offset)
+
+    def exponential_at(self, out: torch.Tensor, index: int, offset: int = 0):
+        return self._draw_at("es_rand_exponential", out, index, offset)
+
     def normal(self, out: torch.Tensor, offset: int = 0):
         """out[i] = draw number offset + i of this call's stream (offset even): a data-parallel rank
         passes its first global row x row length and draws exactly its rows of the global draw."""

@@ -280,6 +280,10 @@ int es_avgpool_bwd(const es_view_t* dy, const void* dyp, const es_view_t* dx, es
 /* rows gathered by index: dst[i,:] = src[idx[i],:] (fp32 rows of `cols`); idx NULL = identity */
 int es_gather_rows(const float* src, int64_t src_ld, const int32_t* idx, int rows, int cols,
                    float* dst, int64_t dst_ld, es_stream_t stream);
+/* Same with idx = perm + start[0], start read on the device (es_router_dispatch's offsets): the
+ * per-expert gather of a captured expert graph (moe.py:121-143). */
+int es_gather_rows_at(const float* src, int64_t src_ld, const int32_t* perm, const int32_t* start, int rows,
+                      int cols, float* dst, int64_t dst_ld, es_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Spectral norm (torch.nn.utils.spectral_norm, n_power_iterations=1, eps=1e-12) for every
@@ -373,6 +377,10 @@ int es_dp_metrics_merge(const float* rows, int world, int E, float* out, es_stre
 /* dst[rows[i]] = src[i] for i < n (rows NULL: identity) -- moe.py:196-198 scatter of the
  * per-sample photon sums into the batch-ordered ED features. */
 int es_scatter_rows(const float* src, const int32_t* rows, int n, float* dst, es_stream_t stream);
+/* Same with the rows read from a dispatch permutation at a DEVICE start position (perm + start[0]),
+ * so a captured per-expert graph stays valid whatever the expert's offset in a later step. */
+int es_scatter_rows_at(const float* src, const int32_t* perm, const int32_t* start, int n, float* dst,
+                       es_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Optimizer (torch.optim.Adam, created at train/training_setup.py:20-40, stepped at
