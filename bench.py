@@ -219,12 +219,16 @@ def run_mode(args, precision, steps, warmup, dev, rank, world, ddp, probe_steps)
     if sg is not None:
         sg.sync_host_state([*og, *od, *oa, orr])
     if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     roof = None
-    if probe_steps and rank == 0:
+    if probe_steps:
+        # every rank runs the probed eager steps (their gradient all-reduces are collectives);
+        # rank 0 reports
         roof = probe_dominant(moe, eager, probe_steps, args.arch, args.batch, precision)
+        if rank != 0:
+            roof = None
     value = args.batch * world * steps / dt
     del moe, og, od, oa, orr, step, sg, t, real, step_args
     torch.cuda.synchronize()
@@ -250,20 +254,34 @@ def main():
                     help="data parallel: global BatchNorm / SDI / router statistics (single-device semantics)")
     ap.add_argument("--ddp", action="store_true",
                     help="run the data-parallel code path even on one process (1-rank RCCL group)")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse several ranks "
+                         "on one GPU)")
     args = ap.parse_args()
+
+    # stdout carries exactly the one JSON line: RCCL's init banner and gloo's connection messages are
+    # written to fd 1 by native code, so fd 1 is pointed at stderr and the JSON goes to a saved copy
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
 
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; ranks beyond the visible devices (gloo rehearsals on a 1-GPU box) share them
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     ddp = world > 1 or args.ddp
     if ddp:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
 
     probe_steps = 0 if args.no_probe else 5
     value, dt, roof, launch = run_mode(args, args.precision, args.steps, args.warmup, dev, rank, world, ddp,
@@ -299,7 +317,7 @@ def main():
             out["parity_fp32"] = parity
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.arch)
-        print(json.dumps(out), flush=True)
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if ddp:
         dist.destroy_process_group()
 
