@@ -20,19 +20,13 @@
 //            Image gradient: dx[i][j] = sum_{r,s} e_rs[i-r][j-s] with e_rs[o] = sum_k dh[o][k] W[k][r][s]
 //            built in LDS (9 x Ho*Wo floats), so dh itself is never stored.
 //
-// Lane layout: thread t handles channel quad g = t & 7 (GroupNorm group g = channels 4g..4g+3)
-// and pooling windows u = t >> 3, u + 64, ...  A window's 2x2 conv outputs come from its 4x4 image
-// patch, read once from LDS and shared by the quad's 4 channels.
-#include "common.h"
+// Lane layout and the per-window helpers: d_front_common.h.
+#include "d_front_common.h"
 
 namespace {
 
-constexpr int FT = 512;                    // threads per image
-constexpr int FK = 32, FG = 8, CPG = 4;    // conv channels, GN groups, channels per group
-constexpr int TAPS = 9;                    // 3x3
-constexpr int MAXPIX = 2048;               // image pixels held in LDS
-constexpr int MAXOUT = 1792;               // conv outputs per image (e_rs planes in LDS)
-constexpr int NW = FT / 64;                // waves per workgroup
+using namespace dfront;
+
 constexpr int NPART = FK * TAPS + 3 * FK;  // per image: dW [32][9] | dbias | dgamma | dbeta
 
 struct FrontArgs {
@@ -48,84 +42,13 @@ struct FrontArgs {
   float* part;                             // [N][NPART]
 };
 
-struct Quad {                              // the thread's 4 channels: W/sigma, bias, gamma, beta
-  float w[CPG][TAPS], b[CPG], gm[CPG], bt[CPG];
-};
-
-__device__ __forceinline__ void load_quad(const FrontArgs& a, int g, Quad& q) {
-  const float sc = a.sigma ? 1.f / a.sigma[0] : 1.f;     // as es_pack_conv_weight
-#pragma unroll
-  for (int c = 0; c < CPG; ++c) {
-    const int k = g * CPG + c;
-#pragma unroll
-    for (int t = 0; t < TAPS; ++t) q.w[c][t] = a.w[k * TAPS + t] * sc;
-    q.b[c] = a.bias ? a.bias[k] : 0.f;
-    q.gm[c] = a.gamma ? a.gamma[k] : 1.f;
-    q.bt[c] = a.beta ? a.beta[k] : 0.f;
-  }
-}
-
-__device__ __forceinline__ void stage_image(const FrontArgs& a, int n, float* im) {
-  const float* src = a.img + n * a.is[0];
-  for (int i = threadIdx.x; i < a.H * a.W; i += FT) {
-    const int h = i / a.W, x = i - h * a.W;
-    im[i] = src[h * a.is[2] + x * a.is[3]];
-  }
-}
-
-// The 4x4 image patch of pooling window (pi, pj) and its 2x2 conv outputs v[pos][c],
-// pos = 2*dy + dx (row-major window order, as the pool's argmax byte).
-__device__ __forceinline__ void window(const float* im, int W, int pi, int pj, const Quad& q,
-                                       float (&x)[4][4], float (&v)[4][CPG]) {
-  const float* p = im + 2 * pi * W + 2 * pj;
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) x[r][s] = p[r * W + s];
-#pragma unroll
-  for (int pos = 0; pos < 4; ++pos)
-#pragma unroll
-    for (int c = 0; c < CPG; ++c) {
-      float s = q.b[c];
-#pragma unroll
-      for (int t = 0; t < TAPS; ++t) s = fmaf(x[(pos >> 1) + t / 3][(pos & 1) + t % 3], q.w[c][t], s);
-      v[pos][c] = s;
-    }
-}
-
-// In place: v[i] <- sum of v[i] over the workgroup's threads with the same channel quad (t & 7).
-// red holds NW * 8 * NV floats.
-template <int NV>
-__device__ __forceinline__ void quad_sum(float (&v)[NV], float* red) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    v[i] += __shfl_xor(v[i], 8, 64);
-    v[i] += __shfl_xor(v[i], 16, 64);
-    v[i] += __shfl_xor(v[i], 32, 64);
-  }
-  __syncthreads();                                   // red may still be read by a previous use
-  if (lane < 8) {
-#pragma unroll
-    for (int i = 0; i < NV; ++i) red[(wid * 8 + lane) * NV + i] = v[i];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    float t = 0.f;
-#pragma unroll
-    for (int k = 0; k < NW; ++k) t += red[(k * 8 + (lane & 7)) * NV + i];
-    v[i] = t;
-  }
-}
-
 __global__ void __launch_bounds__(FT) dfront_fwd_kernel(FrontArgs a) {
   __shared__ float im[MAXPIX];
   __shared__ float red[NW * 8];
   const int n = blockIdx.x, g = threadIdx.x & 7, u = threadIdx.x >> 3;
   Quad q;
-  load_quad(a, g, q);
-  stage_image(a, n, im);
+  load_quad_p(a.w, a.sigma, a.bias, a.gamma, a.beta, g, q);
+  stage_image_p(a.img, a.is, a.H, a.W, n, im);
   __syncthreads();
   const int NP = a.Hp * a.Wp;
   const float cnt = (float)(CPG * a.Ho * a.Wo);
@@ -191,8 +114,8 @@ __global__ void __launch_bounds__(FT) dfront_bwd_kernel(FrontArgs a) {
   __shared__ float ep[TAPS * MAXOUT];      // e_rs planes; also the reduction scratch
   const int n = blockIdx.x, g = threadIdx.x & 7, u = threadIdx.x >> 3;
   Quad q;
-  load_quad(a, g, q);
-  stage_image(a, n, im);
+  load_quad_p(a.w, a.sigma, a.bias, a.gamma, a.beta, g, q);
+  stage_image_p(a.img, a.is, a.H, a.W, n, im);
   __syncthreads();
   const int NP = a.Hp * a.Wp;
   const float cnt = (float)(CPG * a.Ho * a.Wo);

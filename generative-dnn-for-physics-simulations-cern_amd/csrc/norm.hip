@@ -280,39 +280,54 @@ __global__ void sum_finalize_kernel(const float* part, int chunks, int C, float*
   out[c] = (beta != 0.f ? beta * out[c] : 0.f) + s;
 }
 
-// Block-per-channel variants of the finalize kernels (used when there are many chunks).
-__global__ void __launch_bounds__(256) bn_finalize_block_kernel(const float* part, int chunks, int C, float eps,
-                                                                float* mean, float* invstd, float* rmean,
-                                                                float* rvar, float mom) {
+// Block-per-channel variants of the finalize kernels (many chunks, moderate C).  1024 threads,
+// four independent partial loads in flight per thread: with 256 threads and one load chain per
+// thread the merge of a conv epilogue's 16208 row-tile partials (generator conv_layers.9, B = 1024)
+// took 76 us, latency-bound on 64 busy CUs.
+constexpr int FIN_T = 1024;
+
+__global__ void __launch_bounds__(FIN_T) bn_finalize_block_kernel(const float* part, int chunks, int C, float eps,
+                                                                  float* mean, float* invstd, float* rmean,
+                                                                  float* rvar, float mom) {
   // Plain fp64 sums n, sum n_b*m_b, sum (M_b + n_b*m_b^2) instead of a Welford merge per chunk: the
-  // merge's fp64 division made every thread's loop one dependent chain (17 us per call at 2048
-  // chunks); sums let the strided partial loads issue back to back.  fp64 keeps the
-  // S2 - n*mean^2 subtraction exact far beyond fp32 resolution for activation statistics.
+  // merge's fp64 division made every thread's loop one dependent chain; sums let the strided
+  // partial loads issue back to back.  fp64 keeps the S2 - n*mean^2 subtraction exact far beyond
+  // fp32 resolution for activation statistics.
   const int c = blockIdx.x;
   double n_ = 0.0, s1 = 0.0, s2 = 0.0;
-#pragma unroll 4
-  for (int k = threadIdx.x; k < chunks; k += blockDim.x) {
-    const float* p = part + (int64_t)k * 3 * C;
+  const int64_t st = (int64_t)3 * C;
+  int k = threadIdx.x;
+  for (; k + 3 * FIN_T < chunks; k += 4 * FIN_T) {
+    float nb[4], mb[4], Mb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float* p = part + (int64_t)(k + u * FIN_T) * st;
+      nb[u] = p[c]; mb[u] = p[C + c]; Mb[u] = p[2 * C + c];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool has = nb[u] > 0.f;        // an empty chunk's mean / M2 may be 0/0: skip it
+      const double nd = nb[u], md = mb[u];
+      n_ += nd;
+      s1 += has ? nd * md : 0.0;
+      s2 += has ? (double)Mb[u] + nd * md * md : 0.0;
+    }
+  }
+  for (; k < chunks; k += FIN_T) {
+    const float* p = part + (int64_t)k * st;
     const double nb = p[c], mb = p[C + c], Mb = p[2 * C + c];
-    const bool has = nb > 0.0;             // an empty chunk's mean / M2 may be 0/0: skip it
+    const bool has = nb > 0.0;
     n_ += nb;
     s1 += has ? nb * mb : 0.0;
     s2 += has ? Mb + nb * mb * mb : 0.0;
   }
-  __shared__ double sn[256], sm[256], sM[256];
-  sn[threadIdx.x] = n_; sm[threadIdx.x] = s1; sM[threadIdx.x] = s2;
-  __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
-    if (threadIdx.x < off) {
-      sn[threadIdx.x] += sn[threadIdx.x + off];
-      sm[threadIdx.x] += sm[threadIdx.x + off];
-      sM[threadIdx.x] += sM[threadIdx.x + off];
-    }
-    __syncthreads();
-  }
+  __shared__ double sh[FIN_T / 64];
+  n_ = block_sum_d(n_, sh);
+  s1 = block_sum_d(s1, sh);
+  s2 = block_sum_d(s2, sh);
   if (threadIdx.x == 0) {
-    const double nt = sn[0], mt = sm[0] / nt;
-    const double Mt = fmax(sM[0] - nt * mt * mt, 0.0);
+    const double nt = n_, mt = s1 / nt;
+    const double Mt = fmax(s2 - nt * mt * mt, 0.0);
     const double var = Mt / nt;
     mean[c] = (float)mt;
     invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
@@ -321,25 +336,78 @@ __global__ void __launch_bounds__(256) bn_finalize_block_kernel(const float* par
   }
 }
 
-__global__ void __launch_bounds__(256) sums_finalize_block_kernel(const float* part, int chunks, int C, float cnt,
-                                                                  const float* gamma, float* a1, float* a2,
-                                                                  float* out1, float* out2, float beta1) {
-  // out1 (+)= s1 (beta1: scale of old out1), out2 += s2; a1/a2 = gamma*s/cnt (BN backward)
+// out1 (+)= s1 (beta1: scale of old out1), out2 += s2; a1/a2 = gamma*s/cnt (BN backward)
+__device__ __forceinline__ void sums_store(int c, float s1, float s2, float cnt, const float* gamma, float* a1,
+                                           float* a2, float* out1, float* out2, float beta1) {
+  const float g = gamma ? gamma[c] : 1.f;
+  if (a1) { a1[c] = g * s1 / cnt; a2[c] = g * s2 / cnt; }
+  if (out1) out1[c] = (beta1 != 0.f ? beta1 * out1[c] : 0.f) + s1;
+  if (out2) out2[c] += s2;
+}
+
+__global__ void __launch_bounds__(FIN_T) sums_finalize_block_kernel(const float* part, int chunks, int C, float cnt,
+                                                                    const float* gamma, float* a1, float* a2,
+                                                                    float* out1, float* out2, float beta1) {
   const int c = blockIdx.x;
-  __shared__ float sh[8];
+  __shared__ float sh[FIN_T / 64];
   float s1 = 0.f, s2 = 0.f;
-  for (int k = threadIdx.x; k < chunks; k += blockDim.x) {
-    const float* p = part + (int64_t)k * 3 * C;
+  const int64_t st = (int64_t)3 * C;
+  int k = threadIdx.x;
+  for (; k + 3 * FIN_T < chunks; k += 4 * FIN_T) {
+    float v1[4], v2[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float* p = part + (int64_t)(k + u * FIN_T) * st;
+      v1[u] = p[C + c]; v2[u] = p[2 * C + c];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { s1 += v1[u]; s2 += v2[u]; }
+  }
+  for (; k < chunks; k += FIN_T) {
+    const float* p = part + (int64_t)k * st;
     s1 += p[C + c]; s2 += p[2 * C + c];
   }
   s1 = block_sum(s1, sh);
   s2 = block_sum(s2, sh);
-  if (threadIdx.x == 0) {
-    const float g = gamma ? gamma[c] : 1.f;
-    if (a1) { a1[c] = g * s1 / cnt; a2[c] = g * s2 / cnt; }
-    if (out1) out1[c] = (beta1 != 0.f ? beta1 * out1[c] : 0.f) + s1;
-    if (out2) out2[c] += s2;
+  if (threadIdx.x == 0) sums_store(c, s1, s2, cnt, gamma, a1, a2, out1, out2, beta1);
+}
+
+// thread-per-channel form of the same (few chunks, or many channels: coalesced across channels)
+__global__ void __launch_bounds__(256) sums_finalize_kernel(const float* part, int chunks, int C, float cnt,
+                                                            const float* gamma, float* a1, float* a2, float* out1,
+                                                            float* out2, float beta1) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll 4
+  for (int k = 0; k < chunks; ++k) {
+    const float* p = part + (int64_t)k * 3 * C;
+    s1 += p[C + c]; s2 += p[2 * C + c];
   }
+  sums_store(c, s1, s2, cnt, gamma, a1, a2, out1, out2, beta1);
+}
+
+// finalize dispatch: a block per channel while the chunks dominate, a thread per channel otherwise
+bool fin_block(int chunks, int C) { return chunks > 32 && C < 4096; }
+
+void launch_bn_finalize(hipStream_t st, const float* part, int chunks, int C, float eps, float* mean, float* invstd,
+                        float* rmean, float* rvar, float mom) {
+  if (fin_block(chunks, C))
+    hipLaunchKernelGGL(bn_finalize_block_kernel, dim3(C), dim3(FIN_T), 0, st, part, chunks, C, eps, mean, invstd,
+                       rmean, rvar, mom);
+  else
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, chunks, C, eps, mean,
+                       invstd, rmean, rvar, mom);
+}
+
+void launch_sums_finalize(hipStream_t st, const float* part, int chunks, int C, float cnt, const float* gamma,
+                          float* a1, float* a2, float* out1, float* out2, float beta1) {
+  if (fin_block(chunks, C))
+    hipLaunchKernelGGL(sums_finalize_block_kernel, dim3(C), dim3(FIN_T), 0, st, part, chunks, C, cnt, gamma, a1, a2,
+                       out1, out2, beta1);
+  else
+    hipLaunchKernelGGL(sums_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, chunks, C, cnt, gamma,
+                       a1, a2, out1, out2, beta1);
 }
 
 // GroupNorm stats finalize from fast partials [n][chunk][3][C]: one thread per (n, g), Chan merge
@@ -531,11 +599,7 @@ BwdIn mk_bwdin(const es_view_t* x, es_dtype_t xdt, const void* xp, const es_norm
 // dsum += sum of the fast apply's per-block partials (s1 slot of [chunk][3][C])
 void fast_dsum_finalize(int C, int chunks, const float* part, float* dsum, hipStream_t st) {
   if (chunks <= 0 || dsum == nullptr) return;
-  if (chunks > 32)
-    hipLaunchKernelGGL(sums_finalize_block_kernel, dim3(C), dim3(256), 0, st, part, chunks, C, 1.f, nullptr,
-                       (float*)nullptr, (float*)nullptr, dsum, (float*)nullptr, 1.f);
-  else
-    hipLaunchKernelGGL(sum_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, chunks, C, dsum, 1.f);
+  launch_sums_finalize(st, part, chunks, C, 1.f, nullptr, (float*)nullptr, (float*)nullptr, dsum, (float*)nullptr, 1.f);
 }
 
 int64_t stats_groups(const es_view_t* x, int kind, int groups) {
@@ -627,12 +691,7 @@ extern "C" int es_norm_stats(const es_view_t* x, es_dtype_t xdt, const void* xp,
       chunks = es_fast_norm_stats(x, 0, xdt, xp, (float*)ws, st);
     else
       hipLaunchKernelGGL(colred_kernel<RED_STATS>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, (float*)ws);
-    if (chunks > 32)
-      hipLaunchKernelGGL(bn_finalize_block_kernel, dim3(x->c), dim3(256), 0, st, (const float*)ws, chunks, x->c,
-                         eps, mean, invstd, running_mean, running_var, momentum);
-    else
-      hipLaunchKernelGGL(bn_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)ws,
-                         chunks, x->c, eps, mean, invstd, running_mean, running_var, momentum);
+    launch_bn_finalize(st, (const float*)ws, chunks, x->c, eps, mean, invstd, running_mean, running_var, momentum);
   } else {
     const int64_t ng = stats_groups(x, kind, groups);
     hipLaunchKernelGGL(segred_kernel<RED_STATS>, dim3((unsigned)ng), dim3(256), 0, st, b, eps, mean, invstd);
@@ -645,12 +704,7 @@ extern "C" int es_norm_stats_finalize(const float* part, int chunks, int C, floa
                                       float* running_mean, float* running_var, float momentum, es_stream_t stream) {
   ES_CHECK_ARG(part && chunks > 0 && C > 0, "norm_stats_finalize: bad arguments");
   hipStream_t st = (hipStream_t)stream;
-  if (chunks > 32)
-    hipLaunchKernelGGL(bn_finalize_block_kernel, dim3(C), dim3(256), 0, st, part, chunks, C, eps, mean, invstd,
-                       running_mean, running_var, momentum);
-  else
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, chunks, C, eps, mean,
-                       invstd, running_mean, running_var, momentum);
+  launch_bn_finalize(st, part, chunks, C, eps, mean, invstd, running_mean, running_var, momentum);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
@@ -732,12 +786,7 @@ extern "C" int es_norm_act_bwd(const es_view_t* x, es_dtype_t xdt, const void* x
                        nm->gamma, g1, g2);
     if (dgamma || dbeta) {
       const int allc = x->n * fchunks;   // per-channel sums over every (n, chunk) partial
-      if (allc > 32)
-        hipLaunchKernelGGL(sums_finalize_block_kernel, dim3(x->c), dim3(256), 0, st, (const float*)part, allc,
-                           x->c, 1.f, nullptr, (float*)nullptr, (float*)nullptr, dbeta, dgamma, 1.f);
-      else
-        hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)part,
-                           allc, x->c, 1.f, nullptr, (float*)nullptr, (float*)nullptr, dgamma, dbeta);
+      launch_sums_finalize(st, (const float*)part, allc, x->c, 1.f, nullptr, (float*)nullptr, (float*)nullptr, dbeta, dgamma, 1.f);
     }
     if (dxp) fast_dsum_finalize(x->c, es_fast_norm_bwd_apply(x, fk, xdt, xp, dyp, dxp, nm, ch, g1, g2, dsum, part, st),
                                 part, dsum, st);
@@ -746,12 +795,7 @@ extern "C" int es_norm_act_bwd(const es_view_t* x, es_dtype_t xdt, const void* x
   }
   if (fast) {
     const int fchunks = es_fast_norm_bwd_reduce(x, 0, xdt, xp, dyp, nm, ch, part, st);
-    if (fchunks > 32)
-      hipLaunchKernelGGL(sums_finalize_block_kernel, dim3(x->c), dim3(256), 0, st, (const float*)part, fchunks,
-                         x->c, (float)rows, nm->gamma, g1, g2, dbeta, dgamma, 1.f);
-    else
-      hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)part,
-                         fchunks, x->c, (float)rows, nm->gamma, g1, g2, dgamma, dbeta);
+    launch_sums_finalize(st, (const float*)part, fchunks, x->c, (float)rows, nm->gamma, g1, g2, dbeta, dgamma, 1.f);
     if (dxp) fast_dsum_finalize(x->c, es_fast_norm_bwd_apply(x, 0, xdt, xp, dyp, dxp, nm, ch, g1, g2, dsum, part, st),
                                 part, dsum, st);
     ES_CHECK_LAUNCH();
@@ -759,23 +803,13 @@ extern "C" int es_norm_act_bwd(const es_view_t* x, es_dtype_t xdt, const void* x
   }
   if (kind == ES_NORM_BN) {
     hipLaunchKernelGGL(colred_kernel<RED_BWD>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, part);
-    if (chunks > 32)
-      hipLaunchKernelGGL(sums_finalize_block_kernel, dim3(x->c), dim3(256), 0, st, (const float*)part, chunks,
-                         x->c, (float)rows, nm->gamma, g1, g2, dbeta, dgamma, 1.f);
-    else
-      hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)part,
-                         chunks, x->c, (float)rows, nm->gamma, g1, g2, dgamma, dbeta);
+    launch_sums_finalize(st, (const float*)part, chunks, x->c, (float)rows, nm->gamma, g1, g2, dbeta, dgamma, 1.f);
     ap.a1 = g1; ap.a2 = g2;
   } else if (kind == ES_NORM_GN || kind == ES_NORM_LN) {
     hipLaunchKernelGGL(segred_kernel<RED_BWD>, dim3((unsigned)ng), dim3(256), 0, st, b, 0.f, g1, g2);
     if (dgamma || dbeta) {
       hipLaunchKernelGGL(colred_kernel<RED_BWD>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, part);
-      if (chunks > 32)
-        hipLaunchKernelGGL(sums_finalize_block_kernel, dim3(x->c), dim3(256), 0, st, (const float*)part, chunks,
-                           x->c, (float)rows, nullptr, (float*)nullptr, (float*)nullptr, dbeta, dgamma, 1.f);
-      else
-        hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)part,
-                           chunks, x->c, (float)rows, nullptr, (float*)nullptr, (float*)nullptr, dgamma, dbeta);
+      launch_sums_finalize(st, (const float*)part, chunks, x->c, (float)rows, nullptr, (float*)nullptr, (float*)nullptr, dbeta, dgamma, 1.f);
     }
     ap.a1 = g1; ap.a2 = g2;
   }
@@ -802,21 +836,14 @@ extern "C" int es_channel_sum(const es_view_t* x, es_dtype_t xdt, const void* xp
     // rows, instead of 63 of every 64 lanes idling
     const int nb = std::min<int>(chunks, (int)((rows + 255) / 256));
     hipLaunchKernelGGL(sum1_kernel, dim3(nb), dim3(256), 0, st, b, (int)rows, (float*)ws);
-    if (nb > 32)   // (a single thread summing thousands of partials took ~75 us)
-      hipLaunchKernelGGL(sums_finalize_block_kernel, dim3(1), dim3(256), 0, st, (const float*)ws, nb, 1, 1.f,
-                         nullptr, (float*)nullptr, (float*)nullptr, out, (float*)nullptr, beta);
-    else
-      hipLaunchKernelGGL(sum_finalize_kernel, dim3(1), dim3(256), 0, st, (const float*)ws, nb, 1, out, beta);
+    // (a single thread summing thousands of partials took ~75 us: a block for nb > 32)
+    launch_sums_finalize(st, (const float*)ws, nb, 1, 1.f, nullptr, (float*)nullptr, (float*)nullptr, out,
+                         (float*)nullptr, beta);
     ES_CHECK_LAUNCH();
     return ES_OK;
   }
   hipLaunchKernelGGL(colred_kernel<RED_SUM>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, (float*)ws);
-  if (chunks > 32)
-    hipLaunchKernelGGL(sums_finalize_block_kernel, dim3(x->c), dim3(256), 0, st, (const float*)ws, chunks, x->c,
-                       1.f, nullptr, (float*)nullptr, (float*)nullptr, out, (float*)nullptr, beta);
-  else
-    hipLaunchKernelGGL(sum_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)ws,
-                       chunks, x->c, out, beta);
+  launch_sums_finalize(st, (const float*)ws, chunks, x->c, 1.f, nullptr, (float*)nullptr, (float*)nullptr, out, (float*)nullptr, beta);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
@@ -874,12 +901,7 @@ extern "C" int es_norm_bwd_sync(int phase, const es_view_t* x, es_dtype_t xdt, c
     else
       hipLaunchKernelGGL(colred_kernel<RED_BWD>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, part);
     // raw per-channel sums s1 = sum dnorm, s2 = sum dnorm*xhat (+ the local dbeta / dgamma)
-    if (nchunks > 32)
-      hipLaunchKernelGGL(sums_finalize_block_kernel, dim3(x->c), dim3(256), 0, st, (const float*)part, nchunks,
-                         x->c, 1.f, nullptr, sums, sums + x->c, dbeta, dgamma, 1.f);
-    else
-      hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)part,
-                         nchunks, x->c, 1.f, nullptr, sums, sums + x->c, dgamma, dbeta);
+    launch_sums_finalize(st, (const float*)part, nchunks, x->c, 1.f, nullptr, sums, sums + x->c, dbeta, dgamma, 1.f);
     ES_CHECK_LAUNCH();
     return ES_OK;
   }

@@ -54,6 +54,13 @@ class GenLoss(C.Structure):
                 ("in_strength", C.c_float), ("aux_strength", C.c_float), ("std_mean", C.c_void_p)]
 
 
+class DFront2Params(C.Structure):
+    _fields_ = [("w1", C.c_void_p), ("sigma1", C.c_void_p), ("b1", C.c_void_p), ("g1", C.c_void_p),
+                ("be1", C.c_void_p), ("w2", C.c_void_p), ("sigma2", C.c_void_p), ("b2", C.c_void_p),
+                ("g2", C.c_void_p), ("be2", C.c_void_p), ("eps1", C.c_float), ("eps2", C.c_float),
+                ("slope", C.c_float), ("ph", C.c_int), ("pw", C.c_int)]
+
+
 P = C.c_void_p
 I64 = C.c_int64
 _SIGS = {
@@ -94,6 +101,11 @@ _SIGS = {
     "es_dfront_part_floats": (I64, [C.c_int]),
     "es_dfront_bwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, P, P, P, P, C.c_float, C.c_float, P, P, P, P,
                                 P, P, P, P, P, P, P, P]),
+    "es_dfront2_ok": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int]),
+    "es_dfront2_part_floats": (I64, [C.c_int]),
+    "es_dfront2_fwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, P, P, I64, P]),
+    "es_dfront2_bwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, P, P, I64, P, P, P, P, P, P, P, P, P, P,
+                                 P, P]),
     "es_upsample_bwd": (C.c_int, [P, C.c_int, P, P, P, P, P, P, C.c_int, P, C.c_float, P]),
     "es_copy": (C.c_int, [P, C.c_int, P, P, C.c_int, P, C.c_float, C.c_float, P]),
     "es_avgpool_fwd": (C.c_int, [P, C.c_int, P, P, P, P]),

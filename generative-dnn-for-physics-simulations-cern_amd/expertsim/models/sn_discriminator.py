@@ -14,6 +14,7 @@ Program:
 """
 from __future__ import annotations
 
+import ctypes as C
 import os
 
 import torch
@@ -78,6 +79,57 @@ class SNDiscriminator(ExpertModule):
         return (self.fuse_front and x.t.dtype == torch.float32 and Cc == 1 and H >= 4 and W >= 4
                 and (H - 2) % 2 == 0 and (W - 2) % 2 == 0 and H * W <= 2048 and (H - 2) * (W - 2) <= 1792)
 
+    # both conv blocks as one per-image kernel pair (d_front2.hip); ES_NO_DFRONT2=1: block 1 fused,
+    # block 2 on the generic kernels (A/B)
+    fuse_front2 = os.environ.get("ES_NO_DFRONT2") != "1"
+
+    def front2_fused(self, x: Act) -> bool:
+        N, Cc, H, W = x.dims
+        return (self.fuse_front and self.fuse_front2 and x.t.dtype == torch.float32 and Cc == 1
+                and self.compute_dtype == torch.float32
+                and bool(hip.lib().es_dfront2_ok(H, W, self.pool2[0], self.pool2[1])))
+
+    def _front2_params(self, sig):
+        m = lambda n: get_module(self, n)
+        c0, gn1, c4, gn2 = m("conv_layers.0"), m("conv_layers.1"), m("conv_layers.4"), m("conv_layers.5")
+        p = hip.DFront2Params()
+        p.w1, p.sigma1, p.b1 = c0.weight_orig.data_ptr(), sig["conv_layers.0"][0].data_ptr(), c0.bias.data_ptr()
+        p.g1, p.be1 = gn1.weight.data_ptr(), gn1.bias.data_ptr()
+        p.w2, p.sigma2, p.b2 = c4.weight_orig.data_ptr(), sig["conv_layers.4"][0].data_ptr(), c4.bias.data_ptr()
+        p.g2, p.be2 = gn2.weight.data_ptr(), gn2.bias.data_ptr()
+        p.eps1, p.eps2, p.slope = float(gn1.eps), float(gn2.eps), SLOPE
+        p.ph, p.pw = int(self.pool2[0]), int(self.pool2[1])
+        return p
+
+    def front2_bwd(self, ctx, dX: Act, weight_grads, input_grad, sn_jobs):
+        """Backward of both fused conv blocks from the fc1 input gradient rows; returns the image
+        gradient (fp32 Act) or None.  Weight gradients: W/sigma grads into the spectral-norm jobs,
+        biases and GroupNorm affines accumulated."""
+        x = ctx["x"]
+        B, _, H, W = x.dims
+        dev = x.t.device
+        m = lambda n: get_module(self, n)
+        dx = Act.nhwc(B, 1, H, W, torch.float32, dev) if input_grad else None
+        part = g0 = g4 = None
+        grads = [None] * 8
+        if weight_grads:
+            part = torch.empty(hip.lib().es_dfront2_part_floats(B), dtype=torch.float32, device=dev)
+            g0 = torch.empty_like(m("conv_layers.0").weight_orig)
+            g4 = torch.empty_like(m("conv_layers.4").weight_orig)
+            grads = [g0, m("conv_layers.0").bias.grad, m("conv_layers.1").weight.grad, m("conv_layers.1").bias.grad,
+                     g4, m("conv_layers.4").bias.grad, m("conv_layers.5").weight.grad, m("conv_layers.5").bias.grad]
+        F = self.flat_dim + self.cond_dim
+        hip.call("es_dfront2_bwd", x.ptr, hip.strides4(x.strides), B, H, W, C.byref(ctx["front2"]),
+                 hip.ptr(ctx["fstats"]), dX.ptr, F, dx.ptr if dx is not None else None,
+                 hip.strides4(dx.strides) if dx is not None else None, hip.ptr(part),
+                 *[hip.ptr(t) for t in grads], hip.stream_ptr())
+        if weight_grads:
+            sig = ctx["sig"]
+            o = self.ops()
+            sn_jobs.append((o["sn:conv_layers.4"], g4, sig["conv_layers.4"], m("conv_layers.4").weight_orig.grad))
+            sn_jobs.append((o["sn:conv_layers.0"], g0, sig["conv_layers.0"], m("conv_layers.0").weight_orig.grad))
+        return dx
+
     def _front_params(self, sigma):
         c0, gn = get_module(self, "conv_layers.0"), get_module(self, "conv_layers.1")
         return (hip.ptr(c0.weight_orig), hip.ptr(sigma), hip.ptr(c0.bias), hip.ptr(gn.weight), hip.ptr(gn.bias),
@@ -131,6 +183,18 @@ class SNDiscriminator(ExpertModule):
             copy_act(img, x)
         sig = dict(zip(LAYERS, SpectralNorm.sigma_many([o["sn:" + n] for n in LAYERS], update=train)))
         inv = lambda n: sig[n][0]
+        F = self.flat_dim + self.cond_dim
+        if front and self.front2_fused(x):
+            # both conv blocks in one kernel: features straight into the fc1 input rows
+            params = self._front2_params(sig)
+            fstats = torch.empty(B * 32, dtype=torch.float32, device=dev)
+            X = Act.rows(B, F, cdt, dev)
+            Xm = X.t.view(B, F)
+            hip.call("es_dfront2_fwd", x.ptr, hip.strides4(x.strides), B, x.dims[2], x.dims[3], C.byref(params),
+                     hip.ptr(fstats), X.ptr, F, hip.stream_ptr())
+            copy_act(Act.of(cond), Act.of(Xm[:, self.flat_dim:]))
+            return self._fc_fwd(X, B, cdt, dev, sig, dict(x=x, sig=sig, front=True, front2=params, fstats=fstats,
+                                                          X=X))
         if front:
             p1, i1, s1 = self.front_fwd(x, inv("conv_layers.0"))
             if p1.t.dtype != cdt:                   # bf16 mode: the GEMM layers after the front
@@ -144,13 +208,21 @@ class SNDiscriminator(ExpertModule):
             p1, i1 = o["pool1"].fwd(y1)
         h2 = o["conv_layers.4"].fwd(p1, inv_scale=inv("conv_layers.4"))
         y2, s2 = o["gn2"].fwd(h2, lr)
-        F = self.flat_dim + self.cond_dim
         fh, fw = self.feat_hw
         X = Act.rows(B, F, cdt, dev)
         Xm = X.t.view(B, F)
         feat = Act(Xm, (B, 16, fh, fw), (F, fh * fw, fw, 1))       # NCHW flatten order (view(B,-1))
         _, i2 = o["pool2"].fwd(y2, out=feat)
         copy_act(Act.of(cond), Act.of(Xm[:, self.flat_dim:]))
+        return self._fc_fwd(X, B, cdt, dev, sig, dict(x=x, sig=sig, front=front, front2=None, h1=h1, y1=y1, s1=s1,
+                                                      p1=p1, i1=i1, h2=h2, y2=y2, s2=s2, i2=i2, X=X,
+                                                      feat_dims=(B, 16, fh, fw)))
+
+    def _fc_fwd(self, X: Act, B, cdt, dev, sig, ctx):
+        """fc1 -> LN -> LReLU -> fc2 -> LN -> LReLU (latent) -> fc3 on the fc1 input rows X."""
+        o = self.ops()
+        lr = hip.chain_struct(hip.ACT_LRELU, SLOPE)
+        inv = lambda n: sig[n][0]
         h3 = o["fc1.0"].fwd(X, inv_scale=inv("fc1.0"))
         y3, s3 = o["ln1"].fwd(h3, lr)
         h4 = o["fc2.0"].fwd(y3, inv_scale=inv("fc2.0"))
@@ -160,8 +232,7 @@ class SNDiscriminator(ExpertModule):
             lat_c = lat.like_nhwc(cdt)
             copy_act(lat, lat_c)
         out = o["fc3"].fwd(lat_c, inv_scale=inv("fc3"), out_dtype=torch.float32)
-        ctx = dict(x=x, sig=sig, front=front, h1=h1, y1=y1, s1=s1, p1=p1, i1=i1, h2=h2, y2=y2, s2=s2, i2=i2, X=X,
-                   feat_dims=(B, 16, fh, fw), h3=h3, y3=y3, s3=s3, h4=h4, s4=s4, lat=lat_c)
+        ctx.update(h3=h3, y3=y3, s3=s3, h4=h4, s4=s4, lat=lat_c)
         return out, lat, ctx
 
     # --------------------------------------------------------------------------- backward
@@ -219,6 +290,8 @@ class SNDiscriminator(ExpertModule):
                            dbeta=m("fc1.1").bias.grad if weight_grads else None, dsum=bias_g("fc1.0"))
         wgrad("fc1.0", dh3, ctx["X"])
         dX = o["fc1.0"].dgrad(dh3, ctx["X"], inv_scale=sig["fc1.0"][0])
+        if ctx["front2"] is not None:
+            return self.front2_bwd(ctx, dX, weight_grads, input_grad, sn_jobs)
         F = self.flat_dim + self.cond_dim
         B_, Cf, fh, fw = ctx["feat_dims"]
         dfeat = Act(dX.t.view(B, F), (B, 16, fh, fw), (F, fh * fw, fw, 1))

@@ -264,6 +264,36 @@ int es_dfront_bwd(const float* img, const int64_t is[4], int N, int H, int W, co
                   float slope, const float* mean, const float* invstd, const uint8_t* idx,
                   const float* dpooled, float* dx, const int64_t dxs[4], float* part, float* dw,
                   float* dbias, float* dgamma, float* dbeta, es_stream_t stream);
+/* Fused discriminator front, both conv blocks (neutron/discriminator.py:11-24,
+ * proton/discriminator.py:121-134): SNconv3x3 1->32 -> GroupNorm(8, 32) -> LeakyReLU -> MaxPool 2x2
+ * -> SNconv3x3 32->16 -> GroupNorm(8, 16) -> LeakyReLU -> MaxPool (ph, pw) -> flatten (NCHW order),
+ * one workgroup per image: the pooled 32-channel map and the 16-channel conv map stay in LDS (the
+ * second conv on v_mfma_f32_16x16x4_f32), only the flattened features leave the chip.  Replaces
+ * es_dfront_* + es_conv2d_fwd/dgrad/wgrad of conv_layers.4 + the GroupNorm / pool passes after it.
+ * Weights are used as w * (1/sigma[0]) (sigma may be NULL: 1). */
+typedef struct {
+    const float* w1; const float* sigma1; const float* b1; const float* g1; const float* be1;  /* [32][1][3][3], GN(8,32) */
+    const float* w2; const float* sigma2; const float* b2; const float* g2; const float* be2;  /* [16][32][3][3], GN(8,16) */
+    float eps1, eps2, slope;
+    int ph, pw;                       /* second pool window = stride (neutron 2x2, proton 2x1) */
+} es_dfront2_params_t;
+/* 1 when the fused path supports this geometry (H*W <= 2048, H-2 and W-2 even, pooled map <= 448
+ * pixels, second conv map <= 368 pixels) */
+int es_dfront2_ok(int H, int W, int ph, int pw);
+/* Forward.  img fp32 [N][1][H][W] (strides is).  Writes feat[n*feat_stride + f], f < 16*Hq*Wq
+ * (the reference's view(B, -1) order) and stats [N][32] = GN1 mean[8], invstd[8], GN2 mean[8],
+ * invstd[8] (read back by the backward). */
+int es_dfront2_fwd(const float* img, const int64_t is[4], int N, int H, int W, const es_dfront2_params_t* p,
+                   float* stats, float* feat, int64_t feat_stride, es_stream_t stream);
+/* Backward from dfeat (the gradient of the features, same indexing as feat).  dx (optional): fp32
+ * image gradient [N][1][H][W] (strides dxs), written.  part (optional, es_dfront2_part_floats(N)
+ * floats): per-image weight-gradient partials; when given, dw1 / dw2 (gradients of W/sigma, torch
+ * layouts) are written and db*, dg*, dbe* (biases, GN affines) accumulated; each may be NULL. */
+int64_t es_dfront2_part_floats(int N);
+int es_dfront2_bwd(const float* img, const int64_t is[4], int N, int H, int W, const es_dfront2_params_t* p,
+                   const float* stats, const float* dfeat, int64_t dfeat_stride, float* dx, const int64_t dxs[4],
+                   float* part, float* dw1, float* db1, float* dg1, float* dbe1, float* dw2, float* db2,
+                   float* dg2, float* dbe2, es_stream_t stream);
 /* dx[n,c,h,w] = beta*dx + sum over upsampled positions mapping to (h,w).  hstart/hcount (device
  * [H]) and wstart/wcount (device [W]) describe the contiguous preimage of each source row/col. */
 int es_upsample_bwd(const es_view_t* dxu, es_dtype_t dt, const void* dxup, const int32_t* hstart,

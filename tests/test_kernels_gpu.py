@@ -529,6 +529,81 @@ def test_dfront_fused(N, H, W):
     assert rel(dbt.cpu() - 0.5, btr.grad) < 1e-4
 
 
+@pytest.mark.parametrize("N,H,W,pool", [(5, 44, 44, (2, 2)), (3, 56, 30, (2, 1)), (4, 12, 14, (2, 2))])
+def test_dfront2_fused(N, H, W, pool):
+    """es_dfront2_fwd / es_dfront2_bwd (both discriminator conv blocks in one per-image kernel,
+    d_front2.hip) against torch fp32 autograd of the reference block (neutron/discriminator.py:11-24,
+    proton/discriminator.py:121-134): flattened features, GN statistics, image gradient and the
+    gradients of both W/sigma, biases and GroupNorm affines -- for the D-step variant (weight
+    gradients only), the G-step variant (image gradient only) and both at once."""
+    hip = _hip()
+    import ctypes as C
+    torch.manual_seed(23)
+    x = torch.randn(N, 1, H, W)
+    w1 = torch.randn(32, 1, 3, 3) / 3
+    w2 = torch.randn(16, 32, 3, 3) / 17
+    b1, g1, be1 = 0.1 * torch.randn(32), 1 + 0.1 * torch.randn(32), 0.1 * torch.randn(32)
+    b2, g2, be2 = 0.1 * torch.randn(16), 1 + 0.1 * torch.randn(16), 0.1 * torch.randn(16)
+    s1, s2 = torch.tensor([1.7]), torch.tensor([1.3])
+    xr = x.clone().requires_grad_(True)
+    w1e = (w1 * (1.0 / s1)).requires_grad_(True)
+    w2e = (w2 * (1.0 / s2)).requires_grad_(True)
+    leaves = [t.clone().requires_grad_(True) for t in (b1, g1, be1, b2, g2, be2)]
+    b1r, g1r, be1r, b2r, g2r, be2r = leaves
+    h = F.conv2d(xr, w1e, b1r)
+    p = F.max_pool2d(F.leaky_relu(F.group_norm(h, 8, g1r, be1r, 1e-5), 0.1), 2)
+    h2 = F.conv2d(p, w2e, b2r)
+    q = F.max_pool2d(F.leaky_relu(F.group_norm(h2, 8, g2r, be2r, 1e-5), 0.1), pool)
+    feat = q.reshape(N, -1)
+    gf = torch.randn_like(feat)
+    feat.backward(gf)
+    nf = feat.shape[1]
+    Fs = nf + 9                                  # fc1 input rows: features | cond
+
+    dv = {k: t.to(DEV) for k, t in dict(w1=w1, s1=s1, b1=b1, g1=g1, be1=be1, w2=w2, s2=s2, b2=b2, g2=g2,
+                                        be2=be2).items()}
+    prm = hip.DFront2Params()
+    prm.w1, prm.sigma1, prm.b1, prm.g1, prm.be1 = (dv[k].data_ptr() for k in ("w1", "s1", "b1", "g1", "be1"))
+    prm.w2, prm.sigma2, prm.b2, prm.g2, prm.be2 = (dv[k].data_ptr() for k in ("w2", "s2", "b2", "g2", "be2"))
+    prm.eps1 = prm.eps2 = 1e-5
+    prm.slope = 0.1
+    prm.ph, prm.pw = pool
+    assert hip.lib().es_dfront2_ok(H, W, *pool)
+    xd = x.to(DEV)
+    X = torch.full((N, Fs), 7.0, device=DEV)
+    stats = torch.empty(N * 32, device=DEV)
+    hip.call("es_dfront2_fwd", hip.ptr(xd), hip.strides4(xd.stride()), N, H, W, C.byref(prm), hip.ptr(stats),
+             hip.ptr(X), Fs, hip.stream_ptr())
+    assert rel(X[:, :nf].cpu(), feat.detach()) < 1e-5
+    assert torch.all(X[:, nf:] == 7.0)           # the cond columns are left alone
+    st = stats.cpu().view(N, 4, 8)
+    hg, h2g = h.detach().view(N, 8, -1), h2.detach().view(N, 8, -1)
+    assert rel(st[:, 0], hg.mean(-1)) < 1e-5
+    assert rel(st[:, 1], torch.rsqrt(hg.var(-1, unbiased=False) + 1e-5)) < 1e-4
+    assert rel(st[:, 2], h2g.mean(-1)) < 1e-5
+    assert rel(st[:, 3], torch.rsqrt(h2g.var(-1, unbiased=False) + 1e-5)) < 1e-4
+
+    dX = torch.zeros(N, Fs, device=DEV)
+    dX[:, :nf] = gf.to(DEV)
+    refs = [w1e.grad, b1r.grad, g1r.grad, be1r.grad, w2e.grad, b2r.grad, g2r.grad, be2r.grad]
+    for want_dx, want_w in ((False, True), (True, False), (True, True)):
+        dx = torch.empty(N, 1, H, W, device=DEV) if want_dx else None
+        part = torch.empty(hip.lib().es_dfront2_part_floats(N), device=DEV) if want_w else None
+        outs = [torch.empty(32 * 9, device=DEV), torch.full((32,), 0.5, device=DEV),
+                torch.full((32,), 0.5, device=DEV), torch.full((32,), 0.5, device=DEV),
+                torch.empty(16 * 32 * 9, device=DEV), torch.full((16,), 0.5, device=DEV),
+                torch.full((16,), 0.5, device=DEV), torch.full((16,), 0.5, device=DEV)]
+        hip.call("es_dfront2_bwd", hip.ptr(xd), hip.strides4(xd.stride()), N, H, W, C.byref(prm), hip.ptr(stats),
+                 hip.ptr(dX), Fs, hip.ptr(dx), hip.strides4(dx.stride()) if dx is not None else None,
+                 hip.ptr(part), *[hip.ptr(o) if want_w else None for o in outs], hip.stream_ptr())
+        if want_dx:
+            assert rel(dx.cpu(), xr.grad) < 1e-4, (want_dx, want_w)
+        if want_w:
+            for i, (o, r) in enumerate(zip(outs, refs)):
+                got = o.cpu().view(r.shape) - (0.5 if i not in (0, 4) else 0.0)
+                assert rel(got, r) < 1e-4, (i, rel(got, r))
+
+
 @pytest.mark.parametrize("case", [(200, 256, 24, 24, 128, 3), (200, 128, 13, 13, 256, 3)])
 def test_conv_ring256_matches_ring128(case):
     """256 x 256 ring tiles with 32-deep K-steps (sub-pixel FWD with 256 output channels, DGRAD
