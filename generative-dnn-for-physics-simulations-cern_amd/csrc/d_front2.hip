@@ -14,13 +14,16 @@
 //   forward  M = conv-2 pixels, N = 16, K = (tap, channel) = 288 in 72 steps of 4
 //   wgrad    M = 16 (out channel), N = (tap, channel) = 288, K = conv-2 pixels
 //   dgrad    M = pooled block-1 pixels, N = 32, K = (tap, out channel) = 144
-// The operand images use odd pixel strides (33 / 17 floats), so the 16 rows x 4 k of one
-// ds_read_b32 fragment hit distinct banks.
+// A fragments are 16-byte LDS reads (4 consecutive k) feeding four MFMAs (the B registers use
+// the same k permutation); the operand images use pixel strides of 36 / 20 floats, so the 16 rows
+// of one ds_read_b128 cover distinct banks.
 //
-//   forward  reads the image; writes the features and the GN statistics [N][32] (GN1 mean / invstd,
-//            GN2 mean / invstd).  Nothing else: the backward recomputes both conv maps and both
-//            pool argmaxes from the image (same code, same values).
-//   backward reads the image, the feature gradient and the statistics; writes the image gradient
+//   forward  reads the image; writes the features, the GN statistics [N][32] (GN1 mean / invstd,
+//            GN2 mean / invstd) and (training) a per-image save of the pooled block-1 map, the
+//            block-1 conv values at the pool argmaxes and the block-2 conv map (es_dfront2_save_floats)
+//   backward reads the image, the save, the feature gradient and the statistics (the block-1 conv
+//            map is recomputed from the image in LDS: 9 MACs per value, cheaper than its HBM round
+//            trip; the argmaxes with the forward's code); writes the image gradient
 //            (optional: the generator step) and per-image partials of every weight gradient
 //            (optional: the discriminator step), summed over the images by a second launch
 //            (deterministic, no atomics).
@@ -34,12 +37,10 @@ using namespace dfront;
 
 constexpr int K2 = 16;                      // block-2 conv output channels
 constexpr int G2 = 8;                       // block-2 GroupNorm groups (channel pairs)
-constexpr int KS2 = FK * TAPS / 4;          // 72 K-steps of the block-2 forward GEMM
-constexpr int KSD = K2 * TAPS / 4;          // 36 K-steps of the block-2 dgrad GEMM
 constexpr int MAXP1 = 448;                  // pooled block-1 pixels (neutron 21x21, proton 27x14)
-constexpr int P1S = FK + 1;                 // p1 pixel stride (floats)
+constexpr int P1S = FK + 4;                 // p1 pixel stride (floats): 16-byte rows, b128 reads conflict-free
 constexpr int MAXH2 = 384;                  // block-2 conv pixels (neutron 19x19, proton 25x12)
-constexpr int H2S = K2 + 1;                 // h2 pixel stride (floats)
+constexpr int H2S = K2 + 4;                 // h2 pixel stride (floats), likewise
 constexpr int NWT2 = K2 * FK * TAPS;        // 4608 block-2 weights
 // per-image partials: dW2 [16][32][9] | db2 | dg2 | dbe2 | dW1 [32][9] | db1 | dg1 | dbe1
 constexpr int O_DB2 = NWT2, O_DG2 = O_DB2 + K2, O_DBE2 = O_DG2 + K2, O_W1 = O_DBE2 + K2;
@@ -59,40 +60,74 @@ struct F2Args {
   const float* dfeat; int64_t dfs;          // backward input
   float* dx; int64_t dxs[4];                // image gradient (or NULL)
   float* part;                              // [N][NPART2] (or NULL)
+  float* save; int64_t sv;                  // [N][sv]: p1 [NP1][32] | hv1 [NP1][32] | h2 [NO2][16]
+  long long* probe;                         // phase timestamps of workgroup 0 (ES_DF2_PROBE builds)
 };
 
-// GroupNorm(8, 32) statistics of the image's block-1 conv map (two passes, as dfront_fwd_kernel)
+long long* g_probe = nullptr;   // host: es_dfront2_set_probe
+
+#ifdef ES_DF2_PROBE
+#define PROBE(a, i) do { if ((a).probe && blockIdx.x == 0 && threadIdx.x == 0) (a).probe[i] = wall_clock64(); } while (0)
+#else
+#define PROBE(a, i) do { } while (0)
+#endif
+
+// Chan merge of (count, mean, M2) triples
+__device__ __forceinline__ void chan_merge(float& n, float& m, float& M, float nb, float mb, float Mb) {
+  const float nt = n + nb;
+  if (nt > 0.f) {
+    const float d = mb - m, f = nb / nt;
+    m += d * f;
+    M += Mb + d * d * n * f;
+  }
+  n = nt;
+}
+
+// GroupNorm(8, 32) statistics of the image's block-1 conv map in ONE pass: per window the 16
+// values (4 positions x the quad's 4 channels) give (16, mean, M2), Chan-merged over the thread's
+// windows, the 64 window streams of the group (shuffles) and the 8 waves (fixed order)
 __device__ __forceinline__ void block1_stats(const F2Args& a, const float* im, const Quad& q, int u, float* red,
                                              float& mu, float& istd) {
   const int NP = a.Hp * a.Wp;
-  const float cnt = (float)(CPG * a.Ho * a.Wo);
-  float s[1] = {0.f};
+  const int g = threadIdx.x & 7, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float n_ = 0.f, m_ = 0.f, M_ = 0.f;
   for (int pp = u; pp < NP; pp += FT / 8) {
     const int pi = pp / a.Wp, pj = pp - pi * a.Wp;
     float x[4][4], v[4][CPG];
     window(im, a.W, pi, pj, q, x, v);
+    float s = 0.f;
 #pragma unroll
     for (int pos = 0; pos < 4; ++pos)
 #pragma unroll
-      for (int c = 0; c < CPG; ++c) s[0] += v[pos][c];
-  }
-  quad_sum(s, red);
-  mu = s[0] / cnt;
-  float m2[1] = {0.f};
-  for (int pp = u; pp < NP; pp += FT / 8) {
-    const int pi = pp / a.Wp, pj = pp - pi * a.Wp;
-    float x[4][4], v[4][CPG];
-    window(im, a.W, pi, pj, q, x, v);
+      for (int c = 0; c < CPG; ++c) s += v[pos][c];
+    const float wm = s * (1.f / 16.f);
+    float wq = 0.f;
 #pragma unroll
     for (int pos = 0; pos < 4; ++pos)
 #pragma unroll
       for (int c = 0; c < CPG; ++c) {
-        const float d = v[pos][c] - mu;
-        m2[0] = fmaf(d, d, m2[0]);
+        const float d = v[pos][c] - wm;
+        wq = fmaf(d, d, wq);
       }
+    chan_merge(n_, m_, M_, 16.f, wm, wq);
   }
-  quad_sum(m2, red);
-  istd = rsqrtf(m2[0] / cnt + a.p.eps1);
+#pragma unroll
+  for (int o = 8; o < 64; o <<= 1)
+    chan_merge(n_, m_, M_, __shfl_xor(n_, o, 64), __shfl_xor(m_, o, 64), __shfl_xor(M_, o, 64));
+  __syncthreads();                                   // red may still be read by a previous use
+  if (lane < 8) {
+    red[(wid * 8 + lane) * 3 + 0] = n_;
+    red[(wid * 8 + lane) * 3 + 1] = m_;
+    red[(wid * 8 + lane) * 3 + 2] = M_;
+  }
+  __syncthreads();
+  n_ = red[g * 3];
+  m_ = red[g * 3 + 1];
+  M_ = red[g * 3 + 2];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) chan_merge(n_, m_, M_, red[(w * 8 + g) * 3], red[(w * 8 + g) * 3 + 1], red[(w * 8 + g) * 3 + 2]);
+  mu = m_;
+  istd = rsqrtf(M_ / n_ + a.p.eps1);
 }
 
 // window argmax of the block-1 pool (first max in row-major window order, NaN wins, as torch)
@@ -108,29 +143,40 @@ __device__ __forceinline__ int block1_argmax(const float (&v)[4][CPG], int c, co
   return bi;
 }
 
-// block-1 output into LDS: p1[pix * P1S + channel]
+// block-1 output into LDS (p1[pix * P1S + channel], one 16-byte store per window and quad) and,
+// when saving, to the image's save: p1 and the conv values at the argmaxes (hv1)
 __device__ __forceinline__ void block1_out(const F2Args& a, const float* im, const Quad& q, int g, int u, float mu,
-                                           float istd, float* p1) {
+                                           float istd, float* p1, float* sp1, float* shv) {
   const int NP = a.Hp * a.Wp;
   for (int pp = u; pp < NP; pp += FT / 8) {
     const int pi = pp / a.Wp, pj = pp - pi * a.Wp;
     float x[4][4], v[4][CPG];
     window(im, a.W, pi, pj, q, x, v);
+    float best[CPG], hv[CPG];
 #pragma unroll
     for (int c = 0; c < CPG; ++c) {
-      float best;
-      block1_argmax(v, c, q, mu, istd, a.p.slope, best);
-      p1[pp * P1S + g * CPG + c] = best;
+      const int bi = block1_argmax(v, c, q, mu, istd, a.p.slope, best[c]);
+      hv[c] = v[0][c];
+#pragma unroll
+      for (int pos = 1; pos < 4; ++pos) hv[c] = bi == pos ? v[pos][c] : hv[c];
+    }
+    const float4 b4 = make_float4(best[0], best[1], best[2], best[3]);
+    *(float4*)(p1 + pp * P1S + g * CPG) = b4;
+    if (sp1) {
+      *(float4*)(sp1 + pp * FK + g * CPG) = b4;
+      *(float4*)(shv + pp * FK + g * CPG) = make_float4(hv[0], hv[1], hv[2], hv[3]);
     }
   }
 }
 
 // ---------------------------------------------------------------------------- block-2 conv
 // h2[p][k] = b2[k] + sum_{tap, c} p1[(oy + tr, ox + ts)][c] * W2[k][c][tap] / sigma2 for the wave's
-// row tiles rt0, rt0 + 8, ... (J of them, independent accumulators).  A fragment: lane row
-// r16 = pixel, k = 4 channels (ks & 7) * 4 + kq of tap ks >> 3; B: the lane's weight registers.
+// row tiles rt0, rt0 + 8, ... (J of them, independent accumulators).  Per (tap, 16-channel block)
+// lane (row r16 = pixel, kq) reads channels 4 kq .. 4 kq + 3 with one 16-byte LDS read and feeds
+// four MFMAs (MFMA t: k = 4 kq + t); B: the lane's weight registers in the same order.
+constexpr int NB2 = TAPS * 2;               // (tap, 16-channel block) steps of the block-2 forward
 template <int J>
-__device__ __forceinline__ void conv2_tiles(const F2Args& a, const float* p1, float* h2, const float (&bw)[KS2],
+__device__ __forceinline__ void conv2_tiles(const F2Args& a, const float* p1, float* h2, const float (&bw)[NB2 * 4],
                                             int rt0) {
   const int lane = threadIdx.x & 63, r16 = lane & 15, kq = lane >> 4;
   const int NO2 = a.Ho2 * a.Wo2;
@@ -140,16 +186,25 @@ __device__ __forceinline__ void conv2_tiles(const F2Args& a, const float* p1, fl
   for (int j = 0; j < J; ++j) {
     const int p = min((rt0 + j * NW) * 16 + r16, NO2 - 1);
     const int oy = p / a.Wo2, ox = p - oy * a.Wo2;
-    base[j] = (oy * a.Wp + ox) * P1S + kq;
+    base[j] = (oy * a.Wp + ox) * P1S + kq * 4;
     acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 #pragma unroll
-  for (int ks = 0; ks < KS2; ++ks) {
-    const int tap = ks >> 3;
-    const int off = ((tap / 3) * a.Wp + tap % 3) * P1S + (ks & 7) * 4;
+  for (int blk = 0; blk < NB2; ++blk) {
+    const int tap = blk >> 1;
+    const int off = ((tap / 3) * a.Wp + tap % 3) * P1S + (blk & 1) * 16;
+    float4 av[J];
 #pragma unroll
-    for (int j = 0; j < J; ++j)
-      acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(p1[base[j] + off], bw[ks], acc[j], 0, 0, 0);
+    for (int j = 0; j < J; ++j) av[j] = *(const float4*)(p1 + base[j] + off);
+    // tiles innermost: consecutive MFMAs write different accumulators (no dependent issue)
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j].x, bw[blk * 4 + 0], acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j].y, bw[blk * 4 + 1], acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j].z, bw[blk * 4 + 2], acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j].w, bw[blk * 4 + 3], acc[j], 0, 0, 0);
   }
   // D layout: lane holds rows kq*4 + i, column r16
   const float bias = a.p.b2 ? a.p.b2[r16] : 0.f;
@@ -165,12 +220,14 @@ __device__ __forceinline__ void conv2_tiles(const F2Args& a, const float* p1, fl
 __device__ __forceinline__ void block2_conv(const F2Args& a, const float* p1, float* h2) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const float inv = a.p.sigma2 ? 1.f / a.p.sigma2[0] : 1.f;   // as es_pack_conv_weight
-  float bw[KS2];
+  float bw[NB2 * 4];
 #pragma unroll
-  for (int ks = 0; ks < KS2; ++ks) {
-    const int tap = ks >> 3, ch = (ks & 7) * 4 + (lane >> 4);
-    bw[ks] = a.p.w2[((lane & 15) * FK + ch) * TAPS + tap] * inv;
-  }
+  for (int blk = 0; blk < NB2; ++blk)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int tap = blk >> 1, ch = (blk & 1) * 16 + (lane >> 4) * 4 + t;
+      bw[blk * 4 + t] = a.p.w2[((lane & 15) * FK + ch) * TAPS + tap] * inv;
+    }
   const int NT = (a.Ho2 * a.Wo2 + 15) >> 4;                    // <= 24 (host check)
   const int nj = wid < NT ? (NT - wid + NW - 1) / NW : 0;        // wave-uniform
   if (nj >= 3) conv2_tiles<3>(a, p1, h2, bw, wid);
@@ -235,22 +292,32 @@ __device__ __forceinline__ float block2_window(const F2Args& a, const float* h2,
 
 __global__ void __launch_bounds__(FT) dfront2_fwd_kernel(F2Args a) {
   __shared__ float im[MAXPIX];
-  __shared__ float p1[MAXP1 * P1S];
+  __shared__ __attribute__((aligned(16))) float p1[MAXP1 * P1S];
   __shared__ float h2[MAXH2 * H2S];
-  __shared__ float red[NW * 16];
+  __shared__ float red[NW * 24];
   __shared__ float st[4 * FG];                // GN1 mean, invstd, GN2 mean, invstd
   const int n = blockIdx.x, g = threadIdx.x & 7, u = threadIdx.x >> 3;
+  const int NP1 = a.Hp * a.Wp, NO2 = a.Ho2 * a.Wo2;
+  float* sv = a.save ? a.save + (int64_t)n * a.sv : nullptr;
   Quad q;
   load_quad_p(a.p.w1, a.p.sigma1, a.p.b1, a.p.g1, a.p.be1, g, q);
   stage_image_p(a.img, a.is, a.H, a.W, n, im);
   __syncthreads();
   float mu1, is1;
+  PROBE(a, 10);
   block1_stats(a, im, q, u, red, mu1, is1);
   if (threadIdx.x < 8) { st[g] = mu1; st[FG + g] = is1; }
-  block1_out(a, im, q, g, u, mu1, is1, p1);
+  PROBE(a, 11);
+  block1_out(a, im, q, g, u, mu1, is1, p1, sv, sv ? sv + NP1 * FK : nullptr);
   __syncthreads();
+  PROBE(a, 12);
   block2_conv(a, p1, h2);
   __syncthreads();
+  PROBE(a, 13);
+  if (sv) {
+    float* sh2 = sv + 2 * NP1 * FK;
+    for (int i = threadIdx.x; i < NO2 * K2; i += FT) sh2[i] = h2[(i >> 4) * H2S + (i & 15)];
+  }
   float mu2, is2;
   block2_stats(a, h2, red, mu2, is2);
   if (threadIdx.x < 16 && (threadIdx.x & 1) == 0) {
@@ -269,6 +336,7 @@ __global__ void __launch_bounds__(FT) dfront2_fwd_kernel(F2Args a) {
     out[f] = block2_window(a, h2, c, y, x, st[2 * FG + gg], st[3 * FG + gg], a.p.g2 ? a.p.g2[c] : 1.f,
                            a.p.be2 ? a.p.be2[c] : 0.f, bp, bh, ba);
   }
+  PROBE(a, 14);
 }
 
 // ---------------------------------------------------------------------------- backward pieces
@@ -305,17 +373,18 @@ __device__ __forceinline__ void wgrad2_tiles(const F2Args& a, const float* p1, c
 }
 
 // dp1[q][c] = sum_{tap, k} dh2[(iy - tr, ix - ts)][k] * W2[k][c][tap] / sigma2 (0 outside the
-// conv-2 map).  Row tiles of pooled block-1 pixels, two at a time, both 16-channel column tiles.
+// conv-2 map).  Row tiles of pooled block-1 pixels, two at a time, both 16-channel column tiles;
+// per tap one 16-byte read of the lane's 4 channels (k = 4 kq + t) feeds 8 MFMAs.
 __device__ __forceinline__ void dgrad2(const F2Args& a, const float* dh2, float* dp1) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, r16 = lane & 15, kq = lane >> 4;
   const float inv = a.p.sigma2 ? 1.f / a.p.sigma2[0] : 1.f;
-  float bd[KSD][2];
+  float bd[TAPS][4][2];
 #pragma unroll
-  for (int ks = 0; ks < KSD; ++ks) {
-    const int tap = ks >> 2, k = (ks & 3) * 4 + kq;
+  for (int tap = 0; tap < TAPS; ++tap)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) bd[ks][j] = a.p.w2[(k * FK + j * 16 + r16) * TAPS + tap] * inv;
-  }
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bd[tap][t][j] = a.p.w2[((kq * 4 + t) * FK + j * 16 + r16) * TAPS + tap] * inv;
   const int NP1 = a.Hp * a.Wp, NT1 = (NP1 + 15) >> 4;
   for (int rt0 = wid; rt0 < NT1; rt0 += 2 * NW) {   // tiles rt0 and rt0 + 8 (if any)
     const bool two = rt0 + NW < NT1;                 // wave-uniform
@@ -329,17 +398,26 @@ __device__ __forceinline__ void dgrad2(const F2Args& a, const float* dh2, float*
       acc[m][0] = acc[m][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
-    for (int ks = 0; ks < KSD; ++ks) {
-      const int tap = ks >> 2, tr = tap / 3, ts = tap % 3, k = (ks & 3) * 4 + kq;
+    for (int tap = 0; tap < TAPS; ++tap) {
+      const int tr = tap / 3, ts = tap % 3;
+      float4 av[2];
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
-        if (m == 1 && !two) break;
         const int oy = iy[m] - tr, ox = ix[m] - ts;
         const bool ok = (unsigned)oy < (unsigned)a.Ho2 && (unsigned)ox < (unsigned)a.Wo2;
-        const float av = dh2[(ok ? oy * a.Wo2 + ox : 0) * H2S + k];
-        const float am = ok ? av : 0.f;
-        acc[m][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(am, bd[ks][0], acc[m][0], 0, 0, 0);
-        acc[m][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(am, bd[ks][1], acc[m][1], 0, 0, 0);
+        const float4 v = *(const float4*)(dh2 + (ok ? oy * a.Wo2 + ox : 0) * H2S + kq * 4);
+        av[m] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      const float e0[4] = {av[0].x, av[0].y, av[0].z, av[0].w};
+      const float e1[4] = {av[1].x, av[1].y, av[1].z, av[1].w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(e0[t], bd[tap][t][0], acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(e0[t], bd[tap][t][1], acc[0][1], 0, 0, 0);
+        if (two) {
+          acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(e1[t], bd[tap][t][0], acc[1][0], 0, 0, 0);
+          acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(e1[t], bd[tap][t][1], acc[1][1], 0, 0, 0);
+        }
       }
     }
 #pragma unroll
@@ -360,9 +438,9 @@ __device__ __forceinline__ void dgrad2(const F2Args& a, const float* dh2, float*
 template <bool WDX, bool WW>
 __global__ void __launch_bounds__(FT) dfront2_bwd_kernel(F2Args a) {
   __shared__ float im[MAXPIX];
-  __shared__ float p1[MAXP1 * P1S];           // block-1 output, then its gradient
-  __shared__ float R[RFL];                    // h2 (then dh2) | dn; later e_rs planes / scratch
-  __shared__ float red[NW * 16];
+  __shared__ __attribute__((aligned(16))) float p1[MAXP1 * P1S];   // block-1 output, then its gradient
+  __shared__ __attribute__((aligned(16))) float R[RFL];            // h2 (then dh2) | dn; later e_rs / scratch
+  __shared__ float red[NW * 24];
   __shared__ float kk[2 * G2];                // GN2 backward: mean(dn), mean(dn * xhat) per group
   float* h2 = R;
   float* dn = R + MAXH2 * H2S;
@@ -375,12 +453,18 @@ __global__ void __launch_bounds__(FT) dfront2_bwd_kernel(F2Args a) {
   const float* st = a.stats + (int64_t)n * 4 * FG;
   const float mu1 = st[g], is1 = st[FG + g];
   for (int i = threadIdx.x; i < MAXH2 * H2S; i += FT) dn[i] = 0.f;
+  // the forward's save: pooled block-1 map -> p1, block-2 conv map -> h2
+  const int NP1 = a.Hp * a.Wp, NO2 = a.Ho2 * a.Wo2;
+  const float* sv = a.save + (int64_t)n * a.sv;
+  const float* shv = sv + NP1 * FK;
+  PROBE(a, 0);
+  for (int i = threadIdx.x; i < NP1 * (FK / 4); i += FT)
+    *(float4*)(p1 + (i >> 3) * P1S + (i & 7) * 4) = ((const float4*)sv)[i];
+  for (int i = threadIdx.x; i < NO2 * (K2 / 4); i += FT)
+    *(float4*)(h2 + (i >> 2) * H2S + (i & 3) * 4) = ((const float4*)(sv + 2 * NP1 * FK))[i];
   __syncthreads();
-  block1_out(a, im, q, g, u, mu1, is1, p1);
-  __syncthreads();
-  block2_conv(a, p1, h2);
-  __syncthreads();
-  const int NO2 = a.Ho2 * a.Wo2;
+  PROBE(a, 1);
+  PROBE(a, 2);
   const float cnt2 = 2.f * NO2;
 
   // (1) pool-2 routing and the GN2 backward sums.  Thread t: channel c = t >> 5 (wave w holds the
@@ -445,6 +529,7 @@ __global__ void __launch_bounds__(FT) dfront2_bwd_kernel(F2Args a) {
     for (int w = 0; w < NW; ++w) t += red[w * 16 + threadIdx.x];
     part[O_DB2 + threadIdx.x] = t;
   }
+  PROBE(a, 3);
   // (3) block-2 weight gradient (18 column tiles over 8 waves)
   if (WW) {
     const int nj = (18 - wid + NW - 1) / NW;
@@ -452,9 +537,11 @@ __global__ void __launch_bounds__(FT) dfront2_bwd_kernel(F2Args a) {
     else wgrad2_tiles<2>(a, p1, h2, part);
   }
   __syncthreads();                            // p1 read by the wgrad before the dgrad overwrites it
+  PROBE(a, 4);
   // (4) block-2 input gradient into p1's slots
   dgrad2(a, h2, p1);
   __syncthreads();
+  PROBE(a, 5);
 
   // (5) block-1 backward (dfront_bwd_kernel's passes, dpooled from LDS, argmax recomputed)
   const int NP = a.Hp * a.Wp;
@@ -463,17 +550,11 @@ __global__ void __launch_bounds__(FT) dfront2_bwd_kernel(F2Args a) {
 #pragma unroll
   for (int i = 0; i < 2 + 2 * CPG; ++i) r[i] = 0.f;
   for (int pp = u; pp < NP; pp += FT / 8) {
-    const int pi = pp / a.Wp, pj = pp - pi * a.Wp;
-    float x[4][4], v[4][CPG];
-    window(im, a.W, pi, pj, q, x, v);
+    const float4 h4 = *(const float4*)(shv + pp * FK + g * CPG);   // conv values at the argmaxes
+    const float hvs[CPG] = {h4.x, h4.y, h4.z, h4.w};
 #pragma unroll
     for (int c = 0; c < CPG; ++c) {
-      float best;
-      const int bi = block1_argmax(v, c, q, mu1, is1, a.p.slope, best);
-      float hv = v[0][c];
-#pragma unroll
-      for (int pos = 1; pos < 4; ++pos) hv = bi == pos ? v[pos][c] : hv;
-      const float xh = (hv - mu1) * is1;
+      const float xh = (hvs[c] - mu1) * is1;
       const float av = fmaf(xh, q.gm[c], q.bt[c]);
       const float dvc = p1[pp * P1S + g * CPG + c];
       const float da = av > 0.f ? dvc : dvc * a.p.slope;
@@ -494,6 +575,7 @@ __global__ void __launch_bounds__(FT) dfront2_bwd_kernel(F2Args a) {
   }
   const float k1 = r[0] / cnt1, k2 = r[1] / cnt1;
   __syncthreads();                            // R's reduction scratch read by every thread
+  PROBE(a, 6);
   float acc[CPG * TAPS + CPG];
 #pragma unroll
   for (int i = 0; i < CPG * TAPS + CPG; ++i) acc[i] = 0.f;
@@ -531,26 +613,43 @@ __global__ void __launch_bounds__(FT) dfront2_bwd_kernel(F2Args a) {
       }
     }
     if constexpr (WDX) {
+      // sum the 36 values over the window's 8 lanes as a reduce-scatter (halving rounds over lane
+      // bits 2, 1, 0: 20 + 10 + 5 shuffles instead of 3 x 36); lane g ends with values g*5 .. g*5+4
+      // of the 40 (36 padded)
+      float e40[40];
 #pragma unroll
-      for (int pos = 0; pos < 4; ++pos)
+      for (int i = 0; i < 40; ++i) e40[i] = i < 4 * TAPS ? e[i / TAPS][i % TAPS] : 0.f;
+      const bool b2 = g & 4, b1 = g & 2, b0 = g & 1;
+      float h20[20], h10[10], h5[5];
 #pragma unroll
-        for (int t = 0; t < TAPS; ++t) {
-          float s = e[pos][t];
-          s += __shfl_xor(s, 1, 64);
-          s += __shfl_xor(s, 2, 64);
-          s += __shfl_xor(s, 4, 64);
-          e[pos][t] = s;
-        }
+      for (int i = 0; i < 20; ++i) {
+        const float send = b2 ? e40[i] : e40[i + 20], keep = b2 ? e40[i + 20] : e40[i];
+        h20[i] = keep + __shfl_xor(send, 4, 64);
+      }
 #pragma unroll
-      for (int i = 0; i < 4 * TAPS; ++i) {
-        const int pos = i / TAPS, t = i % TAPS;
-        if ((i & 7) == g) {
+      for (int i = 0; i < 10; ++i) {
+        const float send = b1 ? h20[i] : h20[i + 10], keep = b1 ? h20[i + 10] : h20[i];
+        h10[i] = keep + __shfl_xor(send, 2, 64);
+      }
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        const float send = b0 ? h10[i] : h10[i + 5], keep = b0 ? h10[i + 5] : h10[i];
+        h5[i] = keep + __shfl_xor(send, 1, 64);
+      }
+      // lane g holds the sums of entries 20*b2 + 10*b1 + 5*b0 + i
+      const int i0 = (b2 ? 20 : 0) + (b1 ? 10 : 0) + (b0 ? 5 : 0);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        const int idx = i0 + i;
+        if (idx < 4 * TAPS) {
+          const int pos = idx / TAPS, t = idx - pos * TAPS;
           const int o = (2 * pi + (pos >> 1)) * a.Wo + 2 * pj + (pos & 1);
-          R[t * MAXOUT + o] = e[pos][t];
+          R[t * MAXOUT + o] = h5[i];
         }
       }
     }
   }
+  PROBE(a, 7);
   if constexpr (WDX) {
     __syncthreads();
     float* dx = a.dx + n * a.dxs[0];
@@ -576,6 +675,7 @@ __global__ void __launch_bounds__(FT) dfront2_bwd_kernel(F2Args a) {
       }
     }
   }
+  PROBE(a, 8);
 }
 
 // Sum the per-image partials over the images: dw1 / dw2 WRITTEN, the rest ACCUMULATED (+=); any
@@ -620,10 +720,15 @@ int f2_args(F2Args& a, const float* img, const int64_t is[4], int N, int H, int 
   a.Ho2 = a.Hp - 2; a.Wo2 = a.Wp - 2;
   a.Hq = (a.Ho2 - p->ph) / p->ph + 1; a.Wq = (a.Wo2 - p->pw) / p->pw + 1;
   a.p = *p;
+  a.sv = es_dfront2_save_floats(H, W, p->ph, p->pw);
+  a.probe = g_probe;
   return ES_OK;
 }
 
 }  // namespace
+
+// debug hook (ES_DF2_PROBE builds only record): device buffer of >= 16 int64 phase timestamps
+extern "C" void es_dfront2_set_probe(long long* p) { g_probe = p; }
 
 extern "C" int es_dfront2_ok(int H, int W, int ph, int pw) {
   if (ph < 1 || pw < 1 || H < 8 || W < 8) return 0;
@@ -637,24 +742,31 @@ extern "C" int es_dfront2_ok(int H, int W, int ph, int pw) {
 
 extern "C" int64_t es_dfront2_part_floats(int N) { return (int64_t)N * NPART2; }
 
+extern "C" int64_t es_dfront2_save_floats(int H, int W, int ph, int pw) {
+  if (!es_dfront2_ok(H, W, ph, pw)) return 0;
+  const int Hp = (H - 2) / 2, Wp = (W - 2) / 2;
+  return (int64_t)2 * Hp * Wp * FK + (int64_t)(Hp - 2) * (Wp - 2) * K2;
+}
+
 extern "C" int es_dfront2_fwd(const float* img, const int64_t is[4], int N, int H, int W, const es_dfront2_params_t* p,
-                              float* stats, float* feat, int64_t feat_stride, es_stream_t stream) {
+                              float* stats, float* feat, int64_t feat_stride, float* save, es_stream_t stream) {
   F2Args a;
   if (int rc = f2_args(a, img, is, N, H, W, p)) return rc;
   ES_CHECK_ARG(stats && feat && feat_stride >= (int64_t)K2 * a.Hq * a.Wq, "es_dfront2_fwd: outputs");
-  a.stats = stats; a.feat = feat; a.fs = feat_stride;
+  a.stats = stats; a.feat = feat; a.fs = feat_stride; a.save = save;
   hipLaunchKernelGGL(dfront2_fwd_kernel, dim3(N), dim3(FT), 0, (hipStream_t)stream, a);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
 
 extern "C" int es_dfront2_bwd(const float* img, const int64_t is[4], int N, int H, int W, const es_dfront2_params_t* p,
-                              const float* stats, const float* dfeat, int64_t dfeat_stride, float* dx,
+                              const float* stats, const float* save, const float* dfeat, int64_t dfeat_stride, float* dx,
                               const int64_t dxs[4], float* part, float* dw1, float* db1, float* dg1, float* dbe1,
                               float* dw2, float* db2, float* dg2, float* dbe2, es_stream_t stream) {
   F2Args a;
   if (int rc = f2_args(a, img, is, N, H, W, p)) return rc;
-  ES_CHECK_ARG(stats && dfeat && dfeat_stride >= (int64_t)K2 * a.Hq * a.Wq, "es_dfront2_bwd: inputs");
+  ES_CHECK_ARG(stats && save && dfeat && dfeat_stride >= (int64_t)K2 * a.Hq * a.Wq, "es_dfront2_bwd: inputs");
+  a.save = (float*)save;
   ES_CHECK_ARG(!dx || dxs, "es_dfront2_bwd: dx without strides");
   ES_CHECK_ARG(dx || part, "es_dfront2_bwd: nothing to compute (no dx, no part)");
   a.stats = (float*)stats; a.dfeat = dfeat; a.dfs = dfeat_stride; a.dx = dx; a.part = part;

@@ -103,9 +103,11 @@ _SIGS = {
                                 P, P, P, P, P, P, P, P]),
     "es_dfront2_ok": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int]),
     "es_dfront2_part_floats": (I64, [C.c_int]),
-    "es_dfront2_fwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, P, P, I64, P]),
-    "es_dfront2_bwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, P, P, I64, P, P, P, P, P, P, P, P, P, P,
+    "es_dfront2_save_floats": (I64, [C.c_int, C.c_int, C.c_int, C.c_int]),
+    "es_dfront2_fwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, P, P, I64, P, P]),
+    "es_dfront2_bwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, P, P, P, I64, P, P, P, P, P, P, P, P, P, P,
                                  P, P]),
+    "es_dfront2_set_probe": (None, [P]),
     "es_upsample_bwd": (C.c_int, [P, C.c_int, P, P, P, P, P, P, C.c_int, P, C.c_float, P]),
     "es_copy": (C.c_int, [P, C.c_int, P, P, C.c_int, P, C.c_float, C.c_float, P]),
     "es_avgpool_fwd": (C.c_int, [P, C.c_int, P, P, P, P]),

@@ -106,6 +106,7 @@ class SNDiscriminator(ExpertModule):
         gradient (fp32 Act) or None.  Weight gradients: W/sigma grads into the spectral-norm jobs,
         biases and GroupNorm affines accumulated."""
         x = ctx["x"]
+        assert ctx["fsave"] is not None, "discriminator forward ran with grad_ctx=False"
         B, _, H, W = x.dims
         dev = x.t.device
         m = lambda n: get_module(self, n)
@@ -120,7 +121,7 @@ class SNDiscriminator(ExpertModule):
                      g4, m("conv_layers.4").bias.grad, m("conv_layers.5").weight.grad, m("conv_layers.5").bias.grad]
         F = self.flat_dim + self.cond_dim
         hip.call("es_dfront2_bwd", x.ptr, hip.strides4(x.strides), B, H, W, C.byref(ctx["front2"]),
-                 hip.ptr(ctx["fstats"]), dX.ptr, F, dx.ptr if dx is not None else None,
+                 hip.ptr(ctx["fstats"]), hip.ptr(ctx["fsave"]), dX.ptr, F, dx.ptr if dx is not None else None,
                  hip.strides4(dx.strides) if dx is not None else None, hip.ptr(part),
                  *[hip.ptr(t) for t in grads], hip.stream_ptr())
         if weight_grads:
@@ -169,8 +170,9 @@ class SNDiscriminator(ExpertModule):
         return dx
 
     # --------------------------------------------------------------------------- forward
-    def fwd(self, img: Act, cond: torch.Tensor, train=True):
-        """img Act [B,1,H,W] (any dtype), cond [B,9] fp32 -> (out [B,1] fp32, latent [B,64] fp32, ctx)."""
+    def fwd(self, img: Act, cond: torch.Tensor, train=True, grad_ctx=True):
+        """img Act [B,1,H,W] (any dtype), cond [B,9] fp32 -> (out [B,1] fp32, latent [B,64] fp32, ctx).
+        grad_ctx=False: no backward will follow (the fused front then saves no activations)."""
         o = self.ops()
         cdt = self.compute_dtype
         dev = cond.device
@@ -188,13 +190,16 @@ class SNDiscriminator(ExpertModule):
             # both conv blocks in one kernel: features straight into the fc1 input rows
             params = self._front2_params(sig)
             fstats = torch.empty(B * 32, dtype=torch.float32, device=dev)
+            # activations the backward reads (pooled block-1 map, argmax conv values, block-2 map)
+            nsave = hip.lib().es_dfront2_save_floats(x.dims[2], x.dims[3], *self.pool2)
+            fsave = torch.empty(B * nsave, dtype=torch.float32, device=dev) if grad_ctx else None
             X = Act.rows(B, F, cdt, dev)
             Xm = X.t.view(B, F)
             hip.call("es_dfront2_fwd", x.ptr, hip.strides4(x.strides), B, x.dims[2], x.dims[3], C.byref(params),
-                     hip.ptr(fstats), X.ptr, F, hip.stream_ptr())
+                     hip.ptr(fstats), X.ptr, F, hip.ptr(fsave), hip.stream_ptr())
             copy_act(Act.of(cond), Act.of(Xm[:, self.flat_dim:]))
             return self._fc_fwd(X, B, cdt, dev, sig, dict(x=x, sig=sig, front=True, front2=params, fstats=fstats,
-                                                          X=X))
+                                                          fsave=fsave, X=X))
         if front:
             p1, i1, s1 = self.front_fwd(x, inv("conv_layers.0"))
             if p1.t.dtype != cdt:                   # bf16 mode: the GEMM layers after the front

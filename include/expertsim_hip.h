@@ -282,16 +282,20 @@ typedef struct {
 int es_dfront2_ok(int H, int W, int ph, int pw);
 /* Forward.  img fp32 [N][1][H][W] (strides is).  Writes feat[n*feat_stride + f], f < 16*Hq*Wq
  * (the reference's view(B, -1) order) and stats [N][32] = GN1 mean[8], invstd[8], GN2 mean[8],
- * invstd[8] (read back by the backward). */
+ * invstd[8].  save (optional; required by the backward): [N][es_dfront2_save_floats] floats of
+ * per-image activations the backward reads instead of recomputing them. */
+int64_t es_dfront2_save_floats(int H, int W, int ph, int pw);
 int es_dfront2_fwd(const float* img, const int64_t is[4], int N, int H, int W, const es_dfront2_params_t* p,
-                   float* stats, float* feat, int64_t feat_stride, es_stream_t stream);
-/* Backward from dfeat (the gradient of the features, same indexing as feat).  dx (optional): fp32
- * image gradient [N][1][H][W] (strides dxs), written.  part (optional, es_dfront2_part_floats(N)
- * floats): per-image weight-gradient partials; when given, dw1 / dw2 (gradients of W/sigma, torch
- * layouts) are written and db*, dg*, dbe* (biases, GN affines) accumulated; each may be NULL. */
+                   float* stats, float* feat, int64_t feat_stride, float* save, es_stream_t stream);
+/* Backward from dfeat (the gradient of the features, same indexing as feat), with the forward's
+ * stats and save.  dx (optional): fp32 image gradient [N][1][H][W] (strides dxs), written.  part
+ * (optional, es_dfront2_part_floats(N) floats): per-image weight-gradient partials; when given,
+ * dw1 / dw2 (gradients of W/sigma, torch layouts) are written and db*, dg*, dbe* (biases, GN
+ * affines) accumulated; each may be NULL. */
 int64_t es_dfront2_part_floats(int N);
 int es_dfront2_bwd(const float* img, const int64_t is[4], int N, int H, int W, const es_dfront2_params_t* p,
-                   const float* stats, const float* dfeat, int64_t dfeat_stride, float* dx, const int64_t dxs[4],
+                   const float* stats, const float* save, const float* dfeat, int64_t dfeat_stride, float* dx,
+                   const int64_t dxs[4],
                    float* part, float* dw1, float* db1, float* dg1, float* dbe1, float* dw2, float* db2,
                    float* dg2, float* dbe2, es_stream_t stream);
 /* dx[n,c,h,w] = beta*dx + sum over upsampled positions mapping to (h,w).  hstart/hcount (device

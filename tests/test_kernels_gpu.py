@@ -572,9 +572,19 @@ def test_dfront2_fused(N, H, W, pool):
     xd = x.to(DEV)
     X = torch.full((N, Fs), 7.0, device=DEV)
     stats = torch.empty(N * 32, device=DEV)
+    save = torch.empty(N * hip.lib().es_dfront2_save_floats(H, W, *pool), device=DEV)
     hip.call("es_dfront2_fwd", hip.ptr(xd), hip.strides4(xd.stride()), N, H, W, C.byref(prm), hip.ptr(stats),
-             hip.ptr(X), Fs, hip.stream_ptr())
+             hip.ptr(X), Fs, hip.ptr(save), hip.stream_ptr())
     assert rel(X[:, :nf].cpu(), feat.detach()) < 1e-5
+    X2 = torch.full((N, Fs), 7.0, device=DEV)      # inference form (no save): same features
+    hip.call("es_dfront2_fwd", hip.ptr(xd), hip.strides4(xd.stride()), N, H, W, C.byref(prm), hip.ptr(stats),
+             hip.ptr(X2), Fs, None, hip.stream_ptr())
+    assert torch.equal(X, X2)
+    # the save: pooled block-1 map, block-2 conv map
+    sv = save.cpu().view(N, -1)
+    np1 = p.shape[2] * p.shape[3]
+    assert rel(sv[:, :np1 * 32].view(N, p.shape[2], p.shape[3], 32).permute(0, 3, 1, 2), p.detach()) < 1e-5
+    assert rel(sv[:, 2 * np1 * 32:].view(N, h2.shape[2], h2.shape[3], 16).permute(0, 3, 1, 2), h2.detach()) < 1e-5
     assert torch.all(X[:, nf:] == 7.0)           # the cond columns are left alone
     st = stats.cpu().view(N, 4, 8)
     hg, h2g = h.detach().view(N, 8, -1), h2.detach().view(N, 8, -1)
@@ -594,7 +604,7 @@ def test_dfront2_fused(N, H, W, pool):
                 torch.empty(16 * 32 * 9, device=DEV), torch.full((16,), 0.5, device=DEV),
                 torch.full((16,), 0.5, device=DEV), torch.full((16,), 0.5, device=DEV)]
         hip.call("es_dfront2_bwd", hip.ptr(xd), hip.strides4(xd.stride()), N, H, W, C.byref(prm), hip.ptr(stats),
-                 hip.ptr(dX), Fs, hip.ptr(dx), hip.strides4(dx.stride()) if dx is not None else None,
+                 hip.ptr(save), hip.ptr(dX), Fs, hip.ptr(dx), hip.strides4(dx.stride()) if dx is not None else None,
                  hip.ptr(part), *[hip.ptr(o) if want_w else None for o in outs], hip.stream_ptr())
         if want_dx:
             assert rel(dx.cpu(), xr.grad) < 1e-4, (want_dx, want_w)
