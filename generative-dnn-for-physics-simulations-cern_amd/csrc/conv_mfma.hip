@@ -153,6 +153,7 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* img, int k0, int r0) {
 // wait insertion and ring_loop orders them itself (lgkmcnt + an operand fence before the MFMAs).
 typedef int int2v __attribute__((ext_vector_type(2)));
 typedef int int4v __attribute__((ext_vector_type(4)));
+typedef unsigned int v4u32_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint32_t lds_u32(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
@@ -734,6 +735,335 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// PERSISTENT short-K FWD / DGRAD: the generator's conv_layers.9 (neutron/generator.py:33, 2x2 taps
+// x 128 channels -> 64: FWD 8 K-steps of 64 channels, 64 output columns) and its DGRAD (4 K-steps,
+// 128 output columns); stride 1, no upsample, no sub-pixel packing.  With so few K-steps the ring
+// kernel's per-tile pipeline fill and epilogue dominate: one 128 x 64 tile's 8 steps took ~11 us
+// for ~1 us of MFMA work (0.30 of the HBM roofline at B = 1024).  Here
+//   * one workgroup per CU loops over its tiles; the whole packed weight panel (nk K-steps x BN
+//     rows x 128 B <= 64 KiB) is DMA'd into LDS once;
+//   * the A ring runs over the workgroup's (tile, K-step) sequence without draining between tiles:
+//     the next tile's first steps are in flight while the current tile's epilogue stores;
+//   * the epilogue stages each wave's sub-tile in a private LDS region through inline-asm LDS
+//     accesses (invisible to hipcc's wait insertion, ordered by explicit lgkmcnt waits) and stores
+//     16-byte rows with buffer stores (invalid rows: out-of-range offsets, dropped), so every wave
+//     issues a FIXED number of vector-memory ops per tile and the counted vmcnt waits stay exact
+//     (vmcnt retires in issue order across loads, stores and LDS-DMA);
+//   * FWD BatchNorm partials are Chan-merged per lane over the workgroup's tiles and written once
+//     per workgroup at the end (chunks = workgroups instead of row tiles).
+// Tile rows in the ring kernel's image-minor order (NG images x NB = BM / NG pixels per tile).  The
+// tiles are split into 8 contiguous ranges, one per XCD, so the concurrently running tiles of one
+// XCD are neighbouring pixels of the same images (shared input rows in its L2).
+__device__ __forceinline__ void ds_write_u16(uint32_t addr, uint32_t v) {
+  asm volatile("ds_write_b16 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+__device__ __forceinline__ int4v ds_read_b128_asm(uint32_t addr) {
+  int4v r;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr) : "memory");
+  return r;
+}
+
+template <int MODE, int BN>
+__global__ void __launch_bounds__(RT) conv_persist_kernel(ConvArgs a, int ntiles) {
+  constexpr int BM = 128, BK = 64, WGM = 4, WGN = 2;
+  constexpr int WM = BM / WGM, WN = BN / WGN;              // 32 x 32 (BN 64) / 32 x 64 (BN 128)
+  constexpr int RM = WM / 16, RN = WN / 16;
+  constexpr int ROWB = 2 * BK, PROWS = 1024 / ROWB, CPR = ROWB / 16;
+  constexpr int APW = BM / PROWS / 8;                      // A pieces per wave per K-step
+  constexpr int ABYTES = BM * ROWB;
+  constexpr int NS = BN <= 64 ? 4 : 3;                     // ring slots (NS - 1 steps in flight)
+  constexpr int PANEL = 65536;
+  constexpr int SPITCH = WN * 2 + 16, STAGE = WM * SPITCH; // per-wave bf16 staging
+  constexpr int OCPR = WN * 2 / 16, ORPI = 64 / OCPR, NST = WM / ORPI;   // 16-byte stores per tile
+  constexpr int STB = 3 * WGM * BN * 4;
+  __shared__ __attribute__((aligned(16))) char smem[PANEL + NS * ABYTES + 8 * STAGE + STB];
+  char* const panel = smem;
+  char* const ring = smem + PANEL;
+  const es_conv_desc_t& d = a.d;
+  const int nch = MODE == MODE_FWD ? d.C : d.K;
+  const int cpt = nch / BK, nk = a.Kd / BK;
+  const int lane = threadIdx.x & 63, wid = uni(threadIdx.x >> 6);
+  const int wm0 = (wid / WGN) * WM, wn0 = (wid % WGN) * WN;
+  const int lrow = lane / CPR, pc = lane % CPR;
+  const uint32_t stg = lds_u32(ring + NS * ABYTES + wid * STAGE);
+  float* const stb = (float*)(ring + NS * ABYTES + 8 * STAGE);
+  const int NG = a.ng, PPG = NG / PROWS, NB = BM / NG;
+  const int gh = MODE == MODE_FWD ? d.P : d.H, gw = MODE == MODE_FWD ? d.Q : d.W;
+  const int PQ = gh * gw, TT = (PQ + NB - 1) / NB;
+  const int lgNG = uni(31 - __builtin_clz(NG));
+  FastDiv fgw;
+  {
+    uint32_t l2 = 0;
+    while ((1u << l2) < (uint32_t)gw) ++l2;
+    fgw.l = uni((int)l2);
+    fgw.m = (uint32_t)uni((int)(uint32_t)(((1ull << 32) * ((1ull << l2) - (uint32_t)gw)) / (uint32_t)gw + 1));
+  }
+  // this workgroup's tiles: XCD x = blockIdx % 8 owns tiles [x * T / 8, (x + 1) * T / 8); its
+  // workgroups (blockIdx / 8 = l of L) take every L-th tile of that range
+  const int xcd = blockIdx.x & 7, L = (gridDim.x - xcd + 7) >> 3, lw = blockIdx.x >> 3;
+  const int t_lo = (int)(((int64_t)ntiles * xcd) >> 3), t_hi = (int)(((int64_t)ntiles * (xcd + 1)) >> 3);
+  const int my = t_hi - t_lo > lw ? (t_hi - t_lo - lw + L - 1) / L : 0;
+  const int nsteps = my * nk;
+
+  const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * 2));
+  const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)(a.Ng * a.Kd * 2));
+  const __amdgpu_buffer_rsrc_t ores = mkres(a.out, (uint32_t)(d.N * a.os[0] * 2));
+  // the weight panel: K-step k occupies [BN rows][128 B] at panel + k * BN * 128 (ring B layout)
+  for (int pi = wid; pi < nk * (BN / PROWS); pi += 8) {
+    const int k = pi / (BN / PROWS), rb = pi - k * (BN / PROWS);
+    const int rr = rb * PROWS + lrow;
+    bdma16(bres, (uint32_t)((rr * a.Kd + k * BK) * 2 + ((pc ^ swz_x<BK>(rr)) * 16)), panel + k * BN * ROWB + rb * 1024);
+  }
+  wait_vmcnt<0>();
+
+  // issue cursor (tile iteration ii, K-step ik) and the issued tile's A pieces
+  const int as0b = (int)a.as[0] * 2, as2b = (int)a.as[2] * 2, as3b = (int)a.as[3] * 2;
+  uint32_t alane[APW];
+  int pc0[APW], pc1[APW];
+  bool pval[APW];
+  int ii = 0, ik = 0;
+  int icb = 0, ics = 0, icr = 0;   // issue K-step as (channel block, tap column, tap row): no divisions
+  auto issue = [&](char* slot) {
+    const bool live = ii < my;
+    if (ik == 0 && live) {
+      const int t = t_lo + lw + ii * L;
+      const int gi = t / TT, pix0 = (t - gi * TT) * NB;
+#pragma unroll
+      for (int j = 0; j < APW; ++j) {
+        const int pi = wid * APW + j, rr = pi * PROWS + lrow;
+        const int ppix = pi / PPG, pix = pix0 + ppix;
+        pval[j] = pix < PQ;
+        const int pp = pval[j] ? pix : 0;
+        const int y = fdiv(pp, fgw), x = pp - y * gw;
+        const int img = gi * NG + (pi - ppix * PPG) * PROWS + lrow;
+        alane[j] = (uint32_t)(img * as0b + ((pc ^ swz_x<BK>(rr)) * 16));   // images >= N: past num_records
+        pc0[j] = MODE == MODE_FWD ? y - d.pad : y + d.pad;
+        pc1[j] = MODE == MODE_FWD ? x - d.pad : x + d.pad;
+      }
+    }
+    const int cb = icb, cr = icr, cs = ics;
+#pragma unroll
+    for (int j = 0; j < APW; ++j) {
+      int hh, ww;
+      bool ok;
+      if constexpr (MODE == MODE_FWD) {
+        hh = pc0[j] + cr; ww = pc1[j] + cs;
+        ok = (unsigned)hh < (unsigned)d.H && (unsigned)ww < (unsigned)d.W;
+      } else {
+        hh = pc0[j] - cr; ww = pc1[j] - cs;
+        ok = (unsigned)hh < (unsigned)d.P && (unsigned)ww < (unsigned)d.Q;
+      }
+      ok = ok && live && pval[j];
+      const uint32_t u = ok ? (uint32_t)(hh * as2b + ww * as3b + cb * ROWB) : OOB;
+      bdma16(ares, alane[j] + u, slot + (wid * APW + j) * 1024);
+    }
+    if (++icb == cpt) {
+      icb = 0;
+      if (++ics == d.S) {
+        ics = 0;
+        ++icr;
+      }
+    }
+    if (++ik == nk) { ik = 0; ++ii; icb = ics = icr = 0; }
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float rn[RN], rmu[RN], rq2[RN];                 // running BatchNorm partial of the lane's columns
+#pragma unroll
+  for (int j = 0; j < RN; ++j) rn[j] = rmu[j] = rq2[j] = 0.f;
+  // bias of the lane's columns, loaded before the ring starts (a VGPR load inside the loop makes
+  // hipcc drain every DMA in flight with vmcnt(0) at its first use)
+  float bcol[RN];
+#pragma unroll
+  for (int j = 0; j < RN; ++j) bcol[j] = (MODE == MODE_FWD && a.bias) ? a.bias[wn0 + j * 16 + (lane & 15)] : 0.f;
+  const bool want_stats = MODE == MODE_FWD && a.stats_part != nullptr;
+  const int r16 = lane & 15, g16 = lane >> 4, col16 = lane & 15, rq = (lane >> 4) * 4;
+  struct Frag {
+    bf16x8 a[RM], b[RN];
+  };
+  auto load = [&](Frag& f, const char* slot, const char* bk, int kk) {
+    const int seg = kk * 4 + g16;
+#pragma unroll
+    for (int i = 0; i < RM; ++i) f.a[i] = *(const bf16x8*)(slot + swz<BK>(wm0 + i * 16 + r16, seg));
+#pragma unroll
+    for (int j = 0; j < RN; ++j) f.b[j] = *(const bf16x8*)(bk + swz<BK>(wn0 + j * 16 + r16, seg));
+  };
+  auto mma = [&](const Frag& f) {
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
+  };
+
+  // epilogue of tile iteration ci: bias, rounding, fused statistics, staged 16-byte stores
+  auto epilogue = [&](int ci) {
+    const int t = t_lo + lw + ci * L;
+    const int gi = t / TT, pix0 = (t - gi * TT) * NB;
+    auto row_pix = [&](int r) { return pix0 + ((wm0 + r) >> lgNG); };
+    auto row_img = [&](int r) { return gi * NG + ((wm0 + r) & (NG - 1)); };
+    auto row_ok = [&](int r) { return row_pix(r) < PQ && row_img(r) < d.N; };
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) acc[i][j][jj] = (float)(bf16)(acc[i][j][jj] + bcol[j]);
+    }
+    if (want_stats) {
+      // the lane's (up to RM*4) valid values of each column, merged into its running partial:
+      // no cross-lane traffic per tile (the lane groups and row waves are merged once, at the end)
+      bool okr[RM][4];
+      float nb = 0.f;
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          okr[i][jj] = row_ok(i * 16 + rq + jj);
+          nb += okr[i][jj] ? 1.f : 0.f;
+        }
+      if (nb > 0.f) {
+        const float rb = __builtin_amdgcn_rcpf(nb);
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          float sm = 0.f;
+#pragma unroll
+          for (int i = 0; i < RM; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) sm += okr[i][jj] ? acc[i][j][jj] : 0.f;
+          const float mb = sm * rb;
+          float qb = 0.f;
+#pragma unroll
+          for (int i = 0; i < RM; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              const float e = okr[i][jj] ? acc[i][j][jj] - mb : 0.f;
+              qb = fmaf(e, e, qb);
+            }
+          const float nt = rn[j] + nb, f = nb * __builtin_amdgcn_rcpf(nt), dl = mb - rmu[j];
+          rmu[j] = fmaf(dl, f, rmu[j]);
+          rq2[j] += qb + dl * dl * rn[j] * f;
+          rn[j] = nt;
+        }
+      }
+    }
+    // stage the wave's 32 x WN bf16 sub-tile (row pitch SPITCH), then 16-byte row stores
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          const bf16 v = (bf16)acc[i][j][jj];
+          ds_write_u16(stg + (i * 16 + rq + jj) * SPITCH + (j * 16 + col16) * 2, (uint32_t)__builtin_bit_cast(uint16_t, v));
+        }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int lr = lane / OCPR, lch = lane % OCPR;
+    int4v vals[NST];
+#pragma unroll
+    for (int p = 0; p < NST; ++p) vals[p] = ds_read_b128_asm(stg + (p * ORPI + lr) * SPITCH + lch * 16);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int p = 0; p < NST; ++p) {
+      const int r = p * ORPI + lr;
+      uint32_t voff = OOB;
+      if (row_ok(r)) {
+        const int pix = row_pix(r);
+        const int y = fdiv(pix, fgw), x = pix - y * gw;
+        const int64_t off = (int64_t)row_img(r) * a.os[0] + (int64_t)y * a.os[2] + (int64_t)x * a.os[3] + wn0 + lch * 8;
+        voff = (uint32_t)(off * 2);
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, vals[p]), ores, voff, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i) issue(ring + i * ABYTES);
+  int cur = 0, prv = NS - 1, ck = 0, ci = 0, last_epi = -1000;
+  for (int s = 0; s < nsteps; ++s) {
+    // step s landed: younger than its DMA are the NS - 2 later steps' pieces and, when an epilogue
+    // ran within the last NS - 1 iterations (after step s was issued), its NST stores
+    if (s - last_epi <= NS - 1) wait_vmcnt<(NS - 2) * APW + NST>();
+    else wait_vmcnt<(NS - 2) * APW>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of step s - 1 are done
+    ring_barrier();
+    issue(ring + prv * ABYTES);                          // step s + NS - 1 into step s - 1's slot
+    const char* slot = ring + cur * ABYTES;
+    const char* bk = panel + ck * BN * ROWB;
+    Frag f;
+    load(f, slot, bk, 0);
+    mma(f);
+    load(f, slot, bk, 1);
+    mma(f);
+    if (++ck == nk) {
+      epilogue(ci);
+      ck = 0;
+      ++ci;
+      last_epi = s;
+    }
+    prv = cur;
+    cur = cur == NS - 1 ? 0 : cur + 1;
+  }
+  wait_vmcnt<0>();
+  if (want_stats) {   // the workgroup's partial: merge the WGM row waves of each column
+    float (*st_n)[BN] = (float (*)[BN])stb;
+    float (*st_m)[BN] = st_n + WGM;
+    float (*st_q)[BN] = st_n + 2 * WGM;
+    const int wmi = wid / WGN;
+#pragma unroll
+    for (int j = 0; j < RN; ++j)           // the 4 lane groups of a column (rows rq..rq+3)
+#pragma unroll
+      for (int o = 16; o <= 32; o <<= 1) {
+        const float nb = __shfl_xor(rn[j], o, 64), mb = __shfl_xor(rmu[j], o, 64), qb = __shfl_xor(rq2[j], o, 64);
+        const float nt = rn[j] + nb;
+        if (nt > 0.f) {
+          const float dl = mb - rmu[j], f = nb / nt;
+          rmu[j] += dl * f;
+          rq2[j] += qb + dl * dl * rn[j] * f;
+        }
+        rn[j] = nt;
+      }
+    __syncthreads();
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        st_n[wmi][wn0 + j * 16 + col16] = rn[j];
+        st_m[wmi][wn0 + j * 16 + col16] = rmu[j];
+        st_q[wmi][wn0 + j * 16 + col16] = rq2[j];
+      }
+    }
+    __syncthreads();
+    if (wid < WGN) {
+      for (int c = lane; c < WN; c += 64) {
+        const int col = wn0 + c;
+        float n_ = st_n[0][col], m_ = st_m[0][col], q = st_q[0][col];
+        for (int w = 1; w < WGM; ++w) {
+          const float nb = st_n[w][col];
+          if (nb > 0.f) {
+            const float mb = st_m[w][col], nt = n_ + nb, dl = mb - m_, f = nb / nt;
+            m_ += dl * f;
+            q += st_q[w][col] + dl * dl * n_ * f;
+            n_ = nt;
+          }
+        }
+        float* pp = a.stats_part + (int64_t)blockIdx.x * 3 * a.Ng;
+        pp[col] = n_;
+        pp[a.Ng + col] = m_;
+        pp[2 * a.Ng + col] = q;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // WGRAD: dW[m = k][ng = (r, s, c)] = sum over pixels of dy[pix][k] * xu[pix + (r, s)][c].
 // Block tile BM out-channels x BN in-channels of ONE tap (C % BN == 0).  K-step t = (output
 // pixel t / G, image group t % G): 64 images at one pixel.  Split over blockIdx.z with fp32
@@ -940,6 +1270,12 @@ bool g_ring256 = [] { const char* e = getenv("ES_RING256"); return !(e && e[0] =
 // the 2x2 source window at (u, v)): one 256 x 256 GEMM over (class, channel) columns; ES_SP_MERGE=0
 // runs the classes as separate row tiles (A/B)
 bool g_sp_merge = [] { const char* e = getenv("ES_SP_MERGE"); return !(e && e[0] == '0'); }();
+// persistent short-K FWD / DGRAD (conv_persist_kernel); ES_PERSIST=0 keeps the ring kernel (A/B).
+// FWD only with ES_PERSIST_FWD=1: measured at B = 1024 (tools/conv_micro.py), conv_layers.9 FWD
+// 306 us persistent vs 311 us ring without fused statistics but 376 vs 364 us with them, while
+// its DGRAD (4 K-steps, 128 columns) drops from 387 to 259 us
+bool g_persist = [] { const char* e = getenv("ES_PERSIST"); return !(e && e[0] == '0'); }();
+bool g_persist_fwd = [] { const char* e = getenv("ES_PERSIST_FWD"); return e && e[0] == '1'; }();
 
 }  // namespace
 
@@ -982,6 +1318,14 @@ void es_make_subpixel(const es_conv_desc_t& d, int row_tile, SubPixel& sp) {
 extern "C" int es_conv_set_ring(int on) {
   const int old = !g_ring_off;
   g_ring_off = !on;
+  return old;
+}
+
+extern "C" int es_conv_set_persist(int on) {
+  // bit 0: the persistent kernel on / off; bit 1: also for FWD
+  const int old = (g_persist ? 1 : 0) | (g_persist_fwd ? 2 : 0);
+  g_persist = (on & 1) != 0;
+  g_persist_fwd = (on & 2) != 0;
   return old;
 }
 
@@ -1056,6 +1400,38 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
   if (sp_weights && mode == MODE_FWD && g_sp_shortk > 0) {
     const int cls_steps = ((d.R + 1) / 2) * ((d.S + 1) / 2) * d.C / 64;   // K-steps of the largest class
     shortk = cls_steps <= g_sp_shortk;
+  }
+  // persistent short-K kernel (conv_persist_kernel): FWD / DGRAD, stride 1, no upsample / sub-pixel,
+  // <= 8 K-steps, the whole weight panel (nk x Ng x 128 B) within 64 KiB, dense 16-byte output rows
+  {
+    const int nkk = a.Kd / 64;
+    const int nchk = mode == MODE_FWD ? d.C : d.K;
+    const bool rows16 = a.os[1] == 1 && a.beta == 0.f && a.out_bf16 && a.os[0] % 8 == 0 && a.os[2] % 8 == 0 &&
+                        a.os[3] % 8 == 0 && ((uintptr_t)a.out & 15) == 0 &&
+                        (int64_t)d.N * a.os[0] * 2 < (1ll << 31);
+    const bool geo = d.stride == 1 && !sp_weights && !a.fold && d.hmap == nullptr && d.up_h <= 0 &&
+                     d.Hu == d.H && d.Wu == d.W && nchk % 64 == 0 && a.Kd % 64 == 0;
+    const int NS = a.Ng <= 64 ? 4 : 3;
+    if (g_persist && (mode == MODE_DGRAD || g_persist_fwd) && geo && rows16 && (a.Ng == 64 || a.Ng == 128) &&
+        nkk >= NS - 1 && nkk <= 8 &&
+        nkk * a.Ng <= 512 && a.ng >= 16) {
+      const int NB = 128 / a.ng, TT = (PQ + NB - 1) / NB;
+      const int ntiles = NGI * TT;
+      const int nwg = std::min(ntiles, 256);
+      a.stats_part = nullptr;
+      if (mode == MODE_FWD && g_stats_req.part && (int64_t)nwg * 3 * a.Ng <= g_stats_req.floats) {
+        a.stats_part = g_stats_req.part;
+        g_stats_req.chunks = nwg;
+      }
+      if (mode == MODE_FWD) {
+        if (a.Ng == 64) hipLaunchKernelGGL((conv_persist_kernel<MODE_FWD, 64>), dim3(nwg), dim3(RT), 0, st, a, ntiles);
+        else hipLaunchKernelGGL((conv_persist_kernel<MODE_FWD, 128>), dim3(nwg), dim3(RT), 0, st, a, ntiles);
+      } else {
+        if (a.Ng == 64) hipLaunchKernelGGL((conv_persist_kernel<MODE_DGRAD, 64>), dim3(nwg), dim3(RT), 0, st, a, ntiles);
+        else hipLaunchKernelGGL((conv_persist_kernel<MODE_DGRAD, 128>), dim3(nwg), dim3(RT), 0, st, a, ntiles);
+      }
+      return 1;
+    }
   }
   const bool big = !shortk && (int64_t)NGI * a.ng * PQ / 256 * nt128 >= 768;   // >= 3 rounds of 256-row tiles
   const int BM = big ? 256 : 128, NB = BM / a.ng;

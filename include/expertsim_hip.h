@@ -99,6 +99,12 @@ int es_conv_set_ring(int on);
  * 1 = on (default), 0 = 256 x 128 tiles (same accumulation order: bit-identical results).
  * Returns the previous setting. */
 int es_conv_set_ring256(int on);
+/* Persistent short-K FWD / DGRAD kernel (conv_mfma.hip conv_persist_kernel: generator
+ * conv_layers.9 and its dgrad, <= 8 K-steps of 64 channels, 64 or 128 output columns).  on: bit 0
+ * enables it (default: for DGRAD), bit 1 also for FWD (default off); 0 = the ring kernel (same
+ * accumulation order: bit-identical outputs; the fused BatchNorm partials are per workgroup
+ * instead of per row tile).  Returns the previous setting. */
+int es_conv_set_persist(int on);
 /* Sub-pixel decomposition of stride-1 convs over a x2 nearest upsample (conv_mfma.hip): 1 = on
  * (default; wgrad uses it internally, fwd/dgrad when the caller packs mode 2/3 weights and sets
  * desc->subpixel), 0 = off.  Returns the previous setting. */

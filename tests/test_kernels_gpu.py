@@ -650,6 +650,51 @@ def test_conv_ring256_matches_ring128(case):
     assert rel(outs[0][2], outs[1][2]) < 1e-5 and rel(outs[0][3], outs[1][3]) < 1e-5
 
 
+@pytest.mark.parametrize("case", [(200, 128, 46, 46, 64, 2), (70, 128, 23, 21, 64, 2), (33, 64, 9, 7, 128, 2)])
+def test_conv_persist_matches_ring(case):
+    """The persistent short-K kernel (generator conv_layers.9 FWD and its DGRAD: <= 8 K-steps, one
+    workgroup per CU over its tiles, weight panel resident in LDS) accumulates in the ring kernel's
+    K order: bf16 outputs bit-identical to the ring kernel; fused BatchNorm statistics (per
+    workgroup instead of per row tile) equal up to the merge order; both close to torch fp32."""
+    hip = _hip()
+    from expertsim.layers import Act, ConvOp, NormOp
+    N, Cin, H, W, Cout, k = case
+    torch.manual_seed(9)
+    w = torch.randn(Cout, Cin, k, k, device=DEV) / np.sqrt(Cin * k * k)
+    b = torch.randn(Cout, device=DEV)
+    op = ConvOp(torch.nn.Parameter(w), torch.nn.Parameter(b))
+    xa = Act.nhwc(N, Cin, H, W, torch.bfloat16, DEV)
+    xa.t.normal_()
+    outs = []
+    old = hip.lib().es_conv_set_persist(3)
+    try:
+        for on in (3, 0):
+            hip.lib().es_conv_set_persist(on)
+            ya = op.fwd(xa, out_dtype=torch.bfloat16, bn_stats=True)
+            assert ya.bn_part is not None
+            gy = ya.like_nhwc(torch.bfloat16)
+            gy.t.copy_(torch.randn(gy.t.shape, generator=torch.Generator().manual_seed(2)).to(DEV))
+            dxa = op.dgrad(gy, xa, dx_dtype=torch.bfloat16)
+            nm = NormOp(hip.NORM_BN, torch.ones(Cout, device=DEV), torch.zeros(Cout, device=DEV),
+                        running_mean=torch.zeros(Cout, device=DEV), running_var=torch.ones(Cout, device=DEV))
+            m, istd = nm.stats(ya)
+            torch.cuda.synchronize()
+            outs.append((ya.t.clone(), dxa.t.clone(), m.cpu(), istd.cpu(), ya, gy))
+    finally:
+        hip.lib().es_conv_set_persist(old)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    assert rel(outs[0][2], outs[1][2]) < 1e-5 and rel(outs[0][3], outs[1][3]) < 1e-5
+    # against torch fp32 on the bf16 operands
+    xr = xa.torch_nchw().float()
+    wr = w.to(torch.bfloat16).float()
+    yr = F.conv2d(xr, wr, b)
+    assert rel(outs[0][4].torch_nchw().float().cpu(), yr.cpu()) < 1e-2
+    dxr = torch.nn.grad.conv2d_input(xr.shape, wr, outs[0][5].torch_nchw().float())
+    assert rel(from_act(Act(outs[0][1], dxa.dims, dxa.strides)).float(), dxr.cpu()) < 1e-2
+    assert rel(outs[0][2], yr.mean((0, 2, 3)).cpu()) < 1e-2
+
+
 @pytest.mark.parametrize("shape", [(5, 128, 13, 13), (3, 70, 9, 7), (2, 3, 5, 4)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_copy_relayout(shape, dtype):
