@@ -151,6 +151,50 @@ __global__ void __launch_bounds__(256) maxpool_bwd_nhwc(const T* __restrict__ dy
   }
 }
 
+// Forward on dense NHWC views: a thread owns VN channels of one output pixel, reads the window's
+// rows as 16-byte vectors and writes the VN maxima (one 16-byte store) and their argmax bytes
+// (first max in row-major window order, NaN wins, as torch).  The generic kernel above decodes
+// every element's coordinates and moves 2 / 4 bytes per access (~3.5x slower on the aux
+// regressor's pools).
+template <typename T>
+__global__ void __launch_bounds__(256) maxpool_fwd_nhwc(const T* __restrict__ x, int N, int C, int H, int W, int P,
+                                                       int Q, int kh, int kw, int sh, int sw, T* __restrict__ y,
+                                                       uint8_t* __restrict__ idx) {
+  constexpr int VN = 16 / sizeof(T);
+  const int cv = C / VN;
+  const uint32_t total = (uint32_t)N * P * Q * cv;
+  for (uint32_t e = blockIdx.x * 256u + threadIdx.x; e < total; e += gridDim.x * 256u) {
+    const uint32_t pix = e / cv;
+    const int c0 = (int)(e - pix * cv) * VN;
+    const uint32_t np = pix / Q;
+    const int q = (int)(pix - np * Q);
+    const int n = (int)(np / P), p = (int)(np - (uint32_t)n * P);
+    float best[VN];
+    uint8_t bi[VN];
+#pragma unroll
+    for (int v = 0; v < VN; ++v) { best[v] = -INFINITY; bi[v] = 0; }
+    const T* xb = x + ((int64_t)n * H + p * sh) * W * C + (int64_t)(q * sw) * C + c0;
+    for (int i = 0; i < kh; ++i)
+      for (int j = 0; j < kw; ++j) {
+        T xv[VN];
+        *(uint4*)xv = *(const uint4*)(xb + ((int64_t)i * W + j) * C);
+#pragma unroll
+        for (int v = 0; v < VN; ++v) {
+          const float f = to_f(xv[v]);
+          if (f > best[v] || (isnan(f) && !isnan(best[v]))) { best[v] = f; bi[v] = (uint8_t)(i * kw + j); }
+        }
+      }
+    T ov[VN];
+#pragma unroll
+    for (int v = 0; v < VN; ++v) ov[v] = from_f<T>(best[v]);
+    *(uint4*)(y + (int64_t)pix * C + c0) = *(const uint4*)ov;
+    if (idx) {
+      if constexpr (VN == 8) *(uint2*)(idx + (int64_t)pix * C + c0) = *(const uint2*)bi;
+      else *(uint32_t*)(idx + (int64_t)pix * C + c0) = *(const uint32_t*)bi;
+    }
+  }
+}
+
 bool dense_nhwc(const es_view_t* v) {
   const int64_t C = v->c;
   return v->s[1] == 1 && v->s[3] == C && v->s[2] == (int64_t)v->w * C && v->s[0] == (int64_t)v->h * v->w * C;
@@ -306,24 +350,50 @@ __device__ __forceinline__ void sn_power_body(const float* w, int h, int wd, flo
   float* wv = scratch;       // [h]
   float* vt = scratch + h;   // [wd]
   if (update) {
-    // t = W^T u
+    // t = W^T u: groups of 8 column chunks of 64 (lane = column), the block's waves split the
+    // rows, per thread 8 independent column accumulators (loads of a row in flight together),
+    // partials merged in LDS.  (A thread per column looping over every row was one dependent
+    // load chain: ~30 us for the 64 x 128 fc2.)
+    __shared__ float part[16][512];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
     float ss = 0.f;
-    for (int j = threadIdx.x; j < wd; j += blockDim.x) {
-      float t = 0.f;
-      for (int i = 0; i < h; ++i) t += w[(int64_t)i * wd + j] * u[i];
-      vt[j] = t;
-      ss += t * t;
+    for (int j0 = 0; j0 < wd; j0 += 512) {
+      float t[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) t[c] = 0.f;
+      for (int i = wid; i < h; i += nw) {
+        const float ui = u[i];
+        const float* wr = w + (int64_t)i * wd + j0 + lane;
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+          if (j0 + c * 64 + lane < wd) t[c] += wr[c * 64] * ui;
+      }
+#pragma unroll
+      for (int c = 0; c < 8; ++c) part[wid][c * 64 + lane] = t[c];
+      __syncthreads();
+      for (int jj = threadIdx.x; jj < 512 && j0 + jj < wd; jj += blockDim.x) {
+        float sj = 0.f;
+        for (int k = 0; k < nw; ++k) sj += part[k][jj];
+        vt[j0 + jj] = sj;
+        ss += sj * sj;
+      }
+      __syncthreads();
     }
     const float nv = fmaxf(sqrtf(block_sum(ss, sh)), 1e-12f);
     for (int j = threadIdx.x; j < wd; j += blockDim.x) v[j] = vt[j] / nv;
     __syncthreads();
   }
-  // s = W v
+  // s = W v (a wave per row, lanes along the row, two independent accumulators)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   for (int i = wid; i < h; i += nw) {
-    float t = 0.f;
-    for (int j = lane; j < wd; j += 64) t += w[(int64_t)i * wd + j] * v[j];
-    t = wave_sum(t);
+    float t0 = 0.f, t1 = 0.f;
+    int j = lane;
+    for (; j + 64 < wd; j += 128) {
+      t0 += w[(int64_t)i * wd + j] * v[j];
+      t1 += w[(int64_t)i * wd + j + 64] * v[j + 64];
+    }
+    if (j < wd) t0 += w[(int64_t)i * wd + j] * v[j];
+    const float t = wave_sum(t0 + t1);
     if (lane == 0) wv[i] = t;
   }
   __syncthreads();
@@ -450,16 +520,23 @@ __global__ void __launch_bounds__(1024) sn_bwd_batch_kernel(SnBwdJobs j, float b
 }
 __device__ __forceinline__ void sn_bwd_body(const float* w, const float* g, int h, int wd, const float* u,
                                             const float* v, const float* sigma, float* dw, float beta, float* sh) {
-  const int64_t n = (int64_t)h * wd;
-  float d = 0.f;
-  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) d += g[i] * w[i];
-  d = block_sum(d, sh);
+  const int n = h * wd;                     // < 2^20 (host check)
+  const int bd = blockDim.x;
+  float d0 = 0.f, d1 = 0.f;
+  int i = threadIdx.x;
+  for (; i + bd < n; i += 2 * bd) {         // two independent chains
+    d0 += g[i] * w[i];
+    d1 += g[i + bd] * w[i + bd];
+  }
+  if (i < n) d0 += g[i] * w[i];
+  const float d = block_sum(d0 + d1, sh);
   const float s = sigma[0];
   const float c = d / (s * s);
-  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-    const int r = i / wd, col = i % wd;
-    const float val = g[i] / s - c * u[r] * v[col];
-    dw[i] = (beta != 0.f ? beta * dw[i] : 0.f) + val;
+  const float is = 1.f / s;
+  for (int k = threadIdx.x; k < n; k += bd) {
+    const int r = k / wd, col = k - r * wd;  // 32-bit division (a 64-bit one per element cost ~100 instructions)
+    const float val = g[k] * is - c * u[r] * v[col];
+    dw[k] = (beta != 0.f ? beta * dw[k] : 0.f) + val;
   }
 }
 
@@ -562,6 +639,19 @@ extern "C" int es_maxpool_fwd(const es_view_t* x, es_dtype_t dt, const void* xp,
                               int sw, const es_view_t* y, void* yp, uint8_t* idx, es_stream_t stream) {
   ES_CHECK_ARG(y->h == (x->h - kh) / sh + 1 && y->w == (x->w - kw) / sw + 1, "maxpool: output shape");
   const int64_t total = (int64_t)y->n * y->c * y->h * y->w;
+  const int vn = dt == ES_BF16 ? 8 : 4;
+  if (dense_nhwc(x) && dense_nhwc(y) && x->c % vn == 0 && x->c > 1 && total < (1ll << 31)) {
+    const int64_t items = total / vn;
+    const unsigned grid = (unsigned)std::min<int64_t>((items + 255) / 256, 16384);
+    if (dt == ES_BF16)
+      hipLaunchKernelGGL(maxpool_fwd_nhwc<bf16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16*)xp,
+                         x->n, x->c, x->h, x->w, y->h, y->w, kh, kw, sh, sw, (bf16*)yp, idx);
+    else
+      hipLaunchKernelGGL(maxpool_fwd_nhwc<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)xp,
+                         x->n, x->c, x->h, x->w, y->h, y->w, kh, kw, sh, sw, (float*)yp, idx);
+    ES_CHECK_LAUNCH();
+    return ES_OK;
+  }
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
                      mkview(x), xp, dt == ES_BF16, kh, kw, sh, sw, mkview(y), yp, idx);
   ES_CHECK_LAUNCH();
@@ -662,7 +752,7 @@ extern "C" int es_sn_power_iter(const float* w, int h, int wd, float* u, float* 
   // the caller's buffer: sigma[0], scratch [h + wd], then the snapshot of the u, v used [h + wd]
   // (1 + 2 (h + wd) floats)
   hipStream_t st = (hipStream_t)stream;
-  if ((int64_t)h * wd >= 16384) {   // large weights: spread the two mat-vecs over the chip
+  if ((int64_t)h * wd >= 16384) {   // large weights (discriminator fc1): the two mat-vecs over the chip
     float* wv = sigma + 1;
     float* vt = sigma + 1 + h;
     if (update) hipLaunchKernelGGL(sn_wtu_kernel, dim3((wd + 63) / 64), dim3(256), 0, st, w, h, wd, u, vt);

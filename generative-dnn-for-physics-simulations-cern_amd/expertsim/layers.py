@@ -630,7 +630,8 @@ class SpectralNorm:
 
     @staticmethod
     def sigma_many(sns, update=True):
-        """sigma() of several layers: the small ones (h*wd < 16384) share one launch."""
+        """sigma() of several layers: the small ones (h*wd < 16384) share one launch (a block per
+        layer); larger ones (discriminator fc1) run the multi-block mat-vecs."""
         out = [None] * len(sns)
         small = [i for i, sn in enumerate(sns) if sn.h * sn.wd < 16384]
         if len(small) < 2 or os.environ.get("ES_SN_BATCH", "1") == "0":
