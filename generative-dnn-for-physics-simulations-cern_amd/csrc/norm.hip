@@ -233,7 +233,20 @@ __global__ void __launch_bounds__(256) colred_kernel(BwdIn b, int64_t rows, int6
   }
 }
 
-// BN stats finalize: merge chunk partials -> mean/invstd, running stats (torch semantics)
+// BN stats finalize: merge chunk partials -> mean/invstd, running stats (torch semantics).
+__device__ __forceinline__ void bn_stats_store(int c, double n_, double s1, double s2, float eps, float* mean,
+                                               float* invstd, float* rmean, float* rvar, float mom) {
+  const double mt = s1 / n_;
+  const double Mt = fmax(s2 - n_ * mt * mt, 0.0);
+  const double var = Mt / n_;
+  mean[c] = (float)mt;
+  invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (rmean) rmean[c] = (1.f - mom) * rmean[c] + mom * (float)mt;
+  if (rvar) rvar[c] = (1.f - mom) * rvar[c] + mom * (float)(n_ > 1.0 ? Mt / (n_ - 1.0) : var);
+}
+
+// (few chunks: the exact fp64 Welford merge; the gradient parity tests at B = 8 sit on
+// LeakyReLU / dropout kinks that a last-bit change of the statistics can flip)
 __global__ void bn_finalize_kernel(const float* part, int chunks, int C, float eps, float* mean,
                                    float* invstd, float* rmean, float* rvar, float mom) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -254,6 +267,63 @@ __global__ void bn_finalize_kernel(const float* part, int chunks, int C, float e
   invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
   if (rmean) rmean[c] = (1.f - mom) * rmean[c] + mom * (float)mu;
   if (rvar) rvar[c] = (1.f - mom) * rvar[c] + mom * (float)(n_ > 1.0 ? M / (n_ - 1.0) : var);
+}
+
+// Two-level merge for many chunks and few channels (a conv epilogue's per-row-tile partials, e.g.
+// 16208 x 64 for generator conv_layers.9 at B = 1024): level 1, block b Chan-merges the chunk range
+// [b R, (b+1) R) with coalesced reads (threads along the channels) and writes the result IN PLACE
+// into chunk b R of that range (only its own range is touched: no cross-block hazard; the partials
+// are consumed); level 2 merges the G range heads per channel.  (One block per channel reading
+// every chunk with a stride of 3C floats requested one cache line per load: ~50 us.)
+__global__ void __launch_bounds__(256) bn_merge_l1_kernel(float* part, int chunks, int C, int R) {
+  const int k0 = blockIdx.x * R, k1 = min(chunks, k0 + R);
+  const int TS = 256 / C > 0 ? 256 / C : 1;           // chunk streams (C <= 256)
+  const int c = threadIdx.x % C, sidx = threadIdx.x / C;
+  __shared__ double sh[3][256];
+  double n_ = 0.0, s1 = 0.0, s2 = 0.0;
+  if (sidx < TS) {
+#pragma unroll 4
+    for (int k = k0 + sidx; k < k1; k += TS) {
+      const float* p = part + (int64_t)k * 3 * C;
+      const double nb = p[c], mb = p[C + c], Mb = p[2 * C + c];
+      const bool has = nb > 0.0;
+      n_ += nb;
+      s1 += has ? nb * mb : 0.0;
+      s2 += has ? Mb + nb * mb * mb : 0.0;
+    }
+  }
+  sh[0][threadIdx.x] = n_; sh[1][threadIdx.x] = s1; sh[2][threadIdx.x] = s2;
+  __syncthreads();                                      // every read of the range is done
+  if (threadIdx.x < C) {
+    for (int t = 1; t < TS; ++t) {
+      n_ += sh[0][t * C + c]; s1 += sh[1][t * C + c]; s2 += sh[2][t * C + c];
+    }
+    float* p = part + (int64_t)k0 * 3 * C;
+    const double mt = n_ > 0.0 ? s1 / n_ : 0.0;
+    p[c] = (float)n_;
+    p[C + c] = (float)mt;
+    p[2 * C + c] = (float)fmax(s2 - n_ * mt * mt, 0.0);
+  }
+}
+
+__global__ void __launch_bounds__(256) bn_merge_l2_kernel(const float* part, int G, int R, int C, float eps,
+                                                          float* mean, float* invstd, float* rmean, float* rvar,
+                                                          float mom) {
+  const int c = blockIdx.x;
+  __shared__ double sh[8];
+  double n_ = 0.0, s1 = 0.0, s2 = 0.0;
+  for (int b = threadIdx.x; b < G; b += 256) {
+    const float* p = part + (int64_t)b * R * 3 * C;
+    const double nb = p[c], mb = p[C + c], Mb = p[2 * C + c];
+    const bool has = nb > 0.0;
+    n_ += nb;
+    s1 += has ? nb * mb : 0.0;
+    s2 += has ? Mb + nb * mb * mb : 0.0;
+  }
+  n_ = block_sum_d(n_, sh);
+  s1 = block_sum_d(s1, sh);
+  s2 = block_sum_d(s2, sh);
+  if (threadIdx.x == 0) bn_stats_store(c, n_, s1, s2, eps, mean, invstd, rmean, rvar, mom);
 }
 
 // BN backward finalize: per channel A1 = gamma*s1/cnt, A2 = gamma*s2/cnt ; dgamma += s2, dbeta += s1
@@ -325,15 +395,7 @@ __global__ void __launch_bounds__(FIN_T) bn_finalize_block_kernel(const float* p
   n_ = block_sum_d(n_, sh);
   s1 = block_sum_d(s1, sh);
   s2 = block_sum_d(s2, sh);
-  if (threadIdx.x == 0) {
-    const double nt = n_, mt = s1 / nt;
-    const double Mt = fmax(s2 - nt * mt * mt, 0.0);
-    const double var = Mt / nt;
-    mean[c] = (float)mt;
-    invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
-    if (rmean) rmean[c] = (1.f - mom) * rmean[c] + mom * (float)mt;
-    if (rvar) rvar[c] = (1.f - mom) * rvar[c] + mom * (float)(nt > 1.0 ? Mt / (nt - 1.0) : var);
-  }
+  if (threadIdx.x == 0) bn_stats_store(c, n_, s1, s2, eps, mean, invstd, rmean, rvar, mom);
 }
 
 // out1 (+)= s1 (beta1: scale of old out1), out2 += s2; a1/a2 = gamma*s/cnt (BN backward)
@@ -389,9 +451,19 @@ __global__ void __launch_bounds__(256) sums_finalize_kernel(const float* part, i
 
 // finalize dispatch: a block per channel while the chunks dominate, a thread per channel otherwise
 bool fin_block(int chunks, int C) { return chunks > 32 && C < 4096; }
+// two-level in-place merge of many chunk partials (ES_MERGE2=0: the block-per-channel kernel, A/B)
+bool g_merge2 = [] { const char* e = getenv("ES_MERGE2"); return !(e && e[0] == '0'); }();
 
 void launch_bn_finalize(hipStream_t st, const float* part, int chunks, int C, float eps, float* mean, float* invstd,
                         float* rmean, float* rvar, float mom) {
+  if (chunks >= 1024 && C <= 256 && g_merge2) {   // (consumes the partials: they are merged in place)
+    const int G = std::min(256, chunks / 16), R = (chunks + G - 1) / G;
+    const int Gr = (chunks + R - 1) / R;
+    hipLaunchKernelGGL(bn_merge_l1_kernel, dim3(Gr), dim3(256), 0, st, const_cast<float*>(part), chunks, C, R);
+    hipLaunchKernelGGL(bn_merge_l2_kernel, dim3(C), dim3(256), 0, st, part, Gr, R, C, eps, mean, invstd, rmean,
+                       rvar, mom);
+    return;
+  }
   if (fin_block(chunks, C))
     hipLaunchKernelGGL(bn_finalize_block_kernel, dim3(C), dim3(FIN_T), 0, st, part, chunks, C, eps, mean, invstd,
                        rmean, rvar, mom);
