@@ -61,6 +61,13 @@ class DFront2Params(C.Structure):
                 ("slope", C.c_float), ("ph", C.c_int), ("pw", C.c_int)]
 
 
+class DMlpParams(C.Structure):
+    _fields_ = [("w1", C.c_void_p), ("sigma1", C.c_void_p), ("b1", C.c_void_p), ("g1", C.c_void_p),
+                ("be1", C.c_void_p), ("w2", C.c_void_p), ("sigma2", C.c_void_p), ("b2", C.c_void_p),
+                ("g2", C.c_void_p), ("be2", C.c_void_p), ("w3", C.c_void_p), ("sigma3", C.c_void_p),
+                ("b3", C.c_void_p), ("eps1", C.c_float), ("eps2", C.c_float), ("slope", C.c_float)]
+
+
 P = C.c_void_p
 I64 = C.c_int64
 _SIGS = {
@@ -109,6 +116,10 @@ _SIGS = {
     "es_dfront2_bwd": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, P, P, P, I64, P, P, P, P, P, P, P, P, P, P,
                                  P, P]),
     "es_dfront2_set_probe": (None, [P]),
+    "es_dmlp_part_floats": (I64, [C.c_int, C.c_int]),
+    "es_dmlp_fwd": (C.c_int, [P, I64, C.c_int, C.c_int, P, P, P, P, P, P, P, P]),
+    "es_dmlp_bwd": (C.c_int, [P, I64, C.c_int, C.c_int, P, P, P, P, P, P, P, P, P, I64, P, P, P, P, P, P, P, P, P,
+                              P, P, P]),
     "es_upsample_bwd": (C.c_int, [P, C.c_int, P, P, P, P, P, P, C.c_int, P, C.c_float, P]),
     "es_copy": (C.c_int, [P, C.c_int, P, P, C.c_int, P, C.c_float, C.c_float, P]),
     "es_avgpool_fwd": (C.c_int, [P, C.c_int, P, P, P, P]),

@@ -223,9 +223,34 @@ class SNDiscriminator(ExpertModule):
                                                       p1=p1, i1=i1, h2=h2, y2=y2, s2=s2, i2=i2, X=X,
                                                       feat_dims=(B, 16, fh, fw)))
 
+    # the fc tail as one per-16-samples kernel pair (d_mlp.hip); ES_NO_DMLP=1: the layer-by-layer
+    # kernels (A/B)
+    fuse_mlp = os.environ.get("ES_NO_DMLP") != "1"
+
+    def _mlp_params(self, sig):
+        m = lambda n: get_module(self, n)
+        p = hip.DMlpParams()
+        f1, n1, f2, n2, f3 = m("fc1.0"), m("fc1.1"), m("fc2.0"), m("fc2.1"), m("fc3")
+        p.w1, p.sigma1, p.b1 = f1.weight_orig.data_ptr(), sig["fc1.0"][0].data_ptr(), f1.bias.data_ptr()
+        p.g1, p.be1 = n1.weight.data_ptr(), n1.bias.data_ptr()
+        p.w2, p.sigma2, p.b2 = f2.weight_orig.data_ptr(), sig["fc2.0"][0].data_ptr(), f2.bias.data_ptr()
+        p.g2, p.be2 = n2.weight.data_ptr(), n2.bias.data_ptr()
+        p.w3, p.sigma3, p.b3 = f3.weight_orig.data_ptr(), sig["fc3"][0].data_ptr(), f3.bias.data_ptr()
+        p.eps1, p.eps2, p.slope = float(n1.eps), float(n2.eps), SLOPE
+        return p
+
     def _fc_fwd(self, X: Act, B, cdt, dev, sig, ctx):
         """fc1 -> LN -> LReLU -> fc2 -> LN -> LReLU (latent) -> fc3 on the fc1 input rows X."""
         o = self.ops()
+        if self.fuse_mlp and cdt == torch.float32:
+            F = X.dims[1]
+            params = self._mlp_params(sig)
+            f32 = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)
+            h3, s3, h4, s4, lat, out = f32(B, 128), f32(B, 2), f32(B, 64), f32(B, 2), f32(B, 64), f32(B, 1)
+            hip.call("es_dmlp_fwd", X.ptr, X.strides[0], B, F, C.byref(params), hip.ptr(h3), hip.ptr(s3),
+                     hip.ptr(h4), hip.ptr(s4), hip.ptr(lat), hip.ptr(out), hip.stream_ptr())
+            ctx.update(mlp=(params, h3, s3, h4, s4, lat))
+            return Act.of(out), Act.of(lat), ctx
         lr = hip.chain_struct(hip.ACT_LRELU, SLOPE)
         inv = lambda n: sig[n][0]
         h3 = o["fc1.0"].fwd(X, inv_scale=inv("fc1.0"))
@@ -252,8 +277,44 @@ class SNDiscriminator(ExpertModule):
             SpectralNorm.bwd_many(sn_jobs, beta=1.0)
         return dimg
 
+    def _mlp_bwd(self, ctx, dout, dlat, weight_grads, sn_jobs):
+        """Backward of the fused fc tail -> the fc1 input gradient rows dX (fp32 Act [B][F])."""
+        params, h3, s3, h4, s4, lat = ctx["mlp"]
+        X = ctx["X"]
+        B, F = X.dims[0], X.dims[1]
+        dev = X.t.device
+        m = lambda n: get_module(self, n)
+        dX = Act.rows(B, F, torch.float32, dev)
+        part = None
+        outs = [None] * 10
+        if weight_grads:
+            part = torch.empty(hip.lib().es_dmlp_part_floats(B, F), dtype=torch.float32, device=dev)
+            g1 = torch.empty_like(m("fc1.0").weight_orig)
+            g2 = torch.empty_like(m("fc2.0").weight_orig)
+            g3 = torch.empty_like(m("fc3").weight_orig)
+            outs = [g1, m("fc1.0").bias.grad, m("fc1.1").weight.grad, m("fc1.1").bias.grad,
+                    g2, m("fc2.0").bias.grad, m("fc2.1").weight.grad, m("fc2.1").bias.grad,
+                    g3, m("fc3").bias.grad]
+        hip.call("es_dmlp_bwd", X.ptr, X.strides[0], B, F, C.byref(params), hip.ptr(h3), hip.ptr(s3), hip.ptr(h4),
+                 hip.ptr(s4), hip.ptr(lat), dout.ptr if dout is not None else None,
+                 dlat.ptr if dlat is not None else None, dX.ptr, F, hip.ptr(part),
+                 *[hip.ptr(t) for t in outs], hip.stream_ptr())
+        if weight_grads:
+            o = self.ops()
+            sig = ctx["sig"]
+            for name, g in (("fc3", outs[8]), ("fc2.0", outs[4]), ("fc1.0", outs[0])):
+                sn_jobs.append((o["sn:" + name], g, sig[name], m(name).weight_orig.grad))
+        return dX
+
     def _bwd(self, ctx, dout, dlat, weight_grads, input_grad, sn_jobs):
         o = self.ops()
+        if ctx.get("mlp") is not None:
+            assert dout is None or (dout.t.dtype == torch.float32 and dout.strides[0] == 1), "dout: [B,1] fp32"
+            assert dlat is None or (dlat.t.dtype == torch.float32 and dlat.strides[0] == 64), "dlat: [B,64] fp32"
+            dX = self._mlp_bwd(ctx, dout, dlat, weight_grads, sn_jobs)
+            if ctx["front2"] is not None:
+                return self.front2_bwd(ctx, dX, weight_grads, input_grad, sn_jobs)
+            return self._front_bwd_from_dX(ctx, dX, weight_grads, input_grad, sn_jobs)
         cdt = self.compute_dtype
         dev = ctx["X"].t.device
         B = ctx["X"].dims[0]
@@ -297,6 +358,26 @@ class SNDiscriminator(ExpertModule):
         dX = o["fc1.0"].dgrad(dh3, ctx["X"], inv_scale=sig["fc1.0"][0])
         if ctx["front2"] is not None:
             return self.front2_bwd(ctx, dX, weight_grads, input_grad, sn_jobs)
+        return self._front_bwd_from_dX(ctx, dX, weight_grads, input_grad, sn_jobs)
+
+    def _front_bwd_from_dX(self, ctx, dX, weight_grads, input_grad, sn_jobs):
+        """Backward of the conv blocks (unfused / block-1-fused forms) from the fc1 input gradient."""
+        o = self.ops()
+        cdt = self.compute_dtype
+        B = ctx["X"].dims[0]
+        lr = hip.chain_struct(hip.ACT_LRELU, SLOPE)
+        m = lambda n: get_module(self, n)
+        sig = ctx["sig"]
+
+        def wgrad(name, dy, x):
+            if not weight_grads:
+                return
+            mod = m(name)
+            g_sn = torch.empty_like(mod.weight_orig)
+            o[name].wgrad(dy, x, g_sn, None, beta=0.0)          # grad of W/sigma
+            sn_jobs.append((o["sn:" + name], g_sn, sig[name], mod.weight_orig.grad))
+
+        bias_g = (lambda n: m(n).bias.grad) if weight_grads else (lambda n: None)
         F = self.flat_dim + self.cond_dim
         B_, Cf, fh, fw = ctx["feat_dims"]
         dfeat = Act(dX.t.view(B, F), (B, 16, fh, fw), (F, fh * fw, fw, 1))

@@ -304,6 +304,32 @@ int es_dfront2_bwd(const float* img, const int64_t is[4], int N, int H, int W, c
                    const int64_t dxs[4],
                    float* part, float* dw1, float* db1, float* dg1, float* dbe1, float* dw2, float* db2,
                    float* dg2, float* dbe2, es_stream_t stream);
+/* Fused fc tail of the spectral-norm discriminator (neutron/discriminator.py:26-48,
+ * proton/discriminator.py:136-158): SNLinear F->128 -> LayerNorm(128) -> LeakyReLU -> SNLinear
+ * 128->64 -> LayerNorm(64) -> LeakyReLU (latent) -> SNLinear 64->1, 16 samples per workgroup, fp32
+ * (v_mfma_f32_16x16x4_f32), weights used as w * (1/sigma[0]) (sigma may be NULL: 1).  Replaces the
+ * es_conv2d_* / es_norm_* / es_pack_conv_weight launches of those layers. */
+typedef struct {
+    const float* w1; const float* sigma1; const float* b1; const float* g1; const float* be1;  /* [128][F], LN(128) */
+    const float* w2; const float* sigma2; const float* b2; const float* g2; const float* be2;  /* [64][128], LN(64) */
+    const float* w3; const float* sigma3; const float* b3;                                    /* [1][64] */
+    float eps1, eps2, slope;
+} es_dmlp_params_t;
+/* Forward over X [B][F] (row stride xs): writes h3 [B][128] (fc1 output), s3 [B][2] (LN1 mean,
+ * invstd), h4 [B][64], s4 [B][2], lat [B][64] (the latent) and out [B] (the logit). */
+int es_dmlp_fwd(const float* X, int64_t xs, int B, int F, const es_dmlp_params_t* p, float* h3, float* s3,
+                float* h4, float* s4, float* lat, float* out, es_stream_t stream);
+/* Backward from dout [B] and / or dlat [B][64] (either may be NULL) with the forward's saved
+ * values.  dX (optional, row stride dxs): the fc1 input gradient, written.  part (optional,
+ * es_dmlp_part_floats(B, F) floats): per-workgroup partials; when given, dw1 / dw2 / dw3 (gradients
+ * of W/sigma, torch layouts) are written and the bias / LayerNorm-affine gradients accumulated;
+ * any output may be NULL. */
+int64_t es_dmlp_part_floats(int B, int F);
+int es_dmlp_bwd(const float* X, int64_t xs, int B, int F, const es_dmlp_params_t* p, const float* h3,
+                const float* s3, const float* h4, const float* s4, const float* lat, const float* dout,
+                const float* dlat, float* dX, int64_t dxs, float* part, float* dw1, float* db1, float* dg1,
+                float* dbe1, float* dw2, float* db2, float* dg2, float* dbe2, float* dw3, float* db3,
+                es_stream_t stream);
 /* dx[n,c,h,w] = beta*dx + sum over upsampled positions mapping to (h,w).  hstart/hcount (device
  * [H]) and wstart/wcount (device [W]) describe the contiguous preimage of each source row/col. */
 int es_upsample_bwd(const es_view_t* dxu, es_dtype_t dt, const void* dxup, const int32_t* hstart,

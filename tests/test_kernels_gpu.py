@@ -614,6 +614,70 @@ def test_dfront2_fused(N, H, W, pool):
                 assert rel(got, r) < 1e-4, (i, rel(got, r))
 
 
+@pytest.mark.parametrize("B,NF", [(70, 1305), (16, 2313), (5, 37)])
+def test_dmlp_fused(B, NF):
+    """es_dmlp_fwd / es_dmlp_bwd (the discriminator's fc tail in one kernel pair, d_mlp.hip) against
+    torch fp32 autograd of the reference layers (neutron/discriminator.py:26-48): logit, latent,
+    LayerNorm statistics, fc1-input gradient and every weight gradient (of W/sigma), for the
+    D-step variant (weights only), the G-step variant (input gradient only) and both."""
+    hip = _hip()
+    import ctypes as C
+    torch.manual_seed(31)
+    X = torch.randn(B, NF)
+    w1, w2, w3 = torch.randn(128, NF) / NF ** 0.5, torch.randn(64, 128) / 11, torch.randn(1, 64) / 8
+    b1, b2, b3 = 0.1 * torch.randn(128), 0.1 * torch.randn(64), 0.1 * torch.randn(1)
+    g1, be1, g2, be2 = 1 + 0.1 * torch.randn(128), 0.1 * torch.randn(128), 1 + 0.1 * torch.randn(64), 0.1 * torch.randn(64)
+    s1, s2, s3 = torch.tensor([1.3]), torch.tensor([0.9]), torch.tensor([1.7])
+    leaves = [t.clone().requires_grad_(True) for t in (b1, g1, be1, b2, g2, be2, b3)]
+    b1r, g1r, be1r, b2r, g2r, be2r, b3r = leaves
+    w1e, w2e, w3e = ((w * (1.0 / s)).requires_grad_(True) for w, s in ((w1, s1), (w2, s2), (w3, s3)))
+    Xr = X.clone().requires_grad_(True)
+    h3 = F.linear(Xr, w1e, b1r)
+    y3 = F.leaky_relu(F.layer_norm(h3, (128,), g1r, be1r, 1e-5), 0.1)
+    h4 = F.linear(y3, w2e, b2r)
+    lat = F.leaky_relu(F.layer_norm(h4, (64,), g2r, be2r, 1e-5), 0.1)
+    out = F.linear(lat, w3e, b3r)
+    gout, glat = torch.randn(B, 1), torch.randn(B, 64)
+    (out * gout).sum().backward(retain_graph=True)
+    (lat * glat).sum().backward()
+
+    d = {k: t.to(DEV) for k, t in dict(w1=w1, s1=s1, b1=b1, g1=g1, be1=be1, w2=w2, s2=s2, b2=b2, g2=g2, be2=be2,
+                                        w3=w3, s3=s3, b3=b3).items()}
+    prm = hip.DMlpParams()
+    prm.w1, prm.sigma1, prm.b1, prm.g1, prm.be1 = (d[k].data_ptr() for k in ("w1", "s1", "b1", "g1", "be1"))
+    prm.w2, prm.sigma2, prm.b2, prm.g2, prm.be2 = (d[k].data_ptr() for k in ("w2", "s2", "b2", "g2", "be2"))
+    prm.w3, prm.sigma3, prm.b3 = (d[k].data_ptr() for k in ("w3", "s3", "b3"))
+    prm.eps1 = prm.eps2 = 1e-5
+    prm.slope = 0.1
+    Xd = X.to(DEV)
+    f32 = lambda *sh: torch.empty(*sh, device=DEV)
+    H3, S3, H4, S4, LAT, OUT = f32(B, 128), f32(B, 2), f32(B, 64), f32(B, 2), f32(B, 64), f32(B)
+    hip.call("es_dmlp_fwd", hip.ptr(Xd), NF, B, NF, C.byref(prm), hip.ptr(H3), hip.ptr(S3), hip.ptr(H4), hip.ptr(S4),
+             hip.ptr(LAT), hip.ptr(OUT), hip.stream_ptr())
+    assert rel(OUT.cpu(), out.detach().view(-1)) < 1e-4
+    assert rel(LAT.cpu(), lat.detach()) < 1e-4
+    assert rel(H3.cpu(), h3.detach()) < 1e-5 and rel(H4.cpu(), h4.detach()) < 1e-4
+    assert rel(S3[:, 0].cpu(), h3.detach().mean(1)) < 1e-4
+    refs = [w1e.grad, b1r.grad, g1r.grad, be1r.grad, w2e.grad, b2r.grad, g2r.grad, be2r.grad, w3e.grad, b3r.grad]
+    gout_d, glat_d = gout.to(DEV).contiguous(), glat.to(DEV).contiguous()
+    for want_dx, want_w in ((False, True), (True, False), (True, True)):
+        dX = torch.full((B, NF), 3.0, device=DEV) if want_dx else None
+        part = torch.empty(hip.lib().es_dmlp_part_floats(B, NF), device=DEV) if want_w else None
+        outs = [f32(128, NF), torch.full((128,), 0.5, device=DEV), torch.full((128,), 0.5, device=DEV),
+                torch.full((128,), 0.5, device=DEV), f32(64, 128), torch.full((64,), 0.5, device=DEV),
+                torch.full((64,), 0.5, device=DEV), torch.full((64,), 0.5, device=DEV), f32(1, 64),
+                torch.full((1,), 0.5, device=DEV)]
+        hip.call("es_dmlp_bwd", hip.ptr(Xd), NF, B, NF, C.byref(prm), hip.ptr(H3), hip.ptr(S3), hip.ptr(H4),
+                 hip.ptr(S4), hip.ptr(LAT), hip.ptr(gout_d), hip.ptr(glat_d), hip.ptr(dX), NF, hip.ptr(part),
+                 *[hip.ptr(o) if want_w else None for o in outs], hip.stream_ptr())
+        if want_dx:
+            assert rel(dX.cpu(), Xr.grad) < 1e-4, (want_dx, want_w)
+        if want_w:
+            for i, (o, r) in enumerate(zip(outs, refs)):
+                got = o.cpu().view(r.shape) - (0.0 if i in (0, 4, 8) else 0.5)
+                assert rel(got, r) < 1e-4, (i, rel(got, r))
+
+
 @pytest.mark.parametrize("case", [(200, 256, 24, 24, 128, 3), (200, 128, 13, 13, 256, 3)])
 def test_conv_ring256_matches_ring128(case):
     """256 x 256 ring tiles with 32-deep K-steps (sub-pixel FWD with 256 output channels, DGRAD
