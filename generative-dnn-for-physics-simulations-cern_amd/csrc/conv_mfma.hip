@@ -43,6 +43,12 @@ constexpr int RT = 512;   // threads per workgroup (8 waves)
 #define ES_RING_LEAN 0   // 256 x 256 tiles: 1 = single fragment set per step (ring_loop_lean)
 #endif
 constexpr int NSLOT = 3;  // ring depth
+// ES_RING_EXP (diagnostic builds only, tools/ring_exp.sh): 1 = every A row gathers image 0 (the A
+// operand stays L2-resident), 2 = no MFMAs, 4 = no epilogue, 8 = no fused statistics, 16 = DGRAD
+// keeps the per-wave staged epilogue (FWD / DGRAD ring kernel)
+#ifndef ES_RING_EXP
+#define ES_RING_EXP 0
+#endif
 constexpr uint32_t OOB = 0x80000000u;   // buffer offset past every num_records (< 2^31 bytes)
 
 // ES_NO_RING=1 (or es_conv_set_ring(0)) routes these shapes to the 4-wave kernels of
@@ -297,7 +303,9 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   constexpr int KH = BK == 64 ? 2 : 1;                   // MFMA K-halves per step
   constexpr int RMF = RM / (3 - KH);                     // A tiles per fragment set
   constexpr int SROWS = WM < 64 ? WM : 64;               // epilogue staging rows per pass
-  constexpr int STAGE = 8 * SROWS * (WN * 4 + 16);
+  constexpr int STAGE0 = 8 * SROWS * (WN * 4 + 16);
+  constexpr int TPITCH = BN * 2 + 16;                    // BK = 32 bf16 epilogue: whole-tile image
+  constexpr int STAGE = BK == 32 && BM * TPITCH > STAGE0 ? BM * TPITCH : STAGE0;
   constexpr int RING = NS * SLOT > STAGE ? NS * SLOT : STAGE;
   // ONE __shared__ object (a second one beside the DMA ring makes hipcc wait vmcnt(0) before
   // every ds_read of the loop): the ring slots (also the epilogue staging), then the fused-stats
@@ -399,7 +407,7 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
     const int pp = pval[j] ? pix : 0;
     const int y = pp / gw, x = pp - y * gw;
     const int img = gi * NG + (pi - ppix * PPG) * PROWS + lrow;
-    alane[j] = (uint32_t)(img * (int)a.as[0] * 2 + lc * 16);   // images >= N: past num_records
+    alane[j] = (uint32_t)(((ES_RING_EXP & 1) ? 0 : img) * (int)a.as[0] * 2 + lc * 16);   // images >= N: past num_records
     if constexpr (MODE == MODE_FWD && SP) {       // source row = u + oh + d
       pc0[j] = y + sp.oh[cls];
       pc1[j] = x + sp.ow[cls];
@@ -541,6 +549,13 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   };
   auto mma = [&](const Frag& f) {
     const int i0 = KH == 2 ? 0 : f.h * RMF;
+    if constexpr ((ES_RING_EXP & 2) != 0) {
+#pragma unroll
+      for (int i = 0; i < RMF; ++i) asm volatile("" ::"v"(f.a[i]));
+#pragma unroll
+      for (int j = 0; j < RN; ++j) asm volatile("" ::"v"(f.b[j]));
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < RMF; ++i)
 #pragma unroll
@@ -554,6 +569,13 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
     ring_loop<PW, 0, NS>(nk, smem, SLOT, issue, load, mma, nofence);
   }
 
+  if constexpr ((ES_RING_EXP & 4) != 0) {
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
   // epilogue.  Wave row r (0..WM-1) = tile row t = wm0 + r: pixel pix0 + t / NG, image
   // NG gi + t % NG.
   const int col16 = lane & 15, rq = (lane >> 4) * 4;
@@ -606,7 +628,7 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
     // BatchNorm statistics of the stored values (conv -> BatchNorm fusion): per column, count /
     // mean / M2 over the wave's valid rows (lanes own 16 rows, Chan-merged across the 4 row
     // groups by shuffles), then across the 4 row waves in LDS -> one [3][Ng] partial per row tile
-    float* part = MODE == MODE_FWD ? a.stats_part : nullptr;   // (FWD only: compiled out of DGRAD)
+    float* part = (MODE == MODE_FWD && !(ES_RING_EXP & 8)) ? a.stats_part : nullptr;   // (FWD only: compiled out of DGRAD)
     float (*st_n)[BN] = (float (*)[BN])(smem + RING);
     float (*st_m)[BN] = st_n + WGM;
     float (*st_q)[BN] = st_n + 2 * WGM;
@@ -617,8 +639,37 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
       for (int i = 0; i < RM; ++i)
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) okr[i][jj] = row_ok(i * 16 + rq + jj);
+      bool allok = true;
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) allok = allok && okr[i][jj];
+      const bool full = __all(allok);   // wave-uniform: no row of the wave is padding
 #pragma unroll
       for (int j = 0; j < RN; ++j) {
+        float n_, m_, q;
+        if (BK == 32 && full) {
+          // 256 x 256 tiles: per column sum and sum of squares of the lane's 32 values (2 VALU per
+          // value; the two-pass Chan form cost ~85 us of conv_layers.5's B = 1024 FWD epilogue),
+          // summed over the 4 row groups, then (count, mean, M2) of the wave's 128 rows
+          float s = 0.f, s2 = 0.f;
+#pragma unroll
+          for (int i = 0; i < RM; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              const float v = acc[i][j][jj];
+              s += v;
+              s2 = fmaf(v, v, s2);
+            }
+#pragma unroll
+          for (int o = 16; o <= 32; o <<= 1) {
+            s += __shfl_xor(s, o, 64);
+            s2 += __shfl_xor(s2, o, 64);
+          }
+          n_ = (float)(RM * 16);
+          m_ = s * (1.f / (RM * 16));
+          q = fmaxf(s2 - s * m_, 0.f);
+        } else {
         float cnt = 0.f, s = 0.f;
 #pragma unroll
         for (int i = 0; i < RM; ++i)
@@ -626,13 +677,13 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
           for (int jj = 0; jj < 4; ++jj)
             if (okr[i][jj]) { cnt += 1.f; s += acc[i][j][jj]; }
         const float mu = cnt > 0.f ? s / cnt : 0.f;
-        float q = 0.f;
+        q = 0.f;
 #pragma unroll
         for (int i = 0; i < RM; ++i)
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj)
             if (okr[i][jj]) { const float e = acc[i][j][jj] - mu; q += e * e; }
-        float n_ = cnt, m_ = mu;
+        n_ = cnt; m_ = mu;
 #pragma unroll
         for (int o = 16; o <= 32; o <<= 1) {
           const float nb = __shfl_xor(n_, o, 64), mb = __shfl_xor(m_, o, 64), qb = __shfl_xor(q, o, 64);
@@ -644,6 +695,7 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
           }
           n_ = nt;
         }
+        }
         if (lane < 16) {
           st_n[wmi][wn0 + j * 16 + col16] = n_;
           st_m[wmi][wn0 + j * 16 + col16] = m_;
@@ -651,6 +703,50 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
         }
       }
     }
+    if (BK == 32 && BN == 256 && (MODE == MODE_FWD || !(ES_RING_EXP & 16)) && a.out_bf16) {
+      // The whole 256 x 256 tile is staged in LDS ([row][256 columns], pitch TPITCH), then every
+      // store instruction writes two full 512-byte rows: tile rows t0 = (2 pp) NG + n and
+      // t0 + NG, i.e. one image at two consecutive pixels.  Consecutive tile rows are different
+      // images (image-minor order), so the per-wave staging below wrote 128-byte pieces of 8
+      // images per instruction; with 1-KiB runs (merged sub-pixel FWD: pixels 2u..2u+3 of one
+      // output row) the conv_layers.0 / .5 FWD epilogues drop from ~170 / ~245 us (B = 1024).
+      __syncthreads();   // every wave is done with the ring slots
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            *(bf16*)(smem + (wm0 + i * 16 + rq + jj) * TPITCH + (wn0 + j * 16 + col16) * 2) = (bf16)acc[i][j][jj];
+      __syncthreads();
+      const int half = lane >> 5, kq = lane & 31;
+      int scls = cls, sch = n0 + kq * 8;          // class / output channel of this lane's chunk
+      if constexpr (SP && MODE == MODE_FWD) {
+        if (a.sp_merge) {
+          scls = sch / a.Ng;
+          sch -= scls * a.Ng;
+        }
+      }
+      const bool colok = sch < a.Ng && scls < 4;
+      int py0 = 0, px0 = 0;
+      if constexpr (SP && MODE == MODE_FWD) {
+        py0 = (scls >> 1) ? sp.p0[2] : sp.p0[0];
+        px0 = (scls & 1) ? sp.q0[1] : sp.q0[0];
+      }
+      for (int q = wid; q < BM / 2; q += 8) {
+        const int t = ((2 * (q >> lgNG) + half) << lgNG) + (q & (NG - 1));
+        const int pix = pix0 + (t >> lgNG), img = gi * NG + (t & (NG - 1));
+        if (colok && pix < PQ && img < d.N) {
+          int y = fdiv(pix, fgw), x = pix - y * gw;
+          if constexpr (SP && MODE == MODE_FWD) {
+            y = py0 + 2 * y;
+            x = px0 + 2 * x;
+          }
+          const int64_t o = (int64_t)img * a.os[0] + (int64_t)y * a.os[2] + (int64_t)x * a.os[3] + sch;
+          *(uint4*)((bf16*)a.out + o) = *(const uint4*)(smem + t * TPITCH + kq * 16);
+        }
+      }
+    } else {
     // stage the wave's tile in LDS (rows of WN values; passes of SROWS rows), then 16-byte
     // row-contiguous stores
     constexpr int PITCH = WN * 4 + 16;
@@ -681,6 +777,7 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
           if (row_ok(ps * SROWS + r))
             *(uint4*)(obase + row_off(ps * SROWS + r) * esz) = *(const uint4*)(stg + r * pitch + lch * 16);
       }
+    }
     }
     if (part && wid < WGN) {   // the waves of row block 0 merge the WGM row waves of their columns
       for (int c = lane; c < WN; c += 64) {
@@ -756,6 +853,14 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
 // XCD are neighbouring pixels of the same images (shared input rows in its L2).
 __device__ __forceinline__ void ds_write_u16(uint32_t addr, uint32_t v) {
   asm volatile("ds_write_b16 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+__device__ __forceinline__ float ds_read_f32_asm(uint32_t addr) {
+  float r;
+  asm volatile("ds_read_b32 %0, %1" : "=v"(r) : "v"(addr) : "memory");
+  return r;
+}
+__device__ __forceinline__ void ds_write_f32_asm(uint32_t addr, float v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(addr), "v"(v) : "memory");
 }
 __device__ __forceinline__ int4v ds_read_b128_asm(uint32_t addr) {
   int4v r;
@@ -968,6 +1073,8 @@ __global__ void __launch_bounds__(RT) conv_persist_kernel(ConvArgs a, int ntiles
     for (int p = 0; p < NST; ++p) vals[p] = ds_read_b128_asm(stg + (p * ORPI + lr) * SPITCH + lch * 16);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
+    for (int p = 0; p < NST; ++p) asm volatile("" : "+v"(vals[p]));   // no use above the wait
+#pragma unroll
     for (int p = 0; p < NST; ++p) {
       const int r = p * ORPI + lr;
       uint32_t voff = OOB;
@@ -1058,6 +1165,330 @@ __global__ void __launch_bounds__(RT) conv_persist_kernel(ConvArgs a, int ntiles
         pp[col] = n_;
         pp[a.Ng + col] = m_;
         pp[2 * a.Ng + col] = q;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// PERSISTENT 256 x 256 merged sub-pixel FWD: the generator's conv_layers.0 / conv_layers.5
+// (neutron/generator.py:25,30; 3x3 over the x2 upsample, run as one GEMM over (class, channel)
+// columns, see conv_ring_kernel).  Measured on the ring kernel at B = 1024 (tools/ring_exp.py with
+// the ES_RING_EXP builds): conv_layers.5 FWD 766 us with its epilogue, 521 us without; the
+// epilogue (bias, statistics, 128 KiB of stores per tile) ran with the CU's MFMAs idle, since a
+// 128 KiB ring leaves one workgroup per CU.  Here
+//   * 256 workgroups (one per CU) loop over row tiles with a FIXED column tile each: the NT column
+//     tiles of a row tile run side by side on one XCD (workgroups lw = NT l + ct), and each XCD
+//     walks a contiguous range of row tiles (neighbouring pixels of the same images share its L2);
+//   * the 4-slot ring (A and B pieces, 32-deep K-steps) continues across tiles: the next tile's
+//     first steps are in flight while the epilogue runs, and its stores drain under the next
+//     tile's MFMAs (fixed-count buffer stores, invalid rows at out-of-range offsets, so the
+//     counted vmcnt waits stay exact: vmcnt retires in issue order across loads, stores, DMA);
+//   * the epilogue stages 16-row passes of each wave's 128 x 64 sub-tile in a private 2.3 KiB LDS
+//     region (inline-asm LDS accesses with explicit lgkmcnt waits) for 16-byte row stores;
+//   * BatchNorm partials: per lane running sums / sums of squares of its 4 columns over all its
+//     tiles (fixed columns), merged across lanes and row waves once at the end: one [3][Ng]
+//     partial per (workgroup, class), chunks = 4 x 256.
+template <int NT>
+__global__ void __launch_bounds__(RT) conv_p256_kernel(ConvArgs a, int R) {
+  constexpr int BM = 256, BN = 256, BK = 32, WGN = 4;
+  constexpr int WM = 128, WN = 64, RM = WM / 16, RN = WN / 16, RMF = RM / 2;
+  constexpr int ROWB = 2 * BK, PROWS = 1024 / ROWB, CPR = ROWB / 16;
+  constexpr int APW = BM / PROWS / 8, BPW = BN / PROWS / 8, PW = APW + BPW;
+  constexpr int NS = 4, ABYTES = BM * ROWB, SLOT = (BM + BN) * ROWB;
+  constexpr int SPITCH = WN * 2 + 16, STAGE = 16 * SPITCH;   // per-wave staging: 16 rows
+  constexpr int NST = WM / 8;                                 // 16-byte stores per tile per wave
+  constexpr int LR = 32 / NT;                                 // workgroups per column tile per XCD
+  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT + 8 * STAGE + BN * 4 + 2 * 3 * BN * 4];
+  const es_conv_desc_t& d = a.d;
+  const SubPixel& sp = a.sp;
+  const int lane = threadIdx.x & 63, wid = uni(threadIdx.x >> 6);
+  const uint32_t sbias = lds_u32(smem + NS * SLOT + 8 * STAGE);   // [BN] floats
+  const uint32_t sst = sbias + BN * 4;                              // [2][3][BN] floats
+  const int wm0 = (wid / WGN) * WM, wn0 = (wid % WGN) * WN;
+  const int lrow = lane / CPR, pc = lane % CPR;
+  const int r16 = lane & 15, g16 = lane >> 4;
+  const uint32_t stg = lds_u32(smem + NS * SLOT + wid * STAGE);
+
+  // work of this workgroup: XCD x (blockIdx % 8) owns row tiles [R x / 8, R (x + 1) / 8); its
+  // workgroup lw = NT l + ct takes column tile ct and every LR-th row tile from l
+  const int xcd = blockIdx.x & 7, lw = blockIdx.x >> 3;
+  const int ct = lw % NT, lr = lw / NT;
+  const int r_lo = (int)(((int64_t)R * xcd) >> 3), r_hi = (int)(((int64_t)R * (xcd + 1)) >> 3);
+  const int my = r_hi - r_lo > lr ? (r_hi - r_lo - lr + LR - 1) / LR : 0;
+  const int n0 = ct * BN;
+  const int NG = a.ng, PPG = NG / PROWS, NB = BM / NG;
+  const int lgNG = uni(31 - __builtin_clz(NG));
+  const int TT = sp.tile0[1], gh = sp.ph[0], gw = sp.pw[0], PQ = gh * gw;
+  const int oh0 = sp.oh[0], ow0 = sp.ow[0], kw = sp.dw[0];
+  const int ldb = sp.dh[0] * sp.dw[0] * d.C, nk = ldb / BK;
+  FastDiv fgw;
+  {
+    uint32_t l = 0;
+    while ((1u << l) < (uint32_t)gw) ++l;
+    fgw.l = uni((int)l);
+    fgw.m = (uint32_t)uni((int)(uint32_t)(((1ull << 32) * ((1ull << l) - (uint32_t)gw)) / (uint32_t)gw + 1));
+  }
+  // the wave's output class and first channel (a wave's 64 columns never straddle a class)
+  const int ecls = (n0 + wn0) / a.Ng, kc0 = n0 + wn0 - ecls * a.Ng;
+  const int py0 = sp.p0[0] + ((ecls >> 1) ? sp.p0[2] - sp.p0[0] : 0);
+  const int px0 = sp.q0[0] + ((ecls & 1) ? sp.q0[1] - sp.q0[0] : 0);
+
+  const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * 2));
+  const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)(sp.tap0[4] * a.Ng * d.C * 2));
+  const __amdgpu_buffer_rsrc_t ores = mkres(a.out, (uint32_t)(d.N * a.os[0] * 2));
+  const int as0b = (int)a.as[0] * 2, as2b = (int)a.as[2] * 2, as3b = (int)a.as[3] * 2;
+  const int os0 = (int)a.os[0], os2 = (int)a.os[2], os3 = (int)a.os[3];   // (N * os0 * 2 < 2^31: host)
+  uint32_t blane[BPW];
+#pragma unroll
+  for (int j = 0; j < BPW; ++j) {
+    const int rr = (wid * BPW + j) * PROWS + lrow;
+    blane[j] = (uint32_t)((n0 + rr) * ldb * 2 + ((pc ^ swz_x<BK>(rr)) * 16));
+  }
+
+  // issue cursor: tile iteration ii, K-step ik = (tap cr, cs; channel cch); per-tap offset cache
+  uint32_t alane[APW], ua_t[APW], ub_t = OOB;
+  int pc0[APW], pc1[APW];
+  bool pval[APW];
+#pragma unroll
+  for (int j = 0; j < APW; ++j) { alane[j] = 0; ua_t[j] = OOB; pc0[j] = pc1[j] = 0; pval[j] = false; }
+  int ii = 0, ik = 0, cr = 0, cs = 0, cch = 0;
+  auto issue = [&](char* slot) {
+    const bool live = ii < my;
+    if (ik == 0 && live) {   // a new tile: its A pieces (wave-uniform branch)
+      const int tl = r_lo + lr + ii * LR;
+      const int gi = tl / TT, pix0 = (tl - gi * TT) * NB;
+#pragma unroll
+      for (int j = 0; j < APW; ++j) {
+        const int pi = wid * APW + j;
+        const int rr = pi * PROWS + lrow;
+        const int ppix = pi / PPG, pix = pix0 + ppix;
+        pval[j] = pix < PQ;
+        const int pp = pval[j] ? pix : 0;
+        const int y = fdiv(pp, fgw), x = pp - y * gw;
+        const int img = gi * NG + (pi - ppix * PPG) * PROWS + lrow;
+        alane[j] = (uint32_t)(img * as0b + ((pc ^ swz_x<BK>(rr)) * 16));   // images >= N: past num_records
+        pc0[j] = y + oh0;
+        pc1[j] = x + ow0;
+      }
+    }
+    if (cch == 0) {   // first step of a tap
+#pragma unroll
+      for (int j = 0; j < APW; ++j) {
+        const int hs = pc0[j] + cr, ws = pc1[j] + cs;
+        const bool ok = live && pval[j] && (unsigned)hs < (unsigned)d.H && (unsigned)ws < (unsigned)d.W;
+        ua_t[j] = ok ? (uint32_t)(hs * as2b + ws * as3b) : OOB;
+      }
+      ub_t = live ? (uint32_t)((cr * kw + cs) * d.C * 2) : OOB;
+    }
+    const uint32_t co = (uint32_t)(cch * 2);
+#pragma unroll
+    for (int j = 0; j < APW; ++j) bdma16(ares, alane[j] + (ua_t[j] + co), slot + (wid * APW + j) * 1024);
+#pragma unroll
+    for (int j = 0; j < BPW; ++j) bdma16(bres, blane[j] + (ub_t + co), slot + ABYTES + (wid * BPW + j) * 1024);
+    cch += BK;
+    if (cch == d.C) {
+      cch = 0;
+      if (++cs == kw) { cs = 0; ++cr; }
+    }
+    if (++ik == nk) { ik = 0; ++ii; cr = cs = cch = 0; }
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // bias of the lane's columns and the running statistics (sum, sum of squares, count)
+  // the column tile's bias and the workgroup's statistics accumulators [2 row waves][3][BN] in LDS
+  // (nothing of the epilogue stays in registers across the main loop), written through inline asm
+  // like every epilogue LDS access (invisible to hipcc's DMA wait insertion)
+  if (threadIdx.x < BN) {
+    const int gcol = n0 + threadIdx.x;
+    ds_write_f32_asm(sbias + threadIdx.x * 4, a.bias ? a.bias[gcol - (gcol / a.Ng) * a.Ng] : 0.f);
+  }
+  for (int i = threadIdx.x; i < 2 * 3 * BN; i += RT) ds_write_f32_asm(sst + i * 4, 0.f);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const bool want_stats = a.stats_part != nullptr;
+
+  struct Frag {
+    bf16x8 a[RMF], b[RN];
+  };
+  auto load = [&](Frag& f, const char* slot, int kk) {
+#pragma unroll
+    for (int i = 0; i < RMF; ++i) f.a[i] = *(const bf16x8*)(slot + swz<BK>(wm0 + (kk * RMF + i) * 16 + r16, g16));
+#pragma unroll
+    for (int j = 0; j < RN; ++j) f.b[j] = *(const bf16x8*)(slot + ABYTES + swz<BK>(wn0 + j * 16 + r16, g16));
+  };
+  auto mma = [&](const Frag& f, int kk) {
+#pragma unroll
+    for (int i = 0; i < RMF; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+        acc[kk * RMF + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[j], acc[kk * RMF + i][j], 0, 0, 0);
+  };
+
+  auto epilogue = [&](int ci) {
+    const int tl = r_lo + lr + ci * LR;
+    const int gi = tl / TT, pix0 = (tl - gi * TT) * NB;
+    // per-lane values laundered through an empty asm: otherwise hipcc hoists the epilogue's
+    // lane-constant addresses out of the main loop and spills them across it
+    int le = lane;
+    uint32_t stg_e = stg;
+    asm volatile("" : "+v"(le), "+v"(stg_e));
+    const int col16 = le & 15, rq = (le >> 4) * 4;
+    float bcol[RN];
+#pragma unroll
+    for (int j = 0; j < RN; ++j) bcol[j] = ds_read_f32_asm(sbias + (wn0 + j * 16 + col16) * 4);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // (every value an asm LDS read returned is passed through an empty asm after the wait, so no
+    // use of it can be scheduled above the wait)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) asm volatile("" : "+v"(bcol[j]));
+    // store lanes: row lr8 (+ 8) of a pass, 16-byte chunk lch of the wave's 64 columns
+    const int lr8 = le & 7, lch = le >> 3;
+    float ts[8], ts2[8], npad = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ts[k] = ts2[k] = 0.f;
+    // 8 passes of 16 rows: bias + rounding, stage (row pitch SPITCH), then two 16-byte stores of
+    // 8 rows each; the statistics accumulate from the stored rows (channels lch*8 .. of the lane)
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          const bf16 vb = (bf16)(acc[i][j][jj] + bcol[j]);
+          ds_write_u16(stg_e + (rq + jj) * SPITCH + (j * 16 + col16) * 2, (uint32_t)__builtin_bit_cast(uint16_t, vb));
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      int4v v0 = ds_read_b128_asm(stg_e + lr8 * SPITCH + lch * 16);
+      int4v v1 = ds_read_b128_asm(stg_e + (lr8 + 8) * SPITCH + lch * 16);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      asm volatile("" : "+v"(v0), "+v"(v1));
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        // branch-free: the address is computed for every row, padding rows store out of range
+        const int t = wm0 + i * 16 + p * 8 + lr8;
+        const int pix = pix0 + (t >> lgNG), img = gi * NG + (t & (NG - 1));
+        const bool ok = pix < PQ && img < d.N;
+        const int yy = fdiv(pix, fgw), xx = pix - yy * gw;
+        const uint32_t voff = ok ? (uint32_t)(img * os0 + (py0 + 2 * yy) * os2 + (px0 + 2 * xx) * os3 + kc0 + lch * 8) * 2u : OOB;
+        const int4v vv = p ? v1 : v0;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, vv), ores, voff, 0, 0);
+        // a padding row gathered only zeros (out-of-range DMA), so its value is exactly
+        // bf16(bias): summed with the rest, counted, and subtracted at the end of the tile
+        npad += ok ? 0.f : 1.f;
+        if (want_stats) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float lo = __uint_as_float((uint32_t)vv[k] << 16), hi = __uint_as_float((uint32_t)vv[k] & 0xFFFF0000u);
+            ts[2 * k] += lo;
+            ts2[2 * k] = fmaf(lo, lo, ts2[2 * k]);
+            ts[2 * k + 1] += hi;
+            ts2[2 * k + 1] = fmaf(hi, hi, ts2[2 * k + 1]);
+          }
+        }
+      }
+    }
+    if (want_stats) {
+      // the 8 row lanes of a chunk (lane bits 0..2), then lane lr8 == 0 adds the wave's totals of
+      // its 8 channels into the row wave's LDS accumulators (one owner per address: deterministic)
+#pragma unroll
+      for (int o = 1; o <= 4; o <<= 1) {
+        npad += __shfl_xor(npad, o, 64);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          ts[k] += __shfl_xor(ts[k], o, 64);
+          ts2[k] += __shfl_xor(ts2[k], o, 64);
+        }
+      }
+      if (lr8 == 0) {
+        const int wmi = wid / WGN;
+        const uint32_t base = sst + (wmi * 3 * BN + wn0 + lch * 8) * 4;
+        float o0[8], o1[8], o2[8], bb[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          o0[k] = ds_read_f32_asm(base + k * 4);
+          o1[k] = ds_read_f32_asm(base + (BN + k) * 4);
+          o2[k] = ds_read_f32_asm(base + (2 * BN + k) * 4);
+          bb[k] = ds_read_f32_asm(sbias + (wn0 + lch * 8 + k) * 4);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(o0[k]), "+v"(o1[k]), "+v"(o2[k]), "+v"(bb[k]));
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float vb = (float)(bf16)bb[k];
+          ds_write_f32_asm(base + k * 4, o0[k] + ((float)WM - npad));
+          ds_write_f32_asm(base + (BN + k) * 4, o1[k] + (ts[k] - npad * vb));
+          ds_write_f32_asm(base + (2 * BN + k) * 4, o2[k] + (ts2[k] - npad * vb * vb));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  // the ring (ring_loop_lean's single fragment set: register room for the epilogue), continued
+  // across the workgroup's tiles
+  const int nsteps = my * nk;
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i) issue(smem + i * SLOT);
+  int cur = 0, prv = NS - 1, ck = 0, ci = 0, last_epi = -1000;
+  for (int s = 0; s < nsteps; ++s) {
+    // step s landed: younger than its DMA are the NS - 2 later steps' pieces and, when an
+    // epilogue ran within the last NS - 1 iterations (after step s was issued), its NST stores
+    if (s - last_epi <= NS - 1) wait_vmcnt<(NS - 2) * PW + NST>();
+    else wait_vmcnt<(NS - 2) * PW>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of step s - 1 are done
+    ring_barrier();
+    issue(smem + prv * SLOT);                            // step s + NS - 1 into step s - 1's slot
+    Frag f;
+    load(f, smem + cur * SLOT, 0);
+    mma(f, 0);
+    load(f, smem + cur * SLOT, 1);
+    mma(f, 1);
+    if (++ck == nk) {
+      epilogue(ci);
+      ck = 0;
+      ++ci;
+      last_epi = s;
+    }
+    prv = cur;
+    cur = cur == NS - 1 ? 0 : cur + 1;
+  }
+  wait_vmcnt<0>();   // every DMA (zero-fill steps included) and store retired
+  if (want_stats) {
+    // merge the 2 row waves' accumulators -> (count, mean, M2) per (workgroup, class)
+    __syncthreads();
+    for (int col = threadIdx.x; col < BN; col += RT) {
+      float v[6];
+#pragma unroll
+      for (int q = 0; q < 6; ++q) v[q] = ds_read_f32_asm(sst + (q * BN + col) * 4);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int q = 0; q < 6; ++q) asm volatile("" : "+v"(v[q]));
+      const float n_ = v[0] + v[3], s_ = v[1] + v[4], q_ = v[2] + v[5];
+      const float mu = n_ > 0.f ? s_ / n_ : 0.f;
+      const int gcol = n0 + col, cc = gcol / a.Ng, ch = gcol - cc * a.Ng;
+      float* pp = a.stats_part + ((int64_t)blockIdx.x * 4 + cc) * 3 * a.Ng;
+      pp[ch] = n_;
+      pp[a.Ng + ch] = mu;
+      pp[2 * a.Ng + ch] = fmaxf(q_ - s_ * mu, 0.f);
+    }
+    // the classes outside this column tile: empty partials
+    const int c_lo = n0 / a.Ng, c_hi = (n0 + BN - 1) / a.Ng;
+    for (int idx = threadIdx.x; idx < 4 * a.Ng; idx += RT) {
+      const int cc = idx / a.Ng, ch = idx - cc * a.Ng;
+      if (cc < c_lo || cc > c_hi) {
+        float* pp = a.stats_part + ((int64_t)blockIdx.x * 4 + cc) * 3 * a.Ng;
+        pp[ch] = 0.f;
+        pp[a.Ng + ch] = 0.f;
+        pp[2 * a.Ng + ch] = 0.f;
       }
     }
   }
@@ -1276,6 +1707,8 @@ bool g_sp_merge = [] { const char* e = getenv("ES_SP_MERGE"); return !(e && e[0]
 // its DGRAD (4 K-steps, 128 columns) drops from 387 to 259 us
 bool g_persist = [] { const char* e = getenv("ES_PERSIST"); return !(e && e[0] == '0'); }();
 bool g_persist_fwd = [] { const char* e = getenv("ES_PERSIST_FWD"); return e && e[0] == '1'; }();
+// persistent 256 x 256 merged sub-pixel FWD (conv_p256_kernel); ES_P256=0 keeps the ring kernel (A/B)
+bool g_p256 = [] { const char* e = getenv("ES_P256"); return !(e && e[0] == '0'); }();
 
 }  // namespace
 
@@ -1326,6 +1759,12 @@ extern "C" int es_conv_set_persist(int on) {
   const int old = (g_persist ? 1 : 0) | (g_persist_fwd ? 2 : 0);
   g_persist = (on & 1) != 0;
   g_persist_fwd = (on & 2) != 0;
+  return old;
+}
+
+extern "C" int es_conv_set_p256(int on) {
+  const int old = g_p256;
+  g_p256 = on != 0;
   return old;
 }
 
@@ -1469,6 +1908,19 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
     g_stats_req.chunks = chunks;
   }
   if (a.sp_merge) {   // (vec_out: the merged epilogue is the staged one)
+    const int NT = 4 * a.Ng / 256;
+    if (g_p256 && (4 * a.Ng) % 256 == 0 && (NT == 1 || NT == 2 || NT == 4) && row_tiles >= 64 && a.out_bf16 &&
+        (int64_t)d.N * a.os[0] * 2 < (1ll << 31)) {
+      a.stats_part = nullptr;
+      if (g_stats_req.part && (int64_t)256 * 4 * 3 * a.Ng <= g_stats_req.floats) {
+        a.stats_part = g_stats_req.part;
+        g_stats_req.chunks = 256 * 4;
+      }
+      if (NT == 1) hipLaunchKernelGGL((conv_p256_kernel<1>), dim3(256), dim3(RT), 0, st, a, row_tiles);
+      else if (NT == 2) hipLaunchKernelGGL((conv_p256_kernel<2>), dim3(256), dim3(RT), 0, st, a, row_tiles);
+      else hipLaunchKernelGGL((conv_p256_kernel<4>), dim3(256), dim3(RT), 0, st, a, row_tiles);
+      return 1;
+    }
     dim3 grid(row_tiles, (4 * a.Ng + 255) / 256, 1);
     hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 256, true, 32>), grid, dim3(RT), 0, st, a);
     return 1;

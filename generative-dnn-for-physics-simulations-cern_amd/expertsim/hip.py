@@ -79,6 +79,7 @@ _SIGS = {
     "es_conv_set_subpixel": (C.c_int, [C.c_int]),
     "es_conv_set_ring256": (C.c_int, [C.c_int]),
     "es_conv_set_persist": (C.c_int, [C.c_int]),
+    "es_conv_set_p256": (C.c_int, [C.c_int]),
     "es_conv_subpixel_ok": (C.c_int, [P, C.c_int]),
     "es_subpixel_taps": (C.c_int, [C.c_int, C.c_int]),
     "es_conv2d_fwd": (C.c_int, [P, C.c_int, P, P, P, P, P, C.c_int, P, P]),

@@ -105,6 +105,10 @@ int es_conv_set_ring256(int on);
  * accumulation order: bit-identical outputs; the fused BatchNorm partials are per workgroup
  * instead of per row tile).  Returns the previous setting. */
 int es_conv_set_persist(int on);
+/* Persistent 256 x 256 kernel for the merged sub-pixel FWD (conv_mfma.hip conv_p256_kernel:
+ * generator conv_layers.0 / .5): 1 = on (default), 0 = the per-tile ring kernel (same accumulation
+ * order: bit-identical outputs).  Returns the previous setting. */
+int es_conv_set_p256(int on);
 /* Sub-pixel decomposition of stride-1 convs over a x2 nearest upsample (conv_mfma.hip): 1 = on
  * (default; wgrad uses it internally, fwd/dgrad when the caller packs mode 2/3 weights and sets
  * desc->subpixel), 0 = off.  Returns the previous setting. */

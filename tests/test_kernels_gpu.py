@@ -759,6 +759,45 @@ def test_conv_persist_matches_ring(case):
     assert rel(outs[0][2], yr.mean((0, 2, 3)).cpu()) < 1e-2
 
 
+@pytest.mark.parametrize("case", [(70, 256, 24, 24, 128), (130, 128, 13, 13, 256), (600, 64, 20, 20, 64)])
+def test_conv_p256_matches_ring(case):
+    """The persistent 256 x 256 merged sub-pixel FWD (generator conv_layers.0 / .5: workgroups with
+    a fixed column tile looping over row tiles, the ring continued across tiles) accumulates in the
+    ring kernel's K order: bf16 output bit-identical (padding images past N and pixels past the
+    class grid included); fused BatchNorm statistics (per (workgroup, class) partials, padding rows
+    subtracted) equal up to the merge order, and close to torch fp32."""
+    hip = _hip()
+    from expertsim.layers import Act, ConvOp, NormOp, Upsample
+    N, Cin, H, W, Cout = case
+    torch.manual_seed(11)
+    w = torch.randn(Cout, Cin, 3, 3, device=DEV) / np.sqrt(Cin * 9)
+    b = torch.randn(Cout, device=DEV) + 1.0
+    op = ConvOp(torch.nn.Parameter(w), torch.nn.Parameter(b), upsample=Upsample((H, W), scale=(2, 2)))
+    xa = Act.nhwc(N, Cin, H, W, torch.bfloat16, DEV)
+    xa.t.normal_()
+    outs = []
+    old = hip.lib().es_conv_set_p256(1)
+    try:
+        for on in (1, 0):
+            hip.lib().es_conv_set_p256(on)
+            ya = op.fwd(xa, out_dtype=torch.bfloat16, bn_stats=True)
+            assert ya.bn_part is not None
+            # the persistent kernel writes 4 partials per workgroup (256 workgroups)
+            assert (ya.bn_part[1] == 1024) == (on == 1)
+            nm = NormOp(hip.NORM_BN, torch.ones(Cout, device=DEV), torch.zeros(Cout, device=DEV),
+                        running_mean=torch.zeros(Cout, device=DEV), running_var=torch.ones(Cout, device=DEV))
+            m, istd = nm.stats(ya)
+            torch.cuda.synchronize()
+            outs.append((ya.t.clone(), m.cpu(), istd.cpu(), ya))
+    finally:
+        hip.lib().es_conv_set_p256(old)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert rel(outs[0][1], outs[1][1]) < 1e-5 and rel(outs[0][2], outs[1][2]) < 1e-5
+    yb = outs[0][3].torch_nchw().float()
+    assert rel(outs[0][1], yb.mean((0, 2, 3)).cpu()) < 1e-5
+    assert rel(outs[0][2], (1.0 / torch.sqrt(yb.var((0, 2, 3), unbiased=False) + 1e-5)).cpu()) < 1e-4
+
+
 @pytest.mark.parametrize("shape", [(5, 128, 13, 13), (3, 70, 9, 7), (2, 3, 5, 4)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_copy_relayout(shape, dtype):
