@@ -15,7 +15,7 @@ import sys
 # neutron generator conv shapes (Cin, Hin, Win, Cout, Hout, Wout, k) -- generator.py:41-47
 LAYERS = {"c0": (128, 13, 13, 256, 24, 24, 3), "c5": (256, 24, 24, 128, 46, 46, 3),
           "c9": (128, 46, 46, 64, 45, 45, 2)}
-KERNEL = ("conv_ring_kernel", "wgrad_ring_kernel", "conv_igemm_kernel", "conv_persist_kernel")
+KERNEL = ("conv_ring_kernel", "wgrad_ring_kernel", "conv_igemm_kernel", "conv_persist_kernel", "conv_p256_kernel")
 
 
 def _match(name):
