@@ -63,7 +63,28 @@ struct ConvArgs {
                        // many tiles per class (the 4 classes of the same source pixels adjacent)
   int sp_merge;        // ring SP FWD with 4 identical class geometries: ONE GEMM whose columns are
                        // (class, out-channel) (4*Ng columns; the classes share the source gather)
+  // persistent DGRAD fused with the reduction pass of the BatchNorm backward that consumes its
+  // output (es_conv2d_dgrad_bnred): x = the norm's input h (same layout as the dgrad output), its
+  // dropout keep bits and statistics; per workgroup sums of dnorm and dnorm*xhat -> bnr_part
+  const void* bnr_x;
+  const uint8_t* bnr_keep;
+  const float *bnr_mean, *bnr_invstd, *bnr_gamma, *bnr_beta;
+  float bnr_scale, bnr_slope;   // dropout 1/(1-p) (1 without dropout), LeakyReLU slope
+  int bnr_dfirst, bnr_drop;
+  float* bnr_part;              // [workgroup][3][Ng] (slots 1, 2: the two sums)
 };
+
+// es_conv2d_dgrad_bnred: the caller's request (host, per thread); the persistent DGRAD launch
+// sets chunks when it wrote the sums
+struct BnRedRequest {
+  const void* x;
+  const es_norm_t* nm;
+  const es_chain_t* ch;
+  float* part;
+  int64_t floats;
+  int chunks;
+};
+extern thread_local BnRedRequest g_bnr_req;
 
 
 // es_conv2d_fwd_stats: the caller's request for fused BatchNorm partials (host, per thread); the

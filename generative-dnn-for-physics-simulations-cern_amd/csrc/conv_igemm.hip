@@ -1070,6 +1070,18 @@ extern "C" int es_conv2d_dgrad(const es_conv_desc_t* d, es_dtype_t dt, const voi
   return dispatch<MODE_DGRAD>(a, dt, avec, bvec, (hipStream_t)stream);
 }
 
+extern "C" int es_conv2d_dgrad_bnred(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, const int64_t ys[4],
+                                     const void* wd, void* dx, es_dtype_t dxdt, const int64_t dxs[4],
+                                     const void* x, const es_norm_t* nm, const es_chain_t* ch, float* part,
+                                     int64_t part_floats, int* chunks, es_stream_t stream) {
+  ES_CHECK_ARG(part && chunks && x && nm && ch, "conv dgrad bnred: NULL argument");
+  g_bnr_req = BnRedRequest{x, nm, ch, part, part_floats, 0};
+  const int rc = es_conv2d_dgrad(d, dt, dy, ys, wd, dx, dxdt, dxs, 0.f, stream);
+  *chunks = g_bnr_req.chunks;
+  g_bnr_req = BnRedRequest{nullptr, nullptr, nullptr, nullptr, 0, 0};
+  return rc;
+}
+
 extern "C" int es_conv2d_wgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy,
                                const int64_t ys[4], const void* x, const int64_t xs[4], float* dw,
                                es_stream_t stream) {

@@ -867,8 +867,20 @@ __device__ __forceinline__ int4v ds_read_b128_asm(uint32_t addr) {
   asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr) : "memory");
   return r;
 }
+__device__ __forceinline__ uint32_t ds_read_u8_asm(uint32_t addr) {
+  uint32_t r;
+  asm volatile("ds_read_u8 %0, %1" : "=v"(r) : "v"(addr) : "memory");
+  return r;
+}
 
-template <int MODE, int BN>
+// BNR (DGRAD only): the epilogue also runs the reduction pass of the BatchNorm backward that reads
+// this dgrad's output dy (norm_fast.hip bn_reduce_fast, MODE 1): per channel sum of dnorm and
+// dnorm * xhat, dnorm = d(chain)/dz * dy at z = gamma * xhat + beta, xhat = (h - mean) * invstd,
+// with the stored bf16 dy values and the forward's dropout keep bits.  Each tile's epilogue issues
+// LDS-DMA of the h rows (and keep bytes) its lanes just stored dy for into the wave's staging
+// region; the NEXT tile's epilogue consumes them (by then the DMA has long landed, so the ring never
+// drains for it) before it stages its own accumulators there.  The dgrad output is unchanged.
+template <int MODE, int BN, bool BNR = false>
 __global__ void __launch_bounds__(RT) conv_persist_kernel(ConvArgs a, int ntiles) {
   constexpr int BM = 128, BK = 64, WGM = 4, WGN = 2;
   constexpr int WM = BM / WGM, WN = BN / WGN;              // 32 x 32 (BN 64) / 32 x 64 (BN 128)
@@ -881,6 +893,11 @@ __global__ void __launch_bounds__(RT) conv_persist_kernel(ConvArgs a, int ntiles
   constexpr int SPITCH = WN * 2 + 16, STAGE = WM * SPITCH; // per-wave bf16 staging
   constexpr int OCPR = WN * 2 / 16, ORPI = 64 / OCPR, NST = WM / ORPI;   // 16-byte stores per tile
   constexpr int STB = 3 * WGM * BN * 4;
+  // BNR: per wave NST x 1 KiB of h rows (lane-linear: piece p, lane l = the row / chunk the lane
+  // stored in pass p) + 256 B of keep bytes ([32 rows][WN / 8]) in the staging region
+  constexpr int KOFF = NST * 1024, KB = WN / 8, DPR = KB / 4;
+  constexpr int NH = BNR ? NST + 1 : 0;                    // epilogue DMA ops (h pieces + keep)
+  static_assert(!BNR || (MODE == MODE_DGRAD && KOFF + 256 <= STAGE && KB % 4 == 0), "BNR staging");
   __shared__ __attribute__((aligned(16))) char smem[PANEL + NS * ABYTES + 8 * STAGE + STB];
   char* const panel = smem;
   char* const ring = smem + PANEL;
@@ -987,6 +1004,58 @@ __global__ void __launch_bounds__(RT) conv_persist_kernel(ConvArgs a, int ntiles
   for (int j = 0; j < RN; ++j) bcol[j] = (MODE == MODE_FWD && a.bias) ? a.bias[wn0 + j * 16 + (lane & 15)] : 0.f;
   const bool want_stats = MODE == MODE_FWD && a.stats_part != nullptr;
   const int r16 = lane & 15, g16 = lane >> 4, col16 = lane & 15, rq = (lane >> 4) * 4;
+  const int elr = lane / OCPR, elch = lane % OCPR;        // epilogue: row pass / 8-channel chunk
+  // BNR: the lane's 8 channels are fixed (wn0 + 8 elch ..), so are their statistics (loaded before
+  // the ring starts, like bcol)
+  float bmu[8], bis[8], bsc[8], bsh[8], bs1[8], bs2[8];
+  int4v pdy[NST];                                         // the previous tile's stored dy
+  const __amdgpu_buffer_rsrc_t hres = mkres(a.bnr_x, BNR ? (uint32_t)(d.N * a.os[0] * 2) : 0u);
+  const __amdgpu_buffer_rsrc_t kres = mkres(a.bnr_keep, BNR ? (uint32_t)((int64_t)d.N * PQ * (a.Ng / 8)) : 0u);
+  if constexpr (BNR) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = wn0 + elch * 8 + k;
+      bmu[k] = a.bnr_mean[c];
+      bis[k] = a.bnr_invstd[c];
+      const float s = (a.bnr_gamma ? a.bnr_gamma[c] : 1.f) * bis[k];
+      bsc[k] = s;
+      bsh[k] = (a.bnr_beta ? a.bnr_beta[c] : 0.f) - bmu[k] * s;
+      bs1[k] = bs2[k] = 0.f;
+    }
+#pragma unroll
+    for (int p = 0; p < NST; ++p) pdy[p] = int4v{0, 0, 0, 0};
+  }
+  char* const stgp = ring + NS * ABYTES + wid * STAGE;
+  // BNR: fold the previous tile's dy (pdy) with its h / keep bytes (landed in this wave's staging
+  // region) into the per-lane sums; same expressions as bn_reduce_fast (norm_fast.hip)
+  auto bnr_consume = [&]() {
+    int4v hv[NST];
+    uint32_t kb[NST];
+#pragma unroll
+    for (int p = 0; p < NST; ++p) {
+      const int r = p * ORPI + elr;
+      hv[p] = ds_read_b128_asm(stg + r * (WN * 2) + elch * 16);
+      kb[p] = ds_read_u8_asm(stg + KOFF + r * KB + elch);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int p = 0; p < NST; ++p) {
+      asm volatile("" : "+v"(hv[p]), "+v"(kb[p]));
+      const bf16x8 h8 = __builtin_bit_cast(bf16x8, hv[p]), d8 = __builtin_bit_cast(bf16x8, pdy[p]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float v = (float)h8[k], dy = (float)d8[k];
+        const bool keep = !a.bnr_drop || ((kb[p] >> k) & 1u);
+        const float z = v * bsc[k] + bsh[k];
+        const float zs = a.bnr_drop && a.bnr_dfirst ? z * a.bnr_scale : z;
+        const float dsc = a.bnr_drop ? a.bnr_scale : 1.f;
+        const float dn = keep ? dy * (zs > 0.f ? 1.f : a.bnr_slope) * dsc : 0.f;
+        const float xh = (v - bmu[k]) * bis[k];
+        bs1[k] += dn;
+        bs2[k] += dn * xh;
+      }
+    }
+  };
   struct Frag {
     bf16x8 a[RM], b[RN];
   };
@@ -1012,6 +1081,13 @@ __global__ void __launch_bounds__(RT) conv_persist_kernel(ConvArgs a, int ntiles
     auto row_pix = [&](int r) { return pix0 + ((wm0 + r) >> lgNG); };
     auto row_img = [&](int r) { return gi * NG + ((wm0 + r) & (NG - 1)); };
     auto row_ok = [&](int r) { return row_pix(r) < PQ && row_img(r) < d.N; };
+    if constexpr (BNR) {
+      if (ci > 0) {
+        // the previous tile's h / keep DMA: older than the NS - 1 steps issued since (nk >= NS - 1)
+        wait_vmcnt<(NS - 1) * APW>();
+        bnr_consume();
+      }
+    }
 #pragma unroll
     for (int j = 0; j < RN; ++j) {
 #pragma unroll
@@ -1067,13 +1143,14 @@ __global__ void __launch_bounds__(RT) conv_persist_kernel(ConvArgs a, int ntiles
           ds_write_u16(stg + (i * 16 + rq + jj) * SPITCH + (j * 16 + col16) * 2, (uint32_t)__builtin_bit_cast(uint16_t, v));
         }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const int lr = lane / OCPR, lch = lane % OCPR;
+    const int lr = elr, lch = elch;
     int4v vals[NST];
 #pragma unroll
     for (int p = 0; p < NST; ++p) vals[p] = ds_read_b128_asm(stg + (p * ORPI + lr) * SPITCH + lch * 16);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int p = 0; p < NST; ++p) asm volatile("" : "+v"(vals[p]));   // no use above the wait
+    uint32_t voffs[NST];
 #pragma unroll
     for (int p = 0; p < NST; ++p) {
       const int r = p * ORPI + lr;
@@ -1084,7 +1161,22 @@ __global__ void __launch_bounds__(RT) conv_persist_kernel(ConvArgs a, int ntiles
         const int64_t off = (int64_t)row_img(r) * a.os[0] + (int64_t)y * a.os[2] + (int64_t)x * a.os[3] + wn0 + lch * 8;
         voff = (uint32_t)(off * 2);
       }
+      voffs[p] = voff;
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, vals[p]), ores, voff, 0, 0);
+    }
+    if constexpr (BNR) {
+      // this tile's h rows (the stored dy's positions: h has the output's layout) and keep bytes
+      // -> the wave's staging region, consumed by the next epilogue (or after the loop)
+#pragma unroll
+      for (int p = 0; p < NST; ++p) {
+        pdy[p] = vals[p];
+        bdma16(hres, voffs[p], stgp + p * 1024);
+      }
+      const int kr = lane / DPR;
+      uint32_t koff = OOB;
+      if (kr < WM && row_ok(kr))
+        koff = (uint32_t)(((int64_t)row_img(kr) * PQ + row_pix(kr)) * (a.Ng / 8) + (wn0 / 8) + (lane % DPR) * 4);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(kres, (lds_void*)(stgp + KOFF), 4, (int)koff, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < RM; ++i)
@@ -1097,8 +1189,9 @@ __global__ void __launch_bounds__(RT) conv_persist_kernel(ConvArgs a, int ntiles
   int cur = 0, prv = NS - 1, ck = 0, ci = 0, last_epi = -1000;
   for (int s = 0; s < nsteps; ++s) {
     // step s landed: younger than its DMA are the NS - 2 later steps' pieces and, when an epilogue
-    // ran within the last NS - 1 iterations (after step s was issued), its NST stores
-    if (s - last_epi <= NS - 1) wait_vmcnt<(NS - 2) * APW + NST>();
+    // ran within the last NS - 1 iterations (after step s was issued), its NST stores (+ BNR: its
+    // NH h / keep DMA ops)
+    if (s - last_epi <= NS - 1) wait_vmcnt<(NS - 2) * APW + NST + NH>();
     else wait_vmcnt<(NS - 2) * APW>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of step s - 1 are done
     ring_barrier();
@@ -1120,6 +1213,43 @@ __global__ void __launch_bounds__(RT) conv_persist_kernel(ConvArgs a, int ntiles
     cur = cur == NS - 1 ? 0 : cur + 1;
   }
   wait_vmcnt<0>();
+  if constexpr (BNR) {
+    if (my > 0) bnr_consume();   // the last tile's rows
+    // the workgroup's sums: the 64 / OCPR lanes of one channel chunk, then the WGM row waves
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int o = OCPR; o < 64; o <<= 1) {
+        bs1[k] += __shfl_xor(bs1[k], o, 64);
+        bs2[k] += __shfl_xor(bs2[k], o, 64);
+      }
+    float (*s1w)[BN] = (float (*)[BN])stb;
+    float (*s2w)[BN] = s1w + WGM;
+    const int wmi = wid / WGN;
+    __syncthreads();
+    if (lane < OCPR) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s1w[wmi][wn0 + lane * 8 + k] = bs1[k];
+        s2w[wmi][wn0 + lane * 8 + k] = bs2[k];
+      }
+    }
+    __syncthreads();
+    if (wid < WGN) {
+      for (int c = lane; c < WN; c += 64) {
+        const int col = wn0 + c;
+        float t1 = 0.f, t2 = 0.f;
+        for (int w = 0; w < WGM; ++w) {
+          t1 += s1w[w][col];
+          t2 += s2w[w][col];
+        }
+        float* pp = a.bnr_part + (int64_t)blockIdx.x * 3 * a.Ng;
+        pp[col] = 0.f;
+        pp[a.Ng + col] = t1;
+        pp[2 * a.Ng + col] = t2;
+      }
+    }
+  }
   if (want_stats) {   // the workgroup's partial: merge the WGM row waves of each column
     float (*st_n)[BN] = (float (*)[BN])stb;
     float (*st_m)[BN] = st_n + WGM;
@@ -1502,9 +1632,15 @@ __global__ void __launch_bounds__(RT) conv_p256_kernel(ConvArgs a, int R) {
 // SP: the tile's tap is a (class, d, e) tap of the sub-pixel decomposition; its K runs over the
 // class's output pixels, and the epilogue adds the tile into every original tap (r, s) the
 // combined tap covers (r in {2d - a, 2d - a + 1} within [0, R), likewise s).
+// MT (multi-tap; stride 1, pad 0, no upsample, C | BN): the tile's BN columns span BN / C taps.
+// Every tap of a valid output pixel is in range, so a lane's 16-byte chunk carries its tap's
+// (r, s) offset in its per-lane base and the per-step gather offset stays wave-uniform: one tile
+// reads dy once for BN / C taps (generator conv_layers.9, 2 x 2 taps x 128 channels: BN = 256 halves
+// the dy and x re-reads of the one-tap 128-column tiles).
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, bool SP>
+template <int BM, int BN, bool SP, bool MT = false>
 __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
+  static_assert(!(SP && MT), "multi-tap tiles are for plain convs");
   constexpr int WGM = BM >= 64 ? BM / 64 : 1, WGN = 8 / WGM;   // waves along M / N
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int RM = WM / 16, RN = WN / 16;
@@ -1559,7 +1695,14 @@ __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
 #pragma unroll
   for (int j = 0; j < BPW; ++j) {
     const int kr = (wid * BPW + j) * (64 / BLPR) + lane / BLPR;
-    blane[j] = (uint32_t)(kr * bs0b + (cb + ((lane % BLPR) ^ swz_tr<BN>(kr)) * 8) * 2);
+    const int chg = (lane % BLPR) ^ swz_tr<BN>(kr);
+    if constexpr (MT) {
+      const int gcol = n0 + chg * 8, rsl = gcol / d.C, cl = gcol - rsl * d.C;
+      const int trl = rsl / d.S, tsl = rsl - trl * d.S;
+      blane[j] = (uint32_t)(kr * bs0b + cl * 2 + trl * bs2b + tsl * bs3b);
+    } else {
+      blane[j] = (uint32_t)(kr * bs0b + (cb + chg * 8) * 2);
+    }
   }
 
   // K-step cursor (uniform): pixel (p, q) of the grid and image group gi of step t = (p*gq + q)*G + gi
@@ -1581,6 +1724,9 @@ __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
       const int hs = cp + coh + tr, ws = cq + cow + ts;
       const bool ok = live && (unsigned)hs < (unsigned)d.H && (unsigned)ws < (unsigned)d.W;
       ub = ok ? (uint32_t)(cg * 64 * bs0b + hs * bs2b + ws * bs3b) : OOB;
+    } else if constexpr (MT) {   // (the taps' offsets are in blane)
+      ua = live ? (uint32_t)(cg * 64 * as0b + cp * as2b + cq * as3b) : OOB;
+      ub = live ? (uint32_t)(cg * 64 * bs0b + cp * bs2b + cq * bs3b) : OOB;
     } else {
       ua = live ? (uint32_t)(cg * 64 * as0b + cp * as2b + cq * as3b) : OOB;
       const int hu = cp * d.stride - d.pad + tr, wu = cq * d.stride - d.pad + ts;
@@ -1644,9 +1790,10 @@ __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
     s1 = min(d.S - 1, 2 * ts - cbb + 1);
   }
   const int ldo = d.R * d.S * d.C;
+  if constexpr (MT) r0 = r1 = s0 = s1 = 0;
   for (int r = r0; r <= r1; ++r)
     for (int s_ = s0; s_ <= s1; ++s_) {
-      float* o = out + (r * d.S + s_) * d.C + cb + wn0 + col16;
+      float* o = out + (MT ? n0 : (r * d.S + s_) * d.C + cb) + wn0 + col16;
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
@@ -1664,7 +1811,7 @@ void launch_ring(const ConvArgs& a, int row_tiles, hipStream_t st) {
   hipLaunchKernelGGL((conv_ring_kernel<MODE, BM, BN, SP, BK>), grid, dim3(RT), 0, st, a);
 }
 
-template <int BM, int BN, bool SP>
+template <int BM, int BN, bool SP, bool MT = false>
 void launch_wgrad_ring(ConvArgs& a, hipStream_t st) {
   const int taps = SP ? a.sp.tap0[4] : a.d.R * a.d.S;
   const int tiles = (a.M / BM) * (taps * a.d.C / BN);
@@ -1677,7 +1824,7 @@ void launch_wgrad_ring(ConvArgs& a, hipStream_t st) {
   const int per = (ks + want - 1) / want;
   a.k_per_split = per;
   dim3 grid(a.M / BM, taps * a.d.C / BN, (ks + per - 1) / per);
-  hipLaunchKernelGGL((wgrad_ring_kernel<BM, BN, SP>), grid, dim3(RT), 0, st, a);
+  hipLaunchKernelGGL((wgrad_ring_kernel<BM, BN, SP, MT>), grid, dim3(RT), 0, st, a);
 }
 
 // a dense NHWC image stack (n outermost, rows of c contiguous values) below 1 GiB in bytes
@@ -1709,10 +1856,17 @@ bool g_persist = [] { const char* e = getenv("ES_PERSIST"); return !(e && e[0] =
 bool g_persist_fwd = [] { const char* e = getenv("ES_PERSIST_FWD"); return e && e[0] == '1'; }();
 // persistent 256 x 256 merged sub-pixel FWD (conv_p256_kernel); ES_P256=0 keeps the ring kernel (A/B)
 bool g_p256 = [] { const char* e = getenv("ES_P256"); return !(e && e[0] == '0'); }();
+// multi-tap 64 x 256 WGRAD tiles (wgrad_ring_kernel MT) for plain 64-output-channel convs, opt-in
+// with ES_WGRAD_MT=1.  Measured at B = 1024 (tools/gpu_bnred.sh, one box): conv_layers.9 WGRAD
+// 335 us with 2-tap tiles vs 334 us with the one-tap 64 x 128 tiles, although the one-tap tiles
+// re-read dy per tap (PMC: 2.6x the algorithmic HBM bytes): the kernel is bound by its LDS-DMA fill
+// rate (~8-9 TB/s of L2/MALL -> LDS), not by HBM
+bool g_wgrad_mt = [] { const char* e = getenv("ES_WGRAD_MT"); return e && e[0] == '1'; }();
 
 }  // namespace
 
 thread_local StatsRequest g_stats_req;
+thread_local BnRedRequest g_bnr_req;
 
 // Class geometry of the sub-pixel decomposition (see SubPixel): output row p belongs to class
 // a = (p - pad) mod 2, p = p0 + 2u, source row of combined tap d = u + oh + d, dh = taps.
@@ -1774,6 +1928,12 @@ extern "C" int es_conv_set_ring256(int on) {
   return old;
 }
 
+extern "C" int es_conv_set_wgrad_mt(int on) {
+  const int old = g_wgrad_mt;
+  g_wgrad_mt = on != 0;
+  return old;
+}
+
 extern "C" int es_conv_set_subpixel(int on) {
   const int old = !g_subpixel_off;
   g_subpixel_off = !on;
@@ -1810,6 +1970,9 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
     if (d.K % 256 == 0 && d.C % 128 == 0) ES_WG(256, 128);
     else if (d.K % 128 == 0 && d.C % 256 == 0) ES_WG(128, 256);
     else if (d.K % 128 == 0 && d.C % 128 == 0) ES_WG(128, 128);
+    else if (d.K == 64 && g_wgrad_mt && !sp && d.stride == 1 && d.pad == 0 && d.up_h <= 0 && d.Hu == d.H &&
+             d.Wu == d.W && 256 % d.C == 0 && d.C >= 64 && (d.R * d.S * d.C) % 256 == 0)
+      launch_wgrad_ring<64, 256, false, true>(a, st);        // neutron G conv_layers.9: 2 taps per tile
     else if (d.K == 64 && d.C % 128 == 0) ES_WG(64, 128);   // neutron G conv_layers.9 (128 -> 64)
     else return 0;
 #undef ES_WG
@@ -1862,9 +2025,30 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
         a.stats_part = g_stats_req.part;
         g_stats_req.chunks = nwg;
       }
+      // fused BatchNorm-backward reduction over the stored dy (es_conv2d_dgrad_bnred)
+      const BnRedRequest& q = g_bnr_req;
+      bool bnr = false;
+      if (mode == MODE_DGRAD && q.part && (int64_t)nwg * 3 * a.Ng <= q.floats && q.nm && q.ch && q.x &&
+          ((uintptr_t)q.x & 15) == 0 && (q.ch->act == ES_ACT_LRELU || q.ch->act == ES_ACT_RELU) &&
+          (!q.ch->drop.enabled || q.ch->keep) && a.os[3] == a.Ng && a.os[2] == (int64_t)d.W * a.Ng &&
+          a.os[0] == (int64_t)d.H * d.W * a.Ng) {
+        a.bnr_x = q.x;
+        a.bnr_keep = q.ch->keep;
+        a.bnr_mean = q.nm->mean; a.bnr_invstd = q.nm->invstd; a.bnr_gamma = q.nm->gamma; a.bnr_beta = q.nm->beta;
+        a.bnr_drop = q.ch->drop.enabled != 0;
+        a.bnr_scale = a.bnr_drop ? q.ch->drop.scale : 1.f;
+        a.bnr_dfirst = q.ch->dropout_first;
+        a.bnr_slope = q.ch->act == ES_ACT_LRELU ? q.ch->slope : 0.f;
+        a.bnr_part = q.part;
+        g_bnr_req.chunks = nwg;
+        bnr = true;
+      }
       if (mode == MODE_FWD) {
         if (a.Ng == 64) hipLaunchKernelGGL((conv_persist_kernel<MODE_FWD, 64>), dim3(nwg), dim3(RT), 0, st, a, ntiles);
         else hipLaunchKernelGGL((conv_persist_kernel<MODE_FWD, 128>), dim3(nwg), dim3(RT), 0, st, a, ntiles);
+      } else if (bnr) {
+        if (a.Ng == 64) hipLaunchKernelGGL((conv_persist_kernel<MODE_DGRAD, 64, true>), dim3(nwg), dim3(RT), 0, st, a, ntiles);
+        else hipLaunchKernelGGL((conv_persist_kernel<MODE_DGRAD, 128, true>), dim3(nwg), dim3(RT), 0, st, a, ntiles);
       } else {
         if (a.Ng == 64) hipLaunchKernelGGL((conv_persist_kernel<MODE_DGRAD, 64>), dim3(nwg), dim3(RT), 0, st, a, ntiles);
         else hipLaunchKernelGGL((conv_persist_kernel<MODE_DGRAD, 128>), dim3(nwg), dim3(RT), 0, st, a, ntiles);

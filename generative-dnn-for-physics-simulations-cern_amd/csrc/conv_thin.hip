@@ -14,7 +14,7 @@
 #include <algorithm>
 #include <type_traits>
 
-#include "common.h"
+#include "conv_common.h"
 
 namespace {
 
@@ -301,6 +301,100 @@ __global__ void __launch_bounds__(NT) k1_dgrad(Thin t, int LP) {
   }
 }
 
+// k1_dgrad (bf16 in / out, beta 0, dense NHWC dx) fused with the REDUCTION pass of the BatchNorm
+// backward that consumes dx (generator conv_layers.13's dgrad -> BatchNorm2d conv_layers.10 ->
+// Dropout -> LeakyReLU, neutron/generator.py:33-37; es_conv2d_dgrad_bnred): each thread also folds
+// its stored (bf16-rounded) dx values with the norm input h at the same position and the forward's
+// keep bits into per-channel sums of dnorm and dnorm * xhat (the expressions of norm_fast.hip
+// bn_reduce_fast); per block one [3][C] partial (slots 1, 2).
+struct ThinBnr {
+  const bf16* x;
+  const uint8_t* keep;
+  const float *mean, *invstd, *gamma, *beta;
+  float scale, slope;
+  int dfirst, drop;
+  float* part;
+};
+
+template <int RS>
+__global__ void __launch_bounds__(NT) k1_dgrad_bnred(Thin t, int LP, ThinBnr b) {
+  const es_conv_desc_t& d = t.d;
+  __shared__ float wf[1024];                                  // transposed to [R*S][C]
+  __shared__ float r1[NT * 8], r2[NT * 8];
+  for (int i = threadIdx.x; i < RS * d.C; i += NT) {
+    const int c = i / RS, j = i % RS;
+    wf[j * d.C + c] = to_f(((const bf16*)t.w)[i]);
+  }
+  const int PPB = NT / LP;
+  const int l = threadIdx.x % LP;
+  float mu[8], is[8], sc[8], sh[8], s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = l * 8 + e;
+    mu[e] = b.mean[c];
+    is[e] = b.invstd[c];
+    sc[e] = (b.gamma ? b.gamma[c] : 1.f) * is[e];
+    sh[e] = (b.beta ? b.beta[c] : 0.f) - mu[e] * sc[e];
+    s1[e] = s2[e] = 0.f;
+  }
+  __syncthreads();
+  const float dsc = b.drop ? b.scale : 1.f;
+  for (int m = blockIdx.x * PPB + threadIdx.x / LP; m < t.M; m += gridDim.x * PPB) {
+    int n, h, w;
+    pix3(m, d.H, d.W, n, h, w);
+    const bf16* dy = (const bf16*)t.a + n * t.as[0];
+    const int64_t off = n * t.os[0] + h * t.os[2] + w * t.os[3] + l * 8;
+    float hv[8];
+    ld8<bf16>(b.x + off, hv);                                 // issued before the tap loads' FMAs
+    const uint32_t kb = b.drop ? (uint32_t)b.keep[(int64_t)m * (d.C / 8) + l] : 0xFFu;
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int j = 0; j < RS; ++j) {
+      const int ph = h + d.pad - j / d.S, pw = w + d.pad - j % d.S;
+      const bool ok = ph >= 0 && pw >= 0 && ph < d.P && pw < d.Q;
+      const float gv = to_f(dy[ok ? ph * t.as[2] + pw * t.as[3] : 0]);
+      const float g = ok ? gv : 0.f;
+      const float* wr = wf + j * d.C + l * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += g * wr[e];
+    }
+    st8<bf16>((bf16*)t.out + off, acc);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float dv = (float)(bf16)acc[e], v = hv[e];       // the stored dx value
+      const bool keep = (kb >> e) & 1u;
+      const float z = v * sc[e] + sh[e];
+      const float zs = b.drop && b.dfirst ? z * b.scale : z;
+      const float dn = keep ? dv * (zs > 0.f ? 1.f : b.slope) * dsc : 0.f;
+      s1[e] += dn;
+      s2[e] += dn * ((v - mu[e]) * is[e]);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    r1[e * NT + threadIdx.x] = s1[e];
+    r2[e * NT + threadIdx.x] = s2[e];
+  }
+  __syncthreads();
+  if (threadIdx.x < LP) {
+    float* p = b.part + (int64_t)blockIdx.x * 3 * d.C;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float a1 = 0.f, a2 = 0.f;
+      for (int q = 0; q < PPB; ++q) {
+        a1 += r1[e * NT + q * LP + threadIdx.x];
+        a2 += r2[e * NT + q * LP + threadIdx.x];
+      }
+      const int c = threadIdx.x * 8 + e;
+      p[c] = 0.f;
+      p[d.C + c] = a1;
+      p[2 * d.C + c] = a2;
+    }
+  }
+}
+
 // wgrad: dw[r][s][c] = sum over pixels of dy[pix] * x[pix + (r,s)][c]; lane = channel chunk
 template <typename T, int RS>
 __global__ void __launch_bounds__(NT) k1_wgrad(Thin t, int LP) {
@@ -560,6 +654,27 @@ int es_thin_conv_dgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, c
   for (int i = 0; i < 4; ++i) { t.as[i] = ys[i]; t.os[i] = dxs[i]; }
   t.M = d->N * d->H * d->W;
   const int LP = k1 ? d->C / vn : 1;
+  const BnRedRequest& q = g_bnr_req;
+  if (k1 && q.part && q.x && q.nm && q.ch && dt == ES_BF16 && dxdt == ES_BF16 && beta == 0.f && (rs == 4 || rs == 9) &&
+      dxs[3] == d->C && dxs[2] == (int64_t)d->W * d->C && dxs[0] == (int64_t)d->H * d->W * d->C &&
+      ((uintptr_t)q.x & 15) == 0 && (q.ch->act == ES_ACT_LRELU || q.ch->act == ES_ACT_RELU) &&
+      (!q.ch->drop.enabled || q.ch->keep)) {
+    const dim3 grid(capped(blocks(t.M, NT / LP), g_k1_grid));
+    if ((int64_t)grid.x * 3 * d->C <= q.floats) {
+      ThinBnr b{};
+      b.x = (const bf16*)q.x; b.keep = q.ch->keep;
+      b.mean = q.nm->mean; b.invstd = q.nm->invstd; b.gamma = q.nm->gamma; b.beta = q.nm->beta;
+      b.drop = q.ch->drop.enabled != 0;
+      b.scale = b.drop ? q.ch->drop.scale : 1.f;
+      b.dfirst = q.ch->dropout_first;
+      b.slope = q.ch->act == ES_ACT_LRELU ? q.ch->slope : 0.f;
+      b.part = q.part;
+      if (rs == 4) hipLaunchKernelGGL((k1_dgrad_bnred<4>), grid, dim3(NT), 0, st, t, LP, b);
+      else hipLaunchKernelGGL((k1_dgrad_bnred<9>), grid, dim3(NT), 0, st, t, LP, b);
+      g_bnr_req.chunks = (int)grid.x;
+      return 1;
+    }
+  }
   if (dt == ES_BF16) {
     if (dxdt == ES_BF16) launch_dgrad<bf16, bf16>(t, rs, LP, st); else launch_dgrad<bf16, float>(t, rs, LP, st);
   } else {

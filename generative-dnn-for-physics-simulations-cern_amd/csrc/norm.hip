@@ -890,6 +890,33 @@ extern "C" int es_norm_act_bwd(const es_view_t* x, es_dtype_t xdt, const void* x
   return ES_OK;
 }
 
+// BatchNorm backward whose reduction pass already ran in the producing dgrad's epilogue
+// (es_conv2d_dgrad_bnred): finalize the sums partials, then the fast apply pass
+extern "C" int es_norm_act_bwd_sums(const es_view_t* x, es_dtype_t xdt, const void* xp, const es_norm_t* nm,
+                                    const es_chain_t* ch, const es_view_t* dy, es_dtype_t dydt, const void* dyp,
+                                    const es_view_t* dx, es_dtype_t dxdt, void* dxp, const float* sums_part,
+                                    int chunks, float* dgamma, float* dbeta, float* dsum, void* ws,
+                                    es_stream_t stream) {
+  hipStream_t st = (hipStream_t)stream;
+  ES_CHECK_ARG(nm && nm->kind == ES_NORM_BN && sums_part && chunks > 0 && dxp, "norm_act_bwd_sums: bad args");
+  ES_CHECK_ARG(dsum == nullptr || x->c <= 1024, "norm_act_bwd_sums: dsum needs C <= 1024");
+  const int fk = fast_kind(x, ES_NORM_BN, 1);
+  ES_CHECK_ARG(fk == 0 && xdt == dydt && dydt == dxdt && same_view(x, dy) && same_view(x, dx),
+               "norm_act_bwd_sums: needs the dense NHWC fast path");
+  View xv = mkview(x);
+  int cb, cchunks; int64_t rows, per;
+  colred_geometry(xv, cb, cchunks, rows, per);
+  const int64_t part_floats = std::max<int64_t>((int64_t)cchunks * 3 * x->c, es_fast_part_floats(x, 0));
+  float* part = (float*)ws;
+  float* g1 = part + part_floats;
+  float* g2 = g1 + x->c;
+  launch_sums_finalize(st, sums_part, chunks, x->c, (float)rows, nm->gamma, g1, g2, dbeta, dgamma, 1.f);
+  fast_dsum_finalize(x->c, es_fast_norm_bwd_apply(x, 0, xdt, xp, dyp, dxp, nm, ch, g1, g2, dsum, part, st), part,
+                     dsum, st);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
 extern "C" int64_t es_channel_sum_ws_bytes(const es_view_t* x) {
   View v = mkview(x);
   int cb, chunks; int64_t rows, per;

@@ -80,11 +80,13 @@ _SIGS = {
     "es_conv_set_ring256": (C.c_int, [C.c_int]),
     "es_conv_set_persist": (C.c_int, [C.c_int]),
     "es_conv_set_p256": (C.c_int, [C.c_int]),
+    "es_conv_set_wgrad_mt": (C.c_int, [C.c_int]),
     "es_conv_subpixel_ok": (C.c_int, [P, C.c_int]),
     "es_subpixel_taps": (C.c_int, [C.c_int, C.c_int]),
     "es_conv2d_fwd": (C.c_int, [P, C.c_int, P, P, P, P, P, C.c_int, P, P]),
     "es_conv2d_fwd_stats": (C.c_int, [P, C.c_int, P, P, P, P, P, C.c_int, P, P, I64, P, P]),
     "es_conv2d_dgrad": (C.c_int, [P, C.c_int, P, P, P, P, C.c_int, P, C.c_float, P]),
+    "es_conv2d_dgrad_bnred": (C.c_int, [P, C.c_int, P, P, P, P, C.c_int, P, P, P, P, P, I64, P, P]),
     "es_conv2d_wgrad": (C.c_int, [P, C.c_int, P, P, P, P, P, P]),
     "es_pack_conv_weight": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, C.c_int, P]),
     "es_unpack_conv_grad": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, C.c_float, P]),
@@ -96,6 +98,8 @@ _SIGS = {
     "es_norm_bwd_ws_bytes": (I64, [P, C.c_int, C.c_int]),
     "es_norm_act_bwd": (C.c_int, [P, C.c_int, P, P, P, P, C.c_int, P, P, C.c_int, P, P, C.c_int, P,
                                   C.c_float, P, P, P, P, P]),
+    "es_norm_act_bwd_sums": (C.c_int, [P, C.c_int, P, P, P, P, C.c_int, P, P, C.c_int, P, P, C.c_int, P, P, P,
+                                       P, P]),
     "es_norm_stats_merge": (C.c_int, [P, C.c_int, C.c_int, P, P]),
     "es_norm_stats_local": (C.c_int, [P, C.c_int, P, P, P, P]),
     "es_norm_bwd_sync": (C.c_int, [C.c_int, P, C.c_int, P, P, P, P, C.c_int, P, P, C.c_int, P, P, C.c_float, P, P,

@@ -20,10 +20,11 @@ from . import hip
 class Act:
     """Logical (N, C, H, W) tensor over a flat device buffer with explicit element strides."""
 
-    __slots__ = ("t", "dims", "strides", "bn_part")
+    __slots__ = ("t", "dims", "strides", "bn_part", "bn_sums")
 
     def __init__(self, t: torch.Tensor, dims, strides):
         self.bn_part = None       # (partials, chunks) of fused BatchNorm statistics (ConvOp.fwd)
+        self.bn_sums = None       # (partials, chunks, norm) of a fused BatchNorm-backward reduction (ConvOp.dgrad)
         self.t = t
         self.dims = tuple(int(d) for d in dims)
         self.strides = tuple(int(s) for s in strides)
@@ -145,6 +146,10 @@ def copy_act(src: Act, dst: Act, alpha=1.0, beta=0.0):
 
 def ws(nbytes, device):
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+# BatchNorm-backward reduction fused into the producing dgrad (ConvOp.dgrad bn_reduce); A/B switch
+_BNRED = os.environ.get("ES_BNRED", "1") != "0"
 
 
 # --------------------------------------------------------------------------------- upsample
@@ -295,8 +300,14 @@ class ConvOp:
                          hip.ptr(bias), out.ptr, out.dt, hip.strides4(out.strides), hip.stream_ptr())
         return out
 
-    def dgrad(self, dy: Act, x: Act, dx_dtype=None, inv_scale=None, dx: Act = None, beta=0.0) -> Act:
-        """Gradient w.r.t. the conv input x (folded through the upsample when present)."""
+    def dgrad(self, dy: Act, x: Act, dx_dtype=None, inv_scale=None, dx: Act = None, beta=0.0,
+              bn_reduce=None) -> Act:
+        """Gradient w.r.t. the conv input x (folded through the upsample when present).
+
+        bn_reduce = (norm, h, stats, chain): x = chain(norm(h)) is a BatchNorm + dropout + activation
+        output; when the persistent dgrad kernel runs this conv, its epilogue also computes the
+        reduction pass of that norm's backward (es_conv2d_dgrad_bnred) and dx.bn_sums = (part,
+        chunks), which NormOp.bwd then finishes with the apply pass alone."""
         d = self.desc(x)
         cdt = dy.t.dtype
         if self.subpixel(d, cdt):
@@ -309,9 +320,24 @@ class ConvOp:
         if self.up is None or self.up.factor is not None:   # no upsample, or folded in the GEMM
             if dx is None:
                 dx = Act.nhwc(N, Cc, H, W, ddt, dy.t.device)
+            fuse = (bn_reduce is not None and float(beta) == 0.0 and _BNRED and _NORM_SYNC is None
+                    and bn_reduce[0].kind == hip.NORM_BN and bn_reduce[1].t.dtype == ddt == cdt
+                    and bn_reduce[1].dims == dx.dims and tuple(bn_reduce[1].strides) == tuple(dx.strides))
             with _probed(self.label and self.label + ".dgrad"):
-              hip.call("es_conv2d_dgrad", C.byref(d), dy.dt, dy.ptr, hip.strides4(dy.strides), hip.ptr(wd),
-                     dx.ptr, dx.dt, hip.strides4(dx.strides), float(beta), hip.stream_ptr())
+              if fuse:
+                  norm, h, stats, chain = bn_reduce
+                  nm = norm.norm_struct(*stats)
+                  floats = 2048 * 3 * Cc      # >= the thin dgrad's blocks (<= 2048) / persistent workgroups
+                  part = torch.empty(floats, dtype=torch.float32, device=dy.t.device)
+                  chunks = C.c_int(0)
+                  hip.call("es_conv2d_dgrad_bnred", C.byref(d), dy.dt, dy.ptr, hip.strides4(dy.strides),
+                           hip.ptr(wd), dx.ptr, dx.dt, hip.strides4(dx.strides), h.ptr, C.byref(nm),
+                           C.byref(chain), hip.ptr(part), floats, C.byref(chunks), hip.stream_ptr())
+                  if chunks.value > 0:
+                      dx.bn_sums = (part, chunks.value, nm)
+              else:
+                  hip.call("es_conv2d_dgrad", C.byref(d), dy.dt, dy.ptr, hip.strides4(dy.strides), hip.ptr(wd),
+                         dx.ptr, dx.dt, hip.strides4(dx.strides), float(beta), hip.stream_ptr())
             return dx
         dxu = Act.nhwc(N, Cc, d.Hu, d.Wu, torch.float32, dy.t.device)
         with _probed(self.label and self.label + ".dgrad"):
@@ -516,6 +542,15 @@ class NormOp:
         wsb = ws(hip.lib().es_norm_bwd_ws_bytes(C.byref(x.view), self.kind, self.groups), x.t.device)
         assert addend is None, "residual addend handled through act_ref"
         sync = _NORM_SYNC
+        sums = getattr(dy, "bn_sums", None)
+        if (sums is not None and sync is None and self.kind == hip.NORM_BN and act_ref is None and beta == 0.0
+                and x.dt == dy.dt == dx.dt and (dsum is None or x.dims[1] <= 1024)):
+            # the reduction pass ran in the dgrad that produced dy (ConvOp.dgrad bn_reduce)
+            part, chunks, _ = sums
+            hip.call("es_norm_act_bwd_sums", C.byref(x.view), x.dt, x.ptr, C.byref(nm), C.byref(chain),
+                     C.byref(dy.view), dy.dt, dy.ptr, C.byref(dx.view), dx.dt, dx.ptr, hip.ptr(part), chunks,
+                     hip.ptr(dgamma), hip.ptr(dbeta), hip.ptr(dsum), hip.ptr(wsb), hip.stream_ptr())
+            return dx
         if self.kind == hip.NORM_BN and sync is not None:
             # SyncBN backward: the rank's sums of dnorm and dnorm*xhat, all-reduced, applied with the
             # global row count (dgamma / dbeta stay local: parameter gradients are all-reduced later)

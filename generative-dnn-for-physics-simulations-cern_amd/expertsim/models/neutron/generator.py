@@ -127,11 +127,13 @@ class GeneratorNeutron(ExpertModule):
         ch = ctx["ch"]
         dh6 = act_bwd(ctx["h6"], hip.chain_struct(hip.ACT_RELU), dimg, dx_dtype=cdt)
         o["c13"].wgrad(dh6, ctx["y5"], g("conv_layers.13", "weight"), g("conv_layers.13", "bias"))
-        dy5 = o["c13"].dgrad(dh6, ctx["y5"])
+        # (the thin dgrad also runs bn5's backward reduction over dy5, ConvOp.dgrad bn_reduce)
+        dy5 = o["c13"].dgrad(dh6, ctx["y5"], bn_reduce=(o["bn5"], ctx["h5"], ctx["s5"], ch[4]))
         dh5 = o["bn5"].bwd(ctx["h5"], ctx["s5"], ch[4], dy5, dgamma=g("conv_layers.10", "weight"),
                            dbeta=g("conv_layers.10", "bias"), dsum=g("conv_layers.9", "bias"))
         o["c9"].wgrad(dh5, ctx["y4"], g("conv_layers.9", "weight"), None)
-        dy4 = o["c9"].dgrad(dh5, ctx["y4"])
+        # the dgrad epilogue also runs bn4's backward reduction over dy4 (ConvOp.dgrad bn_reduce)
+        dy4 = o["c9"].dgrad(dh5, ctx["y4"], bn_reduce=(o["bn4"], ctx["h4"], ctx["s4"], ch[3]))
         dh4 = o["bn4"].bwd(ctx["h4"], ctx["s4"], ch[3], dy4, dgamma=g("conv_layers.6", "weight"),
                            dbeta=g("conv_layers.6", "bias"), dsum=g("conv_layers.5", "bias"))
         o["c5"].wgrad(dh4, ctx["y3"], g("conv_layers.5", "weight"), None)

@@ -109,6 +109,10 @@ int es_conv_set_persist(int on);
  * generator conv_layers.0 / .5): 1 = on (default), 0 = the per-tile ring kernel (same accumulation
  * order: bit-identical outputs).  Returns the previous setting. */
 int es_conv_set_p256(int on);
+/* Multi-tap 64 x 256 WGRAD tiles for stride-1, pad-0, 64-output-channel convs (conv_mfma.hip
+ * wgrad_ring_kernel MT: generator conv_layers.9 with 2 of its 4 taps per tile): 1 = on, 0 = one-tap
+ * 64 x 128 tiles (default; measured equal).  Returns the previous setting. */
+int es_conv_set_wgrad_mt(int on);
 /* Sub-pixel decomposition of stride-1 convs over a x2 nearest upsample (conv_mfma.hip): 1 = on
  * (default; wgrad uses it internally, fwd/dgrad when the caller packs mode 2/3 weights and sets
  * desc->subpixel), 0 = off.  Returns the previous setting. */
@@ -215,6 +219,28 @@ int es_norm_act_bwd(const es_view_t* x, es_dtype_t xdt, const void* xp, const es
                     const es_view_t* act_ref, es_dtype_t rdt, const void* refp,
                     const es_view_t* dx, es_dtype_t dxdt, void* dxp, float beta, float* dgamma,
                     float* dbeta, float* dsum, void* ws, es_stream_t stream);
+/* es_conv2d_dgrad (beta 0) fused with the REDUCTION pass of the BatchNorm backward that consumes dx
+ * (aten::native_batch_norm_backward's sums, neutron/generator.py:30-33: conv_layers.9's dgrad feeds
+ * BatchNorm2d conv_layers.6 -> Dropout -> LeakyReLU): x = that norm's input (dx's layout), nm its
+ * statistics, ch its dropout / activation chain with the forward's keep bits.  When the
+ * persistent DGRAD kernel runs this conv, its epilogue writes per workgroup the sums of dnorm and
+ * dnorm * xhat over the stored dx to part [chunks][3][C] (slots 1, 2; part_floats available) and
+ * *chunks > 0 (then es_norm_act_bwd_sums finishes the backward); *chunks == 0: dx was computed
+ * but no sums were written (use es_norm_act_bwd). */
+int es_conv2d_dgrad_bnred(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, const int64_t ys[4],
+                          const void* wd, void* dx, es_dtype_t dxdt, const int64_t dxs[4], const void* x,
+                          const es_norm_t* nm, const es_chain_t* ch, float* part, int64_t part_floats,
+                          int* chunks, es_stream_t stream);
+
+/* Rest of the BatchNorm backward after es_conv2d_dgrad_bnred produced its reduction sums
+ * (sums_part [chunks][3][C], slots 1, 2): the finalize (a1, a2, dgamma += , dbeta +=) and the
+ * apply pass of es_norm_act_bwd (dx, and dsum += sum(dx) per channel when dsum != NULL).  BN only,
+ * dense NHWC x / dy / dx of one dtype; ws: es_norm_bwd_ws_bytes(x, BN, 1) bytes. */
+int es_norm_act_bwd_sums(const es_view_t* x, es_dtype_t xdt, const void* xp, const es_norm_t* nm,
+                         const es_chain_t* ch, const es_view_t* dy, es_dtype_t dydt, const void* dyp,
+                         const es_view_t* dx, es_dtype_t dxdt, void* dxp, const float* sums_part, int chunks,
+                         float* dgamma, float* dbeta, float* dsum, void* ws, es_stream_t stream);
+
 
 /* Data-parallel (synchronised) BatchNorm: the batch statistics of the neutron generator's and aux
  * regressor's BatchNorms (neutron/generator.py:13,19,26,31,35; neutron/aux_reg.py:15-47) over the

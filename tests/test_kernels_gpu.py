@@ -759,6 +759,83 @@ def test_conv_persist_matches_ring(case):
     assert rel(outs[0][2], yr.mean((0, 2, 3)).cpu()) < 1e-2
 
 
+@pytest.mark.parametrize("case", [(64, 128, 46, 46, 64, 2), (37, 128, 23, 21, 64, 2), (33, 64, 9, 7, 128, 2),
+                                  (50, 64, 45, 45, 1, 2), (7, 64, 13, 11, 1, 2), (5, 32, 12, 10, 1, 3)])
+@pytest.mark.parametrize("dfirst", [True, False])
+def test_conv_dgrad_bn_reduce_fused(case, dfirst):
+    """The dgrad fused with the reduction pass of the BatchNorm backward that consumes its output
+    (es_conv2d_dgrad_bnred + es_norm_act_bwd_sums): the persistent DGRAD (generator conv_layers.9 ->
+    conv_layers.6 BatchNorm + Dropout + LeakyReLU) and the thin Cout = 1 dgrad (conv_layers.13 ->
+    conv_layers.10).  The dgrad output is bit-identical to the plain dgrad; the norm backward (dh, dgamma, dbeta, conv-bias sum) equals the unfused two-pass
+    backward up to the summation order of the per-channel sums (fp32: <= 1e-4 relative for the
+    parameter gradients; dh is bf16, within one bf16 rounding)."""
+    hip = _hip()
+    from expertsim.layers import Act, ConvOp, NormOp
+    N, Cin, H, W, Cout, k = case
+    torch.manual_seed(11)
+    w = torch.randn(Cout, Cin, k, k, device=DEV) / np.sqrt(Cin * k * k)
+    op = ConvOp(torch.nn.Parameter(w), torch.nn.Parameter(torch.zeros(Cout, device=DEV)))
+    h = Act.nhwc(N, Cin, H, W, torch.bfloat16, DEV)
+    h.t.copy_((torch.randn(h.t.shape) * 2 + 0.3).to(DEV))
+    gamma, beta = (torch.rand(Cin) + 0.5).to(DEV), torch.randn(Cin).to(DEV)
+    bn = NormOp(hip.NORM_BN, gamma, beta, running_mean=torch.zeros(Cin, device=DEV),
+                running_var=torch.ones(Cin, device=DEV))
+    ch = hip.chain_struct(hip.ACT_LRELU, 0.1, hip.dropout_struct(0.2, 4321, 9, enabled=True), dropout_first=dfirst)
+    kb = hip.attach_keep(ch, N * H * W, Cin, DEV)   # noqa: F841 (kept alive for the backward)
+    y, stats = bn.fwd(h, ch)                     # writes the keep bits the backward reads
+    P, Q = H - k + 1, W - k + 1
+    gy = Act.nhwc(N, Cout, P, Q, torch.bfloat16, DEV)
+    gy.t.copy_(torch.randn(gy.t.shape, generator=torch.Generator().manual_seed(3)).to(DEV))
+    outs = []
+    for fused in (False, True):
+        dx = op.dgrad(gy, y, dx_dtype=torch.bfloat16, bn_reduce=(bn, h, stats, ch) if fused else None)
+        if fused:
+            assert getattr(dx, "bn_sums", None) is not None, "persistent dgrad did not fuse the reduction"
+        dg, db, ds = (torch.zeros(Cin, device=DEV) for _ in range(3))
+        dh = bn.bwd(h, stats, ch, dx, dgamma=dg, dbeta=db, dsum=ds)
+        torch.cuda.synchronize()
+        outs.append((dx.t.clone(), dh.t.float().cpu(), dg.cpu(), db.cpu(), ds.cpu()))
+    (dx0, dh0, dg0, db0, ds0), (dx1, dh1, dg1, db1, ds1) = outs
+    assert torch.equal(dx0, dx1)
+    assert rel(dg1, dg0) < 1e-4 and rel(db1, db0) < 1e-4
+    # sum(dh) per channel (the conv-bias gradient) vanishes analytically for a BatchNorm backward:
+    # both are rounding residue, compared against the channel's sum of |dh|
+    scale = float(dh0.abs().reshape(-1, Cin).sum(0).max())
+    assert float((ds1 - ds0).abs().max()) < 1e-4 * scale
+    assert rel(dh1, dh0) < 1e-2
+
+
+@pytest.mark.parametrize("case", [(40, 128, 46, 46, 64, 2), (9, 64, 17, 13, 64, 2), (5, 128, 11, 9, 64, 3)])
+def test_conv_wgrad_multitap(case):
+    """Multi-tap 64 x 256 WGRAD tiles (es_conv_set_wgrad_mt): the generator conv_layers.9 weight
+    gradient with 2 taps per tile (and 4 x 64-channel taps, and a 3 x 3 conv) against torch fp32 on
+    the bf16 operands, and against the one-tap tiles (same K order per tap, fp32 atomics: <= 1e-5)."""
+    hip = _hip()
+    from expertsim.layers import Act, ConvOp
+    N, Cin, H, W, Cout, k = case
+    torch.manual_seed(5)
+    w = torch.randn(Cout, Cin, k, k, device=DEV) / np.sqrt(Cin * k * k)
+    op = ConvOp(torch.nn.Parameter(w), None)
+    xa = Act.nhwc(N, Cin, H, W, torch.bfloat16, DEV)
+    xa.t.normal_()
+    gy = Act.nhwc(N, Cout, H - k + 1, W - k + 1, torch.bfloat16, DEV)
+    gy.t.normal_()
+    outs = []
+    old = hip.lib().es_conv_set_wgrad_mt(1)
+    try:
+        for on in (1, 0):
+            hip.lib().es_conv_set_wgrad_mt(on)
+            dw = torch.zeros_like(w)
+            op.wgrad(gy, xa, dw, None, beta=1.0)
+            torch.cuda.synchronize()
+            outs.append(dw.cpu())
+    finally:
+        hip.lib().es_conv_set_wgrad_mt(old)
+    ref = torch.nn.grad.conv2d_weight(xa.torch_nchw().float(), w.shape, gy.torch_nchw().float()).cpu()
+    assert rel(outs[0], ref) < 1e-2
+    assert rel(outs[0], outs[1]) < 1e-5
+
+
 @pytest.mark.parametrize("case", [(70, 256, 24, 24, 128), (130, 128, 13, 13, 256), (600, 64, 20, 20, 64)])
 def test_conv_p256_matches_ring(case):
     """The persistent 256 x 256 merged sub-pixel FWD (generator conv_layers.0 / .5: workgroups with
