@@ -137,6 +137,8 @@ class GeneratorNeutron(ExpertModule):
         dh4 = o["bn4"].bwd(ctx["h4"], ctx["s4"], ch[3], dy4, dgamma=g("conv_layers.6", "weight"),
                            dbeta=g("conv_layers.6", "bias"), dsum=g("conv_layers.5", "bias"))
         o["c5"].wgrad(dh4, ctx["y3"], g("conv_layers.5", "weight"), None)
+        # (no fused reduction here: the 256 x 256 sub-pixel DGRAD has no registers to spare for it,
+        # measured 585 -> 871 us for a 146 us reduce pass)
         dy3 = o["c5"].dgrad(dh4, ctx["y3"])
         dh3 = o["bn3"].bwd(ctx["h3"], ctx["s3"], ch[2], dy3, dgamma=g("conv_layers.1", "weight"),
                            dbeta=g("conv_layers.1", "bias"), dsum=g("conv_layers.0", "bias"))
