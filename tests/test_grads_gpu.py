@@ -38,6 +38,19 @@ TOL = {"neutron": 1e-2, "proton": 1e-3}
 # torch-fp32 forward's branch choice moves that layer's input gradient by 2.7e-3 norm-relative and
 # every gradient upstream by ~3e-3.  The case is held to the neutron bound instead.
 CASE_TOL = {"proton_e3_b12": 1e-2}
+# Step-0 aux-regressor gradients of the neutron cases against the goldens.  A reads the generator's
+# images, which the HIP path reproduces to ~1e-6 relative, not bitwise; the reference's own A
+# gradients jump on that scale: its step 0 rerun on the oracle (bit-exact to the goldens) with A's
+# input multiplied by (1 + 1e-6 N(0, 1)) gives a worst norm-relative error of 4e-6 in 7 of 8
+# trials and 4.490e-2 (feature_extractor.conv2.weight, one MaxPool near-tie taking the other
+# branch) in the 8th (tools/aux_sensitivity.py neutron_e1_b8).  The HIP path lands on either
+# branch from box to box (r02g: exactly 4.4898e-2 on conv2.weight, earlier runs <= 1e-5).  The
+# golden bound for A is therefore the measured branch spread.  test_aux_grads_on_hip_images feeds
+# the oracle the HIP path's own images instead: proton measured 8.4e-6 (held to 1e-3); neutron
+# still meets near-ties inside A (the HIP and torch-CPU fp32 forwards of A differ by rounding):
+# measured 4.8e-3 on conv1.weight on the r02g box, so it shares the branch-spread bound.
+A_STEP0_TOL = {"neutron": 5e-2}
+A_ORACLE_TOL = {"neutron": 5e-2, "proton": 1e-3}
 STEP1_TOL = {"neutron": 0.25, "proton": 0.25}
 # noise-only set after Adam's +-lr first step: BatchNorm over B_e = 2 samples (neutron_e3 step 1
 # experts 0 and 2) has invstd up to ~1e3, so the analytically-zero bias sums cancel at ~1e-4
@@ -122,7 +135,8 @@ def test_step_gradients_match_reference(case):
         tol = CASE_TOL.get(case, TOL[g.arch]) if s == 0 else STEP1_TOL[g.arch]
         for label, grads in store.items():
             comp = label[3]
-            _check(grad_errors(g, s, label, grads, g.arch, comp), tol, (case, s, label),
+            lt = max(tol, A_STEP0_TOL.get(g.arch, 0.0)) if comp == "A" and s == 0 else tol
+            _check(grad_errors(g, s, label, grads, g.arch, comp), lt, (case, s, label),
                    abs_tol=1e-5 if s == 0 else STEP1_ABS)
 
 
@@ -177,4 +191,57 @@ def test_module_api_backward_matches_reference(case):
     assert abs(float(d_loss) - gm["disc_loss"]) <= 1e-4 * max(abs(gm["disc_loss"]), 1e-3)
     assert abs(float(g_loss) - gm["gen_loss"]) <= 1e-4 * max(abs(gm["gen_loss"]), 1e-3)
     for label, grads in store.items():
-        _check(grad_errors(g, 0, label, grads, g.arch, label[3]), TOL[g.arch], (case, "module-api", label))
+        tol = max(TOL[g.arch], A_STEP0_TOL.get(g.arch, 0.0)) if label[3] == "A" else TOL[g.arch]
+        _check(grad_errors(g, 0, label, grads, g.arch, label[3]), tol, (case, "module-api", label))
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if "_e1_" in c])
+def test_aux_grads_on_hip_images(case):
+    """A's backward on the HIP path's own generated images: the oracle (torch CPU fp32, the same
+    init parameters, the same step-0 Philox dropout masks) evaluates A's forward, the regressor loss
+    (moe.py:558-561) and its parameter gradients on exactly the images the HIP generator produced,
+    so the comparison does not inherit the generator's ~1e-6 differences (see A_STEP0_TOL)."""
+    from expertsim.utils import philox
+    from oracle import expertsim_oracle as O
+    g = Golden(case)
+    moe, (og, od, oa, orr), cfg = _build(g)
+    G, A = moe.generators[0], moe.aux_regs[0]
+    store = {}
+    _capture({"optA0": (oa[0], A)}, store)
+    inp = g.inputs(0)
+    t = lambda k: torch.from_numpy(inp[k]).to(DEV)
+    cond, pos = t("cond"), t("true_positions")
+    n1 = torch.from_numpy(g.noise(0)[(0, 0)]).to(DEV)
+    G.dropout_keys = [(g.seed, 0)]
+    A.dropout_keys = [(g.seed, 16)]
+    oa[0].zero_grad(set_to_none=True)
+    with torch.no_grad():
+        fake = G(n1, cond)
+    coords = A(fake)
+    aux = A.regressor_loss(pos, coords) * cfg.model.aux_reg.strength
+    aux.backward()
+    oa[0].step()
+    torch.cuda.synchronize()
+
+    torch.set_num_threads(1)
+    om = O.OracleMoE(g.arch, g.E, g.oracle_cfg(O.DEFAULT_CFG), seed=g.seed)
+    P = om.state["A"][0]
+    leaves = om._grad_leaves(P)
+    drop = O.Dropper(g.seed, 0, 0, philox.PASS_AUX)
+    oc = O.aux_forward(g.arch, P, fake.detach().cpu(), drop)
+    ol = O.regressor_loss(pos.cpu(), oc) * cfg.model.aux_reg.strength
+    ref = dict(zip(leaves, torch.autograd.grad(ol, list(leaves.values()), allow_unused=True)))
+    assert float(np.max(np.abs(coords.detach().cpu().numpy() - oc.detach().numpy()))) <= \
+        1e-5 * max(float(oc.abs().max()), 1.0)
+    noise = NOISE_ONLY.get(g.arch, {}).get("A", set())
+    worst = (None, 0.0)
+    for n, h in store["optA0"].items():
+        r = ref[n]
+        r = np.zeros_like(h) if r is None else r.double().numpy()
+        if n in noise:
+            assert float(np.linalg.norm(h)) <= 1e-5, (n, float(np.linalg.norm(h)))
+            continue
+        e = float(np.linalg.norm(h - r) / max(np.linalg.norm(r), 1e-30))
+        worst = max(worst, (n, e), key=lambda x: x[1])
+        assert e <= A_ORACLE_TOL[g.arch], (case, n, e)
+    print(case, "A grads vs oracle on the HIP images: worst", worst)
