@@ -1811,6 +1811,8 @@ void launch_ring(const ConvArgs& a, int row_tiles, hipStream_t st) {
   hipLaunchKernelGGL((conv_ring_kernel<MODE, BM, BN, SP, BK>), grid, dim3(RT), 0, st, a);
 }
 
+// minimum K-steps per WGRAD K-split (each split flushes its whole fp32 tile with atomics)
+int g_wgrad_mink = [] { const char* e = getenv("ES_WGRAD_MINK"); return e && atoi(e) > 0 ? atoi(e) : 8; }();
 template <int BM, int BN, bool SP, bool MT = false>
 void launch_wgrad_ring(ConvArgs& a, hipStream_t st) {
   const int taps = SP ? a.sp.tap0[4] : a.d.R * a.d.S;
@@ -1819,8 +1821,8 @@ void launch_wgrad_ring(ConvArgs& a, hipStream_t st) {
   if (SP)
     for (int c = 0; c < 4; ++c) npix = c == 0 ? a.sp.ph[0] * a.sp.pw[0] : max(npix, a.sp.ph[c] * a.sp.pw[c]);
   const int ks = npix * ((a.d.N + 63) / 64);   // K-steps (the largest class)
-  // one workgroup per CU: aim at two full rounds of the 256 CUs, >= 8 K-steps per split
-  const int want = max(1, min(ks / 8, 512 / tiles));
+  // one workgroup per CU: aim at two full rounds of the 256 CUs, >= g_wgrad_mink K-steps per split
+  const int want = max(1, min(ks / g_wgrad_mink, 512 / tiles));
   const int per = (ks + want - 1) / want;
   a.k_per_split = per;
   dim3 grid(a.M / BM, taps * a.d.C / BN, (ks + per - 1) / per);
