@@ -75,6 +75,9 @@ def main():
     case("G c5 BN bf16 keep bits", hip.NORM_BN, 1, 512, 128, 46, 46, bf, True, True)
     case("G c0 BN bf16 24x24x256", hip.NORM_BN, 1, 512, 256, 24, 24, bf, True)
     case("G c9 BN bf16 45x45x64", hip.NORM_BN, 1, 512, 64, 45, 45, bf, True)
+    case("G c9 BN bf16 no dropout", hip.NORM_BN, 1, 512, 64, 45, 45, bf, False)
+    case("G c9-like 44x44x64 (HW%4=0)", hip.NORM_BN, 1, 512, 64, 44, 44, bf, True)
+    case("G c9-like 46x46x128 C=128", hip.NORM_BN, 1, 512, 128, 45, 45, bf, True)
     case("D GN1 fp32 42x42x32", hip.NORM_GN, 8, 512, 32, 42, 42, f32, False)
     case("D GN2 fp32 19x19x16", hip.NORM_GN, 8, 512, 16, 19, 19, f32, False)
     case("BN fp32 42x42x32 (as BN)", hip.NORM_BN, 1, 512, 32, 42, 42, f32, False)
