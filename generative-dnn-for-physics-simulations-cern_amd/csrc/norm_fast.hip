@@ -81,6 +81,82 @@ __device__ __forceinline__ float dactf(const FastArgs& a, float v) {
 // KM_BITS: read the bits a forward pass stored in a.keep (no Philox).
 enum { KM_NONE = 0, KM_HW4 = 1, KM_ROW = 2, KM_GEN = 3, KM_BITS = 4 };
 
+__device__ __forceinline__ uint32_t keep4(const u32x4 w, uint32_t thr) {
+  return (uint32_t)((w.x >> 8) < thr) | ((uint32_t)((w.y >> 8) < thr) << 1) |
+         ((uint32_t)((w.z >> 8) < thr) << 2) | ((uint32_t)((w.w >> 8) < thr) << 3);
+}
+
+// KM_GEN (H*W % 4 != 0) with the wave's counters shared, for C <= 64 (8 or more row groups per
+// wave, e.g. conv_layers.9's 45 x 45 x 64 output).  The 4 rows of a lane's group span two Philox
+// counters per channel when i0 % 4 != 0; the second one is the FIRST counter of the same channel in
+// the next row group, which the lane TCV above computes anyway.  The wave's last row group has no
+// such neighbour, so its 8 second counters are computed one per row group of the wave (channel k
+// by row group k) and gathered by shuffles: 9 calls per lane for every lane, instead of 8 plus a
+// second call per misaligned channel (1.75 per channel on average), which SIMT execution ran for
+// the whole wave whenever one lane needed it.  Returns false (nothing written) when the layout does
+// not apply; lanes whose 4 rows straddle a sample, or whose neighbour does, compute their own.
+__device__ __forceinline__ bool keep_bits_gen_shared(const FastArgs& a, int r0, int c0, uint32_t thr,
+                                                     uint32_t k0, uint32_t k1, uint32_t (&keep)[4]) {
+  const int tcv = min(a.C >> 3, 64);
+  if (64 % tcv != 0 || 64 / tcv < 8) return false;          // uniform over the launch
+  const int lane = threadIdx.x & 63, rgw = lane / tcv, cvl = lane - rgw * tcv, RGW = 64 / tcv;
+  const bool in1 = r0 - (r0 / a.HW) * a.HW + 3 < a.HW && r0 + 3 < a.rows;
+  uint64_t i00 = ~0ull;          // logical index of (row r0, channel c0); sentinel: not in1
+  uint32_t m0 = 0;               // first-counter bits, 4 per channel
+  if (in1) {
+    const int n = r0 / a.HW, hw0 = r0 - n * a.HW;
+    i00 = ((uint64_t)n * a.C + c0) * (uint64_t)a.HW + hw0 + a.drop.index_offset;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint64_t q = (i00 + (uint64_t)k * a.HW) >> 2;
+      m0 |= keep4(philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), a.drop.stream, 0u, k0, k1), thr) << (4 * k);
+    }
+  }
+  // the last row group's second counter of channel k = rgw (its index read from that lane; a
+  // sentinel or stale index only feeds bits that lane does not use)
+  const int last = (RGW - 1) * tcv + cvl;
+  const uint64_t il = ((uint64_t)__shfl((uint32_t)(i00 >> 32), last, 64) << 32) | __shfl((uint32_t)i00, last, 64);
+  uint32_t xb = 0;
+  if (rgw < 8) {
+    const uint64_t q = ((il + (uint64_t)rgw * a.HW) >> 2) + 1;
+    xb = keep4(philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), a.drop.stream, 0u, k0, k1), thr);
+  }
+  uint32_t lx = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) lx |= (__shfl(xb, k * tcv + cvl, 64) & 15u) << (4 * k);
+  // the next row group's first counters (lane + tcv), checked by its logical index
+  const uint32_t nb_m = __shfl_down(m0, tcv, 64);
+  const uint64_t inb = ((uint64_t)__shfl_down((uint32_t)(i00 >> 32), tcv, 64) << 32) |
+                       __shfl_down((uint32_t)i00, tcv, 64);
+  if (!in1) return false;
+  const bool nb_ok = rgw < RGW - 1 && inb == i00 + 4;
+  const bool last_ok = rgw == RGW - 1;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint64_t i0 = i00 + (uint64_t)k * a.HW;
+    const int off = (int)(i0 & 3);
+    uint32_t m = (m0 >> (4 * k)) & 15u;
+    if (off) {
+      uint32_t m1;
+      if (nb_ok) {
+        m1 = (nb_m >> (4 * k)) & 15u;
+      } else if (last_ok) {
+        m1 = (lx >> (4 * k)) & 15u;
+      } else {
+        const uint64_t q1 = (i0 >> 2) + 1;
+        m1 = keep4(philox4x32_10((uint32_t)q1, (uint32_t)(q1 >> 32), a.drop.stream, 0u, k0, k1), thr);
+      }
+      m |= m1 << 4;
+    }
+    m >>= off;
+    keep[0] |= (m & 1u) << k;
+    keep[1] |= ((m >> 1) & 1u) << k;
+    keep[2] |= ((m >> 2) & 1u) << k;
+    keep[3] |= ((m >> 3) & 1u) << k;
+  }
+  return true;
+}
+
 template <int KM>
 __device__ __forceinline__ void keep_bits(const FastArgs& a, int r0, int c0, uint32_t (&keep)[4]) {
   if constexpr (KM == KM_NONE) { keep[0] = keep[1] = keep[2] = keep[3] = 0xFFu; return; }
@@ -122,6 +198,8 @@ __device__ __forceinline__ void keep_bits(const FastArgs& a, int r0, int c0, uin
                     ((uint32_t)((w.z >> 8) < thr) << 2) | ((uint32_t)((w.w >> 8) < thr) << 3)) << (4 * h);
       }
     }
+  } else if (keep_bits_gen_shared(a, r0, c0, thr, k0, k1, keep)) {   // KM_GEN, <= 64 channels
+    return;
   } else if (r0 - (r0 / a.HW) * a.HW + 3 < a.HW && r0 + 3 < a.rows) {   // KM_GEN
     // the 4 rows lie in one sample: their logical indices i0..i0+3 are consecutive and span at
     // most two Philox counters per channel (2 calls instead of 4)
