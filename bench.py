@@ -183,7 +183,7 @@ def probe_dominant(moe, eager_step, steps, arch, batch, precision):
         tnote = (f"HBM bytes per launch: FETCH_SIZE x2 {tj['fetch_bytes']} + WRITE_SIZE {tj['write_bytes']} "
                  f"(algorithmic {tj['algorithmic_bytes']}), {os.path.relpath(tj_path, ROOT)}")
     return {"bound": "mfma", "kernel": f"{dom} (generator conv_layers.5, "
-                                       f"{'conv_ring bf16' if precision == 'bf16' else 'conv_igemm fp32'})",
+                                       f"{'conv_ring bf16' if precision == 'bf16' else 'conv_ring fp32'})",
             "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_note": tnote,
             "mfma_busy_pmc": mfma_busy,

@@ -30,6 +30,10 @@ void es_set_error(const char* fmt, ...);
     }                                                                         \
   } while (0)
 
+// deterministic mode (es_set_deterministic; the fp32 parity mode turns it on): every float
+// reduction in a fixed order, no float atomics (split-K partials + ordered reduces)
+extern bool g_es_det;
+
 // ---------------------------------------------------------------- scalar conversions
 __device__ __forceinline__ float to_f(float x) { return x; }
 __device__ __forceinline__ float to_f(bf16 x) { return (float)x; }

@@ -72,7 +72,18 @@ struct ConvArgs {
   float bnr_scale, bnr_slope;   // dropout 1/(1-p) (1 without dropout), LeakyReLU slope
   int bnr_dfirst, bnr_drop;
   float* bnr_part;              // [workgroup][3][Ng] (slots 1, 2: the two sums)
+  int det;                      // WGRAD (es_conv2d_wgrad_det): split z stores its raw tile into
+                                // g_det_req.ws + z * M * Ng instead of atomics
 };
+
+// es_conv2d_wgrad_det: the partial buffer offered to the generic (register-staged / thin) WGRAD
+// kernels (host, per thread); the launch sets splits = partial slots written
+struct DetRequest {
+  float* ws;
+  int64_t floats;
+  int splits;
+};
+extern thread_local DetRequest g_det_req;
 
 // es_conv2d_dgrad_bnred: the caller's request (host, per thread); the persistent DGRAD launch
 // sets chunks when it wrote the sums
@@ -99,3 +110,13 @@ extern thread_local StatsRequest g_stats_req;
 // 8-wave LDS-DMA ring kernels (conv_mfma.hip).  Return 1 when the call was launched, 0 when the
 // shape is not eligible (the caller falls back to the kernels of conv_igemm.hip), <0 on error.
 int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st);
+// fp32 operands (parity mode): FWD / DGRAD ring kernels over image chunks (same return convention)
+int es_conv_ring_launch_f32(ConvArgs& a, int mode, hipStream_t st);
+// deterministic fp32 WGRAD on the ring (conv_mfma.hip): partial floats needed (-1: not eligible), and
+// the launch (partials + ordered reduce into the torch-layout dW; 1 done, 0 not eligible, < 0 error)
+int64_t es_wgrad_f32_ring_floats(const es_conv_desc_t& d, const int64_t ys[4], const int64_t xs[4]);
+int es_wgrad_f32_ring(const es_conv_desc_t& d, const void* dy, const int64_t ys[4], const void* x,
+                      const int64_t xs[4], float* dw, float beta, float* ws, int64_t ws_floats, hipStream_t st);
+// ordered sum of per-split partials ws[split][K][R*S*C] into dW (torch layout [K][C][R][S])
+void es_wgrad_reduce_plain(const float* ws, int splits, int K, int C, int R, int S, float* dw, float beta,
+                           hipStream_t st);

@@ -22,6 +22,7 @@
 //   fp32 : v_mfma_f32_16x16x4_f32 x4, lane l reads A[l&15][4*(l>>4)+0..3] once and feeds the
 //          four MFMAs with k = 4*(l>>4)+t (A and B use the same permutation of k, so the sum over
 //          k is unchanged; each MFMA is an exact fp32 FMA chain).
+#include <algorithm>
 #include <cstdlib>
 
 #include "conv_common.h"
@@ -42,6 +43,8 @@ namespace {
 bool g_no_glds = [] { const char* e = getenv("ES_NO_GLDS"); return e && e[0] == '1'; }();
 // ES_NARROW_TILES=0 restores 64 x 64 tiles for the narrow fp32 GEMMs (A/B switch)
 bool g_narrow_tiles = [] { const char* e = getenv("ES_NARROW_TILES"); return !(e && e[0] == '0'); }();
+// ES_NO_F32_RING=1 keeps the fp32 (parity-mode) convs on the register-staged kernels (A/B)
+bool g_no_f32_ring = [] { const char* e = getenv("ES_NO_F32_RING"); return e && e[0] == '1'; }();
 // cap on the K splits of a narrow fp32 WGRAD (every split atomically adds the same M x N outputs)
 int g_narrow_wgrad_splits = [] { const char* e = getenv("ES_NARROW_WGRAD_SPLITS"); return e ? atoi(e) : 0; }();
 
@@ -471,7 +474,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const f32x4 (&a
         if (ng >= a.Ng) continue;
         float v = acc[i][j][jj];
         if constexpr (MODE == MODE_WGRAD) {
-          atomicAdd((float*)a.out + (int64_t)m * a.Ng + ng, v);
+          if (a.det) ((float*)a.out)[((int64_t)blockIdx.z * a.M + m) * a.Ng + ng] = v;   // own partial slot
+          else atomicAdd((float*)a.out + (int64_t)m * a.Ng + ng, v);
         } else {
           if constexpr (MODE == MODE_FWD) {
             if (a.bias && blockIdx.z == 0) v += a.bias[ng];
@@ -880,10 +884,27 @@ int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
       return launch_glds<MODE, 128, 64>(a, st);
     }
   }
+  if constexpr (sizeof(T) == 4 && MODE != MODE_WGRAD) {
+    // fp32 parity mode: the 8-wave LDS-DMA ring kernels on v_mfma_f32_16x16x4_f32 (conv_mfma.hip)
+    // for real convolutions whose K-steps are one tap x 32 channels
+    const int nch = MODE == MODE_FWD ? a.d.C : a.d.K;
+    if (avec && bvec && nch % 32 == 0 && a.Kd % 32 == 0 && a.d.stride <= 2 && a.d.hmap == nullptr &&
+        a.d.P * a.d.Q >= 16 && a.M >= 128 && !g_no_glds && !g_no_f32_ring) {
+      a.k_per_split = a.Kd;
+      a.splitk = 0;
+      const int rc = es_conv_ring_launch_f32(a, MODE, st);
+      if (rc < 0) return ES_ERR_ARG;
+      if (rc > 0) {
+        ES_CHECK_LAUNCH();
+        return ES_OK;
+      }
+    }
+  }
   // tile choice: 128x128 for big GEMMs, 64x64 when either side is small, or when the output is
   // split over K anyway (few tiles, long K: more, smaller workgroups)
   const int tiles128 = ((a.M + 127) / 128) * ((a.Ng + 127) / 128);
-  const bool splitk_case = MODE != MODE_WGRAD && a.dense_f32_out && tiles128 < 256 && (a.Kd + BK - 1) / BK >= 16;
+  const bool splitk_case = MODE != MODE_WGRAD && a.dense_f32_out && tiles128 < 256 && (a.Kd + BK - 1) / BK >= 16 &&
+                           !(sizeof(T) == 4 && g_es_det);
   // 128 x 128 only with enough tiles to fill the chip: a small GEMM (the discriminator / router /
   // aux linears at batch 512) is latency-bound per K-step, so more, smaller workgroups finish sooner
   const bool big = a.M >= 128 && a.Ng >= 96 && !splitk_case && tiles128 >= 128;
@@ -895,11 +916,11 @@ int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
   const int BM = big ? 128 : (narrow_n ? 128 : (narrow_m ? 32 : 64));
   const int BN = big ? 128 : (narrow_n ? 32 : (narrow_m ? 128 : 64));
   if constexpr (sizeof(T) == 2 && MODE == MODE_WGRAD) {
-    if (avec && bvec && !g_no_glds && es_conv_ring_launch(a, MODE, st)) {
+    if (!a.det && avec && bvec && !g_no_glds && es_conv_ring_launch(a, MODE, st)) {
       ES_CHECK_LAUNCH();
       return ES_OK;
     }
-    if (avec && bvec && a.d.K % 128 == 0 && a.d.C % 128 == 0 && a.d.stride <= 2 && a.d.hmap == nullptr &&
+    if (!a.det && avec && bvec && a.d.K % 128 == 0 && a.d.C % 128 == 0 && a.d.stride <= 2 && a.d.hmap == nullptr &&
         !g_no_glds) {
       const int t128 = (a.M / 128) * (a.Ng / 128);
       const int ks = (a.Kd + 63) / 64;
@@ -923,9 +944,14 @@ int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
     int want = (2048 + tiles - 1) / tiles;            // ~2048 workgroups
     if (narrow_m && g_narrow_wgrad_splits > 0) want = min(want, g_narrow_wgrad_splits);
     want = max(1, min(want, ksteps / 4 > 0 ? ksteps / 4 : 1));  // >= 4 K-steps per split
+    if (a.det) {   // deterministic: one partial slot per split, within the caller's workspace
+      const int64_t slot = (int64_t)a.M * a.Ng;
+      want = (int)std::max<int64_t>(1, std::min<int64_t>(want, g_det_req.floats / slot));
+    }
     const int per = ((ksteps + want - 1) / want) * BK;
     a.k_per_split = per;
     splits = (a.Kd + per - 1) / per;
+    if (a.det) g_det_req.splits = splits;
   } else if (splitk_case) {
     // few output tiles and a long K (the linears at batch 512): split K over ~1024 workgroups,
     // at least 4 K-steps each
@@ -988,20 +1014,26 @@ int check_desc(const es_conv_desc_t* d) {
 }
 
 // sub-pixel FWD / DGRAD: only the ring kernels read mode 2 / 3 packed weights
-int ring_direct(ConvArgs& a, int mode, hipStream_t st) {
+int ring_direct(ConvArgs& a, int mode, hipStream_t st, es_dtype_t dt) {
   a.fC = mkdiv(a.d.C); a.fS = mkdiv(a.d.S); a.fK = mkdiv(a.d.K); a.fQ = mkdiv(a.d.Q);
   a.fP = mkdiv(a.d.P); a.fWu = mkdiv(a.d.Wu); a.fHu = mkdiv(a.d.Hu);
   a.fUh = mkdiv(2); a.fUw = mkdiv(2);
   a.fRSK = mkdiv(a.d.R * a.d.S * a.d.K); a.fW = mkdiv(a.d.W); a.fH = mkdiv(a.d.H);
   a.k_per_split = a.Kd;
   a.splitk = 0;
-  const int rc = es_conv_ring_launch(a, mode, st);
+  const int rc = dt == ES_F32 ? es_conv_ring_launch_f32(a, mode, st) : es_conv_ring_launch(a, mode, st);
   ES_CHECK_ARG(rc > 0, "conv: sub-pixel operands not dense NHWC (ring kernels required)");
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
 
 }  // namespace
+
+extern "C" int es_set_deterministic(int on) {
+  const int old = g_es_det;
+  g_es_det = on != 0;
+  return old;
+}
 
 extern "C" int es_conv_set_glds(int on) {
   const int old = !g_no_glds;
@@ -1027,7 +1059,7 @@ extern "C" int es_conv2d_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void*
   const int vn = dt == ES_BF16 ? 8 : 4;
   const bool avec = xs[1] == 1 && d->C % vn == 0;
   const bool bvec = a.Kd % vn == 0;
-  if (d->subpixel) return ring_direct(a, MODE_FWD, (hipStream_t)stream);
+  if (d->subpixel) return ring_direct(a, MODE_FWD, (hipStream_t)stream, dt);
   return dispatch<MODE_FWD>(a, dt, avec, bvec, (hipStream_t)stream);
 }
 
@@ -1066,7 +1098,7 @@ extern "C" int es_conv2d_dgrad(const es_conv_desc_t* d, es_dtype_t dt, const voi
   const int vn = dt == ES_BF16 ? 8 : 4;
   const bool avec = ys[1] == 1 && d->K % vn == 0;
   const bool bvec = a.Kd % vn == 0;
-  if (d->subpixel) return ring_direct(a, MODE_DGRAD, (hipStream_t)stream);
+  if (d->subpixel) return ring_direct(a, MODE_DGRAD, (hipStream_t)stream, dt);
   return dispatch<MODE_DGRAD>(a, dt, avec, bvec, (hipStream_t)stream);
 }
 
@@ -1098,6 +1130,71 @@ extern "C" int es_conv2d_wgrad(const es_conv_desc_t* d, es_dtype_t dt, const voi
   const bool avec = ys[1] == 1 && d->K % vn == 0;
   const bool bvec = xs[1] == 1 && d->C % vn == 0;
   return dispatch<MODE_WGRAD>(a, dt, avec, bvec, (hipStream_t)stream);
+}
+
+// ------------------------------------------------------------------------- deterministic WGRAD
+// (parity mode) dW = beta * dW + conv weight gradient, written in the torch layout [K][C][R][S] with
+// a fixed summation order: the K splits store raw partials into the caller's workspace (no float
+// atomics) and one ordered reduce sums them.  fp32 shapes the ring takes run wgrad_f32_kernel
+// (conv_mfma.hip); the rest run the register-staged / thin kernels with per-split partials.
+thread_local DetRequest g_det_req;
+bool g_es_det = false;
+
+namespace {
+// generic path: partial slots offered = clamp(2^26 floats / slot, 8, 2048) (small thin-conv slots
+// keep their ~1024 blocks; the big linear slots stay within ~256 MB)
+int64_t generic_det_floats(const es_conv_desc_t* d) {
+  const int64_t per = (int64_t)d->K * d->R * d->S * d->C;
+  return per * std::max<int64_t>(8, std::min<int64_t>(2048, (1ll << 26) / per));
+}
+}  // namespace
+
+extern "C" int64_t es_conv2d_wgrad_det_ws_bytes(const es_conv_desc_t* d, es_dtype_t dt, const int64_t ys[4],
+                                                const int64_t xs[4]) {
+  if (!d || check_desc(d)) return -1;
+  int64_t f = -1;
+  if (dt == ES_F32) f = es_wgrad_f32_ring_floats(*d, ys, xs);
+  if (f < 0) f = generic_det_floats(d);
+  return f * (int64_t)sizeof(float);
+}
+
+extern "C" int es_conv2d_wgrad_det(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, const int64_t ys[4],
+                                   const void* x, const int64_t xs[4], float* dw, float beta, void* ws,
+                                   int64_t ws_bytes, es_stream_t stream) {
+  if (int e = check_desc(d)) return e;
+  ES_CHECK_ARG(dw && ws, "conv wgrad det: NULL dw / workspace");
+  const hipStream_t st = (hipStream_t)stream;
+  const int64_t floats = ws_bytes / (int64_t)sizeof(float);
+  if (dt == ES_F32) {
+    const int rc = es_wgrad_f32_ring(*d, dy, ys, x, xs, dw, beta, (float*)ws, floats, st);
+    if (rc < 0) return ES_ERR_ARG;
+    if (rc > 0) {
+      ES_CHECK_LAUNCH();
+      return ES_OK;
+    }
+  }
+  const int64_t per = (int64_t)d->K * d->R * d->S * d->C;
+  ES_CHECK_ARG(floats >= per, "conv wgrad det: workspace below one partial");
+  g_det_req = DetRequest{(float*)ws, floats, 0};
+  int rc = es_thin_conv_wgrad(d, dt, dy, ys, x, xs, (float*)ws, st) ? ES_OK : -1;
+  if (rc != ES_OK) {
+    ConvArgs a{};
+    a.d = *d; a.a_src = dy; a.b_src = x; a.out = ws;
+    for (int i = 0; i < 4; ++i) { a.as[i] = ys[i]; a.bs[i] = xs[i]; }
+    a.M = d->K; a.Ng = d->R * d->S * d->C; a.Kd = d->N * d->P * d->Q;
+    const int vn = dt == ES_BF16 ? 8 : 4;
+    const bool avec = ys[1] == 1 && d->K % vn == 0;
+    const bool bvec = xs[1] == 1 && d->C % vn == 0;
+    a.det = 1;
+    rc = dispatch<MODE_WGRAD>(a, dt, avec, bvec, st);
+  }
+  const int splits = g_det_req.splits;
+  g_det_req = DetRequest{nullptr, 0, 0};
+  if (rc != ES_OK) return rc;
+  ES_CHECK_ARG(splits > 0, "conv wgrad det: no partials written");
+  es_wgrad_reduce_plain((const float*)ws, splits, d->K, d->C, d->R, d->S, dw, beta, st);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
 }
 
 // ------------------------------------------------------------------------- weight (un)packing

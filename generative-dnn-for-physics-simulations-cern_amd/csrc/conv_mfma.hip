@@ -289,12 +289,13 @@ __device__ __forceinline__ void ring_loop_lean(int nk, char* smem, int slot_byte
 // BK = 32 (256 x 256 tiles): K-steps of 32 channels (64-byte rows), 4 slots (three steps in flight),
 // 2 x 4 waves of 128 x 64; per step 32 KiB of operands for 4.2 MFLOP (the 256 x 128 BK = 64 tile
 // moves 48 KiB for the same work), and an A row tile is gathered once for 256 output channels.
-template <int MODE, int BM, int BN, bool SP, int BK = 64>
+template <int MODE, int BM, int BN, bool SP, int BK = 64, typename T = bf16>
 __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   constexpr int WGM = BK == 32 ? 2 : 4, WGN = 8 / WGM;   // waves along M / N
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int RM = WM / 16, RN = WN / 16;
   constexpr int ROWB = BK * 2, PROWS = 1024 / ROWB;      // slot row bytes, rows per 1 KiB piece
+  constexpr int EB = sizeof(T), BKC = ROWB / EB;         // operand bytes, channels per K-step (fp32: BK / 2)
   constexpr int CPR = ROWB / 16;                         // 16-byte chunks per row
   constexpr int APW = BM / PROWS / 8, BPW = BN / PROWS / 8;   // pieces per wave per slot
   constexpr int PW = APW + BPW;
@@ -375,22 +376,22 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   const int wm0 = (wid / WGN) * WM, wn0 = (wid % WGN) * WN;
   const int lrow = lane / CPR, pc = lane % CPR;
 
-  const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * 2));
+  const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * EB));
   // packed weights: row stride ldb (elements) and the class's block offset
   int ldb, bbase = 0, bbytes;
   if constexpr (SP && MODE == MODE_FWD) {
     ldb = sp.dh[cls] * sp.dw[cls] * d.C;
     bbase = sp.tap0[cls] * a.Ng * d.C;
-    bbytes = sp.tap0[4] * a.Ng * d.C * 2;
+    bbytes = sp.tap0[4] * a.Ng * d.C * EB;
   } else if constexpr (SP) {
     ldb = sp.tap0[4] * d.K;
-    bbytes = a.Ng * ldb * 2;
+    bbytes = a.Ng * ldb * EB;
   } else {
     ldb = (MODE == MODE_DGRAD && a.fold) ? d.R * d.S * d.K : a.Kd;
-    bbytes = a.Ng * ldb * 2;
+    bbytes = a.Ng * ldb * EB;
   }
   const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)bbytes);
-  const int as2b = (int)a.as[2] * 2, as3b = (int)a.as[3] * 2;
+  const int as2b = (int)a.as[2] * EB, as3b = (int)a.as[3] * EB;
 
   // A pieces: per-lane constant (image, 16-byte chunk) + per-piece uniform pixel coordinates
   uint32_t alane[APW];
@@ -407,7 +408,7 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
     const int pp = pval[j] ? pix : 0;
     const int y = pp / gw, x = pp - y * gw;
     const int img = gi * NG + (pi - ppix * PPG) * PROWS + lrow;
-    alane[j] = (uint32_t)(((ES_RING_EXP & 1) ? 0 : img) * (int)a.as[0] * 2 + lc * 16);   // images >= N: past num_records
+    alane[j] = (uint32_t)(((ES_RING_EXP & 1) ? 0 : img) * (int)a.as[0] * EB + lc * 16);   // images >= N: past num_records
     if constexpr (MODE == MODE_FWD && SP) {       // source row = u + oh + d
       pc0[j] = y + sp.oh[cls];
       pc1[j] = x + sp.ow[cls];
@@ -430,7 +431,7 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   for (int j = 0; j < BPW; ++j) {
     const int rr = (wid * BPW + j) * PROWS + lrow;
     // rows past Ng read garbage columns that the epilogue drops (or zeros past num_records)
-    blane[j] = (uint32_t)((bbase + (n0 + rr) * ldb) * 2 + ((pc ^ swz_x<BK>(rr)) * 16));
+    blane[j] = (uint32_t)((bbase + (n0 + rr) * ldb) * EB + ((pc ^ swz_x<BK>(rr)) * 16));
   }
 
   // K-step cursor (uniform, advanced once per issued slot).
@@ -441,9 +442,9 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   const int nch = MODE == MODE_FWD ? d.C : d.K;
   const int upw = d.up_w > 0 ? d.up_w : 1;
   int nk;
-  if constexpr (SP && MODE == MODE_FWD) nk = ldb / BK;
-  else if constexpr (SP) nk = ldb / BK;
-  else nk = a.Kd / BK;
+  if constexpr (SP && MODE == MODE_FWD) nk = ldb / BKC;
+  else if constexpr (SP) nk = ldb / BKC;
+  else nk = a.Kd / BKC;
   ClsReg Roh, Row, Rph, Rpw, Rp0, Rq0, Rtap0, Rdh, Rdw;
   if constexpr (SP && MODE == MODE_DGRAD) {
     Roh.init(sp.oh); Row.init(sp.ow); Rph.init(sp.ph); Rpw.init(sp.pw); Rp0.init(sp.p0); Rq0.init(sp.q0);
@@ -492,16 +493,16 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
       if constexpr (MODE == MODE_FWD) kb = (cr * kw + cs) * d.C;
       else if constexpr (SP) kb = (Rtap0(ccls) + cr * kw + cs) * d.K;
       else kb = ckb;
-      ub_t = live ? (uint32_t)(kb * 2) : OOB;
+      ub_t = live ? (uint32_t)(kb * EB) : OOB;
     }
     // (OOB + a channel offset stays past every num_records: offsets are < 1 GiB)
-    const uint32_t co = (uint32_t)(cch * 2);
+    const uint32_t co = (uint32_t)(cch * EB);
 #pragma unroll
     for (int j = 0; j < APW; ++j) bdma16(ares, alane[j] + (ua_t[j] + co), slot + (wid * APW + j) * 1024);
 #pragma unroll
     for (int j = 0; j < BPW; ++j) bdma16(bres, blane[j] + (ub_t + co), slot + ABYTES + (wid * BPW + j) * 1024);
     ++cstep;
-    cch += BK;
+    cch += BKC;
     if (cch == nch) {   // tap done: advance the tap cursor (wave-uniform branch)
       cch = 0;
       ckb += nch;
@@ -534,8 +535,11 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   // fragment set kk: BK = 64 -> K half kk (all RM x RN tiles); BK = 32 -> the step's 32 channels
   // for A tiles kk*RM/2 .. (the wave's row half kk) and all RN B tiles
   const int r16 = lane & 15, g16 = lane >> 4;
+  // (fp32: a lane's 16-byte chunk is 4 channels, fed to 4 v_mfma_f32_16x16x4_f32 with k = 4 g16 + t:
+  // A and B use the same permutation of k, so each MFMA stays an exact fp32 FMA chain)
+  typedef typename std::conditional<EB == 2, bf16x8, f32x4>::type FragT;
   struct Frag {
-    bf16x8 a[RMF], b[RN];
+    FragT a[RMF], b[RN];
     int h;
   };
   auto load = [&](Frag& f, const char* slot, int kk) {
@@ -543,9 +547,9 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
     const int i0 = KH == 2 ? 0 : kk * RMF;
     f.h = kk;
 #pragma unroll
-    for (int i = 0; i < RMF; ++i) f.a[i] = *(const bf16x8*)(slot + swz<BK>(wm0 + (i0 + i) * 16 + r16, seg));
+    for (int i = 0; i < RMF; ++i) f.a[i] = *(const FragT*)(slot + swz<BK>(wm0 + (i0 + i) * 16 + r16, seg));
 #pragma unroll
-    for (int j = 0; j < RN; ++j) f.b[j] = *(const bf16x8*)(slot + ABYTES + swz<BK>(wn0 + j * 16 + r16, seg));
+    for (int j = 0; j < RN; ++j) f.b[j] = *(const FragT*)(slot + ABYTES + swz<BK>(wn0 + j * 16 + r16, seg));
   };
   auto mma = [&](const Frag& f) {
     const int i0 = KH == 2 ? 0 : f.h * RMF;
@@ -559,8 +563,15 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < RMF; ++i)
 #pragma unroll
-      for (int j = 0; j < RN; ++j)
-        acc[i0 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[j], acc[i0 + i][j], 0, 0, 0);
+      for (int j = 0; j < RN; ++j) {
+        if constexpr (EB == 2) {
+          acc[i0 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[j], acc[i0 + i][j], 0, 0, 0);
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            acc[i0 + i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a[i][t], f.b[j][t], acc[i0 + i][j], 0, 0, 0);
+        }
+      }
   };
   if constexpr (BK == 32 && ES_RING_LEAN) {
     ring_loop_lean<PW, NS>(nk, smem, SLOT, issue, load, mma);
@@ -1805,10 +1816,195 @@ __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
     }
 }
 
-template <int MODE, int BM, int BN, bool SP, int BK = 64>
+// ---------------------------------------------------------------------------------------------
+// fp32 WGRAD (parity mode, v_mfma_f32_16x16x4_f32): the same product and image-minor K order as
+// wgrad_ring_kernel, with K-steps of KI = 32 images at one pixel (so a slot has the bf16 kernel's
+// byte geometry: 1 KiB DMA pieces, 3-slot ring).  An fp32 operand needs no transposing read: lane l
+// of a 16x16x4 MFMA takes A[m = l & 15][k = l >> 4], one float of k-row k, so the LDS image is the
+// DMA's natural [image][channel] layout read with ds_read_b32.  Odd k-rows have their 64-byte
+// halves swapped (16-byte chunk c stored at c ^ 4): the two k-rows one 32-lane group reads then
+// hit disjoint banks.
+// DETERMINISTIC: every (tile, K split) stores its raw fp32 tile into its own slot of the partial
+// buffer ws[split][M][taps * C] (no atomics); wgrad_reduce_kernel sums the splits (and, for SP, the
+// four classes' combined taps over each original tap) in a fixed order.  The reference's same-seed
+// reruns are bit-identical; with this, so are the parity mode's.
+// ---------------------------------------------------------------------------------------------
+template <int BM, int BN, bool SP>
+__global__ void __launch_bounds__(RT) wgrad_f32_kernel(ConvArgs a, float* __restrict__ ws, int ngt) {
+  constexpr int KI = 32;                                       // images per K-step
+  // waves along M / N: every wave tile at least 16 x 16 (64 x 64 tiles: 2 x 4 waves of 32 x 16)
+  constexpr int WGM = BM >= 128 ? BM / 64 : (BN >= 128 ? 1 : 2), WGN = 8 / WGM;
+  static_assert(BM / WGM >= 16 && BN / WGN >= 16, "wave tile below one 16 x 16 MFMA block");
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int RM = WM / 16, RN = WN / 16;
+  constexpr int AIMG = KI * BM * 4, SLOT = KI * (BM + BN) * 4;
+  constexpr int APW = BM / 64, BPW = BN / 64;                  // 1 KiB pieces per wave per slot
+  constexpr int PW = APW + BPW;
+  constexpr int ALPR = BM / 4, BLPR = BN / 4;                  // lanes (16-byte chunks) per k-row
+  static_assert(ALPR >= 8 && BLPR >= 8, "the k-row swizzle flips 64-byte halves");
+  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT];
+  const es_conv_desc_t& d = a.d;
+  const SubPixel& sp = a.sp;
+  const int G = (d.N + KI - 1) / KI;
+
+  const int mt = gridDim.x, ntl = gridDim.y, tiles = mt * ntl;
+  const int orig = blockIdx.x + (blockIdx.y + blockIdx.z * ntl) * mt;
+  const int wg = xcd_remap(orig, tiles * gridDim.z);
+  const int tile = wg % tiles, split = wg / tiles;
+  const int m0 = (tile % mt) * BM, n0 = (tile / mt) * BN;
+  const int rs = n0 / d.C, cb = n0 - rs * d.C;
+  int cls = 0, tr, ts, gq, npix;
+  if constexpr (SP) {
+    cls = (rs >= sp.tap0[1]) + (rs >= sp.tap0[2]) + (rs >= sp.tap0[3]);
+    const int de = rs - sp.tap0[cls];
+    tr = de / sp.dw[cls];
+    ts = de - tr * sp.dw[cls];
+    gq = sp.pw[cls];
+    npix = sp.ph[cls] * gq;
+  } else {
+    tr = rs / d.S;
+    ts = rs - tr * d.S;
+    gq = d.Q;
+    npix = d.P * d.Q;
+  }
+  const int tbeg = min(split * a.k_per_split, npix * G);
+  const int tend = min(npix * G, tbeg + a.k_per_split);
+
+  const int lane = threadIdx.x & 63, wid = uni(threadIdx.x >> 6);
+  const int wm0 = (wid / WGN) * WM, wn0 = (wid % WGN) * WN;
+  const int col16 = lane & 15, rq = (lane >> 4) * 4;
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (tbeg < tend) {
+    const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * 4));
+    const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)(d.N * a.bs[0] * 4));
+    const int as0b = (int)a.as[0] * 4, as2b = (int)a.as[2] * 4, as3b = (int)a.as[3] * 4;
+    const int bs0b = (int)a.bs[0] * 4, bs2b = (int)a.bs[2] * 4, bs3b = (int)a.bs[3] * 4;
+    uint32_t alane[APW], blane[BPW];
+#pragma unroll
+    for (int j = 0; j < APW; ++j) {
+      const int kr = (wid * APW + j) * (64 / ALPR) + lane / ALPR;   // image of the K-step
+      alane[j] = (uint32_t)(kr * as0b + (m0 + ((lane % ALPR) ^ ((kr & 1) << 2)) * 4) * 4);
+    }
+#pragma unroll
+    for (int j = 0; j < BPW; ++j) {
+      const int kr = (wid * BPW + j) * (64 / BLPR) + lane / BLPR;
+      blane[j] = (uint32_t)(kr * bs0b + (cb + ((lane % BLPR) ^ ((kr & 1) << 2)) * 4) * 4);
+    }
+    int cp, cq, cg, cstep = tbeg;
+    {
+      const int pix = tbeg / G;
+      cg = tbeg - pix * G;
+      cp = pix / gq;
+      cq = pix - cp * gq;
+    }
+    const int cp0 = SP ? uni(sp.p0[cls]) : 0, cq0 = SP ? uni(sp.q0[cls]) : 0;
+    const int coh = SP ? uni(sp.oh[cls]) : 0, cow = SP ? uni(sp.ow[cls]) : 0;
+    auto issue = [&](char* slot) {
+      const bool live = cstep < tend;
+      uint32_t ua, ub;
+      if constexpr (SP) {   // dy at output pixel (p0 + 2p, q0 + 2q), x at source (p + oh + d, q + ow + e)
+        ua = live ? (uint32_t)(cg * KI * as0b + (cp0 + 2 * cp) * as2b + (cq0 + 2 * cq) * as3b) : OOB;
+        const int hs = cp + coh + tr, wsx = cq + cow + ts;
+        const bool ok = live && (unsigned)hs < (unsigned)d.H && (unsigned)wsx < (unsigned)d.W;
+        ub = ok ? (uint32_t)(cg * KI * bs0b + hs * bs2b + wsx * bs3b) : OOB;
+      } else {
+        ua = live ? (uint32_t)(cg * KI * as0b + cp * as2b + cq * as3b) : OOB;
+        const int hu = cp * d.stride - d.pad + tr, wu = cq * d.stride - d.pad + ts;
+        const bool ok = live && (unsigned)hu < (unsigned)d.Hu && (unsigned)wu < (unsigned)d.Wu;
+        ub = ok ? (uint32_t)(cg * KI * bs0b + fdiv(hu, a.fUh) * bs2b + fdiv(wu, a.fUw) * bs3b) : OOB;
+      }
+#pragma unroll
+      for (int j = 0; j < APW; ++j) bdma16(ares, alane[j] + ua, slot + (wid * APW + j) * 1024);
+#pragma unroll
+      for (int j = 0; j < BPW; ++j) bdma16(bres, blane[j] + ub, slot + AIMG + (wid * BPW + j) * 1024);
+      ++cstep;
+      ++cg;
+      const bool w1 = cg == G;
+      cg = w1 ? 0 : cg;
+      cq += w1;
+      const bool w2 = cq == gq;
+      cq = w2 ? 0 : cq;
+      cp += w2;
+    };
+    // fragment set kk: images 16 kk .. 16 kk + 15 of the step, as 4 MFMA k-groups of 4 images
+    struct Frag {
+      float a[4][RM], b[4][RN];
+    };
+    const int kl = lane >> 4;
+    auto rd = [&](const char* img, int rowb, int k, int row) {   // float (k-row k, row) of an image
+      return *(const float*)(img + k * rowb + ((((row >> 2) ^ ((k & 1) << 2)) << 4) | ((row & 3) << 2)));
+    };
+    auto load = [&](Frag& f, const char* slot, int kk) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int k = kk * 16 + 4 * t + kl;
+#pragma unroll
+        for (int i = 0; i < RM; ++i) f.a[t][i] = rd(slot, BM * 4, k, wm0 + i * 16 + col16);
+#pragma unroll
+        for (int j = 0; j < RN; ++j) f.b[t][j] = rd(slot + AIMG, BN * 4, k, wn0 + j * 16 + col16);
+      }
+    };
+    auto mma = [&](const Frag& f) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a[t][i], f.b[t][j], acc[i][j], 0, 0, 0);
+    };
+    auto nofence = [](Frag&) {};
+    ring_loop<PW, 0>(tend - tbeg, smem, SLOT, issue, load, mma, nofence);
+  }
+  // the raw tile of this split (zeros for an empty split): plain stores into its own slot
+  float* o = ws + ((int64_t)split * a.M + m0 + wm0) * ngt + n0 + wn0 + col16;
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) o[(int64_t)(i * 16 + rq + jj) * ngt + j * 16] = acc[i][j][jj];
+}
+
+// dW (torch layout [K][C][R][S], fp32) = beta * dW + sum over the splits of the partials
+// ws[split][K][taps * C]; SP: original tap (r, s) sums the four classes' combined taps
+// (d, e) = ((r + a) >> 1, (s + b) >> 1) of class (a, b).  Fixed summation order: split, then class.
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int K, int C,
+                                                           int R, int S, int ngt, SubPixel sp, float* __restrict__ dw,
+                                                           float beta) {
+  const int64_t n = (int64_t)K * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int k = (int)(i / C), c = (int)(i - (int64_t)k * C);
+    for (int r = 0; r < R; ++r)
+      for (int s = 0; s < S; ++s) {
+        float v = 0.f;
+        for (int z = 0; z < splits; ++z) {
+          const float* p = ws + ((int64_t)z * K + k) * ngt + c;
+          if (sp.on) {
+#pragma unroll
+            for (int cl = 0; cl < 4; ++cl) {
+              const int dd = (r + (cl >> 1)) >> 1, ee = (s + (cl & 1)) >> 1;
+              v += p[(int64_t)(sp.tap0[cl] + dd * sp.dw[cl] + ee) * C];
+            }
+          } else {
+            v += p[(int64_t)(r * S + s) * C];
+          }
+        }
+        float* g = dw + ((int64_t)i * R + r) * S + s;
+        *g = (beta != 0.f ? beta * *g : 0.f) + v;
+      }
+  }
+}
+
+template <int MODE, int BM, int BN, bool SP, int BK = 64, typename T = bf16>
 void launch_ring(const ConvArgs& a, int row_tiles, hipStream_t st) {
   dim3 grid(row_tiles, (a.Ng + BN - 1) / BN, 1);
-  hipLaunchKernelGGL((conv_ring_kernel<MODE, BM, BN, SP, BK>), grid, dim3(RT), 0, st, a);
+  hipLaunchKernelGGL((conv_ring_kernel<MODE, BM, BN, SP, BK, T>), grid, dim3(RT), 0, st, a);
 }
 
 // minimum K-steps per WGRAD K-split (each split flushes its whole fp32 tile with atomics)
@@ -1830,10 +2026,12 @@ void launch_wgrad_ring(ConvArgs& a, hipStream_t st) {
 }
 
 // a dense NHWC image stack (n outermost, rows of c contiguous values) below 1 GiB in bytes
-bool dense_small(const int64_t s[4], int n, int c, int h, int w) {
+template <int EB>
+bool dense_small_t(const int64_t s[4], int n, int c, int h, int w) {
   return s[1] == 1 && s[3] == c && s[2] == (int64_t)w * c && s[0] == (int64_t)h * w * c &&
-         (int64_t)n * s[0] * 2 < (1ll << 30);
+         (int64_t)n * s[0] * EB < (1ll << 30);
 }
+bool dense_small(const int64_t s[4], int n, int c, int h, int w) { return dense_small_t<2>(s, n, c, h, w); }
 
 bool g_ring_shortk = [] { const char* e = getenv("ES_RING_SHORTK"); return !(e && e[0] == '0'); }();
 int g_ring_ng = [] { const char* e = getenv("ES_RING_NG"); return e ? atoi(e) : 0; }();
@@ -1951,13 +2149,20 @@ extern "C" int es_subpixel_taps(int R, int S) {
 // upsample, stride 1, channels % 64 == 0, below the ring's size limits.  The activations must be
 // dense NHWC at call time.
 extern "C" int es_conv_subpixel_ok(const es_conv_desc_t* d, es_dtype_t dt) {
-  if (g_ring_off || g_subpixel_off || !d || dt != ES_BF16) return 0;
+  if (g_ring_off || g_subpixel_off || !d || (dt != ES_BF16 && dt != ES_F32)) return 0;
   if (d->up_h != 2 || d->up_w != 2 || d->hmap || d->stride != 1) return 0;
   if (d->C % 64 || d->K % 64) return 0;
-  const int64_t xbytes = (int64_t)d->N * d->H * d->W * d->C * 2, ybytes = (int64_t)d->N * d->P * d->Q * d->K * 2;
-  const int64_t wbytes = (int64_t)d->K * d->C * es_subpixel_taps(d->R, d->S) * 2;
+  const int eb = dt == ES_F32 ? 4 : 2;
+  const int64_t xbytes = (int64_t)d->N * d->H * d->W * d->C * eb, ybytes = (int64_t)d->N * d->P * d->Q * d->K * eb;
+  const int64_t wbytes = (int64_t)d->K * d->C * es_subpixel_taps(d->R, d->S) * eb;
+  // fp32: the ring launches over image chunks below 1 GiB (es_conv_ring_launch_f32)
+  if (dt == ES_F32) return wbytes < (1ll << 30) && (int64_t)d->H * d->W * d->C * eb < (1ll << 24) &&
+                           (int64_t)d->P * d->Q * d->K * eb < (1ll << 24);
   return xbytes < (1ll << 30) && ybytes < (1ll << 30) && wbytes < (1ll << 30);
 }
+
+template <typename T>
+int ring_fd(ConvArgs& a, int mode, hipStream_t st);
 
 int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
   const es_conv_desc_t& d = a.d;
@@ -1980,16 +2185,26 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
 #undef ES_WG
     return 1;
   }
-  // caller checked: bf16, channels % 64 == 0, K % 64 == 0 per step
+  return ring_fd<bf16>(a, mode, st);
+}
+
+// FWD / DGRAD ring launch for bf16 or fp32 operands (fp32: the parity mode's exact fp32 MFMA; the
+// persistent kernels are bf16-only)
+template <typename T>
+int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
+  const es_conv_desc_t& d = a.d;
+  const bool sp_weights = d.subpixel != 0;
+  constexpr int EB = sizeof(T);
+  // caller checked: channels % (128 / EB) == 0, K % (128 / EB) == 0 per step
   int PQ;
   if (mode == MODE_FWD) {
-    if (!dense_small(a.as, d.N, d.C, d.H, d.W)) return sp_weights ? -1 : 0;
+    if (!dense_small_t<EB>(a.as, d.N, d.C, d.H, d.W)) return sp_weights ? -1 : 0;
     PQ = d.P * d.Q;
   } else {
-    if (!dense_small(a.as, d.N, d.K, d.P, d.Q)) return sp_weights ? -1 : 0;
+    if (!dense_small_t<EB>(a.as, d.N, d.K, d.P, d.Q)) return sp_weights ? -1 : 0;
     PQ = a.fold ? d.H * d.W : d.Hu * d.Wu;
   }
-  if ((int64_t)a.Ng * a.Kd * 2 * (sp_weights ? 2 : 1) >= (1ll << 30)) return sp_weights ? -1 : 0;
+  if ((int64_t)a.Ng * a.Kd * EB * (sp_weights ? 2 : 1) >= (1ll << 30)) return sp_weights ? -1 : 0;
   // image group size of the row order (see conv_ring_kernel).  Measured on the whole train step
   // (tools/gpu_ab.sh, one box): 64 > 16 > 8 for both FWD and DGRAD, although an isolated FWD
   // prefers 8 (less MALL traffic).  ES_RING_NG overrides it (measurement).
@@ -2016,7 +2231,7 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
     const bool geo = d.stride == 1 && !sp_weights && !a.fold && d.hmap == nullptr && d.up_h <= 0 &&
                      d.Hu == d.H && d.Wu == d.W && nchk % 64 == 0 && a.Kd % 64 == 0;
     const int NS = a.Ng <= 64 ? 4 : 3;
-    if (g_persist && (mode == MODE_DGRAD || g_persist_fwd) && geo && rows16 && (a.Ng == 64 || a.Ng == 128) &&
+    if (EB == 2 && g_persist && (mode == MODE_DGRAD || g_persist_fwd) && geo && rows16 && (a.Ng == 64 || a.Ng == 128) &&
         nkk >= NS - 1 && nkk <= 8 &&
         nkk * a.Ng <= 512 && a.ng >= 16) {
       const int NB = 128 / a.ng, TT = (PQ + NB - 1) / NB;
@@ -2095,7 +2310,7 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
   }
   if (a.sp_merge) {   // (vec_out: the merged epilogue is the staged one)
     const int NT = 4 * a.Ng / 256;
-    if (g_p256 && (4 * a.Ng) % 256 == 0 && (NT == 1 || NT == 2 || NT == 4) && row_tiles >= 64 && a.out_bf16 &&
+    if (EB == 2 && g_p256 && (4 * a.Ng) % 256 == 0 && (NT == 1 || NT == 2 || NT == 4) && row_tiles >= 64 && a.out_bf16 &&
         (int64_t)d.N * a.os[0] * 2 < (1ll << 31)) {
       a.stats_part = nullptr;
       if (g_stats_req.part && (int64_t)256 * 4 * 3 * a.Ng <= g_stats_req.floats) {
@@ -2108,21 +2323,21 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
       return 1;
     }
     dim3 grid(row_tiles, (4 * a.Ng + 255) / 256, 1);
-    hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 256, true, 32>), grid, dim3(RT), 0, st, a);
+    hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 256, true, 32, T>), grid, dim3(RT), 0, st, a);
     return 1;
   }
 #define ES_RING(MD, BMV, BNV)                                                                  \
-  (sp_weights ? launch_ring<MD, BMV, BNV, true>(a, row_tiles, st)                              \
-              : launch_ring<MD, BMV, BNV, false>(a, row_tiles, st))
+  (sp_weights ? launch_ring<MD, BMV, BNV, true, 64, T>(a, row_tiles, st)                              \
+              : launch_ring<MD, BMV, BNV, false, 64, T>(a, row_tiles, st))
   const bool wide = g_ring256 && big && !shortk && a.Ng >= 256 && a.ng >= 16 && a.vec_out &&
                     (sp_weights || mode == MODE_DGRAD);   // (plain FWD: register spills at 256 x 256)
   if (wide) {
     if (mode == MODE_FWD) {
-      if (sp_weights) launch_ring<MODE_FWD, 256, 256, true, 32>(a, row_tiles, st);
-      else launch_ring<MODE_FWD, 256, 256, false, 32>(a, row_tiles, st);
+      if (sp_weights) launch_ring<MODE_FWD, 256, 256, true, 32, T>(a, row_tiles, st);
+      else launch_ring<MODE_FWD, 256, 256, false, 32, T>(a, row_tiles, st);
     } else {
-      if (sp_weights) launch_ring<MODE_DGRAD, 256, 256, true, 32>(a, row_tiles, st);
-      else launch_ring<MODE_DGRAD, 256, 256, false, 32>(a, row_tiles, st);
+      if (sp_weights) launch_ring<MODE_DGRAD, 256, 256, true, 32, T>(a, row_tiles, st);
+      else launch_ring<MODE_DGRAD, 256, 256, false, 32, T>(a, row_tiles, st);
     }
     return 1;
   }
@@ -2135,4 +2350,160 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
   }
 #undef ES_RING
   return 1;
+}
+
+// ---------------------------------------------------------------------------------------------
+// fp32 (parity-mode) ring convolutions.  The ring's buffer offsets are 32-bit with an out-of-range
+// marker at 2^31, so every gathered operand must stay below 1 GiB; larger fp32 batches
+// (conv_layers.5's output gradient at B = 1024 is 1.1 GB) run as launches over image chunks on
+// offset base pointers (chunks of whole 64-image groups).
+// ---------------------------------------------------------------------------------------------
+namespace {
+int g_f32_chunk = 0;   // test knob (es_conv_set_f32_chunk): at most this many images per fp32 launch
+// images per launch: equal chunks (whole 64-image groups where the limit allows) below the limit
+int chunk_images(int64_t img_bytes, int N) {
+  int64_t lim = ((1ll << 30) - 1) / std::max<int64_t>(img_bytes, 1);
+  if (g_f32_chunk > 0) lim = std::min<int64_t>(lim, g_f32_chunk);
+  if (lim >= N) return N;
+  lim = std::max<int64_t>(lim, 1);
+  const int64_t nchunks = (N + lim - 1) / lim;
+  int64_t nc = (N + nchunks - 1) / nchunks;
+  if (nc % 64 && (nc + 63) / 64 * 64 <= lim) nc = (nc + 63) / 64 * 64;
+  return (int)nc;
+}
+}  // namespace
+
+// FWD / DGRAD: 1 launched, 0 not eligible (nothing launched), < 0 error
+int es_conv_ring_launch_f32(ConvArgs& a, int mode, hipStream_t st) {
+  const es_conv_desc_t& d = a.d;
+  if (mode == MODE_WGRAD || d.hmap != nullptr || d.stride > 2 || a.splitk) return d.subpixel ? -1 : 0;
+  const int N = d.N;
+  const int nc = chunk_images(a.as[0] * 4, N);
+  const int esz = a.out_bf16 ? 2 : 4;
+  const StatsRequest req = g_stats_req;
+  int used = 0;
+  bool stats_ok = req.part != nullptr;
+  for (int n0 = 0; n0 < N; n0 += nc) {
+    ConvArgs c = a;
+    c.d.N = std::min(nc, N - n0);
+    c.a_src = (const char*)a.a_src + (int64_t)n0 * a.as[0] * 4;
+    c.out = (char*)a.out + (int64_t)n0 * a.os[0] * esz;
+    c.M = mode == MODE_FWD ? c.d.N * d.P * d.Q : (a.fold ? c.d.N * d.H * d.W : c.d.N * d.Hu * d.Wu);
+    if (req.part) g_stats_req = StatsRequest{req.part + (int64_t)used * 3 * a.Ng, req.floats - (int64_t)used * 3 * a.Ng, 0};
+    const int rc = ring_fd<float>(c, mode, st);
+    if (rc <= 0) {
+      g_stats_req = req;
+      if (n0 == 0) return rc;
+      es_set_error("conv f32 ring: chunk %d not eligible", n0);
+      return -1;
+    }
+    if (req.part) {
+      stats_ok = stats_ok && g_stats_req.chunks > 0;
+      used += g_stats_req.chunks;
+    }
+  }
+  g_stats_req = StatsRequest{req.part, req.floats, stats_ok ? used : 0};
+  return 1;
+}
+
+// WGRAD plan of the deterministic fp32 ring kernel: tile, image chunks, K splits per chunk
+struct WgF32Plan {
+  int bm, bn, sp, nc, nchunks, sc, ngt;
+  SubPixel spg;
+};
+static bool wgrad_f32_plan(const es_conv_desc_t& d, const int64_t ys[4], const int64_t xs[4], WgF32Plan& p) {
+  if (g_ring_off || d.hmap != nullptr || d.stride > 2) return false;
+  auto dense = [](const int64_t s[4], int c, int h, int w) {
+    return s[1] == 1 && s[3] == c && s[2] == (int64_t)w * c && s[0] == (int64_t)h * w * c;
+  };
+  if (!dense(ys, d.K, d.P, d.Q) || !dense(xs, d.C, d.H, d.W)) return false;
+  if (d.K % 64 || d.C % 64) return false;
+  p.bm = d.K % 128 == 0 ? 128 : 64;
+  p.bn = d.C % 256 == 0 && p.bm == 128 ? 256 : (d.C % 128 == 0 ? 128 : 64);
+  p.sp = !g_subpixel_off && d.up_h == 2 && d.up_w == 2 && d.stride == 1;
+  p.spg = SubPixel{};
+  int npix = d.P * d.Q, taps = d.R * d.S;
+  if (p.sp) {
+    es_make_subpixel(d, 0, p.spg);
+    taps = p.spg.tap0[4];
+    npix = 0;
+    for (int c = 0; c < 4; ++c) npix = std::max(npix, p.spg.ph[c] * p.spg.pw[c]);
+  }
+  p.ngt = taps * d.C;
+  p.nc = chunk_images(std::max(ys[0], xs[0]) * 4, d.N);
+  p.nchunks = (d.N + p.nc - 1) / p.nc;
+  const int tiles = (d.K / p.bm) * (p.ngt / p.bn);
+  const int ks = npix * ((p.nc + 31) / 32);   // K-steps of a full chunk (the largest class)
+  // one round of 256 one-workgroup-per-CU tiles, >= 16 K-steps per split
+  p.sc = std::max(1, std::min(256 / std::max(tiles, 1), ks / 16));
+  return true;
+}
+
+int64_t es_wgrad_f32_ring_floats(const es_conv_desc_t& d, const int64_t ys[4], const int64_t xs[4]) {
+  WgF32Plan p;
+  if (!wgrad_f32_plan(d, ys, xs, p)) return -1;
+  return (int64_t)p.nchunks * p.sc * d.K * p.ngt;
+}
+
+// launches the partial kernels and the reduce into dw (torch layout); 1 done, 0 not eligible
+int es_wgrad_f32_ring(const es_conv_desc_t& d, const void* dy, const int64_t ys[4], const void* x,
+                      const int64_t xs[4], float* dw, float beta, float* ws, int64_t ws_floats, hipStream_t st) {
+  WgF32Plan p;
+  if (!wgrad_f32_plan(d, ys, xs, p)) return 0;
+  const int64_t need = (int64_t)p.nchunks * p.sc * d.K * p.ngt;
+  if (ws == nullptr || ws_floats < need) {
+    es_set_error("conv wgrad det: workspace of %lld floats, %lld needed", (long long)ws_floats, (long long)need);
+    return -1;
+  }
+  for (int ch = 0; ch < p.nchunks; ++ch) {
+    const int n0 = ch * p.nc;
+    ConvArgs a{};
+    a.d = d;
+    a.d.N = std::min(p.nc, d.N - n0);
+    a.a_src = (const char*)dy + (int64_t)n0 * ys[0] * 4;
+    a.b_src = (const char*)x + (int64_t)n0 * xs[0] * 4;
+    for (int i = 0; i < 4; ++i) { a.as[i] = ys[i]; a.bs[i] = xs[i]; }
+    a.fUh = mkdiv(d.up_h > 0 ? d.up_h : 1); a.fUw = mkdiv(d.up_w > 0 ? d.up_w : 1);
+    a.M = d.K;
+    a.sp = p.spg;
+    int npix = d.P * d.Q;
+    if (p.sp) { npix = 0; for (int c = 0; c < 4; ++c) npix = std::max(npix, p.spg.ph[c] * p.spg.pw[c]); }
+    const int ks = npix * ((a.d.N + 31) / 32);
+    a.k_per_split = (ks + p.sc - 1) / p.sc;
+    float* wsc = ws + (int64_t)ch * p.sc * d.K * p.ngt;
+    dim3 grid(d.K / p.bm, p.ngt / p.bn, p.sc);
+#define ES_WF(BM, BN)                                                                                 \
+  do {                                                                                                \
+    if (p.sp) hipLaunchKernelGGL((wgrad_f32_kernel<BM, BN, true>), grid, dim3(RT), 0, st, a, wsc, p.ngt);   \
+    else hipLaunchKernelGGL((wgrad_f32_kernel<BM, BN, false>), grid, dim3(RT), 0, st, a, wsc, p.ngt);       \
+  } while (0)
+    if (p.bm == 128 && p.bn == 256) ES_WF(128, 256);
+    else if (p.bm == 128 && p.bn == 128) ES_WF(128, 128);
+    else if (p.bm == 128) ES_WF(128, 64);
+    else if (p.bn == 128) ES_WF(64, 128);
+    else ES_WF(64, 64);
+#undef ES_WF
+  }
+  const int64_t n = (int64_t)d.K * d.C;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, p.nchunks * p.sc, d.K, d.C, d.R,
+                     d.S, p.ngt, p.spg, dw, beta);
+  return 1;
+}
+
+// reduce of generic per-split partials ws[split][K][R*S*C] (conv_igemm / thin WGRAD, deterministic
+// mode) into dW (torch layout)
+void es_wgrad_reduce_plain(const float* ws, int splits, int K, int C, int R, int S, float* dw, float beta,
+                           hipStream_t st) {
+  const int64_t n = (int64_t)K * C;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  SubPixel none{};
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, splits, K, C, R, S, R * S * C, none,
+                     dw, beta);
+}
+
+extern "C" int es_conv_set_f32_chunk(int images) {
+  const int old = g_f32_chunk;
+  g_f32_chunk = images > 0 ? images : 0;
+  return old;
 }

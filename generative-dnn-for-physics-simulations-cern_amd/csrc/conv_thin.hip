@@ -56,6 +56,7 @@ struct Thin {
   void* out; int64_t os[4];        // fwd: y; dgrad: dx; wgrad: fp32 dw [K][R*S*C]
   float beta;
   int M;                           // output pixels (fwd, wgrad: N*P*Q; dgrad: N*H*W)
+  int det;                         // wgrad: block b stores its sums into out + b * (K*R*S*C) (no atomics)
 };
 
 __device__ __forceinline__ void pix3(int m, int A, int B, int& n, int& i, int& j) {
@@ -202,8 +203,13 @@ __global__ void __launch_bounds__(NT) c1_wgrad(Thin t) {
   }
   __syncthreads();
   float* dw = (float*)t.out;
-  for (int i = threadIdx.x; i < d.K * RS; i += NT)
-    atomicAdd(&dw[i], red[0][i] + red[1][i] + red[2][i] + red[3][i]);
+  if (t.det) {
+    for (int i = threadIdx.x; i < d.K * RS; i += NT)
+      dw[(int64_t)blockIdx.x * d.K * RS + i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+  } else {
+    for (int i = threadIdx.x; i < d.K * RS; i += NT)
+      atomicAdd(&dw[i], red[0][i] + red[1][i] + red[2][i] + red[3][i]);
+  }
 }
 
 // ============================================================ Cout == 1
@@ -456,8 +462,13 @@ __global__ void __launch_bounds__(NT) k1_wgrad(Thin t, int LP) {
   }
   __syncthreads();
   float* dw = (float*)t.out;
-  for (int i = threadIdx.x; i < RS * d.C; i += NT)
-    atomicAdd(&dw[i], red[0][i] + red[1][i] + red[2][i] + red[3][i]);
+  if (t.det) {
+    for (int i = threadIdx.x; i < RS * d.C; i += NT)
+      dw[(int64_t)blockIdx.x * RS * d.C + i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+  } else {
+    for (int i = threadIdx.x; i < RS * d.C; i += NT)
+      atomicAdd(&dw[i], red[0][i] + red[1][i] + red[2][i] + red[3][i]);
+  }
 }
 
 // ============================================================ small fp32 convs (few channels)
@@ -582,7 +593,12 @@ void launch_wgrad(const Thin& t, int rs, int LP, hipStream_t st) {
   const es_conv_desc_t& d = t.d;
   // ~4 blocks per CU, each reducing a strided slice of the pixels
   const int per = d.C == 1 ? NT / (d.K / 8) : NT / LP;
-  const dim3 grid(capped(blocks(t.M, per), g_thin_wgrid));
+  dim3 grid(capped(blocks(t.M, per), g_thin_wgrid));
+  if (t.det) {   // deterministic mode: one partial slot per block within the caller's workspace
+    const int64_t slot = (int64_t)d.K * rs * d.C;
+    grid.x = (unsigned)std::max<int64_t>(1, std::min<int64_t>(grid.x, g_det_req.floats / slot));
+    g_det_req.splits = (int)grid.x;
+  }
   if (d.C == 1) {
     if (rs == 4) hipLaunchKernelGGL((c1_wgrad<T, 4>), grid, dim3(NT), 0, st, t);
     else hipLaunchKernelGGL((c1_wgrad<T, 9>), grid, dim3(NT), 0, st, t);
@@ -693,6 +709,7 @@ int es_thin_conv_wgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, c
   t.d = *d; t.a = dy; t.b = x; t.out = dw;
   for (int i = 0; i < 4; ++i) { t.as[i] = ys[i]; t.bs[i] = xs[i]; }
   t.M = d->N * d->P * d->Q;
+  t.det = g_det_req.ws != nullptr && (float*)dw == g_det_req.ws;
   const int LP = k1 ? d->C / vn : 1;
   if (dt == ES_BF16) launch_wgrad<bf16>(t, rs, LP, st);
   else launch_wgrad<float>(t, rs, LP, st);

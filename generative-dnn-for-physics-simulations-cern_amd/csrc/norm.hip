@@ -839,6 +839,10 @@ extern "C" int es_norm_act_bwd(const es_view_t* x, es_dtype_t xdt, const void* x
   if (refp) { b.ref = mkview(act_ref); b.refp = refp; b.refbf = rdt == ES_BF16; }
   BwdApply ap{};
   ap.b = b; ap.dx = mkview(dx); ap.dxp = dxp; ap.dxbf = dxdt == ES_BF16; ap.beta = beta; ap.csum = dsum;
+  // deterministic mode: the generic apply's float-atomic channel sums are replaced by an ordered
+  // column reduction of dx after the apply (below)
+  float* det_dsum = nullptr;
+  if (g_es_det && dsum) { det_dsum = dsum; ap.csum = nullptr; }
   const int64_t total = (int64_t)x->n * x->c * x->h * x->w;
   int cb, chunks; int64_t rows, per;
   colred_geometry(b.x, cb, chunks, rows, per);
@@ -887,6 +891,7 @@ extern "C" int es_norm_act_bwd(const es_view_t* x, es_dtype_t xdt, const void* x
   }
   if (dxp) hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(grid_for(total)), dim3(256), 0, st, ap);
   ES_CHECK_LAUNCH();
+  if (det_dsum && dxp) return es_channel_sum(dx, dxdt, dxp, det_dsum, 1.f, part, stream);
   return ES_OK;
 }
 

@@ -151,6 +151,23 @@ def ws(nbytes, device):
 # BatchNorm-backward reduction fused into the producing dgrad (ConvOp.dgrad bn_reduce); A/B switch
 _BNRED = os.environ.get("ES_BNRED", "1") != "0"
 
+# Deterministic reductions (the fp32 parity mode): weight gradients through es_conv2d_wgrad_det (split
+# partials + one ordered reduce, no float atomics), no split-K atomics in the fp32 GEMMs, ordered
+# conv-bias sums.  Two runs of the same step are then bitwise identical, as the reference's are.
+_DET = False
+
+
+def set_deterministic(on: bool):
+    global _DET
+    on = bool(on)
+    if on != _DET:
+        hip.lib().es_set_deterministic(1 if on else 0)
+        _DET = on
+
+
+def deterministic() -> bool:
+    return _DET
+
 
 # --------------------------------------------------------------------------------- upsample
 class Upsample:
@@ -262,9 +279,10 @@ class ConvOp:
         return d
 
     def subpixel(self, d, dtype) -> bool:
-        """Run this x2-upsample conv as 4 parity-class convs on the source grid (bf16 ring path,
-        conv_mfma.hip): es_conv_subpixel_ok decides, the weights are packed in modes 2 / 3."""
-        if self.up is None or self.up.factor != (2, 2) or dtype != torch.bfloat16:
+        """Run this x2-upsample conv as 4 parity-class convs on the source grid (ring kernels,
+        conv_mfma.hip; bf16, and fp32 with combined weights summed in fp32, whose rounding is ~1e-7
+        relative): es_conv_subpixel_ok decides, the weights are packed in modes 2 / 3."""
+        if self.up is None or self.up.factor != (2, 2) or dtype not in (torch.bfloat16, torch.float32):
             return False
         return bool(hip.lib().es_conv_subpixel_ok(C.byref(d), hip.dt_of_dtype(dtype)))
 
@@ -357,6 +375,17 @@ class ConvOp:
         d = self.desc(x)
         dev = dy.t.device
         assert dy.t.dtype == x.t.dtype, (dy.t.dtype, x.t.dtype)
+        if _DET and dw_out is not None and dw_out.dtype == torch.float32 and dw_out.is_contiguous():
+            # ordered partial sums straight into the torch-layout gradient (es_conv2d_wgrad_det)
+            ys, xs = hip.strides4(dy.strides), hip.strides4(x.strides)
+            nb = int(hip.lib().es_conv2d_wgrad_det_ws_bytes(C.byref(d), dy.dt, ys, xs))
+            wsb = ws(nb, dev)
+            with _probed(self.label and self.label + ".wgrad"):
+                hip.call("es_conv2d_wgrad_det", C.byref(d), dy.dt, dy.ptr, ys, x.ptr, xs, hip.ptr(dw_out),
+                         float(beta), hip.ptr(wsb), nb, hip.stream_ptr())
+            if db_out is not None:
+                channel_sum(dy, db_out, beta)
+            return dw_out
         # every wgrad kernel ACCUMULATES into its packed [K][R][S][C] output, so:
         #  * packed == torch layout (1x1 / linear, or Cin = 1) and beta = 1: accumulate straight
         #    into the parameter's gradient (no scratch, no unpack);

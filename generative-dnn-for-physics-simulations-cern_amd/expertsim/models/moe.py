@@ -34,7 +34,7 @@ from torch import nn
 
 from .. import hip
 from ..config import cfg_get
-from ..layers import Act, copy_act, defer_num_batches, set_norm_sync
+from ..layers import Act, copy_act, defer_num_batches, set_deterministic, set_norm_sync
 from ..rng import DeviceRNG
 from ..utils import philox
 
@@ -76,7 +76,10 @@ class MoEWrapper(nn.Module):
         self._static = None
         self._bufs = {}
         self._eager_steps = 0
+        self._expert_eager = set()  # experts that have run one eager step (then graph-capturable)
         self._dstep = None         # device int32 step counter: dropout / noise streams (graph replay)
+        # fp32 parity mode: every float reduction in a fixed order (bitwise-reproducible steps)
+        self.deterministic = bool(cfg_get(cfg, "train.deterministic", True))
         self.set_precision(cfg_get(cfg, "train.precision", "fp32"))
 
     def set_precision(self, precision: str):
@@ -181,6 +184,7 @@ class MoEWrapper(nn.Module):
         # every step-dependent random stream is keyed on the device counter (captured graphs)
         hip.set_step_counter(self._dstep)
         self.rng.begin_step(self._dstep)
+        set_deterministic(self.precision == "fp32" and self.deterministic)
         try:
             with defer_num_batches():
                 return self._train_step(epoch, cond, real_images, true_positions, std, intensity,
@@ -242,11 +246,16 @@ class MoEWrapper(nn.Module):
             if be > 1 or (ddp is not None and ddp.sync_bn and be >= 1):
                 run = lambda: self._expert_step(e, rows, be, B, cond, real_images, true_positions, std, intensity,
                                                 og, od, oa, mbuf, step, dev)
-                if self._graphs is not None:
+                if self._graphs is not None and e in self._expert_eager:
                     self._weight_scalar(be, B, dev)
+                    for o in (og, od, oa):
+                        o.prepare()      # (no lazy state creation inside a capture)
                     self._graphs.run((e, be, B), run)
                 else:
+                    # an expert's first step runs eagerly (its optimizer moments, step counters and
+                    # scratch then exist outside any graph), also when it first trains after step 0
                     run()
+                    self._expert_eager.add(e)
             else:
                 # DDP: expert active globally but (almost) absent from this shard -> zero local
                 # gradients, but join the same collectives and optimizer steps as the other ranks

@@ -38,6 +38,15 @@ class FusedAdam(torch.optim.Optimizer):
                 o += n
         return flat
 
+    def prepare(self):
+        """Create the lazily allocated state (moments, device step) now.  MoEWrapper calls this outside
+        any graph capture before an expert's step may be captured: created inside a capture, the
+        zero fills would be graph nodes and every replay would reset the moments and the step."""
+        self._buffers()
+        flat = self.module.flat_params
+        if self._dstep is None or self._dstep.device != flat.device:
+            self._dstep = torch.full((1,), self._step, dtype=torch.int32, device=flat.device)
+
     def zero_grad(self, set_to_none: bool = True):
         # the flat gradient buffer is kept (views stay valid); zeroing is one memset
         self.module.zero_grads()

@@ -147,6 +147,24 @@ int es_conv2d_dgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, cons
  * caller zeroes dw first; es_unpack_conv_grad converts to torch's [K][C][R][S]). */
 int es_conv2d_wgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, const int64_t ys[4],
                     const void* x, const int64_t xs[4], float* dw, es_stream_t stream);
+/* Deterministic weight gradient (parity mode; replaces the same aten::convolution_backward weight
+ * output as es_conv2d_wgrad): dw (torch layout [K][C][R][S], fp32) = beta * dw + dW, summed in a
+ * fixed order.  The K splits store raw partials into ws (no float atomics), then one ordered reduce
+ * (split, then sub-pixel class) writes dw; the result is bit-identical across runs and boxes.  fp32
+ * ring shapes (channels % 64, dense NHWC) run the LDS-DMA ring kernel on v_mfma_f32_16x16x4_f32.
+ * ws: es_conv2d_wgrad_det_ws_bytes(d, dt, ys, xs) bytes (-1: bad descriptor). */
+int64_t es_conv2d_wgrad_det_ws_bytes(const es_conv_desc_t* d, es_dtype_t dt, const int64_t ys[4],
+                                     const int64_t xs[4]);
+int es_conv2d_wgrad_det(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, const int64_t ys[4],
+                        const void* x, const int64_t xs[4], float* dw, float beta, void* ws, int64_t ws_bytes,
+                        es_stream_t stream);
+/* Deterministic mode on / off (returns the previous setting): fp32 FWD / DGRAD take no split-K
+ * float atomics, the generic norm backward's conv-bias sums become an ordered column reduction.
+ * MoEWrapper turns it on in the fp32 parity mode (train.deterministic, default on). */
+int es_set_deterministic(int on);
+/* Test knob: fp32 ring convolutions launch over chunks of at most `images` images (0: only as the
+ * 1 GiB operand limit requires); returns the previous value. */
+int es_conv_set_f32_chunk(int images);
 
 /* Weight packing for the implicit GEMM (fp32 master [K][C][R][S] -> dt).
  * mode 0: out[k][r][s][c] = w*scale ; mode 1: out[c][r][s][k] = w*scale.

@@ -8,6 +8,8 @@ import numpy as np
 
 GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CASES = ["neutron_e1_b8", "neutron_e3_b12", "proton_e1_b8", "proton_e3_b12", "neutron_e3_b12_router"]
+# BASELINE batch sizes, compact (module outputs > 4096 values as checksums; inputs regenerated)
+LARGE_CASES = ["neutron_e1_b512"]
 
 
 class Golden:
@@ -47,7 +49,17 @@ class Golden:
 
     def inputs(self, step):
         p = f"s{step}/in/"
-        return {k[len(p):]: self.z[k] for k in self.keys(p)}
+        out = {k[len(p):]: self.z[k] for k in self.keys(p)}
+        if out or not self.meta.get("compact"):
+            return out
+        # compact cases: the batch is regenerated from the same synthetic source and pinned by the
+        # checksums the capture recorded (bit-exact: numpy's seeded generator)
+        from expertsim.utils.synthetic import make_batch
+        b = make_batch(self.B, self.arch, seed=self.meta["data_seed"] + step)
+        for k, v in b.items():
+            want = self.z[f"s{step}/in_ck/{k}"]
+            assert np.array_equal(checksum(v), want), f"{self.case}: regenerated input {k} differs"
+        return b
 
     def router_idx(self, step):
         gates = self.z[f"s{step}/R/call0/out0"]

@@ -1,0 +1,82 @@
+"""The HIP fp32 train step at a BASELINE batch size against the reference itself.
+
+Golden ``neutron_e1_b512`` (tests/golden/make_goldens.py, compact): the reference's
+``MoEWrapper.train_step`` (moe.py:52-504) at B = 512 (BASELINE configs[1]), step 0, with injected
+noise / Gumbel / Philox dropout, captured in this container with torch 2.10 CPU on one thread.
+Module outputs larger than 4096 values are stored as checksums (sum, |.|-sum, L2 and 64 strided
+samples); the batch is regenerated from ``make_batch`` and pinned by its checksums.
+
+Tolerances: metrics, generated images, D outputs / latents and aux coords
+<= 1e-4 relative; every parameter gradient entering Adam <= 1e-2 norm-relative (neutron), the
+noise-only BatchNorm-fed biases <= 1e-5 absolute (test_grads_gpu.py).
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_utils import Golden, checksum
+from test_grads_gpu import A_STEP0_TOL, TOL, _capture, _check, grad_errors
+from test_train_step_gpu import _build, _record
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+CASE = "neutron_e1_b512"
+
+
+def _ck_err(mine, ref):
+    """checksum error: max of the |.|-sum / L2 relative errors and the samples' max-relative error"""
+    c = checksum(mine)
+    l1 = abs(c[1] - ref[1]) / max(ref[1], 1e-30)
+    l2 = abs(c[2] - ref[2]) / max(ref[2], 1e-30)
+    smp = np.max(np.abs(c[3:] - ref[3:])) / max(np.max(np.abs(ref[3:])), 1e-30)
+    return float(max(l1, l2, smp))
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-6))
+
+
+def run_step0(g, record=True, grads=True):
+    moe, (og, od, oa, orr), cfg = _build(g)
+    rec = _record(moe) if record else None
+    store = {}
+    if grads:
+        labels = {f"optG0": (og[0], moe.generators[0]), f"optD0": (od[0], moe.discriminators[0]),
+                  f"optA0": (oa[0], moe.aux_regs[0])}
+        _capture(labels, store)
+    inp = g.inputs(0)
+    nz = g.noise(0)
+    moe.noise_fn = lambda e, w, shape: torch.from_numpy(nz[(e, w)])
+    gum = torch.from_numpy(g.gumbel(0))
+    moe.gumbel_fn = lambda shape: gum
+    t = lambda k: torch.from_numpy(inp[k]).to(DEV)
+    met = moe.train_step(g.epoch, t("cond"), t("real_images").unsqueeze(1), t("true_positions"), t("std"),
+                         t("intensity"), oa, og, od, orr, None, DEV)
+    torch.cuda.synchronize()
+    return moe, {k: float(v) for k, v in met.items()}, rec, store
+
+
+def test_b512_step0_matches_reference():
+    g = Golden(CASE)
+    assert g.B == 512 and g.E == 1
+    moe, met, rec, store = run_step0(g)
+    gm = g.metrics(0)
+    assert set(met) == set(gm)
+    for k, v in gm.items():
+        assert abs(met[k] - v) <= 1e-4 * max(abs(v), 1e-3), (k, met[k], v)
+    errs = {}
+    for c, (img, _) in enumerate(rec["G0"]):
+        errs[f"G{c}"] = _ck_err(img.torch_nchw().cpu().numpy(), g[f"s0/G0/call{c}/out0_ck"])
+    for c, (out, lat, _) in enumerate(rec["D0"]):
+        errs[f"D{c}.out"] = _rel(out.rows2d().cpu().numpy(), g[f"s0/D0/call{c}/out0"])
+        errs[f"D{c}.latent"] = _ck_err(lat.rows2d().cpu().numpy(), g[f"s0/D0/call{c}/out1_ck"])
+    for c, (coords, _) in enumerate(rec["A0"]):
+        errs[f"A{c}"] = _rel(coords.rows2d().cpu().numpy(), g[f"s0/A0/call{c}/out0"])
+    print("B=512 output errors:", errs)
+    for k, e in errs.items():
+        assert e <= 1e-4, (k, e)
+    for label, grads in store.items():
+        comp = label[3]
+        tol = max(TOL["neutron"], A_STEP0_TOL.get("neutron", 0.0)) if comp == "A" else TOL["neutron"]
+        _check(grad_errors(g, 0, label, grads, "neutron", comp), tol, (CASE, 0, label))

@@ -97,3 +97,42 @@ def test_expert_graphs_match_eager_multi_expert():
     for k in ("gen_loss", "disc_loss", "div_loss", "intensity_loss", "aux_reg_loss", "router_loss",
               "adaptive_load_balancing_loss"):
         assert abs(ma[k] - mb[k]) <= 1e-2 * max(abs(ma[k]), 1e-3), (k, ma[k], mb[k])
+
+
+def test_expert_graphs_late_expert():
+    """An expert that receives no samples at step 0 and first trains later: its first
+    step runs eagerly, so its Adam moments / device step are created outside any capture, and the
+    replayed graphs then advance them.  The router's last bias forces the routing of step 0 (every
+    sample away from expert 2), then is reset; both runs see the same parameter edits."""
+    from expertsim.utils.synthetic import make_batch
+    import bench
+    b = make_batch(96, "neutron", seed=6)
+    t = {k: torch.from_numpy(v).to(DEV) for k, v in b.items()}
+    real = t["real_images"].unsqueeze(1).contiguous()
+    runs = []
+    for graphs in (False, True):
+        moe, (og, od, oa, orr), cfg = bench.build("neutron", 3, "bf16", 13, torch.device(DEV))
+        moe.expert_graphs = graphs
+        # the router is frozen (its ALB term is infinite while an expert gets no gate mass)
+        moe.cfg.model.router.stop_router_training_epoch = 0
+        bias = dict(moe.router.named_parameters())["fc_layers.6.bias"]
+        args = (0, t["cond"], real, t["true_positions"], t["std"], t["intensity"], oa, og, od, orr, None, DEV)
+        steps2 = []
+        for i in range(5):
+            with torch.no_grad():
+                bias.copy_(torch.tensor([40.0, 40.0, -40.0] if i == 0 else [0.0, 0.0, 0.0]))
+            m = moe.train_step(*args)
+            steps2.append(float(m["n_choosen_experts_mean_epoch_2"]))
+        torch.cuda.synchronize()
+        assert steps2[0] == 0.0 and sum(s > 0 for s in steps2[1:]) >= 3, steps2
+        for o in (*og, *od, *oa):
+            o.sync_step()
+        runs.append(([o._step for o in (*og, *od, *oa)],
+                     {n: p.detach().clone() for n, p in moe.named_parameters()}, cfg))
+    (sa, pa, cfg), (sb, pb, _) = runs
+    assert sa == sb, (sa, sb)          # device step counters advanced by the replays
+    lr = max(cfg.model.generator.lr_g, cfg.model.discriminator.lr_d, cfg.model.aux_reg.lr_a,
+             cfg.model.router.lr_r)
+    for n in pa:
+        d = float((pa[n] - pb[n]).abs().max())
+        assert d <= 5 * 2 * lr + 1e-7, (n, d)
