@@ -73,7 +73,9 @@ struct ConvArgs {
   int bnr_dfirst, bnr_drop;
   float* bnr_part;              // [workgroup][3][Ng] (slots 1, 2: the two sums)
   int det;                      // WGRAD (es_conv2d_wgrad_det): split z stores its raw tile into
-                                // g_det_req.ws + z * M * Ng instead of atomics
+                                // g_det_req.ws + z * M * Ng instead of atomics; split-K FWD / DGRAD
+                                // (es_conv2d_*_det): into det_ws + z * M * Ng
+  float* det_ws;
 };
 
 // es_conv2d_wgrad_det: the partial buffer offered to the generic (register-staged / thin) WGRAD

@@ -482,7 +482,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const f32x4 (&a
           }
           const int64_t o = rowoff + (int64_t)ng * a.os[1];
           if (a.splitk) {
-            atomicAdd((float*)a.out + o, v);
+            if (a.det) ((float*)a.det_ws)[(int64_t)blockIdx.z * a.M * a.Ng + o] = v;   // own partial slot
+            else atomicAdd((float*)a.out + o, v);
           } else if (a.out_bf16) {
             bf16* y = (bf16*)a.out + o;
             if (a.beta != 0.f) v += a.beta * (float)(*y);
@@ -903,8 +904,9 @@ int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
   // tile choice: 128x128 for big GEMMs, 64x64 when either side is small, or when the output is
   // split over K anyway (few tiles, long K: more, smaller workgroups)
   const int tiles128 = ((a.M + 127) / 128) * ((a.Ng + 127) / 128);
+  // (deterministic mode: only with a partial workspace, es_conv2d_fwd_det / es_conv2d_dgrad_det)
   const bool splitk_case = MODE != MODE_WGRAD && a.dense_f32_out && tiles128 < 256 && (a.Kd + BK - 1) / BK >= 16 &&
-                           !(sizeof(T) == 4 && g_es_det);
+                           !(sizeof(T) == 4 && g_es_det && g_det_req.ws == nullptr);
   // 128 x 128 only with enough tiles to fill the chip: a small GEMM (the discriminator / router /
   // aux linears at batch 512) is latency-bound per K-step, so more, smaller workgroups finish sooner
   const bool big = a.M >= 128 && a.Ng >= 96 && !splitk_case && tiles128 >= 128;
@@ -956,12 +958,18 @@ int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
     // few output tiles and a long K (the linears at batch 512): split K over ~1024 workgroups,
     // at least 4 K-steps each
     int want = min((1024 + tiles - 1) / tiles, ksteps / 4);
+    const bool det = g_det_req.ws != nullptr;
+    if (det) want = (int)std::min<int64_t>(want, g_det_req.floats / ((int64_t)a.M * a.Ng));
     if (want > 1) {
       const int per = ((ksteps + want - 1) / want) * BK;
       a.k_per_split = per;
       splits = (a.Kd + per - 1) / per;
       a.splitk = splits > 1;
-      if (a.splitk && hipMemsetAsync(a.out, 0, (size_t)a.M * a.Ng * sizeof(float), st) != hipSuccess) {
+      if (det && a.splitk) {   // ordered: split z stores into its own slot, es_splitk_reduce sums
+        a.det = 1;
+        a.det_ws = g_det_req.ws;
+        g_det_req.splits = splits;
+      } else if (a.splitk && hipMemsetAsync(a.out, 0, (size_t)a.M * a.Ng * sizeof(float), st) != hipSuccess) {
         es_set_error("conv: split-K memset failed");
         return ES_ERR_HIP;
       }
@@ -1195,6 +1203,56 @@ extern "C" int es_conv2d_wgrad_det(const es_conv_desc_t* d, es_dtype_t dt, const
   es_wgrad_reduce_plain((const float*)ws, splits, d->K, d->C, d->R, d->S, dw, beta, st);
   ES_CHECK_LAUNCH();
   return ES_OK;
+}
+
+// deterministic split-K FWD / DGRAD (the fp32 linears with few output tiles and a long K: the
+// generator's fc2 dgrad, K = 21632 / 92160): the splits store partials into ws, one ordered sum
+namespace {
+constexpr int kDetSplitK = 16;
+__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, int64_t n, float* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    for (int z = 0; z < splits; ++z) v += ws[z * n + i];
+    out[i] = v;
+  }
+}
+int splitk_det_finish(int rc, float* out, int64_t n, hipStream_t st) {
+  const int splits = g_det_req.splits;
+  const float* ws = g_det_req.ws;
+  g_det_req = DetRequest{nullptr, 0, 0};
+  if (rc != ES_OK || splits == 0) return rc;   // no split: the kernel wrote out itself
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, splits, n, out);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+}  // namespace
+
+extern "C" int64_t es_conv2d_splitk_ws_bytes(const es_conv_desc_t* d, int mode) {
+  if (!d || check_desc(d) || (mode != MODE_FWD && mode != MODE_DGRAD)) return -1;
+  const int64_t M = mode == MODE_FWD ? (int64_t)d->N * d->P * d->Q
+                                     : (d->up_h > 0 ? (int64_t)d->N * d->H * d->W : (int64_t)d->N * d->Hu * d->Wu);
+  const int64_t Ng = mode == MODE_FWD ? d->K : d->C;
+  return M * Ng * kDetSplitK * (int64_t)sizeof(float);
+}
+
+extern "C" int es_conv2d_fwd_det(const es_conv_desc_t* d, es_dtype_t dt, const void* x, const int64_t xs[4],
+                                 const void* wk, const float* bias, void* y, es_dtype_t ydt, const int64_t ys[4],
+                                 void* ws, int64_t ws_bytes, es_stream_t stream) {
+  ES_CHECK_ARG(ws, "conv fwd det: NULL workspace");
+  g_det_req = DetRequest{(float*)ws, ws_bytes / (int64_t)sizeof(float), 0};
+  const int rc = es_conv2d_fwd(d, dt, x, xs, wk, bias, y, ydt, ys, stream);
+  return splitk_det_finish(rc, (float*)y, (int64_t)d->N * d->P * d->Q * d->K, (hipStream_t)stream);
+}
+
+extern "C" int es_conv2d_dgrad_det(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, const int64_t ys[4],
+                                   const void* wd, void* dxu, es_dtype_t dxdt, const int64_t dxs[4], void* ws,
+                                   int64_t ws_bytes, es_stream_t stream) {
+  ES_CHECK_ARG(ws, "conv dgrad det: NULL workspace");
+  g_det_req = DetRequest{(float*)ws, ws_bytes / (int64_t)sizeof(float), 0};
+  const int rc = es_conv2d_dgrad(d, dt, dy, ys, wd, dxu, dxdt, dxs, 0.f, stream);
+  const int64_t M = d->up_h > 0 ? (int64_t)d->N * d->H * d->W : (int64_t)d->N * d->Hu * d->Wu;
+  return splitk_det_finish(rc, (float*)dxu, M * d->C, (hipStream_t)stream);
 }
 
 // ------------------------------------------------------------------------- weight (un)packing

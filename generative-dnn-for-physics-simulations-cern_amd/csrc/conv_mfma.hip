@@ -1974,30 +1974,38 @@ __global__ void __launch_bounds__(RT) wgrad_f32_kernel(ConvArgs a, float* __rest
 // dW (torch layout [K][C][R][S], fp32) = beta * dW + sum over the splits of the partials
 // ws[split][K][taps * C]; SP: original tap (r, s) sums the four classes' combined taps
 // (d, e) = ((r + a) >> 1, (s + b) >> 1) of class (a, b).  Fixed summation order: split, then class.
+// One thread per (k, r, s, c), c fastest: the partial reads are coalesced, and every thread's
+// splits x classes loads are independent (a thread per (k, c) looping over the taps was latency
+// bound: 174 us for conv_layers.5's 32 splits).
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int K, int C,
                                                            int R, int S, int ngt, SubPixel sp, float* __restrict__ dw,
                                                            float beta) {
-  const int64_t n = (int64_t)K * C;
+  const int64_t n = (int64_t)K * R * S * C;
+  const int64_t zst = (int64_t)K * ngt;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int k = (int)(i / C), c = (int)(i - (int64_t)k * C);
-    for (int r = 0; r < R; ++r)
-      for (int s = 0; s < S; ++s) {
-        float v = 0.f;
-        for (int z = 0; z < splits; ++z) {
-          const float* p = ws + ((int64_t)z * K + k) * ngt + c;
-          if (sp.on) {
+    const int c = (int)(i % C);
+    int64_t t = i / C;
+    const int s = (int)(t % S);
+    t /= S;
+    const int r = (int)(t % R);
+    const int k = (int)(t / R);
+    const float* p = ws + (int64_t)k * ngt + c;
+    float v = 0.f;
+    if (sp.on) {
+      int off[4];
 #pragma unroll
-            for (int cl = 0; cl < 4; ++cl) {
-              const int dd = (r + (cl >> 1)) >> 1, ee = (s + (cl & 1)) >> 1;
-              v += p[(int64_t)(sp.tap0[cl] + dd * sp.dw[cl] + ee) * C];
-            }
-          } else {
-            v += p[(int64_t)(r * S + s) * C];
-          }
-        }
-        float* g = dw + ((int64_t)i * R + r) * S + s;
-        *g = (beta != 0.f ? beta * *g : 0.f) + v;
+      for (int cl = 0; cl < 4; ++cl)
+        off[cl] = (sp.tap0[cl] + ((r + (cl >> 1)) >> 1) * sp.dw[cl] + ((s + (cl & 1)) >> 1)) * C;
+      for (int z = 0; z < splits; ++z, p += zst) {
+#pragma unroll
+        for (int cl = 0; cl < 4; ++cl) v += p[off[cl]];
       }
+    } else {
+      const int off = (r * S + s) * C;
+      for (int z = 0; z < splits; ++z, p += zst) v += p[off];
+    }
+    float* g = dw + (((int64_t)k * C + c) * R + r) * S + s;
+    *g = (beta != 0.f ? beta * *g : 0.f) + v;
   }
 }
 
@@ -2484,8 +2492,8 @@ int es_wgrad_f32_ring(const es_conv_desc_t& d, const void* dy, const int64_t ys[
     else ES_WF(64, 64);
 #undef ES_WF
   }
-  const int64_t n = (int64_t)d.K * d.C;
-  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  const int64_t n = (int64_t)d.K * d.C * d.R * d.S;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 8192);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, p.nchunks * p.sc, d.K, d.C, d.R,
                      d.S, p.ngt, p.spg, dw, beta);
   return 1;
@@ -2495,8 +2503,8 @@ int es_wgrad_f32_ring(const es_conv_desc_t& d, const void* dy, const int64_t ys[
 // mode) into dW (torch layout)
 void es_wgrad_reduce_plain(const float* ws, int splits, int K, int C, int R, int S, float* dw, float beta,
                            hipStream_t st) {
-  const int64_t n = (int64_t)K * C;
-  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  const int64_t n = (int64_t)K * C * R * S;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 8192);
   SubPixel none{};
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, splits, K, C, R, S, R * S * C, none,
                      dw, beta);

@@ -91,6 +91,9 @@ _SIGS = {
     "es_conv2d_wgrad_det_ws_bytes": (I64, [P, C.c_int, P, P]),
     "es_conv2d_wgrad_det": (C.c_int, [P, C.c_int, P, P, P, P, P, C.c_float, P, I64, P]),
     "es_set_deterministic": (C.c_int, [C.c_int]),
+    "es_conv2d_splitk_ws_bytes": (I64, [P, C.c_int]),
+    "es_conv2d_fwd_det": (C.c_int, [P, C.c_int, P, P, P, P, P, C.c_int, P, P, I64, P]),
+    "es_conv2d_dgrad_det": (C.c_int, [P, C.c_int, P, P, P, P, C.c_int, P, P, I64, P]),
     "es_conv_set_f32_chunk": (C.c_int, [C.c_int]),
     "es_pack_conv_weight": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, C.c_int, P]),
     "es_unpack_conv_grad": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, C.c_float, P]),

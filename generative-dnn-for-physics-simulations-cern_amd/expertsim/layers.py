@@ -313,10 +313,23 @@ class ConvOp:
                          C.byref(chunks), hip.stream_ptr())
                 if chunks.value > 0:
                     out.bn_part = (part, chunks.value)
+            elif _DET and self._linear_det(d, d.K, out):
+                # deterministic split-K of a long-K linear (ordered partial sums, no atomics)
+                nb = int(hip.lib().es_conv2d_splitk_ws_bytes(C.byref(d), 0))
+                wsb = ws(nb, x.t.device)
+                hip.call("es_conv2d_fwd_det", C.byref(d), x.dt, x.ptr, hip.strides4(x.strides), hip.ptr(wk),
+                         hip.ptr(bias), out.ptr, out.dt, hip.strides4(out.strides), hip.ptr(wsb), nb,
+                         hip.stream_ptr())
             else:
                 hip.call("es_conv2d_fwd", C.byref(d), x.dt, x.ptr, hip.strides4(x.strides), hip.ptr(wk),
                          hip.ptr(bias), out.ptr, out.dt, hip.strides4(out.strides), hip.stream_ptr())
         return out
+
+    def _linear_det(self, d, ng, out: Act) -> bool:
+        """A linear (1x1 conv of 1x1 images) with a dense fp32 output of <= 4096 columns: the GEMMs
+        whose split-K the deterministic mode runs through es_conv2d_*_det."""
+        return (self.R == 1 and self.S == 1 and d.P == 1 and d.Q == 1 and d.Hu == 1 and d.Wu == 1
+                and out.t.dtype == torch.float32 and ng <= 4096)
 
     def dgrad(self, dy: Act, x: Act, dx_dtype=None, inv_scale=None, dx: Act = None, beta=0.0,
               bn_reduce=None) -> Act:
@@ -353,6 +366,11 @@ class ConvOp:
                            C.byref(chain), hip.ptr(part), floats, C.byref(chunks), hip.stream_ptr())
                   if chunks.value > 0:
                       dx.bn_sums = (part, chunks.value, nm)
+              elif _DET and float(beta) == 0.0 and self._linear_det(d, d.C, dx):
+                  nb = int(hip.lib().es_conv2d_splitk_ws_bytes(C.byref(d), 1))
+                  wsb = ws(nb, dy.t.device)
+                  hip.call("es_conv2d_dgrad_det", C.byref(d), dy.dt, dy.ptr, hip.strides4(dy.strides), hip.ptr(wd),
+                           dx.ptr, dx.dt, hip.strides4(dx.strides), hip.ptr(wsb), nb, hip.stream_ptr())
               else:
                   hip.call("es_conv2d_dgrad", C.byref(d), dy.dt, dy.ptr, hip.strides4(dy.strides), hip.ptr(wd),
                          dx.ptr, dx.dt, hip.strides4(dx.strides), float(beta), hip.stream_ptr())

@@ -71,6 +71,7 @@ class MoEWrapper(nn.Module):
         self._ed_feat = None       # [B] per-sample photon sums for the router's ED term
         self._w_cache = {}         # class_counts_adjusted device scalars
         self.expert_graphs = bool(cfg_get(cfg, "train.expert_graphs", True))
+        self.expert_graphs_concurrent = True
         self._egraphs = None       # ExpertGraphs (n_experts > 1, single process)
         self._graphs = None
         self._static = None
@@ -176,7 +177,7 @@ class MoEWrapper(nn.Module):
             cond, real_images, true_positions, std, intensity = self._static_inputs(
                 dev, cond, real_images, true_positions, std, intensity)
             if self._egraphs is None:
-                self._egraphs = ExpertGraphs()
+                self._egraphs = ExpertGraphs(concurrent=self.expert_graphs_concurrent)
             self._graphs = self._egraphs
         rc = self.cfg.model.router
         if self._dstep is None or self._dstep.device != dev:
@@ -258,9 +259,19 @@ class MoEWrapper(nn.Module):
                     self._expert_eager.add(e)
             else:
                 # DDP: expert active globally but (almost) absent from this shard -> zero local
-                # gradients, but join the same collectives and optimizer steps as the other ranks
-                self._allreduce(self.discriminators[e]); od.step()
-                self._allreduce(self.generators[e]); self._allreduce(self.aux_regs[e]); og.step(); oa.step()
+                # gradients, but join the same collectives (same ranges, same order: D, A, then G's
+                # backward buckets) and optimizer steps as the other ranks
+                G_, D_, A_ = self.generators[e], self.discriminators[e], self.aux_regs[e]
+                ddp.allreduce_async(D_)
+                ddp.wait_all()
+                od.step()
+                ddp.allreduce_async(A_)
+                ready = ddp.bucketer(G_)
+                for name in G_.READY:
+                    ready(name)
+                ddp.wait_all()
+                og.step()
+                oa.step()
 
         if self._graphs is not None:
             self._graphs.join()
@@ -370,12 +381,18 @@ class MoEWrapper(nn.Module):
                  hip.ptr(dfo), hip.stream_ptr())
         D.bwd(dctx_r, dout=Act.of(dro), weight_grads=True, input_grad=False)
         D.bwd(dctx_f, dout=Act.of(dfo), weight_grads=True, input_grad=False)
-        self._allreduce(D)
-        opt_d.step()
-
-        # ---- generator step (moe.py:529-571)
         n2 = self._noise(e, 1, (be, self.noise_dim), dev, row0=n0)
-        fake2, gctx2 = G.fwd(n2, sc, seed=seed, stream_base=sb(philox.PASS_G2), n_offset=n0)
+        if ddp is None:
+            opt_d.step()
+            # ---- generator step (moe.py:529-571)
+            fake2, gctx2 = G.fwd(n2, sc, seed=seed, stream_base=sb(philox.PASS_G2), n_offset=n0)
+        else:
+            # data parallel: D's gradient all-reduce overlaps the second generator forward (which
+            # does not read D); D's Adam waits for it
+            ddp.allreduce_async(D)
+            fake2, gctx2 = G.fwd(n2, sc, seed=seed, stream_base=sb(philox.PASS_G2), n_offset=n0)
+            ddp.wait_all()
+            opt_d.step()
         fo1, fl1, dctx1 = D.fwd(fake1, sc)
         _, fl2, dctx2 = D.fwd(fake2, sc)
         s = torch.empty(be, dtype=torch.float32, device=dev)
@@ -410,13 +427,17 @@ class MoEWrapper(nn.Module):
         dimg1 = D.bwd(dctx1, dout=Act.of(dfo1), dlat=Act.of(dl1), weight_grads=False, input_grad=True)
         dimg2 = D.bwd(dctx2, dout=None, dlat=Act.of(dl2), weight_grads=False, input_grad=True)
         dimga = A.bwd(actx, Act.of(dcoord), input_grad=True)
+        if ddp is not None:
+            ddp.allreduce_async(A)           # overlaps the generator backward
         copy_act(dimga, dimg1, 1.0, 1.0)
         hip.call("es_image_expsum_bwd", C.byref(fake1.view), fake1.dt, fake1.ptr, hip.ptr(coef),
                  C.byref(dimg1.view), dimg1.ptr, 1.0, hip.stream_ptr())
         G.bwd(gctx1, dimg1)
-        G.bwd(gctx2, dimg2)
-        self._allreduce(G)
-        self._allreduce(A)
+        # data parallel: the second backward finalises G's gradients layer by layer; each >= 1 MB
+        # bucket is all-reduced while the remaining layers' backward runs
+        G.bwd(gctx2, dimg2, ready=ddp.bucketer(G) if ddp is not None else None)
+        if ddp is not None:
+            ddp.wait_all()
         opt_g.step()
         opt_a.step()
 
@@ -483,8 +504,9 @@ class ExpertGraphs:
     is captured and then replayed; BatchNorm batch counts recorded at capture are re-applied on
     every replay."""
 
-    def __init__(self, max_graphs: int = 512):
+    def __init__(self, max_graphs: int = 512, concurrent: bool = True):
         self.pools, self.streams = {}, {}
+        self.concurrent = concurrent     # False: every expert's graph on one side stream (serialised)
         self.graphs = {}
         self.max_graphs = max_graphs
         self.captures = 0
@@ -505,7 +527,8 @@ class ExpertGraphs:
         from ..layers import count_batches, nbt_added, nbt_snapshot
         e = key[0]
         if e not in self.streams:
-            self.streams[e] = torch.cuda.Stream()
+            shared = None if self.concurrent or not self.streams else next(iter(self.streams.values()))
+            self.streams[e] = shared or torch.cuda.Stream()
             self.pools[e] = torch.cuda.graph_pool_handle()
         st = self.streams[e]
         st.wait_event(self._ready)
@@ -514,6 +537,12 @@ class ExpertGraphs:
             if len(self.graphs) >= self.max_graphs:
                 self.graphs = {}
             before = nbt_snapshot()
+            # no capture while other experts' graphs are replaying: measured (tests/test_graph_gpu.py,
+            # E = 3 with every expert captured in one step) a capture overlapping the concurrent
+            # replays corrupted them (metrics of the other experts off at the 1e-2 level; bitwise
+            # equal to the eager steps with this device synchronisation, which torch.cuda.graph's
+            # own capture protocol also performs).  A capture happens once per (expert, B_e) key.
+            torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             # capture on the expert's own stream (torch.cuda.graph's gc.collect + empty_cache per
             # capture cost ~10 ms; the experts' captures do not need them)
@@ -537,6 +566,6 @@ class ExpertGraphs:
     def join(self):
         """The current stream waits for every expert graph of this step."""
         cur = torch.cuda.current_stream()
-        for st in self._used:
+        for st in set(self._used):
             cur.wait_stream(st)
         self._used = []

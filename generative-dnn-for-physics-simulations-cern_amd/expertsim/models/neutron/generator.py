@@ -32,6 +32,10 @@ P_DROP = 0.2
 class GeneratorNeutron(ExpertModule):
     base = 13          # fc2 reshapes to 128 x base x base; the image is (4*base - 8)^2
 
+    # the parameters bwd() reports through ready(), in order (data-parallel gradient buckets)
+    READY = ("conv_layers.13.weight", "conv_layers.9.weight", "conv_layers.5.weight", "conv_layers.0.weight",
+             "fc2.0.weight", "fc1.0.weight")
+
     def __init__(self, noise_dim, cond_dim, di_strength, in_strength, **kwargs):
         super().__init__()
         self.name = "Generator-neutron-1-original-architecture"
@@ -119,30 +123,36 @@ class GeneratorNeutron(ExpertModule):
         return img, ctx
 
     # --------------------------------------------------------------------------- backward
-    def bwd(self, ctx, dimg: Act):
-        """Accumulate parameter gradients (flat grad buffer) for d loss / d image."""
+    def bwd(self, ctx, dimg: Act, ready=None):
+        """Accumulate parameter gradients (flat grad buffer) for d loss / d image.  ready(name): the
+        gradients from parameter ``name`` to the end of the flat buffer are final (DP buckets)."""
+        ready = ready or (lambda name: None)
         o = self.ops()
         cdt = self.compute_dtype
         g = lambda n, a: getattr(get_module(self, n), a).grad
         ch = ctx["ch"]
         dh6 = act_bwd(ctx["h6"], hip.chain_struct(hip.ACT_RELU), dimg, dx_dtype=cdt)
         o["c13"].wgrad(dh6, ctx["y5"], g("conv_layers.13", "weight"), g("conv_layers.13", "bias"))
+        ready("conv_layers.13.weight")
         # (the thin dgrad also runs bn5's backward reduction over dy5, ConvOp.dgrad bn_reduce)
         dy5 = o["c13"].dgrad(dh6, ctx["y5"], bn_reduce=(o["bn5"], ctx["h5"], ctx["s5"], ch[4]))
         dh5 = o["bn5"].bwd(ctx["h5"], ctx["s5"], ch[4], dy5, dgamma=g("conv_layers.10", "weight"),
                            dbeta=g("conv_layers.10", "bias"), dsum=g("conv_layers.9", "bias"))
         o["c9"].wgrad(dh5, ctx["y4"], g("conv_layers.9", "weight"), None)
+        ready("conv_layers.9.weight")
         # the dgrad epilogue also runs bn4's backward reduction over dy4 (ConvOp.dgrad bn_reduce)
         dy4 = o["c9"].dgrad(dh5, ctx["y4"], bn_reduce=(o["bn4"], ctx["h4"], ctx["s4"], ch[3]))
         dh4 = o["bn4"].bwd(ctx["h4"], ctx["s4"], ch[3], dy4, dgamma=g("conv_layers.6", "weight"),
                            dbeta=g("conv_layers.6", "bias"), dsum=g("conv_layers.5", "bias"))
         o["c5"].wgrad(dh4, ctx["y3"], g("conv_layers.5", "weight"), None)
+        ready("conv_layers.5.weight")
         # (no fused reduction here: the 256 x 256 sub-pixel DGRAD has no registers to spare for it,
         # measured 585 -> 871 us for a 146 us reduce pass, DESIGN.md §4)
         dy3 = o["c5"].dgrad(dh4, ctx["y3"])
         dh3 = o["bn3"].bwd(ctx["h3"], ctx["s3"], ch[2], dy3, dgamma=g("conv_layers.1", "weight"),
                            dbeta=g("conv_layers.1", "bias"), dsum=g("conv_layers.0", "bias"))
         o["c0"].wgrad(dh3, ctx["y2n"], g("conv_layers.0", "weight"), None)
+        ready("conv_layers.0.weight")
         dy2n = o["c0"].dgrad(dh3, ctx["y2n"])
         B, k, F2 = dy2n.dims[0], self.base, self.fc2_features
         dy2 = Act.rows(B, F2, cdt, dy2n.t.device)
@@ -150,11 +160,13 @@ class GeneratorNeutron(ExpertModule):
         dh2 = o["bn2"].bwd(ctx["h2"], ctx["s2"], ch[1], dy2, dgamma=g("fc2.1", "weight"),
                            dbeta=g("fc2.1", "bias"), dsum=g("fc2.0", "bias"))
         o["fc2"].wgrad(dh2, ctx["y1"], g("fc2.0", "weight"), None)
+        ready("fc2.0.weight")
         # fp32 dense output: lets the K = 21632 GEMM split K across workgroups (8 output tiles)
         dy1 = o["fc2"].dgrad(dh2, ctx["y1"], dx_dtype=torch.float32)
         dh1 = o["bn1"].bwd(ctx["h1"], ctx["s1"], ch[0], dy1, dx_dtype=cdt, dgamma=g("fc1.1", "weight"),
                            dbeta=g("fc1.1", "bias"), dsum=g("fc1.0", "bias"))
         o["fc1"].wgrad(dh1, ctx["x0"], g("fc1.0", "weight"), None)
+        ready("fc1.0.weight")
 
     # --------------------------------------------------------------------------- nn.Module API
     def forward(self, noise, cond):

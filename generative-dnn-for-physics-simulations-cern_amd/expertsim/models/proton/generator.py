@@ -20,6 +20,10 @@ FEAT = 512 * 18 * 10
 
 
 class Generator(ExpertModule):
+    # the parameters bwd() reports through ready(), in order (data-parallel gradient buckets)
+    READY = ("conv_layers.11.weight", "conv_layers.8.weight", "conv_layers.5.weight", "conv_layers.1.weight",
+             "fc2.0.weight", "fc1.0.weight")
+
     def __init__(self, noise_dim, cond_dim, di_strength, in_strength, **kwargs):
         super().__init__()
         self.name = "Generator-v5-bigkernel-res56x30"
@@ -81,31 +85,39 @@ class Generator(ExpertModule):
         img = act_fwd(c["h6"], hip.chain_struct(hip.ACT_RELU))
         return img, c
 
-    def bwd(self, c, dimg: Act):
+    def bwd(self, c, dimg: Act, ready=None):
+        """ready(name): gradients from parameter ``name`` to the end of the flat buffer are final."""
+        ready = ready or (lambda name: None)
         o = self.ops()
         cdt = self.compute_dtype
         g = lambda n, a="weight": getattr(get_module(self, n), a).grad
         lr = hip.chain_struct(hip.ACT_LRELU, SLOPE)
         dh6 = act_bwd(c["h6"], hip.chain_struct(hip.ACT_RELU), dimg, dx_dtype=cdt)
         o["c11"].wgrad(dh6, c["y5"], g("conv_layers.11"), g("conv_layers.11", "bias"))
+        ready("conv_layers.11.weight")
         dy5 = o["c11"].dgrad(dh6, c["y5"])
         dh5 = o["gn3"].bwd(c["h5"], c["s5"], lr, dy5, dgamma=g("conv_layers.9"), dbeta=g("conv_layers.9", "bias"), dsum=g("conv_layers.8", "bias"))
         o["c8"].wgrad(dh5, c["y4"], g("conv_layers.8"), None)
+        ready("conv_layers.8.weight")
         dy4 = o["c8"].dgrad(dh5, c["y4"])
         dh4 = o["gn2"].bwd(c["h4"], c["s4"], lr, dy4, dgamma=g("conv_layers.6"), dbeta=g("conv_layers.6", "bias"), dsum=g("conv_layers.5", "bias"))
         o["c5"].wgrad(dh4, c["y3"], g("conv_layers.5"), None)
+        ready("conv_layers.5.weight")
         dy3 = o["c5"].dgrad(dh4, c["y3"])
         dh3 = o["gn1"].bwd(c["h3"], c["s3"], lr, dy3, dgamma=g("conv_layers.2"), dbeta=g("conv_layers.2", "bias"), dsum=g("conv_layers.1", "bias"))
         o["c1"].wgrad(dh3, c["y2n"], g("conv_layers.1"), None)
+        ready("conv_layers.1.weight")
         dy2n = o["c1"].dgrad(dh3, c["y2n"])
         B = dy2n.dims[0]
         dy2 = Act.rows(B, FEAT, cdt, dy2n.t.device)
         copy_act(dy2n, Act(dy2.t, (B, 512, 18, 10), (FEAT, 180, 10, 1)))
         dh2 = o["ln2"].bwd(c["h2"], c["s2"], lr, dy2, dgamma=g("fc2.1"), dbeta=g("fc2.1", "bias"), dsum=g("fc2.0", "bias"))
         o["fc2"].wgrad(dh2, c["y1"], g("fc2.0"), None)
+        ready("fc2.0.weight")
         dy1 = o["fc2"].dgrad(dh2, c["y1"], dx_dtype=torch.float32)   # fp32: split-K over K = 92160
         dh1 = o["ln1"].bwd(c["h1"], c["s1"], lr, dy1, dx_dtype=cdt, dgamma=g("fc1.1"), dbeta=g("fc1.1", "bias"), dsum=g("fc1.0", "bias"))
         o["fc1"].wgrad(dh1, c["x0"], g("fc1.0"), None)
+        ready("fc1.0.weight")
 
     def forward(self, noise, cond):
         from ..autograd import generator_apply

@@ -28,8 +28,10 @@ data-parallel over a node's GPUs.  Semantics:
     the global batch); a rank with too few local samples contributes zero gradients but joins every
     collective, so the collective sequence is identical on all ranks;
   * metrics are merged across ranks on the device (one all-gather of the [E, 10] metric rows);
-  * one flat all-reduce per model per optimizer phase (D; G and A; router) — the flat parameter
-    buffers make each model a single bucket.
+  * gradient all-reduces overlap the compute (``allreduce_async`` on the process group's stream):
+    the discriminator's with the second generator forward, the aux regressor's with the generator
+    backward, and the generator's in >= 1 MB buckets issued as its second backward finalises each
+    layer group (``bucketer``; the flat buffer's tail first); the optimizer steps wait for them.
 """
 from __future__ import annotations
 
@@ -53,6 +55,8 @@ class DataParallel:
         self.local_batch = None
         self._counts_dev = {}
         self.expert = None         # expert whose step is running (global count for SyncBN)
+        self._pending = []         # async all-reduce works not yet waited for
+        self.issued = []           # (module, lo, hi) of every gradient all-reduce (tests)
 
     # ---------------------------------------------------------------- collectives on device tensors
     def all_reduce_(self, t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
@@ -132,6 +136,42 @@ class DataParallel:
         g = module.flat_grads
         self.all_reduce_(g)
         module._grad_scale = 1.0 / self.world if average else 1.0
+
+    # ---------------------------------------------------------------- overlapped gradient all-reduce
+    def allreduce_async(self, module, average=True, lo=0, hi=None):
+        """SUM-all-reduce flat_grads[lo:hi] on the process group's own stream, overlapping the compute
+        issued after it; wait_all() makes the current stream wait before an optimizer reads the
+        gradients.  Every rank issues the same ranges in the same order (the collectives of one
+        process group run in issue order), so this never reorders collectives across ranks."""
+        g = module.flat_grads
+        hi = g.numel() if hi is None else hi
+        if hi > lo:
+            if self.gloo:
+                self.all_reduce_(g[lo:hi])
+            else:
+                self._pending.append(dist.all_reduce(g[lo:hi], group=self.group, async_op=True))
+            self.issued.append((module, lo, hi))
+        module._grad_scale = 1.0 / self.world if average else 1.0
+
+    def wait_all(self):
+        for w in self._pending:
+            w.wait()
+        self._pending = []
+
+    def bucketer(self, module, min_floats=1 << 18):
+        """``ready(name)`` hook for a module's backward: layers finish in reverse flat-buffer order,
+        so once the backward reports parameter ``name`` done, every gradient from its offset to the
+        end of the buffer is final; they are all-reduced in buckets of >= min_floats floats (1 MB)
+        while the rest of the backward runs (the last call, at offset 0, flushes the remainder)."""
+        offs = {n: o for (n, _), o in zip(module.named_parameters(), module._offsets())}
+        state = {"hi": module.flat_grads.numel()}
+
+        def ready(name):
+            lo = offs[name]
+            if state["hi"] - lo >= min_floats or lo == 0:
+                self.allreduce_async(module, True, lo, state["hi"])
+                state["hi"] = lo
+        return ready
 
     # ---------------------------------------------------------------- metrics
     def merge_metrics(self, mbuf: torch.Tensor):

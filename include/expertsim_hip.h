@@ -158,6 +158,17 @@ int64_t es_conv2d_wgrad_det_ws_bytes(const es_conv_desc_t* d, es_dtype_t dt, con
 int es_conv2d_wgrad_det(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, const int64_t ys[4],
                         const void* x, const int64_t xs[4], float* dw, float beta, void* ws, int64_t ws_bytes,
                         es_stream_t stream);
+/* Deterministic split-K (parity mode) of es_conv2d_fwd / es_conv2d_dgrad (beta 0): when the GEMM
+ * has few output tiles and a long K (the generators' fc2 dgrad, K = 21632 / 92160), the K splits
+ * store partials into ws and one ordered sum writes y / dx (fp32, dense), instead of float
+ * atomics.  ws: es_conv2d_splitk_ws_bytes(d, mode) bytes (mode 0 FWD, 1 DGRAD). */
+int64_t es_conv2d_splitk_ws_bytes(const es_conv_desc_t* d, int mode);
+int es_conv2d_fwd_det(const es_conv_desc_t* d, es_dtype_t dt, const void* x, const int64_t xs[4], const void* wk,
+                      const float* bias, void* y, es_dtype_t ydt, const int64_t ys[4], void* ws, int64_t ws_bytes,
+                      es_stream_t stream);
+int es_conv2d_dgrad_det(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, const int64_t ys[4], const void* wd,
+                        void* dxu, es_dtype_t dxdt, const int64_t dxs[4], void* ws, int64_t ws_bytes,
+                        es_stream_t stream);
 /* Deterministic mode on / off (returns the previous setting): fp32 FWD / DGRAD take no split-K
  * float atomics, the generic norm backward's conv-bias sums become an ordered column reduction.
  * MoEWrapper turns it on in the fp32 parity mode (train.deterministic, default on). */

@@ -52,6 +52,19 @@ def _run(E, B, rank=0, ddp=None):
         m = moe.train_step(0, t["cond"], t["real_images"].unsqueeze(1), t["true_positions"], t["std"],
                            t["intensity"], oa, og, od, orr, None, dev)
         torch.cuda.synchronize()
+        if ddp is not None:
+            # the overlapped / bucketed gradient all-reduces of the step cover every model's flat
+            # gradient buffer exactly once (ddp.bucketer, ddp.allreduce_async)
+            by_mod = {}
+            for mod, lo, hi in ddp.issued:
+                by_mod.setdefault(id(mod), (mod, []))[1].append((lo, hi))
+            for mod, ranges in by_mod.values():
+                ranges.sort()
+                assert ranges[0][0] == 0 and ranges[-1][1] == mod.flat_grads.numel(), ranges
+                assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:])), ranges
+            assert len(by_mod) == 3 * E, len(by_mod)
+            assert any(len(r) > 1 for _, r in by_mod.values())     # the generator's buckets
+            ddp.issued.clear()
         params = {n: p.detach().double().cpu().numpy().copy() for n, p in moe.named_parameters()}
         out.append(({k: float(v) for k, v in m.items()}, params))
     lr = {"generators": cfg.model.generator.lr_g, "discriminators": cfg.model.discriminator.lr_d,

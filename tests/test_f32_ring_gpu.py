@@ -163,3 +163,30 @@ def test_wgrad_det_generic_paths(shape, det):
         outs.append(dw.cpu())
     assert torch.equal(outs[0], outs[1])
     assert rel(outs[0].double() - 0.5, wr.grad) < 2e-5
+
+
+@pytest.mark.parametrize("shape", [(300, 21632, 256), (500, 1305, 128)])
+def test_linear_det_splitk(shape, det):
+    """Long-K fp32 linears (the generator's fc2 dgrad, K = 21632; the discriminator fc1 forward,
+    K = 1305): deterministic split-K (es_conv2d_fwd_det / es_conv2d_dgrad_det), against torch fp64
+    and bitwise on rerun."""
+    _hip()
+    from expertsim.layers import Act, ConvOp
+    N, Fin, Fout = shape
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(N, Fin, generator=g, dtype=torch.float64)
+    w = torch.randn(Fout, Fin, generator=g, dtype=torch.float64) / np.sqrt(Fin)
+    b = torch.randn(Fout, generator=g, dtype=torch.float64)
+    gy = torch.randn(N, Fout, generator=g, dtype=torch.float64)
+    op = ConvOp(torch.nn.Parameter(w.float().to(DEV)), torch.nn.Parameter(b.float().to(DEV)))
+    xa = Act.of(x.float().to(DEV).contiguous())
+    gya = Act.of(gy.float().to(DEV).contiguous())
+    outs = []
+    for _ in range(2):
+        y = op.fwd(xa, out_dtype=torch.float32)
+        dx = op.dgrad(gya, xa, dx_dtype=torch.float32)
+        torch.cuda.synchronize()
+        outs.append((y.rows2d().cpu(), dx.rows2d().cpu()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert rel(outs[0][0].double(), x @ w.T + b) < 2e-5
+    assert rel(outs[0][1].double(), gy @ w) < 2e-5

@@ -1,7 +1,8 @@
 """Run ONE conv op of the neutron generator a few times (for rocprofv3 --pmc passes).
 
 usage: python tools/mb_one.py <c0|c5|c9> <fwd|dgrad|wgrad> [ring 1|0] [reps]
-(ES_MB_BATCH=<images> overrides the batch of 512)"""
+(ES_MB_BATCH=<images> overrides the batch of 512; ES_MB_DTYPE=fp32 runs the parity mode's fp32 ring
+kernels with the deterministic weight gradient)"""
 import os
 import sys
 
@@ -28,21 +29,26 @@ def main():
     w = torch.nn.Parameter(torch.randn(Cout, Cin, k, k, device=dev) / (Cin * k * k) ** 0.5)
     b = torch.nn.Parameter(torch.randn(Cout, device=dev))
     op = ConvOp(w, b, stride=st, pad=pad, upsample=Upsample((H, W), scale=up) if up else None)
-    x = Act.nhwc(N, Cin, H, W, torch.bfloat16, dev)
+    f32 = os.environ.get("ES_MB_DTYPE", "bf16") == "fp32"
+    dt = torch.float32 if f32 else torch.bfloat16
+    if f32:
+        from expertsim import layers
+        layers.set_deterministic(True)
+    x = Act.nhwc(N, Cin, H, W, dt, dev)
     x.t.normal_()
-    y = op.fwd(x, out_dtype=torch.bfloat16)
-    dy = y.like_nhwc(torch.bfloat16)
+    y = op.fwd(x, out_dtype=dt)
+    dy = y.like_nhwc(dt)
     dy.t.normal_()
-    op.packed(torch.bfloat16, 1)
+    dw = torch.zeros_like(w)
     torch.cuda.synchronize()
 
     def run():
         if mode == "fwd":
-            op.fwd(x, out_dtype=torch.bfloat16)
+            op.fwd(x, out_dtype=dt)
         elif mode == "dgrad":
-            op.dgrad(dy, x, dx_dtype=torch.bfloat16)
+            op.dgrad(dy, x, dx_dtype=dt)
         else:
-            op.wgrad(dy, x, None, None)
+            op.wgrad(dy, x, dw, None, beta=0.0)
     run()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
