@@ -97,6 +97,9 @@ __device__ __forceinline__ uint32_t keep4(const u32x4 w, uint32_t thr) {
 // not apply; lanes whose 4 rows straddle a sample, or whose neighbour does, compute their own.
 __device__ __forceinline__ bool keep_bits_gen_shared(const FastArgs& a, int r0, int c0, uint32_t thr,
                                                      uint32_t k0, uint32_t k1, uint32_t (&keep)[4]) {
+#if defined(__AMDGCN_WAVEFRONT_SIZE) && __AMDGCN_WAVEFRONT_SIZE != 64
+  return false;   // the row-group / shuffle arithmetic below is for 64-lane waves (gfx950)
+#endif
   const int tcv = min(a.C >> 3, 64);
   if (64 % tcv != 0 || 64 / tcv < 8) return false;          // uniform over the launch
   const int lane = threadIdx.x & 63, rgw = lane / tcv, cvl = lane - rgw * tcv, RGW = 64 / tcv;

@@ -285,6 +285,35 @@ def test_norm_chain(kind, drop):
         assert torch.equal(dg2, dg) and torch.equal(db2, dbt)
 
 
+@pytest.mark.parametrize("shape", [(4, 64, 9, 7), (3, 64, 8, 6), (5, 16, 9, 9), (2, 32, 45, 45)])
+@pytest.mark.parametrize("k", [1, 2, 3, 6])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_keep_bits_element_offset(shape, k, dtype):
+    """Stored dropout keep bits with an element index_offset that is not a multiple of 4 (ADVICE
+    r02): the fast forward's counter sharing (keep_bits_gen_shared, C <= 64, and the aligned path)
+    depends on (i0 & 3) including the offset.  Bit-exact against the host Philox at that offset."""
+    hip = _hip()
+    from expertsim.layers import NormOp
+    from expertsim.utils import philox
+    torch.manual_seed(3)
+    x = torch.randn(*shape) * 2 + 0.5
+    N, C_, H, W = shape
+    p, seed, stream = 0.2, 99, 41
+    xa = to_act(x, dtype)
+    ch = hip.chain_struct(hip.ACT_LRELU, 0.1, hip.dropout_struct(p, seed, stream, enabled=True, index_offset=k),
+                          dropout_first=True)
+    rows = N * H * W
+    kb = hip.attach_keep(ch, rows, C_, DEV)
+    op = NormOp(hip.NORM_BN, torch.ones(C_, device=DEV), torch.zeros(C_, device=DEV),
+                running_mean=torch.zeros(C_, device=DEV), running_var=torch.ones(C_, device=DEV))
+    op.fwd(xa, ch)
+    torch.cuda.synchronize()
+    bits = philox.random_bits(x.numel(), seed, stream, k)
+    m = ((bits >> np.uint32(8)) < np.uint32(philox.keep_threshold(p))).reshape(shape)
+    keep = np.unpackbits(kb.cpu().numpy().reshape(rows, C_ // 8), axis=1, bitorder="little").astype(bool)
+    assert np.array_equal(keep, m.transpose(0, 2, 3, 1).reshape(rows, C_))
+
+
 def test_dropout_mask_bit_exact():
     hip = _hip()
     from expertsim.utils import philox
