@@ -1,5 +1,5 @@
-"""The BASELINE.json GPU workloads through the HIP path (bf16 performance mode), checked by
-size-independent properties (the elementwise parity pins are the fp32 goldens in
+"""The BASELINE.json GPU workloads through the HIP path, in the fp32 parity mode (the bench headline
+since round 3) and the bf16 performance mode, checked by size-independent properties (the elementwise parity pins are the fp32 goldens in
 test_train_step_gpu.py / test_grads_gpu.py; bf16 statistical parity is test_bf16_stats_gpu.py):
 
   configs[1]  neutron 44x44, E=1, B=512
@@ -36,11 +36,12 @@ def _keys(E):
     return k
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
 @pytest.mark.parametrize("arch,E,B", CONFIGS)
-def test_config_steps(arch, E, B):
+def test_config_steps(arch, E, B, precision):
     import bench
     from expertsim.utils.synthetic import make_batch
-    moe, (og, od, oa, orr), cfg = bench.build(arch, E, "bf16", 1234, torch.device(DEV))
+    moe, (og, od, oa, orr), cfg = bench.build(arch, E, precision, 1234, torch.device(DEV))
     b = make_batch(B, arch, seed=5)
     t = {k: torch.from_numpy(v).to(DEV) for k, v in b.items()}
     real = t["real_images"].unsqueeze(1).contiguous()
