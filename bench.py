@@ -222,7 +222,10 @@ def probe_dominant(moe, eager_step, steps, arch, batch, precision):
                     "decomposition executes 4/9 of those MACs, so frac_executed = MFMA work actually issued / peak",
             "mfma_busy_pmc": mfma_busy,
             "flop_per_launch": flops, "avg_ms": round(avg_ms, 4), "launches": stats[dom]["count"],
-            "all_probed": {k: {"avg_ms": round(v["avg_ms"], 4),
+            "kernel_launches_per_op": stats[dom].get("kernel_launches_per_op"),
+            "launch_note": "avg_ms is per op; an fp32 op over > 1 GiB operands runs as image chunks "
+                           "(kernel_launches_per_op MFMA kernels, rocprof lists each chunk separately)",
+            "all_probed": {k: {"avg_ms": round(v["avg_ms"], 4), "kernels": v.get("kernel_launches_per_op"),
                                "tflops": round(flops / (v["avg_ms"] * 1e-3) / 1e12, 2)}
                            for k, v in stats.items()}}
 

@@ -2009,9 +2009,15 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   }
 }
 
+// host-side count of the MFMA conv kernels issued (ring / persistent / p256 / fp32 wgrad), read by
+// bench.py's probe to state how many launches one probed op is (fp32 image chunks)
+int64_t g_conv_launches = 0;
+extern "C" int64_t es_conv_launch_count() { return g_conv_launches; }
+
 template <int MODE, int BM, int BN, bool SP, int BK = 64, typename T = bf16>
 void launch_ring(const ConvArgs& a, int row_tiles, hipStream_t st) {
   dim3 grid(row_tiles, (a.Ng + BN - 1) / BN, 1);
+  ++g_conv_launches;
   hipLaunchKernelGGL((conv_ring_kernel<MODE, BM, BN, SP, BK, T>), grid, dim3(RT), 0, st, a);
 }
 
@@ -2030,6 +2036,7 @@ void launch_wgrad_ring(ConvArgs& a, hipStream_t st) {
   const int per = (ks + want - 1) / want;
   a.k_per_split = per;
   dim3 grid(a.M / BM, taps * a.d.C / BN, (ks + per - 1) / per);
+  ++g_conv_launches;
   hipLaunchKernelGGL((wgrad_ring_kernel<BM, BN, SP, MT>), grid, dim3(RT), 0, st, a);
 }
 
@@ -2268,6 +2275,7 @@ int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
         g_bnr_req.chunks = nwg;
         bnr = true;
       }
+      ++g_conv_launches;
       if (mode == MODE_FWD) {
         if (a.Ng == 64) hipLaunchKernelGGL((conv_persist_kernel<MODE_FWD, 64>), dim3(nwg), dim3(RT), 0, st, a, ntiles);
         else hipLaunchKernelGGL((conv_persist_kernel<MODE_FWD, 128>), dim3(nwg), dim3(RT), 0, st, a, ntiles);
@@ -2325,12 +2333,14 @@ int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
         a.stats_part = g_stats_req.part;
         g_stats_req.chunks = 256 * 4;
       }
+      ++g_conv_launches;
       if (NT == 1) hipLaunchKernelGGL((conv_p256_kernel<1>), dim3(256), dim3(RT), 0, st, a, row_tiles);
       else if (NT == 2) hipLaunchKernelGGL((conv_p256_kernel<2>), dim3(256), dim3(RT), 0, st, a, row_tiles);
       else hipLaunchKernelGGL((conv_p256_kernel<4>), dim3(256), dim3(RT), 0, st, a, row_tiles);
       return 1;
     }
     dim3 grid(row_tiles, (4 * a.Ng + 255) / 256, 1);
+    ++g_conv_launches;
     hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 256, true, 32, T>), grid, dim3(RT), 0, st, a);
     return 1;
   }
@@ -2482,6 +2492,7 @@ int es_wgrad_f32_ring(const es_conv_desc_t& d, const void* dy, const int64_t ys[
     dim3 grid(d.K / p.bm, p.ngt / p.bn, p.sc);
 #define ES_WF(BM, BN)                                                                                 \
   do {                                                                                                \
+    ++g_conv_launches;                                                                                \
     if (p.sp) hipLaunchKernelGGL((wgrad_f32_kernel<BM, BN, true>), grid, dim3(RT), 0, st, a, wsc, p.ngt);   \
     else hipLaunchKernelGGL((wgrad_f32_kernel<BM, BN, false>), grid, dim3(RT), 0, st, a, wsc, p.ngt);       \
   } while (0)

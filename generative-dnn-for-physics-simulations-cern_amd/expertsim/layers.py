@@ -94,6 +94,7 @@ class KernelProbe:
     def __init__(self, targets):
         self.targets = set(targets)
         self.events = {t: [] for t in targets}
+        self.launches = {t: [] for t in targets}   # MFMA conv kernels issued per probed op
 
     def wants(self, label):
         return label in self.targets
@@ -103,8 +104,10 @@ class KernelProbe:
         ev.record()
         return ev
 
-    def add(self, label, start, end):
+    def add(self, label, start, end, launches=None):
         self.events[label].append((start, end))
+        if launches is not None:
+            self.launches[label].append(launches)
 
     def summary(self):
         torch.cuda.synchronize()
@@ -113,6 +116,8 @@ class KernelProbe:
             if pairs:
                 ms = [a.elapsed_time(b) for a, b in pairs]
                 out[k] = {"count": len(ms), "total_ms": sum(ms), "avg_ms": sum(ms) / len(ms)}
+                if self.launches[k]:
+                    out[k]["kernel_launches_per_op"] = max(self.launches[k])
         return out
 
 
@@ -131,11 +136,12 @@ class _probed:
 
     def __enter__(self):
         if self.on:
+            self.n0 = hip.lib().es_conv_launch_count()
             self.t0 = _PROBE.record(self.label)
 
     def __exit__(self, *exc):
         if self.on:
-            _PROBE.add(self.label, self.t0, _PROBE.record(self.label))
+            _PROBE.add(self.label, self.t0, _PROBE.record(self.label), hip.lib().es_conv_launch_count() - self.n0)
 
 
 def copy_act(src: Act, dst: Act, alpha=1.0, beta=0.0):

@@ -176,6 +176,9 @@ int es_set_deterministic(int on);
 /* Test knob: fp32 ring convolutions launch over chunks of at most `images` images (0: only as the
  * 1 GiB operand limit requires); returns the previous value. */
 int es_conv_set_f32_chunk(int images);
+/* Host-side count of MFMA conv kernels issued so far (ring / persistent / p256 / fp32 WGRAD).
+ * Instrumentation only: lets a profiler state how many kernel launches one conv op was. */
+int64_t es_conv_launch_count(void);
 
 /* Weight packing for the implicit GEMM (fp32 master [K][C][R][S] -> dt).
  * mode 0: out[k][r][s][c] = w*scale ; mode 1: out[c][r][s][k] = w*scale.
