@@ -3,8 +3,9 @@
 
 Default workload = BASELINE configs[2]: neutron 44x44 ZDC GAN with SDI diversity + auxiliary coord
 regressor (always on in the reference), 1 expert, batch 1024 per GPU, synthetic data resident in HBM,
-in the reference's own fp32 arithmetic (exact fp32 MFMA, deterministic reductions: the mode the
-golden parity tests pin).  One "step" = ``MoEWrapper.train_step`` (router, G fwd x2 + bwd x2, D fwd
+in fp32 arithmetic (split-fp32 MFMA: every fp32 operand as the exact sum of three bf16 planes, six
+plane products per fp32 product accumulated in fp32, deterministic reductions: the mode the golden
+parity tests pin; --fp32-mfma exact runs the convs on the fp32 MFMA instead).  One "step" = ``MoEWrapper.train_step`` (router, G fwd x2 + bwd x2, D fwd
 x4 + bwd x4, aux regressor fwd/bwd, losses, four fused Adam updates; with N > 1 also the RCCL
 gradient all-reduces, SyncBN by default).  Beside the headline it measures the bf16 performance
 mode (bf16 GEMM operands, fp32 accumulation) as ``perf_bf16``.
@@ -35,6 +36,10 @@ sys.path.insert(0, ROOT)
 # no reference model) 16.868 GFLOP = 6*2746.3 + 12*8.05 + 3*97.9 MFLOP (same counter on the oracle)
 STEP_FLOP_PER_IMAGE = {"neutron": 10.573e9, "proton": 28.566e9, "neutron56": 16.868e9}
 PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
+# split-fp32 (train.fp32_mfma: split): one fp32 product = 6 bf16 plane products on the 2.5 PF/s
+# dense bf16 MFMA, i.e. an fp32-product ceiling of 2500 / 6 TFLOP/s
+SPLIT_PRODUCTS = 6
+PEAK_SPLIT = PEAK_TFLOPS["bf16"] / SPLIT_PRODUCTS
 IMAGE = {"neutron": "44x44", "proton": "56x30", "neutron56": "56x56"}
 
 
@@ -42,7 +47,7 @@ def traffic_json(arch, batch, precision, mode):
     """Committed PMC passes of the roofline kernel: bf16 tools/gpu_traffic.sh -> tools/traffic_json.py,
     fp32 tools/gpu_traffic32.sh -> tools/traffic32.py."""
     name = (f"traffic_{arch}_c5_{mode}_b{batch}.json" if precision == "bf16"
-            else f"traffic32_{arch}_c5_{mode}_b{batch}.json")
+            else f"traffic32{'s' if FP32_MFMA == 'split' else ''}_{arch}_c5_{mode}_b{batch}.json")
     p = os.path.join(ROOT, "profiles", name)
     return p if os.path.exists(p) else None
 
@@ -81,6 +86,9 @@ def conv_flops_per_image(arch):
     return 2 * 55 * 29 * 128 * (256 * 16)   # proton conv_layers.5: 256x56x30 -> 128x55x29, k4 p1
 
 
+FP32_MFMA = "split"   # train.fp32_mfma of the fp32 line (--fp32-mfma)
+
+
 def build(arch, E, precision, seed, device):
     import torch
     from expertsim.config import inject_shared, load_config
@@ -88,7 +96,7 @@ def build(arch, E, precision, seed, device):
     from expertsim.models.moe import MoEWrapper
     from expertsim.train.training_setup import setup_optimizers
     ov = [f"model.architecture={arch}", f"model.n_experts={E}", f"train.precision={precision}",
-          f"train.rng_seed={seed}"]
+          f"train.rng_seed={seed}", f"train.fp32_mfma={FP32_MFMA}"]
     if E > 1:
         ov.append("model.router.diff_strength=1e-6")     # default.yaml '1-6' 
     cfg = inject_shared(load_config(overrides=ov))
@@ -203,7 +211,8 @@ def probe_dominant(moe, eager_step, steps, arch, batch, precision):
     dom = max(stats, key=lambda k: stats[k]["total_ms"])
     avg_ms = stats[dom]["avg_ms"]
     achieved = flops / (avg_ms * 1e-3) / 1e12
-    peak = PEAK_TFLOPS[precision]
+    split = precision == "fp32" and FP32_MFMA == "split"
+    peak = PEAK_SPLIT if split else PEAK_TFLOPS[precision]
     traffic, tnote, mfma_busy = None, None, None
     tj_path = traffic_json(arch, batch, precision, dom.split(".")[-1])
     if tj_path:
@@ -213,13 +222,17 @@ def probe_dominant(moe, eager_step, steps, arch, batch, precision):
         tnote = (f"HBM bytes per op: FETCH_SIZE x2 {tj['fetch_bytes']} + WRITE_SIZE {tj['write_bytes']} "
                  f"(algorithmic {tj['algorithmic_bytes']}), {os.path.relpath(tj_path, ROOT)}")
     executed = achieved * SUBPIXEL_MAC_RATIO if arch != "proton" else achieved
-    return {"bound": "mfma", "kernel": f"{dom} (generator conv_layers.5, "
-                                       f"{'conv_ring bf16' if precision == 'bf16' else 'conv_ring fp32, v_mfma_f32_16x16x4_f32'})",
+    kname = ("conv_ring bf16" if precision == "bf16" else
+             "conv_ring split-fp32, 6 x v_mfma_f32_16x16x32_bf16 per fp32 product" if split else
+             "conv_ring fp32, v_mfma_f32_16x16x4_f32")
+    return {"bound": "mfma", "kernel": f"{dom} (generator conv_layers.5, {kname})",
             "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_note": tnote,
             "frac_executed": round(executed / peak, 4),
             "note": "achieved = the reference's (algorithmic) 3x3-conv FLOPs / kernel time; the sub-pixel "
-                    "decomposition executes 4/9 of those MACs, so frac_executed = MFMA work actually issued / peak",
+                    "decomposition executes 4/9 of those MACs, so frac_executed = MFMA work actually issued / peak"
+                    + ("; split-fp32 peak = 2500 TFLOP/s dense bf16 / 6 plane products per fp32 product "
+                       "(frac_executed x 6 = bf16 MFMA work issued / 2500)" if split else ""),
             "mfma_busy_pmc": mfma_busy,
             "flop_per_launch": flops, "avg_ms": round(avg_ms, 4), "launches": stats[dom]["count"],
             "kernel_launches_per_op": stats[dom].get("kernel_launches_per_op"),
@@ -282,10 +295,12 @@ def main():
     ap.add_argument("--arch", default="neutron", choices=["neutron", "proton", "neutron56"])
     ap.add_argument("--experts", type=int, default=1)
     ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
-                    help="headline: fp32 = the reference's precision (exact fp32 MFMA, the mode the golden "
-                         "parity tests pin); bf16 = bf16 GEMM operands, fp32 accumulation")
+                    help="headline: fp32 = the reference's precision (split-fp32 or exact fp32 MFMA, the mode "
+                         "the golden parity tests pin); bf16 = bf16 GEMM operands, fp32 accumulation")
     ap.add_argument("--other-steps", type=int, default=50,
                     help="timed steps of the other precision's secondary line (0: skip)")
+    ap.add_argument("--fp32-mfma", choices=["exact", "split"], default="split",
+                    help="fp32 conv arithmetic: exact fp32 MFMA, or split-fp32 (three bf16 planes, six products)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the per-kernel HIP-event probe")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
@@ -301,6 +316,8 @@ def main():
                     help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse several ranks "
                          "on one GPU)")
     args = ap.parse_args()
+    global FP32_MFMA
+    FP32_MFMA = args.fp32_mfma
 
     # stdout carries exactly the one JSON line: RCCL's init banner and gloo's connection messages are
     # written to fd 1 by native code, so fd 1 is pointed at stderr and the JSON goes to a saved copy
@@ -359,9 +376,18 @@ def main():
             "step_mfma_frac": round(step_flops / 1e12 / PEAK_TFLOPS[args.precision], 4),
             "roofline": roof,
         }
-        out["precision_note"] = ("fp32 = the reference's arithmetic (exact fp32 MFMA, deterministic reductions; "
-                                 "the golden parity tests pin this mode within 1e-4)" if args.precision == "fp32"
-                                 else "bf16 GEMM operands, fp32 accumulation")
+        if args.precision == "fp32":
+            out["fp32_mfma"] = FP32_MFMA
+            out["precision_note"] = (
+                "fp32 = the reference's arithmetic precision, deterministic reductions; the golden parity tests "
+                "pin this mode within 1e-4. "
+                + ("split-fp32 convs: each fp32 operand is the exact sum of three bf16 planes, the six plane "
+                   "products with p + q <= 2 run on v_mfma_f32_16x16x32_bf16 into fresh fp32 accumulators that are "
+                   "added to the running sums with round-to-nearest (dropped terms < 2^-23 |a b| per product); "
+                   "step_mfma_frac is against the 157.3 TF fp32 MFMA peak" if FP32_MFMA == "split"
+                   else "exact fp32 MFMA (v_mfma_f32_16x16x4_f32)"))
+        else:
+            out["precision_note"] = "bf16 GEMM operands, fp32 accumulation"
         if other is not None:
             out["perf_bf16" if other_p == "bf16" else "parity_fp32"] = other
         if world == 1 and not args.no_cpu_baseline:

@@ -76,6 +76,7 @@ struct ConvArgs {
                                 // g_det_req.ws + z * M * Ng instead of atomics; split-K FWD / DGRAD
                                 // (es_conv2d_*_det): into det_ws + z * M * Ng
   float* det_ws;
+  int prio;                     // split-fp32 ring kernels: waves 4-7 at s_setprio 1 (VALU arbitration)
 };
 
 // es_conv2d_wgrad_det: the partial buffer offered to the generic (register-staged / thin) WGRAD

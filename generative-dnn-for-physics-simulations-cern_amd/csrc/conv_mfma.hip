@@ -250,7 +250,8 @@ __device__ __forceinline__ void ring_loop(int nk, char* smem, int slot_bytes, Is
 // Single fragment set variant (register-lean, for the 256 x 256 tiles): per step one barrier,
 // then both fragment halves are read and multiplied in turn; the LDS latency is covered by the
 // other wave of the SIMD.  Same slot / vmcnt discipline as ring_loop.
-template <int PW, int NS, typename Issue, typename Load, typename Mma>
+// HALVES = 1: one load + mma per step (the split-fp32 kernels: one fragment set covers the step).
+template <int PW, int NS, int HALVES = 2, typename Issue, typename Load, typename Mma>
 __device__ __forceinline__ void ring_loop_lean(int nk, char* smem, int slot_bytes, Issue& issue, Load& load,
                                                Mma& mma) {
   using Frag = typename std::remove_reference<typename lambda_arg<Load>::type>::type;
@@ -265,12 +266,73 @@ __device__ __forceinline__ void ring_loop_lean(int nk, char* smem, int slot_byte
     Frag f;
     load(f, smem + cur * slot_bytes, 0);
     mma(f);
-    load(f, smem + cur * slot_bytes, 1);
-    mma(f);
+    if constexpr (HALVES == 2) {
+      load(f, smem + cur * slot_bytes, 1);
+      mma(f);
+    }
     prv = cur;
     cur = cur == NS - 1 ? 0 : cur + 1;
   }
   wait_vmcnt<0>();   // drain the zero-fill steps before the workgroup may exit
+}
+
+// ---------------------------------------------------------------------------------------------
+// Split-fp32 arithmetic (the fp32 mode's fast MFMA path, SPL kernels).  An fp32 value is the exact
+// sum of three bf16 values: x0 = rne(x), x1 = rne(x - x0), x2 = x - x0 - x1 (x - x0 has <= 16
+// significant bits and x - x0 - x1 <= 8, so every difference is exact and x2 is representable).
+// A product a*b is then sum_{p+q<=2} a_p b_q (6 bf16 products, each exact in the fp32 MFMA
+// accumulator); the dropped terms a1 b2 + a2 b1 + a2 b2 are below 2^-23 |a b| (|x1| <= 2^-8 |x|,
+// |x2| <= 2^-16 |x|), i.e. the size of one fp32 rounding, and the sums run in fp32 as in the exact
+// fp32 MFMA.  v_mfma_f32_16x16x32_bf16 does 8192 MACs in 16 cycles against 1024 in 32 for
+// v_mfma_f32_16x16x4_f32: the six products cost 6/16 of the fp32 MFMA time.
+// ---------------------------------------------------------------------------------------------
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float x, float y) {   // v_cvt_pk_bf16_f32 (RNE)
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){x, y}, bf16x2_t));
+}
+__device__ __forceinline__ float bf_lo(uint32_t p) { return __builtin_bit_cast(float, p << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t p) { return __builtin_bit_cast(float, p & 0xffff0000u); }
+// two values -> their three bf16 planes, packed per plane (first value in the low half)
+// (plain v_sub_f32: hipcc otherwise pairs the subtractions into v_pk_add_f32, which costs more issue
+// cycles than two scalar ops beside MFMAs, MI355X_MICROARCH.md constants table)
+__device__ __forceinline__ float fsub(float a, float b) {
+  float r;
+  asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ void split_pair(float x, float y, uint32_t& h, uint32_t& m, uint32_t& l) {
+  h = cvt_pk_bf16(x, y);
+  const float rx = fsub(x, bf_lo(h)), ry = fsub(y, bf_hi(h));
+  m = cvt_pk_bf16(rx, ry);
+  l = cvt_pk_bf16(fsub(rx, bf_lo(m)), fsub(ry, bf_hi(m)));
+}
+// 8 fp32 values (a lane's k-slice of a 16x16x32 fragment, two 16-byte LDS chunks) -> planes p[0..2]
+__device__ __forceinline__ void split8(const f32x4& x, const f32x4& y, bf16x8 p[3]) {
+  uint32_t h0, h1, h2, h3, m0, m1, m2, m3, l0, l1, l2, l3;
+  split_pair(x[0], x[1], h0, m0, l0);
+  split_pair(x[2], x[3], h1, m1, l1);
+  split_pair(y[0], y[1], h2, m2, l2);
+  split_pair(y[2], y[3], h3, m3, l3);
+  p[0] = __builtin_bit_cast(bf16x8, (u32x4_t){h0, h1, h2, h3});
+  p[1] = __builtin_bit_cast(bf16x8, (u32x4_t){m0, m1, m2, m3});
+  p[2] = __builtin_bit_cast(bf16x8, (u32x4_t){l0, l1, l2, l3});
+}
+// acc + the K-step's sum of the six plane products, small terms first.  The bf16 MFMA's fp32
+// accumulation rounds with a negative bias (measured, tools/split_bias.py: summed outputs drift by
+// -5e-8 .. -1.2e-6 of sum|y| when every product accumulates into the running sum), so the step's
+// products go into a fresh accumulator (its rounding is on the scale of one K-step's partial sum)
+// and the running sum takes them with one round-to-nearest add per element.  (A plain C++ add: the
+// compiler's MFMA-result hazard wait states do not cover inline asm that reads the MFMA's output.)
+__device__ __forceinline__ f32x4 mfma_split6(const bf16x8 a[3], const bf16x8 b[3], f32x4 acc) {
+  f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
+  return acc + c;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -289,9 +351,18 @@ __device__ __forceinline__ void ring_loop_lean(int nk, char* smem, int slot_byte
 // BK = 32 (256 x 256 tiles): K-steps of 32 channels (64-byte rows), 4 slots (three steps in flight),
 // 2 x 4 waves of 128 x 64; per step 32 KiB of operands for 4.2 MFLOP (the 256 x 128 BK = 64 tile
 // moves 48 KiB for the same work), and an A row tile is gathered once for 256 output channels.
-template <int MODE, int BM, int BN, bool SP, int BK = 64, typename T = bf16>
+//
+// SPL (T = float, BK = 64: 32 fp32 channels per K-step): split-fp32 arithmetic.  A lane reads the
+// 16-byte chunks g16 and g16 + 4 of its fragment row (channels 4 g16 .. +3 and 16 + 4 g16 .. +3, the
+// same k permutation for A and B), splits the 8 values into bf16 planes and issues the 6 plane
+// products as v_mfma_f32_16x16x32_bf16; one fragment set per step (ring_loop_lean, HALVES = 1).
+template <int MODE, int BM, int BN, bool SP, int BK = 64, typename T = bf16, bool SPL = false>
 __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
-  constexpr int WGM = BK == 32 ? 2 : 4, WGN = 8 / WGM;   // waves along M / N
+  static_assert(!SPL || (sizeof(T) == 4 && BK == 64), "split-fp32: fp32 operands, 128-byte slot rows");
+  // (SPL 256 x 256: 2 x 4 waves of 128 x 64 and two 64 KiB slots; one step in flight covers a step
+  // of 192 MFMAs per wave)
+  constexpr bool SPW = SPL && BN == 256;
+  constexpr int WGM = (BK == 32 || SPW) ? 2 : 4, WGN = 8 / WGM;   // waves along M / N
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int RM = WM / 16, RN = WN / 16;
   constexpr int ROWB = BK * 2, PROWS = 1024 / ROWB;      // slot row bytes, rows per 1 KiB piece
@@ -299,7 +370,7 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   constexpr int CPR = ROWB / 16;                         // 16-byte chunks per row
   constexpr int APW = BM / PROWS / 8, BPW = BN / PROWS / 8;   // pieces per wave per slot
   constexpr int PW = APW + BPW;
-  constexpr int NS = BK == 32 ? 4 : NSLOT;
+  constexpr int NS = SPW ? 2 : (BK == 32 ? 4 : NSLOT);
   constexpr int ABYTES = BM * ROWB, SLOT = (BM + BN) * ROWB;
   constexpr int KH = BK == 64 ? 2 : 1;                   // MFMA K-halves per step
   constexpr int RMF = RM / (3 - KH);                     // A tiles per fragment set
@@ -573,7 +644,47 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
         }
       }
   };
-  if constexpr (BK == 32 && ES_RING_LEAN) {
+  if constexpr (SPL) {
+    // The step's B tiles are read up front; the A row tiles are read inside the MFMA sequence, one
+    // tile ahead (registers: the 256 x 256 tile holds 128 accumulators).  B tile j is split just
+    // before its first MFMAs (row tile 0), so the step opens with one A and one B split.
+    struct FragS {
+      const char* slot;
+    };
+    auto rd_a = [&](f32x4 (&r)[2], const char* slot, int i) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) r[h] = *(const f32x4*)(slot + swz<BK>(wm0 + i * 16 + r16, g16 + 4 * h));
+    };
+    auto rd_b = [&](f32x4 (&r)[2], const char* slot, int j) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) r[h] = *(const f32x4*)(slot + ABYTES + swz<BK>(wn0 + j * 16 + r16, g16 + 4 * h));
+    };
+    auto load_s = [&](FragS& f, const char* slot, int) { f.slot = slot; };
+    auto mma_s = [&](const FragS& f) {
+      bf16x8 bp[RN][3], ap[3];
+      f32x4 ra[2][2], rb[2][2];
+      rd_a(ra[0], f.slot, 0);
+      rd_b(rb[0], f.slot, 0);
+      if constexpr (RN > 1) rd_b(rb[1], f.slot, 1);
+      if constexpr (RM > 1) rd_a(ra[1], f.slot, 1);
+      split8(ra[0][0], ra[0][1], ap);
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        split8(rb[j & 1][0], rb[j & 1][1], bp[j]);
+        if (j + 2 < RN) rd_b(rb[j & 1], f.slot, j + 2);
+        acc[0][j] = mfma_split6(ap, bp[j], acc[0][j]);
+      }
+#pragma unroll
+      for (int i = 1; i < RM; ++i) {
+        split8(ra[i & 1][0], ra[i & 1][1], ap);
+        if (i + 1 < RM) rd_a(ra[(i + 1) & 1], f.slot, i + 1);
+#pragma unroll
+        for (int j = 0; j < RN; ++j) acc[i][j] = mfma_split6(ap, bp[j], acc[i][j]);
+      }
+    };
+    if (a.prio && wid >= 4) __builtin_amdgcn_s_setprio(1);   // (wid is wave-uniform: readfirstlane)
+    ring_loop_lean<PW, NS, 1>(nk, smem, SLOT, issue, load_s, mma_s);
+  } else if constexpr (BK == 32 && ES_RING_LEAN) {
     ring_loop_lean<PW, NS>(nk, smem, SLOT, issue, load, mma);
   } else {
     auto nofence = [](Frag&) {};
@@ -1829,7 +1940,11 @@ __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
 // four classes' combined taps over each original tap) in a fixed order.  The reference's same-seed
 // reruns are bit-identical; with this, so are the parity mode's.
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, bool SP>
+// SPL: split-fp32 arithmetic (see split8).  A lane's 8 k-values of a 16x16x32 fragment are the
+// images 4 j + (lane >> 4), j = 0..7, of the step (MFMA k = 8 (lane >> 4) + j; the same permutation
+// for A and B), so each of the 8 ds_read_b32 instructions reads four consecutive k-rows, the access
+// pattern the k-row swizzle was laid out for.
+template <int BM, int BN, bool SP, bool SPL = false>
 __global__ void __launch_bounds__(RT) wgrad_f32_kernel(ConvArgs a, float* __restrict__ ws, int ngt) {
   constexpr int KI = 32;                                       // images per K-step
   // waves along M / N: every wave tile at least 16 x 16 (64 x 64 tiles: 2 x 4 waves of 32 x 16)
@@ -1958,8 +2073,46 @@ __global__ void __launch_bounds__(RT) wgrad_f32_kernel(ConvArgs a, float* __rest
           for (int j = 0; j < RN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a[t][i], f.b[t][j], acc[i][j], 0, 0, 0);
     };
-    auto nofence = [](Frag&) {};
-    ring_loop<PW, 0>(tend - tbeg, smem, SLOT, issue, load, mma, nofence);
+    if constexpr (SPL) {
+      struct FragS {
+        float a[8][RM], b[8][RN];
+      };
+      auto load_s = [&](FragS& f, const char* slot, int) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = 4 * j + kl;
+#pragma unroll
+          for (int i = 0; i < RM; ++i) f.a[j][i] = rd(slot, BM * 4, k, wm0 + i * 16 + col16);
+#pragma unroll
+          for (int jn = 0; jn < RN; ++jn) f.b[j][jn] = rd(slot + AIMG, BN * 4, k, wn0 + jn * 16 + col16);
+        }
+      };
+      auto mma_s = [&](const FragS& f) {
+        bf16x8 bp[RN][3], ap[3];
+        auto sa = [&](int i) {
+          split8(f32x4{f.a[0][i], f.a[1][i], f.a[2][i], f.a[3][i]}, f32x4{f.a[4][i], f.a[5][i], f.a[6][i], f.a[7][i]},
+                 ap);
+        };
+        sa(0);
+#pragma unroll
+        for (int jn = 0; jn < RN; ++jn) {   // B tiles split just before their first MFMAs
+          split8(f32x4{f.b[0][jn], f.b[1][jn], f.b[2][jn], f.b[3][jn]},
+                 f32x4{f.b[4][jn], f.b[5][jn], f.b[6][jn], f.b[7][jn]}, bp[jn]);
+          acc[0][jn] = mfma_split6(ap, bp[jn], acc[0][jn]);
+        }
+#pragma unroll
+        for (int i = 1; i < RM; ++i) {
+          sa(i);
+#pragma unroll
+          for (int jn = 0; jn < RN; ++jn) acc[i][jn] = mfma_split6(ap, bp[jn], acc[i][jn]);
+        }
+      };
+      if (a.prio && wid >= 4) __builtin_amdgcn_s_setprio(1);
+      ring_loop_lean<PW, NSLOT, 1>(tend - tbeg, smem, SLOT, issue, load_s, mma_s);
+    } else {
+      auto nofence = [](Frag&) {};
+      ring_loop<PW, 0>(tend - tbeg, smem, SLOT, issue, load, mma, nofence);
+    }
   }
   // the raw tile of this split (zeros for an empty split): plain stores into its own slot
   float* o = ws + ((int64_t)split * a.M + m0 + wm0) * ngt + n0 + wn0 + col16;
@@ -2014,11 +2167,11 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
 int64_t g_conv_launches = 0;
 extern "C" int64_t es_conv_launch_count() { return g_conv_launches; }
 
-template <int MODE, int BM, int BN, bool SP, int BK = 64, typename T = bf16>
+template <int MODE, int BM, int BN, bool SP, int BK = 64, typename T = bf16, bool SPL = false>
 void launch_ring(const ConvArgs& a, int row_tiles, hipStream_t st) {
   dim3 grid(row_tiles, (a.Ng + BN - 1) / BN, 1);
   ++g_conv_launches;
-  hipLaunchKernelGGL((conv_ring_kernel<MODE, BM, BN, SP, BK, T>), grid, dim3(RT), 0, st, a);
+  hipLaunchKernelGGL((conv_ring_kernel<MODE, BM, BN, SP, BK, T, SPL>), grid, dim3(RT), 0, st, a);
 }
 
 // minimum K-steps per WGRAD K-split (each split flushes its whole fp32 tile with atomics)
@@ -2176,7 +2329,7 @@ extern "C" int es_conv_subpixel_ok(const es_conv_desc_t* d, es_dtype_t dt) {
   return xbytes < (1ll << 30) && ybytes < (1ll << 30) && wbytes < (1ll << 30);
 }
 
-template <typename T>
+template <typename T, bool SPL = false>
 int ring_fd(ConvArgs& a, int mode, hipStream_t st);
 
 int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
@@ -2203,9 +2356,9 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
   return ring_fd<bf16>(a, mode, st);
 }
 
-// FWD / DGRAD ring launch for bf16 or fp32 operands (fp32: the parity mode's exact fp32 MFMA; the
-// persistent kernels are bf16-only)
-template <typename T>
+// FWD / DGRAD ring launch for bf16 or fp32 operands (fp32: the parity mode's exact fp32 MFMA, or with
+// SPL the split-fp32 bf16-plane MFMA on 32-channel K-steps; the persistent kernels are bf16-only)
+template <typename T, bool SPL>
 int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
   const es_conv_desc_t& d = a.d;
   const bool sp_weights = d.subpixel != 0;
@@ -2339,17 +2492,31 @@ int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
       else hipLaunchKernelGGL((conv_p256_kernel<4>), dim3(256), dim3(RT), 0, st, a, row_tiles);
       return 1;
     }
-    dim3 grid(row_tiles, (4 * a.Ng + 255) / 256, 1);
     ++g_conv_launches;
-    hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 256, true, 32, T>), grid, dim3(RT), 0, st, a);
+    if constexpr (SPL) {   // 256 x 256 tiles of 32-channel steps
+      dim3 grid(row_tiles, (4 * a.Ng + 255) / 256, 1);
+      hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 256, true, 64, T, true>), grid, dim3(RT), 0, st, a);
+    } else {
+      dim3 grid(row_tiles, (4 * a.Ng + 255) / 256, 1);
+      hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 256, true, 32, T>), grid, dim3(RT), 0, st, a);
+    }
     return 1;
   }
 #define ES_RING(MD, BMV, BNV)                                                                  \
-  (sp_weights ? launch_ring<MD, BMV, BNV, true, 64, T>(a, row_tiles, st)                              \
-              : launch_ring<MD, BMV, BNV, false, 64, T>(a, row_tiles, st))
+  (sp_weights ? launch_ring<MD, BMV, BNV, true, 64, T, SPL>(a, row_tiles, st)                         \
+              : launch_ring<MD, BMV, BNV, false, 64, T, SPL>(a, row_tiles, st))
   const bool wide = g_ring256 && big && !shortk && a.Ng >= 256 && a.ng >= 16 && a.vec_out &&
                     (sp_weights || mode == MODE_DGRAD);   // (plain FWD: register spills at 256 x 256)
-  if (wide) {
+  if constexpr (SPL) if (wide) {   // split-fp32: 256 x 256 tiles of 32-channel steps
+    if (mode == MODE_FWD) {   // (wide FWD is sub-pixel only)
+      launch_ring<MODE_FWD, 256, 256, true, 64, T, true>(a, row_tiles, st);
+    } else {
+      if (sp_weights) launch_ring<MODE_DGRAD, 256, 256, true, 64, T, true>(a, row_tiles, st);
+      else launch_ring<MODE_DGRAD, 256, 256, false, 64, T, true>(a, row_tiles, st);
+    }
+    return 1;
+  }
+  if constexpr (!SPL) if (wide) {
     if (mode == MODE_FWD) {
       if (sp_weights) launch_ring<MODE_FWD, 256, 256, true, 32, T>(a, row_tiles, st);
       else launch_ring<MODE_FWD, 256, 256, false, 32, T>(a, row_tiles, st);
@@ -2378,6 +2545,11 @@ int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
 // ---------------------------------------------------------------------------------------------
 namespace {
 int g_f32_chunk = 0;   // test knob (es_conv_set_f32_chunk): at most this many images per fp32 launch
+// fp32 MFMA arithmetic of the ring kernels: 0 = exact fp32 (v_mfma_f32_16x16x4_f32), 1 = split-fp32
+// (three bf16 planes, 6 products on v_mfma_f32_16x16x32_bf16); es_conv_set_f32_split / ES_F32_SPLIT
+int g_f32_split = [] { const char* e = getenv("ES_F32_SPLIT"); return e ? atoi(e) : 0; }();
+// split-fp32 kernels: static s_setprio 1 for waves 4-7 (ES_SPL_PRIO=0 off; A/B)
+int g_spl_prio = [] { const char* e = getenv("ES_SPL_PRIO"); return e ? atoi(e) : 1; }();
 // images per launch: equal chunks (whole 64-image groups where the limit allows) below the limit
 int chunk_images(int64_t img_bytes, int N) {
   int64_t lim = ((1ll << 30) - 1) / std::max<int64_t>(img_bytes, 1);
@@ -2408,7 +2580,8 @@ int es_conv_ring_launch_f32(ConvArgs& a, int mode, hipStream_t st) {
     c.out = (char*)a.out + (int64_t)n0 * a.os[0] * esz;
     c.M = mode == MODE_FWD ? c.d.N * d.P * d.Q : (a.fold ? c.d.N * d.H * d.W : c.d.N * d.Hu * d.Wu);
     if (req.part) g_stats_req = StatsRequest{req.part + (int64_t)used * 3 * a.Ng, req.floats - (int64_t)used * 3 * a.Ng, 0};
-    const int rc = ring_fd<float>(c, mode, st);
+    c.prio = g_spl_prio;
+    const int rc = g_f32_split ? ring_fd<float, true>(c, mode, st) : ring_fd<float>(c, mode, st);
     if (rc <= 0) {
       g_stats_req = req;
       if (n0 == 0) return rc;
@@ -2477,6 +2650,7 @@ int es_wgrad_f32_ring(const es_conv_desc_t& d, const void* dy, const int64_t ys[
     const int n0 = ch * p.nc;
     ConvArgs a{};
     a.d = d;
+    a.prio = g_spl_prio;
     a.d.N = std::min(p.nc, d.N - n0);
     a.a_src = (const char*)dy + (int64_t)n0 * ys[0] * 4;
     a.b_src = (const char*)x + (int64_t)n0 * xs[0] * 4;
@@ -2493,7 +2667,10 @@ int es_wgrad_f32_ring(const es_conv_desc_t& d, const void* dy, const int64_t ys[
 #define ES_WF(BM, BN)                                                                                 \
   do {                                                                                                \
     ++g_conv_launches;                                                                                \
-    if (p.sp) hipLaunchKernelGGL((wgrad_f32_kernel<BM, BN, true>), grid, dim3(RT), 0, st, a, wsc, p.ngt);   \
+    if (g_f32_split) {                                                                                \
+      if (p.sp) hipLaunchKernelGGL((wgrad_f32_kernel<BM, BN, true, true>), grid, dim3(RT), 0, st, a, wsc, p.ngt); \
+      else hipLaunchKernelGGL((wgrad_f32_kernel<BM, BN, false, true>), grid, dim3(RT), 0, st, a, wsc, p.ngt);    \
+    } else if (p.sp) hipLaunchKernelGGL((wgrad_f32_kernel<BM, BN, true>), grid, dim3(RT), 0, st, a, wsc, p.ngt); \
     else hipLaunchKernelGGL((wgrad_f32_kernel<BM, BN, false>), grid, dim3(RT), 0, st, a, wsc, p.ngt);       \
   } while (0)
     if (p.bm == 128 && p.bn == 256) ES_WF(128, 256);
@@ -2524,5 +2701,11 @@ void es_wgrad_reduce_plain(const float* ws, int splits, int K, int C, int R, int
 extern "C" int es_conv_set_f32_chunk(int images) {
   const int old = g_f32_chunk;
   g_f32_chunk = images > 0 ? images : 0;
+  return old;
+}
+
+extern "C" int es_conv_set_f32_split(int on) {
+  const int old = g_f32_split;
+  g_f32_split = on > 0 ? 1 : 0;
   return old;
 }

@@ -175,6 +175,23 @@ def deterministic() -> bool:
     return _DET
 
 
+# fp32 MFMA arithmetic of the ring convolutions: exact fp32 (v_mfma_f32_16x16x4_f32) or split-fp32
+# (three bf16 planes per operand, six plane products on v_mfma_f32_16x16x32_bf16; es_conv_set_f32_split)
+_F32_SPLIT = None
+
+
+def set_f32_split(on: bool):
+    global _F32_SPLIT
+    on = bool(on)
+    if on != _F32_SPLIT:
+        hip.lib().es_conv_set_f32_split(1 if on else 0)
+        _F32_SPLIT = on
+
+
+def f32_split() -> bool:
+    return bool(_F32_SPLIT)
+
+
 # --------------------------------------------------------------------------------- upsample
 class Upsample:
     """torch nearest upsample (``scale_factor`` or ``size``) as index maps for the conv gather.

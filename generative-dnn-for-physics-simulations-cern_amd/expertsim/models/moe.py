@@ -34,7 +34,7 @@ from torch import nn
 
 from .. import hip
 from ..config import cfg_get
-from ..layers import Act, copy_act, defer_num_batches, set_deterministic, set_norm_sync
+from ..layers import Act, copy_act, defer_num_batches, set_deterministic, set_f32_split, set_norm_sync
 from ..rng import DeviceRNG
 from ..utils import philox
 
@@ -81,6 +81,11 @@ class MoEWrapper(nn.Module):
         self._dstep = None         # device int32 step counter: dropout / noise streams (graph replay)
         # fp32 parity mode: every float reduction in a fixed order (bitwise-reproducible steps)
         self.deterministic = bool(cfg_get(cfg, "train.deterministic", True))
+        # fp32 conv arithmetic: "exact" (v_mfma_f32_16x16x4_f32) or "split" (three bf16 planes per
+        # operand, six plane products on the bf16 MFMA; es_conv_set_f32_split)
+        self.fp32_mfma = os.environ.get("ES_FP32_MFMA") or str(cfg_get(cfg, "train.fp32_mfma", "split"))
+        if self.fp32_mfma not in ("exact", "split"):
+            raise ValueError(f"train.fp32_mfma must be exact or split, got {self.fp32_mfma!r}")
         self.set_precision(cfg_get(cfg, "train.precision", "fp32"))
 
     def set_precision(self, precision: str):
@@ -186,6 +191,7 @@ class MoEWrapper(nn.Module):
         hip.set_step_counter(self._dstep)
         self.rng.begin_step(self._dstep)
         set_deterministic(self.precision == "fp32" and self.deterministic)
+        set_f32_split(self.fp32_mfma == "split")
         try:
             with defer_num_batches():
                 return self._train_step(epoch, cond, real_images, true_positions, std, intensity,

@@ -176,6 +176,13 @@ int es_set_deterministic(int on);
 /* Test knob: fp32 ring convolutions launch over chunks of at most `images` images (0: only as the
  * 1 GiB operand limit requires); returns the previous value. */
 int es_conv_set_f32_chunk(int images);
+/* fp32 MFMA arithmetic of the ring convolutions (returns the previous setting): 0 = exact fp32
+ * (v_mfma_f32_16x16x4_f32), 1 = split-fp32: each fp32 operand is the exact sum of three bf16
+ * planes and the six plane products with p + q <= 2 run on v_mfma_f32_16x16x32_bf16 into the fp32
+ * accumulator (dropped terms < 2^-23 |a b| per product; deterministic, fixed order).  Replaces the
+ * same fp32 conv2d / conv_transpose products as es_conv2d_fwd / _dgrad / _wgrad_det (neutron
+ * generator.py:23-35, proton generator.py:26-38).  MoEWrapper sets it from train.fp32_mfma. */
+int es_conv_set_f32_split(int on);
 /* Host-side count of MFMA conv kernels issued so far (ring / persistent / p256 / fp32 WGRAD).
  * Instrumentation only: lets a profiler state how many kernel launches one conv op was. */
 int64_t es_conv_launch_count(void);

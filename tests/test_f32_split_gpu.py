@@ -1,0 +1,105 @@
+"""Split-fp32 MFMA arithmetic of the ring convolutions (train.fp32_mfma: split).
+
+Every fp32 operand is the exact sum of three bf16 planes (x0 = rne(x), x1 = rne(x - x0),
+x2 = x - x0 - x1) and a product is the sum of the six plane products with p + q <= 2 on
+v_mfma_f32_16x16x32_bf16, accumulated in fp32 (conv_mfma.hip, split8 / mfma_split6).  The dropped
+terms are below 2^-23 |a b| per product, so the result must be as close to the fp64 reference as
+the exact fp32 MFMA result is.
+
+Reference: torch CPU fp64 of upsample + conv2d (neutron/generator.py:23-35, proton/generator.py:26-38).
+Tolerance: 2e-5 of max|ref| (the exact fp32 path's bound), and at most 2x the exact fp32 path's own
+error + 1e-6; bitwise equality of two runs and of image-chunked launches (fixed order).
+"""
+import pytest
+import torch
+
+from test_f32_ring_gpu import CASES, _ref, _run
+from test_kernels_gpu import _hip, rel
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def det():
+    from expertsim import layers
+    old = layers.deterministic()
+    layers.set_deterministic(True)
+    yield
+    layers.set_deterministic(old)
+    layers.set_f32_split(False)
+
+
+def _both(case, seed):
+    from expertsim import layers
+    x, w, b, gy, *ref = _ref(case, seed)
+    layers.set_f32_split(False)
+    exact = _run(case, x, w, b, gy)[1:]
+    layers.set_f32_split(True)
+    split = _run(case, x, w, b, gy)[1:]
+    return ref, exact, split
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_split_matches_fp64(case, det):
+    _hip()
+    ref, exact, split = _both(case, 0)
+    for r, e, s in zip(ref, exact, split):
+        es, ee = rel(s.double(), r), rel(e.double(), r)
+        assert es < 2e-5, (es, ee)
+        assert es <= 2 * ee + 1e-6, (es, ee)
+
+
+@pytest.mark.parametrize("case", CASES[:3])
+def test_split_bitwise_rerun(case, det):
+    from expertsim import layers
+    _hip()
+    x, w, b, gy, *_ = _ref(case, seed=3)
+    layers.set_f32_split(True)
+    r1 = _run(case, x, w, b, gy)[1:]
+    r2 = _run(case, x, w, b, gy)[1:]
+    for a, c in zip(r1, r2):
+        assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("case", [CASES[1], CASES[2]])
+def test_split_image_chunks(case, det):
+    from expertsim import layers
+    hip = _hip()
+    x, w, b, gy, *_ = _ref(case, seed=4)
+    layers.set_f32_split(True)
+    full = _run(case, x, w, b, gy)[1:]
+    old = hip.lib().es_conv_set_f32_chunk(64)
+    try:
+        part = _run(case, x, w, b, gy)[1:]
+    finally:
+        hip.lib().es_conv_set_f32_chunk(old)
+    assert torch.equal(full[0], part[0])
+    assert torch.equal(full[1], part[1])
+    assert rel(part[2], full[2]) < 1e-5
+
+
+@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("case", [(8, 128, 13, 13, 256, 3, 1, 0, 2), CASES[1], (8, 256, 24, 24, 128, 3, 1, 0, 2)])
+def test_fused_bn_stats_consistency(case, split, det):
+    """The conv epilogue's BatchNorm partials against the stored output (bias x30: channel means far
+    from zero): the mean must reproduce the stored values' mean to a rounding floor,
+    |mean - mean(y)| <= 1e-6 max(|mean(y)|, std(y)) (the normalised map then sums to ~0 per channel,
+    which the analytically-zero conv-bias gradients depend on)."""
+    _hip()
+    from expertsim import hip, layers
+    from expertsim.layers import ConvOp, NormOp, Upsample
+    from test_kernels_gpu import DEV, from_act, to_act
+    layers.set_f32_split(split)
+    x, w, b, gy, *_ = _ref(case, seed=5)
+    N, Cin, H, W, Cout, k, st, pad, up = case
+    op = ConvOp(torch.nn.Parameter(w.to(DEV)), torch.nn.Parameter((b * 30).to(DEV)), stride=st, pad=pad,
+                upsample=Upsample((H, W), scale=(up, up)))
+    ya = op.fwd(to_act(x, torch.float32), out_dtype=torch.float32, bn_stats=True)
+    assert ya.bn_part is not None
+    rm, rv = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
+    mean, invstd = NormOp(hip.NORM_BN, running_mean=rm, running_var=rv).stats(ya)
+    yt = from_act(ya).double()
+    m_ref = yt.mean(dim=(0, 2, 3))
+    scale = torch.maximum(m_ref.abs(), 1.0 / invstd.cpu().double())
+    err = ((mean.cpu().double() - m_ref).abs() / scale).max().item()
+    assert err <= 1e-6, err

@@ -100,6 +100,7 @@ def _check(errs, tol, what, abs_tol=1e-5):
     worst = max((e for e in errs if e[1] == "rel"), key=lambda e: e[2], default=None)
     print(what, "worst rel:", worst, "worst abs:",
           max((e for e in errs if e[1] == "abs"), key=lambda e: e[2], default=None))
+    print(what, "abs:", [(n, f"{e:.2e}") for n, kind, e in errs if kind == "abs"])
     for n, kind, e in errs:
         if kind == "abs":
             assert e <= abs_tol, (what, n, e)

@@ -2,7 +2,7 @@
 
 usage: python tools/mb_one.py <c0|c5|c9> <fwd|dgrad|wgrad> [ring 1|0] [reps]
 (ES_MB_BATCH=<images> overrides the batch of 512; ES_MB_DTYPE=fp32 runs the parity mode's fp32 ring
-kernels with the deterministic weight gradient)"""
+kernels with the deterministic weight gradient, ES_MB_SPLIT=1 with split-fp32 arithmetic)"""
 import os
 import sys
 
@@ -34,6 +34,7 @@ def main():
     if f32:
         from expertsim import layers
         layers.set_deterministic(True)
+        layers.set_f32_split(os.environ.get("ES_MB_SPLIT", "0") == "1")
     x = Act.nhwc(N, Cin, H, W, dt, dev)
     x.t.normal_()
     y = op.fwd(x, out_dtype=dt)
