@@ -110,6 +110,9 @@ struct StatsRequest {
 };
 extern thread_local StatsRequest g_stats_req;
 
+// split-fp32 weight planes: byte offset of the planes behind an fp32 packing of n elements
+extern "C" int64_t es_weight_planes_offset(int64_t n);
+
 // 8-wave LDS-DMA ring kernels (conv_mfma.hip).  Return 1 when the call was launched, 0 when the
 // shape is not eligible (the caller falls back to the kernels of conv_igemm.hip), <0 on error.
 int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st);

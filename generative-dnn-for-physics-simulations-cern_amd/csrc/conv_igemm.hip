@@ -1423,6 +1423,38 @@ extern "C" int es_pack_conv_weight(const float* w, int K, int C, int R, int S, i
   return ES_OK;
 }
 
+// Split-fp32 planes of a packed fp32 weight (es_conv_set_f32_split(2)): every 32-element block g
+// of the packing becomes 192 bytes at planes + 192 g: three planes of 32 bf16, x0 = rne(x),
+// x1 = rne(x - x0), x2 = x - x0 - x1 (exact), position 8 u + j of a plane holding element
+// 4 u + j (j < 4) or 16 + 4 u + j - 4 of the block: the k order of the ring kernels' A fragments.
+__global__ void pack_planes_kernel(const float* __restrict__ w, int64_t nblk, bf16* __restrict__ planes) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nblk * 32; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t g = i >> 5;
+    const int q = (int)(i & 31), u = q >> 3, j = q & 7;
+    const float x = w[g * 32 + (j < 4 ? 4 * u + j : 16 + 4 * u + j - 4)];
+    const bf16 h = (bf16)x;
+    const float r = x - (float)h;
+    const bf16 m = (bf16)r;
+    const bf16 l = (bf16)(r - (float)m);
+    bf16* o = planes + g * 96 + q;
+    o[0] = h;
+    o[32] = m;
+    o[64] = l;
+  }
+}
+
+extern "C" int64_t es_weight_planes_offset(int64_t n) { return (n * 4 + 255) / 256 * 256; }
+
+extern "C" int es_pack_weight_planes(const float* packed, int64_t n, void* base, es_stream_t stream) {
+  const int64_t nblk = n / 32;
+  if (nblk == 0) return ES_OK;
+  const int blocks = (int)std::min<int64_t>((nblk * 32 + 255) / 256, 4096);
+  hipLaunchKernelGGL(pack_planes_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, packed, nblk,
+                     (bf16*)((char*)base + es_weight_planes_offset(n)));
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
 extern "C" int es_unpack_conv_grad_clear(float* dw, int K, int C, int R, int S, float* grad, float beta,
                                          es_stream_t stream) {
   const int64_t n = (int64_t)K * C * R * S;

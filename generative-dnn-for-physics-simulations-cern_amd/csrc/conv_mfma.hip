@@ -356,33 +356,51 @@ __device__ __forceinline__ f32x4 mfma_split6(const bf16x8 a[3], const bf16x8 b[3
 // 16-byte chunks g16 and g16 + 4 of its fragment row (channels 4 g16 .. +3 and 16 + 4 g16 .. +3, the
 // same k permutation for A and B), splits the 8 values into bf16 planes and issues the 6 plane
 // products as v_mfma_f32_16x16x32_bf16; one fragment set per step (ring_loop_lean, HALVES = 1).
-template <int MODE, int BM, int BN, bool SP, int BK = 64, typename T = bf16, bool SPL = false>
+//
+// SPL == 2 (SPB): the B operand (packed weights) arrives pre-split: es_pack_weight_planes stores each
+// 32-element K block of the fp32 packing as three 64-byte bf16 planes (192 bytes, k in the same
+// permutation as the A fragments), so only A is split in the kernel.  The slot holds B plane-major,
+// [3][BN rows][64 B] (swizzled as the BK = 32 images), and the 8 waves are stacked along M (wave
+// tile BM/8 x BN): every A element is split by one wave only.
+template <int MODE, int BM, int BN, bool SP, int BK = 64, typename T = bf16, int SPL = 0>
 __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   static_assert(!SPL || (sizeof(T) == 4 && BK == 64), "split-fp32: fp32 operands, 128-byte slot rows");
   // (SPL 256 x 256: 2 x 4 waves of 128 x 64 and two 64 KiB slots; one step in flight covers a step
   // of 192 MFMAs per wave)
-  constexpr bool SPW = SPL && BN == 256;
-  constexpr int WGM = (BK == 32 || SPW) ? 2 : 4, WGN = 8 / WGM;   // waves along M / N
+  constexpr bool SPB = SPL == 2;
+  constexpr bool SPW = SPL == 1 && BN == 256;
+  constexpr int WGM = SPB ? 8 : ((BK == 32 || SPW) ? 2 : 4), WGN = 8 / WGM;   // waves along M / N
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int RM = WM / 16, RN = WN / 16;
   constexpr int ROWB = BK * 2, PROWS = 1024 / ROWB;      // slot row bytes, rows per 1 KiB piece
   constexpr int EB = sizeof(T), BKC = ROWB / EB;         // operand bytes, channels per K-step (fp32: BK / 2)
   constexpr int CPR = ROWB / 16;                         // 16-byte chunks per row
-  constexpr int APW = BM / PROWS / 8, BPW = BN / PROWS / 8;   // pieces per wave per slot
+  constexpr int EBB = SPB ? 6 : EB;                      // bytes per B element in global memory
+  constexpr int BPL = BN / 16;                           // SPB: 1 KiB pieces per B plane
+  constexpr int BPIECES = SPB ? 3 * BPL : BN / PROWS;    // (SPB, BN = 64: 12 pieces + 4 zero-fill dummies)
+  constexpr int APW = BM / PROWS / 8, BPW = (BPIECES + 7) / 8;   // pieces per wave per slot
   constexpr int PW = APW + BPW;
-  constexpr int NS = SPW ? 2 : (BK == 32 ? 4 : NSLOT);
-  constexpr int ABYTES = BM * ROWB, SLOT = (BM + BN) * ROWB;
+  constexpr int ABYTES = BM * ROWB, BBYTES = SPB ? 3 * BN * 64 : BN * ROWB;
+  constexpr int SLOT = ABYTES + BBYTES;
+  // SPB ring depths: three full slots when they fit (NS = 3); else A gets three slots and B (the
+  // weights, L2-resident) two: A stays two steps ahead, B one (SPLITD)
+  constexpr bool SPLITD = SPB && 3 * SLOT > 144 * 1024;
+  // (SPB 128 x 64: two slots, so that two workgroups share a CU and one's fill / epilogue overlaps
+  // the other's MFMAs, as the short-K bf16 tiles do)
+  constexpr int NS = SPW ? 2 : (SPB ? (BM == 128 && BN == 64 ? 2 : 3) : (BK == 32 ? 4 : NSLOT));
   constexpr int KH = BK == 64 ? 2 : 1;                   // MFMA K-halves per step
   constexpr int RMF = RM / (3 - KH);                     // A tiles per fragment set
   constexpr int SROWS = WM < 64 ? WM : 64;               // epilogue staging rows per pass
   constexpr int STAGE0 = 8 * SROWS * (WN * 4 + 16);
   constexpr int TPITCH = BN * 2 + 16;                    // BK = 32 bf16 epilogue: whole-tile image
   constexpr int STAGE = BK == 32 && BM * TPITCH > STAGE0 ? BM * TPITCH : STAGE0;
-  constexpr int RING = NS * SLOT > STAGE ? NS * SLOT : STAGE;
+  constexpr int RINGB = SPLITD ? 3 * ABYTES + 2 * BBYTES : NS * SLOT;
+  constexpr int RING = RINGB > STAGE ? RINGB : STAGE;
+  constexpr int JUNK = BPW * 8 > BPIECES ? 1024 : 0;     // landing area of the dummy pieces
   // ONE __shared__ object (a second one beside the DMA ring makes hipcc wait vmcnt(0) before
   // every ds_read of the loop): the ring slots (also the epilogue staging), then the fused-stats
   // scratch [3][WGM][BN] floats, which no DMA targets
-  __shared__ __attribute__((aligned(16))) char smem[RING + 3 * WGM * BN * 4];
+  __shared__ __attribute__((aligned(16))) char smem[RING + 3 * WGM * BN * 4 + JUNK];
   const es_conv_desc_t& d = a.d;
   const SubPixel& sp = a.sp;
 
@@ -453,13 +471,13 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   if constexpr (SP && MODE == MODE_FWD) {
     ldb = sp.dh[cls] * sp.dw[cls] * d.C;
     bbase = sp.tap0[cls] * a.Ng * d.C;
-    bbytes = sp.tap0[4] * a.Ng * d.C * EB;
+    bbytes = sp.tap0[4] * a.Ng * d.C * EBB;
   } else if constexpr (SP) {
     ldb = sp.tap0[4] * d.K;
-    bbytes = a.Ng * ldb * EB;
+    bbytes = a.Ng * ldb * EBB;
   } else {
     ldb = (MODE == MODE_DGRAD && a.fold) ? d.R * d.S * d.K : a.Kd;
-    bbytes = a.Ng * ldb * EB;
+    bbytes = a.Ng * ldb * EBB;
   }
   const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)bbytes);
   const int as2b = (int)a.as[2] * EB, as3b = (int)a.as[3] * EB;
@@ -500,9 +518,17 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   uint32_t blane[BPW];
 #pragma unroll
   for (int j = 0; j < BPW; ++j) {
-    const int rr = (wid * BPW + j) * PROWS + lrow;
-    // rows past Ng read garbage columns that the epilogue drops (or zeros past num_records)
-    blane[j] = (uint32_t)((bbase + (n0 + rr) * ldb) * EB + ((pc ^ swz_x<BK>(rr)) * 16));
+    if constexpr (SPB) {   // piece q: plane q / BPL, rows 16 (q % BPL) + lane / 4, 16-byte chunk lane % 4
+      const int q = wid * BPW + j;
+      const int rr = (q % BPL) * 16 + (lane >> 2);
+      blane[j] = q < BPIECES ? (uint32_t)((bbase + (n0 + rr) * ldb) * EBB + (q / BPL) * 64 +
+                                          (((lane & 3) ^ swz_x<32>(rr)) * 16))
+                             : OOB;
+    } else {
+      const int rr = (wid * BPW + j) * PROWS + lrow;
+      // rows past Ng read garbage columns that the epilogue drops (or zeros past num_records)
+      blane[j] = (uint32_t)((bbase + (n0 + rr) * ldb) * EB + ((pc ^ swz_x<BK>(rr)) * 16));
+    }
   }
 
   // K-step cursor (uniform, advanced once per issued slot).
@@ -564,14 +590,20 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
       if constexpr (MODE == MODE_FWD) kb = (cr * kw + cs) * d.C;
       else if constexpr (SP) kb = (Rtap0(ccls) + cr * kw + cs) * d.K;
       else kb = ckb;
-      ub_t = live ? (uint32_t)(kb * EB) : OOB;
+      ub_t = live ? (uint32_t)(kb * EBB) : OOB;
     }
     // (OOB + a channel offset stays past every num_records: offsets are < 1 GiB)
-    const uint32_t co = (uint32_t)(cch * EB);
+    const uint32_t co = (uint32_t)(cch * EB), cob = (uint32_t)(cch * EBB);
 #pragma unroll
     for (int j = 0; j < APW; ++j) bdma16(ares, alane[j] + (ua_t[j] + co), slot + (wid * APW + j) * 1024);
+    if constexpr (!SPLITD) {
 #pragma unroll
-    for (int j = 0; j < BPW; ++j) bdma16(bres, blane[j] + (ub_t + co), slot + ABYTES + (wid * BPW + j) * 1024);
+      for (int j = 0; j < BPW; ++j) {
+        const int q = wid * BPW + j;
+        char* dst = (!JUNK || q < BPIECES) ? slot + ABYTES + q * 1024 : smem + RING + 3 * WGM * BN * 4;
+        bdma16(bres, blane[j] + (ub_t + cob), dst);
+      }
+    }
     ++cstep;
     cch += BKC;
     if (cch == nch) {   // tap done: advance the tap cursor (wave-uniform branch)
@@ -644,7 +676,88 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
         }
       }
   };
-  if constexpr (SPL) {
+  if constexpr (SPB) {
+    // A row tiles (RM = BM / 128) split once per step; B planes read per column tile straight from
+    // the pre-split image (chunk g16 of a 64-byte plane row = MFMA k 8 g16 .. +7)
+    struct FragS {
+      const char* slot;
+      const char* bimg;
+    };
+    auto load_s = [&](FragS& f, const char* slot, int) {
+      f.slot = slot;
+      f.bimg = slot + ABYTES;
+    };
+    // mid(): called after the first column tile's MFMAs (the step's DMA issue, MFMA-first head)
+    auto mma_mid = [&](const FragS& f, auto&& mid) {
+      bf16x8 ap[RM][3];
+      const char* bimg = f.bimg;
+      auto rd_b = [&](bf16x8 (&bp)[3], int j) {
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          bp[pl] = *(const bf16x8*)(bimg + pl * (BN * 64) + swz<32>(wn0 + j * 16 + r16, g16));
+      };
+      bf16x8 bq[2][3];
+      rd_b(bq[0], 0);
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        f32x4 r0 = *(const f32x4*)(f.slot + swz<BK>(wm0 + i * 16 + r16, g16));
+        f32x4 r1 = *(const f32x4*)(f.slot + swz<BK>(wm0 + i * 16 + r16, g16 + 4));
+        split8(r0, r1, ap[i]);
+      }
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        if (j + 1 < RN) rd_b(bq[(j + 1) & 1], j + 1);      // next column tile's planes in flight
+#pragma unroll
+        for (int i = 0; i < RM; ++i) acc[i][j] = mfma_split6(ap[i], bq[j & 1], acc[i][j]);
+        if (j == 0) mid();
+      }
+    };
+    auto mma_s = [&](const FragS& f) { mma_mid(f, [] {}); };
+    if (a.prio && wid >= 4) __builtin_amdgcn_s_setprio(1);
+    if constexpr (SPLITD) {
+      // B step s: the packed weight columns are K-linear, so its offset is (s mod period) * BKC
+      // elements (DGRAD with a folded upsample repeats the R*S*K columns per upsample phase)
+      const int bper = (MODE == MODE_DGRAD && !SP) ? (d.R * d.S * d.K) / BKC : nk;
+      int bs = 0, bsm = 0;
+      auto issue_b = [&](char* bslot) {
+        const uint32_t ub = bs < nk ? (uint32_t)(bsm * BKC * EBB) : OOB;
+#pragma unroll
+        for (int j = 0; j < BPW; ++j) {
+          const int q = wid * BPW + j;
+          char* dst = (!JUNK || q < BPIECES) ? bslot + q * 1024 : smem + RING + 3 * WGM * BN * 4;
+          bdma16(bres, blane[j] + ub, dst);
+        }
+        ++bs;
+        bsm = bsm + 1 == bper ? 0 : bsm + 1;
+      };
+      char* const bring = smem + 3 * ABYTES;
+      // order of issue: B(0), A(0), A(1), then per step t: B(t + 1), A(t + 2).  At the top of step t
+      // everything but the last A group has landed (vmcnt(APW)): A(t) and B(t).
+      issue_b(bring);
+      issue(smem);
+      issue(smem + ABYTES);
+      int ca = 0, cb = 0;
+      for (int t = 0; t < nk; ++t) {
+        wait_vmcnt<APW>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of step t-1 are done
+        ring_barrier();
+        FragS f;
+        f.slot = smem + ca * ABYTES;
+        f.bimg = bring + cb * BBYTES;
+        // the DMA of steps t+1 (B) / t+2 (A) into step t-1's slots, issued once the step's first
+        // MFMAs are queued
+        mma_mid(f, [&] {
+          issue_b(bring + (cb ^ 1) * BBYTES);
+          issue(smem + (ca == 0 ? 2 : ca - 1) * ABYTES);
+        });
+        ca = ca == 2 ? 0 : ca + 1;
+        cb ^= 1;
+      }
+      wait_vmcnt<0>();
+    } else {
+      ring_loop_lean<PW, NS, 1>(nk, smem, SLOT, issue, load_s, mma_s);
+    }
+  } else if constexpr (SPL) {
     // The step's B tiles are read up front; the A row tiles are read inside the MFMA sequence, one
     // tile ahead (registers: the 256 x 256 tile holds 128 accumulators).  B tile j is split just
     // before its first MFMAs (row tile 0), so the step opens with one A and one B split.
@@ -2167,7 +2280,7 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
 int64_t g_conv_launches = 0;
 extern "C" int64_t es_conv_launch_count() { return g_conv_launches; }
 
-template <int MODE, int BM, int BN, bool SP, int BK = 64, typename T = bf16, bool SPL = false>
+template <int MODE, int BM, int BN, bool SP, int BK = 64, typename T = bf16, int SPL = 0>
 void launch_ring(const ConvArgs& a, int row_tiles, hipStream_t st) {
   dim3 grid(row_tiles, (a.Ng + BN - 1) / BN, 1);
   ++g_conv_launches;
@@ -2329,7 +2442,7 @@ extern "C" int es_conv_subpixel_ok(const es_conv_desc_t* d, es_dtype_t dt) {
   return xbytes < (1ll << 30) && ybytes < (1ll << 30) && wbytes < (1ll << 30);
 }
 
-template <typename T, bool SPL = false>
+template <typename T, int SPL = 0>
 int ring_fd(ConvArgs& a, int mode, hipStream_t st);
 
 int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
@@ -2358,10 +2471,14 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
 
 // FWD / DGRAD ring launch for bf16 or fp32 operands (fp32: the parity mode's exact fp32 MFMA, or with
 // SPL the split-fp32 bf16-plane MFMA on 32-channel K-steps; the persistent kernels are bf16-only)
-template <typename T, bool SPL>
+template <typename T, int SPL>
 int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
   const es_conv_desc_t& d = a.d;
   const bool sp_weights = d.subpixel != 0;
+  if constexpr (SPL == 2) {   // the pre-split B planes follow the fp32 packing (es_pack_weight_planes)
+    const int64_t nel = (int64_t)d.K * d.C * (sp_weights ? es_subpixel_taps(d.R, d.S) : d.R * d.S);
+    a.b_src = (const char*)a.b_src + es_weight_planes_offset(nel);
+  }
   constexpr int EB = sizeof(T);
   // caller checked: channels % (128 / EB) == 0, K % (128 / EB) == 0 per step
   int PQ;
@@ -2384,6 +2501,10 @@ int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
   // of LDS, two workgroups per CU) so one tile's fill and epilogue overlap another's MFMAs
   // (measured 201 -> 177 us; the same rule on the DGRAD of that conv was slower)
   bool shortk = g_ring_shortk && mode == MODE_FWD && !sp_weights && a.Kd / 64 <= 8;
+  if constexpr (SPL == 2) {   // A/B knob: 256-row tiles for the short-K split-fp32 FWD
+    static const bool noshort = [] { const char* e = getenv("ES_SPB_NOSHORTK"); return e && e[0] == '1'; }();
+    if (noshort) shortk = false;
+  }
   if (sp_weights && mode == MODE_FWD && g_sp_shortk > 0) {
     const int cls_steps = ((d.R + 1) / 2) * ((d.S + 1) / 2) * d.C / 64;   // K-steps of the largest class
     shortk = cls_steps <= g_sp_shortk;
@@ -2493,9 +2614,18 @@ int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
       return 1;
     }
     ++g_conv_launches;
-    if constexpr (SPL) {   // 256 x 256 tiles of 32-channel steps
+    if constexpr (SPL == 2) {   // 256 x 128 tiles (a wave's 128 columns within one class) or 256 x 64
+      static const bool bn64 = [] { const char* e = getenv("ES_SPB_BN64"); return e && e[0] == '1'; }();
+      if (a.Ng % 128 == 0 && !bn64) {
+        dim3 grid(row_tiles, 4 * a.Ng / 128, 1);
+        hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 128, true, 64, T, 2>), grid, dim3(RT), 0, st, a);
+      } else {
+        dim3 grid(row_tiles, 4 * a.Ng / 64, 1);
+        hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 64, true, 64, T, 2>), grid, dim3(RT), 0, st, a);
+      }
+    } else if constexpr (SPL) {   // 256 x 256 tiles of 32-channel steps
       dim3 grid(row_tiles, (4 * a.Ng + 255) / 256, 1);
-      hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 256, true, 64, T, true>), grid, dim3(RT), 0, st, a);
+      hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 256, true, 64, T, 1>), grid, dim3(RT), 0, st, a);
     } else {
       dim3 grid(row_tiles, (4 * a.Ng + 255) / 256, 1);
       hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 256, true, 32, T>), grid, dim3(RT), 0, st, a);
@@ -2507,13 +2637,19 @@ int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
               : launch_ring<MD, BMV, BNV, false, 64, T, SPL>(a, row_tiles, st))
   const bool wide = g_ring256 && big && !shortk && a.Ng >= 256 && a.ng >= 16 && a.vec_out &&
                     (sp_weights || mode == MODE_DGRAD);   // (plain FWD: register spills at 256 x 256)
-  if constexpr (SPL) if (wide) {   // split-fp32: 256 x 256 tiles of 32-channel steps
+  if constexpr (SPL == 1) if (wide) {   // split-fp32: 256 x 256 tiles of 32-channel steps
     if (mode == MODE_FWD) {   // (wide FWD is sub-pixel only)
-      launch_ring<MODE_FWD, 256, 256, true, 64, T, true>(a, row_tiles, st);
+      launch_ring<MODE_FWD, 256, 256, true, 64, T, 1>(a, row_tiles, st);
     } else {
-      if (sp_weights) launch_ring<MODE_DGRAD, 256, 256, true, 64, T, true>(a, row_tiles, st);
-      else launch_ring<MODE_DGRAD, 256, 256, false, 64, T, true>(a, row_tiles, st);
+      if (sp_weights) launch_ring<MODE_DGRAD, 256, 256, true, 64, T, 1>(a, row_tiles, st);
+      else launch_ring<MODE_DGRAD, 256, 256, false, 64, T, 1>(a, row_tiles, st);
     }
+    return 1;
+  }
+  if constexpr (SPL == 2) if (wide) {   // pre-split B: 256 x 128 tiles (256 x 256 does not fit the LDS)
+    if (mode == MODE_FWD) launch_ring<MODE_FWD, 256, 128, true, 64, T, 2>(a, row_tiles, st);
+    else if (sp_weights) launch_ring<MODE_DGRAD, 256, 128, true, 64, T, 2>(a, row_tiles, st);
+    else launch_ring<MODE_DGRAD, 256, 128, false, 64, T, 2>(a, row_tiles, st);
     return 1;
   }
   if constexpr (!SPL) if (wide) {
@@ -2581,7 +2717,8 @@ int es_conv_ring_launch_f32(ConvArgs& a, int mode, hipStream_t st) {
     c.M = mode == MODE_FWD ? c.d.N * d.P * d.Q : (a.fold ? c.d.N * d.H * d.W : c.d.N * d.Hu * d.Wu);
     if (req.part) g_stats_req = StatsRequest{req.part + (int64_t)used * 3 * a.Ng, req.floats - (int64_t)used * 3 * a.Ng, 0};
     c.prio = g_spl_prio;
-    const int rc = g_f32_split ? ring_fd<float, true>(c, mode, st) : ring_fd<float>(c, mode, st);
+    const int rc = g_f32_split == 2 ? ring_fd<float, 2>(c, mode, st)
+                   : g_f32_split ? ring_fd<float, 1>(c, mode, st) : ring_fd<float>(c, mode, st);
     if (rc <= 0) {
       g_stats_req = req;
       if (n0 == 0) return rc;
@@ -2667,7 +2804,8 @@ int es_wgrad_f32_ring(const es_conv_desc_t& d, const void* dy, const int64_t ys[
 #define ES_WF(BM, BN)                                                                                 \
   do {                                                                                                \
     ++g_conv_launches;                                                                                \
-    if (g_f32_split) {                                                                                \
+    if (g_f32_split && BM == 128) {  /* (64-row tiles: the split is VALU-bound there, measured  */    \
+                                      /*  1.59 ms vs 1.41 exact for conv_layers.9 at B = 1024)   */    \
       if (p.sp) hipLaunchKernelGGL((wgrad_f32_kernel<BM, BN, true, true>), grid, dim3(RT), 0, st, a, wsc, p.ngt); \
       else hipLaunchKernelGGL((wgrad_f32_kernel<BM, BN, false, true>), grid, dim3(RT), 0, st, a, wsc, p.ngt);    \
     } else if (p.sp) hipLaunchKernelGGL((wgrad_f32_kernel<BM, BN, true>), grid, dim3(RT), 0, st, a, wsc, p.ngt); \
@@ -2706,6 +2844,6 @@ extern "C" int es_conv_set_f32_chunk(int images) {
 
 extern "C" int es_conv_set_f32_split(int on) {
   const int old = g_f32_split;
-  g_f32_split = on > 0 ? 1 : 0;
+  g_f32_split = on < 0 ? 0 : (on > 2 ? 2 : on);
   return old;
 }

@@ -176,20 +176,27 @@ def deterministic() -> bool:
 
 
 # fp32 MFMA arithmetic of the ring convolutions: exact fp32 (v_mfma_f32_16x16x4_f32) or split-fp32
-# (three bf16 planes per operand, six plane products on v_mfma_f32_16x16x32_bf16; es_conv_set_f32_split)
+# (three bf16 planes per operand, six plane products on v_mfma_f32_16x16x32_bf16; es_conv_set_f32_split).
+# Level 2 (default when on): the packed weights carry their planes (es_pack_weight_planes), so the
+# FWD / DGRAD kernels split only the activations; ES_F32_SPLIT_LEVEL=1 splits both in the kernel.
 _F32_SPLIT = None
+_SPLIT_LEVEL = int(os.environ.get("ES_F32_SPLIT_LEVEL", "2"))
 
 
 def set_f32_split(on: bool):
     global _F32_SPLIT
-    on = bool(on)
-    if on != _F32_SPLIT:
-        hip.lib().es_conv_set_f32_split(1 if on else 0)
-        _F32_SPLIT = on
+    lvl = _SPLIT_LEVEL if on else 0
+    if lvl != _F32_SPLIT:
+        hip.lib().es_conv_set_f32_split(lvl)
+        _F32_SPLIT = lvl
 
 
 def f32_split() -> bool:
     return bool(_F32_SPLIT)
+
+
+def f32_split_level() -> int:
+    return int(_F32_SPLIT or 0)
 
 
 # --------------------------------------------------------------------------------- upsample
@@ -265,14 +272,22 @@ class ConvOp:
         self._packed.clear()
 
     def packed(self, dtype, mode, inv_scale=None):
-        key = (dtype, mode)
+        """Packed GEMM weights; fp32 with split level 2 also carries the bf16 planes behind the fp32
+        packing (es_pack_weight_planes) that the split-fp32 ring kernels read."""
+        planes = dtype == torch.float32 and f32_split_level() == 2
+        key = (dtype, mode, planes)
         if inv_scale is None and key in self._packed:
             return self._packed[key]
         w = self.weight
         n = w.numel() if mode < 2 else self.K * self.C * hip.lib().es_subpixel_taps(self.R, self.S)
-        out = torch.empty(n, dtype=dtype, device=w.device)
+        total = n
+        if planes:
+            total = (int(hip.lib().es_weight_planes_offset(n)) + 6 * n + 3) // 4
+        out = torch.empty(total, dtype=dtype, device=w.device)
         hip.call("es_pack_conv_weight", hip.ptr(w), self.K, self.C, self.R, self.S, mode,
                  hip.ptr(inv_scale), None, hip.ptr(out), hip.dt_of(out), hip.stream_ptr())
+        if planes:
+            hip.call("es_pack_weight_planes", hip.ptr(out), n, hip.ptr(out), hip.stream_ptr())
         if inv_scale is None:
             self._packed[key] = out
         return out

@@ -183,6 +183,14 @@ int es_conv_set_f32_chunk(int images);
  * same fp32 conv2d / conv_transpose products as es_conv2d_fwd / _dgrad / _wgrad_det (neutron
  * generator.py:23-35, proton generator.py:26-38).  MoEWrapper sets it from train.fp32_mfma. */
 int es_conv_set_f32_split(int on);
+/* on = 2: as 1, and the FWD / DGRAD kernels read the packed weights' bf16 planes precomputed by
+ * es_pack_weight_planes (the caller packs them whenever level 2 is set).
+ * Byte offset of the planes behind an fp32 packing of n elements, and the planes themselves: each
+ * 32-element block g of the packing -> 192 bytes at base + es_weight_planes_offset(n) + 192 g, three
+ * planes of 32 bf16 (x0 = rne(x), x1 = rne(x - x0), x2 = x - x0 - x1), k-permuted as the ring
+ * kernels' fragments.  Same weights as es_pack_conv_weight (neutron generator.py:24,29,33). */
+int64_t es_weight_planes_offset(int64_t n);
+int es_pack_weight_planes(const float* packed, int64_t n, void* base, es_stream_t stream);
 /* Host-side count of MFMA conv kernels issued so far (ring / persistent / p256 / fp32 WGRAD).
  * Instrumentation only: lets a profiler state how many kernel launches one conv op was. */
 int64_t es_conv_launch_count(void);

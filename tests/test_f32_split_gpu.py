@@ -103,3 +103,27 @@ def test_fused_bn_stats_consistency(case, split, det):
     scale = torch.maximum(m_ref.abs(), 1.0 / invstd.cpu().double())
     err = ((mean.cpu().double() - m_ref).abs() / scale).max().item()
     assert err <= 1e-6, err
+
+
+@pytest.mark.parametrize("case", [(256, 256, 24, 24, 128, 3, 1, 0, 2), (320, 128, 13, 13, 256, 3, 1, 0, 2),
+                                  (256, 128, 46, 46, 64, 2, 1, 0, None)])
+def test_split_large_tiles_match_exact(case, det):
+    """Batches that select the 256-row tiles (the bench's kernels; the fp64 cases above are too small
+    for them): split-fp32 fwd / dgrad / wgrad against the exact fp32 MFMA path (itself pinned to
+    fp64 above) within 1e-5 of max|exact|."""
+    from expertsim import layers
+    _hip()
+    N, Cin, H, W, Cout, k, st, pad, up = case
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5
+    b = torch.randn(Cout, generator=g)
+    Ho = (H * (up or 1) + 2 * pad - k) // st + 1
+    Wo = (W * (up or 1) + 2 * pad - k) // st + 1
+    gy = torch.randn(N, Cout, Ho, Wo, generator=g)
+    layers.set_f32_split(False)
+    exact = _run(case, x, w, b, gy)[1:]
+    layers.set_f32_split(True)
+    split = _run(case, x, w, b, gy)[1:]
+    for e, s_ in zip(exact, split):
+        assert rel(s_, e) < 1e-5
