@@ -1,11 +1,11 @@
 # fp32 parity-mode HBM traffic + MFMA busy of one neutron generator conv op (separate rocprofv3
-# passes, MI355X_MICROARCH.md HBM / rocprofv3 section):  bash tools/gpu_traffic32.sh <c5> <fwd> <1024>
+# passes, MI355X_MICROARCH.md HBM / rocprofv3 section):  bash tools/gpu_traffic32.sh <c5> <fwd> <1024> [split 0|1]
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
-L=${1:-c5}; M=${2:-fwd}; NB=${3:-1024}
-O=$GRAFT_REPO_ROOT/gpurun_out/traffic32_${L}_${M}_${NB}
+L=${1:-c5}; M=${2:-fwd}; NB=${3:-1024}; SPL=${4:-0}
+O=$GRAFT_REPO_ROOT/gpurun_out/traffic32$([ "$SPL" = 1 ] && echo s)_${L}_${M}_${NB}
 mkdir -p $O
-export ES_MB_BATCH=$NB ES_MB_DTYPE=fp32
+export ES_MB_BATCH=$NB ES_MB_DTYPE=fp32 ES_MB_SPLIT=$SPL
 P="python3 $GRAFT_REPO_ROOT/tools/mb_one.py $L $M 1 5"
 timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- $P > $O/kt.log 2>&1 && \
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- $P > $O/fetch.log 2>&1 && \

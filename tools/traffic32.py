@@ -2,7 +2,7 @@
 rocprofv3 passes of tools/gpu_traffic32.sh (an op may be several dispatches: image chunks of the
 1 GiB ring limit, plus the deterministic WGRAD's ordered reduce).
 
-usage: python tools/traffic32.py <dir> <out.json> <layer> <mode> <batch> <ops>
+usage: python tools/traffic32.py <dir> <out.json> <layer> <mode> <batch> <ops> [split 0|1]
 FETCH_SIZE (KiB, x2 on gfx950 for 16-byte-per-lane streaming reads) + WRITE_SIZE (KiB) summed over
 the op's dispatches / ops (MI355X_MICROARCH.md HBM / rocprofv3 section); MFMA busy =
 SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8) over the op's conv dispatches."""
@@ -28,6 +28,7 @@ def rows(d, counter, names):
 
 def main():
     d, out, layer, mode, batch, ops = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]), int(sys.argv[6])
+    split = len(sys.argv) > 7 and sys.argv[7] == "1"
     names = NAMES[mode]
     fetch = rows(d + "/fetch", "FETCH_SIZE", names)
     write = rows(d + "/write", "WRITE_SIZE", names)
@@ -44,16 +45,20 @@ def main():
     fb = 2.0 * 1024 * sum(v for _, v in fetch) / ops
     wb = 1024.0 * sum(v for _, v in write) / ops
     res = {"layer": layer, "mode": mode, "batch": batch, "dtype": "fp32", "ops": ops,
+           "fp32_mfma": "split" if split else "exact",
            "dispatches_per_op": len(fetch) / ops, "us_per_op": round(sum(dur.values()), 1), "kernels": dur,
            "fetch_bytes": round(fb), "write_bytes": round(wb), "traffic_bytes": round(fb + wb),
            "algorithmic_bytes": alg,
            "method": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_VALU_MFMA_BUSY_CYCLES+GRBM_GUI_ACTIVE in "
-                     f"separate passes over ES_MB_DTYPE=fp32 tools/mb_one.py {layer} {mode} (B={batch}); "
+                     f"separate passes over ES_MB_DTYPE=fp32{' ES_MB_SPLIT=1' if split else ''} tools/mb_one.py "
+                     f"{layer} {mode} (B={batch}); "
                      f"FETCH_SIZE x2 (gfx950); per op = sum over its dispatches / {ops} ops"}
     if mfma and gui:
         m = sum(v for _, v in mfma)
         g = sum(v for _, v in gui)
         res["mfma_busy_frac"] = round(m / (1024.0 * g / 8.0), 4)
+        if split:
+            res["mfma_note"] = "split-fp32: busy cycles of the bf16 MFMA pipe (6 plane products per fp32 product)"
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
