@@ -596,7 +596,7 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
     const uint32_t co = (uint32_t)(cch * EB), cob = (uint32_t)(cch * EBB);
 #pragma unroll
     for (int j = 0; j < APW; ++j) bdma16(ares, alane[j] + (ua_t[j] + co), slot + (wid * APW + j) * 1024);
-    if constexpr (!SPLITD) {
+    if constexpr (!SPB) {   // (SPB: B has its own ring and issue_b)
 #pragma unroll
       for (int j = 0; j < BPW; ++j) {
         const int q = wid * BPW + j;
@@ -677,86 +677,97 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
       }
   };
   if constexpr (SPB) {
-    // A row tiles (RM = BM / 128) split once per step; B planes read per column tile straight from
-    // the pre-split image (chunk g16 of a 64-byte plane row = MFMA k 8 g16 .. +7)
-    struct FragS {
-      const char* slot;
-      const char* bimg;
-    };
-    auto load_s = [&](FragS& f, const char* slot, int) {
-      f.slot = slot;
-      f.bimg = slot + ABYTES;
-    };
-    // mid(): called after the first column tile's MFMAs (the step's DMA issue, MFMA-first head)
-    auto mma_mid = [&](const FragS& f, auto&& mid) {
-      bf16x8 ap[RM][3];
-      const char* bimg = f.bimg;
-      auto rd_b = [&](bf16x8 (&bp)[3], int j) {
+    // Software-pipelined split-fp32 loop.  A (activations, fp32) and B (pre-split weight planes) have
+    // their own rings: A in NSA slots, B in NSB.  Step t's MFMAs use A planes split during step t-1
+    // (registers) and B(t) read from LDS per column tile; under them the wave reads A(t+1) and splits
+    // it, and issues the DMA of B(t+NSB-1) / A(t+NSA).  Slot reuse: A(s) is read during step s-1 and
+    // B(s) during step s, so behind the barrier of step t the slots of A(t) and B(t-1) are free.
+    // Issue order A(0), B(0), A(1), [B(1), A(2)] ..., then per step B(t+NSB-1), A(t+NSA): at the top
+    // of step t everything but the last (NSA-2) A and (NSB-2) B groups has landed, i.e. B(t), A(t+1).
+    constexpr int NSA = SPLITD ? 3 : NS, NSB = SPLITD ? 2 : NS;
+    constexpr int PROWAIT = (NSA - 1) * APW + (NSB - 1) * BPW, LOOPWAIT = (NSA - 2) * APW + (NSB - 2) * BPW;
+    char* const aring = smem;
+    char* const bring = smem + NSA * ABYTES;
+    // B step s: the packed weight columns are K-linear, so its offset is (s mod period) * BKC elements
+    // (DGRAD with a folded upsample repeats the R*S*K columns per upsample phase)
+    const int bper = (MODE == MODE_DGRAD && !SP) ? (d.R * d.S * d.K) / BKC : nk;
+    int bs = 0, bsm = 0;
+    auto issue_b = [&](char* bslot) {
+      const uint32_t ub = bs < nk ? (uint32_t)(bsm * BKC * EBB) : OOB;
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-          bp[pl] = *(const bf16x8*)(bimg + pl * (BN * 64) + swz<32>(wn0 + j * 16 + r16, g16));
-      };
-      bf16x8 bq[2][3];
-      rd_b(bq[0], 0);
-#pragma unroll
-      for (int i = 0; i < RM; ++i) {
-        f32x4 r0 = *(const f32x4*)(f.slot + swz<BK>(wm0 + i * 16 + r16, g16));
-        f32x4 r1 = *(const f32x4*)(f.slot + swz<BK>(wm0 + i * 16 + r16, g16 + 4));
-        split8(r0, r1, ap[i]);
+      for (int j = 0; j < BPW; ++j) {
+        const int q = wid * BPW + j;
+        char* dst = (!JUNK || q < BPIECES) ? bslot + q * 1024 : smem + RING + 3 * WGM * BN * 4;
+        bdma16(bres, blane[j] + ub, dst);
       }
+      ++bs;
+      bsm = bsm + 1 == bper ? 0 : bsm + 1;
+    };
+    auto rd_a = [&](f32x4 (&r)[RM][2], const char* aslot) {
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) r[i][h] = *(const f32x4*)(aslot + swz<BK>(wm0 + i * 16 + r16, g16 + 4 * h));
+    };
+    auto rd_b = [&](bf16x8 (&bp)[3], const char* bimg, int j) {
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        bp[pl] = *(const bf16x8*)(bimg + pl * (BN * 64) + swz<32>(wn0 + j * 16 + r16, g16));
+    };
+    if (a.prio && wid >= 4) __builtin_amdgcn_s_setprio(1);
+    issue(aring);
+#pragma unroll
+    for (int st = 0; st < NSB - 1; ++st) {
+      issue_b(bring + st * BBYTES);
+      issue(aring + (st + 1) * ABYTES);
+    }
+#pragma unroll
+    for (int st = NSB - 1; st < NSA - 1; ++st) issue(aring + (st + 1) * ABYTES);
+    wait_vmcnt<PROWAIT>();
+    ring_barrier();
+    bf16x8 apc[RM][3];
+    {
+      f32x4 r[RM][2];
+      rd_a(r, aring);
+#pragma unroll
+      for (int i = 0; i < RM; ++i) split8(r[i][0], r[i][1], apc[i]);
+    }
+    int sa1 = 1 % NSA, sb = 0, ia = 0, ib = NSB - 1;   // slots: A(t+1), B(t), A(t+NSA), B(t+NSB-1)
+    constexpr int JS = RN > 2 ? RN / 2 : RN - 1;       // column tile after which A(t+1) is split
+    for (int t = 0; t < nk; ++t) {
+      wait_vmcnt<LOOPWAIT>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of the last step are done
+      ring_barrier();
+      const char* bimg = bring + sb * BBYTES;
+      bf16x8 bq[2][3];
+      rd_b(bq[0], bimg, 0);
+      f32x4 ra[RM][2];
+      rd_a(ra, aring + sa1 * ABYTES);
+      bf16x8 apn[RM][3];
 #pragma unroll
       for (int j = 0; j < RN; ++j) {
-        if (j + 1 < RN) rd_b(bq[(j + 1) & 1], j + 1);      // next column tile's planes in flight
+        if (j + 1 < RN) rd_b(bq[(j + 1) & 1], bimg, j + 1);
 #pragma unroll
-        for (int i = 0; i < RM; ++i) acc[i][j] = mfma_split6(ap[i], bq[j & 1], acc[i][j]);
-        if (j == 0) mid();
-      }
-    };
-    auto mma_s = [&](const FragS& f) { mma_mid(f, [] {}); };
-    if (a.prio && wid >= 4) __builtin_amdgcn_s_setprio(1);
-    if constexpr (SPLITD) {
-      // B step s: the packed weight columns are K-linear, so its offset is (s mod period) * BKC
-      // elements (DGRAD with a folded upsample repeats the R*S*K columns per upsample phase)
-      const int bper = (MODE == MODE_DGRAD && !SP) ? (d.R * d.S * d.K) / BKC : nk;
-      int bs = 0, bsm = 0;
-      auto issue_b = [&](char* bslot) {
-        const uint32_t ub = bs < nk ? (uint32_t)(bsm * BKC * EBB) : OOB;
-#pragma unroll
-        for (int j = 0; j < BPW; ++j) {
-          const int q = wid * BPW + j;
-          char* dst = (!JUNK || q < BPIECES) ? bslot + q * 1024 : smem + RING + 3 * WGM * BN * 4;
-          bdma16(bres, blane[j] + ub, dst);
+        for (int i = 0; i < RM; ++i) acc[i][j] = mfma_split6(apc[i], bq[j & 1], acc[i][j]);
+        if (j == 0) {   // the step's DMA, once its first MFMAs are queued
+          issue_b(bring + ib * BBYTES);
+          issue(aring + ia * ABYTES);
         }
-        ++bs;
-        bsm = bsm + 1 == bper ? 0 : bsm + 1;
-      };
-      char* const bring = smem + 3 * ABYTES;
-      // order of issue: B(0), A(0), A(1), then per step t: B(t + 1), A(t + 2).  At the top of step t
-      // everything but the last A group has landed (vmcnt(APW)): A(t) and B(t).
-      issue_b(bring);
-      issue(smem);
-      issue(smem + ABYTES);
-      int ca = 0, cb = 0;
-      for (int t = 0; t < nk; ++t) {
-        wait_vmcnt<APW>();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of step t-1 are done
-        ring_barrier();
-        FragS f;
-        f.slot = smem + ca * ABYTES;
-        f.bimg = bring + cb * BBYTES;
-        // the DMA of steps t+1 (B) / t+2 (A) into step t-1's slots, issued once the step's first
-        // MFMAs are queued
-        mma_mid(f, [&] {
-          issue_b(bring + (cb ^ 1) * BBYTES);
-          issue(smem + (ca == 0 ? 2 : ca - 1) * ABYTES);
-        });
-        ca = ca == 2 ? 0 : ca + 1;
-        cb ^= 1;
+        if (j == JS) {
+#pragma unroll
+          for (int i = 0; i < RM; ++i) split8(ra[i][0], ra[i][1], apn[i]);
+        }
       }
-      wait_vmcnt<0>();
-    } else {
-      ring_loop_lean<PW, NS, 1>(nk, smem, SLOT, issue, load_s, mma_s);
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) apc[i][pl] = apn[i][pl];
+      sa1 = sa1 + 1 == NSA ? 0 : sa1 + 1;
+      ia = ia + 1 == NSA ? 0 : ia + 1;
+      sb = sb + 1 == NSB ? 0 : sb + 1;
+      ib = ib + 1 == NSB ? 0 : ib + 1;
     }
+    wait_vmcnt<0>();   // drain the zero-fill steps before the workgroup may exit
   } else if constexpr (SPL) {
     // The step's B tiles are read up front; the A row tiles are read inside the MFMA sequence, one
     // tile ahead (registers: the 256 x 256 tile holds 128 accumulators).  B tile j is split just
