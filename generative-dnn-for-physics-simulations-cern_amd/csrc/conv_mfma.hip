@@ -31,6 +31,7 @@
 //   WGRAD      [64 images][rows] per operand (rows contiguous in global memory: channels), read
 //              with ds_read_b64_tr_b16; chunk c of k-row k stored at c ^ (2(k&3) | 8((k>>3)&1)).
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <type_traits>
 
@@ -49,7 +50,10 @@ constexpr int NSLOT = 3;  // ring depth
 #ifndef ES_RING_EXP
 #define ES_RING_EXP 0
 #endif
-constexpr uint32_t OOB = 0x80000000u;   // buffer offset past every num_records (< 2^31 bytes)
+constexpr uint32_t OOB = 0x80000000u;
+#ifndef ES_SPB_PFD
+#define ES_SPB_PFD 2   // split-fp32 SPB loop: column tiles of B planes read ahead of their MFMAs
+#endif   // buffer offset past every num_records (< 2^31 bytes)
 
 // ES_NO_RING=1 (or es_conv_set_ring(0)) routes these shapes to the 4-wave kernels of
 // conv_igemm.hip (A/B measurement)
@@ -739,16 +743,19 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of the last step are done
       ring_barrier();
       const char* bimg = bring + sb * BBYTES;
-      bf16x8 bq[2][3];
-      rd_b(bq[0], bimg, 0);
+      // B planes PFD column tiles ahead (LDS latency under load exceeds one tile's 12 MFMAs)
+      constexpr int PFD = ES_SPB_PFD;
+      bf16x8 bq[PFD + 1][3];
+#pragma unroll
+      for (int j = 0; j < PFD && j < RN; ++j) rd_b(bq[j], bimg, j);
       f32x4 ra[RM][2];
       rd_a(ra, aring + sa1 * ABYTES);
       bf16x8 apn[RM][3];
 #pragma unroll
       for (int j = 0; j < RN; ++j) {
-        if (j + 1 < RN) rd_b(bq[(j + 1) & 1], bimg, j + 1);
+        if (j + PFD < RN) rd_b(bq[(j + PFD) % (PFD + 1)], bimg, j + PFD);
 #pragma unroll
-        for (int i = 0; i < RM; ++i) acc[i][j] = mfma_split6(apc[i], bq[j & 1], acc[i][j]);
+        for (int i = 0; i < RM; ++i) acc[i][j] = mfma_split6(apc[i], bq[j % (PFD + 1)], acc[i][j]);
         if (j == 0) {   // the step's DMA, once its first MFMAs are queued
           issue_b(bring + ib * BBYTES);
           issue(aring + ia * ABYTES);
@@ -2694,9 +2701,16 @@ namespace {
 int g_f32_chunk = 0;   // test knob (es_conv_set_f32_chunk): at most this many images per fp32 launch
 // fp32 MFMA arithmetic of the ring kernels: 0 = exact fp32 (v_mfma_f32_16x16x4_f32), 1 = split-fp32
 // (three bf16 planes, 6 products on v_mfma_f32_16x16x32_bf16); es_conv_set_f32_split / ES_F32_SPLIT
-int g_f32_split = [] { const char* e = getenv("ES_F32_SPLIT"); return e ? atoi(e) : 0; }();
+// (Plain functions, not lambdas: hipcc numbers the namespace-scope lambdas of a second anonymous
+// namespace block from #1 again, and the duplicate symbols resolved to the first block's lambdas, so
+// these globals were initialised by other variables' initialisers.)
+int env_int(const char* name, int def) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : def;
+}
+int g_f32_split = env_int("ES_F32_SPLIT", 0);
 // split-fp32 kernels: static s_setprio 1 for waves 4-7 (ES_SPL_PRIO=0 off; A/B)
-int g_spl_prio = [] { const char* e = getenv("ES_SPL_PRIO"); return e ? atoi(e) : 1; }();
+int g_spl_prio = env_int("ES_SPL_PRIO", 1);
 // images per launch: equal chunks (whole 64-image groups where the limit allows) below the limit
 int chunk_images(int64_t img_bytes, int N) {
   int64_t lim = ((1ll << 30) - 1) / std::max<int64_t>(img_bytes, 1);

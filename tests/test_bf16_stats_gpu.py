@@ -116,8 +116,9 @@ def test_bf16_training_statistics_match_fp32_and_oracle():
 # Three HIP runs, 12 steps each, same init and data: F32a and B16a see the same injected noise /
 # Gumbel draws, F32b another draw of them.  The natural spread of the training process is
 # WS(F32b, F32a): the same fp32 training (pinned to the reference at this batch size by
-# tests/test_b512_gpu.py) with only its random noise changed.  The bf16 run must stay within 3x of
-# it: WS(B16a, F32a) <= 3 * WS(F32b, F32a) (per channel, relative to the channel mean; eval-mode
+# tests/test_b512_gpu.py) with only its random noise changed (F32b, F32c: two other draws, averaged).
+# The bf16 run must stay within 3x of it: WS(B16a, F32a) <= 3 * mean(WS(F32b, F32a), WS(F32c, F32a))
+# (per channel, relative to the channel mean; eval-mode
 # generations of 4096 fixed conditions / noises), and likewise its loss trajectory.  Measured (r03j):
 # WS 0.0428 vs natural 0.0182 (2.35x); trajectory 0.0107 vs natural 0.0572.
 B512, STEPS512, EVAL512 = 512, 12, 4096
@@ -141,16 +142,19 @@ def test_bf16_training_statistics_b512():
     ev = make_batch(EVAL512, "neutron", seed=901)
     eval_cond = torch.from_numpy(ev["cond"])
     eval_noise = [torch.randn(EVAL512, 10, generator=torch.Generator().manual_seed(13))]
-    sa, sb = _inputs512(21), _inputs512(22)
+    sa, sb, sc = _inputs512(21), _inputs512(22), _inputs512(23)
     f32a = _hip_run("fp32", sa, eval_cond, eval_noise)
     f32b = _hip_run("fp32", sb, eval_cond, eval_noise)
+    f32c = _hip_run("fp32", sc, eval_cond, eval_noise)
     b16a = _hip_run("bf16", sa, eval_cond, eval_noise)
 
     def traj_dev(run, ref):
         return max(float(np.max(np.abs(np.array([s[k] for s in run[0]]) - np.array([s[k] for s in ref[0]])))
                          / max(np.mean(np.abs([s[k] for s in ref[0]])), 1e-12)) for k in KEYS)
-    natural_ws = _ws_rel(f32b[1], f32a[1])
-    natural_traj = traj_dev(f32b, f32a)
+    # the natural spread as the mean over two other noise draws (one draw's WS is itself a noisy
+    # estimate: r03 measured 0.0158 and 0.0182 for the same pair of seeds on two fp32 builds)
+    natural_ws = 0.5 * (_ws_rel(f32b[1], f32a[1]) + _ws_rel(f32c[1], f32a[1]))
+    natural_traj = 0.5 * (traj_dev(f32b, f32a) + traj_dev(f32c, f32a))
     ws = _ws_rel(b16a[1], f32a[1])
     tr = traj_dev(b16a, f32a)
     print(f"B=512: WS(bf16, fp32)/mean {ws:.4g} vs natural WS(fp32 noise b, a) {natural_ws:.4g}; "
