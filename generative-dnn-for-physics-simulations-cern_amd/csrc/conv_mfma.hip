@@ -51,6 +51,9 @@ constexpr int NSLOT = 3;  // ring depth
 #define ES_RING_EXP 0
 #endif
 constexpr uint32_t OOB = 0x80000000u;
+#ifndef ES_COOP2
+#define ES_COOP2 0   // wgrad_coop_kernel: two register stages of loads (experiment)
+#endif
 #ifndef ES_SPB_PFD
 #define ES_SPB_PFD 2   // split-fp32 SPB loop: column tiles of B planes read ahead of their MFMAs
 #endif   // buffer offset past every num_records (< 2^31 bytes)
@@ -2084,11 +2087,13 @@ __global__ void __launch_bounds__(RT) wgrad_f32_kernel(ConvArgs a, float* __rest
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int RM = WM / 16, RN = WN / 16;
   constexpr int AIMG = KI * BM * 4, SLOT = KI * (BM + BN) * 4;
+  constexpr int NSW = 3 * SLOT > 150 * 1024 ? 2 : NSLOT;        // (64 x 512 split tiles: 72 KiB slots)
+  constexpr bool MT = BN == 512 && !SP;                         // a tile spans several taps (C < 512)
   constexpr int APW = BM / 64, BPW = BN / 64;                  // 1 KiB pieces per wave per slot
   constexpr int PW = APW + BPW;
   constexpr int ALPR = BM / 4, BLPR = BN / 4;                  // lanes (16-byte chunks) per k-row
   static_assert(ALPR >= 8 && BLPR >= 8, "the k-row swizzle flips 64-byte halves");
-  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT];
+  __shared__ __attribute__((aligned(16))) char smem[NSW * SLOT];
   const es_conv_desc_t& d = a.d;
   const SubPixel& sp = a.sp;
   const int G = (d.N + KI - 1) / KI;
@@ -2131,6 +2136,7 @@ __global__ void __launch_bounds__(RT) wgrad_f32_kernel(ConvArgs a, float* __rest
     const int as0b = (int)a.as[0] * 4, as2b = (int)a.as[2] * 4, as3b = (int)a.as[3] * 4;
     const int bs0b = (int)a.bs[0] * 4, bs2b = (int)a.bs[2] * 4, bs3b = (int)a.bs[3] * 4;
     uint32_t alane[APW], blane[BPW];
+    int btr[MT ? BPW : 1], bts[MT ? BPW : 1];
 #pragma unroll
     for (int j = 0; j < APW; ++j) {
       const int kr = (wid * APW + j) * (64 / ALPR) + lane / ALPR;   // image of the K-step
@@ -2138,11 +2144,26 @@ __global__ void __launch_bounds__(RT) wgrad_f32_kernel(ConvArgs a, float* __rest
     }
 #pragma unroll
     for (int j = 0; j < BPW; ++j) {
-      const int kr = (wid * BPW + j) * (64 / BLPR) + lane / BLPR;
-      blane[j] = (uint32_t)(kr * bs0b + (cb + ((lane % BLPR) ^ ((kr & 1) << 2)) * 4) * 4);
+      // (a k-row of a 512-column tile spans two pieces)
+      const int pc = wid * BPW + j;
+      const int kr = BLPR > 64 ? pc / (BLPR / 64) : pc * (64 / BLPR) + lane / BLPR;
+      const int ch = BLPR > 64 ? (pc % (BLPR / 64)) * 64 + lane : lane % BLPR;
+      if constexpr (MT) {   // the lane's own tap and channel (the swizzle stays inside a tap: C % 32 == 0)
+        const int ng = n0 + (ch ^ ((kr & 1) << 2)) * 4, rl = ng / d.C;
+        btr[j] = rl / d.S;
+        bts[j] = rl - btr[j] * d.S;
+        blane[j] = (uint32_t)(kr * bs0b + (ng - rl * d.C) * 4);
+      } else {
+        blane[j] = (uint32_t)(kr * bs0b + (cb + (ch ^ ((kr & 1) << 2)) * 4) * 4);
+      }
     }
     int cp, cq, cg, cstep = tbeg;
-    {
+    if constexpr (MT) {   // pixel-minor K order: a step's right-hand taps are the next step's left ones (L2)
+      cg = tbeg / npix;
+      const int pix = tbeg - cg * npix;
+      cp = pix / gq;
+      cq = pix - cp * gq;
+    } else {
       const int pix = tbeg / G;
       cg = tbeg - pix * G;
       cp = pix / gq;
@@ -2158,6 +2179,17 @@ __global__ void __launch_bounds__(RT) wgrad_f32_kernel(ConvArgs a, float* __rest
         const int hs = cp + coh + tr, wsx = cq + cow + ts;
         const bool ok = live && (unsigned)hs < (unsigned)d.H && (unsigned)wsx < (unsigned)d.W;
         ub = ok ? (uint32_t)(cg * KI * bs0b + hs * bs2b + wsx * bs3b) : OOB;
+      } else if constexpr (MT) {   // one pixel per lane group: the B pieces' own taps
+        ua = live ? (uint32_t)(cg * KI * as0b + cp * as2b + cq * as3b) : OOB;
+        const int hb = cp * d.stride - d.pad, wb = cq * d.stride - d.pad;
+#pragma unroll
+        for (int j = 0; j < BPW; ++j) {
+          const int hu = hb + btr[j], wu = wb + bts[j];
+          const bool ok = live && (unsigned)hu < (unsigned)d.Hu && (unsigned)wu < (unsigned)d.Wu;
+          const uint32_t u = ok ? (uint32_t)(cg * KI * bs0b + fdiv(hu, a.fUh) * bs2b + fdiv(wu, a.fUw) * bs3b) : OOB;
+          bdma16(bres, blane[j] + u, slot + AIMG + (wid * BPW + j) * 1024);
+        }
+        ub = 0;
       } else {
         ua = live ? (uint32_t)(cg * KI * as0b + cp * as2b + cq * as3b) : OOB;
         const int hu = cp * d.stride - d.pad + tr, wu = cq * d.stride - d.pad + ts;
@@ -2166,16 +2198,28 @@ __global__ void __launch_bounds__(RT) wgrad_f32_kernel(ConvArgs a, float* __rest
       }
 #pragma unroll
       for (int j = 0; j < APW; ++j) bdma16(ares, alane[j] + ua, slot + (wid * APW + j) * 1024);
+      if constexpr (!MT) {
 #pragma unroll
-      for (int j = 0; j < BPW; ++j) bdma16(bres, blane[j] + ub, slot + AIMG + (wid * BPW + j) * 1024);
+        for (int j = 0; j < BPW; ++j) bdma16(bres, blane[j] + ub, slot + AIMG + (wid * BPW + j) * 1024);
+      }
       ++cstep;
-      ++cg;
-      const bool w1 = cg == G;
-      cg = w1 ? 0 : cg;
-      cq += w1;
-      const bool w2 = cq == gq;
-      cq = w2 ? 0 : cq;
-      cp += w2;
+      if constexpr (MT) {
+        ++cq;
+        const bool w1 = cq == gq;
+        cq = w1 ? 0 : cq;
+        cp += w1;
+        const bool w2 = cp == d.P;
+        cp = w2 ? 0 : cp;
+        cg += w2;
+      } else {
+        ++cg;
+        const bool w1 = cg == G;
+        cg = w1 ? 0 : cg;
+        cq += w1;
+        const bool w2 = cq == gq;
+        cq = w2 ? 0 : cq;
+        cp += w2;
+      }
     };
     // fragment set kk: images 16 kk .. 16 kk + 15 of the step, as 4 MFMA k-groups of 4 images
     struct Frag {
@@ -2208,14 +2252,21 @@ __global__ void __launch_bounds__(RT) wgrad_f32_kernel(ConvArgs a, float* __rest
       struct FragS {
         float a[8][RM], b[8][RN];
       };
+      // the lane's byte offsets of float (k-row 4 j + kl, row base + 16 i + col16) for i even / odd
+      // (the odd-k-row swizzle flips bit 0 of base / 16 + i); the rest is an immediate 4 j rowb + 64 i
+      const int sw = (kl & 1) * 64;
+      const int sa0 = (wm0 >> 4) & 1 ? -sw : sw, sb0 = (wn0 >> 4) & 1 ? -sw : sw;
+      const int oa0 = kl * BM * 4 + (wm0 + col16) * 4 + sa0, oa1 = oa0 - 2 * sa0;
+      const int ob0 = AIMG + kl * BN * 4 + (wn0 + col16) * 4 + sb0, ob1 = ob0 - 2 * sb0;
       auto load_s = [&](FragS& f, const char* slot, int) {
+        const char* pa[2] = {slot + oa0, slot + oa1};
+        const char* pb[2] = {slot + ob0, slot + ob1};
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const int k = 4 * j + kl;
 #pragma unroll
-          for (int i = 0; i < RM; ++i) f.a[j][i] = rd(slot, BM * 4, k, wm0 + i * 16 + col16);
+          for (int i = 0; i < RM; ++i) f.a[j][i] = *(const float*)(pa[i & 1] + j * 4 * BM * 4 + 64 * i);
 #pragma unroll
-          for (int jn = 0; jn < RN; ++jn) f.b[j][jn] = rd(slot + AIMG, BN * 4, k, wn0 + jn * 16 + col16);
+          for (int jn = 0; jn < RN; ++jn) f.b[j][jn] = *(const float*)(pb[jn & 1] + j * 4 * BN * 4 + 64 * jn);
         }
       };
       auto mma_s = [&](const FragS& f) {
@@ -2239,13 +2290,370 @@ __global__ void __launch_bounds__(RT) wgrad_f32_kernel(ConvArgs a, float* __rest
         }
       };
       if (a.prio && wid >= 4) __builtin_amdgcn_s_setprio(1);
-      ring_loop_lean<PW, NSLOT, 1>(tend - tbeg, smem, SLOT, issue, load_s, mma_s);
+      ring_loop_lean<PW, NSW, 1>(tend - tbeg, smem, SLOT, issue, load_s, mma_s);
     } else {
       auto nofence = [](Frag&) {};
       ring_loop<PW, 0>(tend - tbeg, smem, SLOT, issue, load, mma, nofence);
     }
   }
   // the raw tile of this split (zeros for an empty split): plain stores into its own slot
+  float* o = ws + ((int64_t)split * a.M + m0 + wm0) * ngt + n0 + wn0 + col16;
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) o[(int64_t)(i * 16 + rq + jj) * ngt + j * 16] = acc[i][j][jj];
+}
+
+// Ring loop that keeps the previous step's slot: compute of step t reads slots t and t-1, so the DMA
+// issued at step t (step t + NS - 2) goes into step t-2's slot; NS - 2 steps in flight.
+template <int PW, int NS, typename Issue, typename Load, typename Mma>
+__device__ __forceinline__ void ring_loop_keep(int nk, char* smem, int slot_bytes, Issue& issue, Load& load,
+                                               Mma& mma) {
+  using Frag = typename std::remove_reference<typename lambda_arg<Load>::type>::type;
+  static_assert(NS >= 3, "two live slots plus one in flight");
+#pragma unroll
+  for (int i = 0; i < NS - 2; ++i) issue(smem + i * slot_bytes);
+  int cur = 0, prv = NS - 1, nxt = NS - 2;
+  for (int t = 0; t < nk; ++t) {
+    wait_vmcnt<(NS - 3) * PW>();                         // step t landed (this wave's pieces)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of step t-1 are done
+    ring_barrier();
+    issue(smem + nxt * slot_bytes);                      // step t + NS - 2 into step t-2's slot
+    Frag f;
+    load(f, smem + cur * slot_bytes, smem + prv * slot_bytes);
+    mma(f);
+    prv = cur;
+    cur = cur == NS - 1 ? 0 : cur + 1;
+    nxt = nxt == NS - 1 ? 0 : nxt + 1;
+  }
+  wait_vmcnt<0>();   // drain the zero-fill steps before the workgroup may exit
+}
+
+// Split-fp32 WGRAD of a 2 x 2, stride-1 convolution with 128 input and 64 output channels (neutron
+// G conv_layers.9: 128 -> 64 on 46 x 46): one 64 x 512 tile (the four taps x 128 channels) whose
+// K-steps walk the output columns of one row: column-step j of (image group g, row p) DMAs the input
+// column x[g][p - pad + {0, 1}][j - pad][:] (2 rows x 128 channels) and dy[g][p][j - 1][:] (64
+// channels), and multiplies dy(p, j - 1) with its four taps: the right-hand taps from this step's
+// slot, the left-hand ones from the previous step's, so every input pixel is DMA'd into LDS once per
+// row instead of once per tap (40 KiB per step instead of 72 KiB: the multi-tap tiles of
+// wgrad_f32_kernel<64, 512> are LDS-fill bound).  A row is Q + 1 column-steps (the first loads only);
+// a split starting inside a row first reloads the column before it (no MFMAs on such steps).
+// Same deterministic partial slots and ordered reduce as wgrad_f32_kernel.
+__global__ void __launch_bounds__(RT) wgrad_f32_col_kernel(ConvArgs a, float* __restrict__ ws, int ngt) {
+  constexpr int KI = 32, BM = 64, CC = 128;                     // (N = 4 taps x CC = 512)
+  constexpr int RM = 4, RN = 4;                                // 8 waves of 64 x 64 (one tap, 64 channels)
+  constexpr int AIMG = KI * BM * 4, SLOT = AIMG + KI * 2 * CC * 4;   // 8 + 32 KiB
+  constexpr int NS = 4;
+  constexpr int APW = 1, BPW = 4, PW = APW + BPW;
+  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
+  const es_conv_desc_t& d = a.d;
+  const int G = (d.N + KI - 1) / KI, Q1 = d.Q + 1;
+  const int split = xcd_remap(blockIdx.z, gridDim.z);
+  const int nst = G * d.P * Q1;
+  const int tbeg = min(split * a.k_per_split, nst), tend = min(nst, tbeg + a.k_per_split);
+
+  const int lane = threadIdx.x & 63, wid = uni(threadIdx.x >> 6);
+  const int tap = wid >> 1, wtr = tap >> 1, wts = tap & 1, wc0 = (wid & 1) * 64;
+  const int col16 = lane & 15, rq = (lane >> 4) * 4;
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (tbeg < tend) {
+    const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * 4));
+    const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)(d.N * a.bs[0] * 4));
+    const int as0b = (int)a.as[0] * 4, as2b = (int)a.as[2] * 4, as3b = (int)a.as[3] * 4;
+    const int bs0b = (int)a.bs[0] * 4, bs2b = (int)a.bs[2] * 4, bs3b = (int)a.bs[3] * 4;
+    uint32_t alane, blane[BPW];
+    {
+      const int kr = wid * 4 + (lane >> 4);                    // 4 images of 64 channels per piece
+      alane = (uint32_t)(kr * as0b + (((lane & 15) ^ ((kr & 1) << 2)) * 4) * 4);
+    }
+    const int ltr = lane >> 5;                                 // the lane's input row (the swizzle
+#pragma unroll                                                 //  stays inside a 32-chunk half)
+    for (int j = 0; j < BPW; ++j) {
+      const int kr = wid * BPW + j;                            // one image (2 x 128 channels) per piece
+      blane[j] = (uint32_t)(kr * bs0b + (((lane ^ ((kr & 1) << 2)) & 31) * 4) * 4);
+    }
+    // the first step: the column before tbeg when tbeg is inside a row
+    int cg, cp, cj;
+    {
+      cg = tbeg / (d.P * Q1);
+      const int r = tbeg - cg * d.P * Q1;
+      cp = r / Q1;
+      cj = r - cp * Q1;
+    }
+    const int s0 = tbeg - (cj > 0);
+    cj -= cj > 0;
+    int cstep = s0;
+    {   // zero the B image of the slot the first step takes as its previous one
+      float4* z = (float4*)(smem + (NS - 1) * SLOT + AIMG);
+      for (int i = threadIdx.x; i < KI * 2 * CC / 4; i += RT) z[i] = float4{0.f, 0.f, 0.f, 0.f};
+    }
+    auto issue = [&](char* slot) {
+      const bool live = cstep < tend;
+      const uint32_t ua =
+          live && cj > 0 && cstep >= tbeg ? (uint32_t)(cg * KI * as0b + cp * as2b + (cj - 1) * as3b) : OOB;
+      const int hu = cp - d.pad + ltr, wu = cj - d.pad;
+      const bool ok = live && (unsigned)hu < (unsigned)d.H && (unsigned)wu < (unsigned)d.W;
+      const uint32_t ub = ok ? (uint32_t)(cg * KI * bs0b + hu * bs2b + wu * bs3b) : OOB;
+      bdma16(ares, alane + ua, slot + wid * 1024);
+#pragma unroll
+      for (int j = 0; j < BPW; ++j) bdma16(bres, blane[j] + ub, slot + AIMG + (wid * BPW + j) * 1024);
+      ++cstep;
+      ++cj;
+      const bool w1 = cj == Q1;
+      cj = w1 ? 0 : cj;
+      cp += w1;
+      const bool w2 = cp == d.P;
+      cp = w2 ? 0 : cp;
+      cg += w2;
+    };
+    struct FragS {
+      float a[8][RM], b[8][RN];
+    };
+    const int kl = lane >> 4;
+    // the lane's byte offsets of float (k-row 4 j + kl, row base + 16 i + col16), i even / odd: the
+    // swizzle of odd k-rows flips bit 0 of i (base % 32 == 0), the rest is an immediate 4 j rowb + 64 i
+    const int sw = (kl & 1) * 64;
+    const int oa0 = kl * BM * 4 + col16 * 4 + sw, oa1 = oa0 - 2 * sw;
+    const int ob0 = kl * 2 * CC * 4 + (wtr * CC + wc0 + col16) * 4 + sw, ob1 = ob0 - 2 * sw;
+    auto load_s = [&](FragS& f, const char* slot, const char* prev) {
+      const char* bimg = (wts ? slot : prev) + AIMG;
+      const char* pa[2] = {slot + oa0, slot + oa1};
+      const char* pb[2] = {bimg + ob0, bimg + ob1};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+#pragma unroll
+        for (int i = 0; i < RM; ++i) f.a[j][i] = *(const float*)(pa[i & 1] + j * 4 * BM * 4 + 64 * i);
+#pragma unroll
+        for (int jn = 0; jn < RN; ++jn) f.b[j][jn] = *(const float*)(pb[jn & 1] + j * 4 * 2 * CC * 4 + 64 * jn);
+      }
+    };
+    // steps without MFMAs of their own (a row's first column, a split's reloaded column) have
+    // A = 0 (OOB fill): they run the same MFMAs, which add exact zeros (the previous slot of the
+    // first step is zeroed below, so no uninitialised LDS reaches them)
+    auto mma_s = [&](const FragS& f) {
+      bf16x8 bp[RN][3], ap[3];
+      auto sa = [&](int i) {
+        split8(f32x4{f.a[0][i], f.a[1][i], f.a[2][i], f.a[3][i]}, f32x4{f.a[4][i], f.a[5][i], f.a[6][i], f.a[7][i]},
+               ap);
+      };
+      sa(0);
+#pragma unroll
+      for (int jn = 0; jn < RN; ++jn) {
+        split8(f32x4{f.b[0][jn], f.b[1][jn], f.b[2][jn], f.b[3][jn]},
+               f32x4{f.b[4][jn], f.b[5][jn], f.b[6][jn], f.b[7][jn]}, bp[jn]);
+        acc[0][jn] = mfma_split6(ap, bp[jn], acc[0][jn]);
+      }
+#pragma unroll
+      for (int i = 1; i < RM; ++i) {
+        sa(i);
+#pragma unroll
+        for (int jn = 0; jn < RN; ++jn) acc[i][jn] = mfma_split6(ap, bp[jn], acc[i][jn]);
+      }
+    };
+    ring_loop_keep<PW, NS>(tend - s0, smem, SLOT, issue, load_s, mma_s);
+  }
+  float* o = ws + (int64_t)split * a.M * ngt + tap * CC + wc0 + col16;
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) o[(int64_t)(i * 16 + rq + jj) * ngt + j * 16] = acc[i][j][jj];
+}
+
+// Split-fp32 WGRAD with a cooperative split (BM = 128: 2 x 4 waves of 64 x BN / 4).  In the
+// DMA-ring kernels every wave splits its own A rows and B columns, so each value is split by the
+// BN / WN (A) or BM / WM (B) waves that share it: 64 values per lane per K-step of 128 x 256,
+// ~5.5 VALU instructions each, more vector issue than the step's 96 MFMAs leave free.  Here each
+// value is split once: a K-step's A and B values are loaded straight into registers (one step
+// ahead, plain buffer loads, zero outside the tensor), split by the lane that loaded them and
+// written to LDS as three bf16 planes in the MFMA fragment layout ([plane][16-row block][lane]
+// [8 k-values]: a wave's fragment is one conflict-free ds_read_b128), double-buffered behind one
+// barrier per step.  (BM + BN) / 64 half-blocks of 4 values per lane: 24 values per lane per
+// step of 128 x 256.  Same K order, arithmetic and partial slots as wgrad_f32_kernel<SPL>.
+template <int BM, int BN, bool SP>
+__global__ void __launch_bounds__(RT) wgrad_coop_kernel(ConvArgs a, float* __restrict__ ws, int ngt) {
+  constexpr int KI = 32;
+  constexpr int WGM = BM / 64, WGN = 8 / WGM;
+  constexpr int WM = BM / WGM, WN = BN / WGN, RM = WM / 16, RN = WN / 16;
+  static_assert(BM == 128 && WN >= 16, "128-row tiles, wave tiles of >= 16 columns");
+  constexpr int NBA = BM / 16, NB = (BM + BN) / 16;            // 16-row blocks: A's, A's and B's
+  constexpr int NH = NB * 2 / 8, NHA = NBA * 2 / 8;             // half-blocks per wave (A's first)
+  static_assert(NB * 2 % 8 == 0 && NBA * 2 % 8 == 0, "half-blocks split evenly over 8 waves");
+  constexpr int PLANE = NB * 1024, PBUF = 3 * PLANE;
+  __shared__ __attribute__((aligned(16))) char smem[2 * PBUF];
+  const es_conv_desc_t& d = a.d;
+  const SubPixel& sp = a.sp;
+  const int G = (d.N + KI - 1) / KI;
+
+  const int mt = gridDim.x, ntl = gridDim.y, tiles = mt * ntl;
+  const int orig = blockIdx.x + (blockIdx.y + blockIdx.z * ntl) * mt;
+  const int wg = xcd_remap(orig, tiles * gridDim.z);
+  const int tile = wg % tiles, split = wg / tiles;
+  const int m0 = (tile % mt) * BM, n0 = (tile / mt) * BN;
+  const int rs = n0 / d.C, cb = n0 - rs * d.C;
+  int cls = 0, tr, ts, gq, npix;
+  if constexpr (SP) {
+    cls = (rs >= sp.tap0[1]) + (rs >= sp.tap0[2]) + (rs >= sp.tap0[3]);
+    const int de = rs - sp.tap0[cls];
+    tr = de / sp.dw[cls];
+    ts = de - tr * sp.dw[cls];
+    gq = sp.pw[cls];
+    npix = sp.ph[cls] * gq;
+  } else {
+    tr = rs / d.S;
+    ts = rs - tr * d.S;
+    gq = d.Q;
+    npix = d.P * d.Q;
+  }
+  const int tbeg = min(split * a.k_per_split, npix * G);
+  const int tend = min(npix * G, tbeg + a.k_per_split);
+
+  const int lane = threadIdx.x & 63, wid = uni(threadIdx.x >> 6);
+  const int wm0 = (wid / WGN) * WM, wn0 = (wid % WGN) * WN;
+  const int col16 = lane & 15, rq = (lane >> 4) * 4, kl = lane >> 4;
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (tbeg < tend) {
+    const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * 4));
+    const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)(d.N * a.bs[0] * 4));
+    const int as0b = (int)a.as[0] * 4, as2b = (int)a.as[2] * 4, as3b = (int)a.as[3] * 4;
+    const int bs0b = (int)a.bs[0] * 4, bs2b = (int)a.bs[2] * 4, bs3b = (int)a.bs[3] * 4;
+    // half-block h of this wave: block b = (8 h + wid) / 2, k-half hh = wid & 1 (images
+    // 4 (4 hh + jj) + kl, jj = 0..3, of the step), row / column 16 b + col16 of the tile
+    uint32_t lofs[NH];
+    int wofs[NH];   // LDS byte offset of the lane's 8 bytes in plane 0
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      const int hb = 8 * h + wid, b = hb >> 1, hh = hb & 1;
+      if (h < NHA) lofs[h] = (uint32_t)((16 * hh + kl) * as0b + (m0 + 16 * b + col16) * 4);
+      else lofs[h] = (uint32_t)((16 * hh + kl) * bs0b + (cb + 16 * (b - NBA) + col16) * 4);
+      wofs[h] = b * 1024 + lane * 16 + hh * 8;
+    }
+    int cp, cq, cg;
+    {
+      const int pix = tbeg / G;
+      cg = tbeg - pix * G;
+      cp = pix / gq;
+      cq = pix - cp * gq;
+    }
+    int cstep = tbeg;
+    const int cp0 = SP ? uni(sp.p0[cls]) : 0, cq0 = SP ? uni(sp.q0[cls]) : 0;
+    const int coh = SP ? uni(sp.oh[cls]) : 0, cow = SP ? uni(sp.ow[cls]) : 0;
+    typedef float Stage[NH][4];
+    auto load = [&](Stage& v) {   // the next K-step's values (zero past tend or outside the tensor)
+      const bool live = cstep < tend;
+      uint32_t ua, ub;
+      if constexpr (SP) {
+        ua = live ? (uint32_t)(cg * KI * as0b + (cp0 + 2 * cp) * as2b + (cq0 + 2 * cq) * as3b) : OOB;
+        const int hs = cp + coh + tr, wsx = cq + cow + ts;
+        const bool ok = live && (unsigned)hs < (unsigned)d.H && (unsigned)wsx < (unsigned)d.W;
+        ub = ok ? (uint32_t)(cg * KI * bs0b + hs * bs2b + wsx * bs3b) : OOB;
+      } else {
+        ua = live ? (uint32_t)(cg * KI * as0b + cp * as2b + cq * as3b) : OOB;
+        const int hu = cp * d.stride - d.pad + tr, wu = cq * d.stride - d.pad + ts;
+        const bool ok = live && (unsigned)hu < (unsigned)d.Hu && (unsigned)wu < (unsigned)d.Wu;
+        ub = ok ? (uint32_t)(cg * KI * bs0b + fdiv(hu, a.fUh) * bs2b + fdiv(wu, a.fUw) * bs3b) : OOB;
+      }
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const uint32_t o = h < NHA ? ua + lofs[h] + jj * 4 * as0b : ub + lofs[h] + jj * 4 * bs0b;
+          v[h][jj] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(h < NHA ? ares : bres,
+                                                                                   (int)o, 0, 0));
+        }
+      ++cstep;
+      ++cg;
+      const bool w1 = cg == G;
+      cg = w1 ? 0 : cg;
+      cq += w1;
+      const bool w2 = cq == gq;
+      cq = w2 ? 0 : cq;
+      cp += w2;
+    };
+    auto store = [&](const Stage& v, char* pb) {   // split and write the three planes
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        uint32_t h0, m0_, l0, h1, m1, l1;
+        split_pair(v[h][0], v[h][1], h0, m0_, l0);
+        split_pair(v[h][2], v[h][3], h1, m1, l1);
+        *(uint2*)(pb + wofs[h]) = uint2{h0, h1};
+        *(uint2*)(pb + PLANE + wofs[h]) = uint2{m0_, m1};
+        *(uint2*)(pb + 2 * PLANE + wofs[h]) = uint2{l0, l1};
+      }
+    };
+    auto compute = [&](const char* pb) {
+      const char* q = pb + lane * 16;
+      bf16x8 ap[3], bp[RN][3];
+#pragma unroll
+      for (int jn = 0; jn < RN; ++jn)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) bp[jn][p] = *(const bf16x8*)(q + p * PLANE + (NBA + wn0 / 16 + jn) * 1024);
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p) ap[p] = *(const bf16x8*)(q + p * PLANE + (wm0 / 16 + i) * 1024);
+#pragma unroll
+        for (int jn = 0; jn < RN; ++jn) acc[i][jn] = mfma_split6(ap, bp[jn], acc[i][jn]);
+      }
+    };
+    auto sync = [] {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      ring_barrier();
+    };
+    Stage s0;
+    const int nk = tend - tbeg;
+#if ES_COOP2
+    Stage s1;
+    load(s1);
+    load(s0);
+    store(s1, smem);
+#else
+    load(s0);
+    store(s0, smem);
+#endif
+    sync();
+#if ES_COOP2
+    for (int t = 0; t < nk; t += 2) {
+      load(s1);                 // step t + 2
+      __builtin_amdgcn_sched_barrier(0);
+      compute(smem);            // step t
+      store(s0, smem + PBUF);   // step t + 1
+      sync();
+      if (t + 1 >= nk) break;
+      load(s0);                 // step t + 3
+      __builtin_amdgcn_sched_barrier(0);
+      compute(smem + PBUF);     // step t + 1
+      store(s1, smem);          // step t + 2
+      sync();
+    }
+#else
+    // one stage of registers: step t + 1's loads are issued before step t's MFMAs and split after
+    // them (two stages, 24 more registers, spill at 128 x 256)
+    for (int t = 0; t < nk; ++t) {
+      char* cur = smem + (t & 1) * PBUF;
+      char* nxt = smem + ((t & 1) ^ 1) * PBUF;
+      load(s0);                 // step t + 1
+      asm volatile("" ::: "memory");
+      compute(cur);             // step t
+      store(s0, nxt);           // step t + 1 (its buffer was last read in step t - 1)
+      sync();
+    }
+#endif
+    wait_vmcnt<0>();
+  }
   float* o = ws + ((int64_t)split * a.M + m0 + wm0) * ngt + n0 + wn0 + col16;
 #pragma unroll
   for (int i = 0; i < RM; ++i)
@@ -2709,6 +3117,9 @@ int env_int(const char* name, int def) {
   return e ? atoi(e) : def;
 }
 int g_f32_split = env_int("ES_F32_SPLIT", 0);
+int g_wgrad_col = env_int("ES_WGRAD_COL", 1);       // wgrad_f32_col_kernel for conv_layers.9-shaped WGRAD
+int g_wgrad_coop = env_int("ES_WGRAD_COOP", 1);     // wgrad_coop_kernel for 128-row split WGRAD tiles
+int g_wgrad_bn128 = env_int("ES_WGRAD_BN128", 0);   // split WGRAD: 128 x 128 tiles where 128 x 256 fit
 // split-fp32 kernels: static s_setprio 1 for waves 4-7 (ES_SPL_PRIO=0 off; A/B)
 int g_spl_prio = env_int("ES_SPL_PRIO", 1);
 // images per launch: equal chunks (whole 64-image groups where the limit allows) below the limit
@@ -2761,7 +3172,7 @@ int es_conv_ring_launch_f32(ConvArgs& a, int mode, hipStream_t st) {
 
 // WGRAD plan of the deterministic fp32 ring kernel: tile, image chunks, K splits per chunk
 struct WgF32Plan {
-  int bm, bn, sp, nc, nchunks, sc, ngt;
+  int bm, bn, sp, col, nc, nchunks, sc, ngt;
   SubPixel spg;
 };
 static bool wgrad_f32_plan(const es_conv_desc_t& d, const int64_t ys[4], const int64_t xs[4], WgF32Plan& p) {
@@ -2772,8 +3183,13 @@ static bool wgrad_f32_plan(const es_conv_desc_t& d, const int64_t ys[4], const i
   if (!dense(ys, d.K, d.P, d.Q) || !dense(xs, d.C, d.H, d.W)) return false;
   if (d.K % 64 || d.C % 64) return false;
   p.bm = d.K % 128 == 0 ? 128 : 64;
-  p.bn = d.C % 256 == 0 && p.bm == 128 ? 256 : (d.C % 128 == 0 ? 128 : 64);
+  p.bn = d.C % 256 == 0 && p.bm == 128 && !(g_f32_split && g_wgrad_bn128) ? 256 : (d.C % 128 == 0 ? 128 : 64);
+  // split-fp32 with 64 output channels: 64 x 512 tiles (8 waves of 64 x 64, the per-wave shape of the
+  // 128 x 256 tiles; 64 x 128 tiles make the in-kernel split VALU-bound)
   p.sp = !g_subpixel_off && d.up_h == 2 && d.up_w == 2 && d.stride == 1;
+  if (g_f32_split && p.bm == 64 && !p.sp && (d.R * d.S * d.C) % 512 == 0) p.bn = 512;
+  p.col = g_f32_split && g_wgrad_col && !p.sp && d.R == 2 && d.S == 2 && d.stride == 1 && d.Hu == d.H &&
+          d.Wu == d.W && d.C == 128 && d.K == 64;
   p.spg = SubPixel{};
   int npix = d.P * d.Q, taps = d.R * d.S;
   if (p.sp) {
@@ -2822,14 +3238,32 @@ int es_wgrad_f32_ring(const es_conv_desc_t& d, const void* dy, const int64_t ys[
     a.sp = p.spg;
     int npix = d.P * d.Q;
     if (p.sp) { npix = 0; for (int c = 0; c < 4; ++c) npix = std::max(npix, p.spg.ph[c] * p.spg.pw[c]); }
-    const int ks = npix * ((a.d.N + 31) / 32);
+    const int ks = p.col ? d.P * (d.Q + 1) * ((a.d.N + 31) / 32) : npix * ((a.d.N + 31) / 32);
     a.k_per_split = (ks + p.sc - 1) / p.sc;
     float* wsc = ws + (int64_t)ch * p.sc * d.K * p.ngt;
     dim3 grid(d.K / p.bm, p.ngt / p.bn, p.sc);
+    if (p.col) {
+      ++g_conv_launches;
+      hipLaunchKernelGGL(wgrad_f32_col_kernel, grid, dim3(RT), 0, st, a, wsc, p.ngt);
+      continue;
+    }
+    if (g_f32_split && g_wgrad_coop && p.bm == 128) {
+      ++g_conv_launches;
+#define ES_WC(BN)                                                                                          \
+  do {                                                                                                     \
+    if (p.sp) hipLaunchKernelGGL((wgrad_coop_kernel<128, BN, true>), grid, dim3(RT), 0, st, a, wsc, p.ngt); \
+    else hipLaunchKernelGGL((wgrad_coop_kernel<128, BN, false>), grid, dim3(RT), 0, st, a, wsc, p.ngt);     \
+  } while (0)
+      if (p.bn == 256) ES_WC(256);
+      else if (p.bn == 128) ES_WC(128);
+      else ES_WC(64);
+#undef ES_WC
+      continue;
+    }
 #define ES_WF(BM, BN)                                                                                 \
   do {                                                                                                \
     ++g_conv_launches;                                                                                \
-    if (g_f32_split && BM == 128) {  /* (64-row tiles: the split is VALU-bound there, measured  */    \
+    if (g_f32_split && (BM == 128 || BN == 512)) {  /* (64 x 128 tiles: VALU-bound split,      */    \
                                       /*  1.59 ms vs 1.41 exact for conv_layers.9 at B = 1024)   */    \
       if (p.sp) hipLaunchKernelGGL((wgrad_f32_kernel<BM, BN, true, true>), grid, dim3(RT), 0, st, a, wsc, p.ngt); \
       else hipLaunchKernelGGL((wgrad_f32_kernel<BM, BN, false, true>), grid, dim3(RT), 0, st, a, wsc, p.ngt);    \
@@ -2839,6 +3273,10 @@ int es_wgrad_f32_ring(const es_conv_desc_t& d, const void* dy, const int64_t ys[
     if (p.bm == 128 && p.bn == 256) ES_WF(128, 256);
     else if (p.bm == 128 && p.bn == 128) ES_WF(128, 128);
     else if (p.bm == 128) ES_WF(128, 64);
+    else if (p.bn == 512) {   // (planned for split-fp32 without sub-pixel classes only)
+      ++g_conv_launches;
+      hipLaunchKernelGGL((wgrad_f32_kernel<64, 512, false, true>), grid, dim3(RT), 0, st, a, wsc, p.ngt);
+    }
     else if (p.bn == 128) ES_WF(64, 128);
     else ES_WF(64, 64);
 #undef ES_WF

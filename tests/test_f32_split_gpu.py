@@ -39,7 +39,12 @@ def _both(case, seed):
     return ref, exact, split
 
 
-@pytest.mark.parametrize("case", CASES)
+# 64 output channels, taps x C a multiple of 512 without sub-pixel classes: the 64 x 512 split WGRAD
+# tiles, whose B lanes carry taps of their own (pad 1: boundary taps masked per lane)
+MT_CASES = [(9, 128, 20, 12, 64, 2, 1, 1, None), (7, 64, 11, 9, 64, 4, 2, 1, None)]
+
+
+@pytest.mark.parametrize("case", CASES + MT_CASES)
 def test_split_matches_fp64(case, det):
     _hip()
     ref, exact, split = _both(case, 0)
