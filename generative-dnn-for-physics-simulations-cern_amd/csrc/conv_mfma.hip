@@ -2468,6 +2468,162 @@ __global__ void __launch_bounds__(RT) wgrad_f32_col_kernel(ConvArgs a, float* __
       for (int j = 0; j < RN; ++j) o[(int64_t)(i * 16 + rq + jj) * ngt + j * 16] = acc[i][j][jj];
 }
 
+// wgrad_f32_col_kernel with dy split once per workgroup: the 8 waves share the tile's 64 dy rows,
+// so instead of every wave splitting all of them (32 of a lane's 64 split values per step), dy is
+// buffer-loaded into registers one step ahead (4 values per lane), split by the loading lane and
+// written to LDS as bf16 planes in the fragment layout (as wgrad_coop_kernel), double-buffered; the
+// x columns keep the DMA ring (32 KiB slots, two steps ahead, the previous slot kept).
+__global__ void __launch_bounds__(RT) wgrad_f32_col2_kernel(ConvArgs a, float* __restrict__ ws, int ngt) {
+  constexpr int KI = 32, CC = 128;
+  constexpr int RM = 4, RN = 4;
+  constexpr int SLOT = KI * 2 * CC * 4;                        // x: 32 images x 2 rows x 128 channels
+  constexpr int NS = 4, BPW = 4;
+  constexpr int APL = 4 * 1024, ABUF = 3 * APL;                // dy planes [plane][block][lane][8 k]
+  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT + 2 * ABUF];
+  char* const abase = smem + NS * SLOT;
+  const es_conv_desc_t& d = a.d;
+  const int G = (d.N + KI - 1) / KI, Q1 = d.Q + 1;
+  const int split = xcd_remap(blockIdx.z, gridDim.z);
+  const int nst = G * d.P * Q1;
+  const int tbeg = min(split * a.k_per_split, nst), tend = min(nst, tbeg + a.k_per_split);
+
+  const int lane = threadIdx.x & 63, wid = uni(threadIdx.x >> 6);
+  const int tap = wid >> 1, wtr = tap >> 1, wts = tap & 1, wc0 = (wid & 1) * 64;
+  const int col16 = lane & 15, rq = (lane >> 4) * 4, kl = lane >> 4;
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (tbeg < tend) {
+    const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * 4));
+    const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)(d.N * a.bs[0] * 4));
+    const int as0b = (int)a.as[0] * 4, as2b = (int)a.as[2] * 4, as3b = (int)a.as[3] * 4;
+    const int bs0b = (int)a.bs[0] * 4, bs2b = (int)a.bs[2] * 4, bs3b = (int)a.bs[3] * 4;
+    // dy half-block of this wave: rows 16 (wid >> 1) + col16, images 4 (4 (wid & 1) + jj) + kl
+    const uint32_t alo = (uint32_t)((16 * (wid & 1) + kl) * as0b + (16 * (wid >> 1) + col16) * 4);
+    const int awo = (wid >> 1) * 1024 + lane * 16 + (wid & 1) * 8;
+    uint32_t blane[BPW];
+    const int ltr = lane >> 5;
+#pragma unroll
+    for (int j = 0; j < BPW; ++j) {
+      const int kr = wid * BPW + j;
+      blane[j] = (uint32_t)(kr * bs0b + (((lane ^ ((kr & 1) << 2)) & 31) * 4) * 4);
+    }
+    int cg, cp, cj;
+    {
+      cg = tbeg / (d.P * Q1);
+      const int r = tbeg - cg * d.P * Q1;
+      cp = r / Q1;
+      cj = r - cp * Q1;
+    }
+    const int s0 = tbeg - (cj > 0);
+    cj -= cj > 0;
+    int bstep = s0, bg = cg, bpr = cp, bj = cj;                 // DMA side (two steps ahead)
+    int astep = s0, ag = cg, apr = cp, aj = cj;                 // dy side (one step ahead)
+    {
+      float4* z = (float4*)(smem + (NS - 1) * SLOT);
+      for (int i = threadIdx.x; i < SLOT / 16; i += RT) z[i] = float4{0.f, 0.f, 0.f, 0.f};
+    }
+    auto adv = [&](int& st, int& g, int& pr, int& j) {
+      ++st;
+      ++j;
+      const bool w1 = j == Q1;
+      j = w1 ? 0 : j;
+      pr += w1;
+      const bool w2 = pr == d.P;
+      pr = w2 ? 0 : pr;
+      g += w2;
+    };
+    auto issue_b = [&](char* slot) {
+      const int hu = bpr - d.pad + ltr, wu = bj - d.pad;
+      const bool ok = bstep < tend && (unsigned)hu < (unsigned)d.H && (unsigned)wu < (unsigned)d.W;
+      const uint32_t ub = ok ? (uint32_t)(bg * KI * bs0b + hu * bs2b + wu * bs3b) : OOB;
+#pragma unroll
+      for (int j = 0; j < BPW; ++j) bdma16(bres, blane[j] + ub, slot + (wid * BPW + j) * 1024);
+      adv(bstep, bg, bpr, bj);
+    };
+    auto load_a = [&](float (&v)[4]) {   // zero on a row's first column and on a reloaded column
+      const uint32_t ua = astep < tend && aj > 0 && astep >= tbeg
+                              ? (uint32_t)(ag * KI * as0b + apr * as2b + (aj - 1) * as3b) : OOB;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        v[jj] = __builtin_bit_cast(float,
+                                   __builtin_amdgcn_raw_buffer_load_b32(ares, (int)(ua + alo + jj * 4 * as0b), 0, 0));
+      adv(astep, ag, apr, aj);
+    };
+    auto store_a = [&](const float (&v)[4], char* pb) {
+      uint32_t h0, m0_, l0, h1, m1, l1;
+      split_pair(v[0], v[1], h0, m0_, l0);
+      split_pair(v[2], v[3], h1, m1, l1);
+      *(uint2*)(pb + awo) = uint2{h0, h1};
+      *(uint2*)(pb + APL + awo) = uint2{m0_, m1};
+      *(uint2*)(pb + 2 * APL + awo) = uint2{l0, l1};
+    };
+    const int sw = (kl & 1) * 64;
+    const int ob0 = kl * 2 * CC * 4 + (wtr * CC + wc0 + col16) * 4 + sw, ob1 = ob0 - 2 * sw;
+    auto compute = [&](const char* slot, const char* prev, const char* pa) {
+      const char* bimg = wts ? slot : prev;
+      const char* pb[2] = {bimg + ob0, bimg + ob1};
+      float fb[8][RN];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int jn = 0; jn < RN; ++jn) fb[j][jn] = *(const float*)(pb[jn & 1] + j * 4 * 2 * CC * 4 + 64 * jn);
+      bf16x8 bp[RN][3], ap[3];
+      const char* q = pa + lane * 16;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) ap[p] = *(const bf16x8*)(q + p * APL);
+#pragma unroll
+      for (int jn = 0; jn < RN; ++jn) {
+        split8(f32x4{fb[0][jn], fb[1][jn], fb[2][jn], fb[3][jn]}, f32x4{fb[4][jn], fb[5][jn], fb[6][jn], fb[7][jn]},
+               bp[jn]);
+        acc[0][jn] = mfma_split6(ap, bp[jn], acc[0][jn]);
+      }
+#pragma unroll
+      for (int i = 1; i < RM; ++i) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p) ap[p] = *(const bf16x8*)(q + p * APL + i * 1024);
+#pragma unroll
+        for (int jn = 0; jn < RN; ++jn) acc[i][jn] = mfma_split6(ap, bp[jn], acc[i][jn]);
+      }
+    };
+    float av[4];
+    load_a(av);                       // dy of the first step
+    asm volatile("" ::: "memory");
+    issue_b(smem);                    // x of the first two steps
+    issue_b(smem + SLOT);
+    store_a(av, abase);
+    int cur = 0, prv = NS - 1, nxt = 2;
+    const int nk = tend - s0;
+    // (the x DMA of step t + 2 is issued after the dy planes are written: hipcc makes an LDS store
+    // wait for every LDS-DMA in flight, vmcnt(0), which would otherwise drain it one step early)
+    for (int t = 0; t < nk; ++t) {
+      wait_vmcnt<BPW>();                                   // x of step t landed
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // dy planes of step t written, step t-1 read
+      ring_barrier();
+      load_a(av);                                          // dy of step t + 1
+      asm volatile("" ::: "memory");
+      compute(smem + cur * SLOT, smem + prv * SLOT, abase + (t & 1) * ABUF);
+      store_a(av, abase + ((t & 1) ^ 1) * ABUF);           // (last read in step t - 1)
+      asm volatile("" ::: "memory");
+      issue_b(smem + nxt * SLOT);                          // x of step t + 2 (step t-2's slot)
+      prv = cur;
+      cur = cur == NS - 1 ? 0 : cur + 1;
+      nxt = nxt == NS - 1 ? 0 : nxt + 1;
+    }
+    wait_vmcnt<0>();
+  }
+  float* o = ws + (int64_t)split * a.M * ngt + tap * CC + wc0 + col16;
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) o[(int64_t)(i * 16 + rq + jj) * ngt + j * 16] = acc[i][j][jj];
+}
+
 // Split-fp32 WGRAD with a cooperative split (BM = 128: 2 x 4 waves of 64 x BN / 4).  In the
 // DMA-ring kernels every wave splits its own A rows and B columns, so each value is split by the
 // BN / WN (A) or BM / WM (B) waves that share it: 64 values per lane per K-step of 128 x 256,
@@ -2665,39 +2821,56 @@ __global__ void __launch_bounds__(RT) wgrad_coop_kernel(ConvArgs a, float* __res
 
 // dW (torch layout [K][C][R][S], fp32) = beta * dW + sum over the splits of the partials
 // ws[split][K][taps * C]; SP: original tap (r, s) sums the four classes' combined taps
-// (d, e) = ((r + a) >> 1, (s + b) >> 1) of class (a, b).  Fixed summation order: split, then class.
-// One thread per (k, r, s, c), c fastest: the partial reads are coalesced, and every thread's
-// splits x classes loads are independent (a thread per (k, c) looping over the taps was latency
-// bound: 174 us for conv_layers.5's 32 splits).
+// (d, e) = ((r + a) >> 1, (s + b) >> 1) of class (a, b).  A workgroup takes 32 consecutive outputs
+// (c fastest: coalesced partial reads) x 8 split lanes; lane q sums splits q, q + 8, ... (classes
+// innermost) and lane 0 adds the 8 lane sums in order: a fixed summation order, so reruns are bitwise
+// equal.  (One thread per output looping over all splits was latency bound: 166 us for
+// conv_layers.9's 512 splits.)
+constexpr int WR_LANES = 8;
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int K, int C,
                                                            int R, int S, int ngt, SubPixel sp, float* __restrict__ dw,
                                                            float beta) {
+  __shared__ float part[WR_LANES][32];
   const int64_t n = (int64_t)K * R * S * C;
   const int64_t zst = (int64_t)K * ngt;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    int64_t t = i / C;
-    const int s = (int)(t % S);
-    t /= S;
-    const int r = (int)(t % R);
-    const int k = (int)(t / R);
-    const float* p = ws + (int64_t)k * ngt + c;
+  const int o = threadIdx.x & 31, q = threadIdx.x >> 5;
+  for (int64_t i0 = blockIdx.x * (int64_t)32; i0 < n; i0 += (int64_t)gridDim.x * 32) {
+    const int64_t i = i0 + o;
     float v = 0.f;
-    if (sp.on) {
-      int off[4];
+    int k = 0, r = 0, s = 0, c = 0;
+    if (i < n) {
+      c = (int)(i % C);
+      int64_t t = i / C;
+      s = (int)(t % S);
+      t /= S;
+      r = (int)(t % R);
+      k = (int)(t / R);
+      const float* p = ws + (int64_t)k * ngt + c + q * zst;
+      if (sp.on) {
+        int off[4];
 #pragma unroll
-      for (int cl = 0; cl < 4; ++cl)
-        off[cl] = (sp.tap0[cl] + ((r + (cl >> 1)) >> 1) * sp.dw[cl] + ((s + (cl & 1)) >> 1)) * C;
-      for (int z = 0; z < splits; ++z, p += zst) {
+        for (int cl = 0; cl < 4; ++cl)
+          off[cl] = (sp.tap0[cl] + ((r + (cl >> 1)) >> 1) * sp.dw[cl] + ((s + (cl & 1)) >> 1)) * C;
+        for (int z = q; z < splits; z += WR_LANES, p += WR_LANES * zst) {
 #pragma unroll
-        for (int cl = 0; cl < 4; ++cl) v += p[off[cl]];
+          for (int cl = 0; cl < 4; ++cl) v += p[off[cl]];
+        }
+      } else {
+        const int off = (r * S + s) * C;
+#pragma unroll 4
+        for (int z = q; z < splits; z += WR_LANES, p += WR_LANES * zst) v += p[off];
       }
-    } else {
-      const int off = (r * S + s) * C;
-      for (int z = 0; z < splits; ++z, p += zst) v += p[off];
     }
-    float* g = dw + (((int64_t)k * C + c) * R + r) * S + s;
-    *g = (beta != 0.f ? beta * *g : 0.f) + v;
+    part[q][o] = v;
+    __syncthreads();
+    if (q == 0 && i < n) {
+      float u = part[0][o];
+#pragma unroll
+      for (int l = 1; l < WR_LANES; ++l) u += part[l][o];
+      float* g = dw + (((int64_t)k * C + c) * R + r) * S + s;
+      *g = (beta != 0.f ? beta * *g : 0.f) + u;
+    }
+    __syncthreads();
   }
 }
 
@@ -3117,7 +3290,7 @@ int env_int(const char* name, int def) {
   return e ? atoi(e) : def;
 }
 int g_f32_split = env_int("ES_F32_SPLIT", 0);
-int g_wgrad_col = env_int("ES_WGRAD_COL", 1);       // wgrad_f32_col_kernel for conv_layers.9-shaped WGRAD
+int g_wgrad_col = env_int("ES_WGRAD_COL", 1);       // conv_layers.9-shaped WGRAD: 1 col2, 2 col kernel
 int g_wgrad_coop = env_int("ES_WGRAD_COOP", 1);     // wgrad_coop_kernel for 128-row split WGRAD tiles
 int g_wgrad_bn128 = env_int("ES_WGRAD_BN128", 0);   // split WGRAD: 128 x 128 tiles where 128 x 256 fit
 // split-fp32 kernels: static s_setprio 1 for waves 4-7 (ES_SPL_PRIO=0 off; A/B)
@@ -3244,7 +3417,8 @@ int es_wgrad_f32_ring(const es_conv_desc_t& d, const void* dy, const int64_t ys[
     dim3 grid(d.K / p.bm, p.ngt / p.bn, p.sc);
     if (p.col) {
       ++g_conv_launches;
-      hipLaunchKernelGGL(wgrad_f32_col_kernel, grid, dim3(RT), 0, st, a, wsc, p.ngt);
+      if (g_wgrad_col == 2) hipLaunchKernelGGL(wgrad_f32_col_kernel, grid, dim3(RT), 0, st, a, wsc, p.ngt);
+      else hipLaunchKernelGGL(wgrad_f32_col2_kernel, grid, dim3(RT), 0, st, a, wsc, p.ngt);
       continue;
     }
     if (g_f32_split && g_wgrad_coop && p.bm == 128) {
@@ -3282,7 +3456,7 @@ int es_wgrad_f32_ring(const es_conv_desc_t& d, const void* dy, const int64_t ys[
 #undef ES_WF
   }
   const int64_t n = (int64_t)d.K * d.C * d.R * d.S;
-  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 8192);
+  const int blocks = (int)std::min<int64_t>((n + 31) / 32, 16384);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, p.nchunks * p.sc, d.K, d.C, d.R,
                      d.S, p.ngt, p.spg, dw, beta);
   return 1;
@@ -3293,7 +3467,7 @@ int es_wgrad_f32_ring(const es_conv_desc_t& d, const void* dy, const int64_t ys[
 void es_wgrad_reduce_plain(const float* ws, int splits, int K, int C, int R, int S, float* dw, float beta,
                            hipStream_t st) {
   const int64_t n = (int64_t)K * C * R * S;
-  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 8192);
+  const int blocks = (int)std::min<int64_t>((n + 31) / 32, 16384);
   SubPixel none{};
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, splits, K, C, R, S, R * S * C, none,
                      dw, beta);

@@ -14,7 +14,7 @@ import sys
 LAYERS = {"c0": (128, 13, 13, 256, 24, 24, 3), "c5": (256, 24, 24, 128, 46, 46, 3),
           "c9": (128, 46, 46, 64, 45, 45, 2)}
 NAMES = {"fwd": ("conv_ring_kernel<0",), "dgrad": ("conv_ring_kernel<1",),
-         "wgrad": ("wgrad_f32_kernel", "wgrad_reduce_kernel")}
+         "wgrad": ("wgrad_f32_kernel", "wgrad_f32_col_kernel", "wgrad_f32_col2_kernel", "wgrad_coop_kernel", "wgrad_reduce_kernel")}
 
 
 def rows(d, counter, names):
