@@ -36,10 +36,13 @@ sys.path.insert(0, ROOT)
 # no reference model) 16.868 GFLOP = 6*2746.3 + 12*8.05 + 3*97.9 MFLOP (same counter on the oracle)
 STEP_FLOP_PER_IMAGE = {"neutron": 10.573e9, "proton": 28.566e9, "neutron56": 16.868e9}
 PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
-# split-fp32 (train.fp32_mfma: split): one fp32 product = 6 bf16 plane products on the 2.5 PF/s
-# dense bf16 MFMA, i.e. an fp32-product ceiling of 2500 / 6 TFLOP/s
+# split-fp32 (train.fp32_mfma: split): one fp32 product = 6 bf16 plane products, all executed on the
+# bf16 MFMA pipe, so the roofline of a split kernel is the EXECUTED bf16 work against the 2.5 PF/s
+# dense bf16 peak (no derived "split peak")
 SPLIT_PRODUCTS = 6
-PEAK_SPLIT = PEAK_TFLOPS["bf16"] / SPLIT_PRODUCTS
+# timed loop: at most this many replayed steps queued ahead of the GPU (a replay is ~1000 AQL packets;
+# an unbounded loop queued ~10.5k packets, which is where a profiled run aborted, profiles/r03t_*)
+MAX_INFLIGHT = 2
 IMAGE = {"neutron": "44x44", "proton": "56x30", "neutron56": "56x56"}
 
 
@@ -171,14 +174,21 @@ def cpu_baseline(arch, batches=(64, 512), budget_s=25.0):
 
 
 def timed(step, steps, world):
+    """K steps between barrier + synchronize; the host stays at most MAX_INFLIGHT steps ahead of the
+    GPU (it waits on the event of step i - MAX_INFLIGHT before issuing step i, which keeps the queue
+    fed: a step is ~45 ms of GPU work against ~1 ms of host issue)."""
     import torch
     import torch.distributed as dist
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    evs = [torch.cuda.Event() for _ in range(MAX_INFLIGHT)]
     t0 = time.perf_counter()
-    for _ in range(steps):
+    for i in range(steps):
+        if i >= MAX_INFLIGHT:
+            evs[i % MAX_INFLIGHT].synchronize()
         step()
+        evs[i % MAX_INFLIGHT].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -195,24 +205,52 @@ def make_step(moe, step_args, use_graph):
     return sg.replay, sg
 
 
+def exec_profile(arch, precision):
+    """(executed MACs / the reference's MACs, MFMA products per reference product, MFMA pipe) of the
+    roofline kernel, the generator's conv_layers.5: a x2-upsample 3x3 conv run as 4 parity-class
+    2x2 convs on the source grid (sub-pixel: 16 of 36 taps), bf16 or split-fp32 (6 bf16 plane products
+    per fp32 product) on the bf16 pipe, or exact fp32 MFMA; proton's conv_layers.5 (non-integer
+    resize) runs on the generic kernels without the sub-pixel reduction."""
+    ratio = 1.0 if arch == "proton" else SUBPIXEL_MAC_RATIO
+    split = precision == "fp32" and FP32_MFMA == "split" and arch != "proton"
+    if precision == "bf16":
+        return ratio, 1, "bf16"
+    return (ratio, SPLIT_PRODUCTS, "bf16") if split else (ratio, 1, "fp32")
+
+
+def exec_flops(reset=False):
+    """Host tally of the executed conv MFMA work (es_conv_exec_flops): [bf16 pipe, fp32 MFMA, VALU]."""
+    import ctypes
+    from expertsim import hip
+    out = (ctypes.c_double * 3)()
+    hip.call("es_conv_exec_flops", out, 1 if reset else 0)
+    return list(out)
+
+
 def probe_dominant(moe, eager_step, steps, arch, batch, precision):
     """Per-launch HIP events around the dominant conv's launches (on its launch stream) over
-    eager steps of the same model and batch -> the roofline object."""
+    eager steps of the same model and batch -> the roofline object; the same steps' executed conv
+    MFMA work (es_conv_exec_flops) -> the step's executed MFMA fraction."""
     import torch
     from expertsim import layers
     probe = layers.KernelProbe(["G0.c5.fwd", "G0.c5.dgrad", "G0.c5.wgrad"])
     layers.set_probe(probe)
+    exec_flops(reset=True)
     for _ in range(steps):
         eager_step()
     torch.cuda.synchronize()
+    ef = [v / steps for v in exec_flops(reset=True)]
     layers.set_probe(None)
     stats = probe.summary()
     flops = conv_flops_per_image(arch) * batch
     dom = max(stats, key=lambda k: stats[k]["total_ms"])
     avg_ms = stats[dom]["avg_ms"]
-    achieved = flops / (avg_ms * 1e-3) / 1e12
-    split = precision == "fp32" and FP32_MFMA == "split"
-    peak = PEAK_SPLIT if split else PEAK_TFLOPS[precision]
+    ratio, products, pipe = exec_profile(arch, precision)
+    exec_per_launch = flops * ratio * products
+    achieved = exec_per_launch / (avg_ms * 1e-3) / 1e12
+    alg_rate = flops / (avg_ms * 1e-3) / 1e12
+    split = products > 1
+    peak = PEAK_TFLOPS[pipe]
     traffic, tnote, mfma_busy = None, None, None
     tj_path = traffic_json(arch, batch, precision, dom.split(".")[-1])
     if tj_path:
@@ -221,26 +259,40 @@ def probe_dominant(moe, eager_step, steps, arch, batch, precision):
         mfma_busy = tj.get("mfma_busy_frac")
         tnote = (f"HBM bytes per op: FETCH_SIZE x2 {tj['fetch_bytes']} + WRITE_SIZE {tj['write_bytes']} "
                  f"(algorithmic {tj['algorithmic_bytes']}), {os.path.relpath(tj_path, ROOT)}")
-    executed = achieved * SUBPIXEL_MAC_RATIO if arch != "proton" else achieved
     kname = ("conv_ring bf16" if precision == "bf16" else
              "conv_ring split-fp32, 6 x v_mfma_f32_16x16x32_bf16 per fp32 product" if split else
              "conv_ring fp32, v_mfma_f32_16x16x4_f32")
     return {"bound": "mfma", "kernel": f"{dom} (generator conv_layers.5, {kname})",
             "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_note": tnote,
-            "frac_executed": round(executed / peak, 4),
-            "note": "achieved = the reference's (algorithmic) 3x3-conv FLOPs / kernel time; the sub-pixel "
-                    "decomposition executes 4/9 of those MACs, so frac_executed = MFMA work actually issued / peak"
-                    + ("; split-fp32 peak = 2500 TFLOP/s dense bf16 / 6 plane products per fp32 product "
-                       "(frac_executed x 6 = bf16 MFMA work issued / 2500)" if split else ""),
+            "achieved_fp32_equiv_alg": round(alg_rate, 2),
+            "note": f"achieved = EXECUTED MFMA FLOPs per launch ({exec_per_launch:.4g} = the reference's 3x3-conv "
+                    f"FLOPs {flops:.4g} x {ratio:.4f} sub-pixel MAC ratio x {products} MFMA products per "
+                    f"reference product) / kernel time, against the dense {pipe} MFMA peak {peak} TFLOP/s "
+                    "(MI355X_MICROARCH.md); achieved_fp32_equiv_alg = the reference's FLOPs / kernel time "
+                    "(an algorithmic rate, not a utilisation)",
             "mfma_busy_pmc": mfma_busy,
-            "flop_per_launch": flops, "avg_ms": round(avg_ms, 4), "launches": stats[dom]["count"],
+            "flop_per_launch": flops, "exec_flop_per_launch": exec_per_launch,
+            "avg_ms": round(avg_ms, 4), "launches": stats[dom]["count"],
+            "step_exec_flops": {"bf16_pipe": ef[0], "fp32_mfma": ef[1], "valu_thin": ef[2]},
             "kernel_launches_per_op": stats[dom].get("kernel_launches_per_op"),
             "launch_note": "avg_ms is per op; an fp32 op over > 1 GiB operands runs as image chunks "
                            "(kernel_launches_per_op MFMA kernels, rocprof lists each chunk separately)",
             "all_probed": {k: {"avg_ms": round(v["avg_ms"], 4), "kernels": v.get("kernel_launches_per_op"),
-                               "tflops": round(flops / (v["avg_ms"] * 1e-3) / 1e12, 2)}
+                               "exec_tflops": round(exec_per_launch / (v["avg_ms"] * 1e-3) / 1e12, 2),
+                               "frac": round(exec_per_launch / (v["avg_ms"] * 1e-3) / 1e12 / peak, 4)}
                            for k, v in stats.items()}}
+
+
+def step_exec_frac(roof, ms_per_step):
+    """Executed conv MFMA work of one step (es_conv_exec_flops over the probe's eager steps) at the
+    dense peaks of the pipes it ran on, as a fraction of the measured step time: the share of the step
+    the MFMA pipes would be busy if every conv ran at peak."""
+    if not roof or "step_exec_flops" not in roof:
+        return None
+    e = roof["step_exec_flops"]
+    t = e["bf16_pipe"] / (PEAK_TFLOPS["bf16"] * 1e12) + e["fp32_mfma"] / (PEAK_TFLOPS["fp32"] * 1e12)
+    return round(t / (ms_per_step * 1e-3), 4)
 
 
 def run_mode(args, precision, steps, warmup, dev, rank, world, ddp, probe_steps):
@@ -354,7 +406,7 @@ def main():
                                            3 if probe_steps else 0)
         other = {"dtype": other_p, "value": round(vo, 2), "unit": "images/s", "steps": args.other_steps,
                  "ms_per_step": round(dto / args.other_steps * 1e3, 3), "step_launch": launcho,
-                 "step_mfma_frac": round(STEP_FLOP_PER_IMAGE[args.arch] * vo / 1e12 / PEAK_TFLOPS[other_p], 4),
+                 "step_mfma_frac": step_exec_frac(roofo, dto / args.other_steps * 1e3),
                  "roofline": roofo,
                  "note": ("bf16 performance mode: bf16 GEMM operands, fp32 accumulation / statistics / "
                           "parameters; validated statistically (tests/test_bf16_stats_gpu.py)" if other_p == "bf16"
@@ -372,8 +424,11 @@ def main():
                        "arch": args.arch, "n_experts": args.experts, "batch_per_gpu": args.batch,
                        "global_batch": args.batch * world, "image": IMAGE[args.arch],
                        "parallelism": f"dp{world}", "sync_bn": bool(args.sync_bn) if ddp else None},
-            "step_tflops": round(step_flops / 1e12, 2),
-            "step_mfma_frac": round(step_flops / 1e12 / PEAK_TFLOPS[args.precision], 4),
+            "step_tflops_alg": round(step_flops / 1e12, 2),
+            "step_mfma_frac": step_exec_frac(roof, dt / args.steps * 1e3),
+            "step_mfma_frac_note": "executed conv MFMA FLOPs per step (bf16 pipe incl. split-fp32 plane products "
+                                   "at 2500 TF, exact fp32 MFMA at 157.3 TF) / step time; step_tflops_alg = the "
+                                   "reference's 10.573 GFLOP/image x images/s (an algorithmic rate)",
             "roofline": roof,
         }
         if args.precision == "fp32":
@@ -383,8 +438,8 @@ def main():
                 "pin this mode within 1e-4. "
                 + ("split-fp32 convs: each fp32 operand is the exact sum of three bf16 planes, the six plane "
                    "products with p + q <= 2 run on v_mfma_f32_16x16x32_bf16 into fresh fp32 accumulators that are "
-                   "added to the running sums with round-to-nearest (dropped terms < 2^-23 |a b| per product); "
-                   "step_mfma_frac is against the 157.3 TF fp32 MFMA peak" if FP32_MFMA == "split"
+                   "added to the running sums with round-to-nearest (dropped terms < 2^-23 |a b| per product)"
+                   if FP32_MFMA == "split"
                    else "exact fp32 MFMA (v_mfma_f32_16x16x4_f32)"))
         else:
             out["precision_note"] = "bf16 GEMM operands, fp32 accumulation"

@@ -110,6 +110,10 @@ struct StatsRequest {
 };
 extern thread_local StatsRequest g_stats_req;
 
+// which ring path the last conv launch took (host, per thread; es_conv_exec_flops accounting):
+// bit 0 a ring kernel ran, bit 1 split-fp32 planes, bit 2 the sub-pixel decomposition
+extern thread_local int g_ring_hit;
+
 // split-fp32 weight planes: byte offset of the planes behind an fp32 packing of n elements
 extern "C" int64_t es_weight_planes_offset(int64_t n);
 

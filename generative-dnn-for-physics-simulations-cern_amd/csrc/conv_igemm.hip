@@ -1037,6 +1037,37 @@ int ring_direct(ConvArgs& a, int mode, hipStream_t st, es_dtype_t dt) {
 
 }  // namespace
 
+// ---------------------------------------------------------------- executed-work tally (es_conv_exec_flops)
+thread_local int g_ring_hit = 0;
+namespace {
+double g_exec_flops[3] = {0.0, 0.0, 0.0};
+// RAII around one conv entry: classifies the path the call took and adds its executed FLOPs
+struct ExecTally {
+  const es_conv_desc_t* d;
+  es_dtype_t dt;
+  bool thin = false;
+  ExecTally(const es_conv_desc_t* d_, es_dtype_t dt_) : d(d_), dt(dt_) { g_ring_hit = 0; }
+  ~ExecTally() {
+    if (!d) return;
+    double f = 2.0 * d->N * d->P * d->Q * (double)d->K * d->C * d->R * d->S;
+    if (g_ring_hit & 4) f *= (double)es_subpixel_taps(d->R, d->S) / (4.0 * d->R * d->S);
+    if (thin) g_exec_flops[2] += f;
+    else if (dt == ES_BF16) g_exec_flops[0] += f;
+    else if (g_ring_hit & 2) g_exec_flops[0] += 6.0 * f;
+    else g_exec_flops[1] += f;
+  }
+};
+}  // namespace
+
+extern "C" int es_conv_exec_flops(double out[3], int reset) {
+  ES_CHECK_ARG(out != nullptr, "conv exec flops: NULL out");
+  for (int i = 0; i < 3; ++i) {
+    out[i] = g_exec_flops[i];
+    if (reset) g_exec_flops[i] = 0.0;
+  }
+  return ES_OK;
+}
+
 extern "C" int es_set_deterministic(int on) {
   const int old = g_es_det;
   g_es_det = on != 0;
@@ -1053,8 +1084,10 @@ extern "C" int es_conv2d_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void*
                              const int64_t xs[4], const void* wk, const float* bias, void* y,
                              es_dtype_t ydt, const int64_t ys[4], es_stream_t stream) {
   if (int e = check_desc(d)) return e;
+  ExecTally tally(d, dt);
   if (d->subpixel) ES_CHECK_ARG(es_conv_subpixel_ok(d, dt), "conv fwd: sub-pixel weights for a conv the sub-pixel path cannot run");
   if (es_thin_conv_fwd(d, dt, x, xs, wk, bias, y, ydt, ys, (hipStream_t)stream)) {
+    tally.thin = true;
     ES_CHECK_LAUNCH();
     return ES_OK;
   }
@@ -1086,8 +1119,10 @@ extern "C" int es_conv2d_dgrad(const es_conv_desc_t* d, es_dtype_t dt, const voi
                                const int64_t ys[4], const void* wd, void* dxu, es_dtype_t dxdt,
                                const int64_t dxs[4], float beta, es_stream_t stream) {
   if (int e = check_desc(d)) return e;
+  ExecTally tally(d, dt);
   if (d->subpixel) ES_CHECK_ARG(es_conv_subpixel_ok(d, dt), "conv dgrad: sub-pixel weights for a conv the sub-pixel path cannot run");
   if (es_thin_conv_dgrad(d, dt, dy, ys, wd, dxu, dxdt, dxs, beta, (hipStream_t)stream)) {
+    tally.thin = true;
     ES_CHECK_LAUNCH();
     return ES_OK;
   }
@@ -1126,7 +1161,9 @@ extern "C" int es_conv2d_wgrad(const es_conv_desc_t* d, es_dtype_t dt, const voi
                                const int64_t ys[4], const void* x, const int64_t xs[4], float* dw,
                                es_stream_t stream) {
   if (int e = check_desc(d)) return e;
+  ExecTally tally(d, dt);
   if (es_thin_conv_wgrad(d, dt, dy, ys, x, xs, dw, (hipStream_t)stream)) {
+    tally.thin = true;
     ES_CHECK_LAUNCH();
     return ES_OK;
   }
@@ -1171,6 +1208,7 @@ extern "C" int es_conv2d_wgrad_det(const es_conv_desc_t* d, es_dtype_t dt, const
                                    int64_t ws_bytes, es_stream_t stream) {
   if (int e = check_desc(d)) return e;
   ES_CHECK_ARG(dw && ws, "conv wgrad det: NULL dw / workspace");
+  ExecTally tally(d, dt);
   const hipStream_t st = (hipStream_t)stream;
   const int64_t floats = ws_bytes / (int64_t)sizeof(float);
   if (dt == ES_F32) {
@@ -1185,6 +1223,7 @@ extern "C" int es_conv2d_wgrad_det(const es_conv_desc_t* d, es_dtype_t dt, const
   ES_CHECK_ARG(floats >= per, "conv wgrad det: workspace below one partial");
   g_det_req = DetRequest{(float*)ws, floats, 0};
   int rc = es_thin_conv_wgrad(d, dt, dy, ys, x, xs, (float*)ws, st) ? ES_OK : -1;
+  tally.thin = rc == ES_OK;
   if (rc != ES_OK) {
     ConvArgs a{};
     a.d = *d; a.a_src = dy; a.b_src = x; a.out = ws;

@@ -3063,9 +3063,12 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
     else if (d.K == 64 && d.C % 128 == 0) ES_WG(64, 128);   // neutron G conv_layers.9 (128 -> 64)
     else return 0;
 #undef ES_WG
+    g_ring_hit = 1 | (sp ? 4 : 0);
     return 1;
   }
-  return ring_fd<bf16>(a, mode, st);
+  const int rc = ring_fd<bf16>(a, mode, st);
+  if (rc > 0) g_ring_hit = 1 | (sp_weights ? 4 : 0);
+  return rc;
 }
 
 // FWD / DGRAD ring launch for bf16 or fp32 operands (fp32: the parity mode's exact fp32 MFMA, or with
@@ -3340,6 +3343,7 @@ int es_conv_ring_launch_f32(ConvArgs& a, int mode, hipStream_t st) {
     }
   }
   g_stats_req = StatsRequest{req.part, req.floats, stats_ok ? used : 0};
+  g_ring_hit = 1 | (g_f32_split ? 2 : 0) | (d.subpixel ? 4 : 0);
   return 1;
 }
 
@@ -3459,6 +3463,7 @@ int es_wgrad_f32_ring(const es_conv_desc_t& d, const void* dy, const int64_t ys[
   const int blocks = (int)std::min<int64_t>((n + 31) / 32, 16384);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, p.nchunks * p.sc, d.K, d.C, d.R,
                      d.S, p.ngt, p.spg, dw, beta);
+  g_ring_hit = 1 | (g_f32_split ? 2 : 0) | (p.sp ? 4 : 0);
   return 1;
 }
 

@@ -1019,8 +1019,13 @@ extern "C" int es_norm_bwd_sync(int phase, const es_view_t* x, es_dtype_t xdt, c
     BwdApply ap{};
     ap.b = b; ap.dx = mkview(dx); ap.dxp = dxp; ap.dxbf = dxdt == ES_BF16; ap.beta = 0.f; ap.csum = dsum;
     ap.a1 = g1; ap.a2 = g2;
+    // deterministic mode: as in es_norm_act_bwd, the apply's float-atomic channel sums are replaced
+    // by an ordered column reduction of dx after the apply
+    if (g_es_det && dsum) ap.csum = nullptr;
     const int64_t total = (int64_t)x->n * x->c * x->h * x->w;
     hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(grid_for(total)), dim3(256), 0, st, ap);
+    ES_CHECK_LAUNCH();
+    if (g_es_det && dsum) return es_channel_sum(dx, dxdt, dxp, dsum, 1.f, part, stream);
   }
   ES_CHECK_LAUNCH();
   return ES_OK;

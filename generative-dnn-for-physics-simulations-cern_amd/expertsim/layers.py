@@ -179,24 +179,34 @@ def deterministic() -> bool:
 # (three bf16 planes per operand, six plane products on v_mfma_f32_16x16x32_bf16; es_conv_set_f32_split).
 # Level 2 (default when on): the packed weights carry their planes (es_pack_weight_planes), so the
 # FWD / DGRAD kernels split only the activations; ES_F32_SPLIT_LEVEL=1 splits both in the kernel.
+# The level the C side uses is the single source of truth: es_conv_set_f32_split clamps to {0, 1, 2}
+# and ES_F32_SPLIT may set it before any call from here, so the Python mirror is read back from C
+# (packing the weight planes must follow the level the kernels actually run).
 _F32_SPLIT = None
-_SPLIT_LEVEL = int(os.environ.get("ES_F32_SPLIT_LEVEL", "2"))
+_SPLIT_LEVEL = min(max(int(os.environ.get("ES_F32_SPLIT_LEVEL", "2")), 1), 2)
 
 
 def set_f32_split(on: bool):
     global _F32_SPLIT
     lvl = _SPLIT_LEVEL if on else 0
-    if lvl != _F32_SPLIT:
+    if lvl != f32_split_level():
         hip.lib().es_conv_set_f32_split(lvl)
-        _F32_SPLIT = lvl
+        _F32_SPLIT = None
+        f32_split_level()
 
 
 def f32_split() -> bool:
-    return bool(_F32_SPLIT)
+    return f32_split_level() > 0
 
 
 def f32_split_level() -> int:
-    return int(_F32_SPLIT or 0)
+    global _F32_SPLIT
+    if _F32_SPLIT is None:   # read the C level back (set returns the previous value)
+        lib = hip.lib()
+        cur = int(lib.es_conv_set_f32_split(0))
+        lib.es_conv_set_f32_split(cur)
+        _F32_SPLIT = cur
+    return _F32_SPLIT
 
 
 # --------------------------------------------------------------------------------- upsample

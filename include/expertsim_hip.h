@@ -194,6 +194,14 @@ int es_pack_weight_planes(const float* packed, int64_t n, void* base, es_stream_
 /* Host-side count of MFMA conv kernels issued so far (ring / persistent / p256 / fp32 WGRAD).
  * Instrumentation only: lets a profiler state how many kernel launches one conv op was. */
 int64_t es_conv_launch_count(void);
+/* Host-side tally of the MFMA work the conv entry points (es_conv2d_fwd / _dgrad / _wgrad /
+ * _wgrad_det and their _stats / _bnred / _det variants) issued, as executed FLOPs (2 per MAC):
+ * out[0] on the bf16 pipe (bf16 operands, and split-fp32: 6 plane products per fp32 product),
+ * out[1] on the fp32 MFMA (v_mfma_f32_16x16x4_f32), out[2] on the VALU (thin Cin/Cout = 1 convs).
+ * A sub-pixel conv counts its 4 parity-class convs (es_subpixel_taps / (4 R S) of the reference's
+ * MACs).  reset != 0 zeroes the tally after reading it.  Instrumentation only (bench.py's executed
+ * step MFMA fraction); the same products as neutron generator.py:23-35 / proton generator.py:26-38. */
+int es_conv_exec_flops(double out[3], int reset);
 
 /* Weight packing for the implicit GEMM (fp32 master [K][C][R][S] -> dt).
  * mode 0: out[k][r][s][c] = w*scale ; mode 1: out[c][r][s][k] = w*scale.

@@ -14,13 +14,13 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _build(seed=7):
+def _build(seed=7, precision="fp32"):
     from expertsim.config import inject_shared, load_config
     from expertsim.models import build_model
     from expertsim.models.moe import MoEWrapper
     from expertsim.train.training_setup import setup_optimizers
     cfg = inject_shared(load_config(overrides=["model.architecture=neutron", "model.n_experts=1",
-                                               "train.precision=fp32", f"train.rng_seed={seed}"]))
+                                               f"train.precision={precision}", f"train.rng_seed={seed}"]))
     torch.manual_seed(seed)
     parts = [build_model(f"neutron.{k}", getattr(cfg.model, k), DEV) for k in ("generator", "discriminator", "aux_reg")]
     router = build_model("router_v1", cfg.model.router, DEV)
@@ -137,3 +137,68 @@ def test_expert_graphs_late_expert(concurrent):
     assert sa == sb, (sa, sb)          # device step counters advanced by the replays
     diff = [n for n in pa if not torch.equal(pa[n], pb[n])]
     assert not diff, diff
+
+
+def _close_bf16(ma, mb, pa, pb, lr, steps):
+    """bf16 performance mode (float-atomic reductions, not bitwise reproducible): the replayed steps
+    track the eager ones within the round-2 tolerance -- metrics 1e-2 relative, every parameter within
+    k * lr of the eager run (Adam moves a parameter by <= ~lr per step)."""
+    for k in ma:
+        assert abs(ma[k] - mb[k]) <= 1e-2 * max(abs(ma[k]), 1e-2), (k, ma[k], mb[k])
+    for n in pa:
+        d = float((pa[n] - pb[n]).abs().max())
+        assert d <= 2 * lr * steps + 1e-6, (n, d)
+
+
+def test_graph_replay_tracks_eager_bf16():
+    """the whole-step capture of the bf16 performance mode (the bench's secondary line)."""
+    from expertsim.graph import StepGraph
+    from expertsim.utils.synthetic import make_batch
+    b = make_batch(64, "neutron", seed=3)
+    t = {k: torch.from_numpy(v).to(DEV) for k, v in b.items()}
+    real = t["real_images"].unsqueeze(1).contiguous()
+    runs = []
+    for mode in ("eager", "graph"):
+        moe, (og, od, oa, orr), cfg = _build(precision="bf16")
+        args = (0, t["cond"], real, t["true_positions"], t["std"], t["intensity"], oa, og, od, orr, None, DEV)
+        if mode == "eager":
+            for _ in range(3):
+                m = moe.train_step(*args)
+        else:
+            sg = StepGraph(moe, args, warmup=1)
+            for _ in range(2):
+                m = sg.replay()
+            sg.sync_host_state([og[0], od[0], oa[0], orr])
+            assert og[0]._step == 3 and moe.step_count == 3
+        torch.cuda.synchronize()
+        runs.append(({k: float(v) for k, v in m.items()},
+                     {n: p.detach().clone() for n, p in moe.named_parameters()}, cfg))
+    (ma, pa, cfg), (mb, pb, _) = runs
+    lr = max(float(cfg.model.generator.lr_g), float(cfg.model.discriminator.lr_d), float(cfg.model.aux_reg.lr_a))
+    _close_bf16(ma, mb, pa, pb, lr, 3)
+
+
+def test_expert_graphs_track_eager_bf16():
+    """per-expert graphs (E = 3, concurrent replay) in the bf16 performance mode."""
+    from expertsim.utils.synthetic import make_batch
+    import bench
+    b = make_batch(96, "neutron", seed=4)
+    t = {k: torch.from_numpy(v).to(DEV) for k, v in b.items()}
+    real = t["real_images"].unsqueeze(1).contiguous()
+    runs = []
+    for graphs in (False, True):
+        moe, (og, od, oa, orr), cfg = bench.build("neutron", 3, "bf16", 11, torch.device(DEV))
+        moe.expert_graphs = graphs
+        args = (0, t["cond"], real, t["true_positions"], t["std"], t["intensity"], oa, og, od, orr, None, DEV)
+        for _ in range(5):
+            m = moe.train_step(*args)
+        torch.cuda.synchronize()
+        if graphs:
+            eg = moe._egraphs
+            assert eg is not None and eg.captures >= 1 and eg.replays >= 1, (eg.captures, eg.replays)
+        runs.append(({k: float(v) for k, v in m.items()},
+                     {n: p.detach().clone() for n, p in moe.named_parameters()}, cfg))
+    (ma, pa, cfg), (mb, pb, _) = runs
+    lr = max(float(cfg.model.generator.lr_g), float(cfg.model.discriminator.lr_d), float(cfg.model.aux_reg.lr_a),
+             float(cfg.model.router.lr_r))
+    _close_bf16(ma, mb, pa, pb, lr, 5)

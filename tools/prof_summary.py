@@ -1,6 +1,9 @@
 """Summarise rocprofv3 --kernel-trace --stats output into markdown.
 
-usage: python tools/prof_summary.py <run_kernel_stats.csv> <steps> [<run_kernel_trace.csv>]
+usage: python tools/prof_summary.py <run_kernel_stats.csv> <steps | marker kernel> [<run_kernel_trace.csv>]
+
+<steps> is an integer, or the name (substring) of a kernel launched once per step (bench.py:
+step_metrics_kernel), whose launch count in the stats is then the step count.
 
 Table 1 is rocprofv3's own per-kernel-name statistics (kernel_stats.csv) divided per step.
 Table 2 (needs the trace) splits each kernel name by launch grid, so that one layer's launches
@@ -21,10 +24,18 @@ def short(name):
 
 
 def main():
-    path, steps = sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    path = sys.argv[1]
     rows = list(csv.DictReader(open(path)))
+    arg = sys.argv[2] if len(sys.argv) > 2 else "1"
+    if arg.isdigit():
+        steps, how = int(arg), "given"
+    else:
+        steps = sum(int(r["Calls"]) for r in rows if arg in r["Name"])
+        how = f"launches of {arg}"
+        if steps == 0:
+            sys.exit(f"no launches of {arg} in {path}")
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
-    print(f"total kernel time {tot/1e6:.2f} ms over {steps} steps = {tot/1e6/steps:.2f} ms/step\n")
+    print(f"total kernel time {tot/1e6:.2f} ms over {steps} steps ({how}) = {tot/1e6/steps:.2f} ms/step\n")
     print("| kernel | calls/step | ms/step | avg us | % |")
     print("|---|---|---|---|---|")
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:40]:
