@@ -37,6 +37,9 @@
 
 #include "conv_common.h"
 
+// the 4-wave split-fp32 FWD / DGRAD launches (conv_spb4.hip, see there)
+void es_spb4_launch(int mode, bool sp, const ConvArgs& a, dim3 grid, hipStream_t st);
+
 namespace {
 
 constexpr int RT = 512;   // threads per workgroup (8 waves)
@@ -54,6 +57,9 @@ constexpr uint32_t OOB = 0x80000000u;
 #ifndef ES_COOP2
 #define ES_COOP2 0   // wgrad_coop_kernel: two register stages of loads (experiment)
 #endif
+#ifndef ES_SPB4_PFD
+#define ES_SPB4_PFD 1   // SPB4 loop: column tiles of B planes read ahead of their MFMAs
+#endif
 #ifndef ES_SPB_PFD
 #define ES_SPB_PFD 2   // split-fp32 SPB loop: column tiles of B planes read ahead of their MFMAs
 #endif   // buffer offset past every num_records (< 2^31 bytes)
@@ -61,6 +67,9 @@ constexpr uint32_t OOB = 0x80000000u;
 // ES_NO_RING=1 (or es_conv_set_ring(0)) routes these shapes to the 4-wave kernels of
 // conv_igemm.hip (A/B measurement)
 bool g_ring_off = [] { const char* e = getenv("ES_NO_RING"); return e && e[0] == '1'; }();
+// split-fp32 FWD / DGRAD 256 x 128 tiles on the 4-wave SPB kernel (conv_ring_kernel SPL = 3);
+// ES_SPB4=0 / es_conv_set_spb4(0) keeps the 8-wave SPL = 2 kernel (A/B)
+bool g_spb4 = [] { const char* e = getenv("ES_SPB4"); return !(e && e[0] == '0'); }();
 
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -369,14 +378,24 @@ __device__ __forceinline__ f32x4 mfma_split6(const bf16x8 a[3], const bf16x8 b[3
 // permutation as the A fragments), so only A is split in the kernel.  The slot holds B plane-major,
 // [3][BN rows][64 B] (swizzled as the BK = 32 images), and the 8 waves are stacked along M (wave
 // tile BM/8 x BN): every A element is split by one wave only.
+//
+// SPL == 3 (SPB4): SPB with FOUR waves, one per SIMD (256 threads), wave tiles 64 x BN (BN = 128:
+// 4 x 8 accumulator tiles).  Each wave DMAs exactly the 64 A rows it multiplies (one pixel x 64
+// images), so A needs no cross-wave synchronisation; the B planes (shared) are read by 4 instead of 8
+// waves (half the LDS fragment traffic of SPB), and a wave interleaves its own LDS reads, splits and
+// DMA issue between its MFMAs instead of relying on a partner wave in the same phase.  A(t+1) is read
+// and split one row tile per two column tiles of step t, into the other of two plane sets (the step
+// loop is unrolled by two so the sets swap roles without copies).
 template <int MODE, int BM, int BN, bool SP, int BK = 64, typename T = bf16, int SPL = 0>
-__global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
+__global__ void __launch_bounds__(SPL == 3 ? 256 : RT) conv_ring_kernel(ConvArgs a) {
   static_assert(!SPL || (sizeof(T) == 4 && BK == 64), "split-fp32: fp32 operands, 128-byte slot rows");
   // (SPL 256 x 256: 2 x 4 waves of 128 x 64 and two 64 KiB slots; one step in flight covers a step
   // of 192 MFMAs per wave)
-  constexpr bool SPB = SPL == 2;
+  constexpr bool SPB = SPL >= 2;
+  constexpr bool SPB4 = SPL == 3;
+  constexpr int NW = SPB4 ? 4 : 8, NT = 64 * NW;         // waves / threads per workgroup
   constexpr bool SPW = SPL == 1 && BN == 256;
-  constexpr int WGM = SPB ? 8 : ((BK == 32 || SPW) ? 2 : 4), WGN = 8 / WGM;   // waves along M / N
+  constexpr int WGM = SPB ? NW : ((BK == 32 || SPW) ? 2 : 4), WGN = NW / WGM;   // waves along M / N
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int RM = WM / 16, RN = WN / 16;
   constexpr int ROWB = BK * 2, PROWS = 1024 / ROWB;      // slot row bytes, rows per 1 KiB piece
@@ -385,7 +404,7 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   constexpr int EBB = SPB ? 6 : EB;                      // bytes per B element in global memory
   constexpr int BPL = BN / 16;                           // SPB: 1 KiB pieces per B plane
   constexpr int BPIECES = SPB ? 3 * BPL : BN / PROWS;    // (SPB, BN = 64: 12 pieces + 4 zero-fill dummies)
-  constexpr int APW = BM / PROWS / 8, BPW = (BPIECES + 7) / 8;   // pieces per wave per slot
+  constexpr int APW = BM / PROWS / NW, BPW = (BPIECES + NW - 1) / NW;   // pieces per wave per slot
   constexpr int PW = APW + BPW;
   constexpr int ABYTES = BM * ROWB, BBYTES = SPB ? 3 * BN * 64 : BN * ROWB;
   constexpr int SLOT = ABYTES + BBYTES;
@@ -398,12 +417,12 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   constexpr int KH = BK == 64 ? 2 : 1;                   // MFMA K-halves per step
   constexpr int RMF = RM / (3 - KH);                     // A tiles per fragment set
   constexpr int SROWS = WM < 64 ? WM : 64;               // epilogue staging rows per pass
-  constexpr int STAGE0 = 8 * SROWS * (WN * 4 + 16);
+  constexpr int STAGE0 = NW * SROWS * (WN * 4 + 16);
   constexpr int TPITCH = BN * 2 + 16;                    // BK = 32 bf16 epilogue: whole-tile image
   constexpr int STAGE = BK == 32 && BM * TPITCH > STAGE0 ? BM * TPITCH : STAGE0;
-  constexpr int RINGB = SPLITD ? 3 * ABYTES + 2 * BBYTES : NS * SLOT;
+  constexpr int RINGB = SPB4 ? 2 * ABYTES + 2 * BBYTES : (SPLITD ? 3 * ABYTES + 2 * BBYTES : NS * SLOT);
   constexpr int RING = RINGB > STAGE ? RINGB : STAGE;
-  constexpr int JUNK = BPW * 8 > BPIECES ? 1024 : 0;     // landing area of the dummy pieces
+  constexpr int JUNK = BPW * NW > BPIECES ? 1024 : 0;    // landing area of the dummy pieces
   // ONE __shared__ object (a second one beside the DMA ring makes hipcc wait vmcnt(0) before
   // every ds_read of the loop): the ring slots (also the epilogue staging), then the fused-stats
   // scratch [3][WGM][BN] floats, which no DMA targets
@@ -440,7 +459,7 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
       if (jt >= sp.tile0[cls + 1] - sp.tile0[cls]) {
         if (a.stats_part) {   // empty partial (count 0) for this tile
           float* pp = a.stats_part + (int64_t)tl * 3 * a.Ng;
-          for (int c = threadIdx.x; c < BN; c += RT)
+          for (int c = threadIdx.x; c < BN; c += NT)
             if (n0 + c < a.Ng) pp[n0 + c] = 0.f;
         }
         return;
@@ -489,12 +508,16 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)bbytes);
   const int as2b = (int)a.as[2] * EB, as3b = (int)a.as[3] * EB;
 
-  // A pieces: per-lane constant (image, 16-byte chunk) + per-piece uniform pixel coordinates
-  uint32_t alane[APW];
-  int pc0[APW], pc1[APW];
-  bool pval[APW];
+  // A pieces: per-lane constant (image, 16-byte chunk) + per-piece uniform pixel coordinates.
+  // SPB4 (host: ng == 64): the wave's APW = 8 pieces are ONE pixel (pix0 + wid) x 64 images, so one
+  // set of pixel coordinates, and two per-lane constants (the swizzle depends on the piece's parity;
+  // piece j adds the uniform image offset (j & ~1) * 8 rows)
+  constexpr int APC = SPB4 ? 1 : APW, ALN = SPB4 ? 2 : APW;
+  uint32_t alane[ALN];
+  int pc0[APC], pc1[APC];
+  bool pval[APC];
 #pragma unroll
-  for (int j = 0; j < APW; ++j) {
+  for (int j = 0; j < ALN; ++j) {
     const int pi = wid * APW + j;                 // piece of the tile: pixel pix0 + pi / PPG
     const int rr = pi * PROWS + lrow;             // row within the tile (swizzle)
     const int lc = pc ^ swz_x<BK>(rr);
@@ -505,6 +528,7 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
     const int y = pp / gw, x = pp - y * gw;
     const int img = gi * NG + (pi - ppix * PPG) * PROWS + lrow;
     alane[j] = (uint32_t)(((ES_RING_EXP & 1) ? 0 : img) * (int)a.as[0] * EB + lc * 16);   // images >= N: past num_records
+    if (j >= APC) continue;
     if constexpr (MODE == MODE_FWD && SP) {       // source row = u + oh + d
       pc0[j] = y + sp.oh[cls];
       pc1[j] = x + sp.ow[cls];
@@ -522,11 +546,15 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
       pc1[j] = x + d.pad;
     }
   }
-  uint32_t blane[BPW];
+  // (SPB4: every piece is valid and its swizzle term depends on the lane only, so one per-lane
+  // constant plus the piece's uniform offset, b_off below)
+  constexpr int BLN = SPB4 ? 1 : BPW;
+  static_assert(!SPB4 || BPW * NW == BPIECES, "SPB4: no dummy B pieces");
+  uint32_t blane[BLN];
 #pragma unroll
-  for (int j = 0; j < BPW; ++j) {
+  for (int j = 0; j < BLN; ++j) {
     if constexpr (SPB) {   // piece q: plane q / BPL, rows 16 (q % BPL) + lane / 4, 16-byte chunk lane % 4
-      const int q = wid * BPW + j;
+      const int q = SPB4 ? 0 : wid * BPW + j;
       const int rr = (q % BPL) * 16 + (lane >> 2);
       blane[j] = q < BPIECES ? (uint32_t)((bbase + (n0 + rr) * ldb) * EBB + (q / BPL) * 64 +
                                           (((lane & 3) ^ swz_x<32>(rr)) * 16))
@@ -559,14 +587,15 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   // nch / BK steps); inside a tap a step adds BK channels.  Recomputing them every step cost
   // ~100 scalar instructions per K-step, which made the loop issue-bound (the CU's scalar unit
   // is shared by its 8 waves).
-  uint32_t ua_t[APW], ub_t = 0;
+  uint32_t ua_t[APC], ub_t = 0;
 #pragma unroll
-  for (int j = 0; j < APW; ++j) ua_t[j] = OOB;
+  for (int j = 0; j < APC; ++j) ua_t[j] = OOB;
+  const uint32_t as8b = (uint32_t)(8 * (int)a.as[0] * EB);   // (SPB4) 8 images
   auto issue = [&](char* slot) {
     if (cch == 0) {   // first step of a tap (wave-uniform branch, scalar work only)
       const bool live = cstep < nk;
 #pragma unroll
-      for (int j = 0; j < APW; ++j) {
+      for (int j = 0; j < APC; ++j) {
         uint32_t u;
         if constexpr (MODE == MODE_FWD && SP) {
           const int hs = pc0[j] + cr, ws = pc1[j] + cs;
@@ -602,7 +631,10 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
     // (OOB + a channel offset stays past every num_records: offsets are < 1 GiB)
     const uint32_t co = (uint32_t)(cch * EB), cob = (uint32_t)(cch * EBB);
 #pragma unroll
-    for (int j = 0; j < APW; ++j) bdma16(ares, alane[j] + (ua_t[j] + co), slot + (wid * APW + j) * 1024);
+    for (int j = 0; j < APW; ++j) {
+      if constexpr (SPB4) bdma16(ares, alane[j & 1] + (ua_t[0] + co + (uint32_t)(j & ~1) * as8b), slot + (wid * APW + j) * 1024);
+      else bdma16(ares, alane[j] + (ua_t[j] + co), slot + (wid * APW + j) * 1024);
+    }
     if constexpr (!SPB) {   // (SPB: B has its own ring and issue_b)
 #pragma unroll
       for (int j = 0; j < BPW; ++j) {
@@ -683,7 +715,147 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
         }
       }
   };
-  if constexpr (SPB) {
+  if constexpr (SPB4) {
+    // 4-wave SPB loop (see above the kernel).  Two A slots (A(t+1) landed, A(t+2) in flight: a wave's
+    // A rows are its own, so only its own vmcnt orders them) and two B slots (B(t) read, B(t+1) in
+    // flight); one barrier per step, for the shared B ring.
+    //   Step t runs row groups of IG = 2 A row tiles; per column tile j (one "iteration", fenced by
+    //   sched_barrier so the pipeline below is what issues): the three B planes of column j + 1 are
+    //   read, the group's 2 x 6 plane products of column j issued into fresh accumulators, the fresh
+    //   accumulators of column j - 1 added to the running sums (their MFMAs long done: no hazard
+    //   stall), and one pair of A values split into planes.
+    //   Planes: one set P (48 VGPRs).  During group g the wave splits the rows of group g - 1 of
+    //   A(t+1) (whose step-t MFMAs are done); during group 0, the LAST group's rows of A(t) itself,
+    //   whose step-t MFMAs come after it.  So A(t+1) is read at group 1 (A(t+2)'s DMA follows it into
+    //   A(t)'s slot once group 0 has read that slot's last rows).
+    constexpr int IG = 2, NGR = RM / IG;
+    static_assert(RM % IG == 0 && NGR == 2 && RN == 8, "SPB4: 4 x 8 tiles, two row groups of two");
+    char* const aring = smem;                   // [2][ABYTES]
+    char* const bring = smem + 2 * ABYTES;      // [2][BBYTES]
+    const int bper = (MODE == MODE_DGRAD && !SP) ? (d.R * d.S * d.K) / BKC : nk;
+    int bs = 0, bsm = 0;
+    const uint32_t brow16 = (uint32_t)(16 * ldb * EBB);      // 16 packed weight rows
+    auto issue_b = [&](char* bslot) {
+      const uint32_t ub = bs < nk ? (uint32_t)(bsm * BKC * EBB) : OOB;
+#pragma unroll
+      for (int j = 0; j < BPW; ++j) {
+        const int q = wid * BPW + j;   // plane q / BPL, rows 16 (q % BPL) + lane / 4 (blane[0]: q = 0)
+        const uint32_t b_off = (uint32_t)(q % BPL) * brow16 + (uint32_t)(q / BPL) * 64;
+        bdma16(bres, blane[0] + (ub + b_off), bslot + q * 1024);
+      }
+      ++bs;
+      bsm = bsm + 1 == bper ? 0 : bsm + 1;
+    };
+    auto rd_a1 = [&](f32x4 (&r)[2], const char* aslot, int i) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) r[h] = *(const f32x4*)(aslot + swz<BK>(wm0 + i * 16 + r16, g16 + 4 * h));
+    };
+    auto rd_b = [&](bf16x8 (&bp)[3], const char* bimg, int j) {
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        bp[pl] = *(const bf16x8*)(bimg + pl * (BN * 64) + swz<32>(wn0 + j * 16 + r16, g16));
+    };
+    // plane registers as dwords: P[i][plane][e] packs the bf16 planes of values 2e, 2e + 1 of the
+    // lane's 8-value k-slice of row tile i (split8's layout)
+    u32x4_t P[RM][3];
+    auto split_e = [&](const f32x4 (&r)[2], int i, int e) {
+      const float x = e < 2 ? r[0][2 * e] : r[1][2 * e - 4], y = e < 2 ? r[0][2 * e + 1] : r[1][2 * e - 3];
+      uint32_t h, m, l;
+      split_pair(x, y, h, m, l);
+      P[i][0][e] = h;
+      P[i][1][e] = m;
+      P[i][2][e] = l;
+    };
+    auto planes = [&](int i, bf16x8 (&ap)[3]) {
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) ap[pl] = __builtin_bit_cast(bf16x8, P[i][pl]);
+    };
+    auto chain6 = [&](const bf16x8 (&ap)[3], const bf16x8 (&bp)[3]) {
+      f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[2], bp[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[1], bp[1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[0], bp[2], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[1], bp[0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[0], bp[1], c, 0, 0, 0);
+      return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[0], bp[0], c, 0, 0, 0);
+    };
+    // four scalar adds (not v_pk_add_f32: filler price; this translation unit is built without SLP),
+    // each pinned to the iteration it is written in by an empty volatile asm on its result (without
+    // it the adds were sunk to the end of the step).  The adds themselves stay compiler code: they
+    // read MFMA results, and only the compiler's hazard recognizer inserts the MFMA -> VALU wait
+    // states (it does not see into inline asm).
+    auto add4 = [&](f32x4& s, const f32x4& c) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = s[e] + c[e];
+        asm volatile("" : "+v"(v));
+        s[e] = v;
+      }
+    };
+    // prologue: B(0), A(0), A(1); A(0)'s group-0 rows split (group 1's: during step 0, group 0)
+    issue_b(bring);
+    issue(aring);
+    issue(aring + ABYTES);
+    wait_vmcnt<0>();
+    ring_barrier();
+#pragma unroll
+    for (int i = 0; i < IG; ++i) {
+      f32x4 r[2];
+      rd_a1(r, aring, i);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) split_e(r, i, e);
+    }
+    for (int t = 0; t < nk; ++t) {
+      if (t > 0) {
+        wait_vmcnt<APW>();                                   // B(t) landed (A(t+1) may be in flight)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of step t-1 are done
+        ring_barrier();
+      }
+      const char* bimg = bring + (t & 1) * BBYTES;
+      issue_b(bring + ((t + 1) & 1) * BBYTES);               // B(t+1) into B(t-1)'s slot
+#pragma unroll
+      for (int gr = 0; gr < NGR; ++gr) {
+        __builtin_amdgcn_sched_barrier(0);
+        const int sg = gr == 0 ? NGR - 1 : gr - 1;           // row group split during this group
+        const char* asrc;
+        if (gr == 0) {
+          asrc = aring + (t & 1) * ABYTES;                   // A(t), its last group's rows
+        } else {
+          wait_vmcnt<BPW>();                                 // A(t+1) landed (B(t+1) may be in flight)
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // group 0's reads of A(t)'s slot done
+          issue(aring + (t & 1) * ABYTES);                   // A(t+2) into A(t)'s slot
+          asrc = aring + ((t + 1) & 1) * ABYTES;
+        }
+        f32x4 ra[IG][2];
+#pragma unroll
+        for (int ii = 0; ii < IG; ++ii) rd_a1(ra[ii], asrc, sg * IG + ii);
+        bf16x8 ap[IG][3];
+#pragma unroll
+        for (int ii = 0; ii < IG; ++ii) planes(gr * IG + ii, ap[ii]);
+        bf16x8 bq[2][3];
+        rd_b(bq[0], bimg, 0);
+        f32x4 cp[IG];
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          __builtin_amdgcn_sched_barrier(0);
+          if (j + 1 < RN) rd_b(bq[(j + 1) & 1], bimg, j + 1);
+          f32x4 cn[IG];
+#pragma unroll
+          for (int ii = 0; ii < IG; ++ii) cn[ii] = chain6(ap[ii], bq[j & 1]);
+          if (j > 0) {
+#pragma unroll
+            for (int ii = 0; ii < IG; ++ii) add4(acc[gr * IG + ii][j - 1], cp[ii]);
+          }
+          split_e(ra[j >> 2], sg * IG + (j >> 2), j & 3);
+#pragma unroll
+          for (int ii = 0; ii < IG; ++ii) cp[ii] = cn[ii];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ii = 0; ii < IG; ++ii) add4(acc[gr * IG + ii][RN - 1], cp[ii]);
+      }
+    }
+    wait_vmcnt<0>();   // drain the zero-fill steps before the workgroup may exit
+  } else if constexpr (SPB) {
     // Software-pipelined split-fp32 loop.  A (activations, fp32) and B (pre-split weight planes) have
     // their own rings: A in NSA slots, B in NSB.  Step t's MFMAs use A planes split during step t-1
     // (registers) and B(t) read from LDS per column tile; under them the wave reads A(t+1) and splits
@@ -2874,6 +3046,20 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   }
 }
 
+#ifdef ES_SPB4_TU
+}  // namespace
+
+// conv_spb4.hip = this file with ES_SPB4_TU: only the 4-wave split-fp32 kernels (conv_ring_kernel
+// SPL = 3) are instantiated, built with VGPR-form MFMA (-mllvm -amdgpu-mfma-vgpr-form) and without
+// SLP vectorisation: their per-step fresh accumulators are added to the running sums by the VALU, so
+// AGPR destinations would cost an accvgpr read per element and SLP's v_pk_add_f32 costs issue cycles
+// beside MFMAs (MI355X_MICROARCH.md, filler prices)
+void es_spb4_launch(int mode, bool sp, const ConvArgs& a, dim3 grid, hipStream_t st) {
+  (void)sp;   // (sub-pixel convs only, see launch_ring)
+  if (mode == MODE_FWD) hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 128, true, 64, float, 3>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((conv_ring_kernel<MODE_DGRAD, 256, 128, true, 64, float, 3>), grid, dim3(256), 0, st, a);
+}
+#else
 // host-side count of the MFMA conv kernels issued (ring / persistent / p256 / fp32 wgrad), read by
 // bench.py's probe to state how many launches one probed op is (fp32 image chunks)
 int64_t g_conv_launches = 0;
@@ -2883,6 +3069,14 @@ template <int MODE, int BM, int BN, bool SP, int BK = 64, typename T = bf16, int
 void launch_ring(const ConvArgs& a, int row_tiles, hipStream_t st) {
   dim3 grid(row_tiles, (a.Ng + BN - 1) / BN, 1);
   ++g_conv_launches;
+  // the 4-wave kernel for the sub-pixel convs (conv_layers.0 / .5 at B = 1024, tools/mb_spb4.py r04b:
+  // FWD 1.06-1.11x, DGRAD 0.997-1.07x); the plain conv_layers.9 DGRAD measured 0.89x, so it keeps SPB
+  if constexpr (SPL == 2 && BM == 256 && BN == 128 && SP) {
+    if (g_spb4 && a.ng == 64) {   // (the 4-wave kernel: one pixel x 64 images per wave)
+      es_spb4_launch(MODE, SP, a, grid, st);
+      return;
+    }
+  }
   hipLaunchKernelGGL((conv_ring_kernel<MODE, BM, BN, SP, BK, T, SPL>), grid, dim3(RT), 0, st, a);
 }
 
@@ -3011,6 +3205,12 @@ extern "C" int es_conv_set_ring256(int on) {
 extern "C" int es_conv_set_wgrad_mt(int on) {
   const int old = g_wgrad_mt;
   g_wgrad_mt = on != 0;
+  return old;
+}
+
+extern "C" int es_conv_set_spb4(int on) {
+  const int old = g_spb4;
+  g_spb4 = on != 0;
   return old;
 }
 
@@ -3220,7 +3420,8 @@ int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
       static const bool bn64 = [] { const char* e = getenv("ES_SPB_BN64"); return e && e[0] == '1'; }();
       if (a.Ng % 128 == 0 && !bn64) {
         dim3 grid(row_tiles, 4 * a.Ng / 128, 1);
-        hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 128, true, 64, T, 2>), grid, dim3(RT), 0, st, a);
+        if (g_spb4 && a.ng == 64) es_spb4_launch(MODE_FWD, true, a, grid, st);
+        else hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 128, true, 64, T, 2>), grid, dim3(RT), 0, st, a);
       } else {
         dim3 grid(row_tiles, 4 * a.Ng / 64, 1);
         hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 64, true, 64, T, 2>), grid, dim3(RT), 0, st, a);
@@ -3489,3 +3690,4 @@ extern "C" int es_conv_set_f32_split(int on) {
   g_f32_split = on < 0 ? 0 : (on > 2 ? 2 : on);
   return old;
 }
+#endif  // ES_SPB4_TU

@@ -194,6 +194,11 @@ int es_pack_weight_planes(const float* packed, int64_t n, void* base, es_stream_
 /* Host-side count of MFMA conv kernels issued so far (ring / persistent / p256 / fp32 WGRAD).
  * Instrumentation only: lets a profiler state how many kernel launches one conv op was. */
 int64_t es_conv_launch_count(void);
+/* A/B knob of the split-fp32 FWD / DGRAD 256 x 128 tiles: 1 (default) = the 4-wave kernel (one wave
+ * per SIMD, wave tiles 64 x 128), 0 = the 8-wave kernel; same products in the same order (bitwise
+ * equal outputs).  Returns the previous setting.  Replaces nothing of the reference (a kernel choice
+ * for neutron generator.py:24,29 conv_layers.0 / .5). */
+int es_conv_set_spb4(int on);
 /* Host-side tally of the MFMA work the conv entry points (es_conv2d_fwd / _dgrad / _wgrad /
  * _wgrad_det and their _stats / _bnred / _det variants) issued, as executed FLOPs (2 per MAC):
  * out[0] on the bf16 pipe (bf16 operands, and split-fp32: 6 plane products per fp32 product),

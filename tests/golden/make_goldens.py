@@ -330,6 +330,8 @@ CASES = {
     # BASELINE configs[1] batch size: step 0 at B = 512, compact (inputs
     # regenerated from make_batch and pinned by checksum; images / latents as checksums)
     "neutron_e1_b512": dict(arch="neutron", n_experts=1, batch=512, steps=1, compact=True),
+    # BASELINE configs[2] batch size = the bench workload: step 0 at B = 1024
+    "neutron_e1_b1024": dict(arch="neutron", n_experts=1, batch=1024, steps=1, compact=True),
 }
 
 

@@ -9,7 +9,7 @@ import numpy as np
 GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CASES = ["neutron_e1_b8", "neutron_e3_b12", "proton_e1_b8", "proton_e3_b12", "neutron_e3_b12_router"]
 # BASELINE batch sizes, compact (module outputs > 4096 values as checksums; inputs regenerated)
-LARGE_CASES = ["neutron_e1_b512"]
+LARGE_CASES = ["neutron_e1_b512", "neutron_e1_b1024"]
 
 
 class Golden:

@@ -1,7 +1,8 @@
-"""The HIP fp32 train step at a BASELINE batch size against the reference itself.
+"""The HIP fp32 train step at the BASELINE batch sizes against the reference itself.
 
-Golden ``neutron_e1_b512`` (tests/golden/make_goldens.py, compact): the reference's
-``MoEWrapper.train_step`` (moe.py:52-504) at B = 512 (BASELINE configs[1]), step 0, with injected
+Goldens ``neutron_e1_b512`` / ``neutron_e1_b1024`` (tests/golden/make_goldens.py, compact): the
+reference's ``MoEWrapper.train_step`` (moe.py:52-504) at B = 512 (BASELINE configs[1]) and B = 1024
+(configs[2], the bench workload), step 0, with injected
 noise / Gumbel / Philox dropout, captured in this container with torch 2.10 CPU on one thread.
 Module outputs larger than 4096 values are stored as checksums (sum, |.|-sum, L2 and 64 strided
 samples); the batch is regenerated from ``make_batch`` and pinned by its checksums.
@@ -21,6 +22,7 @@ from test_train_step_gpu import _build, _record
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 CASE = "neutron_e1_b512"
+LARGE = ["neutron_e1_b512", "neutron_e1_b1024"]
 
 
 def _ck_err(mine, ref):
@@ -57,9 +59,10 @@ def run_step0(g, record=True, grads=True):
     return moe, {k: float(v) for k, v in met.items()}, rec, store
 
 
-def test_b512_step0_matches_reference():
-    g = Golden(CASE)
-    assert g.B == 512 and g.E == 1
+@pytest.mark.parametrize("case", LARGE)
+def test_large_batch_step0_matches_reference(case):
+    g = Golden(case)
+    assert g.B == int(case.rsplit("_b", 1)[1]) and g.E == 1
     moe, met, rec, store = run_step0(g)
     gm = g.metrics(0)
     assert set(met) == set(gm)
@@ -73,10 +76,10 @@ def test_b512_step0_matches_reference():
         errs[f"D{c}.latent"] = _ck_err(lat.rows2d().cpu().numpy(), g[f"s0/D0/call{c}/out1_ck"])
     for c, (coords, _) in enumerate(rec["A0"]):
         errs[f"A{c}"] = _rel(coords.rows2d().cpu().numpy(), g[f"s0/A0/call{c}/out0"])
-    print("B=512 output errors:", errs)
+    print(f"B={g.B} output errors:", errs)
     for k, e in errs.items():
         assert e <= 1e-4, (k, e)
     for label, grads in store.items():
         comp = label[3]
         tol = max(TOL["neutron"], A_STEP0_TOL.get("neutron", 0.0)) if comp == "A" else TOL["neutron"]
-        _check(grad_errors(g, 0, label, grads, "neutron", comp), tol, (CASE, 0, label))
+        _check(grad_errors(g, 0, label, grads, "neutron", comp), tol, (case, 0, label))

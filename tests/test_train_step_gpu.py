@@ -74,6 +74,12 @@ def test_train_step_matches_reference(case):
     rec = _record(moe)
     lrs = {"G": cfg.model.generator.lr_g, "D": cfg.model.discriminator.lr_d, "A": cfg.model.aux_reg.lr_a,
            "R": cfg.model.router.lr_r}
+    worst = {}   # per step: the largest relative error of each quantity (printed: the bounds' evidence)
+
+    def note(s, what, e):
+        k = (s, what)
+        worst[k] = max(worst.get(k, 0.0), float(e))
+        return e
     for s in range(g.steps):
         rec.clear()
         tol = 1e-4 if s == 0 else STEP1_TOL[case]
@@ -90,16 +96,16 @@ def test_train_step_matches_reference(case):
         assert set(met) == set(gm)
         for k, v in gm.items():
             mine = float(met[k])
-            assert abs(mine - v) <= tol * max(abs(v), 1e-3), (s, k, mine, v)
+            assert note(s, "metric", abs(mine - v) / max(abs(v), 1e-3)) <= tol, (s, k, mine, v)
         for e in range(g.E):
             for c, (img, _) in enumerate(rec.get(f"G{e}", [])):
                 ref = g[f"s{s}/G{e}/call{c}/out0"]
-                assert _rel(img.torch_nchw().cpu().numpy(), ref) <= tol, (s, e, c)
+                assert note(s, "G", _rel(img.torch_nchw().cpu().numpy(), ref)) <= tol, (s, e, c)
             for c, (out, lat, _) in enumerate(rec.get(f"D{e}", [])):
-                assert _rel(out.rows2d().cpu().numpy(), g[f"s{s}/D{e}/call{c}/out0"]) <= tol, (s, e, c)
-                assert _rel(lat.rows2d().cpu().numpy(), g[f"s{s}/D{e}/call{c}/out1"]) <= tol, (s, e, c)
+                assert note(s, "D", _rel(out.rows2d().cpu().numpy(), g[f"s{s}/D{e}/call{c}/out0"])) <= tol, (s, e, c)
+                assert note(s, "D", _rel(lat.rows2d().cpu().numpy(), g[f"s{s}/D{e}/call{c}/out1"])) <= tol, (s, e, c)
             for c, (coords, _) in enumerate(rec.get(f"A{e}", [])):
-                assert _rel(coords.rows2d().cpu().numpy(), g[f"s{s}/A{e}/call{c}/out0"]) <= tol, (s, e, c)
+                assert note(s, "A", _rel(coords.rows2d().cpu().numpy(), g[f"s{s}/A{e}/call{c}/out0"])) <= tol, (s, e, c)
         # post-Adam parameters
         mods = [("optG", moe.generators, "G"), ("optD", moe.discriminators, "D"), ("optA", moe.aux_regs, "A")]
         for lab, mlist, comp in mods:
@@ -112,4 +118,8 @@ def test_train_step_matches_reference(case):
                     a = p.detach().double().reshape(-1).cpu().numpy()
                     idx = (np.arange(64) * a.size) // 64 if a.size >= 64 else np.arange(a.size)
                     bound = 2 * lrs[comp] * (s + 1) + 1e-6
-                    assert np.max(np.abs(a[idx] - ref[3:])) <= bound, (s, lab, e, n)
+                    dp = float(np.max(np.abs(a[idx] - ref[3:])))
+                    note(s, f"param/{comp} (x lr)", dp / lrs[comp])
+                    assert dp <= bound, (s, lab, e, n)
+        print(case, f"step {s} worst relative errors:",
+              {k[1]: f"{v:.2e}" for k, v in sorted(worst.items()) if k[0] == s})

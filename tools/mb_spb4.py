@@ -1,0 +1,88 @@
+"""A/B of the split-fp32 FWD / DGRAD kernels: 4-wave SPB4 (es_conv_set_spb4(1)) vs 8-wave SPB, on the
+neutron generator's conv shapes at B = 1024 (fp32, split level 2).  Checks that both give the same
+bits (same products in the same order) and times them with HIP events.
+
+usage: python tools/mb_spb4.py [B] [reps]"""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "generative-dnn-for-physics-simulations-cern_amd"))
+
+from expertsim import hip, layers  # noqa: E402
+from expertsim.layers import Act, ConvOp, Upsample  # noqa: E402
+
+SHAPES = {"c0": (128, 13, 13, 256, 3, (2, 2)), "c5": (256, 24, 24, 128, 3, (2, 2)), "c9": (128, 46, 46, 64, 2, None)}
+
+
+def timeit(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3
+
+
+def main():
+    N = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    dev = "cuda"
+    layers.set_deterministic(True)
+    layers.set_f32_split(True)
+    torch.manual_seed(0)
+    bad = 0
+    for name, (Cin, H, W, Cout, k, up) in SHAPES.items():
+        w = torch.nn.Parameter(torch.randn(Cout, Cin, k, k, device=dev) / (Cin * k * k) ** 0.5)
+        b = torch.nn.Parameter(torch.randn(Cout, device=dev))
+        op = ConvOp(w, b, upsample=Upsample((H, W), scale=up) if up else None)
+        x = Act.nhwc(N, Cin, H, W, torch.float32, dev)
+        x.t.normal_()
+        y = op.fwd(x, out_dtype=torch.float32)
+        dy = y.like_nhwc(torch.float32)
+        dy.t.normal_()
+        # executed bf16-pipe FLOPs per op: sub-pixel 4/9 of the 3x3 taps, 6 plane products
+        alg = 2.0 * N * y.dims[2] * y.dims[3] * Cout * Cin * k * k
+        ex = alg * (4.0 / 9.0 if up else 1.0) * 6
+        res = {}
+        for v in (0, 1):
+            hip.lib().es_conv_set_spb4(v)
+            n0 = hip.lib().es_conv_launch_count()
+            tf = timeit(lambda: op.fwd(x, out_dtype=torch.float32), reps)
+            of = op.fwd(x, out_dtype=torch.float32).t.clone()
+            td = timeit(lambda: op.dgrad(dy, x, dx_dtype=torch.float32), reps)
+            od = op.dgrad(dy, x, dx_dtype=torch.float32).t.clone()
+            torch.cuda.synchronize()
+            res[v] = (tf, td, of, od)
+        for m, i in (("fwd", 0), ("dgrad", 1)):
+            a8, a4 = res[0][2 + i], res[1][2 + i]
+            same = torch.equal(a8, a4)
+            bad += not same
+            if not same:
+                dif = (a8 - a4).abs()
+                nz = torch.nonzero(dif.reshape(-1) > 0)
+                first = int(nz[0]) if nz.numel() else -1
+                shape = tuple(a8.shape)
+                print(f"  {name} {m}: max|diff| {float(dif.max()):.3e} (max|y| {float(a8.abs().max()):.3e}), "
+                      f"{nz.numel()} of {a8.numel()} differ, first flat index {first} of shape {shape} "
+                      f"(nhwc strides), nan8 {bool(torch.isnan(a8).any())} nan4 {bool(torch.isnan(a4).any())}",
+                      flush=True)
+                # which (image, pixel, channel) blocks differ
+                v = dif.reshape(N, -1, a8.shape[-1] if a8.dim() == 2 else 1)
+                print("   images with diffs:", torch.nonzero(dif.reshape(N, -1).amax(1) > 0).reshape(-1)[:16].tolist(),
+                      flush=True)
+            t8, t4 = res[0][i], res[1][i]
+            print(f"{name} {m} B={N}: 8-wave {t8:8.1f} us ({ex / t8 / 1e6 / 2500:.3f} of bf16 peak) | 4-wave {t4:8.1f} us "
+                  f"({ex / t4 / 1e6 / 2500:.3f}) | x{t8 / t4:.3f} | bitwise {'same' if same else 'DIFFERENT'}", flush=True)
+    hip.lib().es_conv_set_spb4(1)
+    if bad:
+        sys.exit(f"{bad} outputs differ between the 4-wave and 8-wave kernels")
+
+
+if __name__ == "__main__":
+    main()
