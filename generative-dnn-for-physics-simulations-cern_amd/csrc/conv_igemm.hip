@@ -1039,6 +1039,7 @@ int ring_direct(ConvArgs& a, int mode, hipStream_t st, es_dtype_t dt) {
 
 // ---------------------------------------------------------------- executed-work tally (es_conv_exec_flops)
 thread_local int g_ring_hit = 0;
+thread_local PlanesRequest g_planes_req{0, 0};
 namespace {
 double g_exec_flops[3] = {0.0, 0.0, 0.0};
 // RAII around one conv entry: classifies the path the call took and adds its executed FLOPs
@@ -1093,6 +1094,7 @@ extern "C" int es_conv2d_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void*
   }
   ConvArgs a{};
   a.d = *d; a.a_src = x; a.b_src = wk; a.out = y; a.bias = bias; a.beta = 0.f;
+  a.a_planes = g_planes_req.on;
   a.out_bf16 = ydt == ES_BF16;
   for (int i = 0; i < 4; ++i) { a.as[i] = xs[i]; a.os[i] = ys[i]; }
   a.M = d->N * d->P * d->Q; a.Ng = d->K; a.Kd = d->R * d->S * d->C;
@@ -1128,6 +1130,7 @@ extern "C" int es_conv2d_dgrad(const es_conv_desc_t* d, es_dtype_t dt, const voi
   }
   ConvArgs a{};
   a.d = *d; a.a_src = dy; a.b_src = wd; a.out = dxu; a.bias = nullptr; a.beta = beta;
+  a.a_planes = g_planes_req.on;
   a.out_bf16 = dxdt == ES_BF16;
   for (int i = 0; i < 4; ++i) { a.as[i] = ys[i]; a.os[i] = dxs[i]; }
   a.fold = d->up_h > 0;
@@ -1155,6 +1158,45 @@ extern "C" int es_conv2d_dgrad_bnred(const es_conv_desc_t* d, es_dtype_t dt, con
   *chunks = g_bnr_req.chunks;
   g_bnr_req = BnRedRequest{nullptr, nullptr, nullptr, nullptr, 0, 0};
   return rc;
+}
+
+// FWD / DGRAD whose gathered operand is an es_split_planes image (fp32 parity mode, split-fp32
+// arithmetic, the sub-pixel convs of the 4-wave kernel); error when the conv takes another path
+namespace {
+int planes_call(int (*fn)(void*), void* ctx) {
+  g_planes_req = PlanesRequest{1, 0};
+  const int rc = fn(ctx);
+  const int used = g_planes_req.used;
+  g_planes_req = PlanesRequest{0, 0};
+  if (rc != ES_OK) return rc;
+  ES_CHECK_ARG(used, "conv planes: the conv did not run the planes kernel (sub-pixel split-fp32 4-wave path only)");
+  return ES_OK;
+}
+}  // namespace
+
+extern "C" int es_conv2d_fwd_planes(const es_conv_desc_t* d, const void* xp, const int64_t xs[4], const void* wk,
+                                    const float* bias, void* y, es_dtype_t ydt, const int64_t ys[4], float* part,
+                                    int64_t part_floats, int* chunks, es_stream_t stream) {
+  ES_CHECK_ARG(d && d->subpixel, "conv fwd planes: sub-pixel convs only");
+  struct C_ { const es_conv_desc_t* d; const void* x; const int64_t* xs; const void* wk; const float* bias; void* y;
+              es_dtype_t ydt; const int64_t* ys; float* part; int64_t pf; int* chunks; es_stream_t st; } c{d, xp, xs, wk,
+              bias, y, ydt, ys, part, part_floats, chunks, stream};
+  return planes_call([](void* p) {
+    C_& c = *(C_*)p;
+    if (c.part) return es_conv2d_fwd_stats(c.d, ES_F32, c.x, c.xs, c.wk, c.bias, c.y, c.ydt, c.ys, c.part, c.pf, c.chunks, c.st);
+    return es_conv2d_fwd(c.d, ES_F32, c.x, c.xs, c.wk, c.bias, c.y, c.ydt, c.ys, c.st);
+  }, &c);
+}
+
+extern "C" int es_conv2d_dgrad_planes(const es_conv_desc_t* d, const void* dyp, const int64_t ys[4], const void* wd,
+                                      void* dx, es_dtype_t dxdt, const int64_t dxs[4], es_stream_t stream) {
+  ES_CHECK_ARG(d && d->subpixel, "conv dgrad planes: sub-pixel convs only");
+  struct C_ { const es_conv_desc_t* d; const void* dy; const int64_t* ys; const void* wd; void* dx; es_dtype_t dxdt;
+              const int64_t* dxs; es_stream_t st; } c{d, dyp, ys, wd, dx, dxdt, dxs, stream};
+  return planes_call([](void* p) {
+    C_& c = *(C_*)p;
+    return es_conv2d_dgrad(c.d, ES_F32, c.dy, c.ys, c.wd, c.dx, c.dxdt, c.dxs, 0.f, c.st);
+  }, &c);
 }
 
 extern "C" int es_conv2d_wgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy,
@@ -1480,6 +1522,50 @@ __global__ void pack_planes_kernel(const float* __restrict__ w, int64_t nblk, bf
     o[32] = m;
     o[64] = l;
   }
+}
+
+// fp32 activations [rows][C] -> split-fp32 planes [rows][C / 32][3][32] bf16 (es_split_planes): the
+// weight planes' layout (pack_planes_kernel) per 32-channel block.  A thread owns 8 channels c0..c0+7
+// (c0 % 8 == 0) of one row: channels cc = c0 % 32 + e land in slots 8 u + j of the block (u = cc % 16
+// / 4, j = cc / 16 * 4 + cc % 4), i.e. two runs of 4 slots per plane (8-byte stores).
+__global__ void split_planes_kernel(const float* __restrict__ x, int64_t rows, int C, bf16* __restrict__ out) {
+  const int cv = C >> 3;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < rows * cv; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / cv;
+    const int c0 = (int)(i - r * cv) * 8;
+    const f32x4 v0 = *(const f32x4*)(x + r * C + c0);
+    const f32x4 v1 = *(const f32x4*)(x + r * C + c0 + 4);
+    const int cc = c0 & 31, u0 = (cc & 15) >> 2, jh = (cc >> 4) * 4;
+    bf16* blk = out + (r * (C >> 5) + (c0 >> 5)) * 96;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {   // channels c0 + 4h .. +3 -> slots 8 (u0 + h) + jh .. +3
+      const f32x4 v = h ? v1 : v0;
+      bf16x4 ph, pm, pl;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bf16 hi = (bf16)v[e];
+        const float rr = v[e] - (float)hi;
+        const bf16 mi = (bf16)rr;
+        ph[e] = hi;
+        pm[e] = mi;
+        pl[e] = (bf16)(rr - (float)mi);
+      }
+      bf16* o = blk + 8 * (u0 + h) + jh;
+      *(bf16x4*)o = ph;
+      *(bf16x4*)(o + 32) = pm;
+      *(bf16x4*)(o + 64) = pl;
+    }
+  }
+}
+
+extern "C" int es_split_planes(const float* x, int64_t rows, int C, void* planes, es_stream_t stream) {
+  ES_CHECK_ARG(x && planes && rows >= 0 && C > 0 && C % 32 == 0, "split planes: C %% 32 == 0 required");
+  const int64_t n = rows * (C / 8);
+  if (n == 0) return ES_OK;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 16384);
+  hipLaunchKernelGGL(split_planes_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, rows, C, (bf16*)planes);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
 }
 
 extern "C" int64_t es_weight_planes_offset(int64_t n) { return (n * 4 + 255) / 256 * 256; }

@@ -57,6 +57,12 @@ constexpr uint32_t OOB = 0x80000000u;
 #ifndef ES_COOP2
 #define ES_COOP2 0   // wgrad_coop_kernel: two register stages of loads (experiment)
 #endif
+#ifndef ES_SPB4_EXP
+#define ES_SPB4_EXP 0
+#endif
+#ifndef ES_SPB4_SB
+#define ES_SPB4_SB 1    // SPB4 / SPA loops: sched_barrier between column-tile iterations
+#endif
 #ifndef ES_SPB4_PFD
 #define ES_SPB4_PFD 1   // SPB4 loop: column tiles of B planes read ahead of their MFMAs
 #endif
@@ -67,9 +73,11 @@ constexpr uint32_t OOB = 0x80000000u;
 // ES_NO_RING=1 (or es_conv_set_ring(0)) routes these shapes to the 4-wave kernels of
 // conv_igemm.hip (A/B measurement)
 bool g_ring_off = [] { const char* e = getenv("ES_NO_RING"); return e && e[0] == '1'; }();
-// split-fp32 FWD / DGRAD 256 x 128 tiles on the 4-wave SPB kernel (conv_ring_kernel SPL = 3);
-// ES_SPB4=0 / es_conv_set_spb4(0) keeps the 8-wave SPL = 2 kernel (A/B)
-bool g_spb4 = [] { const char* e = getenv("ES_SPB4"); return !(e && e[0] == '0'); }();
+// split-fp32 FWD / DGRAD 256 x 128 tiles of the sub-pixel convs on the 4-wave kernel (conv_ring_kernel
+// SPL = 3; SPL = 4 with a planes operand).  Opt-in (ES_SPB4=1 / es_conv_set_spb4(1)): measured on one
+// box at B = 1024 with alternating best-of-3 timing (tools/mb_spb4.py, r04), conv_layers.5 fwd / dgrad
+// 8-wave 2935 / 2898 us vs 4-wave 3238 / 3179 us (and 2941 / 2894 us for its row-group variant).
+bool g_spb4 = [] { const char* e = getenv("ES_SPB4"); return e && e[0] == '1'; }();
 
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -386,27 +394,33 @@ __device__ __forceinline__ f32x4 mfma_split6(const bf16x8 a[3], const bf16x8 b[3
 // DMA issue between its MFMAs instead of relying on a partner wave in the same phase.  A(t+1) is read
 // and split one row tile per two column tiles of step t, into the other of two plane sets (the step
 // loop is unrolled by two so the sets swap roles without copies).
+//
+// SPL == 4 (SPA): SPB4 with the gathered operand ALSO pre-split: a_src is an activation-planes image
+// (es_split_planes: [rows][C / 32][3][32] bf16, 6 bytes per value, strides as[] in values), DMA'd as
+// planes ([3][BM rows][64 B] per slot, the B planes' image) and fed to the MFMAs as read: no split in
+// the kernel.  Same products in the same order as SPB / SPB4 (bitwise equal outputs).
 template <int MODE, int BM, int BN, bool SP, int BK = 64, typename T = bf16, int SPL = 0>
-__global__ void __launch_bounds__(SPL == 3 ? 256 : RT) conv_ring_kernel(ConvArgs a) {
+__global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs a) {
   static_assert(!SPL || (sizeof(T) == 4 && BK == 64), "split-fp32: fp32 operands, 128-byte slot rows");
   // (SPL 256 x 256: 2 x 4 waves of 128 x 64 and two 64 KiB slots; one step in flight covers a step
   // of 192 MFMAs per wave)
   constexpr bool SPB = SPL >= 2;
-  constexpr bool SPB4 = SPL == 3;
-  constexpr int NW = SPB4 ? 4 : 8, NT = 64 * NW;         // waves / threads per workgroup
+  constexpr bool SPB4 = SPL == 3, SPA = SPL == 4, W4 = SPB4 || SPA;
+  constexpr int NW = W4 ? 4 : 8, NT = 64 * NW;           // waves / threads per workgroup
   constexpr bool SPW = SPL == 1 && BN == 256;
   constexpr int WGM = SPB ? NW : ((BK == 32 || SPW) ? 2 : 4), WGN = NW / WGM;   // waves along M / N
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int RM = WM / 16, RN = WN / 16;
   constexpr int ROWB = BK * 2, PROWS = 1024 / ROWB;      // slot row bytes, rows per 1 KiB piece
   constexpr int EB = sizeof(T), BKC = ROWB / EB;         // operand bytes, channels per K-step (fp32: BK / 2)
+  constexpr int EA = SPA ? 6 : EB;                       // bytes per value of the gathered (A) image
   constexpr int CPR = ROWB / 16;                         // 16-byte chunks per row
   constexpr int EBB = SPB ? 6 : EB;                      // bytes per B element in global memory
   constexpr int BPL = BN / 16;                           // SPB: 1 KiB pieces per B plane
   constexpr int BPIECES = SPB ? 3 * BPL : BN / PROWS;    // (SPB, BN = 64: 12 pieces + 4 zero-fill dummies)
-  constexpr int APW = BM / PROWS / NW, BPW = (BPIECES + NW - 1) / NW;   // pieces per wave per slot
+  constexpr int APW = SPA ? 3 * (BM / NW / 16) : BM / PROWS / NW, BPW = (BPIECES + NW - 1) / NW;   // pieces per wave per slot
   constexpr int PW = APW + BPW;
-  constexpr int ABYTES = BM * ROWB, BBYTES = SPB ? 3 * BN * 64 : BN * ROWB;
+  constexpr int ABYTES = SPA ? 3 * BM * 64 : BM * ROWB, BBYTES = SPB ? 3 * BN * 64 : BN * ROWB;
   constexpr int SLOT = ABYTES + BBYTES;
   // SPB ring depths: three full slots when they fit (NS = 3); else A gets three slots and B (the
   // weights, L2-resident) two: A stays two steps ahead, B one (SPLITD)
@@ -420,7 +434,7 @@ __global__ void __launch_bounds__(SPL == 3 ? 256 : RT) conv_ring_kernel(ConvArgs
   constexpr int STAGE0 = NW * SROWS * (WN * 4 + 16);
   constexpr int TPITCH = BN * 2 + 16;                    // BK = 32 bf16 epilogue: whole-tile image
   constexpr int STAGE = BK == 32 && BM * TPITCH > STAGE0 ? BM * TPITCH : STAGE0;
-  constexpr int RINGB = SPB4 ? 2 * ABYTES + 2 * BBYTES : (SPLITD ? 3 * ABYTES + 2 * BBYTES : NS * SLOT);
+  constexpr int RINGB = W4 ? 2 * ABYTES + 2 * BBYTES : (SPLITD ? 3 * ABYTES + 2 * BBYTES : NS * SLOT);
   constexpr int RING = RINGB > STAGE ? RINGB : STAGE;
   constexpr int JUNK = BPW * NW > BPIECES ? 1024 : 0;    // landing area of the dummy pieces
   // ONE __shared__ object (a second one beside the DMA ring makes hipcc wait vmcnt(0) before
@@ -491,7 +505,7 @@ __global__ void __launch_bounds__(SPL == 3 ? 256 : RT) conv_ring_kernel(ConvArgs
   const int wm0 = (wid / WGN) * WM, wn0 = (wid % WGN) * WN;
   const int lrow = lane / CPR, pc = lane % CPR;
 
-  const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * EB));
+  const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * EA));
   // packed weights: row stride ldb (elements) and the class's block offset
   int ldb, bbase = 0, bbytes;
   if constexpr (SP && MODE == MODE_FWD) {
@@ -506,19 +520,21 @@ __global__ void __launch_bounds__(SPL == 3 ? 256 : RT) conv_ring_kernel(ConvArgs
     bbytes = a.Ng * ldb * EBB;
   }
   const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)bbytes);
-  const int as2b = (int)a.as[2] * EB, as3b = (int)a.as[3] * EB;
+  const int as2b = (int)a.as[2] * EA, as3b = (int)a.as[3] * EA;
 
   // A pieces: per-lane constant (image, 16-byte chunk) + per-piece uniform pixel coordinates.
   // SPB4 (host: ng == 64): the wave's APW = 8 pieces are ONE pixel (pix0 + wid) x 64 images, so one
   // set of pixel coordinates, and two per-lane constants (the swizzle depends on the piece's parity;
   // piece j adds the uniform image offset (j & ~1) * 8 rows)
-  constexpr int APC = SPB4 ? 1 : APW, ALN = SPB4 ? 2 : APW;
+  // SPA: the same one pixel per wave; pieces are (plane, 16 rows): lane l -> row l / 4, 16-byte chunk
+  // l % 4 of the row's 64-byte plane run, swizzled as the B planes (depends on the lane only)
+  constexpr int APC = W4 ? 1 : APW, ALN = SPB4 ? 2 : (SPA ? 1 : APW);
   uint32_t alane[ALN];
   int pc0[APC], pc1[APC];
   bool pval[APC];
 #pragma unroll
   for (int j = 0; j < ALN; ++j) {
-    const int pi = wid * APW + j;                 // piece of the tile: pixel pix0 + pi / PPG
+    const int pi = (W4 ? wid * (BM / NW / PROWS) : wid * APW) + j;   // piece of the tile: pixel pix0 + pi / PPG
     const int rr = pi * PROWS + lrow;             // row within the tile (swizzle)
     const int lc = pc ^ swz_x<BK>(rr);
     const int ppix = pi / PPG;
@@ -528,6 +544,10 @@ __global__ void __launch_bounds__(SPL == 3 ? 256 : RT) conv_ring_kernel(ConvArgs
     const int y = pp / gw, x = pp - y * gw;
     const int img = gi * NG + (pi - ppix * PPG) * PROWS + lrow;
     alane[j] = (uint32_t)(((ES_RING_EXP & 1) ? 0 : img) * (int)a.as[0] * EB + lc * 16);   // images >= N: past num_records
+    if constexpr (SPA) {
+      const int prow = lane >> 2;   // row of the 16-row piece
+      alane[j] = (uint32_t)((gi * NG + prow) * (int)a.as[0] * EA + (((lane & 3) ^ swz_x<32>(prow)) * 16));
+    }
     if (j >= APC) continue;
     if constexpr (MODE == MODE_FWD && SP) {       // source row = u + oh + d
       pc0[j] = y + sp.oh[cls];
@@ -548,13 +568,13 @@ __global__ void __launch_bounds__(SPL == 3 ? 256 : RT) conv_ring_kernel(ConvArgs
   }
   // (SPB4: every piece is valid and its swizzle term depends on the lane only, so one per-lane
   // constant plus the piece's uniform offset, b_off below)
-  constexpr int BLN = SPB4 ? 1 : BPW;
-  static_assert(!SPB4 || BPW * NW == BPIECES, "SPB4: no dummy B pieces");
+  constexpr int BLN = W4 ? 1 : BPW;
+  static_assert(!W4 || BPW * NW == BPIECES, "SPB4: no dummy B pieces");
   uint32_t blane[BLN];
 #pragma unroll
   for (int j = 0; j < BLN; ++j) {
     if constexpr (SPB) {   // piece q: plane q / BPL, rows 16 (q % BPL) + lane / 4, 16-byte chunk lane % 4
-      const int q = SPB4 ? 0 : wid * BPW + j;
+      const int q = W4 ? 0 : wid * BPW + j;
       const int rr = (q % BPL) * 16 + (lane >> 2);
       blane[j] = q < BPIECES ? (uint32_t)((bbase + (n0 + rr) * ldb) * EBB + (q / BPL) * 64 +
                                           (((lane & 3) ^ swz_x<32>(rr)) * 16))
@@ -590,7 +610,7 @@ __global__ void __launch_bounds__(SPL == 3 ? 256 : RT) conv_ring_kernel(ConvArgs
   uint32_t ua_t[APC], ub_t = 0;
 #pragma unroll
   for (int j = 0; j < APC; ++j) ua_t[j] = OOB;
-  const uint32_t as8b = (uint32_t)(8 * (int)a.as[0] * EB);   // (SPB4) 8 images
+  const uint32_t as8b = (uint32_t)(8 * (int)a.as[0] * EA);   // (SPB4 / SPA) 8 images
   auto issue = [&](char* slot) {
     if (cch == 0) {   // first step of a tap (wave-uniform branch, scalar work only)
       const bool live = cstep < nk;
@@ -629,11 +649,18 @@ __global__ void __launch_bounds__(SPL == 3 ? 256 : RT) conv_ring_kernel(ConvArgs
       ub_t = live ? (uint32_t)(kb * EBB) : OOB;
     }
     // (OOB + a channel offset stays past every num_records: offsets are < 1 GiB)
-    const uint32_t co = (uint32_t)(cch * EB), cob = (uint32_t)(cch * EBB);
+    const uint32_t co = (uint32_t)(cch * EA), cob = (uint32_t)(cch * EBB);
 #pragma unroll
     for (int j = 0; j < APW; ++j) {
-      if constexpr (SPB4) bdma16(ares, alane[j & 1] + (ua_t[0] + co + (uint32_t)(j & ~1) * as8b), slot + (wid * APW + j) * 1024);
-      else bdma16(ares, alane[j] + (ua_t[j] + co), slot + (wid * APW + j) * 1024);
+      if constexpr (SPA) {   // piece j: plane j / 4, rows 16 (j % 4) .. of the wave's 64
+        const int pl = j >> 2, rq = j & 3;
+        bdma16(ares, alane[0] + (ua_t[0] + co + (uint32_t)(rq * 2) * as8b + (uint32_t)(pl * 64)),
+               slot + pl * (BM * 64) + (wm0 + rq * 16) * 64);
+      } else if constexpr (SPB4) {
+        bdma16(ares, alane[j & 1] + (ua_t[0] + co + (uint32_t)(j & ~1) * as8b), slot + (wid * APW + j) * 1024);
+      } else {
+        bdma16(ares, alane[j] + (ua_t[j] + co), slot + (wid * APW + j) * 1024);
+      }
     }
     if constexpr (!SPB) {   // (SPB: B has its own ring and issue_b)
 #pragma unroll
@@ -715,21 +742,118 @@ __global__ void __launch_bounds__(SPL == 3 ? 256 : RT) conv_ring_kernel(ConvArgs
         }
       }
   };
-  if constexpr (SPB4) {
-    // 4-wave SPB loop (see above the kernel).  Two A slots (A(t+1) landed, A(t+2) in flight: a wave's
-    // A rows are its own, so only its own vmcnt orders them) and two B slots (B(t) read, B(t+1) in
-    // flight); one barrier per step, for the shared B ring.
-    //   Step t runs row groups of IG = 2 A row tiles; per column tile j (one "iteration", fenced by
-    //   sched_barrier so the pipeline below is what issues): the three B planes of column j + 1 are
-    //   read, the group's 2 x 6 plane products of column j issued into fresh accumulators, the fresh
-    //   accumulators of column j - 1 added to the running sums (their MFMAs long done: no hazard
-    //   stall), and one pair of A values split into planes.
-    //   Planes: one set P (48 VGPRs).  During group g the wave splits the rows of group g - 1 of
-    //   A(t+1) (whose step-t MFMAs are done); during group 0, the LAST group's rows of A(t) itself,
-    //   whose step-t MFMAs come after it.  So A(t+1) is read at group 1 (A(t+2)'s DMA follows it into
-    //   A(t)'s slot once group 0 has read that slot's last rows).
+  if constexpr (SPA) {
+    // 4-wave loop on pre-split A planes (see above the kernel).  Two A slots and two B slots: A(t+1) and
+    // B(t+1) are issued at the top of step t (after its barrier) into the slots of step t-1, so the top
+    // of step t+1 waits for everything (vmcnt(0)) and one barrier publishes B(t+1).  A is private per
+    // wave: the next step's first row group is read from A(t+1) late in step t, after the wave's own
+    // vmcnt covers it.  Per row group of IG = 2 row tiles and column tile j: B planes of j + 1 read,
+    // 2 x 6 plane products of j issued into fresh accumulators, the fresh accumulators of j - 1 added.
     constexpr int IG = 2, NGR = RM / IG;
-    static_assert(RM % IG == 0 && NGR == 2 && RN == 8, "SPB4: 4 x 8 tiles, two row groups of two");
+    static_assert(NGR == 2 && RN == 8, "SPA: 4 x 8 tiles, two row groups of two");
+    char* const aring = smem;                   // [2][ABYTES]
+    char* const bring = smem + 2 * ABYTES;      // [2][BBYTES]
+    const int bper = (MODE == MODE_DGRAD && !SP) ? (d.R * d.S * d.K) / BKC : nk;
+    int bs = 0, bsm = 0;
+    const uint32_t brow16 = (uint32_t)(16 * ldb * EBB);      // 16 packed weight rows
+    auto issue_b = [&](char* bslot) {
+      const uint32_t ub = bs < nk ? (uint32_t)(bsm * BKC * EBB) : OOB;
+#pragma unroll
+      for (int j = 0; j < BPW; ++j) {
+        const int q = wid * BPW + j;   // plane q / BPL, rows 16 (q % BPL) + lane / 4 (blane[0]: q = 0)
+        const uint32_t b_off = (uint32_t)(q % BPL) * brow16 + (uint32_t)(q / BPL) * 64;
+        bdma16(bres, blane[0] + (ub + b_off), bslot + q * 1024);
+      }
+      ++bs;
+      bsm = bsm + 1 == bper ? 0 : bsm + 1;
+    };
+    auto rd_pl = [&](bf16x8 (&p)[3], const char* img, int rows, int r0) {   // [3][rows][64 B] planes image
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) p[pl] = *(const bf16x8*)(img + pl * (rows * 64) + swz<32>(r0 + r16, g16));
+    };
+    auto chain6 = [&](const bf16x8 (&ap)[3], const bf16x8 (&bp)[3]) {
+      f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[2], bp[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[1], bp[1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[0], bp[2], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[1], bp[0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[0], bp[1], c, 0, 0, 0);
+      return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[0], bp[0], c, 0, 0, 0);
+    };
+    auto add4 = [&](f32x4& s, const f32x4& c) {   // as in the SPB4 loop
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = s[e] + c[e];
+        asm volatile("" : "+v"(v));
+        s[e] = v;
+      }
+    };
+    issue(aring);
+    issue_b(bring);
+    wait_vmcnt<0>();
+    ring_barrier();
+    bf16x8 AP[2][IG][3];   // planes of row group 0 / 1
+#pragma unroll
+    for (int ii = 0; ii < IG; ++ii) rd_pl(AP[0][ii], aring, BM, wm0 + ii * 16);
+    for (int t = 0; t < nk; ++t) {
+      if (t > 0) {
+        wait_vmcnt<0>();                                     // A(t), B(t): issued at the top of step t-1
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of step t-1 are done
+        ring_barrier();
+      }
+      const char* acur = aring + (t & 1) * ABYTES;
+      const char* anext = aring + ((t + 1) & 1) * ABYTES;
+      const char* bimg = bring + (t & 1) * BBYTES;
+      issue(aring + ((t + 1) & 1) * ABYTES);                 // A(t+1) into A(t-1)'s slot
+      issue_b(bring + ((t + 1) & 1) * BBYTES);               // B(t+1) into B(t-1)'s slot
+#pragma unroll
+      for (int gr = 0; gr < NGR; ++gr) {
+        __builtin_amdgcn_sched_barrier(0);
+        constexpr int PFD = ES_SPB4_PFD;
+        bf16x8 bq[PFD + 1][3];
+#pragma unroll
+        for (int jj = 0; jj < PFD; ++jj) rd_pl(bq[jj], bimg, BN, wn0 + jj * 16);
+        f32x4 cp[IG];
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          if constexpr (ES_SPB4_SB) __builtin_amdgcn_sched_barrier(0);
+          if (j + PFD < RN) rd_pl(bq[(j + PFD) % (PFD + 1)], bimg, BN, wn0 + (j + PFD) * 16);
+          if (gr == 0 && j == 0) {   // group 1's planes of A(t)
+#pragma unroll
+            for (int ii = 0; ii < IG; ++ii) rd_pl(AP[1][ii], acur, BM, wm0 + (IG + ii) * 16);
+          }
+          if (gr == 1 && j == RN / 2) {   // the next step's group 0 (A(t+1), this wave's own DMA)
+            wait_vmcnt<BPW>();
+#pragma unroll
+            for (int ii = 0; ii < IG; ++ii) rd_pl(AP[0][ii], anext, BM, wm0 + ii * 16);
+          }
+          f32x4 cn[IG];
+#pragma unroll
+          for (int ii = 0; ii < IG; ++ii) cn[ii] = chain6(AP[gr][ii], bq[j % (PFD + 1)]);
+          if (j > 0) {
+#pragma unroll
+            for (int ii = 0; ii < IG; ++ii) add4(acc[gr * IG + ii][j - 1], cp[ii]);
+          }
+#pragma unroll
+          for (int ii = 0; ii < IG; ++ii) cp[ii] = cn[ii];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ii = 0; ii < IG; ++ii) add4(acc[gr * IG + ii][RN - 1], cp[ii]);
+      }
+    }
+    wait_vmcnt<0>();   // drain the zero-fill steps before the workgroup may exit
+  } else if constexpr (SPB4) {
+    // 4-wave SPB loop, B planes cached in AGPRs (see above the kernel).
+    //   * B(t): a wave's 8 column tiles x 3 planes (24 fragments, 96 AGPRs) are read from LDS ONCE per
+    //     step (inline-asm ds_read into AGPRs, MFMA srcB straight from them) and used by all 4 row
+    //     tiles: 24 B fragment reads per wave per step instead of 48 (the B re-reads bounded the
+    //     loop: removing them alone made it 1.75x faster, ES_SPB4_EXP study r04).
+    //   * A: row tile after row tile; the fp32 row i+1 is read and split (one pair per two column
+    //     tiles) while row i's 48 MFMAs issue, into the other of two plane sets.
+    //   * Step t, row tile 3: vmcnt(0) + the one barrier of the step publish B(t+1) and A(t+1); B(t+1)'s
+    //     fragments are read into the AGPRs one column tile behind row 3's MFMAs (the last after the
+    //     step), and the DMA of B(t+2) / A(t+2) goes into the slots of B(t) / A(t) (read before).
+    //   Two A slots, two B slots.
     char* const aring = smem;                   // [2][ABYTES]
     char* const bring = smem + 2 * ABYTES;      // [2][BBYTES]
     const int bper = (MODE == MODE_DGRAD && !SP) ? (d.R * d.S * d.K) / BKC : nk;
@@ -750,39 +874,41 @@ __global__ void __launch_bounds__(SPL == 3 ? 256 : RT) conv_ring_kernel(ConvArgs
 #pragma unroll
       for (int h = 0; h < 2; ++h) r[h] = *(const f32x4*)(aslot + swz<BK>(wm0 + i * 16 + r16, g16 + 4 * h));
     };
-    auto rd_b = [&](bf16x8 (&bp)[3], const char* bimg, int j) {
+    // B fragments in AGPRs (int4v for the asm constraint; bit-cast for the MFMA)
+    int4v Bc[RN][3];
+    auto ld_bc = [&](int j, const char* bimg) {
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
-        bp[pl] = *(const bf16x8*)(bimg + pl * (BN * 64) + swz<32>(wn0 + j * 16 + r16, g16));
+        asm volatile("ds_read_b128 %0, %1" : "=a"(Bc[j][pl]) : "v"(lds_u32(bimg + pl * (BN * 64) + swz<32>(wn0 + j * 16 + r16, g16))));
     };
-    // plane registers as dwords: P[i][plane][e] packs the bf16 planes of values 2e, 2e + 1 of the
-    // lane's 8-value k-slice of row tile i (split8's layout)
-    u32x4_t P[RM][3];
-    auto split_e = [&](const f32x4 (&r)[2], int i, int e) {
+    auto fence_bc = [&]() {   // after an lgkmcnt wait: the MFMAs reading Bc cannot move above it
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) asm volatile("" : "+a"(Bc[j][pl]));
+    };
+    auto chain6b = [&](const u32x4_t (&ap)[3], int j) {
+      const bf16x8 a0 = __builtin_bit_cast(bf16x8, ap[0]), a1 = __builtin_bit_cast(bf16x8, ap[1]),
+                   a2 = __builtin_bit_cast(bf16x8, ap[2]);
+      const bf16x8 b0 = __builtin_bit_cast(bf16x8, Bc[j][0]), b1 = __builtin_bit_cast(bf16x8, Bc[j][1]),
+                   b2 = __builtin_bit_cast(bf16x8, Bc[j][2]);
+      f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b0, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b2, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b0, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b1, c, 0, 0, 0);
+      return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, c, 0, 0, 0);
+    };
+    auto split_e = [&](const f32x4 (&r)[2], u32x4_t (&P)[3], int e) {   // pair e of the lane's 8 values
       const float x = e < 2 ? r[0][2 * e] : r[1][2 * e - 4], y = e < 2 ? r[0][2 * e + 1] : r[1][2 * e - 3];
       uint32_t h, m, l;
       split_pair(x, y, h, m, l);
-      P[i][0][e] = h;
-      P[i][1][e] = m;
-      P[i][2][e] = l;
+      P[0][e] = h;
+      P[1][e] = m;
+      P[2][e] = l;
     };
-    auto planes = [&](int i, bf16x8 (&ap)[3]) {
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl) ap[pl] = __builtin_bit_cast(bf16x8, P[i][pl]);
-    };
-    auto chain6 = [&](const bf16x8 (&ap)[3], const bf16x8 (&bp)[3]) {
-      f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[2], bp[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[1], bp[1], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[0], bp[2], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[1], bp[0], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[0], bp[1], c, 0, 0, 0);
-      return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[0], bp[0], c, 0, 0, 0);
-    };
-    // four scalar adds (not v_pk_add_f32: filler price; this translation unit is built without SLP),
-    // each pinned to the iteration it is written in by an empty volatile asm on its result (without
-    // it the adds were sunk to the end of the step).  The adds themselves stay compiler code: they
-    // read MFMA results, and only the compiler's hazard recognizer inserts the MFMA -> VALU wait
-    // states (it does not see into inline asm).
+    // fresh-accumulator adds: plain (the compiler's MFMA -> VALU hazard waits apply), pinned to their
+    // column tile by an empty volatile asm (unpinned they were sunk to the end of the step)
     auto add4 = [&](f32x4& s, const f32x4& c) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -791,70 +917,61 @@ __global__ void __launch_bounds__(SPL == 3 ? 256 : RT) conv_ring_kernel(ConvArgs
         s[e] = v;
       }
     };
-    // prologue: B(0), A(0), A(1); A(0)'s group-0 rows split (group 1's: during step 0, group 0)
-    issue_b(bring);
+    // prologue: A(0), B(0); B(0) into the AGPRs; A(0) row 0 split; then B(1), A(1)
     issue(aring);
-    issue(aring + ABYTES);
+    issue_b(bring);
     wait_vmcnt<0>();
     ring_barrier();
 #pragma unroll
-    for (int i = 0; i < IG; ++i) {
+    for (int j = 0; j < RN; ++j) ld_bc(j, bring);
+    u32x4_t PA[3], PB[3];
+    {
       f32x4 r[2];
-      rd_a1(r, aring, i);
+      rd_a1(r, aring, 0);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) split_e(r, i, e);
+      for (int e = 0; e < 4; ++e) split_e(r, PA, e);
     }
+    issue_b(bring + BBYTES);
+    issue(aring + ABYTES);
     for (int t = 0; t < nk; ++t) {
-      if (t > 0) {
-        wait_vmcnt<APW>();                                   // B(t) landed (A(t+1) may be in flight)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of step t-1 are done
-        ring_barrier();
-      }
-      const char* bimg = bring + (t & 1) * BBYTES;
-      issue_b(bring + ((t + 1) & 1) * BBYTES);               // B(t+1) into B(t-1)'s slot
+      const char* acur = aring + (t & 1) * ABYTES;
+      const char* anext = aring + ((t + 1) & 1) * ABYTES;
+      const char* bnext = bring + ((t + 1) & 1) * BBYTES;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // B(t)'s fragments have landed in the AGPRs
+      fence_bc();
 #pragma unroll
-      for (int gr = 0; gr < NGR; ++gr) {
-        __builtin_amdgcn_sched_barrier(0);
-        const int sg = gr == 0 ? NGR - 1 : gr - 1;           // row group split during this group
-        const char* asrc;
-        if (gr == 0) {
-          asrc = aring + (t & 1) * ABYTES;                   // A(t), its last group's rows
-        } else {
-          wait_vmcnt<BPW>();                                 // A(t+1) landed (B(t+1) may be in flight)
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // group 0's reads of A(t)'s slot done
+      for (int i = 0; i < RM; ++i) {
+        u32x4_t (&Pc)[3] = (i & 1) ? PB : PA;               // row i's planes (split during row i-1)
+        u32x4_t (&Pn)[3] = (i & 1) ? PA : PB;               // row i+1's (or A(t+1)'s row 0)
+        if (i == RM - 1) {
+          wait_vmcnt<0>();                                   // B(t+1), A(t+1) (issued in step t-1)
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of B(t) / A(t) done
+          ring_barrier();
+          issue_b(bring + (t & 1) * BBYTES);                 // B(t+2) into B(t)'s slot
           issue(aring + (t & 1) * ABYTES);                   // A(t+2) into A(t)'s slot
-          asrc = aring + ((t + 1) & 1) * ABYTES;
         }
-        f32x4 ra[IG][2];
-#pragma unroll
-        for (int ii = 0; ii < IG; ++ii) rd_a1(ra[ii], asrc, sg * IG + ii);
-        bf16x8 ap[IG][3];
-#pragma unroll
-        for (int ii = 0; ii < IG; ++ii) planes(gr * IG + ii, ap[ii]);
-        bf16x8 bq[2][3];
-        rd_b(bq[0], bimg, 0);
-        f32x4 cp[IG];
+        f32x4 ra[2];
+        rd_a1(ra, i < RM - 1 ? acur : anext, i < RM - 1 ? i + 1 : 0);
+        f32x4 cp;
 #pragma unroll
         for (int j = 0; j < RN; ++j) {
           __builtin_amdgcn_sched_barrier(0);
-          if (j + 1 < RN) rd_b(bq[(j + 1) & 1], bimg, j + 1);
-          f32x4 cn[IG];
-#pragma unroll
-          for (int ii = 0; ii < IG; ++ii) cn[ii] = chain6(ap[ii], bq[j & 1]);
-          if (j > 0) {
-#pragma unroll
-            for (int ii = 0; ii < IG; ++ii) add4(acc[gr * IG + ii][j - 1], cp[ii]);
-          }
-          split_e(ra[j >> 2], sg * IG + (j >> 2), j & 3);
-#pragma unroll
-          for (int ii = 0; ii < IG; ++ii) cp[ii] = cn[ii];
+          const f32x4 cn = chain6b(Pc, j);
+          if (j > 0) add4(acc[i][j - 1], cp);
+          if (j & 1) split_e(ra, Pn, j >> 1);
+          if (i == RM - 1 && j > 0) ld_bc(j - 1, bnext);     // B(t+1) column j-1: its MFMAs are 6+ back
+          cp = cn;
         }
         __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int ii = 0; ii < IG; ++ii) add4(acc[gr * IG + ii][RN - 1], cp[ii]);
+        add4(acc[i][RN - 1], cp);
       }
+      // the last column's B(t+1) fragments, behind its MFMAs (srcB read early in an MFMA; the nops
+      // keep the asm overwrite clear of them)
+      asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
+      ld_bc(RN - 1, bnext);
     }
     wait_vmcnt<0>();   // drain the zero-fill steps before the workgroup may exit
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   } else if constexpr (SPB) {
     // Software-pipelined split-fp32 loop.  A (activations, fp32) and B (pre-split weight planes) have
     // their own rings: A in NSA slots, B in NSB.  Step t's MFMAs use A planes split during step t-1
@@ -3056,6 +3173,12 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
 // beside MFMAs (MI355X_MICROARCH.md, filler prices)
 void es_spb4_launch(int mode, bool sp, const ConvArgs& a, dim3 grid, hipStream_t st) {
   (void)sp;   // (sub-pixel convs only, see launch_ring)
+  if (a.a_planes) {   // pre-split operand planes (SPA)
+    if (mode == MODE_FWD) hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 128, true, 64, float, 4>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((conv_ring_kernel<MODE_DGRAD, 256, 128, true, 64, float, 4>), grid, dim3(256), 0, st, a);
+    g_planes_req.used = 1;
+    return;
+  }
   if (mode == MODE_FWD) hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 128, true, 64, float, 3>), grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((conv_ring_kernel<MODE_DGRAD, 256, 128, true, 64, float, 3>), grid, dim3(256), 0, st, a);
 }
@@ -3069,10 +3192,9 @@ template <int MODE, int BM, int BN, bool SP, int BK = 64, typename T = bf16, int
 void launch_ring(const ConvArgs& a, int row_tiles, hipStream_t st) {
   dim3 grid(row_tiles, (a.Ng + BN - 1) / BN, 1);
   ++g_conv_launches;
-  // the 4-wave kernel for the sub-pixel convs (conv_layers.0 / .5 at B = 1024, tools/mb_spb4.py r04b:
-  // FWD 1.06-1.11x, DGRAD 0.997-1.07x); the plain conv_layers.9 DGRAD measured 0.89x, so it keeps SPB
+  // the 4-wave kernel (opt-in, see g_spb4) for the sub-pixel convs; a planes operand requires it
   if constexpr (SPL == 2 && BM == 256 && BN == 128 && SP) {
-    if (g_spb4 && a.ng == 64) {   // (the 4-wave kernel: one pixel x 64 images per wave)
+    if ((g_spb4 || a.a_planes) && a.ng == 64) {   // (the 4-wave kernel: one pixel x 64 images per wave)
       es_spb4_launch(MODE, SP, a, grid, st);
       return;
     }
@@ -3365,7 +3487,8 @@ int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
       return 1;
     }
   }
-  const bool big = !shortk && (int64_t)NGI * a.ng * PQ / 256 * nt128 >= 768;   // >= 3 rounds of 256-row tiles
+  // >= 3 rounds of 256-row tiles; the planes operand (SPA) exists for the 256 x 128 4-wave kernel only
+  const bool big = !shortk && ((int64_t)NGI * a.ng * PQ / 256 * nt128 >= 768 || a.a_planes);
   const int BM = big ? 256 : 128, NB = BM / a.ng;
   int row_tiles = NGI * ((PQ + NB - 1) / NB);
   if (sp_weights) {
@@ -3420,7 +3543,7 @@ int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
       static const bool bn64 = [] { const char* e = getenv("ES_SPB_BN64"); return e && e[0] == '1'; }();
       if (a.Ng % 128 == 0 && !bn64) {
         dim3 grid(row_tiles, 4 * a.Ng / 128, 1);
-        if (g_spb4 && a.ng == 64) es_spb4_launch(MODE_FWD, true, a, grid, st);
+        if ((g_spb4 || a.a_planes) && a.ng == 64) es_spb4_launch(MODE_FWD, true, a, grid, st);
         else hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 128, true, 64, T, 2>), grid, dim3(RT), 0, st, a);
       } else {
         dim3 grid(row_tiles, 4 * a.Ng / 64, 1);
@@ -3517,7 +3640,8 @@ int es_conv_ring_launch_f32(ConvArgs& a, int mode, hipStream_t st) {
   const es_conv_desc_t& d = a.d;
   if (mode == MODE_WGRAD || d.hmap != nullptr || d.stride > 2 || a.splitk) return d.subpixel ? -1 : 0;
   const int N = d.N;
-  const int nc = chunk_images(a.as[0] * 4, N);
+  const int ea = a.a_planes ? 6 : 4;   // bytes per value of the gathered operand
+  const int nc = chunk_images(a.as[0] * ea, N);
   const int esz = a.out_bf16 ? 2 : 4;
   const StatsRequest req = g_stats_req;
   int used = 0;
@@ -3525,7 +3649,7 @@ int es_conv_ring_launch_f32(ConvArgs& a, int mode, hipStream_t st) {
   for (int n0 = 0; n0 < N; n0 += nc) {
     ConvArgs c = a;
     c.d.N = std::min(nc, N - n0);
-    c.a_src = (const char*)a.a_src + (int64_t)n0 * a.as[0] * 4;
+    c.a_src = (const char*)a.a_src + (int64_t)n0 * a.as[0] * ea;
     c.out = (char*)a.out + (int64_t)n0 * a.os[0] * esz;
     c.M = mode == MODE_FWD ? c.d.N * d.P * d.Q : (a.fold ? c.d.N * d.H * d.W : c.d.N * d.Hu * d.Wu);
     if (req.part) g_stats_req = StatsRequest{req.part + (int64_t)used * 3 * a.Ng, req.floats - (int64_t)used * 3 * a.Ng, 0};

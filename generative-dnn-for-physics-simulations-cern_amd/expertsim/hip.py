@@ -98,6 +98,9 @@ _SIGS = {
     "es_conv_set_f32_split": (C.c_int, [C.c_int]),
     "es_weight_planes_offset": (C.c_int64, [C.c_int64]),
     "es_pack_weight_planes": (C.c_int, [P, C.c_int64, P, P]),
+    "es_split_planes": (C.c_int, [P, C.c_int64, C.c_int, P, P]),
+    "es_conv2d_fwd_planes": (C.c_int, [P, P, P, P, P, P, C.c_int, P, P, I64, P, P]),
+    "es_conv2d_dgrad_planes": (C.c_int, [P, P, P, P, P, C.c_int, P, P]),
     "es_conv_launch_count": (C.c_int64, []),
     "es_conv_exec_flops": (C.c_int, [C.POINTER(C.c_double), C.c_int]),
     "es_conv_set_spb4": (C.c_int, [C.c_int]),

@@ -335,10 +335,11 @@ class ConvOp:
         return bool(hip.lib().es_conv_subpixel_ok(C.byref(d), hip.dt_of_dtype(dtype)))
 
     def fwd(self, x: Act, out_dtype=None, inv_scale=None, out: Act = None, with_bias=True,
-            bn_stats=False) -> Act:
+            bn_stats=False, planes=None) -> Act:
         """bn_stats: also ask for the BatchNorm partials of the output (es_conv2d_fwd_stats); when
         the kernel provides them, out.bn_part = (part, chunks) and NormOp.stats merges those instead
-        of re-reading the output."""
+        of re-reading the output.  planes: x's es_split_planes image (fp32 split-fp32 sub-pixel convs:
+        the kernel reads it instead of splitting x; es_conv2d_fwd_planes)."""
         d = self.desc(x)
         cdt = x.t.dtype
         if self.subpixel(d, cdt):
@@ -350,7 +351,19 @@ class ConvOp:
             out = Act.nhwc(d.N, d.K, d.P, d.Q, out_dtype or cdt, x.t.device)
         bias = self.bias if (with_bias and self.bias is not None) else None
         with _probed(self.label and self.label + ".fwd"):
-            if bn_stats:
+            if planes is not None:
+                assert d.subpixel == 1 and cdt == torch.float32, "planes: fp32 sub-pixel convs only"
+                part, floats, chunks = None, 0, C.c_int(0)
+                if bn_stats:
+                    tiles = ((d.N + 7) // 8) * (d.P * d.Q // 16 + 8) + ((d.N + 63) // 64) * (d.P * d.Q // 2 + 8)
+                    floats = tiles * 3 * d.K
+                    part = torch.empty(floats, dtype=torch.float32, device=x.t.device)
+                hip.call("es_conv2d_fwd_planes", C.byref(d), hip.ptr(planes), hip.strides4(x.strides), hip.ptr(wk),
+                         hip.ptr(bias), out.ptr, out.dt, hip.strides4(out.strides), hip.ptr(part), floats,
+                         C.byref(chunks), hip.stream_ptr())
+                if bn_stats and chunks.value > 0:
+                    out.bn_part = (part, chunks.value)
+            elif bn_stats:
                 # >= the ring's row tiles for every image-group size it may pick (8..64)
                 tiles = ((d.N + 7) // 8) * (d.P * d.Q // 16 + 8) + ((d.N + 63) // 64) * (d.P * d.Q // 2 + 8)
                 floats = tiles * 3 * d.K
@@ -380,7 +393,7 @@ class ConvOp:
                 and out.t.dtype == torch.float32 and ng <= 4096)
 
     def dgrad(self, dy: Act, x: Act, dx_dtype=None, inv_scale=None, dx: Act = None, beta=0.0,
-              bn_reduce=None) -> Act:
+              bn_reduce=None, planes=None) -> Act:
         """Gradient w.r.t. the conv input x (folded through the upsample when present).
 
         bn_reduce = (norm, h, stats, chain): x = chain(norm(h)) is a BatchNorm + dropout + activation
@@ -403,7 +416,11 @@ class ConvOp:
                     and bn_reduce[0].kind == hip.NORM_BN and bn_reduce[1].t.dtype == ddt == cdt
                     and bn_reduce[1].dims == dx.dims and tuple(bn_reduce[1].strides) == tuple(dx.strides))
             with _probed(self.label and self.label + ".dgrad"):
-              if fuse:
+              if planes is not None:   # dy's es_split_planes image (es_conv2d_dgrad_planes)
+                  assert d.subpixel == 1 and cdt == torch.float32 and float(beta) == 0.0, "planes: fp32 sub-pixel"
+                  hip.call("es_conv2d_dgrad_planes", C.byref(d), hip.ptr(planes), hip.strides4(dy.strides),
+                           hip.ptr(wd), dx.ptr, dx.dt, hip.strides4(dx.strides), hip.stream_ptr())
+              elif fuse:
                   norm, h, stats, chain = bn_reduce
                   nm = norm.norm_struct(*stats)
                   floats = 2048 * 3 * Cc      # >= the thin dgrad's blocks (<= 2048) / persistent workgroups
@@ -479,6 +496,17 @@ class ConvOp:
         if db_out is not None:
             channel_sum(dy, db_out, beta)
         return dwk
+
+
+def split_planes(x: Act, out: torch.Tensor = None) -> torch.Tensor:
+    """x's split-fp32 planes image (es_split_planes): dense NHWC fp32, C % 32 == 0 -> bf16 tensor of
+    [N*H*W][C/32][3][32] values (6 bytes per value)."""
+    N, Cc, H, W = x.dims
+    assert x.t.dtype == torch.float32 and Cc % 32 == 0 and tuple(x.strides) == (H * W * Cc, 1, W * Cc, Cc)
+    if out is None:
+        out = torch.empty(N * H * W * Cc * 3, dtype=torch.bfloat16, device=x.t.device)
+    hip.call("es_split_planes", x.ptr, N * H * W, Cc, hip.ptr(out), hip.stream_ptr())
+    return out
 
 
 def channel_sum(x: Act, out: torch.Tensor, beta=1.0):

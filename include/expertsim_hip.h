@@ -191,6 +191,22 @@ int es_conv_set_f32_split(int on);
  * kernels' fragments.  Same weights as es_pack_conv_weight (neutron generator.py:24,29,33). */
 int64_t es_weight_planes_offset(int64_t n);
 int es_pack_weight_planes(const float* packed, int64_t n, void* base, es_stream_t stream);
+/* Split-fp32 planes of an fp32 activation image [rows][C] (C % 32 == 0): out [rows][C / 32][3][32] bf16,
+ * each 32-channel block as the weight planes above (x0 = rne(x), x1 = rne(x - x0), x2 = x - x0 - x1, k
+ * permuted as the ring kernels' fragments), 6 bytes per value.  The FWD / DGRAD *_planes entries read
+ * their gathered operand from it instead of splitting it in the kernel.  Same values as the fp32
+ * activations of neutron generator.py:24,29 (conv_layers.0 / .5 inputs and output gradients). */
+int es_split_planes(const float* x, int64_t rows, int C, void* planes, es_stream_t stream);
+/* es_conv2d_fwd (part == NULL) / es_conv2d_fwd_stats and es_conv2d_dgrad (beta 0) in fp32 whose
+ * gathered operand (x, resp. dy) is given as its es_split_planes image (xs / ys: the strides of the
+ * fp32 image in values): the split-fp32 kernels then read the planes instead of splitting in the
+ * kernel (same products, same order, bitwise the same output).  Sub-pixel convs (d->subpixel) on the
+ * 4-wave path only; error otherwise.  neutron generator.py:24,29 (conv_layers.0 / .5). */
+int es_conv2d_fwd_planes(const es_conv_desc_t* d, const void* xp, const int64_t xs[4], const void* wk,
+                         const float* bias, void* y, es_dtype_t ydt, const int64_t ys[4], float* part,
+                         int64_t part_floats, int* chunks, es_stream_t stream);
+int es_conv2d_dgrad_planes(const es_conv_desc_t* d, const void* dyp, const int64_t ys[4], const void* wd, void* dx,
+                           es_dtype_t dxdt, const int64_t dxs[4], es_stream_t stream);
 /* Host-side count of MFMA conv kernels issued so far (ring / persistent / p256 / fp32 WGRAD).
  * Instrumentation only: lets a profiler state how many kernel launches one conv op was. */
 int64_t es_conv_launch_count(void);

