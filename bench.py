@@ -38,8 +38,7 @@ STEP_FLOP_PER_IMAGE = {"neutron": 10.573e9, "proton": 28.566e9, "neutron56": 16.
 PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
 # split-fp32 (train.fp32_mfma: split): one fp32 product = 6 bf16 plane products, all executed on the
 # bf16 MFMA pipe, so the roofline of a split kernel is the EXECUTED bf16 work against the 2.5 PF/s
-# dense bf16 peak (no derived "split peak")
-SPLIT_PRODUCTS = 6
+# dense bf16 peak (no derived "split peak"); the executed work is the library's own tally
 # timed loop: at most this many replayed steps queued ahead of the GPU (a replay is ~1000 AQL packets;
 # an unbounded loop queued ~10.5k packets, which is where a profiled run aborted, profiles/r03t_*)
 MAX_INFLIGHT = 2
@@ -55,9 +54,6 @@ def traffic_json(arch, batch, precision, mode):
     return p if os.path.exists(p) else None
 
 
-# executed / algorithmic MACs of the x2-upsample convs on the sub-pixel path (conv_layers.5: the
-# 3x3 conv over the upsampled map becomes four 2x2 convs on the source grid, 16 / 36 MACs)
-SUBPIXEL_MAC_RATIO = 4.0 / 9.0
 
 
 def workload_label(arch, E, batch, world):
@@ -79,14 +75,21 @@ def workload_label(arch, E, batch, world):
             f"E={E}, B={batch} per GPU, global {gb} ({k})")
 
 
+# Forward FLOPs per image of the probed generator convs (= the algorithmic count charged to each of
+# their fwd / dgrad / wgrad ops, as torch's flop counter does), by (arch, op key)
+PROBED = {
+    "neutron": {"c5": 2 * 46 * 46 * 128 * (256 * 9)},      # conv_layers.5: 256x48x48 -> 128x46x46, k3
+    "neutron56": {"c5": 2 * 58 * 58 * 128 * (256 * 9)},    # conv_layers.5: 256x60x60 -> 128x58x58, k3
+    # conv_layers.1: 512x36x20 (x2 upsample of 18x10) -> 256x35x19, k4 p1 (sub-pixel split ring);
+    # conv_layers.5: 256x56x30 (resize of 35x19) -> 128x55x29, k4 p1 (register-staged fp32 MFMA)
+    "proton": {"c1": 2 * 35 * 19 * 256 * (512 * 16), "c5": 2 * 55 * 29 * 128 * (256 * 16)},
+}
+LAYER_NAME = {"c1": "conv_layers.1", "c5": "conv_layers.5"}
+
+
 def conv_flops_per_image(arch):
-    """Forward FLOPs of the dominant generator conv per image (= the algorithmic count charged to
-    each of its fwd / dgrad / wgrad launches, as torch's flop counter does)."""
-    if arch == "neutron":   # conv_layers.5: 256x48x48 -> 128x46x46, k3
-        return 2 * 46 * 46 * 128 * (256 * 9)
-    if arch == "neutron56":  # conv_layers.5: 256x60x60 -> 128x58x58, k3
-        return 2 * 58 * 58 * 128 * (256 * 9)
-    return 2 * 55 * 29 * 128 * (256 * 16)   # proton conv_layers.5: 256x56x30 -> 128x55x29, k4 p1
+    """Algorithmic forward FLOPs per image of the arch's conv_layers.5 (the headline's roofline conv)."""
+    return PROBED[arch]["c5"]
 
 
 FP32_MFMA = "split"   # train.fp32_mfma of the fp32 line (--fp32-mfma)
@@ -205,19 +208,6 @@ def make_step(moe, step_args, use_graph):
     return sg.replay, sg
 
 
-def exec_profile(arch, precision):
-    """(executed MACs / the reference's MACs, MFMA products per reference product, MFMA pipe) of the
-    roofline kernel, the generator's conv_layers.5: a x2-upsample 3x3 conv run as 4 parity-class
-    2x2 convs on the source grid (sub-pixel: 16 of 36 taps), bf16 or split-fp32 (6 bf16 plane products
-    per fp32 product) on the bf16 pipe, or exact fp32 MFMA; proton's conv_layers.5 (non-integer
-    resize) runs on the generic kernels without the sub-pixel reduction."""
-    ratio = 1.0 if arch == "proton" else SUBPIXEL_MAC_RATIO
-    split = precision == "fp32" and FP32_MFMA == "split" and arch != "proton"
-    if precision == "bf16":
-        return ratio, 1, "bf16"
-    return (ratio, SPLIT_PRODUCTS, "bf16") if split else (ratio, 1, "fp32")
-
-
 def exec_flops(reset=False):
     """Host tally of the executed conv MFMA work (es_conv_exec_flops): [bf16 pipe, fp32 MFMA, VALU]."""
     import ctypes
@@ -228,12 +218,15 @@ def exec_flops(reset=False):
 
 
 def probe_dominant(moe, eager_step, steps, arch, batch, precision):
-    """Per-launch HIP events around the dominant conv's launches (on its launch stream) over
-    eager steps of the same model and batch -> the roofline object; the same steps' executed conv
-    MFMA work (es_conv_exec_flops) -> the step's executed MFMA fraction."""
+    """Per-launch HIP events around the probed generator convs' ops (on their launch stream) over eager
+    steps of the same model and batch -> the roofline object of the op with the largest total time.
+    Executed MFMA work per op comes from the library's own tally (es_conv_exec_flops, read around each
+    op: sub-pixel 4-class convs, split-fp32's 6 plane products, exact fp32 MFMA), so `achieved` is
+    executed FLOPs / kernel time against the dense peak of the pipe the op ran on."""
     import torch
     from expertsim import layers
-    probe = layers.KernelProbe(["G0.c5.fwd", "G0.c5.dgrad", "G0.c5.wgrad"])
+    keys = list(PROBED[arch])
+    probe = layers.KernelProbe([f"G0.{k}.{m}" for k in keys for m in ("fwd", "dgrad", "wgrad")])
     layers.set_probe(probe)
     exec_flops(reset=True)
     for _ in range(steps):
@@ -242,45 +235,50 @@ def probe_dominant(moe, eager_step, steps, arch, batch, precision):
     ef = [v / steps for v in exec_flops(reset=True)]
     layers.set_probe(None)
     stats = probe.summary()
-    flops = conv_flops_per_image(arch) * batch
+
+    def rate(label, v):
+        alg = PROBED[arch][label.split(".")[1]] * batch
+        ex = v.get("exec_flops_per_op", [alg, 0.0, 0.0])
+        pipe = "bf16" if ex[0] >= ex[1] else "fp32"
+        exe = ex[0] if pipe == "bf16" else ex[1]
+        t = v["avg_ms"] * 1e-3
+        return alg, exe, pipe, exe / t / 1e12, alg / t / 1e12
     dom = max(stats, key=lambda k: stats[k]["total_ms"])
+    alg, exe, pipe, achieved, alg_rate = rate(dom, stats[dom])
     avg_ms = stats[dom]["avg_ms"]
-    ratio, products, pipe = exec_profile(arch, precision)
-    exec_per_launch = flops * ratio * products
-    achieved = exec_per_launch / (avg_ms * 1e-3) / 1e12
-    alg_rate = flops / (avg_ms * 1e-3) / 1e12
-    split = products > 1
     peak = PEAK_TFLOPS[pipe]
+    layer = LAYER_NAME[dom.split(".")[1]]
+    split = precision == "fp32" and pipe == "bf16"
     traffic, tnote, mfma_busy = None, None, None
-    tj_path = traffic_json(arch, batch, precision, dom.split(".")[-1])
+    tj_path = traffic_json(arch, batch, precision, dom.split(".")[-1]) if dom.split(".")[1] == "c5" else None
     if tj_path:
         tj = json.load(open(tj_path))
         traffic = tj["traffic_bytes"]
         mfma_busy = tj.get("mfma_busy_frac")
         tnote = (f"HBM bytes per op: FETCH_SIZE x2 {tj['fetch_bytes']} + WRITE_SIZE {tj['write_bytes']} "
                  f"(algorithmic {tj['algorithmic_bytes']}), {os.path.relpath(tj_path, ROOT)}")
-    kname = ("conv_ring bf16" if precision == "bf16" else
-             "conv_ring split-fp32, 6 x v_mfma_f32_16x16x32_bf16 per fp32 product" if split else
-             "conv_ring fp32, v_mfma_f32_16x16x4_f32")
-    return {"bound": "mfma", "kernel": f"{dom} (generator conv_layers.5, {kname})",
+    kname = ("bf16 MFMA" if precision == "bf16" else
+             "split-fp32, 6 x v_mfma_f32_16x16x32_bf16 per fp32 product" if split else
+             "fp32, v_mfma_f32_16x16x4_f32")
+    return {"bound": "mfma", "kernel": f"{dom} (generator {layer}, {kname})",
             "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_note": tnote,
             "achieved_fp32_equiv_alg": round(alg_rate, 2),
-            "note": f"achieved = EXECUTED MFMA FLOPs per launch ({exec_per_launch:.4g} = the reference's 3x3-conv "
-                    f"FLOPs {flops:.4g} x {ratio:.4f} sub-pixel MAC ratio x {products} MFMA products per "
-                    f"reference product) / kernel time, against the dense {pipe} MFMA peak {peak} TFLOP/s "
-                    "(MI355X_MICROARCH.md); achieved_fp32_equiv_alg = the reference's FLOPs / kernel time "
-                    "(an algorithmic rate, not a utilisation)",
+            "note": f"achieved = EXECUTED MFMA FLOPs per op ({exe:.4g}, the library's tally es_conv_exec_flops "
+                    f"read around the op; the reference's FLOPs are {alg:.4g}: sub-pixel 4-class convs execute "
+                    f"es_subpixel_taps / 4RS of them, split-fp32 6 bf16 products per fp32 product) / op time, "
+                    f"against the dense {pipe} MFMA peak {peak} TFLOP/s (MI355X_MICROARCH.md); "
+                    "achieved_fp32_equiv_alg = the reference's FLOPs / op time (an algorithmic rate, not a utilisation)",
             "mfma_busy_pmc": mfma_busy,
-            "flop_per_launch": flops, "exec_flop_per_launch": exec_per_launch,
+            "flop_per_launch": alg, "exec_flop_per_launch": exe,
             "avg_ms": round(avg_ms, 4), "launches": stats[dom]["count"],
             "step_exec_flops": {"bf16_pipe": ef[0], "fp32_mfma": ef[1], "valu_thin": ef[2]},
             "kernel_launches_per_op": stats[dom].get("kernel_launches_per_op"),
             "launch_note": "avg_ms is per op; an fp32 op over > 1 GiB operands runs as image chunks "
                            "(kernel_launches_per_op MFMA kernels, rocprof lists each chunk separately)",
-            "all_probed": {k: {"avg_ms": round(v["avg_ms"], 4), "kernels": v.get("kernel_launches_per_op"),
-                               "exec_tflops": round(exec_per_launch / (v["avg_ms"] * 1e-3) / 1e12, 2),
-                               "frac": round(exec_per_launch / (v["avg_ms"] * 1e-3) / 1e12 / peak, 4)}
+            "all_probed": {k: (lambda r: {"avg_ms": round(v["avg_ms"], 4), "kernels": v.get("kernel_launches_per_op"),
+                                          "pipe": r[2], "exec_tflops": round(r[3], 2),
+                                          "frac": round(r[3] / PEAK_TFLOPS[r[2]], 4)})(rate(k, v))
                            for k, v in stats.items()}}
 
 

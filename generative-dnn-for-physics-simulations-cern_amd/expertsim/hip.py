@@ -142,6 +142,7 @@ _SIGS = {
     "es_dmlp_bwd": (C.c_int, [P, I64, C.c_int, C.c_int, P, P, P, P, P, P, P, P, P, I64, P, P, P, P, P, P, P, P, P,
                               P, P, P]),
     "es_upsample_bwd": (C.c_int, [P, C.c_int, P, P, P, P, P, P, C.c_int, P, C.c_float, P]),
+    "es_upsample_fwd": (C.c_int, [P, C.c_int, P, P, P, P, P, P]),
     "es_copy": (C.c_int, [P, C.c_int, P, P, C.c_int, P, C.c_float, C.c_float, P]),
     "es_avgpool_fwd": (C.c_int, [P, C.c_int, P, P, P, P]),
     "es_avgpool_bwd": (C.c_int, [P, P, P, C.c_int, P, C.c_float, P]),

@@ -95,6 +95,7 @@ class KernelProbe:
         self.targets = set(targets)
         self.events = {t: [] for t in targets}
         self.launches = {t: [] for t in targets}   # MFMA conv kernels issued per probed op
+        self.exec = {t: [] for t in targets}       # executed FLOPs per op [bf16 pipe, fp32 MFMA, VALU]
 
     def wants(self, label):
         return label in self.targets
@@ -104,10 +105,12 @@ class KernelProbe:
         ev.record()
         return ev
 
-    def add(self, label, start, end, launches=None):
+    def add(self, label, start, end, launches=None, exec_flops=None):
         self.events[label].append((start, end))
         if launches is not None:
             self.launches[label].append(launches)
+        if exec_flops is not None:
+            self.exec[label].append(exec_flops)
 
     def summary(self):
         torch.cuda.synchronize()
@@ -118,6 +121,8 @@ class KernelProbe:
                 out[k] = {"count": len(ms), "total_ms": sum(ms), "avg_ms": sum(ms) / len(ms)}
                 if self.launches[k]:
                     out[k]["kernel_launches_per_op"] = max(self.launches[k])
+                if self.exec[k]:
+                    out[k]["exec_flops_per_op"] = [max(e[i] for e in self.exec[k]) for i in range(3)]
         return out
 
 
@@ -137,11 +142,22 @@ class _probed:
     def __enter__(self):
         if self.on:
             self.n0 = hip.lib().es_conv_launch_count()
+            self.f0 = _exec_tally()
             self.t0 = _PROBE.record(self.label)
 
     def __exit__(self, *exc):
         if self.on:
-            _PROBE.add(self.label, self.t0, _PROBE.record(self.label), hip.lib().es_conv_launch_count() - self.n0)
+            t1 = _PROBE.record(self.label)
+            f1 = _exec_tally()
+            _PROBE.add(self.label, self.t0, t1, hip.lib().es_conv_launch_count() - self.n0,
+                       [b - a for a, b in zip(self.f0, f1)])
+
+
+def _exec_tally():
+    """The host tally of executed conv MFMA work so far (es_conv_exec_flops): [bf16 pipe, fp32 MFMA, VALU]."""
+    out = (C.c_double * 3)()
+    hip.call("es_conv_exec_flops", out, 0)
+    return list(out)
 
 
 def copy_act(src: Act, dst: Act, alpha=1.0, beta=0.0):
@@ -271,15 +287,44 @@ class ConvOp:
         self.pad = pad
         self.up = upsample
         self.label = None
+        # a non-integer nearest resize (the proton generator's 35x19 -> 56x30 before conv_layers.5):
+        # the resized input is materialised (es_upsample_fwd) and the conv runs as a plain conv on it,
+        # on the ring kernels (the gather-map conv only runs on the generic register-staged kernels)
+        self._plain = None
+        if upsample is not None and upsample.factor is None and os.environ.get("ES_RESIZE_MAT", "1") != "0":
+            self._plain = ConvOp(weight, bias, stride=stride, pad=pad, upsample=None)
         w = weight
         self.K = w.shape[0]
         self.C = w.shape[1]
         self.R = w.shape[2] if w.dim() == 4 else 1
         self.S = w.shape[3] if w.dim() == 4 else 1
         self._packed = {}
+        if self._plain is not None:
+            self._plain._packed = self._packed   # same weights, same packings (modes 0 / 1)
 
     def invalidate(self):
         self._packed.clear()
+
+    def _resized(self, x: Act) -> bool:
+        """Materialise the resize for this call: dense NHWC input with 16-byte channel chunks."""
+        if self._plain is None:
+            return False
+        N, Cc, H, W = x.dims
+        vec = 4 if x.t.dtype == torch.float32 else 8
+        return Cc % vec == 0 and tuple(x.strides) == (H * W * Cc, 1, W * Cc, Cc)
+
+    def _resize(self, x: Act) -> Act:
+        N, Cc, H, W = x.dims
+        Hu, Wu = self.up.out_hw
+        xu = Act.nhwc(N, Cc, Hu, Wu, x.t.dtype, x.t.device)
+        maps = self.up.device_maps(x.t.device)
+        hip.call("es_upsample_fwd", C.byref(x.view), x.dt, x.ptr, hip.ptr(maps[0]), hip.ptr(maps[1]),
+                 C.byref(xu.view), xu.ptr, hip.stream_ptr())
+        return xu
+
+    def _plain_op(self):
+        self._plain.label = self.label
+        return self._plain
 
     def packed(self, dtype, mode, inv_scale=None):
         """Packed GEMM weights; fp32 with split level 2 also carries the bf16 planes behind the fp32
@@ -340,6 +385,8 @@ class ConvOp:
         the kernel provides them, out.bn_part = (part, chunks) and NormOp.stats merges those instead
         of re-reading the output.  planes: x's es_split_planes image (fp32 split-fp32 sub-pixel convs:
         the kernel reads it instead of splitting x; es_conv2d_fwd_planes)."""
+        if planes is None and self._resized(x):
+            return self._plain_op().fwd(self._resize(x), out_dtype, inv_scale, out, with_bias, bn_stats)
         d = self.desc(x)
         cdt = x.t.dtype
         if self.subpixel(d, cdt):
@@ -441,9 +488,13 @@ class ConvOp:
                          dx.ptr, dx.dt, hip.strides4(dx.strides), float(beta), hip.stream_ptr())
             return dx
         dxu = Act.nhwc(N, Cc, d.Hu, d.Wu, torch.float32, dy.t.device)
-        with _probed(self.label and self.label + ".dgrad"):
-          hip.call("es_conv2d_dgrad", C.byref(d), dy.dt, dy.ptr, hip.strides4(dy.strides), hip.ptr(wd),
-                 dxu.ptr, dxu.dt, hip.strides4(dxu.strides), 0.0, hip.stream_ptr())
+        if self._resized(x):   # the plain conv's dgrad w.r.t. the materialised resized input
+            self._plain_op().dgrad(dy, Act(x.t, (N, Cc, d.Hu, d.Wu), (d.Hu * d.Wu * Cc, 1, d.Wu * Cc, Cc)),
+                                   dx_dtype=torch.float32, inv_scale=inv_scale, dx=dxu)
+        else:
+          with _probed(self.label and self.label + ".dgrad"):
+            hip.call("es_conv2d_dgrad", C.byref(d), dy.dt, dy.ptr, hip.strides4(dy.strides), hip.ptr(wd),
+                     dxu.ptr, dxu.dt, hip.strides4(dxu.strides), 0.0, hip.stream_ptr())
         if dx is None:
             dx = Act.nhwc(N, Cc, H, W, ddt, dy.t.device)
         maps = self.up.device_maps(dy.t.device)
@@ -455,6 +506,8 @@ class ConvOp:
     def wgrad(self, dy: Act, x: Act, dw_out: torch.Tensor = None, db_out: torch.Tensor = None,
               beta=1.0):
         """dW (torch layout, fp32) accumulated into dw_out (beta=1) or written (beta=0)."""
+        if self._resized(x):   # on the re-materialised resized input (not kept from the forward)
+            return self._plain_op().wgrad(dy, self._resize(x), dw_out, db_out, beta)
         d = self.desc(x)
         dev = dy.t.device
         assert dy.t.dtype == x.t.dtype, (dy.t.dtype, x.t.dtype)

@@ -436,8 +436,14 @@ int es_dmlp_bwd(const float* X, int64_t xs, int B, int F, const es_dmlp_params_t
                 const float* dlat, float* dX, int64_t dxs, float* part, float* dw1, float* db1, float* dg1,
                 float* dbe1, float* dw2, float* db2, float* dg2, float* dbe2, float* dw3, float* db3,
                 es_stream_t stream);
+/* Nearest resize gather y[n, :, hu, wu] = x[n, :, hmap[hu], wmap[wu]] (torch upsample_nearest2d's index
+ * maps; dense NHWC, C % 4 == 0 fp32 / % 8 bf16): the proton generator's 35x19 -> 56x30 resize feeding
+ * conv_layers.5 (proton/generator.py:33-34), materialised so that the conv runs on the ring kernels. */
+int es_upsample_fwd(const es_view_t* x, es_dtype_t dt, const void* xp, const int32_t* hmap, const int32_t* wmap,
+                    const es_view_t* y, void* yp, es_stream_t stream);
 /* dx[n,c,h,w] = beta*dx + sum over upsampled positions mapping to (h,w).  hstart/hcount (device
- * [H]) and wstart/wcount (device [W]) describe the contiguous preimage of each source row/col. */
+ * [H]) and wstart/wcount (device [W]) describe the contiguous preimage of each source row/col.
+ * Dense NHWC views with C % 4 == 0 take a vectorised kernel. */
 int es_upsample_bwd(const es_view_t* dxu, es_dtype_t dt, const void* dxup, const int32_t* hstart,
                     const int32_t* hcount, const int32_t* wstart, const int32_t* wcount,
                     const es_view_t* dx, es_dtype_t dxdt, void* dxp, float beta, es_stream_t stream);

@@ -51,7 +51,12 @@ CASE_TOL = {"proton_e3_b12": 1e-2}
 # proton 1.7e-5 (r03b).
 A_STEP0_TOL = {"neutron": 1e-2}
 A_ORACLE_TOL = {"neutron": 1e-2, "proton": 1e-3}
-STEP1_TOL = {"neutron": 0.25, "proton": 0.25}
+# step-1 gradients, per case: ~2x the fixed outcome of the deterministic fp32 mode (r04d, worst
+# parameter per case: neutron_e1_b8 1.6e-2 (A conv1.weight), neutron_e3_b12 0.127 (expert 1 A
+# conv1_bd.weight; B_e = 2-4 BatchNorm after Adam's +-lr first step), proton_e1_b8 0.093 (G
+# conv_layers.11.bias), proton_e3_b12 1.7e-2); round 3 held every case to 0.25
+STEP1_TOL = {"neutron_e1_b8": 0.05, "neutron_e3_b12": 0.25, "neutron_e3_b12_router": 0.25, "proton_e1_b8": 0.2,
+             "proton_e3_b12": 0.05}
 # noise-only set after Adam's +-lr first step: BatchNorm over B_e = 2 samples (neutron_e3 step 1
 # experts 0 and 2) has invstd up to ~1e3, so the analytically-zero bias sums cancel at ~1e-4
 # (measured 2.0e-5 and 1.06e-4 on fc1.0.bias)
@@ -133,7 +138,7 @@ def test_step_gradients_match_reference(case):
         torch.cuda.synchronize()
         want = {k.split("/")[1] for k in g.keys(f"s{s}/") if "/grad/" in k}
         assert set(store) == want, (s, sorted(store), sorted(want))
-        tol = CASE_TOL.get(case, TOL[g.arch]) if s == 0 else STEP1_TOL[g.arch]
+        tol = CASE_TOL.get(case, TOL[g.arch]) if s == 0 else STEP1_TOL[case]
         for label, grads in store.items():
             comp = label[3]
             lt = max(tol, A_STEP0_TOL.get(g.arch, 0.0)) if comp == "A" and s == 0 else tol

@@ -9,9 +9,13 @@ Tolerances (derived from the reference's own 1-vs-8-thread dri
   step 1: the same quantities <= STEP1_TOL[case] relative.  Adam's first step moves every
           parameter by ~+-lr whatever its gradient's size, so rounding-level differences that flip
           the sign of a tiny gradient (e.g. a ReLU-threshold pixel) become +-lr parameter moves.
-          The tolerance is the reference's OWN step-1 sensitivity: the oracle (bit-exact to the
-          reference) with 3e-6 relative noise injected on every conv output moves step-1 metrics by
-          up to 2.5e-3 (neutron_e3), 1.3e-4 (..._e1 cases at 1e-6) and 4.6e-2 (proton_e3_b12).
+          The reference's OWN step-1 sensitivity: the oracle (bit-exact to the reference) with 3e-6
+          relative noise injected on every conv output moves step-1 metrics by up to 2.5e-3
+          (neutron_e3), 1.3e-4 (..._e1 cases at 1e-6) and 4.6e-2 (proton_e3_b12).
+          Round 4: the fp32 mode is bitwise deterministic, so each case's step-1 outcome is one fixed
+          number; STEP1_TOL is ~3x that outcome (r04d, worst of metrics / images / D / A printed by this
+          test: neutron_e1_b8 5.9e-5, neutron_e3_b12 1.5e-3, proton_e1_b8 2.1e-4, proton_e3_b12 1.7e-4)
+          and never above 3x the reference's sensitivity (3.9e-4 for the E = 1 cases, 7.5e-3 neutron_e3).
 """
 import numpy as np
 import pytest
@@ -21,8 +25,8 @@ from golden_utils import CASES, Golden
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-STEP1_TOL = {"neutron_e1_b8": 1e-2, "neutron_e3_b12": 1e-2, "proton_e1_b8": 1e-2, "proton_e3_b12": 5e-2,
-             "neutron_e3_b12_router": 1e-2}
+STEP1_TOL = {"neutron_e1_b8": 2e-4, "neutron_e3_b12": 5e-3, "proton_e1_b8": 3.9e-4, "proton_e3_b12": 5e-4,
+             "neutron_e3_b12_router": 5e-3}
 
 
 def _build(g: Golden):
