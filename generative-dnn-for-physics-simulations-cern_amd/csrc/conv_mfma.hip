@@ -1177,6 +1177,69 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
     float (*st_n)[BN] = (float (*)[BN])(smem + RING);
     float (*st_m)[BN] = st_n + WGM;
     float (*st_q)[BN] = st_n + 2 * WGM;
+    // fp32 DGRAD fused with the REDUCTION pass of the BatchNorm backward that consumes its output
+    // (es_conv2d_dgrad_bnred; the generator's conv_layers.9 / .5 dgrads -> BatchNorm conv_layers.6 /
+    // .1 + Dropout + LeakyReLU, neutron/generator.py:13-40): each stored 16-byte chunk (4 channels of one
+    // output row) is folded with the norm input h and the keep bits at the same position into the
+    // lane's per-channel sums of dnorm and dnorm * xhat (norm_fast.hip bn_reduce_fast's expressions);
+    // lanes, then the WGM row waves, are merged in a fixed order into one [3][Ng] partial per row
+    // tile (slots 1, 2), which es_norm_act_bwd_sums finalises (deterministic).  Output unchanged.
+    const bool bnr_on = MODE == MODE_DGRAD && EB == 4 && a.bnr_part != nullptr;
+    float bs1[4] = {0.f, 0.f, 0.f, 0.f}, bs2[4] = {0.f, 0.f, 0.f, 0.f};
+    auto bnr_fold = [&](int64_t o, const f32x4& dyv) {   // o: element offset of the chunk's first channel
+      const f32x4 hv = *(const f32x4*)((const float*)a.bnr_x + o);
+      const int c0 = (int)(o % a.Ng);
+      const uint32_t kb = a.bnr_drop ? ((uint32_t)a.bnr_keep[o >> 3] >> (c0 & 7)) : 0xFu;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = c0 + e;
+        const float is = a.bnr_invstd[c], mu = a.bnr_mean[c];
+        const float sc = (a.bnr_gamma ? a.bnr_gamma[c] : 1.f) * is;
+        const float z = hv[e] * sc + ((a.bnr_beta ? a.bnr_beta[c] : 0.f) - mu * sc);
+        const bool keep = !a.bnr_drop || ((kb >> e) & 1u);
+        const float zs = a.bnr_drop && a.bnr_dfirst ? z * a.bnr_scale : z;
+        const float dsc = a.bnr_drop ? a.bnr_scale : 1.f;
+        const float dn = keep ? dyv[e] * (zs > 0.f ? 1.f : a.bnr_slope) * dsc : 0.f;
+        bs1[e] += dn;
+        bs2[e] += dn * ((hv[e] - mu) * is);
+      }
+    };
+    auto bnr_flush = [&]() {
+      const int cpr4 = WN / 4, rpi4 = 64 / cpr4;   // fp32 staging: lanes l, l + cpr4, ... share channels
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        for (int o = cpr4; o < 64; o <<= 1) {
+          bs1[e] += __shfl_xor(bs1[e], o, 64);
+          bs2[e] += __shfl_xor(bs2[e], o, 64);
+        }
+      (void)rpi4;
+      const int wmi = wid / WGN;
+      __syncthreads();   // (the stats scratch beside the ring: no DMA targets it)
+      if (lane < cpr4) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          st_m[wmi][wn0 + lane * 4 + e] = bs1[e];
+          st_q[wmi][wn0 + lane * 4 + e] = bs2[e];
+        }
+      }
+      __syncthreads();
+      if (wid < WGN) {   // row block 0's waves merge the WGM row waves of their columns, in order
+        for (int c = lane; c < WN; c += 64) {
+          float u1 = 0.f, u2 = 0.f;
+          for (int w = 0; w < WGM; ++w) {
+            u1 += st_m[w][wn0 + c];
+            u2 += st_q[w][wn0 + c];
+          }
+          const int kc = kc0 + c;
+          if (kc < a.Ng) {
+            float* pp = a.bnr_part + (int64_t)tl * 3 * a.Ng;
+            pp[kc] = 0.f;
+            pp[a.Ng + kc] = u1;
+            pp[2 * a.Ng + kc] = u2;
+          }
+        }
+      }
+    };
     if (part) {
       const int wmi = wid / WGN;
       bool okr[RM][4];
@@ -1319,9 +1382,18 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
       if (kc0 + lch * 16 / esz < a.Ng) {
         char* obase = (char*)a.out + (int64_t)kc0 * esz + lch * 16;
         for (int r = lr; r < SROWS; r += rpi)
-          if (row_ok(ps * SROWS + r))
-            *(uint4*)(obase + row_off(ps * SROWS + r) * esz) = *(const uint4*)(stg + r * pitch + lch * 16);
+          if (row_ok(ps * SROWS + r)) {
+            const int64_t ro = row_off(ps * SROWS + r);
+            const f32x4 vv = *(const f32x4*)(stg + r * pitch + lch * 16);
+            *(uint4*)(obase + ro * esz) = __builtin_bit_cast(uint4, vv);
+            if constexpr (MODE == MODE_DGRAD && EB == 4) {
+              if (bnr_on) bnr_fold(ro + kc0 + lch * 4, vv);
+            }
+          }
       }
+    }
+    if constexpr (MODE == MODE_DGRAD && EB == 4) {
+      if (bnr_on) bnr_flush();
     }
     }
     if (part && wid < WGN) {   // the waves of row block 0 merge the WGM row waves of their columns
@@ -3516,6 +3588,27 @@ int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
     for (int c = 0; c < 4; ++c) a.sp_tpc = std::max(a.sp_tpc, a.sp.tile0[c + 1] - a.sp.tile0[c]);
     row_tiles = NGI * 4 * a.sp_tpc;
   }
+  // fp32 DGRAD fused with the BatchNorm-backward reduction over its output (es_conv2d_dgrad_bnred):
+  // one [3][Ng] partial per row tile, written by the staged epilogue (conv_ring_kernel, bnr_fold)
+  a.bnr_part = nullptr;
+  if constexpr (EB == 4) {
+    const BnRedRequest& q = g_bnr_req;
+    const int64_t orow = (int64_t)a.os[0];
+    if (mode == MODE_DGRAD && q.part && q.x && q.nm && q.ch && a.vec_out && !a.out_bf16 && a.os[1] == 1 &&
+        a.os[3] == a.Ng && orow % a.Ng == 0 && ((uintptr_t)q.x & 15) == 0 &&
+        (q.ch->act == ES_ACT_LRELU || q.ch->act == ES_ACT_RELU) && (!q.ch->drop.enabled || q.ch->keep) &&
+        (int64_t)row_tiles * 3 * a.Ng <= q.floats) {
+      a.bnr_x = q.x;
+      a.bnr_keep = q.ch->keep;
+      a.bnr_mean = q.nm->mean; a.bnr_invstd = q.nm->invstd; a.bnr_gamma = q.nm->gamma; a.bnr_beta = q.nm->beta;
+      a.bnr_drop = q.ch->drop.enabled != 0;
+      a.bnr_scale = a.bnr_drop ? q.ch->drop.scale : 1.f;
+      a.bnr_dfirst = q.ch->dropout_first;
+      a.bnr_slope = q.ch->act == ES_ACT_LRELU ? q.ch->slope : 0.f;
+      a.bnr_part = q.part;
+      g_bnr_req.chunks = row_tiles;
+    }
+  }
   // fused BatchNorm statistics (es_conv2d_fwd_stats): one [3][Ng] partial per row tile
   a.stats_part = nullptr;
   const int chunks = a.sp_merge ? 4 * row_tiles : row_tiles;
@@ -3646,6 +3739,10 @@ int es_conv_ring_launch_f32(ConvArgs& a, int mode, hipStream_t st) {
   const StatsRequest req = g_stats_req;
   int used = 0;
   bool stats_ok = req.part != nullptr;
+  const BnRedRequest breq = g_bnr_req;   // DGRAD + BatchNorm-backward reduction: per-chunk offsets
+  int bused = 0;
+  bool bnr_ok = breq.part != nullptr;
+  es_chain_t bch{};
   for (int n0 = 0; n0 < N; n0 += nc) {
     ConvArgs c = a;
     c.d.N = std::min(nc, N - n0);
@@ -3653,11 +3750,18 @@ int es_conv_ring_launch_f32(ConvArgs& a, int mode, hipStream_t st) {
     c.out = (char*)a.out + (int64_t)n0 * a.os[0] * esz;
     c.M = mode == MODE_FWD ? c.d.N * d.P * d.Q : (a.fold ? c.d.N * d.H * d.W : c.d.N * d.Hu * d.Wu);
     if (req.part) g_stats_req = StatsRequest{req.part + (int64_t)used * 3 * a.Ng, req.floats - (int64_t)used * 3 * a.Ng, 0};
+    if (breq.part) {   // the norm input h and the keep bits share the output's row layout
+      bch = *breq.ch;
+      if (bch.keep) bch.keep += (int64_t)n0 * a.os[0] / 8;
+      g_bnr_req = BnRedRequest{(const char*)breq.x + (int64_t)n0 * a.os[0] * 4, breq.nm, &bch,
+                               breq.part + (int64_t)bused * 3 * a.Ng, breq.floats - (int64_t)bused * 3 * a.Ng, 0};
+    }
     c.prio = g_spl_prio;
     const int rc = g_f32_split == 2 ? ring_fd<float, 2>(c, mode, st)
                    : g_f32_split ? ring_fd<float, 1>(c, mode, st) : ring_fd<float>(c, mode, st);
     if (rc <= 0) {
       g_stats_req = req;
+      g_bnr_req = breq;
       if (n0 == 0) return rc;
       es_set_error("conv f32 ring: chunk %d not eligible", n0);
       return -1;
@@ -3666,8 +3770,13 @@ int es_conv_ring_launch_f32(ConvArgs& a, int mode, hipStream_t st) {
       stats_ok = stats_ok && g_stats_req.chunks > 0;
       used += g_stats_req.chunks;
     }
+    if (breq.part) {
+      bnr_ok = bnr_ok && g_bnr_req.chunks > 0;
+      bused += g_bnr_req.chunks;
+    }
   }
   g_stats_req = StatsRequest{req.part, req.floats, stats_ok ? used : 0};
+  if (breq.part) g_bnr_req = BnRedRequest{breq.x, breq.nm, breq.ch, breq.part, breq.floats, bnr_ok ? bused : 0};
   g_ring_hit = 1 | (g_f32_split ? 2 : 0) | (d.subpixel ? 4 : 0);
   return 1;
 }

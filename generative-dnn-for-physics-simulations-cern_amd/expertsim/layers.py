@@ -470,7 +470,9 @@ class ConvOp:
               elif fuse:
                   norm, h, stats, chain = bn_reduce
                   nm = norm.norm_struct(*stats)
-                  floats = 2048 * 3 * Cc      # >= the thin dgrad's blocks (<= 2048) / persistent workgroups
+                  # >= the thin dgrad's blocks (<= 2048) / persistent workgroups / fp32 ring row tiles (one
+                  # partial per 128- or 256-row tile of 64 images x >= 2 pixels, per image chunk)
+                  floats = 3 * Cc * max(2048, ((N + 63) // 64 + 2) * ((H * W + 1) // 2 + 1))
                   part = torch.empty(floats, dtype=torch.float32, device=dy.t.device)
                   chunks = C.c_int(0)
                   hip.call("es_conv2d_dgrad_bnred", C.byref(d), dy.dt, dy.ptr, hip.strides4(dy.strides),

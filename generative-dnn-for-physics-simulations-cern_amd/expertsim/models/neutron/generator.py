@@ -17,6 +17,8 @@ Dropout masks come from Philox streams (expertsim/utils/philox.py), layer index 
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 
@@ -24,6 +26,8 @@ from ... import hip
 from ...layers import Act, ConvOp, NormOp, Upsample, act_bwd, act_fwd, copy_act
 from ...utils import philox
 from ..base import ExpertModule, build_tree, get_module
+
+_RING_BNRED = os.environ.get("ES_RING_BNRED", "0") == "1"     # A/B switch
 
 SLOPE = 0.1
 P_DROP = 0.2
@@ -146,9 +150,12 @@ class GeneratorNeutron(ExpertModule):
                            dbeta=g("conv_layers.6", "bias"), dsum=g("conv_layers.5", "bias"))
         o["c5"].wgrad(dh4, ctx["y3"], g("conv_layers.5", "weight"), None)
         ready("conv_layers.5.weight")
-        # (no fused reduction here: the 256 x 256 sub-pixel DGRAD has no registers to spare for it,
-        # measured 585 -> 871 us for a 146 us reduce pass)
-        dy3 = o["c5"].dgrad(dh4, ctx["y3"])
+        # no fused reduction here by default: the 256 x 256 sub-pixel DGRAD has no registers to spare for
+        # it in bf16 (585 -> 871 us for a 146 us reduce pass), and the split-fp32 ring DGRAD's staged
+        # epilogue fold (ES_RING_BNRED=1, bitwise-tested) costs more than the reduce pass it removes
+        # (B = 1024 c5 DGRAD 3.16 -> 3.62 ms)
+        bnr = (o["bn3"], ctx["h3"], ctx["s3"], ch[2]) if _RING_BNRED else None
+        dy3 = o["c5"].dgrad(dh4, ctx["y3"], bn_reduce=bnr)
         dh3 = o["bn3"].bwd(ctx["h3"], ctx["s3"], ch[2], dy3, dgamma=g("conv_layers.1", "weight"),
                            dbeta=g("conv_layers.1", "bias"), dsum=g("conv_layers.0", "bias"))
         o["c0"].wgrad(dh3, ctx["y2n"], g("conv_layers.0", "weight"), None)
