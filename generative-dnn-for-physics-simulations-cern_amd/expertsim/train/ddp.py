@@ -181,8 +181,13 @@ class DataParallel:
         rows = torch.empty(E, 10, dtype=torch.float32, device=mbuf.device)
         rows[:, :9].copy_(mbuf)
         ran = self._local >= (1 if self.sync_bn else 2)        # the ranks that ran the expert's step
-        n = torch.from_numpy(np.where(ran, self._local, 0).astype(np.float32))
-        rows[:, 9].copy_(n)
+        n = np.where(ran, self._local, 0).astype(np.float32)
+        # cached per value on the device: a pageable host -> device copy_ synchronises the stream
+        # (it would drain the GPU at the end of every data-parallel step)
+        key = ("n", str(mbuf.device), tuple(float(v) for v in n))
+        if key not in self._counts_dev:
+            self._counts_dev[key] = torch.from_numpy(n).to(mbuf.device)
+        rows[:, 9].copy_(self._counts_dev[key])
         allr = self.all_gather(rows)
         hip.call("es_dp_metrics_merge", hip.ptr(allr), self.world, E, hip.ptr(mbuf), hip.stream_ptr())
         return mbuf

@@ -16,13 +16,16 @@ from expertsim.layers import Act, NormOp  # noqa: E402
 def timed(fn, reps=20):
     fn()
     torch.cuda.synchronize()
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record()
-    for _ in range(reps):
-        fn()
-    b.record()
-    torch.cuda.synchronize()
-    return a.elapsed_time(b) / reps * 1e3   # us
+    best = 1e30
+    for _ in range(3):                      # best of 3 (clock ramp)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        best = min(best, a.elapsed_time(b) / reps * 1e3)
+    return best   # us
 
 
 def case(name, kind, groups, N, C, H, W, dtype, drop, bits=False):
@@ -70,6 +73,11 @@ def main():
     pool_case("D pool1 fp32 42x42x32", 512, 32, 42, 42, 2, torch.float32)
     pool_case("A pool1 bf16 42x42x32", 512, 32, 42, 42, (2, 2), torch.bfloat16)
     bf, f32 = torch.bfloat16, torch.float32
+    if os.environ.get("MB_NORM_F32"):    # the fp32 bench's generator BatchNorms (B = 1024, keep bits)
+        case("G bn3 fp32 24x24x256", hip.NORM_BN, 1, 1024, 256, 24, 24, f32, True, True)
+        case("G bn4 fp32 46x46x128", hip.NORM_BN, 1, 1024, 128, 46, 46, f32, True, True)
+        case("G bn5 fp32 45x45x64", hip.NORM_BN, 1, 1024, 64, 45, 45, f32, True, True)
+        return
     case("G c5 BN bf16 46x46x128", hip.NORM_BN, 1, 512, 128, 46, 46, bf, True)
     case("G c5 BN bf16 no dropout", hip.NORM_BN, 1, 512, 128, 46, 46, bf, False)
     case("G c5 BN bf16 keep bits", hip.NORM_BN, 1, 512, 128, 46, 46, bf, True, True)

@@ -12,8 +12,9 @@ import json
 import sys
 
 LAYERS = {"c0": (128, 13, 13, 256, 24, 24, 3), "c5": (256, 24, 24, 128, 46, 46, 3),
-          "c9": (128, 46, 46, 64, 45, 45, 2)}
-NAMES = {"fwd": ("conv_ring_kernel<0",), "dgrad": ("conv_ring_kernel<1",),
+          "c9": (128, 46, 46, 64, 45, 45, 2),
+          "p1": (512, 18, 10, 256, 35, 19, 4), "p5": (256, 35, 19, 128, 55, 29, 4)}
+NAMES = {"fwd": ("conv_ring_kernel<0", "upsample_fwd_nhwc"), "dgrad": ("conv_ring_kernel<1", "upsample_bwd_nhwc"),
          "wgrad": ("wgrad_f32_kernel", "wgrad_f32_col_kernel", "wgrad_f32_col2_kernel", "wgrad_coop_kernel", "wgrad_reduce_kernel")}
 
 
@@ -32,7 +33,7 @@ def main():
     names = NAMES[mode]
     fetch = rows(d + "/fetch", "FETCH_SIZE", names)
     write = rows(d + "/write", "WRITE_SIZE", names)
-    conv = tuple(n for n in names if "reduce" not in n)
+    conv = tuple(n for n in names if "reduce" not in n and "upsample" not in n)
     mfma = rows(d + "/mfma", "SQ_VALU_MFMA_BUSY_CYCLES", conv)
     gui = rows(d + "/mfma", "GRBM_GUI_ACTIVE", conv)
     dur = {}
