@@ -10,8 +10,15 @@ next training step:
   * both counters are advanced by kernels inside the step.
 Inputs are the static tensors passed at capture time: copy new batches into them before replay.
 
+Data parallel (RCCL process group, n_experts == 1): the step's collectives -- the SyncBN
+statistics / backward-sum reductions, the bucketed gradient all-reduces on the process group's
+stream (joined back by ``wait``) and the metric all-gather -- are captured into the same graph, so a
+replay issues no host work and no host synchronisation (the global counts of E = 1 are known on the
+host without a collective, ``DataParallel.global_groups``).  Every rank must capture and replay in
+lockstep (same step count), as it issues the same collectives in the same order.
+
 Not captured: n_experts > 1 (the expert sizes are read on the host for the reference's
-``B_e <= 1`` skip rule) and data-parallel runs (collectives stay eager).
+``B_e <= 1`` skip rule) and gloo process groups (their collectives go through the host).
 """
 from __future__ import annotations
 
@@ -20,13 +27,13 @@ import torch
 
 def graph_supported(moe) -> bool:
     """True when ``moe.train_step`` issues no host synchronisation and can be captured."""
-    return moe.n_experts == 1 and moe.ddp is None
+    return moe.n_experts == 1 and (moe.ddp is None or not moe.ddp.gloo)
 
 
 class StepGraph:
     def __init__(self, moe, step_args, warmup: int = 2):
         if not graph_supported(moe):
-            raise ValueError("StepGraph captures single-process, single-expert train steps only")
+            raise ValueError("StepGraph captures single-expert train steps (single process or RCCL data parallel)")
         self.moe = moe
         self.args = tuple(step_args)
         torch.cuda.synchronize()
