@@ -80,8 +80,13 @@ def test_ddp_graph_replay_matches_eager_rccl_world1():
     q = ctx.Queue()
     p = ctx.Process(target=_worker, args=(_free_port(), q))
     p.start()
-    runs, err = q.get(timeout=240)
-    p.join(timeout=60)
+    try:
+        runs, err = q.get(timeout=240)
+        p.join(timeout=60)
+    finally:
+        if p.is_alive():           # a stuck worker must not outlive the test holding the GPU
+            p.kill()
+            p.join(timeout=30)
     assert err is None, err
     (ma, pa), (mb, pb) = runs
     assert ma == mb, (ma, mb)
