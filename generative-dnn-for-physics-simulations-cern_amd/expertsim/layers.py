@@ -200,6 +200,7 @@ def deterministic() -> bool:
 # (packing the weight planes must follow the level the kernels actually run).
 _F32_SPLIT = None
 _SPLIT_LEVEL = min(max(int(os.environ.get("ES_F32_SPLIT_LEVEL", "2")), 1), 2)
+_LIN_PIX = os.environ.get("ES_LIN_PIX", "1") != "0"                  # A/B switch (ConvOp._pixel_view)
 
 
 def set_f32_split(on: bool):
@@ -387,6 +388,12 @@ class ConvOp:
         the kernel reads it instead of splitting x; es_conv2d_fwd_planes)."""
         if planes is None and self._resized(x):
             return self._plain_op().fwd(self._resize(x), out_dtype, inv_scale, out, with_bias, bn_stats)
+        xv = self._pixel_view(x) if planes is None and out is None else None
+        if xv is not None:
+            o = self.fwd(xv, out_dtype, inv_scale, None, with_bias, bn_stats)
+            res = Act(o.t, (x.dims[0], self.K, 1, 1), (self.K, 1, 1, 1))
+            res.bn_part = o.bn_part
+            return res
         d = self.desc(x)
         cdt = x.t.dtype
         if self.subpixel(d, cdt):
@@ -432,6 +439,23 @@ class ConvOp:
                 hip.call("es_conv2d_fwd", C.byref(d), x.dt, x.ptr, hip.strides4(x.strides), hip.ptr(wk),
                          hip.ptr(bias), out.ptr, out.dt, hip.strides4(out.strides), hip.stream_ptr())
         return out
+
+    def _pixel_view(self, x: Act):
+        """A wide linear ([B, C] -> [B, K], K >= 1024) as a 1x1 conv over 16-pixel images of the same
+        memory, NHWC (B/16, C, 16, 1): the ring FWD kernels (conv_mfma.hip) tile rows as (image group,
+        pixel), so a linear's 1-pixel images would leave 3/4 of every 256-row tile empty (bf16) or miss
+        the fp32 ring (>= 16 output pixels per image) and fall to the register-staged fp32-MFMA GEMM;
+        the generators' fc2 (256 -> 21632 neutron, neutron/generator.py:17) is the case.  None when the
+        layout does not apply (ES_LIN_PIX=0 disables it)."""
+        if not _LIN_PIX or self.R != 1 or self.S != 1 or self.up is not None or self.stride != 1 or self.pad != 0:
+            return None
+        N, Cc, H, W = x.dims
+        dt = x.t.dtype
+        if H != 1 or W != 1 or N % 16 or N < 256 or self.K < 1024 or self.K % 64 or x.strides[:2] != (Cc, 1):
+            return None
+        if not ((dt == torch.float32 and f32_split_level() > 0 and Cc % 32 == 0) or (dt == torch.bfloat16 and Cc % 64 == 0)):
+            return None
+        return Act(x.t, (N // 16, Cc, 16, 1), (16 * Cc, 1, Cc, Cc))
 
     def _linear_det(self, d, ng, out: Act) -> bool:
         """A linear (1x1 conv of 1x1 images) with a dense fp32 output of <= 4096 columns: the GEMMs

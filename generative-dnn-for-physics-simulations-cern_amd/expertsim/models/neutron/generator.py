@@ -109,7 +109,7 @@ class GeneratorNeutron(ExpertModule):
             ch[i].drop.index_offset = int(n_offset) * r * c
         h1 = o["fc1"].fwd(x0)
         y1, s1 = o["bn1"].fwd(h1, ch[0], train=train)
-        h2 = o["fc2"].fwd(y1)
+        h2 = o["fc2"].fwd(y1, bn_stats=train)        # (ring FWD over 16-row pixel blocks: stats in its epilogue)
         y2, s2 = o["bn2"].fwd(h2, ch[1], train=train)
         # [B, 21632] rows are NCHW [B,128,13,13]; re-layout to NHWC for the vector gather
         y2n = Act.nhwc(B, 128, k, k, cdt, dev)

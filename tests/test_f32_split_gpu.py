@@ -132,3 +132,42 @@ def test_split_large_tiles_match_exact(case, det):
     split = _run(case, x, w, b, gy)[1:]
     for e, s_ in zip(exact, split):
         assert rel(s_, e) < 1e-5
+
+
+@pytest.mark.parametrize("B,Cin,K,split", [(512, 256, 2048, True), (1024, 256, 21632, True), (256, 64, 1152, True),
+                                           (512, 256, 2048, False)])
+def test_wide_linear_pixel_view(B, Cin, K, split, det):
+    """A wide linear (the generators' fc2, neutron/generator.py:17) runs as a 1x1 conv over 16-row
+    pixel blocks of the same memory (ConvOp._pixel_view) on the ring FWD, with the BatchNorm1d
+    statistics from its epilogue: output against torch fp64 F.linear at the fp32 bound (2e-5 of
+    max|ref|), equal to the plain-linear path within the same bound, statistics against torch."""
+    from expertsim import layers
+    from expertsim.layers import Act, ConvOp, NormOp
+    hip = _hip()
+    layers.set_f32_split(split)
+    torch.manual_seed(11)
+    x = torch.randn(B, Cin, device="cuda")
+    w = torch.nn.Parameter(torch.randn(K, Cin, device="cuda") / Cin ** 0.5)
+    b = torch.nn.Parameter(0.1 * torch.randn(K, device="cuda"))
+    op = ConvOp(w, b)
+    xa = Act.of(x)
+    assert (op._pixel_view(xa) is not None) == split      # (fp32 exact MFMA: the plain path)
+    y = op.fwd(xa, bn_stats=True)
+    ref = torch.nn.functional.linear(x.double().cpu(), w.detach().double().cpu(), b.detach().double().cpu())
+    got = y.rows2d().double().cpu()
+    assert rel(got, ref) < 2e-5, rel(got, ref)
+    if split:
+        assert y.bn_part is not None                       # statistics from the ring epilogue
+        old = layers._LIN_PIX
+        layers._LIN_PIX = False
+        try:
+            plain = op.fwd(xa).rows2d().double().cpu()
+        finally:
+            layers._LIN_PIX = old
+        assert rel(got, plain) < 2e-5
+        rm, rv = torch.zeros(K, device="cuda"), torch.ones(K, device="cuda")
+        bn = NormOp(hip.NORM_BN, torch.ones(K, device="cuda"), torch.zeros(K, device="cuda"), running_mean=rm,
+                    running_var=rv, momentum=0.1, eps=1e-5)
+        mean, invstd = bn.stats(y)
+        assert rel(mean.double().cpu(), ref.mean(0)) < 1e-5
+        assert rel(invstd.double().cpu(), torch.rsqrt(ref.var(0, unbiased=False) + 1e-5)) < 1e-5
