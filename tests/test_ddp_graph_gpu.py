@@ -12,6 +12,7 @@ runs in a spawned process so the process group does not outlive the test.
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.multiprocessing as mp
@@ -65,7 +66,9 @@ def _worker(port, q):
                 assert moe.step_count == 3
             torch.cuda.synchronize()
             runs.append(({k: float(v) for k, v in m.items()},
-                         {n: p.detach().cpu().clone() for n, p in moe.named_parameters()}))
+                         # numpy: pickled by value (torch CPU tensors travel as shared-memory fds,
+                         # which need the worker alive when the parent unpickles them)
+                         {n: p.detach().cpu().numpy().copy() for n, p in moe.named_parameters()}))
         q.put((runs, None))
     except Exception as e:         # report instead of hanging the parent
         q.put((None, repr(e)))
@@ -90,5 +93,5 @@ def test_ddp_graph_replay_matches_eager_rccl_world1():
     assert err is None, err
     (ma, pa), (mb, pb) = runs
     assert ma == mb, (ma, mb)
-    diff = [n for n in pa if not torch.equal(pa[n], pb[n])]
+    diff = [n for n in pa if not np.array_equal(pa[n], pb[n])]
     assert not diff, diff

@@ -3,7 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out
-bash tools/gpu_norm_ab.sh n_base n_ldst n_ld n_base n_ldst || exit $?
+mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_ddp_graph_gpu.py -m gpu -q -x --timeout 300 --timeout-method thread > $O/ddpgraph_r04h.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py --steps 20 --other-steps 0 --no-cpu-baseline --no-probe --graph off > $O/eager_r04h.json 2> $O/eager_r04h.err || exit $?
 timeout -k 10 300 python bench.py --ddp --sync-bn --steps 20 --other-steps 0 --no-cpu-baseline --no-probe > $O/ddp1_r04h.json 2> $O/ddp1_r04h.err || exit $?
