@@ -1,7 +1,13 @@
-# proton fp32 B = 512 bench, proton conv_layers.1 / .5 PMC traffic (split-fp32, B = 1024)
+# A/B of the wide-linear pixel view (ES_LIN_PIX) on one box, alternating; proton fp32 B = 512 bench;
+# proton conv_layers.1 / .5 PMC traffic (split-fp32, B = 1024)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out
+for i in 1 2; do
+  for v in 0 1; do
+    ES_LIN_PIX=$v timeout -k 10 300 python bench.py --steps 30 --other-steps 0 --no-cpu-baseline --no-probe > $O/linpix${v}_$i.json 2> $O/linpix${v}_$i.err || exit $?
+  done
+done
 timeout -k 10 300 python bench.py --arch proton --batch 512 --steps 20 --other-steps 0 --no-cpu-baseline > $O/proton512_r04i.json 2> $O/proton512_r04i.err || exit $?
 for L in p1 p5; do
   for m in fwd dgrad wgrad; do
