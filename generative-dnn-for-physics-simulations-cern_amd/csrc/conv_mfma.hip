@@ -3486,6 +3486,17 @@ extern "C" int es_conv_set_wgrad_mt(int on) {
   return old;
 }
 
+namespace {
+// fp32 ring DGRAD + BatchNorm-backward reduction in the staged epilogue: opt-in (measured slower)
+bool g_ring_bnred = [] { const char* e = getenv("ES_RING_BNRED"); return e && e[0] == '1'; }();
+}  // namespace
+
+extern "C" int es_conv_set_ring_bnred(int on) {
+  const int old = g_ring_bnred;
+  g_ring_bnred = on != 0;
+  return old;
+}
+
 extern "C" int es_conv_set_spb4(int on) {
   const int old = g_spb4;
   g_spb4 = on != 0;
@@ -3675,7 +3686,7 @@ int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
   // fp32 DGRAD fused with the BatchNorm-backward reduction over its output (es_conv2d_dgrad_bnred):
   // one [3][Ng] partial per row tile, written by the staged epilogue (conv_ring_kernel, bnr_fold)
   a.bnr_part = nullptr;
-  if constexpr (EB == 4) {
+  if constexpr (EB == 4) if (g_ring_bnred) {
     const BnRedRequest& q = g_bnr_req;
     const int64_t orow = (int64_t)a.os[0];
     if (mode == MODE_DGRAD && q.part && q.x && q.nm && q.ch && a.vec_out && !a.out_bf16 && a.os[1] == 1 &&

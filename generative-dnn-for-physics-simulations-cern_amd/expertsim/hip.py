@@ -104,6 +104,7 @@ _SIGS = {
     "es_conv_launch_count": (C.c_int64, []),
     "es_conv_exec_flops": (C.c_int, [C.POINTER(C.c_double), C.c_int]),
     "es_conv_set_spb4": (C.c_int, [C.c_int]),
+    "es_conv_set_ring_bnred": (C.c_int, [C.c_int]),
     "es_pack_conv_weight": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, C.c_int, P]),
     "es_unpack_conv_grad": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, C.c_float, P]),
     "es_unpack_conv_grad_clear": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_float, P]),

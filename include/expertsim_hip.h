@@ -210,11 +210,17 @@ int es_conv2d_dgrad_planes(const es_conv_desc_t* d, const void* dyp, const int64
 /* Host-side count of MFMA conv kernels issued so far (ring / persistent / p256 / fp32 WGRAD).
  * Instrumentation only: lets a profiler state how many kernel launches one conv op was. */
 int64_t es_conv_launch_count(void);
-/* A/B knob of the split-fp32 FWD / DGRAD 256 x 128 tiles: 1 (default) = the 4-wave kernel (one wave
- * per SIMD, wave tiles 64 x 128), 0 = the 8-wave kernel; same products in the same order (bitwise
- * equal outputs).  Returns the previous setting.  Replaces nothing of the reference (a kernel choice
- * for neutron generator.py:24,29 conv_layers.0 / .5). */
+/* A/B knob of the split-fp32 FWD / DGRAD 256 x 128 tiles: 0 (default) = the 8-wave kernel, 1 = the
+ * 4-wave kernel (one wave per SIMD, wave tiles 64 x 128; measured slower); same products in the same
+ * order (bitwise equal outputs).  Returns the previous setting.  Replaces nothing of the reference (a
+ * kernel choice for neutron generator.py:24,29 conv_layers.0 / .5). */
 int es_conv_set_spb4(int on);
+/* Opt-in (default 0, or ES_RING_BNRED=1): es_conv2d_dgrad_bnred on an fp32 ring DGRAD folds the
+ * BatchNorm-backward reduction into the kernel's staged epilogue (bitwise equal dgrad output; measured
+ * slower than the separate reduction pass).  Off, such calls report no partials and the
+ * caller runs the reduction pass.  Returns the previous setting.  (The backward of neutron
+ * generator.py:26-35's BatchNorm2d layers.) */
+int es_conv_set_ring_bnred(int on);
 /* Host-side tally of the MFMA work the conv entry points (es_conv2d_fwd / _dgrad / _wgrad /
  * _wgrad_det and their _stats / _bnred / _det variants) issued, as executed FLOPs (2 per MAC):
  * out[0] on the bf16 pipe (bf16 operands, and split-fp32: 6 plane products per fp32 product),

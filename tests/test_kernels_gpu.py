@@ -850,6 +850,7 @@ def test_ring_dgrad_bn_reduce_fused_fp32(case, split):
     old_det, old_split = layers.deterministic(), layers.f32_split()
     layers.set_deterministic(True)
     layers.set_f32_split(split)
+    old_bnred = hip.lib().es_conv_set_ring_bnred(1)     # opt-in fold (measured slower than the pass)
     try:
         torch.manual_seed(13)
         w = torch.randn(Cout, Cin, k, k, device=DEV) / np.sqrt(Cin * k * k)
@@ -881,7 +882,13 @@ def test_ring_dgrad_bn_reduce_fused_fp32(case, split):
         scale = float(dh0.abs().reshape(-1, Cin).sum(0).max())
         assert float((ds1 - ds0).abs().max()) < 1e-5 * scale
         assert rel(dh1, dh0) < 1e-5
+        # off (the default): the fp32 ring DGRAD reports no partials, the caller runs the reduce pass
+        hip.lib().es_conv_set_ring_bnred(0)
+        dx = op.dgrad(gy, y, dx_dtype=torch.float32, bn_reduce=(bn, h, stats, ch))
+        assert getattr(dx, "bn_sums", None) is None
+        assert torch.equal(dx.t, dx0)
     finally:
+        hip.lib().es_conv_set_ring_bnred(old_bnred)
         layers.set_f32_split(old_split)
         layers.set_deterministic(old_det)
 
