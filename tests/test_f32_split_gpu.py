@@ -171,3 +171,30 @@ def test_wide_linear_pixel_view(B, Cin, K, split, det):
         mean, invstd = bn.stats(y)
         assert rel(mean.double().cpu(), ref.mean(0)) < 1e-5
         assert rel(invstd.double().cpu(), torch.rsqrt(ref.var(0, unbiased=False) + 1e-5)) < 1e-5
+
+
+def test_wide_linear_pixel_view_bf16():
+    """The bf16 performance mode takes the same pixel-block layout for the generators' fc2: against
+    torch fp32 F.linear of the bf16-rounded operands (1e-2 of max|ref|), and the BatchNorm1d
+    statistics from the epilogue against torch on the kernel's own output."""
+    from expertsim.layers import Act, ConvOp, NormOp
+    hip = _hip()
+    torch.manual_seed(12)
+    B, Cin, K = 1024, 256, 21632
+    x = torch.randn(B, Cin, device="cuda").bfloat16()
+    w = torch.nn.Parameter(torch.randn(K, Cin, device="cuda") / Cin ** 0.5)
+    b = torch.nn.Parameter(0.1 * torch.randn(K, device="cuda"))
+    op = ConvOp(w, b)
+    xa = Act.of(x)
+    assert op._pixel_view(xa) is not None
+    y = op.fwd(xa, bn_stats=True)
+    assert y.bn_part is not None
+    ref = torch.nn.functional.linear(x.float(), w.detach().bfloat16().float(), b.detach())
+    got = y.rows2d().float()
+    assert rel(got.cpu(), ref.cpu()) < 1e-2, rel(got.cpu(), ref.cpu())
+    bn = NormOp(hip.NORM_BN, torch.ones(K, device="cuda"), torch.zeros(K, device="cuda"),
+                running_mean=torch.zeros(K, device="cuda"), running_var=torch.ones(K, device="cuda"),
+                momentum=0.1, eps=1e-5)
+    mean, invstd = bn.stats(y)
+    assert rel(mean.cpu(), got.mean(0).cpu()) < 1e-3
+    assert rel(invstd.cpu(), torch.rsqrt(got.var(0, unbiased=False) + 1e-5).cpu()) < 1e-3
