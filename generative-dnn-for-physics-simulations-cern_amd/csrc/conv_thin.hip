@@ -213,9 +213,9 @@ __global__ void __launch_bounds__(NT) c1_wgrad(Thin t) {
 }
 
 // ============================================================ Cout == 1
-// A pixel is served by LP = C/VN lanes (one 16-byte channel chunk each); 64/LP pixels per wave.
-// fwd: y = bias + sum over taps of <x row chunk, w chunk>, reduced over the LP lanes.
-template <typename T, typename TO, int RS>
+// A pixel is served by LP = C/(VN*CH) lanes (CH 16-byte channel chunks each); 64/LP pixels per wave.
+// fwd: y = bias + sum over taps of <x row chunks, w chunks>, reduced over the LP lanes.
+template <typename T, typename TO, int RS, int CH = 1>
 __global__ void __launch_bounds__(NT) k1_fwd(Thin t, int LP) {
   constexpr int VN = V16<T>::N;
   const es_conv_desc_t& d = t.d;
@@ -231,22 +231,25 @@ __global__ void __launch_bounds__(NT) k1_fwd(Thin t, int LP) {
   const bool live = m < t.M;
   int n, p, q;
   pix3(live ? m : 0, d.P, d.Q, n, p, q);
-  const T* x = (const T*)t.a + n * t.as[0] + l * VN;
+  const T* x = (const T*)t.a + n * t.as[0] + l * VN * CH;
   float s = 0.f;
 #pragma unroll
   for (int j = 0; j < RS; ++j) {
     const int hu = p - d.pad + j / d.S, wu = q - d.pad + j % d.S;
     const bool ok = live && hu >= 0 && hu < d.H && wu >= 0 && wu < d.W;
     const T* px = x + (ok ? hu * t.as[2] + wu * t.as[3] : 0);   // clamped: the taps' loads issue together
-    const float* pw = wf + j * d.C + l * VN;
-    if constexpr (VN == 8) {
-      float v[8];
-      ld8<T>(px, v);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s += (ok ? v[e] : 0.f) * pw[e];
-    } else {
-      const float4 v = *(const float4*)px;
-      if (ok) s += v.x * pw[0] + v.y * pw[1] + v.z * pw[2] + v.w * pw[3];
+    for (int c = 0; c < CH; ++c) {
+      const float* pw = wf + j * d.C + (l * CH + c) * VN;
+      if constexpr (VN == 8) {
+        float v[8];
+        ld8<T>(px + c * VN, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += (ok ? v[e] : 0.f) * pw[e];
+      } else {
+        const float4 v = *(const float4*)(px + c * VN);
+        if (ok) s += v.x * pw[0] + v.y * pw[1] + v.z * pw[2] + v.w * pw[3];
+      }
     }
   }
   for (int o = LP >> 1; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
@@ -258,7 +261,7 @@ __global__ void __launch_bounds__(NT) k1_fwd(Thin t, int LP) {
 }
 
 // dgrad: dx[n,h,w,c] = sum over taps of dy[n, h+pad-r, w+pad-s] * w[c][r][s]   (wd = [C][R][S])
-template <typename T, typename TO, int RS>
+template <typename T, typename TO, int RS, int CH = 1>
 __global__ void __launch_bounds__(NT) k1_dgrad(Thin t, int LP) {
   constexpr int VN = V16<T>::N;
   const es_conv_desc_t& d = t.d;
@@ -274,34 +277,42 @@ __global__ void __launch_bounds__(NT) k1_dgrad(Thin t, int LP) {
   int n, h, w;
   pix3(m, d.H, d.W, n, h, w);
   const T* dy = (const T*)t.a + n * t.as[0];
-  float acc[VN];
+  float acc[CH][VN];
 #pragma unroll
-  for (int e = 0; e < VN; ++e) acc[e] = 0.f;
+  for (int c = 0; c < CH; ++c)
+#pragma unroll
+    for (int e = 0; e < VN; ++e) acc[c][e] = 0.f;
 #pragma unroll
   for (int j = 0; j < RS; ++j) {
     const int ph = h + d.pad - j / d.S, pw = w + d.pad - j % d.S;
     const bool ok = ph >= 0 && pw >= 0 && ph < d.P && pw < d.Q;
     const float gv = to_f(dy[ok ? ph * t.as[2] + pw * t.as[3] : 0]);   // clamped, then select
     const float g = ok ? gv : 0.f;
-    const float* wr = wf + j * d.C + l * VN;
 #pragma unroll
-    for (int e = 0; e < VN; ++e) acc[e] += g * wr[e];
-  }
-  TO* o = (TO*)t.out + n * t.os[0] + h * t.os[2] + w * t.os[3] + l * VN;
-  if constexpr (VN == 8) {
-    if (t.beta != 0.f) {
-      float old[8];
-      ld8<TO>(o, old);
+    for (int c = 0; c < CH; ++c) {
+      const float* wr = wf + j * d.C + (l * CH + c) * VN;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += t.beta * old[e];
+      for (int e = 0; e < VN; ++e) acc[c][e] += g * wr[e];
     }
-    st8<TO>(o, acc);
-  } else {
+  }
 #pragma unroll
-    for (int e = 0; e < VN; ++e) {
-      float v = acc[e];
-      if (t.beta != 0.f) v += t.beta * to_f(o[e]);
-      o[e] = from_f<TO>(v);
+  for (int c = 0; c < CH; ++c) {
+    TO* o = (TO*)t.out + n * t.os[0] + h * t.os[2] + w * t.os[3] + (l * CH + c) * VN;
+    if constexpr (VN == 8) {
+      if (t.beta != 0.f) {
+        float old[8];
+        ld8<TO>(o, old);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[c][e] += t.beta * old[e];
+      }
+      st8<TO>(o, acc[c]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < VN; ++e) {
+        float v = acc[c][e];
+        if (t.beta != 0.f) v += t.beta * to_f(o[e]);
+        o[e] = from_f<TO>(v);
+      }
     }
   }
   }
@@ -401,56 +412,60 @@ __global__ void __launch_bounds__(NT) k1_dgrad_bnred(Thin t, int LP, ThinBnr b) 
   }
 }
 
-// wgrad: dw[r][s][c] = sum over pixels of dy[pix] * x[pix + (r,s)][c]; lane = channel chunk
-template <typename T, int RS>
+// wgrad: dw[r][s][c] = sum over pixels of dy[pix] * x[pix + (r,s)][c]; lane = CH channel chunks
+template <typename T, int RS, int CH = 1>
 __global__ void __launch_bounds__(NT) k1_wgrad(Thin t, int LP) {
-  constexpr int VN = V16<T>::N;
+  constexpr int VN = V16<T>::N, VC = VN * CH;
   const es_conv_desc_t& d = t.d;
   const int PPB = NT / LP;
   const int l = threadIdx.x % LP;
-  float acc[RS][VN];
+  float acc[RS][VC];
 #pragma unroll
   for (int j = 0; j < RS; ++j)
 #pragma unroll
-    for (int e = 0; e < VN; ++e) acc[j][e] = 0.f;
-  // two pixels per trip: both pixels' tap loads are issued before the FMAs
+    for (int e = 0; e < VC; ++e) acc[j][e] = 0.f;
+  // two pixels per trip (one with CH > 1): the tap loads are issued before the FMAs
+  constexpr int U = CH > 1 ? 1 : 2;
   const int stride = gridDim.x * PPB;
-  for (int m0 = blockIdx.x * PPB + threadIdx.x / LP; m0 < t.M; m0 += 2 * stride) {
-    float gj[2][RS];
-    float v[2][RS][VN];
+  for (int m0 = blockIdx.x * PPB + threadIdx.x / LP; m0 < t.M; m0 += U * stride) {
+    float gj[U][RS];
+    float v[U][RS][VC];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int mu = m0 + u * stride;
       const bool live = mu < t.M;
       int n, p, q;
       pix3(live ? mu : m0, d.P, d.Q, n, p, q);
       const float g = to_f(((const T*)t.a)[n * t.as[0] + p * t.as[2] + q * t.as[3]]);
-      const T* x = (const T*)t.b + n * t.bs[0] + l * VN;
+      const T* x = (const T*)t.b + n * t.bs[0] + l * VC;
 #pragma unroll
       for (int j = 0; j < RS; ++j) {
         const int hu = p - d.pad + j / d.S, wu = q - d.pad + j % d.S;
         const bool ok = live && hu >= 0 && hu < d.H && wu >= 0 && wu < d.W;
         const T* px = x + (ok ? hu * t.bs[2] + wu * t.bs[3] : 0);   // clamped: loads issue together
         gj[u][j] = ok ? g : 0.f;
-        if constexpr (VN == 8) {
-          ld8<T>(px, v[u][j]);
-        } else {
-          const float4 w4 = *(const float4*)px;
-          v[u][j][0] = w4.x; v[u][j][1] = w4.y; v[u][j][2] = w4.z; v[u][j][3] = w4.w;
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+          if constexpr (VN == 8) {
+            ld8<T>(px + c * VN, &v[u][j][c * VN]);
+          } else {
+            const float4 w4 = *(const float4*)(px + c * VN);
+            v[u][j][c * 4 + 0] = w4.x; v[u][j][c * 4 + 1] = w4.y; v[u][j][c * 4 + 2] = w4.z; v[u][j][c * 4 + 3] = w4.w;
+          }
         }
       }
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int j = 0; j < RS; ++j)
 #pragma unroll
-        for (int e = 0; e < VN; ++e) acc[j][e] += gj[u][j] * v[u][j][e];
+        for (int e = 0; e < VC; ++e) acc[j][e] += gj[u][j] * v[u][j][e];
   }
 #pragma unroll
   for (int j = 0; j < RS; ++j)
 #pragma unroll
-    for (int e = 0; e < VN; ++e)
+    for (int e = 0; e < VC; ++e)
       for (int o = LP; o < 64; o <<= 1) acc[j][e] += __shfl_xor(acc[j][e], o, 64);
   __shared__ float red[4][1024];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -458,7 +473,7 @@ __global__ void __launch_bounds__(NT) k1_wgrad(Thin t, int LP) {
 #pragma unroll
     for (int j = 0; j < RS; ++j)
 #pragma unroll
-      for (int e = 0; e < VN; ++e) red[wid][j * d.C + l * VN + e] = acc[j][e];
+      for (int e = 0; e < VC; ++e) red[wid][j * d.C + l * VC + e] = acc[j][e];
   }
   __syncthreads();
   float* dw = (float*)t.out;
@@ -560,6 +575,27 @@ const int g_k1_grid = env_int("ES_K1_GRID", 2048);
 const int g_thin_wgrid = env_int("ES_THIN_WGRID", 1024);
 unsigned capped(unsigned b, int cap) { return cap > 0 ? std::min<unsigned>(b, (unsigned)cap) : b; }
 
+// channel chunks per lane of the Cout == 1 kernels: 1 = one 16-byte chunk per lane (C / VN lanes per
+// pixel); 2 / 4 = fewer lanes per pixel, more loads in flight per lane, fewer shuffle rounds.  Measured
+// on conv_layers.13 at B = 1024 fp32 (tools/gpu_r04p.sh, us, CH = 1 / 2 / 4): fwd 241 / 226 / 414,
+// dgrad 218 / 323 / 586, wgrad 207 / 169 / 197 -> fwd 2 (ES_K1_CH), dgrad 1 (ES_K1_CH_DG), wgrad 2
+// (ES_K1_CH_WG)
+const int g_k1_ch = env_int("ES_K1_CH", 2);
+const int g_k1_ch_dg = env_int("ES_K1_CH_DG", 1);
+const int g_k1_ch_wg = env_int("ES_K1_CH_WG", 2);
+// CH usable for C / VN chunks (LP = chunks / CH >= 1, a power of two)
+int k1_ch(int chunks, int want) {
+  int ch = want == 4 || want == 2 ? want : 1;
+  while (ch > 1 && chunks % ch) ch >>= 1;
+  return ch;
+}
+#define ES_K1_CH_DISPATCH(CHV, BODY)                                             \
+  do {                                                                          \
+    if ((CHV) == 4) { constexpr int CH = 4; BODY; }                             \
+    else if ((CHV) == 2) { constexpr int CH = 2; BODY; }                        \
+    else { constexpr int CH = 1; BODY; }                                        \
+  } while (0)
+
 template <typename T, typename TO>
 void launch_fwd(const Thin& t, int rs, int LP, hipStream_t st) {
   const es_conv_desc_t& d = t.d;
@@ -568,9 +604,12 @@ void launch_fwd(const Thin& t, int rs, int LP, hipStream_t st) {
     if (rs == 4) hipLaunchKernelGGL((c1_fwd<T, TO, 4>), grid, dim3(NT), 0, st, t);
     else hipLaunchKernelGGL((c1_fwd<T, TO, 9>), grid, dim3(NT), 0, st, t);
   } else {
-    const dim3 grid(capped(blocks(t.M, NT / LP), g_k1_grid));
-    if (rs == 4) hipLaunchKernelGGL((k1_fwd<T, TO, 4>), grid, dim3(NT), 0, st, t, LP);
-    else hipLaunchKernelGGL((k1_fwd<T, TO, 9>), grid, dim3(NT), 0, st, t, LP);
+    const int ch = k1_ch(LP, g_k1_ch), lp = LP / ch;
+    const dim3 grid(capped(blocks(t.M, NT / lp), g_k1_grid));
+    ES_K1_CH_DISPATCH(ch, {
+      if (rs == 4) hipLaunchKernelGGL((k1_fwd<T, TO, 4, CH>), grid, dim3(NT), 0, st, t, lp);
+      else hipLaunchKernelGGL((k1_fwd<T, TO, 9, CH>), grid, dim3(NT), 0, st, t, lp);
+    });
   }
 }
 
@@ -582,17 +621,21 @@ void launch_dgrad(const Thin& t, int rs, int LP, hipStream_t st) {
     if (rs == 4) hipLaunchKernelGGL((c1_dgrad<T, TO, 4>), grid, dim3(NT), 0, st, t);
     else hipLaunchKernelGGL((c1_dgrad<T, TO, 9>), grid, dim3(NT), 0, st, t);
   } else {
-    const dim3 grid(capped(blocks(t.M, NT / LP), g_k1_grid));
-    if (rs == 4) hipLaunchKernelGGL((k1_dgrad<T, TO, 4>), grid, dim3(NT), 0, st, t, LP);
-    else hipLaunchKernelGGL((k1_dgrad<T, TO, 9>), grid, dim3(NT), 0, st, t, LP);
+    const int ch = k1_ch(LP, g_k1_ch_dg), lp = LP / ch;
+    const dim3 grid(capped(blocks(t.M, NT / lp), g_k1_grid));
+    ES_K1_CH_DISPATCH(ch, {
+      if (rs == 4) hipLaunchKernelGGL((k1_dgrad<T, TO, 4, CH>), grid, dim3(NT), 0, st, t, lp);
+      else hipLaunchKernelGGL((k1_dgrad<T, TO, 9, CH>), grid, dim3(NT), 0, st, t, lp);
+    });
   }
 }
 
 template <typename T>
 void launch_wgrad(const Thin& t, int rs, int LP, hipStream_t st) {
   const es_conv_desc_t& d = t.d;
+  const int ch = d.C == 1 ? 1 : k1_ch(LP, g_k1_ch_wg), lp = d.C == 1 ? LP : LP / ch;
   // ~4 blocks per CU, each reducing a strided slice of the pixels
-  const int per = d.C == 1 ? NT / (d.K / 8) : NT / LP;
+  const int per = d.C == 1 ? NT / (d.K / 8) : NT / lp;
   dim3 grid(capped(blocks(t.M, per), g_thin_wgrid));
   if (t.det) {   // deterministic mode: one partial slot per block within the caller's workspace
     const int64_t slot = (int64_t)d.K * rs * d.C;
@@ -603,8 +646,10 @@ void launch_wgrad(const Thin& t, int rs, int LP, hipStream_t st) {
     if (rs == 4) hipLaunchKernelGGL((c1_wgrad<T, 4>), grid, dim3(NT), 0, st, t);
     else hipLaunchKernelGGL((c1_wgrad<T, 9>), grid, dim3(NT), 0, st, t);
   } else {
-    if (rs == 4) hipLaunchKernelGGL((k1_wgrad<T, 4>), grid, dim3(NT), 0, st, t, LP);
-    else hipLaunchKernelGGL((k1_wgrad<T, 9>), grid, dim3(NT), 0, st, t, LP);
+    ES_K1_CH_DISPATCH(ch, {
+      if (rs == 4) hipLaunchKernelGGL((k1_wgrad<T, 4, CH>), grid, dim3(NT), 0, st, t, lp);
+      else hipLaunchKernelGGL((k1_wgrad<T, 9, CH>), grid, dim3(NT), 0, st, t, lp);
+    });
   }
 }
 

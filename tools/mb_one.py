@@ -1,6 +1,6 @@
 """Run ONE conv op of the neutron generator a few times (for rocprofv3 --pmc passes).
 
-usage: python tools/mb_one.py <c0|c5|c9|p1|p5> <fwd|dgrad|wgrad> [ring 1|0] [reps]
+usage: python tools/mb_one.py <c0|c5|c9|c13|p1|p5> <fwd|dgrad|wgrad> [ring 1|0] [reps]
 (ES_MB_BATCH=<images> overrides the batch of 512; ES_MB_DTYPE=fp32 runs the parity mode's fp32 ring
 kernels with the deterministic weight gradient, ES_MB_SPLIT=1 with split-fp32 arithmetic)"""
 import os
@@ -15,7 +15,7 @@ from expertsim import hip  # noqa: E402
 from expertsim.layers import Act, ConvOp, Upsample  # noqa: E402
 
 SHAPES = {"c0": (512, 128, 13, 13, 256, 3, 1, 0, (2, 2)), "c5": (512, 256, 24, 24, 128, 3, 1, 0, (2, 2)),
-          "c9": (512, 128, 46, 46, 64, 2, 1, 0, None),
+          "c9": (512, 128, 46, 46, 64, 2, 1, 0, None), "c13": (512, 64, 45, 45, 1, 2, 1, 0, None),
           # proton (proton/generator.py:26-38): conv_layers.1 on the x2 upsample, conv_layers.5 on the
           # 35x19 -> 56x30 resize
           "p1": (512, 512, 18, 10, 256, 4, 1, 1, (2, 2)), "p5": (512, 256, 35, 19, 128, 4, 1, 1, "56x30")}
