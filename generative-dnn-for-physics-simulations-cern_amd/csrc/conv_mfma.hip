@@ -68,6 +68,13 @@ constexpr uint32_t OOB = 0x80000000u;
 #endif
 #ifndef ES_SPB_PFD
 #define ES_SPB_PFD 2   // split-fp32 SPB loop: column tiles of B planes read ahead of their MFMAs
+#endif
+#ifndef ES_SPB_FRESH
+// SPB loop (8-wave split-fp32 FWD / DGRAD): K-steps per fresh accumulator.  Measured (tools/gpu_r04w.sh,
+// alternating on one box, B = 1024): 1 -> 2 conv_layers.5 FWD 3.06-3.13 -> 2.94, DGRAD 2.99-3.03 ->
+// 2.82-2.84 ms, step -1.4..-2.3 %; 4 is slower (3.34 / 3.50 ms: the carried accumulators crowd the
+// registers).  The noise-only bias gradients of the B = 1024 golden stay at 4-5e-6 (1e-5 with 1).
+#define ES_SPB_FRESH 2
 #endif   // buffer offset past every num_records (< 2^31 bytes)
 
 // ES_NO_RING=1 (or es_conv_set_ring(0)) routes these shapes to the 4-wave kernels of
@@ -347,8 +354,18 @@ __device__ __forceinline__ void split8(const f32x4& x, const f32x4& y, bf16x8 p[
 // accumulation rounds with a negative bias (measured, tools/split_bias.py: summed outputs drift by
 // -5e-8 .. -1.2e-6 of sum|y| when every product accumulates into the running sum), so the step's
 // products go into a fresh accumulator (its rounding is on the scale of one K-step's partial sum)
-// and the running sum takes them with one round-to-nearest add per element.  (A plain C++ add: the
+// and the running sum takes them with one round-to-nearest add per element.  (The 8-wave FWD /
+// DGRAD loop carries one fresh accumulator over ES_SPB_FRESH = 2 K-steps: mfma_chain6.)  (A plain C++ add: the
 // compiler's MFMA-result hazard wait states do not cover inline asm that reads the MFMA's output.)
+// the six plane products chained onto c (small terms first), without the running-sum add
+__device__ __forceinline__ f32x4 mfma_chain6(const bf16x8 a[3], const bf16x8 b[3], f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
+}
 __device__ __forceinline__ f32x4 mfma_split6(const bf16x8 a[3], const bf16x8 b[3], f32x4 acc) {
   f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], c, 0, 0, 0);
@@ -1030,7 +1047,12 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
     }
     int sa1 = 1 % NSA, sb = 0, ia = 0, ib = NSB - 1;   // slots: A(t+1), B(t), A(t+NSA), B(t+NSB-1)
     constexpr int JS = RN > 2 ? RN / 2 : RN - 1;       // column tile after which A(t+1) is split
-    for (int t = 0; t < nk; ++t) {
+    // ES_SPB_FRESH = G > 1: the first step of every group of G starts a fresh accumulator (cst), the
+    // middle ones continue it, the last continues it and adds it to the running sums
+    constexpr int FG = ES_SPB_FRESH, CR = FG > 1 ? RM : 1, CN = FG > 1 ? RN : 1;
+    f32x4 cst[CR][CN];
+    auto step = [&](auto phase) {   // phase: 0 = one-step group, 1 = first, 3 = middle, 2 = last
+      constexpr int PH = decltype(phase)::value;
       wait_vmcnt<LOOPWAIT>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of the last step are done
       ring_barrier();
@@ -1047,7 +1069,12 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
       for (int j = 0; j < RN; ++j) {
         if (j + PFD < RN) rd_b(bq[(j + PFD) % (PFD + 1)], bimg, j + PFD);
 #pragma unroll
-        for (int i = 0; i < RM; ++i) acc[i][j] = mfma_split6(apc[i], bq[j % (PFD + 1)], acc[i][j]);
+        for (int i = 0; i < RM; ++i) {
+          if constexpr (PH == 0) acc[i][j] = mfma_split6(apc[i], bq[j % (PFD + 1)], acc[i][j]);
+          else if constexpr (PH == 1) cst[i % CR][j % CN] = mfma_chain6(apc[i], bq[j % (PFD + 1)], f32x4{0.f, 0.f, 0.f, 0.f});
+          else if constexpr (PH == 3) cst[i % CR][j % CN] = mfma_chain6(apc[i], bq[j % (PFD + 1)], cst[i % CR][j % CN]);
+          else acc[i][j] = acc[i][j] + mfma_chain6(apc[i], bq[j % (PFD + 1)], cst[i % CR][j % CN]);
+        }
         if (j == 0) {   // the step's DMA, once its first MFMAs are queued
           issue_b(bring + ib * BBYTES);
           issue(aring + ia * ABYTES);
@@ -1065,6 +1092,18 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
       ia = ia + 1 == NSA ? 0 : ia + 1;
       sb = sb + 1 == NSB ? 0 : sb + 1;
       ib = ib + 1 == NSB ? 0 : ib + 1;
+    };
+    if constexpr (FG > 1) {
+      int t = 0;
+      for (; t + FG <= nk; t += FG) {
+        step(std::integral_constant<int, 1>{});
+#pragma unroll
+        for (int u = 1; u < FG - 1; ++u) step(std::integral_constant<int, 3>{});
+        step(std::integral_constant<int, 2>{});
+      }
+      for (; t < nk; ++t) step(std::integral_constant<int, 0>{});   // (the remainder one step at a time)
+    } else {
+      for (int t = 0; t < nk; ++t) step(std::integral_constant<int, 0>{});
     }
     wait_vmcnt<0>();   // drain the zero-fill steps before the workgroup may exit
   } else if constexpr (SPL) {
