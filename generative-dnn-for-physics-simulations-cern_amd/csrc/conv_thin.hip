@@ -325,7 +325,7 @@ __global__ void __launch_bounds__(NT) k1_dgrad(Thin t, int LP) {
 // keep bits into per-channel sums of dnorm and dnorm * xhat (the expressions of norm_fast.hip
 // bn_reduce_fast); per block one [3][C] partial (slots 1, 2).
 struct ThinBnr {
-  const bf16* x;
+  const void* x;                    // the norm input h (the dgrad's dtype)
   const uint8_t* keep;
   const float *mean, *invstd, *gamma, *beta;
   float scale, slope;
@@ -333,14 +333,15 @@ struct ThinBnr {
   float* part;
 };
 
-template <int RS>
+// T = bf16 or float (round 4: the fp32 parity mode too; a lane owns 8 channels either way)
+template <typename T, int RS>
 __global__ void __launch_bounds__(NT) k1_dgrad_bnred(Thin t, int LP, ThinBnr b) {
   const es_conv_desc_t& d = t.d;
   __shared__ float wf[1024];                                  // transposed to [R*S][C]
   __shared__ float r1[NT * 8], r2[NT * 8];
   for (int i = threadIdx.x; i < RS * d.C; i += NT) {
     const int c = i / RS, j = i % RS;
-    wf[j * d.C + c] = to_f(((const bf16*)t.w)[i]);
+    wf[j * d.C + c] = to_f(((const T*)t.w)[i]);
   }
   const int PPB = NT / LP;
   const int l = threadIdx.x % LP;
@@ -359,10 +360,10 @@ __global__ void __launch_bounds__(NT) k1_dgrad_bnred(Thin t, int LP, ThinBnr b) 
   for (int m = blockIdx.x * PPB + threadIdx.x / LP; m < t.M; m += gridDim.x * PPB) {
     int n, h, w;
     pix3(m, d.H, d.W, n, h, w);
-    const bf16* dy = (const bf16*)t.a + n * t.as[0];
+    const T* dy = (const T*)t.a + n * t.as[0];
     const int64_t off = n * t.os[0] + h * t.os[2] + w * t.os[3] + l * 8;
     float hv[8];
-    ld8<bf16>(b.x + off, hv);                                 // issued before the tap loads' FMAs
+    ld8<T>((const T*)b.x + off, hv);                          // issued before the tap loads' FMAs
     const uint32_t kb = b.drop ? (uint32_t)b.keep[(int64_t)m * (d.C / 8) + l] : 0xFFu;
     float acc[8];
 #pragma unroll
@@ -377,10 +378,10 @@ __global__ void __launch_bounds__(NT) k1_dgrad_bnred(Thin t, int LP, ThinBnr b) 
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[e] += g * wr[e];
     }
-    st8<bf16>((bf16*)t.out + off, acc);
+    st8<T>((T*)t.out + off, acc);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float dv = (float)(bf16)acc[e], v = hv[e];       // the stored dx value
+      const float dv = std::is_same<T, bf16>::value ? (float)(bf16)acc[e] : acc[e], v = hv[e];   // the stored dx
       const bool keep = (kb >> e) & 1u;
       const float z = v * sc[e] + sh[e];
       const float zs = b.drop && b.dfirst ? z * b.scale : z;
@@ -581,6 +582,8 @@ unsigned capped(unsigned b, int cap) { return cap > 0 ? std::min<unsigned>(b, (u
 // dgrad 218 / 323 / 586, wgrad 207 / 169 / 197 -> fwd 2 (ES_K1_CH), dgrad 1 (ES_K1_CH_DG), wgrad 2
 // (ES_K1_CH_WG)
 const int g_k1_ch = env_int("ES_K1_CH", 2);
+// thin Cout = 1 dgrad + BatchNorm-backward reduction (k1_dgrad_bnred); ES_THIN_BNRED=0 off (A/B)
+const bool g_thin_bnred = env_int("ES_THIN_BNRED", 1) != 0;
 const int g_k1_ch_dg = env_int("ES_K1_CH_DG", 1);
 const int g_k1_ch_wg = env_int("ES_K1_CH_WG", 2);
 // CH usable for C / VN chunks (LP = chunks / CH >= 1, a power of two)
@@ -716,22 +719,29 @@ int es_thin_conv_dgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, c
   t.M = d->N * d->H * d->W;
   const int LP = k1 ? d->C / vn : 1;
   const BnRedRequest& q = g_bnr_req;
-  if (k1 && q.part && q.x && q.nm && q.ch && dt == ES_BF16 && dxdt == ES_BF16 && beta == 0.f && (rs == 4 || rs == 9) &&
+  const int lp8 = d->C / 8;   // the fused kernel's lanes per pixel: 8 channels per lane in both dtypes
+  if (k1 && q.part && q.x && q.nm && q.ch && dt == dxdt && g_thin_bnred && beta == 0.f && (rs == 4 || rs == 9) &&
+      pow2(lp8) && lp8 <= 64 && d->C % 8 == 0 &&
       dxs[3] == d->C && dxs[2] == (int64_t)d->W * d->C && dxs[0] == (int64_t)d->H * d->W * d->C &&
       ((uintptr_t)q.x & 15) == 0 && (q.ch->act == ES_ACT_LRELU || q.ch->act == ES_ACT_RELU) &&
       (!q.ch->drop.enabled || q.ch->keep)) {
-    const dim3 grid(capped(blocks(t.M, NT / LP), g_k1_grid));
+    const dim3 grid(capped(blocks(t.M, NT / lp8), g_k1_grid));
     if ((int64_t)grid.x * 3 * d->C <= q.floats) {
       ThinBnr b{};
-      b.x = (const bf16*)q.x; b.keep = q.ch->keep;
+      b.x = q.x; b.keep = q.ch->keep;
       b.mean = q.nm->mean; b.invstd = q.nm->invstd; b.gamma = q.nm->gamma; b.beta = q.nm->beta;
       b.drop = q.ch->drop.enabled != 0;
       b.scale = b.drop ? q.ch->drop.scale : 1.f;
       b.dfirst = q.ch->dropout_first;
       b.slope = q.ch->act == ES_ACT_LRELU ? q.ch->slope : 0.f;
       b.part = q.part;
-      if (rs == 4) hipLaunchKernelGGL((k1_dgrad_bnred<4>), grid, dim3(NT), 0, st, t, LP, b);
-      else hipLaunchKernelGGL((k1_dgrad_bnred<9>), grid, dim3(NT), 0, st, t, LP, b);
+      if (dt == ES_BF16) {
+        if (rs == 4) hipLaunchKernelGGL((k1_dgrad_bnred<bf16, 4>), grid, dim3(NT), 0, st, t, lp8, b);
+        else hipLaunchKernelGGL((k1_dgrad_bnred<bf16, 9>), grid, dim3(NT), 0, st, t, lp8, b);
+      } else {
+        if (rs == 4) hipLaunchKernelGGL((k1_dgrad_bnred<float, 4>), grid, dim3(NT), 0, st, t, lp8, b);
+        else hipLaunchKernelGGL((k1_dgrad_bnred<float, 9>), grid, dim3(NT), 0, st, t, lp8, b);
+      }
       g_bnr_req.chunks = (int)grid.x;
       return 1;
     }

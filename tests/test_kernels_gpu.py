@@ -834,6 +834,53 @@ def test_conv_dgrad_bn_reduce_fused(case, dfirst):
     assert rel(dh1, dh0) < 1e-2
 
 
+@pytest.mark.parametrize("case", [(50, 64, 45, 45, 1, 2), (7, 64, 13, 11, 1, 2), (5, 32, 12, 10, 1, 3)])
+@pytest.mark.parametrize("dfirst", [True, False])
+def test_thin_dgrad_bn_reduce_fused_fp32(case, dfirst):
+    """Round 4: the thin Cout = 1 dgrad fused with the BatchNorm-backward reduction in the fp32 parity
+    mode (conv_layers.13 -> BatchNorm conv_layers.10 + Dropout + LeakyReLU, neutron/generator.py:33-37;
+    k1_dgrad_bnred<float>): the dgrad output is bitwise the unfused one; dgamma / dbeta / the conv-bias
+    sum / dh equal the two-pass backward up to the order of the per-channel sums."""
+    hip = _hip()
+    from expertsim import layers
+    from expertsim.layers import Act, ConvOp, NormOp
+    N, Cin, H, W, Cout, k = case
+    old_det = layers.deterministic()
+    layers.set_deterministic(True)
+    try:
+        torch.manual_seed(17)
+        w = torch.randn(Cout, Cin, k, k, device=DEV) / np.sqrt(Cin * k * k)
+        op = ConvOp(torch.nn.Parameter(w), torch.nn.Parameter(torch.zeros(Cout, device=DEV)))
+        h = Act.nhwc(N, Cin, H, W, torch.float32, DEV)
+        h.t.copy_((torch.randn(h.t.shape) * 2 + 0.3).to(DEV))
+        gamma, beta = (torch.rand(Cin) + 0.5).to(DEV), torch.randn(Cin).to(DEV)
+        bn = NormOp(hip.NORM_BN, gamma, beta, running_mean=torch.zeros(Cin, device=DEV),
+                    running_var=torch.ones(Cin, device=DEV))
+        ch = hip.chain_struct(hip.ACT_LRELU, 0.1, hip.dropout_struct(0.2, 4321, 9, enabled=True), dropout_first=dfirst)
+        kb = hip.attach_keep(ch, N * H * W, Cin, DEV)   # noqa: F841 (kept alive for the backward)
+        y, stats = bn.fwd(h, ch)
+        P, Q = H - k + 1, W - k + 1
+        gy = Act.nhwc(N, Cout, P, Q, torch.float32, DEV)
+        gy.t.copy_(torch.randn(gy.t.shape, generator=torch.Generator().manual_seed(3)).to(DEV))
+        outs = []
+        for fused in (False, True):
+            dx = op.dgrad(gy, y, dx_dtype=torch.float32, bn_reduce=(bn, h, stats, ch) if fused else None)
+            if fused:
+                assert getattr(dx, "bn_sums", None) is not None, "fp32 thin dgrad did not fuse the reduction"
+            dg, db, ds = (torch.zeros(Cin, device=DEV) for _ in range(3))
+            dh = bn.bwd(h, stats, ch, dx, dgamma=dg, dbeta=db, dsum=ds)
+            torch.cuda.synchronize()
+            outs.append((dx.t.clone(), dh.t.float().cpu(), dg.cpu(), db.cpu(), ds.cpu()))
+        (dx0, dh0, dg0, db0, ds0), (dx1, dh1, dg1, db1, ds1) = outs
+        assert torch.equal(dx0, dx1)
+        assert rel(dg1, dg0) < 1e-5 and rel(db1, db0) < 1e-5
+        scale = float(dh0.abs().reshape(-1, Cin).sum(0).max())
+        assert float((ds1 - ds0).abs().max()) < 1e-5 * scale
+        assert rel(dh1, dh0) < 1e-5
+    finally:
+        layers.set_deterministic(old_det)
+
+
 @pytest.mark.parametrize("case", [(64, 128, 46, 46, 64, 2, None), (70, 128, 23, 21, 64, 2, None),
                                   (64, 256, 12, 12, 128, 3, (2, 2)), (40, 128, 13, 13, 256, 3, (2, 2))])
 @pytest.mark.parametrize("split", [True, False])
