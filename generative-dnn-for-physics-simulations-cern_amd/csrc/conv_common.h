@@ -109,6 +109,16 @@ struct BnRedRequest {
 };
 extern thread_local BnRedRequest g_bnr_req;
 
+// Normalise-on-load (es_conv_norm_on_load): the conv's activation operand x is the PRE-norm h of a
+// BatchNorm + dropout + activation chain, applied per element as it is loaded (the thin Cout = 1
+// fwd / wgrad, fp32).  on: set by the host call; used: set by the kernel path that honoured it.
+struct NolRequest {
+  int on, used;
+  es_norm_t nm;
+  es_chain_t ch;
+};
+extern thread_local NolRequest g_nol_req;
+
 
 // es_conv2d_fwd_stats: the caller's request for fused BatchNorm partials (host, per thread); the
 // ring FWD launch sets chunks when it writes them.

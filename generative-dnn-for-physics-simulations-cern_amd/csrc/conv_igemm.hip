@@ -1081,6 +1081,23 @@ extern "C" int es_conv_set_glds(int on) {
   return old;
 }
 
+thread_local NolRequest g_nol_req;
+
+// normalise-on-load for the next conv entry call(s) on this thread (nm == NULL clears); only the thin
+// Cout = 1 fp32 fwd / wgrad honour it, every other path fails with ES_ERR_ARG while it is set
+extern "C" int es_conv_norm_on_load(const es_norm_t* nm, const es_chain_t* ch) {
+  if (!nm) {
+    g_nol_req = NolRequest{};
+    return ES_OK;
+  }
+  ES_CHECK_ARG(ch && nm->mean && nm->invstd, "es_conv_norm_on_load: statistics / chain missing");
+  g_nol_req.on = 1;
+  g_nol_req.used = 0;
+  g_nol_req.nm = *nm;
+  g_nol_req.ch = *ch;
+  return ES_OK;
+}
+
 extern "C" int es_conv2d_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x,
                              const int64_t xs[4], const void* wk, const float* bias, void* y,
                              es_dtype_t ydt, const int64_t ys[4], es_stream_t stream) {
@@ -1092,6 +1109,7 @@ extern "C" int es_conv2d_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void*
     ES_CHECK_LAUNCH();
     return ES_OK;
   }
+  ES_CHECK_ARG(!g_nol_req.on, "conv fwd: normalise-on-load requested for a conv off the thin fp32 path");
   ConvArgs a{};
   a.d = *d; a.a_src = x; a.b_src = wk; a.out = y; a.bias = bias; a.beta = 0.f;
   a.a_planes = g_planes_req.on;
@@ -1209,6 +1227,7 @@ extern "C" int es_conv2d_wgrad(const es_conv_desc_t* d, es_dtype_t dt, const voi
     ES_CHECK_LAUNCH();
     return ES_OK;
   }
+  ES_CHECK_ARG(!g_nol_req.on, "conv wgrad: normalise-on-load requested for a conv off the thin fp32 path");
   ConvArgs a{};
   a.d = *d; a.a_src = dy; a.b_src = x; a.out = dw;
   for (int i = 0; i < 4; ++i) { a.as[i] = ys[i]; a.bs[i] = xs[i]; }
@@ -1253,7 +1272,7 @@ extern "C" int es_conv2d_wgrad_det(const es_conv_desc_t* d, es_dtype_t dt, const
   ExecTally tally(d, dt);
   const hipStream_t st = (hipStream_t)stream;
   const int64_t floats = ws_bytes / (int64_t)sizeof(float);
-  if (dt == ES_F32) {
+  if (dt == ES_F32 && !g_nol_req.on) {
     const int rc = es_wgrad_f32_ring(*d, dy, ys, x, xs, dw, beta, (float*)ws, floats, st);
     if (rc < 0) return ES_ERR_ARG;
     if (rc > 0) {
@@ -1266,6 +1285,10 @@ extern "C" int es_conv2d_wgrad_det(const es_conv_desc_t* d, es_dtype_t dt, const
   g_det_req = DetRequest{(float*)ws, floats, 0};
   int rc = es_thin_conv_wgrad(d, dt, dy, ys, x, xs, (float*)ws, st) ? ES_OK : -1;
   tally.thin = rc == ES_OK;
+  if (rc != ES_OK && g_nol_req.on) {
+    g_det_req = DetRequest{nullptr, 0, 0};
+    ES_CHECK_ARG(false, "conv wgrad det: normalise-on-load requested for a conv off the thin fp32 path");
+  }
   if (rc != ES_OK) {
     ConvArgs a{};
     a.d = *d; a.a_src = dy; a.b_src = x; a.out = ws;

@@ -47,7 +47,23 @@ template <> __device__ __forceinline__ void st8<float>(float* p, const float* f)
   ((float4*)p)[1] = make_float4(f[4], f[5], f[6], f[7]);
 }
 
+// normalise-on-load parameters (NolRequest): y = chain(gamma * (h - mean) * invstd + beta, keep), the
+// expressions of norm_fast.hip bn_fwd_fast (bitwise the same y)
+struct NolArgs {
+  const float *mean, *invstd, *gamma, *beta;
+  const uint8_t* keep;              // [n*h*w][C/8] (dropout on)
+  float scale, slope;
+  int drop, dfirst, act;
+};
+__device__ __forceinline__ float nol_chain(const NolArgs& q, float z, bool keep) {
+  auto act = [&](float v) { return q.act == ES_ACT_RELU ? fmaxf(v, 0.f) : (q.act == ES_ACT_LRELU ? lrelu(v, q.slope) : v); };
+  if (!q.drop) return act(z);
+  if (q.dfirst) return act(keep ? z * q.scale : 0.f);
+  return keep ? act(z) * q.scale : 0.f;
+}
+
 struct Thin {
+  NolArgs nl;                      // fwd / wgrad x: normalise-on-load (NOL kernels only)
   es_conv_desc_t d;
   const void* a; int64_t as[4];    // fwd: x;  dgrad / wgrad: dy
   const void* b; int64_t bs[4];    // wgrad: x
@@ -215,15 +231,26 @@ __global__ void __launch_bounds__(NT) c1_wgrad(Thin t) {
 // ============================================================ Cout == 1
 // A pixel is served by LP = C/(VN*CH) lanes (CH 16-byte channel chunks each); 64/LP pixels per wave.
 // fwd: y = bias + sum over taps of <x row chunks, w chunks>, reduced over the LP lanes.
-template <typename T, typename TO, int RS, int CH = 1>
+template <typename T, typename TO, int RS, int CH = 1, bool NOL = false>
 __global__ void __launch_bounds__(NT) k1_fwd(Thin t, int LP) {
   constexpr int VN = V16<T>::N;
+  static_assert(!NOL || VN * CH == 8, "normalise-on-load: 8 channels (one keep byte) per lane");
   const es_conv_desc_t& d = t.d;
   __shared__ float wf[1024];
   for (int i = threadIdx.x; i < RS * d.C; i += NT) wf[i] = to_f(((const T*)t.w)[i]);   // [R][S][C]
   __syncthreads();
   const int PPB = NT / LP;
   const int l = threadIdx.x % LP;
+  float nsc[NOL ? 8 : 1], nsh[NOL ? 8 : 1];
+  if constexpr (NOL) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = l * 8 + e;
+      const float sc = (t.nl.gamma ? t.nl.gamma[c] : 1.f) * t.nl.invstd[c];
+      nsc[e] = sc;
+      nsh[e] = (t.nl.beta ? t.nl.beta[c] : 0.f) - t.nl.mean[c] * sc;
+    }
+  }
   // block-uniform grid-stride loop (the weights are staged once per block; the LP lanes of a
   // pixel stay in step for the shuffle reduction)
   for (int mb = blockIdx.x * PPB; mb < t.M; mb += gridDim.x * PPB) {
@@ -238,6 +265,10 @@ __global__ void __launch_bounds__(NT) k1_fwd(Thin t, int LP) {
     const int hu = p - d.pad + j / d.S, wu = q - d.pad + j % d.S;
     const bool ok = live && hu >= 0 && hu < d.H && wu >= 0 && wu < d.W;
     const T* px = x + (ok ? hu * t.as[2] + wu * t.as[3] : 0);   // clamped: the taps' loads issue together
+    uint32_t kb = 0xFFu;
+    if constexpr (NOL) {
+      if (t.nl.drop) kb = t.nl.keep[((int64_t)n * d.H * d.W + (ok ? hu * d.W + wu : 0)) * (d.C >> 3) + l];
+    }
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const float* pw = wf + j * d.C + (l * CH + c) * VN;
@@ -247,7 +278,14 @@ __global__ void __launch_bounds__(NT) k1_fwd(Thin t, int LP) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) s += (ok ? v[e] : 0.f) * pw[e];
       } else {
-        const float4 v = *(const float4*)(px + c * VN);
+        float4 v = *(const float4*)(px + c * VN);
+        if constexpr (NOL) {
+          const int e0 = c * 4;
+          v.x = nol_chain(t.nl, v.x * nsc[e0 + 0] + nsh[e0 + 0], (kb >> (e0 + 0)) & 1u);
+          v.y = nol_chain(t.nl, v.y * nsc[e0 + 1] + nsh[e0 + 1], (kb >> (e0 + 1)) & 1u);
+          v.z = nol_chain(t.nl, v.z * nsc[e0 + 2] + nsh[e0 + 2], (kb >> (e0 + 2)) & 1u);
+          v.w = nol_chain(t.nl, v.w * nsc[e0 + 3] + nsh[e0 + 3], (kb >> (e0 + 3)) & 1u);
+        }
         if (ok) s += v.x * pw[0] + v.y * pw[1] + v.z * pw[2] + v.w * pw[3];
       }
     }
@@ -414,12 +452,23 @@ __global__ void __launch_bounds__(NT) k1_dgrad_bnred(Thin t, int LP, ThinBnr b) 
 }
 
 // wgrad: dw[r][s][c] = sum over pixels of dy[pix] * x[pix + (r,s)][c]; lane = CH channel chunks
-template <typename T, int RS, int CH = 1>
+template <typename T, int RS, int CH = 1, bool NOL = false>
 __global__ void __launch_bounds__(NT) k1_wgrad(Thin t, int LP) {
   constexpr int VN = V16<T>::N, VC = VN * CH;
+  static_assert(!NOL || VC == 8, "normalise-on-load: 8 channels (one keep byte) per lane");
   const es_conv_desc_t& d = t.d;
   const int PPB = NT / LP;
   const int l = threadIdx.x % LP;
+  float nsc[NOL ? 8 : 1], nsh[NOL ? 8 : 1];
+  if constexpr (NOL) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = l * 8 + e;
+      const float sc = (t.nl.gamma ? t.nl.gamma[c] : 1.f) * t.nl.invstd[c];
+      nsc[e] = sc;
+      nsh[e] = (t.nl.beta ? t.nl.beta[c] : 0.f) - t.nl.mean[c] * sc;
+    }
+  }
   float acc[RS][VC];
 #pragma unroll
   for (int j = 0; j < RS; ++j)
@@ -453,6 +502,12 @@ __global__ void __launch_bounds__(NT) k1_wgrad(Thin t, int LP) {
             const float4 w4 = *(const float4*)(px + c * VN);
             v[u][j][c * 4 + 0] = w4.x; v[u][j][c * 4 + 1] = w4.y; v[u][j][c * 4 + 2] = w4.z; v[u][j][c * 4 + 3] = w4.w;
           }
+        }
+        if constexpr (NOL) {
+          const uint32_t kb = t.nl.drop ? t.nl.keep[((int64_t)n * d.H * d.W + (ok ? hu * d.W + wu : 0)) * (d.C >> 3) + l]
+                                        : 0xFFu;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[u][j][e] = nol_chain(t.nl, v[u][j][e] * nsc[e] + nsh[e], (kb >> e) & 1u);
         }
       }
     }
@@ -600,13 +655,22 @@ int k1_ch(int chunks, int want) {
   } while (0)
 
 template <typename T, typename TO>
-void launch_fwd(const Thin& t, int rs, int LP, hipStream_t st) {
+void launch_fwd(const Thin& t, int rs, int LP, hipStream_t st, bool nol = false) {
   const es_conv_desc_t& d = t.d;
   if (d.C == 1) {
     const dim3 grid(blocks(t.M, NT / (d.K / (16 / (int)sizeof(TO)))));
     if (rs == 4) hipLaunchKernelGGL((c1_fwd<T, TO, 4>), grid, dim3(NT), 0, st, t);
     else hipLaunchKernelGGL((c1_fwd<T, TO, 9>), grid, dim3(NT), 0, st, t);
   } else {
+    if constexpr (std::is_same<T, float>::value) {
+      if (nol) {   // normalise-on-load: 8 channels (2 chunks) per lane
+        const int lp = LP / 2;
+        const dim3 grid(capped(blocks(t.M, NT / lp), g_k1_grid));
+        if (rs == 4) hipLaunchKernelGGL((k1_fwd<T, TO, 4, 2, true>), grid, dim3(NT), 0, st, t, lp);
+        else hipLaunchKernelGGL((k1_fwd<T, TO, 9, 2, true>), grid, dim3(NT), 0, st, t, lp);
+        return;
+      }
+    }
     const int ch = k1_ch(LP, g_k1_ch), lp = LP / ch;
     const dim3 grid(capped(blocks(t.M, NT / lp), g_k1_grid));
     ES_K1_CH_DISPATCH(ch, {
@@ -634,9 +698,9 @@ void launch_dgrad(const Thin& t, int rs, int LP, hipStream_t st) {
 }
 
 template <typename T>
-void launch_wgrad(const Thin& t, int rs, int LP, hipStream_t st) {
+void launch_wgrad(const Thin& t, int rs, int LP, hipStream_t st, bool nol = false) {
   const es_conv_desc_t& d = t.d;
-  const int ch = d.C == 1 ? 1 : k1_ch(LP, g_k1_ch_wg), lp = d.C == 1 ? LP : LP / ch;
+  const int ch = nol ? 2 : (d.C == 1 ? 1 : k1_ch(LP, g_k1_ch_wg)), lp = d.C == 1 ? LP : LP / ch;
   // ~4 blocks per CU, each reducing a strided slice of the pixels
   const int per = d.C == 1 ? NT / (d.K / 8) : NT / lp;
   dim3 grid(capped(blocks(t.M, per), g_thin_wgrid));
@@ -648,6 +712,11 @@ void launch_wgrad(const Thin& t, int rs, int LP, hipStream_t st) {
   if (d.C == 1) {
     if (rs == 4) hipLaunchKernelGGL((c1_wgrad<T, 4>), grid, dim3(NT), 0, st, t);
     else hipLaunchKernelGGL((c1_wgrad<T, 9>), grid, dim3(NT), 0, st, t);
+  } else if (nol) {
+    if constexpr (std::is_same<T, float>::value) {
+      if (rs == 4) hipLaunchKernelGGL((k1_wgrad<T, 4, 2, true>), grid, dim3(NT), 0, st, t, lp);
+      else hipLaunchKernelGGL((k1_wgrad<T, 9, 2, true>), grid, dim3(NT), 0, st, t, lp);
+    }
   } else {
     ES_K1_CH_DISPATCH(ch, {
       if (rs == 4) hipLaunchKernelGGL((k1_wgrad<T, 4, CH>), grid, dim3(NT), 0, st, t, lp);
@@ -670,6 +739,25 @@ void small_dispatch(int K, F&& f) {
   else f(std::integral_constant<int, 16>{});
 }
 
+// normalise-on-load request for a thin fp32 Cout = 1 fwd / wgrad over a dense NHWC x (8-channel lanes);
+// returns true (and fills t.nl, marks the request used) when it applies
+bool take_nol(Thin& t, const es_conv_desc_t* d, es_dtype_t dt, const int64_t xs[4], int LP, bool k1) {
+  NolRequest& q = g_nol_req;
+  if (!q.on) return false;
+  if (!k1 || dt != ES_F32 || LP % 2 || d->C % 8 || xs[1] != 1 || xs[3] != d->C || xs[2] != (int64_t)d->W * d->C ||
+      xs[0] != (int64_t)d->H * d->W * d->C || q.nm.kind != ES_NORM_BN || (q.ch.drop.enabled && !q.ch.keep))
+    return false;
+  t.nl.mean = q.nm.mean; t.nl.invstd = q.nm.invstd; t.nl.gamma = q.nm.gamma; t.nl.beta = q.nm.beta;
+  t.nl.keep = q.ch.keep;
+  t.nl.drop = q.ch.drop.enabled != 0;
+  t.nl.scale = t.nl.drop ? q.ch.drop.scale : 1.f;
+  t.nl.slope = q.ch.slope;
+  t.nl.dfirst = q.ch.dropout_first;
+  t.nl.act = q.ch.act;
+  q.used = 1;
+  return true;
+}
+
 // ------------------------------------------------------------------------------- entry points
 // Each returns 1 if it launched (caller checks the launch), 0 if the shape is not a thin conv.
 int es_thin_conv_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x, const int64_t xs[4], const void* wk,
@@ -677,6 +765,7 @@ int es_thin_conv_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x, cons
   const int rs = d->R * d->S, vn = dt == ES_BF16 ? 8 : 4;
   const bool c1 = c1_ok(d, rs) && ys[1] == 1 && aligned(ys, 8);
   const bool k1 = k1_ok(d, rs, vn) && xs[1] == 1 && xs[3] == d->C && aligned(xs, vn);
+  if (g_nol_req.on && !k1) return 0;   // normalise-on-load: the Cout = 1 kernels only
   if (!c1 && !k1 && small_ok(d, dt) && ydt == ES_F32 && xs[1] == 1 && aligned(xs, 4) && ys[1] == 1 &&
       aligned(ys, 4)) {
     Thin t{};
@@ -698,10 +787,12 @@ int es_thin_conv_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x, cons
   for (int i = 0; i < 4; ++i) { t.as[i] = xs[i]; t.os[i] = ys[i]; }
   t.M = d->N * d->P * d->Q;
   const int LP = k1 ? d->C / vn : 1;
+  const bool nol = take_nol(t, d, dt, xs, LP, k1);
+  if (g_nol_req.on && !nol) return 0;   // (the caller reports the request it could not honour)
   if (dt == ES_BF16) {
     if (ydt == ES_BF16) launch_fwd<bf16, bf16>(t, rs, LP, st); else launch_fwd<bf16, float>(t, rs, LP, st);
   } else {
-    if (ydt == ES_BF16) launch_fwd<float, bf16>(t, rs, LP, st); else launch_fwd<float, float>(t, rs, LP, st);
+    if (ydt == ES_BF16) launch_fwd<float, bf16>(t, rs, LP, st, nol); else launch_fwd<float, float>(t, rs, LP, st, nol);
   }
   return 1;
 }
@@ -766,7 +857,9 @@ int es_thin_conv_wgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, c
   t.M = d->N * d->P * d->Q;
   t.det = g_det_req.ws != nullptr && (float*)dw == g_det_req.ws;
   const int LP = k1 ? d->C / vn : 1;
+  const bool nol = take_nol(t, d, dt, xs, LP, k1);
+  if (g_nol_req.on && !nol) return 0;
   if (dt == ES_BF16) launch_wgrad<bf16>(t, rs, LP, st);
-  else launch_wgrad<float>(t, rs, LP, st);
+  else launch_wgrad<float>(t, rs, LP, st, nol);
   return 1;
 }

@@ -781,6 +781,17 @@ extern "C" int es_norm_stats_finalize(const float* part, int chunks, int C, floa
   return ES_OK;
 }
 
+// the dropout keep bits es_norm_act_fwd would store for x's shape (the forward of a norm whose
+// apply runs in the consuming conv: es_conv_norm_on_load)
+extern "C" int es_norm_keep_bits(const es_view_t* x, const es_chain_t* ch, es_stream_t stream) {
+  ES_CHECK_ARG(x && ch, "es_norm_keep_bits: null argument");
+  if (!ch->drop.enabled) return ES_OK;
+  ES_CHECK_ARG(ch->keep && x->c % 8 == 0, "es_norm_keep_bits: keep buffer and C %% 8 == 0 required");
+  es_fast_keep_bits(x, ch, (hipStream_t)stream);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
 extern "C" int es_norm_act_fwd(const es_view_t* x, es_dtype_t xdt, const es_norm_t* nm,
                                const es_chain_t* ch, const es_view_t* addend, es_dtype_t adt,
                                const void* addend_ptr, const void* xp, const es_view_t* y,

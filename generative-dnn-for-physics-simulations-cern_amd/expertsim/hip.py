@@ -105,6 +105,8 @@ _SIGS = {
     "es_conv_exec_flops": (C.c_int, [C.POINTER(C.c_double), C.c_int]),
     "es_conv_set_spb4": (C.c_int, [C.c_int]),
     "es_conv_set_ring_bnred": (C.c_int, [C.c_int]),
+    "es_conv_norm_on_load": (C.c_int, [P, P]),
+    "es_norm_keep_bits": (C.c_int, [P, P, P]),
     "es_pack_conv_weight": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, C.c_int, P]),
     "es_unpack_conv_grad": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, C.c_float, P]),
     "es_unpack_conv_grad_clear": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_float, P]),

@@ -20,11 +20,12 @@ from . import hip
 class Act:
     """Logical (N, C, H, W) tensor over a flat device buffer with explicit element strides."""
 
-    __slots__ = ("t", "dims", "strides", "bn_part", "bn_sums")
+    __slots__ = ("t", "dims", "strides", "bn_part", "bn_sums", "nol")
 
     def __init__(self, t: torch.Tensor, dims, strides):
         self.bn_part = None       # (partials, chunks) of fused BatchNorm statistics (ConvOp.fwd)
         self.bn_sums = None       # (partials, chunks, norm) of a fused BatchNorm-backward reduction (ConvOp.dgrad)
+        self.nol = None           # (norm struct, chain): t holds the PRE-norm h, the conv applies the norm on load
         self.t = t
         self.dims = tuple(int(d) for d in dims)
         self.strides = tuple(int(s) for s in strides)
@@ -273,6 +274,26 @@ class Upsample:
 
 
 # ------------------------------------------------------------------------------ conv / linear
+class _norm_on_load:
+    """Context of one conv call on an Act whose ``nol`` is set (NormOp.fwd_deferred): the C library
+    applies that BatchNorm + dropout + activation to the operand as it loads it
+    (es_conv_norm_on_load; the conv call fails if its path cannot)."""
+
+    def __init__(self, x):
+        self.nol = getattr(x, "nol", None)
+
+    def __enter__(self):
+        if self.nol is not None:
+            nm, chain = self.nol
+            hip.call("es_conv_norm_on_load", C.byref(nm), C.byref(chain))
+        return self
+
+    def __exit__(self, *exc):
+        if self.nol is not None:
+            hip.call("es_conv_norm_on_load", None, None)
+        return False
+
+
 class ConvOp:
     """nn.Conv2d / nn.Linear on the implicit-GEMM kernels.
 
@@ -404,7 +425,7 @@ class ConvOp:
         if out is None:
             out = Act.nhwc(d.N, d.K, d.P, d.Q, out_dtype or cdt, x.t.device)
         bias = self.bias if (with_bias and self.bias is not None) else None
-        with _probed(self.label and self.label + ".fwd"):
+        with _probed(self.label and self.label + ".fwd"), _norm_on_load(x):
             if planes is not None:
                 assert d.subpixel == 1 and cdt == torch.float32, "planes: fp32 sub-pixel convs only"
                 part, floats, chunks = None, 0, C.c_int(0)
@@ -542,7 +563,7 @@ class ConvOp:
             ys, xs = hip.strides4(dy.strides), hip.strides4(x.strides)
             nb = int(hip.lib().es_conv2d_wgrad_det_ws_bytes(C.byref(d), dy.dt, ys, xs))
             wsb = ws(nb, dev)
-            with _probed(self.label and self.label + ".wgrad"):
+            with _probed(self.label and self.label + ".wgrad"), _norm_on_load(x):
                 hip.call("es_conv2d_wgrad_det", C.byref(d), dy.dt, dy.ptr, ys, x.ptr, xs, hip.ptr(dw_out),
                          float(beta), hip.ptr(wsb), nb, hip.stream_ptr())
             if db_out is not None:
@@ -563,7 +584,7 @@ class ConvOp:
                 dwk = self._dwk = torch.zeros(self.weight.numel(), dtype=torch.float32, device=dev)
         else:
             dwk = torch.zeros(self.weight.numel(), dtype=torch.float32, device=dev)
-        with _probed(self.label and self.label + ".wgrad"):
+        with _probed(self.label and self.label + ".wgrad"), _norm_on_load(x):
           hip.call("es_conv2d_wgrad", C.byref(d), dy.dt, dy.ptr, hip.strides4(dy.strides), x.ptr,
                  hip.strides4(x.strides), hip.ptr(dwk), hip.stream_ptr())
         if dw_out is not None and legacy:
@@ -731,6 +752,18 @@ class NormOp:
                  C.byref(addend.view) if addend is not None else None,
                  addend.dt if addend is not None else 0, addend.ptr if addend is not None else None,
                  x.ptr, C.byref(y.view), y.dt, y.ptr, hip.stream_ptr())
+        return y, (mean, invstd)
+
+    def fwd_deferred(self, x: Act, chain: hip.Chain, train=True):
+        """The forward of a BatchNorm whose apply runs in the consuming conv (es_conv_norm_on_load):
+        statistics and the dropout keep bits only.  Returns (a view of x carrying ``nol``, stats); a
+        conv given that view normalises on load, so y is never written."""
+        assert self.kind == hip.NORM_BN
+        mean, invstd = self.stats(x, train)
+        nm = self.norm_struct(mean, invstd)
+        hip.call("es_norm_keep_bits", C.byref(x.view), C.byref(chain), hip.stream_ptr())
+        y = Act(x.t, x.dims, x.strides)
+        y.nol = (nm, chain)
         return y, (mean, invstd)
 
     def bwd(self, x: Act, stats, chain: hip.Chain, dy: Act, dx_dtype=None, act_ref: Act = None,

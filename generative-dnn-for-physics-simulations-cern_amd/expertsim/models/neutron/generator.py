@@ -28,6 +28,10 @@ from ...utils import philox
 from ..base import ExpertModule, build_tree, get_module
 
 _RING_BNRED = os.environ.get("ES_RING_BNRED", "0") == "1"     # A/B switch
+# fp32, opt-in (ES_NOL=1): conv_layers.10's BatchNorm + Dropout + LeakyReLU applied by conv_layers.13's
+# thin kernels as they load it (NormOp.fwd_deferred, es_conv_norm_on_load), y5 never written.  Measured
+# slower than the apply pass it removes (45.5-45.8 vs 44.9-45.1 ms/step)
+_NOL = os.environ.get("ES_NOL", "0") == "1"
 
 SLOPE = 0.1
 P_DROP = 0.2
@@ -119,7 +123,10 @@ class GeneratorNeutron(ExpertModule):
         h4 = o["c5"].fwd(y3, bn_stats=train)
         y4, s4 = o["bn4"].fwd(h4, ch[3], train=train)
         h5 = o["c9"].fwd(y4, bn_stats=train)
-        y5, s5 = o["bn5"].fwd(h5, ch[4], train=train)
+        if _NOL and cdt == torch.float32:
+            y5, s5 = o["bn5"].fwd_deferred(h5, ch[4], train=train)
+        else:
+            y5, s5 = o["bn5"].fwd(h5, ch[4], train=train)
         h6 = o["c13"].fwd(y5, out_dtype=torch.float32)
         img = act_fwd(h6, hip.chain_struct(hip.ACT_RELU))
         ctx = dict(x0=x0, h1=h1, y1=y1, s1=s1, h2=h2, y2=y2, s2=s2, y2n=y2n, h3=h3, y3=y3, s3=s3,

@@ -291,6 +291,17 @@ int es_norm_stats_finalize(const float* part, int chunks, int C, float eps, floa
 int es_norm_act_fwd(const es_view_t* x, es_dtype_t xdt, const es_norm_t* nm, const es_chain_t* ch,
                     const es_view_t* addend, es_dtype_t adt, const void* addend_ptr, const void* xp,
                     const es_view_t* y, es_dtype_t ydt, void* yp, es_stream_t stream);
+/* The dropout keep bits es_norm_act_fwd would write into ch->keep for x's shape, without the apply
+ * (no-op without dropout).  For a BatchNorm whose apply runs in the consuming conv
+ * (es_conv_norm_on_load); same Philox draws as neutron/generator.py:33-37's nn.Dropout there. */
+int es_norm_keep_bits(const es_view_t* x, const es_chain_t* ch, es_stream_t stream);
+/* Normalise-on-load for the following conv calls on this thread (nm == NULL clears): the activation
+ * operand x handed to es_conv2d_fwd / es_conv2d_wgrad(_det) is the PRE-norm tensor h, and the conv
+ * applies y = chain(BatchNorm(h)) (statistics nm, dropout keep bits / activation ch) as it loads it;
+ * y is never stored.  Honoured by the thin Cout = 1 fp32 fwd / wgrad (the neutron generator's
+ * conv_layers.13 on BatchNorm conv_layers.10 + Dropout + LeakyReLU, neutron/generator.py:33-38);
+ * every other conv path returns ES_ERR_ARG while it is set. */
+int es_conv_norm_on_load(const es_norm_t* nm, const es_chain_t* ch);
 /* Backward of es_norm_act_fwd.  dy: gradient of y.  act_ref (optional): evaluate the activation
  * derivative on this stored tensor (the block output) instead of the recomputed pre-activation.
  * Writes dx (beta=1 accumulates), accumulates dgamma/dbeta (fp32, may be NULL) and, when dsum is
