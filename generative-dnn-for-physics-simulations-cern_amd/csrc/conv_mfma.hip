@@ -69,6 +69,17 @@ constexpr uint32_t OOB = 0x80000000u;
 #ifndef ES_SPB_PFD
 #define ES_SPB_PFD 2   // split-fp32 SPB loop: column tiles of B planes read ahead of their MFMAs
 #endif
+#ifndef ES_SPB_DMA_HI
+// SPB loop: column tile at which waves 4-7 issue their step's DMA (capped at RN - 1; waves 0-3 issue
+// after column tile 0).  The two waves of a SIMD (w, w + 4) otherwise stall on their 7 LDS-DMA issues
+// at the same point, leaving the SIMD's matrix pipe idle.  Measured (tools/gpu_libab.sh, alternating,
+// B = 1024, ms/step): base 44.8-45.3; tile 2 45.34, 4 44.54, 5 44.60 / 44.60, 6 44.19 / 44.12,
+// 7 44.05 / 44.50 (conv_layers.5 FWD / DGRAD 3.15 / 3.05 -> 2.95 / 2.85 ms at 6)
+#define ES_SPB_DMA_HI 6
+#endif
+#ifndef ES_SPB_SPLIT_HI
+#define ES_SPB_SPLIT_HI -1     // SPB loop: column tile after which waves 4-7 split A(t+1) (-1: as waves 0-3)
+#endif
 #ifndef ES_SPB_FRESH
 // SPB loop (8-wave split-fp32 FWD / DGRAD): K-steps per fresh accumulator.  Measured (tools/gpu_r04w.sh,
 // alternating on one box, B = 1024): 1 -> 2 conv_layers.5 FWD 3.06-3.13 -> 2.94, DGRAD 2.99-3.03 ->
@@ -1078,11 +1089,13 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
           else if constexpr (PH == 3) cst[i % CR][j % CN] = mfma_chain6(apc[i], bq[j % (PFD + 1)], cst[i % CR][j % CN]);
           else acc[i][j] = acc[i][j] + mfma_chain6(apc[i], bq[j % (PFD + 1)], cst[i % CR][j % CN]);
         }
-        if (j == 0) {   // the step's DMA, once its first MFMAs are queued
+        // the step's DMA, once its first MFMAs are queued (STAGGER: the two waves of a SIMD, w and
+        // w + 4, at different column tiles, so one issues MFMAs while the other stalls on the issue)
+        if (j == (wid >= 4 ? (ES_SPB_DMA_HI < RN ? ES_SPB_DMA_HI : RN - 1) : 0)) {
           issue_b(bring + ib * BBYTES);
           issue(aring + ia * ABYTES);
         }
-        if (j == JS) {
+        if (j == (ES_SPB_SPLIT_HI >= 0 && ES_SPB_SPLIT_HI < RN && wid >= 4 ? ES_SPB_SPLIT_HI : JS)) {
 #pragma unroll
           for (int i = 0; i < RM; ++i) split8(ra[i][0], ra[i][1], apn[i]);
         }

@@ -9,7 +9,7 @@ run() {
   python3 -c "import json; d=json.load(open('$O/libab.json')); r=d['roofline']; print('$1', d['ms_per_step'], {k: v['avg_ms'] for k, v in r['all_probed'].items()})" >> $O/libab.log
 }
 base=$1; shift
-for i in 1 2; do
+for i in $(seq 1 ${REPS:-2}); do
   for v in "$@"; do
     run $base || exit $?
     run $v || exit $?
