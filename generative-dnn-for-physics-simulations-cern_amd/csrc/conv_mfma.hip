@@ -57,6 +57,9 @@ constexpr uint32_t OOB = 0x80000000u;
 #ifndef ES_COOP2
 #define ES_COOP2 0   // wgrad_coop_kernel: two register stages of loads (experiment)
 #endif
+#ifndef ES_COOP_STAG
+#define ES_COOP_STAG 0   // wgrad_coop_kernel: row tile after which waves 4-7 split the next step (0: after all)
+#endif
 #ifndef ES_SPB4_EXP
 #define ES_SPB4_EXP 0
 #endif
@@ -3166,20 +3169,29 @@ __global__ void __launch_bounds__(RT) wgrad_coop_kernel(ConvArgs a, float* __res
         *(uint2*)(pb + 2 * PLANE + wofs[h]) = uint2{l0, l1};
       }
     };
-    auto compute = [&](const char* pb) {
+    auto load_b = [&](const char* pb, bf16x8 (&bp)[RN][3]) {
       const char* q = pb + lane * 16;
-      bf16x8 ap[3], bp[RN][3];
 #pragma unroll
       for (int jn = 0; jn < RN; ++jn)
 #pragma unroll
         for (int p = 0; p < 3; ++p) bp[jn][p] = *(const bf16x8*)(q + p * PLANE + (NBA + wn0 / 16 + jn) * 1024);
+    };
+    auto rows = [&](const char* pb, const bf16x8 (&bp)[RN][3], int i0, int i1) {   // rows [i0, i1) of the tile
+      const char* q = pb + lane * 16;
+      bf16x8 ap[3];
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
+        if (i < i0 || i >= i1) continue;
 #pragma unroll
         for (int p = 0; p < 3; ++p) ap[p] = *(const bf16x8*)(q + p * PLANE + (wm0 / 16 + i) * 1024);
 #pragma unroll
         for (int jn = 0; jn < RN; ++jn) acc[i][jn] = mfma_split6(ap, bp[jn], acc[i][jn]);
       }
+    };
+    auto compute = [&](const char* pb) {
+      bf16x8 bp[RN][3];
+      load_b(pb, bp);
+      rows(pb, bp, 0, RM);
     };
     auto sync = [] {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -3219,8 +3231,27 @@ __global__ void __launch_bounds__(RT) wgrad_coop_kernel(ConvArgs a, float* __res
       char* nxt = smem + ((t & 1) ^ 1) * PBUF;
       load(s0);                 // step t + 1
       asm volatile("" ::: "memory");
-      compute(cur);             // step t
-      store(s0, nxt);           // step t + 1 (its buffer was last read in step t - 1)
+      if (ES_COOP_STAG > 0 && ES_COOP_STAG < RM && wid >= 4) {
+        // waves 4-7 split step t + 1 between their row tiles ES_COOP_STAG - 1 and ES_COOP_STAG, under
+        // the MFMAs of their SIMD partner (wave w - 4), which splits after all its rows
+        bf16x8 bp[RN][3];
+        load_b(cur, bp);
+        rows(cur, bp, 0, ES_COOP_STAG);
+        // (opaque here and fenced: hipcc otherwise speculates the split above the branch or schedules
+        // it into the first MFMAs, and its vmcnt wait with it)
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int h = 0; h < NH; ++h)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) asm volatile("" : "+v"(s0[h][jj]));
+        store(s0, nxt);
+        __builtin_amdgcn_sched_barrier(0);
+        rows(cur, bp, ES_COOP_STAG, RM);
+      } else {
+        compute(cur);           // step t
+        if (ES_COOP_STAG > 0) __builtin_amdgcn_sched_barrier(0);
+        store(s0, nxt);         // step t + 1 (its buffer was last read in step t - 1)
+      }
       sync();
     }
 #endif
