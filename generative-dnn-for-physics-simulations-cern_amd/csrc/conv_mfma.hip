@@ -80,6 +80,9 @@ constexpr uint32_t OOB = 0x80000000u;
 // 7 44.05 / 44.50 (conv_layers.5 FWD / DGRAD 3.15 / 3.05 -> 2.95 / 2.85 ms at 6)
 #define ES_SPB_DMA_HI 6
 #endif
+#ifndef ES_SPB_DMA_LO
+#define ES_SPB_DMA_LO 0        // SPB loop: column tile at which waves 0-3 issue their step's DMA
+#endif
 #ifndef ES_SPB_SPLIT_HI
 #define ES_SPB_SPLIT_HI -1     // SPB loop: column tile after which waves 4-7 split A(t+1) (-1: as waves 0-3)
 #endif
@@ -1094,7 +1097,7 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
         }
         // the step's DMA, once its first MFMAs are queued (STAGGER: the two waves of a SIMD, w and
         // w + 4, at different column tiles, so one issues MFMAs while the other stalls on the issue)
-        if (j == (wid >= 4 ? (ES_SPB_DMA_HI < RN ? ES_SPB_DMA_HI : RN - 1) : 0)) {
+        if (j == (wid >= 4 ? (ES_SPB_DMA_HI < RN ? ES_SPB_DMA_HI : RN - 1) : (ES_SPB_DMA_LO < RN ? ES_SPB_DMA_LO : RN - 1))) {
           issue_b(bring + ib * BBYTES);
           issue(aring + ia * ABYTES);
         }
