@@ -80,6 +80,9 @@ constexpr uint32_t OOB = 0x80000000u;
 // 7 44.05 / 44.50 (conv_layers.5 FWD / DGRAD 3.15 / 3.05 -> 2.95 / 2.85 ms at 6)
 #define ES_SPB_DMA_HI 6
 #endif
+#ifndef ES_RING_STAG
+#define ES_RING_STAG 0         // ring_loop (bf16 kernels): waves 4-7 issue their step's DMA after their MFMAs
+#endif
 #ifndef ES_SPB_DMA_LO
 #define ES_SPB_DMA_LO 0        // SPB loop: column tile at which waves 0-3 issue their step's DMA
 #endif
@@ -280,8 +283,11 @@ __device__ __forceinline__ void ring_loop(int nk, char* smem, int slot_bytes, Is
     if constexpr (NLDS > 0) fence(f1);
     ring_barrier();
     load(f0, smem + nxt * slot_bytes, 0);
-    issue(smem + cur * slot_bytes);                      // step t + NS
+    // (ES_RING_STAG: waves 4-7 issue after their MFMAs, under those of their SIMD partner w - 4)
+    const bool late = ES_RING_STAG && __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4;
+    if (!late) issue(smem + cur * slot_bytes);           // step t + NS
     mma(f1);
+    if (late) issue(smem + cur * slot_bytes);
     cur = nxt;
   }
   load(f1, smem + cur * slot_bytes, 1);
