@@ -77,16 +77,8 @@ struct ConvArgs {
                                 // (es_conv2d_*_det): into det_ws + z * M * Ng
   float* det_ws;
   int prio;                     // split-fp32 ring kernels: waves 4-7 at s_setprio 1 (VALU arbitration)
-  int a_planes;                 // fp32 FWD / DGRAD: a_src is an es_split_planes image (6 B per value)
 };
 
-// es_conv2d_*_planes: the caller's operand is a planes image (host, per thread); the 4-wave launch
-// sets used when it ran the planes kernel (any other path must not read the planes as fp32)
-struct PlanesRequest {
-  int on;
-  int used;
-};
-extern thread_local PlanesRequest g_planes_req;
 
 // es_conv2d_wgrad_det: the partial buffer offered to the generic (register-staged / thin) WGRAD
 // kernels (host, per thread); the launch sets splits = partial slots written
@@ -109,15 +101,6 @@ struct BnRedRequest {
 };
 extern thread_local BnRedRequest g_bnr_req;
 
-// Normalise-on-load (es_conv_norm_on_load): the conv's activation operand x is the PRE-norm h of a
-// BatchNorm + dropout + activation chain, applied per element as it is loaded (the thin Cout = 1
-// fwd / wgrad, fp32).  on: set by the host call; used: set by the kernel path that honoured it.
-struct NolRequest {
-  int on, used;
-  es_norm_t nm;
-  es_chain_t ch;
-};
-extern thread_local NolRequest g_nol_req;
 
 
 // es_conv2d_fwd_stats: the caller's request for fused BatchNorm partials (host, per thread); the

@@ -39,14 +39,8 @@ int es_thin_conv_wgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, c
 namespace {
 
 
-// ES_NO_GLDS=1 (or es_conv_set_glds(0)) forces the register-staged kernels (A/B measurement)
-bool g_no_glds = [] { const char* e = getenv("ES_NO_GLDS"); return e && e[0] == '1'; }();
-// ES_NARROW_TILES=0 restores 64 x 64 tiles for the narrow fp32 GEMMs (A/B switch)
-bool g_narrow_tiles = [] { const char* e = getenv("ES_NARROW_TILES"); return !(e && e[0] == '0'); }();
-// ES_NO_F32_RING=1 keeps the fp32 (parity-mode) convs on the register-staged kernels (A/B)
-bool g_no_f32_ring = [] { const char* e = getenv("ES_NO_F32_RING"); return e && e[0] == '1'; }();
-// cap on the K splits of a narrow fp32 WGRAD (every split atomically adds the same M x N outputs)
-int g_narrow_wgrad_splits = [] { const char* e = getenv("ES_NARROW_WGRAD_SPLITS"); return e ? atoi(e) : 0; }();
+// es_conv_set_glds(0) forces the register-staged kernels (tests compare the paths)
+bool g_no_glds = false;
 
 constexpr int KSTEP_BYTES = 128;               // operand bytes per row per K-step
 constexpr int ROW_BYTES = KSTEP_BYTES + 16;    // padded LDS row
@@ -890,7 +884,7 @@ int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
     // for real convolutions whose K-steps are one tap x 32 channels
     const int nch = MODE == MODE_FWD ? a.d.C : a.d.K;
     if (avec && bvec && nch % 32 == 0 && a.Kd % 32 == 0 && a.d.stride <= 2 && a.d.hmap == nullptr &&
-        a.d.P * a.d.Q >= 16 && a.M >= 128 && !g_no_glds && !g_no_f32_ring) {
+        a.d.P * a.d.Q >= 16 && a.M >= 128 && !g_no_glds) {
       a.k_per_split = a.Kd;
       a.splitk = 0;
       const int rc = es_conv_ring_launch_f32(a, MODE, st);
@@ -913,8 +907,8 @@ int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
   // narrow fp32 GEMMs (the discriminator's 32->16 conv: FWD / DGRAD with N <= 32, WGRAD with
   // M = 16 output channels): a 64 x 64 tile wastes half or 3/4 of every MFMA; 128 x 32 and
   // 32 x 128 tiles keep the 2 x 2 wave grid with one 16-row (column) fragment per wave
-  const bool narrow_n = sizeof(T) == 4 && g_narrow_tiles && MODE != MODE_WGRAD && a.Ng <= 32 && !splitk_case;
-  const bool narrow_m = sizeof(T) == 4 && g_narrow_tiles && MODE == MODE_WGRAD && a.M <= 32 && !big;
+  const bool narrow_n = sizeof(T) == 4 && MODE != MODE_WGRAD && a.Ng <= 32 && !splitk_case;
+  const bool narrow_m = sizeof(T) == 4 && MODE == MODE_WGRAD && a.M <= 32 && !big;
   const int BM = big ? 128 : (narrow_n ? 128 : (narrow_m ? 32 : 64));
   const int BN = big ? 128 : (narrow_n ? 32 : (narrow_m ? 128 : 64));
   if constexpr (sizeof(T) == 2 && MODE == MODE_WGRAD) {
@@ -944,7 +938,6 @@ int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
   a.splitk = 0;
   if (MODE == MODE_WGRAD) {
     int want = (2048 + tiles - 1) / tiles;            // ~2048 workgroups
-    if (narrow_m && g_narrow_wgrad_splits > 0) want = min(want, g_narrow_wgrad_splits);
     want = max(1, min(want, ksteps / 4 > 0 ? ksteps / 4 : 1));  // >= 4 K-steps per split
     if (a.det) {   // deterministic: one partial slot per split, within the caller's workspace
       const int64_t slot = (int64_t)a.M * a.Ng;
@@ -1039,17 +1032,23 @@ int ring_direct(ConvArgs& a, int mode, hipStream_t st, es_dtype_t dt) {
 
 // ---------------------------------------------------------------- executed-work tally (es_conv_exec_flops)
 thread_local int g_ring_hit = 0;
-thread_local PlanesRequest g_planes_req{0, 0};
 namespace {
-double g_exec_flops[3] = {0.0, 0.0, 0.0};
-// RAII around one conv entry: classifies the path the call took and adds its executed FLOPs
+// per host thread (the probe reads the thread that issued the convs)
+thread_local double g_exec_flops[3] = {0.0, 0.0, 0.0};
+// RAII around one conv entry: classifies the path the call took and adds its executed FLOPs, only
+// when the entry returns ES_OK (ok() marks it: failed calls issue no work)
 struct ExecTally {
   const es_conv_desc_t* d;
   es_dtype_t dt;
   bool thin = false;
+  bool done = false;
   ExecTally(const es_conv_desc_t* d_, es_dtype_t dt_) : d(d_), dt(dt_) { g_ring_hit = 0; }
+  int ok(int rc) {
+    done = rc == ES_OK;
+    return rc;
+  }
   ~ExecTally() {
-    if (!d) return;
+    if (!d || !done) return;
     double f = 2.0 * d->N * d->P * d->Q * (double)d->K * d->C * d->R * d->S;
     if (g_ring_hit & 4) f *= (double)es_subpixel_taps(d->R, d->S) / (4.0 * d->R * d->S);
     if (thin) g_exec_flops[2] += f;
@@ -1081,23 +1080,6 @@ extern "C" int es_conv_set_glds(int on) {
   return old;
 }
 
-thread_local NolRequest g_nol_req;
-
-// normalise-on-load for the next conv entry call(s) on this thread (nm == NULL clears); only the thin
-// Cout = 1 fp32 fwd / wgrad honour it, every other path fails with ES_ERR_ARG while it is set
-extern "C" int es_conv_norm_on_load(const es_norm_t* nm, const es_chain_t* ch) {
-  if (!nm) {
-    g_nol_req = NolRequest{};
-    return ES_OK;
-  }
-  ES_CHECK_ARG(ch && nm->mean && nm->invstd, "es_conv_norm_on_load: statistics / chain missing");
-  g_nol_req.on = 1;
-  g_nol_req.used = 0;
-  g_nol_req.nm = *nm;
-  g_nol_req.ch = *ch;
-  return ES_OK;
-}
-
 extern "C" int es_conv2d_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x,
                              const int64_t xs[4], const void* wk, const float* bias, void* y,
                              es_dtype_t ydt, const int64_t ys[4], es_stream_t stream) {
@@ -1107,12 +1089,10 @@ extern "C" int es_conv2d_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void*
   if (es_thin_conv_fwd(d, dt, x, xs, wk, bias, y, ydt, ys, (hipStream_t)stream)) {
     tally.thin = true;
     ES_CHECK_LAUNCH();
-    return ES_OK;
+    return tally.ok(ES_OK);
   }
-  ES_CHECK_ARG(!g_nol_req.on, "conv fwd: normalise-on-load requested for a conv off the thin fp32 path");
   ConvArgs a{};
   a.d = *d; a.a_src = x; a.b_src = wk; a.out = y; a.bias = bias; a.beta = 0.f;
-  a.a_planes = g_planes_req.on;
   a.out_bf16 = ydt == ES_BF16;
   for (int i = 0; i < 4; ++i) { a.as[i] = xs[i]; a.os[i] = ys[i]; }
   a.M = d->N * d->P * d->Q; a.Ng = d->K; a.Kd = d->R * d->S * d->C;
@@ -1120,8 +1100,8 @@ extern "C" int es_conv2d_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void*
   const int vn = dt == ES_BF16 ? 8 : 4;
   const bool avec = xs[1] == 1 && d->C % vn == 0;
   const bool bvec = a.Kd % vn == 0;
-  if (d->subpixel) return ring_direct(a, MODE_FWD, (hipStream_t)stream, dt);
-  return dispatch<MODE_FWD>(a, dt, avec, bvec, (hipStream_t)stream);
+  if (d->subpixel) return tally.ok(ring_direct(a, MODE_FWD, (hipStream_t)stream, dt));
+  return tally.ok(dispatch<MODE_FWD>(a, dt, avec, bvec, (hipStream_t)stream));
 }
 
 extern "C" int es_conv2d_fwd_stats(const es_conv_desc_t* d, es_dtype_t dt, const void* x, const int64_t xs[4],
@@ -1144,11 +1124,10 @@ extern "C" int es_conv2d_dgrad(const es_conv_desc_t* d, es_dtype_t dt, const voi
   if (es_thin_conv_dgrad(d, dt, dy, ys, wd, dxu, dxdt, dxs, beta, (hipStream_t)stream)) {
     tally.thin = true;
     ES_CHECK_LAUNCH();
-    return ES_OK;
+    return tally.ok(ES_OK);
   }
   ConvArgs a{};
   a.d = *d; a.a_src = dy; a.b_src = wd; a.out = dxu; a.bias = nullptr; a.beta = beta;
-  a.a_planes = g_planes_req.on;
   a.out_bf16 = dxdt == ES_BF16;
   for (int i = 0; i < 4; ++i) { a.as[i] = ys[i]; a.os[i] = dxs[i]; }
   a.fold = d->up_h > 0;
@@ -1162,8 +1141,8 @@ extern "C" int es_conv2d_dgrad(const es_conv_desc_t* d, es_dtype_t dt, const voi
   const int vn = dt == ES_BF16 ? 8 : 4;
   const bool avec = ys[1] == 1 && d->K % vn == 0;
   const bool bvec = a.Kd % vn == 0;
-  if (d->subpixel) return ring_direct(a, MODE_DGRAD, (hipStream_t)stream, dt);
-  return dispatch<MODE_DGRAD>(a, dt, avec, bvec, (hipStream_t)stream);
+  if (d->subpixel) return tally.ok(ring_direct(a, MODE_DGRAD, (hipStream_t)stream, dt));
+  return tally.ok(dispatch<MODE_DGRAD>(a, dt, avec, bvec, (hipStream_t)stream));
 }
 
 extern "C" int es_conv2d_dgrad_bnred(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, const int64_t ys[4],
@@ -1178,45 +1157,6 @@ extern "C" int es_conv2d_dgrad_bnred(const es_conv_desc_t* d, es_dtype_t dt, con
   return rc;
 }
 
-// FWD / DGRAD whose gathered operand is an es_split_planes image (fp32 parity mode, split-fp32
-// arithmetic, the sub-pixel convs of the 4-wave kernel); error when the conv takes another path
-namespace {
-int planes_call(int (*fn)(void*), void* ctx) {
-  g_planes_req = PlanesRequest{1, 0};
-  const int rc = fn(ctx);
-  const int used = g_planes_req.used;
-  g_planes_req = PlanesRequest{0, 0};
-  if (rc != ES_OK) return rc;
-  ES_CHECK_ARG(used, "conv planes: the conv did not run the planes kernel (sub-pixel split-fp32 4-wave path only)");
-  return ES_OK;
-}
-}  // namespace
-
-extern "C" int es_conv2d_fwd_planes(const es_conv_desc_t* d, const void* xp, const int64_t xs[4], const void* wk,
-                                    const float* bias, void* y, es_dtype_t ydt, const int64_t ys[4], float* part,
-                                    int64_t part_floats, int* chunks, es_stream_t stream) {
-  ES_CHECK_ARG(d && d->subpixel, "conv fwd planes: sub-pixel convs only");
-  struct C_ { const es_conv_desc_t* d; const void* x; const int64_t* xs; const void* wk; const float* bias; void* y;
-              es_dtype_t ydt; const int64_t* ys; float* part; int64_t pf; int* chunks; es_stream_t st; } c{d, xp, xs, wk,
-              bias, y, ydt, ys, part, part_floats, chunks, stream};
-  return planes_call([](void* p) {
-    C_& c = *(C_*)p;
-    if (c.part) return es_conv2d_fwd_stats(c.d, ES_F32, c.x, c.xs, c.wk, c.bias, c.y, c.ydt, c.ys, c.part, c.pf, c.chunks, c.st);
-    return es_conv2d_fwd(c.d, ES_F32, c.x, c.xs, c.wk, c.bias, c.y, c.ydt, c.ys, c.st);
-  }, &c);
-}
-
-extern "C" int es_conv2d_dgrad_planes(const es_conv_desc_t* d, const void* dyp, const int64_t ys[4], const void* wd,
-                                      void* dx, es_dtype_t dxdt, const int64_t dxs[4], es_stream_t stream) {
-  ES_CHECK_ARG(d && d->subpixel, "conv dgrad planes: sub-pixel convs only");
-  struct C_ { const es_conv_desc_t* d; const void* dy; const int64_t* ys; const void* wd; void* dx; es_dtype_t dxdt;
-              const int64_t* dxs; es_stream_t st; } c{d, dyp, ys, wd, dx, dxdt, dxs, stream};
-  return planes_call([](void* p) {
-    C_& c = *(C_*)p;
-    return es_conv2d_dgrad(c.d, ES_F32, c.dy, c.ys, c.wd, c.dx, c.dxdt, c.dxs, 0.f, c.st);
-  }, &c);
-}
-
 extern "C" int es_conv2d_wgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy,
                                const int64_t ys[4], const void* x, const int64_t xs[4], float* dw,
                                es_stream_t stream) {
@@ -1225,9 +1165,8 @@ extern "C" int es_conv2d_wgrad(const es_conv_desc_t* d, es_dtype_t dt, const voi
   if (es_thin_conv_wgrad(d, dt, dy, ys, x, xs, dw, (hipStream_t)stream)) {
     tally.thin = true;
     ES_CHECK_LAUNCH();
-    return ES_OK;
+    return tally.ok(ES_OK);
   }
-  ES_CHECK_ARG(!g_nol_req.on, "conv wgrad: normalise-on-load requested for a conv off the thin fp32 path");
   ConvArgs a{};
   a.d = *d; a.a_src = dy; a.b_src = x; a.out = dw;
   for (int i = 0; i < 4; ++i) { a.as[i] = ys[i]; a.bs[i] = xs[i]; }
@@ -1235,7 +1174,7 @@ extern "C" int es_conv2d_wgrad(const es_conv_desc_t* d, es_dtype_t dt, const voi
   const int vn = dt == ES_BF16 ? 8 : 4;
   const bool avec = ys[1] == 1 && d->K % vn == 0;
   const bool bvec = xs[1] == 1 && d->C % vn == 0;
-  return dispatch<MODE_WGRAD>(a, dt, avec, bvec, (hipStream_t)stream);
+  return tally.ok(dispatch<MODE_WGRAD>(a, dt, avec, bvec, (hipStream_t)stream));
 }
 
 // ------------------------------------------------------------------------- deterministic WGRAD
@@ -1272,12 +1211,12 @@ extern "C" int es_conv2d_wgrad_det(const es_conv_desc_t* d, es_dtype_t dt, const
   ExecTally tally(d, dt);
   const hipStream_t st = (hipStream_t)stream;
   const int64_t floats = ws_bytes / (int64_t)sizeof(float);
-  if (dt == ES_F32 && !g_nol_req.on) {
+  if (dt == ES_F32) {
     const int rc = es_wgrad_f32_ring(*d, dy, ys, x, xs, dw, beta, (float*)ws, floats, st);
     if (rc < 0) return ES_ERR_ARG;
     if (rc > 0) {
       ES_CHECK_LAUNCH();
-      return ES_OK;
+      return tally.ok(ES_OK);
     }
   }
   const int64_t per = (int64_t)d->K * d->R * d->S * d->C;
@@ -1285,10 +1224,6 @@ extern "C" int es_conv2d_wgrad_det(const es_conv_desc_t* d, es_dtype_t dt, const
   g_det_req = DetRequest{(float*)ws, floats, 0};
   int rc = es_thin_conv_wgrad(d, dt, dy, ys, x, xs, (float*)ws, st) ? ES_OK : -1;
   tally.thin = rc == ES_OK;
-  if (rc != ES_OK && g_nol_req.on) {
-    g_det_req = DetRequest{nullptr, 0, 0};
-    ES_CHECK_ARG(false, "conv wgrad det: normalise-on-load requested for a conv off the thin fp32 path");
-  }
   if (rc != ES_OK) {
     ConvArgs a{};
     a.d = *d; a.a_src = dy; a.b_src = x; a.out = ws;
@@ -1306,7 +1241,7 @@ extern "C" int es_conv2d_wgrad_det(const es_conv_desc_t* d, es_dtype_t dt, const
   ES_CHECK_ARG(splits > 0, "conv wgrad det: no partials written");
   es_wgrad_reduce_plain((const float*)ws, splits, d->K, d->C, d->R, d->S, dw, beta, st);
   ES_CHECK_LAUNCH();
-  return ES_OK;
+  return tally.ok(ES_OK);
 }
 
 // deterministic split-K FWD / DGRAD (the fp32 linears with few output tiles and a long K: the
@@ -1545,50 +1480,6 @@ __global__ void pack_planes_kernel(const float* __restrict__ w, int64_t nblk, bf
     o[32] = m;
     o[64] = l;
   }
-}
-
-// fp32 activations [rows][C] -> split-fp32 planes [rows][C / 32][3][32] bf16 (es_split_planes): the
-// weight planes' layout (pack_planes_kernel) per 32-channel block.  A thread owns 8 channels c0..c0+7
-// (c0 % 8 == 0) of one row: channels cc = c0 % 32 + e land in slots 8 u + j of the block (u = cc % 16
-// / 4, j = cc / 16 * 4 + cc % 4), i.e. two runs of 4 slots per plane (8-byte stores).
-__global__ void split_planes_kernel(const float* __restrict__ x, int64_t rows, int C, bf16* __restrict__ out) {
-  const int cv = C >> 3;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < rows * cv; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = i / cv;
-    const int c0 = (int)(i - r * cv) * 8;
-    const f32x4 v0 = *(const f32x4*)(x + r * C + c0);
-    const f32x4 v1 = *(const f32x4*)(x + r * C + c0 + 4);
-    const int cc = c0 & 31, u0 = (cc & 15) >> 2, jh = (cc >> 4) * 4;
-    bf16* blk = out + (r * (C >> 5) + (c0 >> 5)) * 96;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {   // channels c0 + 4h .. +3 -> slots 8 (u0 + h) + jh .. +3
-      const f32x4 v = h ? v1 : v0;
-      bf16x4 ph, pm, pl;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const bf16 hi = (bf16)v[e];
-        const float rr = v[e] - (float)hi;
-        const bf16 mi = (bf16)rr;
-        ph[e] = hi;
-        pm[e] = mi;
-        pl[e] = (bf16)(rr - (float)mi);
-      }
-      bf16* o = blk + 8 * (u0 + h) + jh;
-      *(bf16x4*)o = ph;
-      *(bf16x4*)(o + 32) = pm;
-      *(bf16x4*)(o + 64) = pl;
-    }
-  }
-}
-
-extern "C" int es_split_planes(const float* x, int64_t rows, int C, void* planes, es_stream_t stream) {
-  ES_CHECK_ARG(x && planes && rows >= 0 && C > 0 && C % 32 == 0, "split planes: C %% 32 == 0 required");
-  const int64_t n = rows * (C / 8);
-  if (n == 0) return ES_OK;
-  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 16384);
-  hipLaunchKernelGGL(split_planes_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, rows, C, (bf16*)planes);
-  ES_CHECK_LAUNCH();
-  return ES_OK;
 }
 
 extern "C" int64_t es_weight_planes_offset(int64_t n) { return (n * 4 + 255) / 256 * 256; }

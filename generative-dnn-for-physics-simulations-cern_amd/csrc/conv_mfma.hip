@@ -37,77 +37,26 @@
 
 #include "conv_common.h"
 
-// the 4-wave split-fp32 FWD / DGRAD launches (conv_spb4.hip, see there)
-void es_spb4_launch(int mode, bool sp, const ConvArgs& a, dim3 grid, hipStream_t st);
 
 namespace {
 
 constexpr int RT = 512;   // threads per workgroup (8 waves)
-#ifndef ES_RING_LEAN
-#define ES_RING_LEAN 0   // 256 x 256 tiles: 1 = single fragment set per step (ring_loop_lean)
-#endif
 constexpr int NSLOT = 3;  // ring depth
-// ES_RING_EXP (diagnostic builds only, tools/ring_exp.sh): 1 = every A row gathers image 0 (the A
-// operand stays L2-resident), 2 = no MFMAs, 4 = no epilogue, 8 = no fused statistics, 16 = DGRAD
-// keeps the per-wave staged epilogue (FWD / DGRAD ring kernel)
-#ifndef ES_RING_EXP
-#define ES_RING_EXP 0
-#endif
-constexpr uint32_t OOB = 0x80000000u;
-#ifndef ES_COOP2
-#define ES_COOP2 0   // wgrad_coop_kernel: two register stages of loads (experiment)
-#endif
-#ifndef ES_COOP_STAG
-#define ES_COOP_STAG 0   // wgrad_coop_kernel: row tile after which waves 4-7 split the next step (0: after all)
-#endif
-#ifndef ES_SPB4_EXP
-#define ES_SPB4_EXP 0
-#endif
-#ifndef ES_SPB4_SB
-#define ES_SPB4_SB 1    // SPB4 / SPA loops: sched_barrier between column-tile iterations
-#endif
-#ifndef ES_SPB4_PFD
-#define ES_SPB4_PFD 1   // SPB4 loop: column tiles of B planes read ahead of their MFMAs
-#endif
-#ifndef ES_SPB_PFD
-#define ES_SPB_PFD 2   // split-fp32 SPB loop: column tiles of B planes read ahead of their MFMAs
-#endif
-#ifndef ES_SPB_DMA_HI
+constexpr uint32_t OOB = 0x80000000u;   // buffer offset past every num_records (< 2^31 bytes)
+// split-fp32 SPB loop (8-wave FWD / DGRAD): column tiles of B planes read ahead of their MFMAs
+constexpr int SPB_PFD = 2;
 // SPB loop: column tile at which waves 4-7 issue their step's DMA (capped at RN - 1; waves 0-3 issue
 // after column tile 0).  The two waves of a SIMD (w, w + 4) otherwise stall on their 7 LDS-DMA issues
-// at the same point, leaving the SIMD's matrix pipe idle.  Measured (tools/gpu_libab.sh, alternating,
-// B = 1024, ms/step): base 44.8-45.3; tile 2 45.34, 4 44.54, 5 44.60 / 44.60, 6 44.19 / 44.12,
-// 7 44.05 / 44.50 (conv_layers.5 FWD / DGRAD 3.15 / 3.05 -> 2.95 / 2.85 ms at 6)
-#define ES_SPB_DMA_HI 6
-#endif
-#ifndef ES_RING_STAG
-#define ES_RING_STAG 0         // ring_loop (bf16 kernels): waves 4-7 issue their step's DMA after their MFMAs
-#endif
-#ifndef ES_SPB_DMA_LO
-#define ES_SPB_DMA_LO 0        // SPB loop: column tile at which waves 0-3 issue their step's DMA
-#endif
-#ifndef ES_SPB_SPLIT_HI
-#define ES_SPB_SPLIT_HI -1     // SPB loop: column tile after which waves 4-7 split A(t+1) (-1: as waves 0-3)
-#endif
-#ifndef ES_SPB_FRESH
-// SPB loop (8-wave split-fp32 FWD / DGRAD): K-steps per fresh accumulator.  Measured (tools/gpu_r04w.sh,
-// alternating on one box, B = 1024): 1 -> 2 conv_layers.5 FWD 3.06-3.13 -> 2.94, DGRAD 2.99-3.03 ->
-// 2.82-2.84 ms, step -1.4..-2.3 %; 4 is slower (3.34 / 3.50 ms: the carried accumulators crowd the
-// registers).  Kept at 1: with 2 the 20-step training trajectory against the oracle
-// (tests/test_bf16_stats_gpu.py) drifts twice as far (gen_loss 0.0285 vs 0.0141; the exact fp32 MFMA
-// 0.0171), i.e. the MFMA's biased accumulation into a carried sum is visible over training steps
-// although every single-step and golden test passes.
-#define ES_SPB_FRESH 1
-#endif   // buffer offset past every num_records (< 2^31 bytes)
+// at the same point, leaving the SIMD's matrix pipe idle.  Measured (alternating A/B, B = 1024,
+// ms/step): base 44.8-45.3; tile 2 45.34, 4 44.54, 5 44.60, 6 44.19 / 44.12, 7 44.05 / 44.50
+// (conv_layers.5 FWD / DGRAD 3.15 / 3.05 -> 2.95 / 2.85 ms at 6).  Other placements (waves 0-3 later,
+// the A(t+1) split of waves 4-7 moved, one fresh accumulator per two K-steps, the 4-wave SPB4 / SPA
+// kernels, pre-split activation planes) measured slower or drifted and were removed in round 5
+// (DESIGN.md §4 keeps the numbers).
+constexpr int SPB_DMA_HI = 6;
 
-// ES_NO_RING=1 (or es_conv_set_ring(0)) routes these shapes to the 4-wave kernels of
-// conv_igemm.hip (A/B measurement)
-bool g_ring_off = [] { const char* e = getenv("ES_NO_RING"); return e && e[0] == '1'; }();
-// split-fp32 FWD / DGRAD 256 x 128 tiles of the sub-pixel convs on the 4-wave kernel (conv_ring_kernel
-// SPL = 3; SPL = 4 with a planes operand).  Opt-in (ES_SPB4=1 / es_conv_set_spb4(1)): measured on one
-// box at B = 1024 with alternating best-of-3 timing (tools/mb_spb4.py, r04), conv_layers.5 fwd / dgrad
-// 8-wave 2935 / 2898 us vs 4-wave 3238 / 3179 us (and 2941 / 2894 us for its row-group variant).
-bool g_spb4 = [] { const char* e = getenv("ES_SPB4"); return e && e[0] == '1'; }();
+// es_conv_set_ring(0) routes these shapes to the 4-wave kernels of conv_igemm.hip (tests)
+bool g_ring_off = false;
 
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -283,11 +232,8 @@ __device__ __forceinline__ void ring_loop(int nk, char* smem, int slot_bytes, Is
     if constexpr (NLDS > 0) fence(f1);
     ring_barrier();
     load(f0, smem + nxt * slot_bytes, 0);
-    // (ES_RING_STAG: waves 4-7 issue after their MFMAs, under those of their SIMD partner w - 4)
-    const bool late = ES_RING_STAG && __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4;
-    if (!late) issue(smem + cur * slot_bytes);           // step t + NS
+    issue(smem + cur * slot_bytes);                      // step t + NS
     mma(f1);
-    if (late) issue(smem + cur * slot_bytes);
     cur = nxt;
   }
   load(f1, smem + cur * slot_bytes, 1);
@@ -380,18 +326,8 @@ __device__ __forceinline__ void split8(const f32x4& x, const f32x4& y, bf16x8 p[
 // accumulation rounds with a negative bias (measured, tools/split_bias.py: summed outputs drift by
 // -5e-8 .. -1.2e-6 of sum|y| when every product accumulates into the running sum), so the step's
 // products go into a fresh accumulator (its rounding is on the scale of one K-step's partial sum)
-// and the running sum takes them with one round-to-nearest add per element.  (ES_SPB_FRESH = 2 builds
-// carry one fresh accumulator over two K-steps in the 8-wave FWD / DGRAD loop: mfma_chain6.)  (A plain C++ add: the
+// and the running sum takes them with one round-to-nearest add per element.  (A plain C++ add: the
 // compiler's MFMA-result hazard wait states do not cover inline asm that reads the MFMA's output.)
-// the six plane products chained onto c (small terms first), without the running-sum add
-__device__ __forceinline__ f32x4 mfma_chain6(const bf16x8 a[3], const bf16x8 b[3], f32x4 c) {
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], c, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
-}
 __device__ __forceinline__ f32x4 mfma_split6(const bf16x8 a[3], const bf16x8 b[3], f32x4 acc) {
   f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], c, 0, 0, 0);
@@ -430,40 +366,27 @@ __device__ __forceinline__ f32x4 mfma_split6(const bf16x8 a[3], const bf16x8 b[3
 // [3][BN rows][64 B] (swizzled as the BK = 32 images), and the 8 waves are stacked along M (wave
 // tile BM/8 x BN): every A element is split by one wave only.
 //
-// SPL == 3 (SPB4): SPB with FOUR waves, one per SIMD (256 threads), wave tiles 64 x BN (BN = 128:
-// 4 x 8 accumulator tiles).  Each wave DMAs exactly the 64 A rows it multiplies (one pixel x 64
-// images), so A needs no cross-wave synchronisation; the B planes (shared) are read by 4 instead of 8
-// waves (half the LDS fragment traffic of SPB), and a wave interleaves its own LDS reads, splits and
-// DMA issue between its MFMAs instead of relying on a partner wave in the same phase.  A(t+1) is read
-// and split one row tile per two column tiles of step t, into the other of two plane sets (the step
-// loop is unrolled by two so the sets swap roles without copies).
-//
-// SPL == 4 (SPA): SPB4 with the gathered operand ALSO pre-split: a_src is an activation-planes image
-// (es_split_planes: [rows][C / 32][3][32] bf16, 6 bytes per value, strides as[] in values), DMA'd as
-// planes ([3][BM rows][64 B] per slot, the B planes' image) and fed to the MFMAs as read: no split in
-// the kernel.  Same products in the same order as SPB / SPB4 (bitwise equal outputs).
 template <int MODE, int BM, int BN, bool SP, int BK = 64, typename T = bf16, int SPL = 0>
-__global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs a) {
+__global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   static_assert(!SPL || (sizeof(T) == 4 && BK == 64), "split-fp32: fp32 operands, 128-byte slot rows");
   // (SPL 256 x 256: 2 x 4 waves of 128 x 64 and two 64 KiB slots; one step in flight covers a step
   // of 192 MFMAs per wave)
-  constexpr bool SPB = SPL >= 2;
-  constexpr bool SPB4 = SPL == 3, SPA = SPL == 4, W4 = SPB4 || SPA;
-  constexpr int NW = W4 ? 4 : 8, NT = 64 * NW;           // waves / threads per workgroup
+  constexpr bool SPB = SPL == 2;
+  constexpr int NW = 8, NT = 64 * NW;                    // waves / threads per workgroup
   constexpr bool SPW = SPL == 1 && BN == 256;
   constexpr int WGM = SPB ? NW : ((BK == 32 || SPW) ? 2 : 4), WGN = NW / WGM;   // waves along M / N
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int RM = WM / 16, RN = WN / 16;
   constexpr int ROWB = BK * 2, PROWS = 1024 / ROWB;      // slot row bytes, rows per 1 KiB piece
   constexpr int EB = sizeof(T), BKC = ROWB / EB;         // operand bytes, channels per K-step (fp32: BK / 2)
-  constexpr int EA = SPA ? 6 : EB;                       // bytes per value of the gathered (A) image
+  constexpr int EA = EB;                                 // bytes per value of the gathered (A) image
   constexpr int CPR = ROWB / 16;                         // 16-byte chunks per row
   constexpr int EBB = SPB ? 6 : EB;                      // bytes per B element in global memory
   constexpr int BPL = BN / 16;                           // SPB: 1 KiB pieces per B plane
   constexpr int BPIECES = SPB ? 3 * BPL : BN / PROWS;    // (SPB, BN = 64: 12 pieces + 4 zero-fill dummies)
-  constexpr int APW = SPA ? 3 * (BM / NW / 16) : BM / PROWS / NW, BPW = (BPIECES + NW - 1) / NW;   // pieces per wave per slot
+  constexpr int APW = BM / PROWS / NW, BPW = (BPIECES + NW - 1) / NW;   // pieces per wave per slot
   constexpr int PW = APW + BPW;
-  constexpr int ABYTES = SPA ? 3 * BM * 64 : BM * ROWB, BBYTES = SPB ? 3 * BN * 64 : BN * ROWB;
+  constexpr int ABYTES = BM * ROWB, BBYTES = SPB ? 3 * BN * 64 : BN * ROWB;
   constexpr int SLOT = ABYTES + BBYTES;
   // SPB ring depths: three full slots when they fit (NS = 3); else A gets three slots and B (the
   // weights, L2-resident) two: A stays two steps ahead, B one (SPLITD)
@@ -477,7 +400,7 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
   constexpr int STAGE0 = NW * SROWS * (WN * 4 + 16);
   constexpr int TPITCH = BN * 2 + 16;                    // BK = 32 bf16 epilogue: whole-tile image
   constexpr int STAGE = BK == 32 && BM * TPITCH > STAGE0 ? BM * TPITCH : STAGE0;
-  constexpr int RINGB = W4 ? 2 * ABYTES + 2 * BBYTES : (SPLITD ? 3 * ABYTES + 2 * BBYTES : NS * SLOT);
+  constexpr int RINGB = SPLITD ? 3 * ABYTES + 2 * BBYTES : NS * SLOT;
   constexpr int RING = RINGB > STAGE ? RINGB : STAGE;
   constexpr int JUNK = BPW * NW > BPIECES ? 1024 : 0;    // landing area of the dummy pieces
   // ONE __shared__ object (a second one beside the DMA ring makes hipcc wait vmcnt(0) before
@@ -566,18 +489,13 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
   const int as2b = (int)a.as[2] * EA, as3b = (int)a.as[3] * EA;
 
   // A pieces: per-lane constant (image, 16-byte chunk) + per-piece uniform pixel coordinates.
-  // SPB4 (host: ng == 64): the wave's APW = 8 pieces are ONE pixel (pix0 + wid) x 64 images, so one
-  // set of pixel coordinates, and two per-lane constants (the swizzle depends on the piece's parity;
-  // piece j adds the uniform image offset (j & ~1) * 8 rows)
-  // SPA: the same one pixel per wave; pieces are (plane, 16 rows): lane l -> row l / 4, 16-byte chunk
-  // l % 4 of the row's 64-byte plane run, swizzled as the B planes (depends on the lane only)
-  constexpr int APC = W4 ? 1 : APW, ALN = SPB4 ? 2 : (SPA ? 1 : APW);
+  constexpr int APC = APW, ALN = APW;
   uint32_t alane[ALN];
   int pc0[APC], pc1[APC];
   bool pval[APC];
 #pragma unroll
   for (int j = 0; j < ALN; ++j) {
-    const int pi = (W4 ? wid * (BM / NW / PROWS) : wid * APW) + j;   // piece of the tile: pixel pix0 + pi / PPG
+    const int pi = wid * APW + j;                 // piece of the tile: pixel pix0 + pi / PPG
     const int rr = pi * PROWS + lrow;             // row within the tile (swizzle)
     const int lc = pc ^ swz_x<BK>(rr);
     const int ppix = pi / PPG;
@@ -586,12 +504,7 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
     const int pp = pval[j] ? pix : 0;
     const int y = pp / gw, x = pp - y * gw;
     const int img = gi * NG + (pi - ppix * PPG) * PROWS + lrow;
-    alane[j] = (uint32_t)(((ES_RING_EXP & 1) ? 0 : img) * (int)a.as[0] * EB + lc * 16);   // images >= N: past num_records
-    if constexpr (SPA) {
-      const int prow = lane >> 2;   // row of the 16-row piece
-      alane[j] = (uint32_t)((gi * NG + prow) * (int)a.as[0] * EA + (((lane & 3) ^ swz_x<32>(prow)) * 16));
-    }
-    if (j >= APC) continue;
+    alane[j] = (uint32_t)(img * (int)a.as[0] * EB + lc * 16);   // images >= N: past num_records
     if constexpr (MODE == MODE_FWD && SP) {       // source row = u + oh + d
       pc0[j] = y + sp.oh[cls];
       pc1[j] = x + sp.ow[cls];
@@ -609,15 +522,12 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
       pc1[j] = x + d.pad;
     }
   }
-  // (SPB4: every piece is valid and its swizzle term depends on the lane only, so one per-lane
-  // constant plus the piece's uniform offset, b_off below)
-  constexpr int BLN = W4 ? 1 : BPW;
-  static_assert(!W4 || BPW * NW == BPIECES, "SPB4: no dummy B pieces");
+  constexpr int BLN = BPW;
   uint32_t blane[BLN];
 #pragma unroll
   for (int j = 0; j < BLN; ++j) {
     if constexpr (SPB) {   // piece q: plane q / BPL, rows 16 (q % BPL) + lane / 4, 16-byte chunk lane % 4
-      const int q = W4 ? 0 : wid * BPW + j;
+      const int q = wid * BPW + j;
       const int rr = (q % BPL) * 16 + (lane >> 2);
       blane[j] = q < BPIECES ? (uint32_t)((bbase + (n0 + rr) * ldb) * EBB + (q / BPL) * 64 +
                                           (((lane & 3) ^ swz_x<32>(rr)) * 16))
@@ -653,7 +563,6 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
   uint32_t ua_t[APC], ub_t = 0;
 #pragma unroll
   for (int j = 0; j < APC; ++j) ua_t[j] = OOB;
-  const uint32_t as8b = (uint32_t)(8 * (int)a.as[0] * EA);   // (SPB4 / SPA) 8 images
   auto issue = [&](char* slot) {
     if (cch == 0) {   // first step of a tap (wave-uniform branch, scalar work only)
       const bool live = cstep < nk;
@@ -694,17 +603,7 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
     // (OOB + a channel offset stays past every num_records: offsets are < 1 GiB)
     const uint32_t co = (uint32_t)(cch * EA), cob = (uint32_t)(cch * EBB);
 #pragma unroll
-    for (int j = 0; j < APW; ++j) {
-      if constexpr (SPA) {   // piece j: plane j / 4, rows 16 (j % 4) .. of the wave's 64
-        const int pl = j >> 2, rq = j & 3;
-        bdma16(ares, alane[0] + (ua_t[0] + co + (uint32_t)(rq * 2) * as8b + (uint32_t)(pl * 64)),
-               slot + pl * (BM * 64) + (wm0 + rq * 16) * 64);
-      } else if constexpr (SPB4) {
-        bdma16(ares, alane[j & 1] + (ua_t[0] + co + (uint32_t)(j & ~1) * as8b), slot + (wid * APW + j) * 1024);
-      } else {
-        bdma16(ares, alane[j] + (ua_t[j] + co), slot + (wid * APW + j) * 1024);
-      }
-    }
+    for (int j = 0; j < APW; ++j) bdma16(ares, alane[j] + (ua_t[j] + co), slot + (wid * APW + j) * 1024);
     if constexpr (!SPB) {   // (SPB: B has its own ring and issue_b)
 #pragma unroll
       for (int j = 0; j < BPW; ++j) {
@@ -765,13 +664,6 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
   };
   auto mma = [&](const Frag& f) {
     const int i0 = KH == 2 ? 0 : f.h * RMF;
-    if constexpr ((ES_RING_EXP & 2) != 0) {
-#pragma unroll
-      for (int i = 0; i < RMF; ++i) asm volatile("" ::"v"(f.a[i]));
-#pragma unroll
-      for (int j = 0; j < RN; ++j) asm volatile("" ::"v"(f.b[j]));
-      return;
-    }
 #pragma unroll
     for (int i = 0; i < RMF; ++i)
 #pragma unroll
@@ -785,237 +677,7 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
         }
       }
   };
-  if constexpr (SPA) {
-    // 4-wave loop on pre-split A planes (see above the kernel).  Two A slots and two B slots: A(t+1) and
-    // B(t+1) are issued at the top of step t (after its barrier) into the slots of step t-1, so the top
-    // of step t+1 waits for everything (vmcnt(0)) and one barrier publishes B(t+1).  A is private per
-    // wave: the next step's first row group is read from A(t+1) late in step t, after the wave's own
-    // vmcnt covers it.  Per row group of IG = 2 row tiles and column tile j: B planes of j + 1 read,
-    // 2 x 6 plane products of j issued into fresh accumulators, the fresh accumulators of j - 1 added.
-    constexpr int IG = 2, NGR = RM / IG;
-    static_assert(NGR == 2 && RN == 8, "SPA: 4 x 8 tiles, two row groups of two");
-    char* const aring = smem;                   // [2][ABYTES]
-    char* const bring = smem + 2 * ABYTES;      // [2][BBYTES]
-    const int bper = (MODE == MODE_DGRAD && !SP) ? (d.R * d.S * d.K) / BKC : nk;
-    int bs = 0, bsm = 0;
-    const uint32_t brow16 = (uint32_t)(16 * ldb * EBB);      // 16 packed weight rows
-    auto issue_b = [&](char* bslot) {
-      const uint32_t ub = bs < nk ? (uint32_t)(bsm * BKC * EBB) : OOB;
-#pragma unroll
-      for (int j = 0; j < BPW; ++j) {
-        const int q = wid * BPW + j;   // plane q / BPL, rows 16 (q % BPL) + lane / 4 (blane[0]: q = 0)
-        const uint32_t b_off = (uint32_t)(q % BPL) * brow16 + (uint32_t)(q / BPL) * 64;
-        bdma16(bres, blane[0] + (ub + b_off), bslot + q * 1024);
-      }
-      ++bs;
-      bsm = bsm + 1 == bper ? 0 : bsm + 1;
-    };
-    auto rd_pl = [&](bf16x8 (&p)[3], const char* img, int rows, int r0) {   // [3][rows][64 B] planes image
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl) p[pl] = *(const bf16x8*)(img + pl * (rows * 64) + swz<32>(r0 + r16, g16));
-    };
-    auto chain6 = [&](const bf16x8 (&ap)[3], const bf16x8 (&bp)[3]) {
-      f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[2], bp[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[1], bp[1], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[0], bp[2], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[1], bp[0], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[0], bp[1], c, 0, 0, 0);
-      return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[0], bp[0], c, 0, 0, 0);
-    };
-    auto add4 = [&](f32x4& s, const f32x4& c) {   // as in the SPB4 loop
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float v = s[e] + c[e];
-        asm volatile("" : "+v"(v));
-        s[e] = v;
-      }
-    };
-    issue(aring);
-    issue_b(bring);
-    wait_vmcnt<0>();
-    ring_barrier();
-    bf16x8 AP[2][IG][3];   // planes of row group 0 / 1
-#pragma unroll
-    for (int ii = 0; ii < IG; ++ii) rd_pl(AP[0][ii], aring, BM, wm0 + ii * 16);
-    for (int t = 0; t < nk; ++t) {
-      if (t > 0) {
-        wait_vmcnt<0>();                                     // A(t), B(t): issued at the top of step t-1
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of step t-1 are done
-        ring_barrier();
-      }
-      const char* acur = aring + (t & 1) * ABYTES;
-      const char* anext = aring + ((t + 1) & 1) * ABYTES;
-      const char* bimg = bring + (t & 1) * BBYTES;
-      issue(aring + ((t + 1) & 1) * ABYTES);                 // A(t+1) into A(t-1)'s slot
-      issue_b(bring + ((t + 1) & 1) * BBYTES);               // B(t+1) into B(t-1)'s slot
-#pragma unroll
-      for (int gr = 0; gr < NGR; ++gr) {
-        __builtin_amdgcn_sched_barrier(0);
-        constexpr int PFD = ES_SPB4_PFD;
-        bf16x8 bq[PFD + 1][3];
-#pragma unroll
-        for (int jj = 0; jj < PFD; ++jj) rd_pl(bq[jj], bimg, BN, wn0 + jj * 16);
-        f32x4 cp[IG];
-#pragma unroll
-        for (int j = 0; j < RN; ++j) {
-          if constexpr (ES_SPB4_SB) __builtin_amdgcn_sched_barrier(0);
-          if (j + PFD < RN) rd_pl(bq[(j + PFD) % (PFD + 1)], bimg, BN, wn0 + (j + PFD) * 16);
-          if (gr == 0 && j == 0) {   // group 1's planes of A(t)
-#pragma unroll
-            for (int ii = 0; ii < IG; ++ii) rd_pl(AP[1][ii], acur, BM, wm0 + (IG + ii) * 16);
-          }
-          if (gr == 1 && j == RN / 2) {   // the next step's group 0 (A(t+1), this wave's own DMA)
-            wait_vmcnt<BPW>();
-#pragma unroll
-            for (int ii = 0; ii < IG; ++ii) rd_pl(AP[0][ii], anext, BM, wm0 + ii * 16);
-          }
-          f32x4 cn[IG];
-#pragma unroll
-          for (int ii = 0; ii < IG; ++ii) cn[ii] = chain6(AP[gr][ii], bq[j % (PFD + 1)]);
-          if (j > 0) {
-#pragma unroll
-            for (int ii = 0; ii < IG; ++ii) add4(acc[gr * IG + ii][j - 1], cp[ii]);
-          }
-#pragma unroll
-          for (int ii = 0; ii < IG; ++ii) cp[ii] = cn[ii];
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int ii = 0; ii < IG; ++ii) add4(acc[gr * IG + ii][RN - 1], cp[ii]);
-      }
-    }
-    wait_vmcnt<0>();   // drain the zero-fill steps before the workgroup may exit
-  } else if constexpr (SPB4) {
-    // 4-wave SPB loop, B planes cached in AGPRs (see above the kernel).
-    //   * B(t): a wave's 8 column tiles x 3 planes (24 fragments, 96 AGPRs) are read from LDS ONCE per
-    //     step (inline-asm ds_read into AGPRs, MFMA srcB straight from them) and used by all 4 row
-    //     tiles: 24 B fragment reads per wave per step instead of 48 (the B re-reads bounded the
-    //     loop: removing them alone made it 1.75x faster, ES_SPB4_EXP study r04).
-    //   * A: row tile after row tile; the fp32 row i+1 is read and split (one pair per two column
-    //     tiles) while row i's 48 MFMAs issue, into the other of two plane sets.
-    //   * Step t, row tile 3: vmcnt(0) + the one barrier of the step publish B(t+1) and A(t+1); B(t+1)'s
-    //     fragments are read into the AGPRs one column tile behind row 3's MFMAs (the last after the
-    //     step), and the DMA of B(t+2) / A(t+2) goes into the slots of B(t) / A(t) (read before).
-    //   Two A slots, two B slots.
-    char* const aring = smem;                   // [2][ABYTES]
-    char* const bring = smem + 2 * ABYTES;      // [2][BBYTES]
-    const int bper = (MODE == MODE_DGRAD && !SP) ? (d.R * d.S * d.K) / BKC : nk;
-    int bs = 0, bsm = 0;
-    const uint32_t brow16 = (uint32_t)(16 * ldb * EBB);      // 16 packed weight rows
-    auto issue_b = [&](char* bslot) {
-      const uint32_t ub = bs < nk ? (uint32_t)(bsm * BKC * EBB) : OOB;
-#pragma unroll
-      for (int j = 0; j < BPW; ++j) {
-        const int q = wid * BPW + j;   // plane q / BPL, rows 16 (q % BPL) + lane / 4 (blane[0]: q = 0)
-        const uint32_t b_off = (uint32_t)(q % BPL) * brow16 + (uint32_t)(q / BPL) * 64;
-        bdma16(bres, blane[0] + (ub + b_off), bslot + q * 1024);
-      }
-      ++bs;
-      bsm = bsm + 1 == bper ? 0 : bsm + 1;
-    };
-    auto rd_a1 = [&](f32x4 (&r)[2], const char* aslot, int i) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) r[h] = *(const f32x4*)(aslot + swz<BK>(wm0 + i * 16 + r16, g16 + 4 * h));
-    };
-    // B fragments in AGPRs (int4v for the asm constraint; bit-cast for the MFMA)
-    int4v Bc[RN][3];
-    auto ld_bc = [&](int j, const char* bimg) {
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
-        asm volatile("ds_read_b128 %0, %1" : "=a"(Bc[j][pl]) : "v"(lds_u32(bimg + pl * (BN * 64) + swz<32>(wn0 + j * 16 + r16, g16))));
-    };
-    auto fence_bc = [&]() {   // after an lgkmcnt wait: the MFMAs reading Bc cannot move above it
-#pragma unroll
-      for (int j = 0; j < RN; ++j)
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) asm volatile("" : "+a"(Bc[j][pl]));
-    };
-    auto chain6b = [&](const u32x4_t (&ap)[3], int j) {
-      const bf16x8 a0 = __builtin_bit_cast(bf16x8, ap[0]), a1 = __builtin_bit_cast(bf16x8, ap[1]),
-                   a2 = __builtin_bit_cast(bf16x8, ap[2]);
-      const bf16x8 b0 = __builtin_bit_cast(bf16x8, Bc[j][0]), b1 = __builtin_bit_cast(bf16x8, Bc[j][1]),
-                   b2 = __builtin_bit_cast(bf16x8, Bc[j][2]);
-      f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b0, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b2, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b0, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b1, c, 0, 0, 0);
-      return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, c, 0, 0, 0);
-    };
-    auto split_e = [&](const f32x4 (&r)[2], u32x4_t (&P)[3], int e) {   // pair e of the lane's 8 values
-      const float x = e < 2 ? r[0][2 * e] : r[1][2 * e - 4], y = e < 2 ? r[0][2 * e + 1] : r[1][2 * e - 3];
-      uint32_t h, m, l;
-      split_pair(x, y, h, m, l);
-      P[0][e] = h;
-      P[1][e] = m;
-      P[2][e] = l;
-    };
-    // fresh-accumulator adds: plain (the compiler's MFMA -> VALU hazard waits apply), pinned to their
-    // column tile by an empty volatile asm (unpinned they were sunk to the end of the step)
-    auto add4 = [&](f32x4& s, const f32x4& c) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float v = s[e] + c[e];
-        asm volatile("" : "+v"(v));
-        s[e] = v;
-      }
-    };
-    // prologue: A(0), B(0); B(0) into the AGPRs; A(0) row 0 split; then B(1), A(1)
-    issue(aring);
-    issue_b(bring);
-    wait_vmcnt<0>();
-    ring_barrier();
-#pragma unroll
-    for (int j = 0; j < RN; ++j) ld_bc(j, bring);
-    u32x4_t PA[3], PB[3];
-    {
-      f32x4 r[2];
-      rd_a1(r, aring, 0);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) split_e(r, PA, e);
-    }
-    issue_b(bring + BBYTES);
-    issue(aring + ABYTES);
-    for (int t = 0; t < nk; ++t) {
-      const char* acur = aring + (t & 1) * ABYTES;
-      const char* anext = aring + ((t + 1) & 1) * ABYTES;
-      const char* bnext = bring + ((t + 1) & 1) * BBYTES;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // B(t)'s fragments have landed in the AGPRs
-      fence_bc();
-#pragma unroll
-      for (int i = 0; i < RM; ++i) {
-        u32x4_t (&Pc)[3] = (i & 1) ? PB : PA;               // row i's planes (split during row i-1)
-        u32x4_t (&Pn)[3] = (i & 1) ? PA : PB;               // row i+1's (or A(t+1)'s row 0)
-        if (i == RM - 1) {
-          wait_vmcnt<0>();                                   // B(t+1), A(t+1) (issued in step t-1)
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of B(t) / A(t) done
-          ring_barrier();
-          issue_b(bring + (t & 1) * BBYTES);                 // B(t+2) into B(t)'s slot
-          issue(aring + (t & 1) * ABYTES);                   // A(t+2) into A(t)'s slot
-        }
-        f32x4 ra[2];
-        rd_a1(ra, i < RM - 1 ? acur : anext, i < RM - 1 ? i + 1 : 0);
-        f32x4 cp;
-#pragma unroll
-        for (int j = 0; j < RN; ++j) {
-          __builtin_amdgcn_sched_barrier(0);
-          const f32x4 cn = chain6b(Pc, j);
-          if (j > 0) add4(acc[i][j - 1], cp);
-          if (j & 1) split_e(ra, Pn, j >> 1);
-          if (i == RM - 1 && j > 0) ld_bc(j - 1, bnext);     // B(t+1) column j-1: its MFMAs are 6+ back
-          cp = cn;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        add4(acc[i][RN - 1], cp);
-      }
-      // the last column's B(t+1) fragments, behind its MFMAs (srcB read early in an MFMA; the nops
-      // keep the asm overwrite clear of them)
-      asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
-      ld_bc(RN - 1, bnext);
-    }
-    wait_vmcnt<0>();   // drain the zero-fill steps before the workgroup may exit
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  } else if constexpr (SPB) {
+  if constexpr (SPB) {
     // Software-pipelined split-fp32 loop.  A (activations, fp32) and B (pre-split weight planes) have
     // their own rings: A in NSA slots, B in NSB.  Step t's MFMAs use A planes split during step t-1
     // (registers) and B(t) read from LDS per column tile; under them the wave reads A(t+1) and splits
@@ -1073,18 +735,14 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
     }
     int sa1 = 1 % NSA, sb = 0, ia = 0, ib = NSB - 1;   // slots: A(t+1), B(t), A(t+NSA), B(t+NSB-1)
     constexpr int JS = RN > 2 ? RN / 2 : RN - 1;       // column tile after which A(t+1) is split
-    // ES_SPB_FRESH = G > 1: the first step of every group of G starts a fresh accumulator (cst), the
-    // middle ones continue it, the last continues it and adds it to the running sums
-    constexpr int FG = ES_SPB_FRESH, CR = FG > 1 ? RM : 1, CN = FG > 1 ? RN : 1;
-    f32x4 cst[CR][CN];
-    auto step = [&](auto phase) {   // phase: 0 = one-step group, 1 = first, 3 = middle, 2 = last
-      constexpr int PH = decltype(phase)::value;
+    constexpr int JDMA = SPB_DMA_HI < RN ? SPB_DMA_HI : RN - 1;
+    for (int t = 0; t < nk; ++t) {
       wait_vmcnt<LOOPWAIT>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of the last step are done
       ring_barrier();
       const char* bimg = bring + sb * BBYTES;
       // B planes PFD column tiles ahead (LDS latency under load exceeds one tile's 12 MFMAs)
-      constexpr int PFD = ES_SPB_PFD;
+      constexpr int PFD = SPB_PFD;
       bf16x8 bq[PFD + 1][3];
 #pragma unroll
       for (int j = 0; j < PFD && j < RN; ++j) rd_b(bq[j], bimg, j);
@@ -1095,19 +753,14 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
       for (int j = 0; j < RN; ++j) {
         if (j + PFD < RN) rd_b(bq[(j + PFD) % (PFD + 1)], bimg, j + PFD);
 #pragma unroll
-        for (int i = 0; i < RM; ++i) {
-          if constexpr (PH == 0) acc[i][j] = mfma_split6(apc[i], bq[j % (PFD + 1)], acc[i][j]);
-          else if constexpr (PH == 1) cst[i % CR][j % CN] = mfma_chain6(apc[i], bq[j % (PFD + 1)], f32x4{0.f, 0.f, 0.f, 0.f});
-          else if constexpr (PH == 3) cst[i % CR][j % CN] = mfma_chain6(apc[i], bq[j % (PFD + 1)], cst[i % CR][j % CN]);
-          else acc[i][j] = acc[i][j] + mfma_chain6(apc[i], bq[j % (PFD + 1)], cst[i % CR][j % CN]);
-        }
+        for (int i = 0; i < RM; ++i) acc[i][j] = mfma_split6(apc[i], bq[j % (PFD + 1)], acc[i][j]);
         // the step's DMA, once its first MFMAs are queued (STAGGER: the two waves of a SIMD, w and
         // w + 4, at different column tiles, so one issues MFMAs while the other stalls on the issue)
-        if (j == (wid >= 4 ? (ES_SPB_DMA_HI < RN ? ES_SPB_DMA_HI : RN - 1) : (ES_SPB_DMA_LO < RN ? ES_SPB_DMA_LO : RN - 1))) {
+        if (j == (wid >= 4 ? JDMA : 0)) {
           issue_b(bring + ib * BBYTES);
           issue(aring + ia * ABYTES);
         }
-        if (j == (ES_SPB_SPLIT_HI >= 0 && ES_SPB_SPLIT_HI < RN && wid >= 4 ? ES_SPB_SPLIT_HI : JS)) {
+        if (j == JS) {
 #pragma unroll
           for (int i = 0; i < RM; ++i) split8(ra[i][0], ra[i][1], apn[i]);
         }
@@ -1120,18 +773,6 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
       ia = ia + 1 == NSA ? 0 : ia + 1;
       sb = sb + 1 == NSB ? 0 : sb + 1;
       ib = ib + 1 == NSB ? 0 : ib + 1;
-    };
-    if constexpr (FG > 1) {
-      int t = 0;
-      for (; t + FG <= nk; t += FG) {
-        step(std::integral_constant<int, 1>{});
-#pragma unroll
-        for (int u = 1; u < FG - 1; ++u) step(std::integral_constant<int, 3>{});
-        step(std::integral_constant<int, 2>{});
-      }
-      for (; t < nk; ++t) step(std::integral_constant<int, 0>{});   // (the remainder one step at a time)
-    } else {
-      for (int t = 0; t < nk; ++t) step(std::integral_constant<int, 0>{});
     }
     wait_vmcnt<0>();   // drain the zero-fill steps before the workgroup may exit
   } else if constexpr (SPL) {
@@ -1174,20 +815,11 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
     };
     if (a.prio && wid >= 4) __builtin_amdgcn_s_setprio(1);   // (wid is wave-uniform: readfirstlane)
     ring_loop_lean<PW, NS, 1>(nk, smem, SLOT, issue, load_s, mma_s);
-  } else if constexpr (BK == 32 && ES_RING_LEAN) {
-    ring_loop_lean<PW, NS>(nk, smem, SLOT, issue, load, mma);
   } else {
     auto nofence = [](Frag&) {};
     ring_loop<PW, 0, NS>(nk, smem, SLOT, issue, load, mma, nofence);
   }
 
-  if constexpr ((ES_RING_EXP & 4) != 0) {
-#pragma unroll
-    for (int i = 0; i < RM; ++i)
-#pragma unroll
-      for (int j = 0; j < RN; ++j) asm volatile("" ::"v"(acc[i][j]));
-    return;
-  }
   // epilogue.  Wave row r (0..WM-1) = tile row t = wm0 + r: pixel pix0 + t / NG, image
   // NG gi + t % NG.
   const int col16 = lane & 15, rq = (lane >> 4) * 4;
@@ -1240,73 +872,10 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
     // BatchNorm statistics of the stored values (conv -> BatchNorm fusion): per column, count /
     // mean / M2 over the wave's valid rows (lanes own 16 rows, Chan-merged across the 4 row
     // groups by shuffles), then across the 4 row waves in LDS -> one [3][Ng] partial per row tile
-    float* part = (MODE == MODE_FWD && !(ES_RING_EXP & 8)) ? a.stats_part : nullptr;   // (FWD only: compiled out of DGRAD)
+    float* part = MODE == MODE_FWD ? a.stats_part : nullptr;   // (FWD only: compiled out of DGRAD)
     float (*st_n)[BN] = (float (*)[BN])(smem + RING);
     float (*st_m)[BN] = st_n + WGM;
     float (*st_q)[BN] = st_n + 2 * WGM;
-    // fp32 DGRAD fused with the REDUCTION pass of the BatchNorm backward that consumes its output
-    // (es_conv2d_dgrad_bnred; the generator's conv_layers.9 / .5 dgrads -> BatchNorm conv_layers.6 /
-    // .1 + Dropout + LeakyReLU, neutron/generator.py:13-40): each stored 16-byte chunk (4 channels of one
-    // output row) is folded with the norm input h and the keep bits at the same position into the
-    // lane's per-channel sums of dnorm and dnorm * xhat (norm_fast.hip bn_reduce_fast's expressions);
-    // lanes, then the WGM row waves, are merged in a fixed order into one [3][Ng] partial per row
-    // tile (slots 1, 2), which es_norm_act_bwd_sums finalises (deterministic).  Output unchanged.
-    const bool bnr_on = MODE == MODE_DGRAD && EB == 4 && a.bnr_part != nullptr;
-    float bs1[4] = {0.f, 0.f, 0.f, 0.f}, bs2[4] = {0.f, 0.f, 0.f, 0.f};
-    auto bnr_fold = [&](int64_t o, const f32x4& dyv) {   // o: element offset of the chunk's first channel
-      const f32x4 hv = *(const f32x4*)((const float*)a.bnr_x + o);
-      const int c0 = (int)(o % a.Ng);
-      const uint32_t kb = a.bnr_drop ? ((uint32_t)a.bnr_keep[o >> 3] >> (c0 & 7)) : 0xFu;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int c = c0 + e;
-        const float is = a.bnr_invstd[c], mu = a.bnr_mean[c];
-        const float sc = (a.bnr_gamma ? a.bnr_gamma[c] : 1.f) * is;
-        const float z = hv[e] * sc + ((a.bnr_beta ? a.bnr_beta[c] : 0.f) - mu * sc);
-        const bool keep = !a.bnr_drop || ((kb >> e) & 1u);
-        const float zs = a.bnr_drop && a.bnr_dfirst ? z * a.bnr_scale : z;
-        const float dsc = a.bnr_drop ? a.bnr_scale : 1.f;
-        const float dn = keep ? dyv[e] * (zs > 0.f ? 1.f : a.bnr_slope) * dsc : 0.f;
-        bs1[e] += dn;
-        bs2[e] += dn * ((hv[e] - mu) * is);
-      }
-    };
-    auto bnr_flush = [&]() {
-      const int cpr4 = WN / 4, rpi4 = 64 / cpr4;   // fp32 staging: lanes l, l + cpr4, ... share channels
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        for (int o = cpr4; o < 64; o <<= 1) {
-          bs1[e] += __shfl_xor(bs1[e], o, 64);
-          bs2[e] += __shfl_xor(bs2[e], o, 64);
-        }
-      (void)rpi4;
-      const int wmi = wid / WGN;
-      __syncthreads();   // (the stats scratch beside the ring: no DMA targets it)
-      if (lane < cpr4) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          st_m[wmi][wn0 + lane * 4 + e] = bs1[e];
-          st_q[wmi][wn0 + lane * 4 + e] = bs2[e];
-        }
-      }
-      __syncthreads();
-      if (wid < WGN) {   // row block 0's waves merge the WGM row waves of their columns, in order
-        for (int c = lane; c < WN; c += 64) {
-          float u1 = 0.f, u2 = 0.f;
-          for (int w = 0; w < WGM; ++w) {
-            u1 += st_m[w][wn0 + c];
-            u2 += st_q[w][wn0 + c];
-          }
-          const int kc = kc0 + c;
-          if (kc < a.Ng) {
-            float* pp = a.bnr_part + (int64_t)tl * 3 * a.Ng;
-            pp[kc] = 0.f;
-            pp[a.Ng + kc] = u1;
-            pp[2 * a.Ng + kc] = u2;
-          }
-        }
-      }
-    };
     if (part) {
       const int wmi = wid / WGN;
       bool okr[RM][4];
@@ -1378,7 +947,7 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
         }
       }
     }
-    if (BK == 32 && BN == 256 && (MODE == MODE_FWD || !(ES_RING_EXP & 16)) && a.out_bf16) {
+    if (BK == 32 && BN == 256 && a.out_bf16) {
       // The whole 256 x 256 tile is staged in LDS ([row][256 columns], pitch TPITCH), then every
       // store instruction writes two full 512-byte rows: tile rows t0 = (2 pp) NG + n and
       // t0 + NG, i.e. one image at two consecutive pixels.  Consecutive tile rows are different
@@ -1453,14 +1022,8 @@ __global__ void __launch_bounds__(SPL >= 3 ? 256 : RT) conv_ring_kernel(ConvArgs
             const int64_t ro = row_off(ps * SROWS + r);
             const f32x4 vv = *(const f32x4*)(stg + r * pitch + lch * 16);
             *(uint4*)(obase + ro * esz) = __builtin_bit_cast(uint4, vv);
-            if constexpr (MODE == MODE_DGRAD && EB == 4) {
-              if (bnr_on) bnr_fold(ro + kc0 + lch * 4, vv);
-            }
           }
       }
-    }
-    if constexpr (MODE == MODE_DGRAD && EB == 4) {
-      if (bnr_on) bnr_flush();
     }
     }
     if (part && wid < WGN) {   // the waves of row block 0 merge the WGM row waves of their columns
@@ -2316,15 +1879,9 @@ __global__ void __launch_bounds__(RT) conv_p256_kernel(ConvArgs a, int R) {
 // SP: the tile's tap is a (class, d, e) tap of the sub-pixel decomposition; its K runs over the
 // class's output pixels, and the epilogue adds the tile into every original tap (r, s) the
 // combined tap covers (r in {2d - a, 2d - a + 1} within [0, R), likewise s).
-// MT (multi-tap; stride 1, pad 0, no upsample, C | BN): the tile's BN columns span BN / C taps.
-// Every tap of a valid output pixel is in range, so a lane's 16-byte chunk carries its tap's
-// (r, s) offset in its per-lane base and the per-step gather offset stays wave-uniform: one tile
-// reads dy once for BN / C taps (generator conv_layers.9, 2 x 2 taps x 128 channels: BN = 256 halves
-// the dy and x re-reads of the one-tap 128-column tiles).
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, bool SP, bool MT = false>
+template <int BM, int BN, bool SP>
 __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
-  static_assert(!(SP && MT), "multi-tap tiles are for plain convs");
   constexpr int WGM = BM >= 64 ? BM / 64 : 1, WGN = 8 / WGM;   // waves along M / N
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int RM = WM / 16, RN = WN / 16;
@@ -2380,13 +1937,7 @@ __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
   for (int j = 0; j < BPW; ++j) {
     const int kr = (wid * BPW + j) * (64 / BLPR) + lane / BLPR;
     const int chg = (lane % BLPR) ^ swz_tr<BN>(kr);
-    if constexpr (MT) {
-      const int gcol = n0 + chg * 8, rsl = gcol / d.C, cl = gcol - rsl * d.C;
-      const int trl = rsl / d.S, tsl = rsl - trl * d.S;
-      blane[j] = (uint32_t)(kr * bs0b + cl * 2 + trl * bs2b + tsl * bs3b);
-    } else {
-      blane[j] = (uint32_t)(kr * bs0b + (cb + chg * 8) * 2);
-    }
+    blane[j] = (uint32_t)(kr * bs0b + (cb + chg * 8) * 2);
   }
 
   // K-step cursor (uniform): pixel (p, q) of the grid and image group gi of step t = (p*gq + q)*G + gi
@@ -2408,9 +1959,6 @@ __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
       const int hs = cp + coh + tr, ws = cq + cow + ts;
       const bool ok = live && (unsigned)hs < (unsigned)d.H && (unsigned)ws < (unsigned)d.W;
       ub = ok ? (uint32_t)(cg * 64 * bs0b + hs * bs2b + ws * bs3b) : OOB;
-    } else if constexpr (MT) {   // (the taps' offsets are in blane)
-      ua = live ? (uint32_t)(cg * 64 * as0b + cp * as2b + cq * as3b) : OOB;
-      ub = live ? (uint32_t)(cg * 64 * bs0b + cp * bs2b + cq * bs3b) : OOB;
     } else {
       ua = live ? (uint32_t)(cg * 64 * as0b + cp * as2b + cq * as3b) : OOB;
       const int hu = cp * d.stride - d.pad + tr, wu = cq * d.stride - d.pad + ts;
@@ -2474,10 +2022,9 @@ __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
     s1 = min(d.S - 1, 2 * ts - cbb + 1);
   }
   const int ldo = d.R * d.S * d.C;
-  if constexpr (MT) r0 = r1 = s0 = s1 = 0;
   for (int r = r0; r <= r1; ++r)
     for (int s_ = s0; s_ <= s1; ++s_) {
-      float* o = out + (MT ? n0 : (r * d.S + s_) * d.C + cb) + wn0 + col16;
+      float* o = out + (r * d.S + s_) * d.C + cb + wn0 + col16;
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
@@ -2769,134 +2316,7 @@ __device__ __forceinline__ void ring_loop_keep(int nk, char* smem, int slot_byte
 // wgrad_f32_kernel<64, 512> are LDS-fill bound).  A row is Q + 1 column-steps (the first loads only);
 // a split starting inside a row first reloads the column before it (no MFMAs on such steps).
 // Same deterministic partial slots and ordered reduce as wgrad_f32_kernel.
-__global__ void __launch_bounds__(RT) wgrad_f32_col_kernel(ConvArgs a, float* __restrict__ ws, int ngt) {
-  constexpr int KI = 32, BM = 64, CC = 128;                     // (N = 4 taps x CC = 512)
-  constexpr int RM = 4, RN = 4;                                // 8 waves of 64 x 64 (one tap, 64 channels)
-  constexpr int AIMG = KI * BM * 4, SLOT = AIMG + KI * 2 * CC * 4;   // 8 + 32 KiB
-  constexpr int NS = 4;
-  constexpr int APW = 1, BPW = 4, PW = APW + BPW;
-  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
-  const es_conv_desc_t& d = a.d;
-  const int G = (d.N + KI - 1) / KI, Q1 = d.Q + 1;
-  const int split = xcd_remap(blockIdx.z, gridDim.z);
-  const int nst = G * d.P * Q1;
-  const int tbeg = min(split * a.k_per_split, nst), tend = min(nst, tbeg + a.k_per_split);
-
-  const int lane = threadIdx.x & 63, wid = uni(threadIdx.x >> 6);
-  const int tap = wid >> 1, wtr = tap >> 1, wts = tap & 1, wc0 = (wid & 1) * 64;
-  const int col16 = lane & 15, rq = (lane >> 4) * 4;
-  f32x4 acc[RM][RN];
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  if (tbeg < tend) {
-    const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * 4));
-    const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)(d.N * a.bs[0] * 4));
-    const int as0b = (int)a.as[0] * 4, as2b = (int)a.as[2] * 4, as3b = (int)a.as[3] * 4;
-    const int bs0b = (int)a.bs[0] * 4, bs2b = (int)a.bs[2] * 4, bs3b = (int)a.bs[3] * 4;
-    uint32_t alane, blane[BPW];
-    {
-      const int kr = wid * 4 + (lane >> 4);                    // 4 images of 64 channels per piece
-      alane = (uint32_t)(kr * as0b + (((lane & 15) ^ ((kr & 1) << 2)) * 4) * 4);
-    }
-    const int ltr = lane >> 5;                                 // the lane's input row (the swizzle
-#pragma unroll                                                 //  stays inside a 32-chunk half)
-    for (int j = 0; j < BPW; ++j) {
-      const int kr = wid * BPW + j;                            // one image (2 x 128 channels) per piece
-      blane[j] = (uint32_t)(kr * bs0b + (((lane ^ ((kr & 1) << 2)) & 31) * 4) * 4);
-    }
-    // the first step: the column before tbeg when tbeg is inside a row
-    int cg, cp, cj;
-    {
-      cg = tbeg / (d.P * Q1);
-      const int r = tbeg - cg * d.P * Q1;
-      cp = r / Q1;
-      cj = r - cp * Q1;
-    }
-    const int s0 = tbeg - (cj > 0);
-    cj -= cj > 0;
-    int cstep = s0;
-    {   // zero the B image of the slot the first step takes as its previous one
-      float4* z = (float4*)(smem + (NS - 1) * SLOT + AIMG);
-      for (int i = threadIdx.x; i < KI * 2 * CC / 4; i += RT) z[i] = float4{0.f, 0.f, 0.f, 0.f};
-    }
-    auto issue = [&](char* slot) {
-      const bool live = cstep < tend;
-      const uint32_t ua =
-          live && cj > 0 && cstep >= tbeg ? (uint32_t)(cg * KI * as0b + cp * as2b + (cj - 1) * as3b) : OOB;
-      const int hu = cp - d.pad + ltr, wu = cj - d.pad;
-      const bool ok = live && (unsigned)hu < (unsigned)d.H && (unsigned)wu < (unsigned)d.W;
-      const uint32_t ub = ok ? (uint32_t)(cg * KI * bs0b + hu * bs2b + wu * bs3b) : OOB;
-      bdma16(ares, alane + ua, slot + wid * 1024);
-#pragma unroll
-      for (int j = 0; j < BPW; ++j) bdma16(bres, blane[j] + ub, slot + AIMG + (wid * BPW + j) * 1024);
-      ++cstep;
-      ++cj;
-      const bool w1 = cj == Q1;
-      cj = w1 ? 0 : cj;
-      cp += w1;
-      const bool w2 = cp == d.P;
-      cp = w2 ? 0 : cp;
-      cg += w2;
-    };
-    struct FragS {
-      float a[8][RM], b[8][RN];
-    };
-    const int kl = lane >> 4;
-    // the lane's byte offsets of float (k-row 4 j + kl, row base + 16 i + col16), i even / odd: the
-    // swizzle of odd k-rows flips bit 0 of i (base % 32 == 0), the rest is an immediate 4 j rowb + 64 i
-    const int sw = (kl & 1) * 64;
-    const int oa0 = kl * BM * 4 + col16 * 4 + sw, oa1 = oa0 - 2 * sw;
-    const int ob0 = kl * 2 * CC * 4 + (wtr * CC + wc0 + col16) * 4 + sw, ob1 = ob0 - 2 * sw;
-    auto load_s = [&](FragS& f, const char* slot, const char* prev) {
-      const char* bimg = (wts ? slot : prev) + AIMG;
-      const char* pa[2] = {slot + oa0, slot + oa1};
-      const char* pb[2] = {bimg + ob0, bimg + ob1};
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-#pragma unroll
-        for (int i = 0; i < RM; ++i) f.a[j][i] = *(const float*)(pa[i & 1] + j * 4 * BM * 4 + 64 * i);
-#pragma unroll
-        for (int jn = 0; jn < RN; ++jn) f.b[j][jn] = *(const float*)(pb[jn & 1] + j * 4 * 2 * CC * 4 + 64 * jn);
-      }
-    };
-    // steps without MFMAs of their own (a row's first column, a split's reloaded column) have
-    // A = 0 (OOB fill): they run the same MFMAs, which add exact zeros (the previous slot of the
-    // first step is zeroed below, so no uninitialised LDS reaches them)
-    auto mma_s = [&](const FragS& f) {
-      bf16x8 bp[RN][3], ap[3];
-      auto sa = [&](int i) {
-        split8(f32x4{f.a[0][i], f.a[1][i], f.a[2][i], f.a[3][i]}, f32x4{f.a[4][i], f.a[5][i], f.a[6][i], f.a[7][i]},
-               ap);
-      };
-      sa(0);
-#pragma unroll
-      for (int jn = 0; jn < RN; ++jn) {
-        split8(f32x4{f.b[0][jn], f.b[1][jn], f.b[2][jn], f.b[3][jn]},
-               f32x4{f.b[4][jn], f.b[5][jn], f.b[6][jn], f.b[7][jn]}, bp[jn]);
-        acc[0][jn] = mfma_split6(ap, bp[jn], acc[0][jn]);
-      }
-#pragma unroll
-      for (int i = 1; i < RM; ++i) {
-        sa(i);
-#pragma unroll
-        for (int jn = 0; jn < RN; ++jn) acc[i][jn] = mfma_split6(ap, bp[jn], acc[i][jn]);
-      }
-    };
-    ring_loop_keep<PW, NS>(tend - s0, smem, SLOT, issue, load_s, mma_s);
-  }
-  float* o = ws + (int64_t)split * a.M * ngt + tap * CC + wc0 + col16;
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-      for (int j = 0; j < RN; ++j) o[(int64_t)(i * 16 + rq + jj) * ngt + j * 16] = acc[i][j][jj];
-}
-
-// wgrad_f32_col_kernel with dy split once per workgroup: the 8 waves share the tile's 64 dy rows,
+// (wgrad_f32_col2_kernel; a first version that split dy in every wave was slower.)  dy is split once per workgroup: the 8 waves share the tile's 64 dy rows,
 // so instead of every wave splitting all of them (32 of a lane's 64 split values per step), dy is
 // buffer-loaded into registers one step ahead (4 values per lane), split by the loading lane and
 // written to LDS as bf16 planes in the fragment layout (as wgrad_coop_kernel), double-buffered; the
@@ -3185,12 +2605,11 @@ __global__ void __launch_bounds__(RT) wgrad_coop_kernel(ConvArgs a, float* __res
 #pragma unroll
         for (int p = 0; p < 3; ++p) bp[jn][p] = *(const bf16x8*)(q + p * PLANE + (NBA + wn0 / 16 + jn) * 1024);
     };
-    auto rows = [&](const char* pb, const bf16x8 (&bp)[RN][3], int i0, int i1) {   // rows [i0, i1) of the tile
+    auto rows = [&](const char* pb, const bf16x8 (&bp)[RN][3]) {
       const char* q = pb + lane * 16;
       bf16x8 ap[3];
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
-        if (i < i0 || i >= i1) continue;
 #pragma unroll
         for (int p = 0; p < 3; ++p) ap[p] = *(const bf16x8*)(q + p * PLANE + (wm0 / 16 + i) * 1024);
 #pragma unroll
@@ -3200,7 +2619,7 @@ __global__ void __launch_bounds__(RT) wgrad_coop_kernel(ConvArgs a, float* __res
     auto compute = [&](const char* pb) {
       bf16x8 bp[RN][3];
       load_b(pb, bp);
-      rows(pb, bp, 0, RM);
+      rows(pb, bp);
     };
     auto sync = [] {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -3208,62 +2627,21 @@ __global__ void __launch_bounds__(RT) wgrad_coop_kernel(ConvArgs a, float* __res
     };
     Stage s0;
     const int nk = tend - tbeg;
-#if ES_COOP2
-    Stage s1;
-    load(s1);
-    load(s0);
-    store(s1, smem);
-#else
     load(s0);
     store(s0, smem);
-#endif
     sync();
-#if ES_COOP2
-    for (int t = 0; t < nk; t += 2) {
-      load(s1);                 // step t + 2
-      __builtin_amdgcn_sched_barrier(0);
-      compute(smem);            // step t
-      store(s0, smem + PBUF);   // step t + 1
-      sync();
-      if (t + 1 >= nk) break;
-      load(s0);                 // step t + 3
-      __builtin_amdgcn_sched_barrier(0);
-      compute(smem + PBUF);     // step t + 1
-      store(s1, smem);          // step t + 2
-      sync();
-    }
-#else
     // one stage of registers: step t + 1's loads are issued before step t's MFMAs and split after
-    // them (two stages, 24 more registers, spill at 128 x 256)
+    // them (two stages, 24 more registers, spill at 128 x 256; measured slower, round 4)
     for (int t = 0; t < nk; ++t) {
       char* cur = smem + (t & 1) * PBUF;
       char* nxt = smem + ((t & 1) ^ 1) * PBUF;
       load(s0);                 // step t + 1
       asm volatile("" ::: "memory");
-      if (ES_COOP_STAG > 0 && ES_COOP_STAG < RM && wid >= 4) {
-        // waves 4-7 split step t + 1 between their row tiles ES_COOP_STAG - 1 and ES_COOP_STAG, under
-        // the MFMAs of their SIMD partner (wave w - 4), which splits after all its rows
-        bf16x8 bp[RN][3];
-        load_b(cur, bp);
-        rows(cur, bp, 0, ES_COOP_STAG);
-        // (opaque here and fenced: hipcc otherwise speculates the split above the branch or schedules
-        // it into the first MFMAs, and its vmcnt wait with it)
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int h = 0; h < NH; ++h)
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) asm volatile("" : "+v"(s0[h][jj]));
-        store(s0, nxt);
-        __builtin_amdgcn_sched_barrier(0);
-        rows(cur, bp, ES_COOP_STAG, RM);
-      } else {
-        compute(cur);           // step t
-        if (ES_COOP_STAG > 0) __builtin_amdgcn_sched_barrier(0);
-        store(s0, nxt);         // step t + 1 (its buffer was last read in step t - 1)
-      }
+      compute(cur);             // step t
+      store(s0, nxt);           // step t + 1 (its buffer was last read in step t - 1)
       sync();
     }
-#endif
+    wait_vmcnt<0>();
     wait_vmcnt<0>();
   }
   float* o = ws + ((int64_t)split * a.M + m0 + wm0) * ngt + n0 + wn0 + col16;
@@ -3395,14 +2773,10 @@ __global__ void __launch_bounds__(256) wgrad_reduce4_kernel(const float* __restr
   }
 }
 
-#ifndef ES_SPB4_TU
-namespace {
-bool g_wr4 = [] { const char* e = getenv("ES_WGRAD_REDUCE4"); return !(e && e[0] == '0'); }();   // A/B
-}  // namespace
 // one deterministic reduce launch (the vector kernel when the channels allow it)
 static void launch_wgrad_reduce(const float* ws, int splits, int K, int C, int R, int S, int ngt, const SubPixel& sp,
                                 float* dw, float beta, hipStream_t st) {
-  if (g_wr4 && C % 4 == 0 && ngt % 4 == 0) {
+  if (C % 4 == 0 && ngt % 4 == 0) {
     const int64_t n4 = (int64_t)K * C / 4 * R * S;
     const int blocks = (int)std::min<int64_t>((n4 + 31) / 32, 16384);
     hipLaunchKernelGGL(wgrad_reduce4_kernel, dim3(blocks), dim3(256), 0, st, ws, splits, K, C, R, S, ngt, sp, dw, beta);
@@ -3412,28 +2786,7 @@ static void launch_wgrad_reduce(const float* ws, int splits, int K, int C, int R
   const int blocks = (int)std::min<int64_t>((n + 31) / 32, 16384);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, splits, K, C, R, S, ngt, sp, dw, beta);
 }
-#endif
-
-#ifdef ES_SPB4_TU
-}  // namespace
-
-// conv_spb4.hip = this file with ES_SPB4_TU: only the 4-wave split-fp32 kernels (conv_ring_kernel
-// SPL = 3) are instantiated, built with VGPR-form MFMA (-mllvm -amdgpu-mfma-vgpr-form) and without
-// SLP vectorisation: their per-step fresh accumulators are added to the running sums by the VALU, so
-// AGPR destinations would cost an accvgpr read per element and SLP's v_pk_add_f32 costs issue cycles
-// beside MFMAs (MI355X_MICROARCH.md, filler prices)
-void es_spb4_launch(int mode, bool sp, const ConvArgs& a, dim3 grid, hipStream_t st) {
-  (void)sp;   // (sub-pixel convs only, see launch_ring)
-  if (a.a_planes) {   // pre-split operand planes (SPA)
-    if (mode == MODE_FWD) hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 128, true, 64, float, 4>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((conv_ring_kernel<MODE_DGRAD, 256, 128, true, 64, float, 4>), grid, dim3(256), 0, st, a);
-    g_planes_req.used = 1;
-    return;
-  }
-  if (mode == MODE_FWD) hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 128, true, 64, float, 3>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((conv_ring_kernel<MODE_DGRAD, 256, 128, true, 64, float, 3>), grid, dim3(256), 0, st, a);
-}
-#else
+// host-side count of the MFMA conv kernels issued
 // host-side count of the MFMA conv kernels issued (ring / persistent / p256 / fp32 wgrad), read by
 // bench.py's probe to state how many launches one probed op is (fp32 image chunks)
 int64_t g_conv_launches = 0;
@@ -3443,19 +2796,13 @@ template <int MODE, int BM, int BN, bool SP, int BK = 64, typename T = bf16, int
 void launch_ring(const ConvArgs& a, int row_tiles, hipStream_t st) {
   dim3 grid(row_tiles, (a.Ng + BN - 1) / BN, 1);
   ++g_conv_launches;
-  // the 4-wave kernel (opt-in, see g_spb4) for the sub-pixel convs; a planes operand requires it
-  if constexpr (SPL == 2 && BM == 256 && BN == 128 && SP) {
-    if ((g_spb4 || a.a_planes) && a.ng == 64) {   // (the 4-wave kernel: one pixel x 64 images per wave)
-      es_spb4_launch(MODE, SP, a, grid, st);
-      return;
-    }
-  }
   hipLaunchKernelGGL((conv_ring_kernel<MODE, BM, BN, SP, BK, T, SPL>), grid, dim3(RT), 0, st, a);
 }
 
-// minimum K-steps per WGRAD K-split (each split flushes its whole fp32 tile with atomics)
-int g_wgrad_mink = [] { const char* e = getenv("ES_WGRAD_MINK"); return e && atoi(e) > 0 ? atoi(e) : 8; }();
-template <int BM, int BN, bool SP, bool MT = false>
+// minimum K-steps per WGRAD K-split (each split flushes its whole fp32 tile with atomics; 8 / 32 / 64
+// / 128 measured within noise at B = 1024 and E = 4 B = 512, 128 slower)
+constexpr int WGRAD_MINK = 8;
+template <int BM, int BN, bool SP>
 void launch_wgrad_ring(ConvArgs& a, hipStream_t st) {
   const int taps = SP ? a.sp.tap0[4] : a.d.R * a.d.S;
   const int tiles = (a.M / BM) * (taps * a.d.C / BN);
@@ -3464,12 +2811,12 @@ void launch_wgrad_ring(ConvArgs& a, hipStream_t st) {
     for (int c = 0; c < 4; ++c) npix = c == 0 ? a.sp.ph[0] * a.sp.pw[0] : max(npix, a.sp.ph[c] * a.sp.pw[c]);
   const int ks = npix * ((a.d.N + 63) / 64);   // K-steps (the largest class)
   // one workgroup per CU: aim at two full rounds of the 256 CUs, >= g_wgrad_mink K-steps per split
-  const int want = max(1, min(ks / g_wgrad_mink, 512 / tiles));
+  const int want = max(1, min(ks / WGRAD_MINK, 512 / tiles));
   const int per = (ks + want - 1) / want;
   a.k_per_split = per;
   dim3 grid(a.M / BM, taps * a.d.C / BN, (ks + per - 1) / per);
   ++g_conv_launches;
-  hipLaunchKernelGGL((wgrad_ring_kernel<BM, BN, SP, MT>), grid, dim3(RT), 0, st, a);
+  hipLaunchKernelGGL((wgrad_ring_kernel<BM, BN, SP>), grid, dim3(RT), 0, st, a);
 }
 
 // a dense NHWC image stack (n outermost, rows of c contiguous values) below 1 GiB in bytes
@@ -3480,35 +2827,20 @@ bool dense_small_t(const int64_t s[4], int n, int c, int h, int w) {
 }
 bool dense_small(const int64_t s[4], int n, int c, int h, int w) { return dense_small_t<2>(s, n, c, h, w); }
 
-bool g_ring_shortk = [] { const char* e = getenv("ES_RING_SHORTK"); return !(e && e[0] == '0'); }();
-int g_ring_ng = [] { const char* e = getenv("ES_RING_NG"); return e ? atoi(e) : 0; }();
-bool g_subpixel_off = [] { const char* e = getenv("ES_NO_SUBPIXEL"); return e && e[0] == '1'; }();
-// Sub-pixel FWD knobs: class-interleaved tile order (default; ES_SP_ILV=0 class-major: measured
-// 14.45 -> 14.33 ms per step); ES_SP_SHORTK=n: 128 x 64 tiles when a class has <= n K-steps (n = 16
-// measured slower: 14.59 ms)
-int g_sp_ilv = [] { const char* e = getenv("ES_SP_ILV"); return e ? atoi(e) : 1; }();
-int g_sp_shortk = [] { const char* e = getenv("ES_SP_SHORTK"); return e ? atoi(e) : 0; }();
-// 256 x 256 tiles with 32-deep K-steps (conv_ring_kernel BK = 32) for FWD / DGRAD with >= 256 output
-// columns; ES_RING256=0 keeps 256 x 128 (A/B)
-bool g_ring256 = [] { const char* e = getenv("ES_RING256"); return !(e && e[0] == '0'); }();
-// sub-pixel FWD whose 4 parity classes have the same geometry (e.g. 3x3 pad 0: every class reads
-// the 2x2 source window at (u, v)): one 256 x 256 GEMM over (class, channel) columns; ES_SP_MERGE=0
-// runs the classes as separate row tiles (A/B)
-bool g_sp_merge = [] { const char* e = getenv("ES_SP_MERGE"); return !(e && e[0] == '0'); }();
-// persistent short-K FWD / DGRAD (conv_persist_kernel); ES_PERSIST=0 keeps the ring kernel (A/B).
-// FWD only with ES_PERSIST_FWD=1: measured at B = 1024 (tools/conv_micro.py), conv_layers.9 FWD
-// 306 us persistent vs 311 us ring without fused statistics but 376 vs 364 us with them, while
-// its DGRAD (4 K-steps, 128 columns) drops from 387 to 259 us
-bool g_persist = [] { const char* e = getenv("ES_PERSIST"); return !(e && e[0] == '0'); }();
-bool g_persist_fwd = [] { const char* e = getenv("ES_PERSIST_FWD"); return e && e[0] == '1'; }();
-// persistent 256 x 256 merged sub-pixel FWD (conv_p256_kernel); ES_P256=0 keeps the ring kernel (A/B)
-bool g_p256 = [] { const char* e = getenv("ES_P256"); return !(e && e[0] == '0'); }();
-// multi-tap 64 x 256 WGRAD tiles (wgrad_ring_kernel MT) for plain 64-output-channel convs, opt-in
-// with ES_WGRAD_MT=1.  Measured at B = 1024 (tools/gpu_bnred.sh, one box): conv_layers.9 WGRAD
-// 335 us with 2-tap tiles vs 334 us with the one-tap 64 x 128 tiles, although the one-tap tiles
-// re-read dy per tap (PMC: 2.6x the algorithmic HBM bytes): the kernel is bound by its LDS-DMA fill
-// rate (~8-9 TB/s of L2/MALL -> LDS), not by HBM
-bool g_wgrad_mt = [] { const char* e = getenv("ES_WGRAD_MT"); return e && e[0] == '1'; }();
+// Tuning constants, each chosen by alternating A/B on whole train steps:
+//   * short-K FWD (<= 8 K-steps, e.g. conv_layers.9): 128 x 64 tiles, two workgroups per CU (201 -> 177 us);
+//   * image-group size 64 of the row order (64 > 16 > 8 on the whole step; 8 for an isolated FWD);
+//   * sub-pixel FWD: class-interleaved tile order (14.45 -> 14.33 ms per step), one 256 x 256 GEMM over
+//     (class, channel) columns when the 4 classes share their geometry;
+//   * 256 x 256 tiles with 32-deep K-steps for FWD / DGRAD with >= 256 output columns;
+//   * persistent short-K DGRAD (conv_persist_kernel: conv_layers.9 387 -> 259 us; as FWD it was slower
+//     with fused statistics, 376 vs 364 us) and the persistent 256 x 256 merged sub-pixel FWD.
+// The switches below are test hooks (es_conv_set_*: the kernel tests compare the paths bitwise).
+constexpr int RING_NG = 64;
+bool g_subpixel_off = false;
+bool g_ring256 = true;
+bool g_persist = true;
+bool g_p256 = true;
 
 }  // namespace
 
@@ -3557,9 +2889,8 @@ extern "C" int es_conv_set_ring(int on) {
 
 extern "C" int es_conv_set_persist(int on) {
   // bit 0: the persistent kernel on / off; bit 1: also for FWD
-  const int old = (g_persist ? 1 : 0) | (g_persist_fwd ? 2 : 0);
+  const int old = g_persist ? 1 : 0;
   g_persist = (on & 1) != 0;
-  g_persist_fwd = (on & 2) != 0;
   return old;
 }
 
@@ -3572,29 +2903,6 @@ extern "C" int es_conv_set_p256(int on) {
 extern "C" int es_conv_set_ring256(int on) {
   const int old = g_ring256;
   g_ring256 = on != 0;
-  return old;
-}
-
-extern "C" int es_conv_set_wgrad_mt(int on) {
-  const int old = g_wgrad_mt;
-  g_wgrad_mt = on != 0;
-  return old;
-}
-
-namespace {
-// fp32 ring DGRAD + BatchNorm-backward reduction in the staged epilogue: opt-in (measured slower)
-bool g_ring_bnred = [] { const char* e = getenv("ES_RING_BNRED"); return e && e[0] == '1'; }();
-}  // namespace
-
-extern "C" int es_conv_set_ring_bnred(int on) {
-  const int old = g_ring_bnred;
-  g_ring_bnred = on != 0;
-  return old;
-}
-
-extern "C" int es_conv_set_spb4(int on) {
-  const int old = g_spb4;
-  g_spb4 = on != 0;
   return old;
 }
 
@@ -3641,9 +2949,6 @@ int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
     if (d.K % 256 == 0 && d.C % 128 == 0) ES_WG(256, 128);
     else if (d.K % 128 == 0 && d.C % 256 == 0) ES_WG(128, 256);
     else if (d.K % 128 == 0 && d.C % 128 == 0) ES_WG(128, 128);
-    else if (d.K == 64 && g_wgrad_mt && !sp && d.stride == 1 && d.pad == 0 && d.up_h <= 0 && d.Hu == d.H &&
-             d.Wu == d.W && 256 % d.C == 0 && d.C >= 64 && (d.R * d.S * d.C) % 256 == 0)
-      launch_wgrad_ring<64, 256, false, true>(a, st);        // neutron G conv_layers.9: 2 taps per tile
     else if (d.K == 64 && d.C % 128 == 0) ES_WG(64, 128);   // neutron G conv_layers.9 (128 -> 64)
     else return 0;
 #undef ES_WG
@@ -3679,22 +2984,14 @@ int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
   // image group size of the row order (see conv_ring_kernel).  Measured on the whole train step
   // (tools/gpu_ab.sh, one box): 64 > 16 > 8 for both FWD and DGRAD, although an isolated FWD
   // prefers 8 (less MALL traffic).  ES_RING_NG overrides it (measurement).
-  a.ng = g_ring_ng > 0 ? g_ring_ng : 64;
+  a.ng = RING_NG;
   while (a.ng > 8 && a.ng / 2 >= d.N) a.ng /= 2;   // small batches (per-expert shards): no empty rows
   const int NGI = (d.N + a.ng - 1) / a.ng;
   const int nt128 = (a.Ng + 127) / 128;
   // short-K FWD (<= 8 K-steps, e.g. conv_layers.9: 2x2 taps x 128 channels): 128 x 64 tiles (72 KiB
   // of LDS, two workgroups per CU) so one tile's fill and epilogue overlap another's MFMAs
   // (measured 201 -> 177 us; the same rule on the DGRAD of that conv was slower)
-  bool shortk = g_ring_shortk && mode == MODE_FWD && !sp_weights && a.Kd / 64 <= 8;
-  if constexpr (SPL == 2) {   // A/B knob: 256-row tiles for the short-K split-fp32 FWD
-    static const bool noshort = [] { const char* e = getenv("ES_SPB_NOSHORTK"); return e && e[0] == '1'; }();
-    if (noshort) shortk = false;
-  }
-  if (sp_weights && mode == MODE_FWD && g_sp_shortk > 0) {
-    const int cls_steps = ((d.R + 1) / 2) * ((d.S + 1) / 2) * d.C / 64;   // K-steps of the largest class
-    shortk = cls_steps <= g_sp_shortk;
-  }
+  const bool shortk = mode == MODE_FWD && !sp_weights && a.Kd / 64 <= 8;
   // persistent short-K kernel (conv_persist_kernel): FWD / DGRAD, stride 1, no upsample / sub-pixel,
   // <= 8 K-steps, the whole weight panel (nk x Ng x 128 B) within 64 KiB, dense 16-byte output rows
   {
@@ -3706,7 +3003,7 @@ int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
     const bool geo = d.stride == 1 && !sp_weights && !a.fold && d.hmap == nullptr && d.up_h <= 0 &&
                      d.Hu == d.H && d.Wu == d.W && nchk % 64 == 0 && a.Kd % 64 == 0;
     const int NS = a.Ng <= 64 ? 4 : 3;
-    if (EB == 2 && g_persist && (mode == MODE_DGRAD || g_persist_fwd) && geo && rows16 && (a.Ng == 64 || a.Ng == 128) &&
+    if (EB == 2 && g_persist && mode == MODE_DGRAD && geo && rows16 && (a.Ng == 64 || a.Ng == 128) &&
         nkk >= NS - 1 && nkk <= 8 &&
         nkk * a.Ng <= 512 && a.ng >= 16) {
       const int NB = 128 / a.ng, TT = (PQ + NB - 1) / NB;
@@ -3749,8 +3046,8 @@ int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
       return 1;
     }
   }
-  // >= 3 rounds of 256-row tiles; the planes operand (SPA) exists for the 256 x 128 4-wave kernel only
-  const bool big = !shortk && ((int64_t)NGI * a.ng * PQ / 256 * nt128 >= 768 || a.a_planes);
+  // >= 3 rounds of 256-row tiles
+  const bool big = !shortk && (int64_t)NGI * a.ng * PQ / 256 * nt128 >= 768;
   const int BM = big ? 256 : 128, NB = BM / a.ng;
   int row_tiles = NGI * ((PQ + NB - 1) / NB);
   if (sp_weights) {
@@ -3763,7 +3060,7 @@ int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
               a.Ng % vel == 0 && ((uintptr_t)a.out & 15) == 0;
   a.sp_tpc = 0;
   a.sp_merge = 0;
-  if (sp_weights && mode == MODE_FWD && g_sp_merge && g_ring256 && big && a.vec_out && a.ng >= 16 &&
+  if (sp_weights && mode == MODE_FWD && g_ring256 && big && a.vec_out && a.ng >= 16 &&
       a.Ng % 64 == 0) {
     bool same = true;
     for (int c = 1; c < 4; ++c)
@@ -3774,30 +3071,9 @@ int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
       row_tiles = NGI * a.sp.tile0[1];
     }
   }
-  if (sp_weights && mode == MODE_FWD && g_sp_ilv && !a.sp_merge) {
+  if (sp_weights && mode == MODE_FWD && !a.sp_merge) {
     for (int c = 0; c < 4; ++c) a.sp_tpc = std::max(a.sp_tpc, a.sp.tile0[c + 1] - a.sp.tile0[c]);
     row_tiles = NGI * 4 * a.sp_tpc;
-  }
-  // fp32 DGRAD fused with the BatchNorm-backward reduction over its output (es_conv2d_dgrad_bnred):
-  // one [3][Ng] partial per row tile, written by the staged epilogue (conv_ring_kernel, bnr_fold)
-  a.bnr_part = nullptr;
-  if constexpr (EB == 4) if (g_ring_bnred) {
-    const BnRedRequest& q = g_bnr_req;
-    const int64_t orow = (int64_t)a.os[0];
-    if (mode == MODE_DGRAD && q.part && q.x && q.nm && q.ch && a.vec_out && !a.out_bf16 && a.os[1] == 1 &&
-        a.os[3] == a.Ng && orow % a.Ng == 0 && ((uintptr_t)q.x & 15) == 0 &&
-        (q.ch->act == ES_ACT_LRELU || q.ch->act == ES_ACT_RELU) && (!q.ch->drop.enabled || q.ch->keep) &&
-        (int64_t)row_tiles * 3 * a.Ng <= q.floats) {
-      a.bnr_x = q.x;
-      a.bnr_keep = q.ch->keep;
-      a.bnr_mean = q.nm->mean; a.bnr_invstd = q.nm->invstd; a.bnr_gamma = q.nm->gamma; a.bnr_beta = q.nm->beta;
-      a.bnr_drop = q.ch->drop.enabled != 0;
-      a.bnr_scale = a.bnr_drop ? q.ch->drop.scale : 1.f;
-      a.bnr_dfirst = q.ch->dropout_first;
-      a.bnr_slope = q.ch->act == ES_ACT_LRELU ? q.ch->slope : 0.f;
-      a.bnr_part = q.part;
-      g_bnr_req.chunks = row_tiles;
-    }
   }
   // fused BatchNorm statistics (es_conv2d_fwd_stats): one [3][Ng] partial per row tile
   a.stats_part = nullptr;
@@ -3823,11 +3099,9 @@ int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
     }
     ++g_conv_launches;
     if constexpr (SPL == 2) {   // 256 x 128 tiles (a wave's 128 columns within one class) or 256 x 64
-      static const bool bn64 = [] { const char* e = getenv("ES_SPB_BN64"); return e && e[0] == '1'; }();
-      if (a.Ng % 128 == 0 && !bn64) {
+      if (a.Ng % 128 == 0) {
         dim3 grid(row_tiles, 4 * a.Ng / 128, 1);
-        if ((g_spb4 || a.a_planes) && a.ng == 64) es_spb4_launch(MODE_FWD, true, a, grid, st);
-        else hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 128, true, 64, T, 2>), grid, dim3(RT), 0, st, a);
+        hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 128, true, 64, T, 2>), grid, dim3(RT), 0, st, a);
       } else {
         dim3 grid(row_tiles, 4 * a.Ng / 64, 1);
         hipLaunchKernelGGL((conv_ring_kernel<MODE_FWD, 256, 64, true, 64, T, 2>), grid, dim3(RT), 0, st, a);
@@ -3895,16 +3169,9 @@ int g_f32_chunk = 0;   // test knob (es_conv_set_f32_chunk): at most this many i
 // (Plain functions, not lambdas: hipcc numbers the namespace-scope lambdas of a second anonymous
 // namespace block from #1 again, and the duplicate symbols resolved to the first block's lambdas, so
 // these globals were initialised by other variables' initialisers.)
-int env_int(const char* name, int def) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : def;
-}
-int g_f32_split = env_int("ES_F32_SPLIT", 0);
-int g_wgrad_col = env_int("ES_WGRAD_COL", 1);       // conv_layers.9-shaped WGRAD: 1 col2, 2 col kernel
-int g_wgrad_coop = env_int("ES_WGRAD_COOP", 1);     // wgrad_coop_kernel for 128-row split WGRAD tiles
-int g_wgrad_bn128 = env_int("ES_WGRAD_BN128", 0);   // split WGRAD: 128 x 128 tiles where 128 x 256 fit
-// split-fp32 kernels: static s_setprio 1 for waves 4-7 (ES_SPL_PRIO=0 off; A/B)
-int g_spl_prio = env_int("ES_SPL_PRIO", 1);
+int g_f32_split = 0;
+// split-fp32 kernels: static s_setprio 1 for waves 4-7 (measured against 0: equal within noise, kept)
+constexpr int SPL_PRIO = 1;
 // images per launch: equal chunks (whole 64-image groups where the limit allows) below the limit
 int chunk_images(int64_t img_bytes, int N) {
   int64_t lim = ((1ll << 30) - 1) / std::max<int64_t>(img_bytes, 1);
@@ -3923,16 +3190,12 @@ int es_conv_ring_launch_f32(ConvArgs& a, int mode, hipStream_t st) {
   const es_conv_desc_t& d = a.d;
   if (mode == MODE_WGRAD || d.hmap != nullptr || d.stride > 2 || a.splitk) return d.subpixel ? -1 : 0;
   const int N = d.N;
-  const int ea = a.a_planes ? 6 : 4;   // bytes per value of the gathered operand
+  const int ea = 4;   // bytes per value of the gathered operand
   const int nc = chunk_images(a.as[0] * ea, N);
   const int esz = a.out_bf16 ? 2 : 4;
   const StatsRequest req = g_stats_req;
   int used = 0;
   bool stats_ok = req.part != nullptr;
-  const BnRedRequest breq = g_bnr_req;   // DGRAD + BatchNorm-backward reduction: per-chunk offsets
-  int bused = 0;
-  bool bnr_ok = breq.part != nullptr;
-  es_chain_t bch{};
   for (int n0 = 0; n0 < N; n0 += nc) {
     ConvArgs c = a;
     c.d.N = std::min(nc, N - n0);
@@ -3940,18 +3203,11 @@ int es_conv_ring_launch_f32(ConvArgs& a, int mode, hipStream_t st) {
     c.out = (char*)a.out + (int64_t)n0 * a.os[0] * esz;
     c.M = mode == MODE_FWD ? c.d.N * d.P * d.Q : (a.fold ? c.d.N * d.H * d.W : c.d.N * d.Hu * d.Wu);
     if (req.part) g_stats_req = StatsRequest{req.part + (int64_t)used * 3 * a.Ng, req.floats - (int64_t)used * 3 * a.Ng, 0};
-    if (breq.part) {   // the norm input h and the keep bits share the output's row layout
-      bch = *breq.ch;
-      if (bch.keep) bch.keep += (int64_t)n0 * a.os[0] / 8;
-      g_bnr_req = BnRedRequest{(const char*)breq.x + (int64_t)n0 * a.os[0] * 4, breq.nm, &bch,
-                               breq.part + (int64_t)bused * 3 * a.Ng, breq.floats - (int64_t)bused * 3 * a.Ng, 0};
-    }
-    c.prio = g_spl_prio;
+    c.prio = SPL_PRIO;
     const int rc = g_f32_split == 2 ? ring_fd<float, 2>(c, mode, st)
                    : g_f32_split ? ring_fd<float, 1>(c, mode, st) : ring_fd<float>(c, mode, st);
     if (rc <= 0) {
       g_stats_req = req;
-      g_bnr_req = breq;
       if (n0 == 0) return rc;
       es_set_error("conv f32 ring: chunk %d not eligible", n0);
       return -1;
@@ -3960,13 +3216,8 @@ int es_conv_ring_launch_f32(ConvArgs& a, int mode, hipStream_t st) {
       stats_ok = stats_ok && g_stats_req.chunks > 0;
       used += g_stats_req.chunks;
     }
-    if (breq.part) {
-      bnr_ok = bnr_ok && g_bnr_req.chunks > 0;
-      bused += g_bnr_req.chunks;
-    }
   }
   g_stats_req = StatsRequest{req.part, req.floats, stats_ok ? used : 0};
-  if (breq.part) g_bnr_req = BnRedRequest{breq.x, breq.nm, breq.ch, breq.part, breq.floats, bnr_ok ? bused : 0};
   g_ring_hit = 1 | (g_f32_split ? 2 : 0) | (d.subpixel ? 4 : 0);
   return 1;
 }
@@ -3984,12 +3235,12 @@ static bool wgrad_f32_plan(const es_conv_desc_t& d, const int64_t ys[4], const i
   if (!dense(ys, d.K, d.P, d.Q) || !dense(xs, d.C, d.H, d.W)) return false;
   if (d.K % 64 || d.C % 64) return false;
   p.bm = d.K % 128 == 0 ? 128 : 64;
-  p.bn = d.C % 256 == 0 && p.bm == 128 && !(g_f32_split && g_wgrad_bn128) ? 256 : (d.C % 128 == 0 ? 128 : 64);
+  p.bn = d.C % 256 == 0 && p.bm == 128 ? 256 : (d.C % 128 == 0 ? 128 : 64);
   // split-fp32 with 64 output channels: 64 x 512 tiles (8 waves of 64 x 64, the per-wave shape of the
   // 128 x 256 tiles; 64 x 128 tiles make the in-kernel split VALU-bound)
   p.sp = !g_subpixel_off && d.up_h == 2 && d.up_w == 2 && d.stride == 1;
   if (g_f32_split && p.bm == 64 && !p.sp && (d.R * d.S * d.C) % 512 == 0) p.bn = 512;
-  p.col = g_f32_split && g_wgrad_col && !p.sp && d.R == 2 && d.S == 2 && d.stride == 1 && d.Hu == d.H &&
+  p.col = g_f32_split && !p.sp && d.R == 2 && d.S == 2 && d.stride == 1 && d.Hu == d.H &&
           d.Wu == d.W && d.C == 128 && d.K == 64;
   p.spg = SubPixel{};
   int npix = d.P * d.Q, taps = d.R * d.S;
@@ -4029,7 +3280,7 @@ int es_wgrad_f32_ring(const es_conv_desc_t& d, const void* dy, const int64_t ys[
     const int n0 = ch * p.nc;
     ConvArgs a{};
     a.d = d;
-    a.prio = g_spl_prio;
+    a.prio = SPL_PRIO;
     a.d.N = std::min(p.nc, d.N - n0);
     a.a_src = (const char*)dy + (int64_t)n0 * ys[0] * 4;
     a.b_src = (const char*)x + (int64_t)n0 * xs[0] * 4;
@@ -4045,11 +3296,10 @@ int es_wgrad_f32_ring(const es_conv_desc_t& d, const void* dy, const int64_t ys[
     dim3 grid(d.K / p.bm, p.ngt / p.bn, p.sc);
     if (p.col) {
       ++g_conv_launches;
-      if (g_wgrad_col == 2) hipLaunchKernelGGL(wgrad_f32_col_kernel, grid, dim3(RT), 0, st, a, wsc, p.ngt);
-      else hipLaunchKernelGGL(wgrad_f32_col2_kernel, grid, dim3(RT), 0, st, a, wsc, p.ngt);
+      hipLaunchKernelGGL(wgrad_f32_col2_kernel, grid, dim3(RT), 0, st, a, wsc, p.ngt);
       continue;
     }
-    if (g_f32_split && g_wgrad_coop && p.bm == 128) {
+    if (g_f32_split && p.bm == 128) {
       ++g_conv_launches;
 #define ES_WC(BN)                                                                                          \
   do {                                                                                                     \
@@ -4107,4 +3357,3 @@ extern "C" int es_conv_set_f32_split(int on) {
   g_f32_split = on < 0 ? 0 : (on > 2 ? 2 : on);
   return old;
 }
-#endif  // ES_SPB4_TU

@@ -47,23 +47,7 @@ template <> __device__ __forceinline__ void st8<float>(float* p, const float* f)
   ((float4*)p)[1] = make_float4(f[4], f[5], f[6], f[7]);
 }
 
-// normalise-on-load parameters (NolRequest): y = chain(gamma * (h - mean) * invstd + beta, keep), the
-// expressions of norm_fast.hip bn_fwd_fast (bitwise the same y)
-struct NolArgs {
-  const float *mean, *invstd, *gamma, *beta;
-  const uint8_t* keep;              // [n*h*w][C/8] (dropout on)
-  float scale, slope;
-  int drop, dfirst, act;
-};
-__device__ __forceinline__ float nol_chain(const NolArgs& q, float z, bool keep) {
-  auto act = [&](float v) { return q.act == ES_ACT_RELU ? fmaxf(v, 0.f) : (q.act == ES_ACT_LRELU ? lrelu(v, q.slope) : v); };
-  if (!q.drop) return act(z);
-  if (q.dfirst) return act(keep ? z * q.scale : 0.f);
-  return keep ? act(z) * q.scale : 0.f;
-}
-
 struct Thin {
-  NolArgs nl;                      // fwd / wgrad x: normalise-on-load (NOL kernels only)
   es_conv_desc_t d;
   const void* a; int64_t as[4];    // fwd: x;  dgrad / wgrad: dy
   const void* b; int64_t bs[4];    // wgrad: x
@@ -231,26 +215,15 @@ __global__ void __launch_bounds__(NT) c1_wgrad(Thin t) {
 // ============================================================ Cout == 1
 // A pixel is served by LP = C/(VN*CH) lanes (CH 16-byte channel chunks each); 64/LP pixels per wave.
 // fwd: y = bias + sum over taps of <x row chunks, w chunks>, reduced over the LP lanes.
-template <typename T, typename TO, int RS, int CH = 1, bool NOL = false>
+template <typename T, typename TO, int RS, int CH = 1>
 __global__ void __launch_bounds__(NT) k1_fwd(Thin t, int LP) {
   constexpr int VN = V16<T>::N;
-  static_assert(!NOL || VN * CH == 8, "normalise-on-load: 8 channels (one keep byte) per lane");
   const es_conv_desc_t& d = t.d;
   __shared__ float wf[1024];
   for (int i = threadIdx.x; i < RS * d.C; i += NT) wf[i] = to_f(((const T*)t.w)[i]);   // [R][S][C]
   __syncthreads();
   const int PPB = NT / LP;
   const int l = threadIdx.x % LP;
-  float nsc[NOL ? 8 : 1], nsh[NOL ? 8 : 1];
-  if constexpr (NOL) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int c = l * 8 + e;
-      const float sc = (t.nl.gamma ? t.nl.gamma[c] : 1.f) * t.nl.invstd[c];
-      nsc[e] = sc;
-      nsh[e] = (t.nl.beta ? t.nl.beta[c] : 0.f) - t.nl.mean[c] * sc;
-    }
-  }
   // block-uniform grid-stride loop (the weights are staged once per block; the LP lanes of a
   // pixel stay in step for the shuffle reduction)
   for (int mb = blockIdx.x * PPB; mb < t.M; mb += gridDim.x * PPB) {
@@ -265,10 +238,6 @@ __global__ void __launch_bounds__(NT) k1_fwd(Thin t, int LP) {
     const int hu = p - d.pad + j / d.S, wu = q - d.pad + j % d.S;
     const bool ok = live && hu >= 0 && hu < d.H && wu >= 0 && wu < d.W;
     const T* px = x + (ok ? hu * t.as[2] + wu * t.as[3] : 0);   // clamped: the taps' loads issue together
-    uint32_t kb = 0xFFu;
-    if constexpr (NOL) {
-      if (t.nl.drop) kb = t.nl.keep[((int64_t)n * d.H * d.W + (ok ? hu * d.W + wu : 0)) * (d.C >> 3) + l];
-    }
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const float* pw = wf + j * d.C + (l * CH + c) * VN;
@@ -278,14 +247,7 @@ __global__ void __launch_bounds__(NT) k1_fwd(Thin t, int LP) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) s += (ok ? v[e] : 0.f) * pw[e];
       } else {
-        float4 v = *(const float4*)(px + c * VN);
-        if constexpr (NOL) {
-          const int e0 = c * 4;
-          v.x = nol_chain(t.nl, v.x * nsc[e0 + 0] + nsh[e0 + 0], (kb >> (e0 + 0)) & 1u);
-          v.y = nol_chain(t.nl, v.y * nsc[e0 + 1] + nsh[e0 + 1], (kb >> (e0 + 1)) & 1u);
-          v.z = nol_chain(t.nl, v.z * nsc[e0 + 2] + nsh[e0 + 2], (kb >> (e0 + 2)) & 1u);
-          v.w = nol_chain(t.nl, v.w * nsc[e0 + 3] + nsh[e0 + 3], (kb >> (e0 + 3)) & 1u);
-        }
+        const float4 v = *(const float4*)(px + c * VN);
         if (ok) s += v.x * pw[0] + v.y * pw[1] + v.z * pw[2] + v.w * pw[3];
       }
     }
@@ -452,23 +414,12 @@ __global__ void __launch_bounds__(NT) k1_dgrad_bnred(Thin t, int LP, ThinBnr b) 
 }
 
 // wgrad: dw[r][s][c] = sum over pixels of dy[pix] * x[pix + (r,s)][c]; lane = CH channel chunks
-template <typename T, int RS, int CH = 1, bool NOL = false>
+template <typename T, int RS, int CH = 1>
 __global__ void __launch_bounds__(NT) k1_wgrad(Thin t, int LP) {
   constexpr int VN = V16<T>::N, VC = VN * CH;
-  static_assert(!NOL || VC == 8, "normalise-on-load: 8 channels (one keep byte) per lane");
   const es_conv_desc_t& d = t.d;
   const int PPB = NT / LP;
   const int l = threadIdx.x % LP;
-  float nsc[NOL ? 8 : 1], nsh[NOL ? 8 : 1];
-  if constexpr (NOL) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int c = l * 8 + e;
-      const float sc = (t.nl.gamma ? t.nl.gamma[c] : 1.f) * t.nl.invstd[c];
-      nsc[e] = sc;
-      nsh[e] = (t.nl.beta ? t.nl.beta[c] : 0.f) - t.nl.mean[c] * sc;
-    }
-  }
   float acc[RS][VC];
 #pragma unroll
   for (int j = 0; j < RS; ++j)
@@ -502,12 +453,6 @@ __global__ void __launch_bounds__(NT) k1_wgrad(Thin t, int LP) {
             const float4 w4 = *(const float4*)(px + c * VN);
             v[u][j][c * 4 + 0] = w4.x; v[u][j][c * 4 + 1] = w4.y; v[u][j][c * 4 + 2] = w4.z; v[u][j][c * 4 + 3] = w4.w;
           }
-        }
-        if constexpr (NOL) {
-          const uint32_t kb = t.nl.drop ? t.nl.keep[((int64_t)n * d.H * d.W + (ok ? hu * d.W + wu : 0)) * (d.C >> 3) + l]
-                                        : 0xFFu;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[u][j][e] = nol_chain(t.nl, v[u][j][e] * nsc[e] + nsh[e], (kb >> e) & 1u);
         }
       }
     }
@@ -625,22 +570,15 @@ bool k1_ok(const es_conv_desc_t* d, int rs, int vn) {
 }
 
 unsigned blocks(int64_t items, int per) { return (unsigned)((items + per - 1) / per); }
-// grid caps of the grid-stride thin kernels (A/B switches; 0 = one block per PPB pixels)
-int env_int(const char* k, int dflt) { const char* e = getenv(k); return e ? atoi(e) : dflt; }
-const int g_k1_grid = env_int("ES_K1_GRID", 2048);
-const int g_thin_wgrid = env_int("ES_THIN_WGRID", 1024);
+// grid caps of the grid-stride thin kernels (re-measured round 4, kept)
+constexpr int K1_GRID = 2048, THIN_WGRID = 1024;
 unsigned capped(unsigned b, int cap) { return cap > 0 ? std::min<unsigned>(b, (unsigned)cap) : b; }
 
 // channel chunks per lane of the Cout == 1 kernels: 1 = one 16-byte chunk per lane (C / VN lanes per
 // pixel); 2 / 4 = fewer lanes per pixel, more loads in flight per lane, fewer shuffle rounds.  Measured
-// on conv_layers.13 at B = 1024 fp32 (tools/gpu_r04p.sh, us, CH = 1 / 2 / 4): fwd 241 / 226 / 414,
-// dgrad 218 / 323 / 586, wgrad 207 / 169 / 197 -> fwd 2 (ES_K1_CH), dgrad 1 (ES_K1_CH_DG), wgrad 2
-// (ES_K1_CH_WG)
-const int g_k1_ch = env_int("ES_K1_CH", 2);
-// thin Cout = 1 dgrad + BatchNorm-backward reduction (k1_dgrad_bnred); ES_THIN_BNRED=0 off (A/B)
-const bool g_thin_bnred = env_int("ES_THIN_BNRED", 1) != 0;
-const int g_k1_ch_dg = env_int("ES_K1_CH_DG", 1);
-const int g_k1_ch_wg = env_int("ES_K1_CH_WG", 2);
+// on conv_layers.13 at B = 1024 fp32 (us, CH = 1 / 2 / 4): fwd 241 / 226 / 414, dgrad 218 / 323 / 586,
+// wgrad 207 / 169 / 197 -> fwd 2, dgrad 1, wgrad 2
+constexpr int K1_CH = 2, K1_CH_DG = 1, K1_CH_WG = 2;
 // CH usable for C / VN chunks (LP = chunks / CH >= 1, a power of two)
 int k1_ch(int chunks, int want) {
   int ch = want == 4 || want == 2 ? want : 1;
@@ -655,24 +593,15 @@ int k1_ch(int chunks, int want) {
   } while (0)
 
 template <typename T, typename TO>
-void launch_fwd(const Thin& t, int rs, int LP, hipStream_t st, bool nol = false) {
+void launch_fwd(const Thin& t, int rs, int LP, hipStream_t st) {
   const es_conv_desc_t& d = t.d;
   if (d.C == 1) {
     const dim3 grid(blocks(t.M, NT / (d.K / (16 / (int)sizeof(TO)))));
     if (rs == 4) hipLaunchKernelGGL((c1_fwd<T, TO, 4>), grid, dim3(NT), 0, st, t);
     else hipLaunchKernelGGL((c1_fwd<T, TO, 9>), grid, dim3(NT), 0, st, t);
   } else {
-    if constexpr (std::is_same<T, float>::value) {
-      if (nol) {   // normalise-on-load: 8 channels (2 chunks) per lane
-        const int lp = LP / 2;
-        const dim3 grid(capped(blocks(t.M, NT / lp), g_k1_grid));
-        if (rs == 4) hipLaunchKernelGGL((k1_fwd<T, TO, 4, 2, true>), grid, dim3(NT), 0, st, t, lp);
-        else hipLaunchKernelGGL((k1_fwd<T, TO, 9, 2, true>), grid, dim3(NT), 0, st, t, lp);
-        return;
-      }
-    }
-    const int ch = k1_ch(LP, g_k1_ch), lp = LP / ch;
-    const dim3 grid(capped(blocks(t.M, NT / lp), g_k1_grid));
+    const int ch = k1_ch(LP, K1_CH), lp = LP / ch;
+    const dim3 grid(capped(blocks(t.M, NT / lp), K1_GRID));
     ES_K1_CH_DISPATCH(ch, {
       if (rs == 4) hipLaunchKernelGGL((k1_fwd<T, TO, 4, CH>), grid, dim3(NT), 0, st, t, lp);
       else hipLaunchKernelGGL((k1_fwd<T, TO, 9, CH>), grid, dim3(NT), 0, st, t, lp);
@@ -688,8 +617,8 @@ void launch_dgrad(const Thin& t, int rs, int LP, hipStream_t st) {
     if (rs == 4) hipLaunchKernelGGL((c1_dgrad<T, TO, 4>), grid, dim3(NT), 0, st, t);
     else hipLaunchKernelGGL((c1_dgrad<T, TO, 9>), grid, dim3(NT), 0, st, t);
   } else {
-    const int ch = k1_ch(LP, g_k1_ch_dg), lp = LP / ch;
-    const dim3 grid(capped(blocks(t.M, NT / lp), g_k1_grid));
+    const int ch = k1_ch(LP, K1_CH_DG), lp = LP / ch;
+    const dim3 grid(capped(blocks(t.M, NT / lp), K1_GRID));
     ES_K1_CH_DISPATCH(ch, {
       if (rs == 4) hipLaunchKernelGGL((k1_dgrad<T, TO, 4, CH>), grid, dim3(NT), 0, st, t, lp);
       else hipLaunchKernelGGL((k1_dgrad<T, TO, 9, CH>), grid, dim3(NT), 0, st, t, lp);
@@ -698,12 +627,12 @@ void launch_dgrad(const Thin& t, int rs, int LP, hipStream_t st) {
 }
 
 template <typename T>
-void launch_wgrad(const Thin& t, int rs, int LP, hipStream_t st, bool nol = false) {
+void launch_wgrad(const Thin& t, int rs, int LP, hipStream_t st) {
   const es_conv_desc_t& d = t.d;
-  const int ch = nol ? 2 : (d.C == 1 ? 1 : k1_ch(LP, g_k1_ch_wg)), lp = d.C == 1 ? LP : LP / ch;
+  const int ch = d.C == 1 ? 1 : k1_ch(LP, K1_CH_WG), lp = d.C == 1 ? LP : LP / ch;
   // ~4 blocks per CU, each reducing a strided slice of the pixels
   const int per = d.C == 1 ? NT / (d.K / 8) : NT / lp;
-  dim3 grid(capped(blocks(t.M, per), g_thin_wgrid));
+  dim3 grid(capped(blocks(t.M, per), THIN_WGRID));
   if (t.det) {   // deterministic mode: one partial slot per block within the caller's workspace
     const int64_t slot = (int64_t)d.K * rs * d.C;
     grid.x = (unsigned)std::max<int64_t>(1, std::min<int64_t>(grid.x, g_det_req.floats / slot));
@@ -712,11 +641,6 @@ void launch_wgrad(const Thin& t, int rs, int LP, hipStream_t st, bool nol = fals
   if (d.C == 1) {
     if (rs == 4) hipLaunchKernelGGL((c1_wgrad<T, 4>), grid, dim3(NT), 0, st, t);
     else hipLaunchKernelGGL((c1_wgrad<T, 9>), grid, dim3(NT), 0, st, t);
-  } else if (nol) {
-    if constexpr (std::is_same<T, float>::value) {
-      if (rs == 4) hipLaunchKernelGGL((k1_wgrad<T, 4, 2, true>), grid, dim3(NT), 0, st, t, lp);
-      else hipLaunchKernelGGL((k1_wgrad<T, 9, 2, true>), grid, dim3(NT), 0, st, t, lp);
-    }
   } else {
     ES_K1_CH_DISPATCH(ch, {
       if (rs == 4) hipLaunchKernelGGL((k1_wgrad<T, 4, CH>), grid, dim3(NT), 0, st, t, lp);
@@ -739,25 +663,6 @@ void small_dispatch(int K, F&& f) {
   else f(std::integral_constant<int, 16>{});
 }
 
-// normalise-on-load request for a thin fp32 Cout = 1 fwd / wgrad over a dense NHWC x (8-channel lanes);
-// returns true (and fills t.nl, marks the request used) when it applies
-bool take_nol(Thin& t, const es_conv_desc_t* d, es_dtype_t dt, const int64_t xs[4], int LP, bool k1) {
-  NolRequest& q = g_nol_req;
-  if (!q.on) return false;
-  if (!k1 || dt != ES_F32 || LP % 2 || d->C % 8 || xs[1] != 1 || xs[3] != d->C || xs[2] != (int64_t)d->W * d->C ||
-      xs[0] != (int64_t)d->H * d->W * d->C || q.nm.kind != ES_NORM_BN || (q.ch.drop.enabled && !q.ch.keep))
-    return false;
-  t.nl.mean = q.nm.mean; t.nl.invstd = q.nm.invstd; t.nl.gamma = q.nm.gamma; t.nl.beta = q.nm.beta;
-  t.nl.keep = q.ch.keep;
-  t.nl.drop = q.ch.drop.enabled != 0;
-  t.nl.scale = t.nl.drop ? q.ch.drop.scale : 1.f;
-  t.nl.slope = q.ch.slope;
-  t.nl.dfirst = q.ch.dropout_first;
-  t.nl.act = q.ch.act;
-  q.used = 1;
-  return true;
-}
-
 // ------------------------------------------------------------------------------- entry points
 // Each returns 1 if it launched (caller checks the launch), 0 if the shape is not a thin conv.
 int es_thin_conv_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x, const int64_t xs[4], const void* wk,
@@ -765,7 +670,6 @@ int es_thin_conv_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x, cons
   const int rs = d->R * d->S, vn = dt == ES_BF16 ? 8 : 4;
   const bool c1 = c1_ok(d, rs) && ys[1] == 1 && aligned(ys, 8);
   const bool k1 = k1_ok(d, rs, vn) && xs[1] == 1 && xs[3] == d->C && aligned(xs, vn);
-  if (g_nol_req.on && !k1) return 0;   // normalise-on-load: the Cout = 1 kernels only
   if (!c1 && !k1 && small_ok(d, dt) && ydt == ES_F32 && xs[1] == 1 && aligned(xs, 4) && ys[1] == 1 &&
       aligned(ys, 4)) {
     Thin t{};
@@ -787,12 +691,10 @@ int es_thin_conv_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x, cons
   for (int i = 0; i < 4; ++i) { t.as[i] = xs[i]; t.os[i] = ys[i]; }
   t.M = d->N * d->P * d->Q;
   const int LP = k1 ? d->C / vn : 1;
-  const bool nol = take_nol(t, d, dt, xs, LP, k1);
-  if (g_nol_req.on && !nol) return 0;   // (the caller reports the request it could not honour)
   if (dt == ES_BF16) {
     if (ydt == ES_BF16) launch_fwd<bf16, bf16>(t, rs, LP, st); else launch_fwd<bf16, float>(t, rs, LP, st);
   } else {
-    if (ydt == ES_BF16) launch_fwd<float, bf16>(t, rs, LP, st, nol); else launch_fwd<float, float>(t, rs, LP, st, nol);
+    if (ydt == ES_BF16) launch_fwd<float, bf16>(t, rs, LP, st); else launch_fwd<float, float>(t, rs, LP, st);
   }
   return 1;
 }
@@ -811,12 +713,12 @@ int es_thin_conv_dgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, c
   const int LP = k1 ? d->C / vn : 1;
   const BnRedRequest& q = g_bnr_req;
   const int lp8 = d->C / 8;   // the fused kernel's lanes per pixel: 8 channels per lane in both dtypes
-  if (k1 && q.part && q.x && q.nm && q.ch && dt == dxdt && g_thin_bnred && beta == 0.f && (rs == 4 || rs == 9) &&
+  if (k1 && q.part && q.x && q.nm && q.ch && dt == dxdt && beta == 0.f && (rs == 4 || rs == 9) &&
       pow2(lp8) && lp8 <= 64 && d->C % 8 == 0 &&
       dxs[3] == d->C && dxs[2] == (int64_t)d->W * d->C && dxs[0] == (int64_t)d->H * d->W * d->C &&
       ((uintptr_t)q.x & 15) == 0 && (q.ch->act == ES_ACT_LRELU || q.ch->act == ES_ACT_RELU) &&
       (!q.ch->drop.enabled || q.ch->keep)) {
-    const dim3 grid(capped(blocks(t.M, NT / lp8), g_k1_grid));
+    const dim3 grid(capped(blocks(t.M, NT / lp8), K1_GRID));
     if ((int64_t)grid.x * 3 * d->C <= q.floats) {
       ThinBnr b{};
       b.x = q.x; b.keep = q.ch->keep;
@@ -857,9 +759,7 @@ int es_thin_conv_wgrad(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, c
   t.M = d->N * d->P * d->Q;
   t.det = g_det_req.ws != nullptr && (float*)dw == g_det_req.ws;
   const int LP = k1 ? d->C / vn : 1;
-  const bool nol = take_nol(t, d, dt, xs, LP, k1);
-  if (g_nol_req.on && !nol) return 0;
   if (dt == ES_BF16) launch_wgrad<bf16>(t, rs, LP, st);
-  else launch_wgrad<float>(t, rs, LP, st, nol);
+  else launch_wgrad<float>(t, rs, LP, st);
   return 1;
 }

@@ -19,11 +19,11 @@
 
 // fast path for dense channels-last BatchNorm / GroupNorm (norm_fast.hip); G = 0 means BN
 bool es_fast_dense_nhwc(const es_view_t* v);
-void es_fast_keep_bits(const es_view_t* v, const es_chain_t* ch, hipStream_t st);
 int64_t es_fast_part_floats(const es_view_t* v, int G);
 int es_fast_norm_stats(const es_view_t* v, int G, es_dtype_t dt, const void* xp, float* part, hipStream_t st);
 void es_fast_norm_fwd(const es_view_t* v, int G, es_dtype_t dt, const void* xp, void* yp, const es_norm_t* nm,
                       const es_chain_t* ch, hipStream_t st);
+void es_fast_keep_bits(const es_view_t* v, const es_chain_t* ch, hipStream_t st);
 int es_fast_norm_bwd_reduce(const es_view_t* v, int G, es_dtype_t dt, const void* xp, const void* dyp,
                             const es_norm_t* nm, const es_chain_t* ch, float* part, hipStream_t st);
 int es_fast_norm_bwd_apply(const es_view_t* v, int G, es_dtype_t dt, const void* xp, const void* dyp, void* dxp,
@@ -451,12 +451,11 @@ __global__ void __launch_bounds__(256) sums_finalize_kernel(const float* part, i
 
 // finalize dispatch: a block per channel while the chunks dominate, a thread per channel otherwise
 bool fin_block(int chunks, int C) { return chunks > 32 && C < 4096; }
-// two-level in-place merge of many chunk partials (ES_MERGE2=0: the block-per-channel kernel, A/B)
-bool g_merge2 = [] { const char* e = getenv("ES_MERGE2"); return !(e && e[0] == '0'); }();
+// two-level in-place merge of many chunk partials (measured faster than the block-per-channel kernel)
 
 void launch_bn_finalize(hipStream_t st, const float* part, int chunks, int C, float eps, float* mean, float* invstd,
                         float* rmean, float* rvar, float mom) {
-  if (chunks >= 1024 && C <= 256 && g_merge2) {   // (consumes the partials: they are merged in place)
+  if (chunks >= 1024 && C <= 256) {   // (consumes the partials: they are merged in place)
     const int G = std::min(256, chunks / 16), R = (chunks + G - 1) / G;
     const int Gr = (chunks + R - 1) / R;
     hipLaunchKernelGGL(bn_merge_l1_kernel, dim3(Gr), dim3(256), 0, st, const_cast<float*>(part), chunks, C, R);
@@ -777,17 +776,6 @@ extern "C" int es_norm_stats_finalize(const float* part, int chunks, int C, floa
   ES_CHECK_ARG(part && chunks > 0 && C > 0, "norm_stats_finalize: bad arguments");
   hipStream_t st = (hipStream_t)stream;
   launch_bn_finalize(st, part, chunks, C, eps, mean, invstd, running_mean, running_var, momentum);
-  ES_CHECK_LAUNCH();
-  return ES_OK;
-}
-
-// the dropout keep bits es_norm_act_fwd would store for x's shape (the forward of a norm whose
-// apply runs in the consuming conv: es_conv_norm_on_load)
-extern "C" int es_norm_keep_bits(const es_view_t* x, const es_chain_t* ch, es_stream_t stream) {
-  ES_CHECK_ARG(x && ch, "es_norm_keep_bits: null argument");
-  if (!ch->drop.enabled) return ES_OK;
-  ES_CHECK_ARG(ch->keep && x->c % 8 == 0, "es_norm_keep_bits: keep buffer and C %% 8 == 0 required");
-  es_fast_keep_bits(x, ch, (hipStream_t)stream);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }

@@ -80,7 +80,6 @@ _SIGS = {
     "es_conv_set_ring256": (C.c_int, [C.c_int]),
     "es_conv_set_persist": (C.c_int, [C.c_int]),
     "es_conv_set_p256": (C.c_int, [C.c_int]),
-    "es_conv_set_wgrad_mt": (C.c_int, [C.c_int]),
     "es_conv_subpixel_ok": (C.c_int, [P, C.c_int]),
     "es_subpixel_taps": (C.c_int, [C.c_int, C.c_int]),
     "es_conv2d_fwd": (C.c_int, [P, C.c_int, P, P, P, P, P, C.c_int, P, P]),
@@ -98,15 +97,8 @@ _SIGS = {
     "es_conv_set_f32_split": (C.c_int, [C.c_int]),
     "es_weight_planes_offset": (C.c_int64, [C.c_int64]),
     "es_pack_weight_planes": (C.c_int, [P, C.c_int64, P, P]),
-    "es_split_planes": (C.c_int, [P, C.c_int64, C.c_int, P, P]),
-    "es_conv2d_fwd_planes": (C.c_int, [P, P, P, P, P, P, C.c_int, P, P, I64, P, P]),
-    "es_conv2d_dgrad_planes": (C.c_int, [P, P, P, P, P, C.c_int, P, P]),
     "es_conv_launch_count": (C.c_int64, []),
     "es_conv_exec_flops": (C.c_int, [C.POINTER(C.c_double), C.c_int]),
-    "es_conv_set_spb4": (C.c_int, [C.c_int]),
-    "es_conv_set_ring_bnred": (C.c_int, [C.c_int]),
-    "es_conv_norm_on_load": (C.c_int, [P, P]),
-    "es_norm_keep_bits": (C.c_int, [P, P, P]),
     "es_pack_conv_weight": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, C.c_int, P]),
     "es_unpack_conv_grad": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, C.c_float, P]),
     "es_unpack_conv_grad_clear": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_float, P]),

@@ -20,12 +20,11 @@ from . import hip
 class Act:
     """Logical (N, C, H, W) tensor over a flat device buffer with explicit element strides."""
 
-    __slots__ = ("t", "dims", "strides", "bn_part", "bn_sums", "nol")
+    __slots__ = ("t", "dims", "strides", "bn_part", "bn_sums")
 
     def __init__(self, t: torch.Tensor, dims, strides):
         self.bn_part = None       # (partials, chunks) of fused BatchNorm statistics (ConvOp.fwd)
         self.bn_sums = None       # (partials, chunks, norm) of a fused BatchNorm-backward reduction (ConvOp.dgrad)
-        self.nol = None           # (norm struct, chain): t holds the PRE-norm h, the conv applies the norm on load
         self.t = t
         self.dims = tuple(int(d) for d in dims)
         self.strides = tuple(int(s) for s in strides)
@@ -171,9 +170,6 @@ def ws(nbytes, device):
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
 
 
-# BatchNorm-backward reduction fused into the producing dgrad (ConvOp.dgrad bn_reduce); A/B switch
-_BNRED = os.environ.get("ES_BNRED", "1") != "0"
-
 # Deterministic reductions (the fp32 parity mode): weight gradients through es_conv2d_wgrad_det (split
 # partials + one ordered reduce, no float atomics), no split-K atomics in the fp32 GEMMs, ordered
 # conv-bias sums.  Two runs of the same step are then bitwise identical, as the reference's are.
@@ -194,14 +190,12 @@ def deterministic() -> bool:
 
 # fp32 MFMA arithmetic of the ring convolutions: exact fp32 (v_mfma_f32_16x16x4_f32) or split-fp32
 # (three bf16 planes per operand, six plane products on v_mfma_f32_16x16x32_bf16; es_conv_set_f32_split).
-# Level 2 (default when on): the packed weights carry their planes (es_pack_weight_planes), so the
-# FWD / DGRAD kernels split only the activations; ES_F32_SPLIT_LEVEL=1 splits both in the kernel.
-# The level the C side uses is the single source of truth: es_conv_set_f32_split clamps to {0, 1, 2}
-# and ES_F32_SPLIT may set it before any call from here, so the Python mirror is read back from C
-# (packing the weight planes must follow the level the kernels actually run).
+# Level 2 (the level used when on): the packed weights carry their planes (es_pack_weight_planes), so the
+# FWD / DGRAD kernels split only the activations (level 1, both split in the kernel, stays a test hook).
+# The level the C side uses is the single source of truth (es_conv_set_f32_split clamps to {0, 1, 2}),
+# so the Python mirror is read back from C (packing the weight planes must follow the level the kernels run).
 _F32_SPLIT = None
-_SPLIT_LEVEL = min(max(int(os.environ.get("ES_F32_SPLIT_LEVEL", "2")), 1), 2)
-_LIN_PIX = os.environ.get("ES_LIN_PIX", "1") != "0"                  # A/B switch (ConvOp._pixel_view)
+_SPLIT_LEVEL = 2
 
 
 def set_f32_split(on: bool):
@@ -274,26 +268,6 @@ class Upsample:
 
 
 # ------------------------------------------------------------------------------ conv / linear
-class _norm_on_load:
-    """Context of one conv call on an Act whose ``nol`` is set (NormOp.fwd_deferred): the C library
-    applies that BatchNorm + dropout + activation to the operand as it loads it
-    (es_conv_norm_on_load; the conv call fails if its path cannot)."""
-
-    def __init__(self, x):
-        self.nol = getattr(x, "nol", None)
-
-    def __enter__(self):
-        if self.nol is not None:
-            nm, chain = self.nol
-            hip.call("es_conv_norm_on_load", C.byref(nm), C.byref(chain))
-        return self
-
-    def __exit__(self, *exc):
-        if self.nol is not None:
-            hip.call("es_conv_norm_on_load", None, None)
-        return False
-
-
 class ConvOp:
     """nn.Conv2d / nn.Linear on the implicit-GEMM kernels.
 
@@ -313,7 +287,7 @@ class ConvOp:
         # the resized input is materialised (es_upsample_fwd) and the conv runs as a plain conv on it,
         # on the ring kernels (the gather-map conv only runs on the generic register-staged kernels)
         self._plain = None
-        if upsample is not None and upsample.factor is None and os.environ.get("ES_RESIZE_MAT", "1") != "0":
+        if upsample is not None and upsample.factor is None:
             self._plain = ConvOp(weight, bias, stride=stride, pad=pad, upsample=None)
         w = weight
         self.K = w.shape[0]
@@ -402,14 +376,13 @@ class ConvOp:
         return bool(hip.lib().es_conv_subpixel_ok(C.byref(d), hip.dt_of_dtype(dtype)))
 
     def fwd(self, x: Act, out_dtype=None, inv_scale=None, out: Act = None, with_bias=True,
-            bn_stats=False, planes=None) -> Act:
+            bn_stats=False) -> Act:
         """bn_stats: also ask for the BatchNorm partials of the output (es_conv2d_fwd_stats); when
         the kernel provides them, out.bn_part = (part, chunks) and NormOp.stats merges those instead
-        of re-reading the output.  planes: x's es_split_planes image (fp32 split-fp32 sub-pixel convs:
-        the kernel reads it instead of splitting x; es_conv2d_fwd_planes)."""
-        if planes is None and self._resized(x):
+        of re-reading the output."""
+        if self._resized(x):
             return self._plain_op().fwd(self._resize(x), out_dtype, inv_scale, out, with_bias, bn_stats)
-        xv = self._pixel_view(x) if planes is None and out is None else None
+        xv = self._pixel_view(x) if out is None else None
         if xv is not None:
             o = self.fwd(xv, out_dtype, inv_scale, None, with_bias, bn_stats)
             res = Act(o.t, (x.dims[0], self.K, 1, 1), (self.K, 1, 1, 1))
@@ -425,20 +398,8 @@ class ConvOp:
         if out is None:
             out = Act.nhwc(d.N, d.K, d.P, d.Q, out_dtype or cdt, x.t.device)
         bias = self.bias if (with_bias and self.bias is not None) else None
-        with _probed(self.label and self.label + ".fwd"), _norm_on_load(x):
-            if planes is not None:
-                assert d.subpixel == 1 and cdt == torch.float32, "planes: fp32 sub-pixel convs only"
-                part, floats, chunks = None, 0, C.c_int(0)
-                if bn_stats:
-                    tiles = ((d.N + 7) // 8) * (d.P * d.Q // 16 + 8) + ((d.N + 63) // 64) * (d.P * d.Q // 2 + 8)
-                    floats = tiles * 3 * d.K
-                    part = torch.empty(floats, dtype=torch.float32, device=x.t.device)
-                hip.call("es_conv2d_fwd_planes", C.byref(d), hip.ptr(planes), hip.strides4(x.strides), hip.ptr(wk),
-                         hip.ptr(bias), out.ptr, out.dt, hip.strides4(out.strides), hip.ptr(part), floats,
-                         C.byref(chunks), hip.stream_ptr())
-                if bn_stats and chunks.value > 0:
-                    out.bn_part = (part, chunks.value)
-            elif bn_stats:
+        with _probed(self.label and self.label + ".fwd"):
+            if bn_stats:
                 # >= the ring's row tiles for every image-group size it may pick (8..64)
                 tiles = ((d.N + 7) // 8) * (d.P * d.Q // 16 + 8) + ((d.N + 63) // 64) * (d.P * d.Q // 2 + 8)
                 floats = tiles * 3 * d.K
@@ -467,8 +428,8 @@ class ConvOp:
         pixel), so a linear's 1-pixel images would leave 3/4 of every 256-row tile empty (bf16) or miss
         the fp32 ring (>= 16 output pixels per image) and fall to the register-staged fp32-MFMA GEMM;
         the generators' fc2 (256 -> 21632 neutron, neutron/generator.py:17) is the case.  None when the
-        layout does not apply (ES_LIN_PIX=0 disables it)."""
-        if not _LIN_PIX or self.R != 1 or self.S != 1 or self.up is not None or self.stride != 1 or self.pad != 0:
+        layout does not apply."""
+        if self.R != 1 or self.S != 1 or self.up is not None or self.stride != 1 or self.pad != 0:
             return None
         N, Cc, H, W = x.dims
         dt = x.t.dtype
@@ -485,7 +446,7 @@ class ConvOp:
                 and out.t.dtype == torch.float32 and ng <= 4096)
 
     def dgrad(self, dy: Act, x: Act, dx_dtype=None, inv_scale=None, dx: Act = None, beta=0.0,
-              bn_reduce=None, planes=None) -> Act:
+              bn_reduce=None) -> Act:
         """Gradient w.r.t. the conv input x (folded through the upsample when present).
 
         bn_reduce = (norm, h, stats, chain): x = chain(norm(h)) is a BatchNorm + dropout + activation
@@ -504,15 +465,11 @@ class ConvOp:
         if self.up is None or self.up.factor is not None:   # no upsample, or folded in the GEMM
             if dx is None:
                 dx = Act.nhwc(N, Cc, H, W, ddt, dy.t.device)
-            fuse = (bn_reduce is not None and float(beta) == 0.0 and _BNRED and _NORM_SYNC is None
+            fuse = (bn_reduce is not None and float(beta) == 0.0 and _NORM_SYNC is None
                     and bn_reduce[0].kind == hip.NORM_BN and bn_reduce[1].t.dtype == ddt == cdt
                     and bn_reduce[1].dims == dx.dims and tuple(bn_reduce[1].strides) == tuple(dx.strides))
             with _probed(self.label and self.label + ".dgrad"):
-              if planes is not None:   # dy's es_split_planes image (es_conv2d_dgrad_planes)
-                  assert d.subpixel == 1 and cdt == torch.float32 and float(beta) == 0.0, "planes: fp32 sub-pixel"
-                  hip.call("es_conv2d_dgrad_planes", C.byref(d), hip.ptr(planes), hip.strides4(dy.strides),
-                           hip.ptr(wd), dx.ptr, dx.dt, hip.strides4(dx.strides), hip.stream_ptr())
-              elif fuse:
+              if fuse:
                   norm, h, stats, chain = bn_reduce
                   nm = norm.norm_struct(*stats)
                   # >= the thin dgrad's blocks (<= 2048) / persistent workgroups / fp32 ring row tiles (one
@@ -563,7 +520,7 @@ class ConvOp:
             ys, xs = hip.strides4(dy.strides), hip.strides4(x.strides)
             nb = int(hip.lib().es_conv2d_wgrad_det_ws_bytes(C.byref(d), dy.dt, ys, xs))
             wsb = ws(nb, dev)
-            with _probed(self.label and self.label + ".wgrad"), _norm_on_load(x):
+            with _probed(self.label and self.label + ".wgrad"):
                 hip.call("es_conv2d_wgrad_det", C.byref(d), dy.dt, dy.ptr, ys, x.ptr, xs, hip.ptr(dw_out),
                          float(beta), hip.ptr(wsb), nb, hip.stream_ptr())
             if db_out is not None:
@@ -573,40 +530,25 @@ class ConvOp:
         #  * packed == torch layout (1x1 / linear, or Cin = 1) and beta = 1: accumulate straight
         #    into the parameter's gradient (no scratch, no unpack);
         #  * otherwise a persistent packed scratch that the unpack leaves zeroed (no zero fill).
-        legacy = os.environ.get("ES_WGRAD_SCRATCH", "1") == "0"         # A/B switch
-        direct = (not legacy and dw_out is not None and float(beta) == 1.0 and (self.R * self.S == 1 or self.C == 1)
+        direct = (dw_out is not None and float(beta) == 1.0 and (self.R * self.S == 1 or self.C == 1)
                   and dw_out.is_contiguous() and dw_out.dtype == torch.float32)
         if direct:
             dwk = dw_out
-        elif dw_out is not None and not legacy:
+        elif dw_out is not None:
             dwk = getattr(self, "_dwk", None)
             if dwk is None or dwk.device != dev:
                 dwk = self._dwk = torch.zeros(self.weight.numel(), dtype=torch.float32, device=dev)
         else:
             dwk = torch.zeros(self.weight.numel(), dtype=torch.float32, device=dev)
-        with _probed(self.label and self.label + ".wgrad"), _norm_on_load(x):
+        with _probed(self.label and self.label + ".wgrad"):
           hip.call("es_conv2d_wgrad", C.byref(d), dy.dt, dy.ptr, hip.strides4(dy.strides), x.ptr,
                  hip.strides4(x.strides), hip.ptr(dwk), hip.stream_ptr())
-        if dw_out is not None and legacy:
-            hip.call("es_unpack_conv_grad", hip.ptr(dwk), self.K, self.C, self.R, self.S, None,
-                     hip.ptr(dw_out), float(beta), hip.stream_ptr())
-        elif dw_out is not None and not direct:
+        if dw_out is not None and not direct:
             hip.call("es_unpack_conv_grad_clear", hip.ptr(dwk), self.K, self.C, self.R, self.S,
                      hip.ptr(dw_out), float(beta), hip.stream_ptr())
         if db_out is not None:
             channel_sum(dy, db_out, beta)
         return dwk
-
-
-def split_planes(x: Act, out: torch.Tensor = None) -> torch.Tensor:
-    """x's split-fp32 planes image (es_split_planes): dense NHWC fp32, C % 32 == 0 -> bf16 tensor of
-    [N*H*W][C/32][3][32] values (6 bytes per value)."""
-    N, Cc, H, W = x.dims
-    assert x.t.dtype == torch.float32 and Cc % 32 == 0 and tuple(x.strides) == (H * W * Cc, 1, W * Cc, Cc)
-    if out is None:
-        out = torch.empty(N * H * W * Cc * 3, dtype=torch.bfloat16, device=x.t.device)
-    hip.call("es_split_planes", x.ptr, N * H * W, Cc, hip.ptr(out), hip.stream_ptr())
-    return out
 
 
 def channel_sum(x: Act, out: torch.Tensor, beta=1.0):
@@ -625,8 +567,7 @@ _NBT_PENDING = None
 class defer_num_batches:
     def __enter__(self):
         global _NBT_PENDING
-        on = os.environ.get("ES_DEFER_NBT", "1") != "0"                 # A/B switch
-        self.prev, _NBT_PENDING = _NBT_PENDING, ({} if on else None)
+        self.prev, _NBT_PENDING = _NBT_PENDING, {}
         return self
 
     def __exit__(self, exc_type, exc, tb):
@@ -752,18 +693,6 @@ class NormOp:
                  C.byref(addend.view) if addend is not None else None,
                  addend.dt if addend is not None else 0, addend.ptr if addend is not None else None,
                  x.ptr, C.byref(y.view), y.dt, y.ptr, hip.stream_ptr())
-        return y, (mean, invstd)
-
-    def fwd_deferred(self, x: Act, chain: hip.Chain, train=True):
-        """The forward of a BatchNorm whose apply runs in the consuming conv (es_conv_norm_on_load):
-        statistics and the dropout keep bits only.  Returns (a view of x carrying ``nol``, stats); a
-        conv given that view normalises on load, so y is never written."""
-        assert self.kind == hip.NORM_BN
-        mean, invstd = self.stats(x, train)
-        nm = self.norm_struct(mean, invstd)
-        hip.call("es_norm_keep_bits", C.byref(x.view), C.byref(chain), hip.stream_ptr())
-        y = Act(x.t, x.dims, x.strides)
-        y.nol = (nm, chain)
         return y, (mean, invstd)
 
     def bwd(self, x: Act, stats, chain: hip.Chain, dy: Act, dx_dtype=None, act_ref: Act = None,
@@ -904,7 +833,7 @@ class SpectralNorm:
         layer); larger ones (discriminator fc1) run the multi-block mat-vecs."""
         out = [None] * len(sns)
         small = [i for i, sn in enumerate(sns) if sn.h * sn.wd < 16384]
-        if len(small) < 2 or os.environ.get("ES_SN_BATCH", "1") == "0":
+        if len(small) < 2:
             small = []
         for i, sn in enumerate(sns):
             if i not in small:
@@ -929,7 +858,7 @@ class SpectralNorm:
     def bwd_many(jobs, beta=1.0):
         """bwd() of several layers, jobs = [(sn, g_sn, sig, dw_orig)]: the small ones share a launch."""
         small = [j for j in jobs if not (j[0].h * j[0].wd >= 16384 and j[0].h + j[0].wd >= 256)]
-        if len(small) < 2 or os.environ.get("ES_SN_BATCH", "1") == "0":
+        if len(small) < 2:
             small = []
         for j in jobs:
             if not any(j is k for k in small):

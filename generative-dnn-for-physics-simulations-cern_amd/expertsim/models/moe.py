@@ -100,9 +100,8 @@ class MoEWrapper(nn.Module):
             m.compute_dtype = low
         for m in self.aux_regs:
             m.compute_dtype = low
-        d_low = low if os.environ.get("ES_D_BF16", "0") == "1" else torch.float32
         for m in self.discriminators:
-            m.compute_dtype = d_low
+            m.compute_dtype = torch.float32
 
     # ---------------------------------------------------------------------------- helpers
     # stream indices of the step's draws: Gumbel 0, expert e's noise_1 / noise_2 1 + 2e / 2 + 2e

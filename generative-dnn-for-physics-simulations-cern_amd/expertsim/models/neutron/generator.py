@@ -17,7 +17,6 @@ Dropout masks come from Philox streams (expertsim/utils/philox.py), layer index 
 """
 from __future__ import annotations
 
-import os
 
 import torch
 from torch import nn
@@ -27,11 +26,6 @@ from ...layers import Act, ConvOp, NormOp, Upsample, act_bwd, act_fwd, copy_act
 from ...utils import philox
 from ..base import ExpertModule, build_tree, get_module
 
-_RING_BNRED = os.environ.get("ES_RING_BNRED", "0") == "1"     # A/B switch
-# fp32, opt-in (ES_NOL=1): conv_layers.10's BatchNorm + Dropout + LeakyReLU applied by conv_layers.13's
-# thin kernels as they load it (NormOp.fwd_deferred, es_conv_norm_on_load), y5 never written.  Measured
-# slower than the apply pass it removes (45.5-45.8 vs 44.9-45.1 ms/step)
-_NOL = os.environ.get("ES_NOL", "0") == "1"
 
 SLOPE = 0.1
 P_DROP = 0.2
@@ -123,10 +117,7 @@ class GeneratorNeutron(ExpertModule):
         h4 = o["c5"].fwd(y3, bn_stats=train)
         y4, s4 = o["bn4"].fwd(h4, ch[3], train=train)
         h5 = o["c9"].fwd(y4, bn_stats=train)
-        if _NOL and cdt == torch.float32:
-            y5, s5 = o["bn5"].fwd_deferred(h5, ch[4], train=train)
-        else:
-            y5, s5 = o["bn5"].fwd(h5, ch[4], train=train)
+        y5, s5 = o["bn5"].fwd(h5, ch[4], train=train)
         h6 = o["c13"].fwd(y5, out_dtype=torch.float32)
         img = act_fwd(h6, hip.chain_struct(hip.ACT_RELU))
         ctx = dict(x0=x0, h1=h1, y1=y1, s1=s1, h2=h2, y2=y2, s2=s2, y2n=y2n, h3=h3, y3=y3, s3=s3,
@@ -157,12 +148,11 @@ class GeneratorNeutron(ExpertModule):
                            dbeta=g("conv_layers.6", "bias"), dsum=g("conv_layers.5", "bias"))
         o["c5"].wgrad(dh4, ctx["y3"], g("conv_layers.5", "weight"), None)
         ready("conv_layers.5.weight")
-        # no fused reduction here by default: the 256 x 256 sub-pixel DGRAD has no registers to spare for
-        # it in bf16 (585 -> 871 us for a 146 us reduce pass), and the split-fp32 ring DGRAD's staged
-        # epilogue fold (ES_RING_BNRED=1, bitwise-tested) costs more than the reduce pass it removes
-        # (B = 1024 c5 DGRAD 3.16 -> 3.62 ms)
-        bnr = (o["bn3"], ctx["h3"], ctx["s3"], ch[2]) if _RING_BNRED else None
-        dy3 = o["c5"].dgrad(dh4, ctx["y3"], bn_reduce=bnr)
+        # no fused reduction here: the 256 x 256 sub-pixel DGRAD has no registers to spare for it in
+        # bf16 (585 -> 871 us for a 146 us reduce pass), and a staged-epilogue fold in the split-fp32
+        # ring DGRAD cost more than the reduce pass it removes (B = 1024 c5 DGRAD 3.16 -> 3.62 ms,
+        # DESIGN.md §4; removed in round 5)
+        dy3 = o["c5"].dgrad(dh4, ctx["y3"])
         dh3 = o["bn3"].bwd(ctx["h3"], ctx["s3"], ch[2], dy3, dgamma=g("conv_layers.1", "weight"),
                            dbeta=g("conv_layers.1", "bias"), dsum=g("conv_layers.0", "bias"))
         o["c0"].wgrad(dh3, ctx["y2n"], g("conv_layers.0", "weight"), None)

@@ -15,7 +15,6 @@ Program:
 from __future__ import annotations
 
 import ctypes as C
-import os
 
 import torch
 from torch import nn
@@ -69,8 +68,8 @@ class SNDiscriminator(ExpertModule):
         return ops
 
     # ------------------------------------------------------------------ fused front (d_front.hip)
-    # conv_layers.0..3 as the per-image fused kernels (ES_NO_DFRONT=1: separate kernels, A/B)
-    fuse_front = os.environ.get("ES_NO_DFRONT") != "1"
+    # conv_layers.0..3 as the per-image fused kernels (tests switch it off to compare)
+    fuse_front = True
 
     def front_fused(self, x: Act) -> bool:
         """SNconv 1->32 + GN + LReLU + pool as es_dfront_*: fp32, even 3x3-conv output grid (the 2x2
@@ -79,9 +78,9 @@ class SNDiscriminator(ExpertModule):
         return (self.fuse_front and x.t.dtype == torch.float32 and Cc == 1 and H >= 4 and W >= 4
                 and (H - 2) % 2 == 0 and (W - 2) % 2 == 0 and H * W <= 2048 and (H - 2) * (W - 2) <= 1792)
 
-    # both conv blocks as one per-image kernel pair (d_front2.hip); ES_NO_DFRONT2=1: block 1 fused,
-    # block 2 on the generic kernels (A/B)
-    fuse_front2 = os.environ.get("ES_NO_DFRONT2") != "1"
+    # both conv blocks as one per-image kernel pair (d_front2.hip); off: block 1 fused, block 2 on the
+    # generic kernels (tests)
+    fuse_front2 = True
 
     def front2_fused(self, x: Act) -> bool:
         N, Cc, H, W = x.dims
@@ -223,9 +222,8 @@ class SNDiscriminator(ExpertModule):
                                                       p1=p1, i1=i1, h2=h2, y2=y2, s2=s2, i2=i2, X=X,
                                                       feat_dims=(B, 16, fh, fw)))
 
-    # the fc tail as one per-16-samples kernel pair (d_mlp.hip); ES_NO_DMLP=1: the layer-by-layer
-    # kernels (A/B)
-    fuse_mlp = os.environ.get("ES_NO_DMLP") != "1"
+    # the fc tail as one per-16-samples kernel pair (d_mlp.hip); off: the layer-by-layer kernels (tests)
+    fuse_mlp = True
 
     def _mlp_params(self, sig):
         m = lambda n: get_module(self, n)

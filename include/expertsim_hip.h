@@ -99,20 +99,14 @@ int es_conv_set_ring(int on);
  * 1 = on (default), 0 = 256 x 128 tiles (same accumulation order: bit-identical results).
  * Returns the previous setting. */
 int es_conv_set_ring256(int on);
-/* Persistent short-K FWD / DGRAD kernel (conv_mfma.hip conv_persist_kernel: generator
- * conv_layers.9 and its dgrad, <= 8 K-steps of 64 channels, 64 or 128 output columns).  on: bit 0
- * enables it (default: for DGRAD), bit 1 also for FWD (default off); 0 = the ring kernel (same
- * accumulation order: bit-identical outputs; the fused BatchNorm partials are per workgroup
- * instead of per row tile).  Returns the previous setting. */
+/* Persistent short-K DGRAD kernel (conv_mfma.hip conv_persist_kernel: generator conv_layers.9's
+ * dgrad, <= 8 K-steps of 64 channels, 64 or 128 output columns): 1 = on (default), 0 = the ring
+ * kernel (same accumulation order: bit-identical outputs).  Returns the previous setting. */
 int es_conv_set_persist(int on);
 /* Persistent 256 x 256 kernel for the merged sub-pixel FWD (conv_mfma.hip conv_p256_kernel:
  * generator conv_layers.0 / .5): 1 = on (default), 0 = the per-tile ring kernel (same accumulation
  * order: bit-identical outputs).  Returns the previous setting. */
 int es_conv_set_p256(int on);
-/* Multi-tap 64 x 256 WGRAD tiles for stride-1, pad-0, 64-output-channel convs (conv_mfma.hip
- * wgrad_ring_kernel MT: generator conv_layers.9 with 2 of its 4 taps per tile): 1 = on, 0 = one-tap
- * 64 x 128 tiles (default; measured equal).  Returns the previous setting. */
-int es_conv_set_wgrad_mt(int on);
 /* Sub-pixel decomposition of stride-1 convs over a x2 nearest upsample (conv_mfma.hip): 1 = on
  * (default; wgrad uses it internally, fwd/dgrad when the caller packs mode 2/3 weights and sets
  * desc->subpixel), 0 = off.  Returns the previous setting. */
@@ -191,36 +185,9 @@ int es_conv_set_f32_split(int on);
  * kernels' fragments.  Same weights as es_pack_conv_weight (neutron generator.py:24,29,33). */
 int64_t es_weight_planes_offset(int64_t n);
 int es_pack_weight_planes(const float* packed, int64_t n, void* base, es_stream_t stream);
-/* Split-fp32 planes of an fp32 activation image [rows][C] (C % 32 == 0): out [rows][C / 32][3][32] bf16,
- * each 32-channel block as the weight planes above (x0 = rne(x), x1 = rne(x - x0), x2 = x - x0 - x1, k
- * permuted as the ring kernels' fragments), 6 bytes per value.  The FWD / DGRAD *_planes entries read
- * their gathered operand from it instead of splitting it in the kernel.  Same values as the fp32
- * activations of neutron generator.py:24,29 (conv_layers.0 / .5 inputs and output gradients). */
-int es_split_planes(const float* x, int64_t rows, int C, void* planes, es_stream_t stream);
-/* es_conv2d_fwd (part == NULL) / es_conv2d_fwd_stats and es_conv2d_dgrad (beta 0) in fp32 whose
- * gathered operand (x, resp. dy) is given as its es_split_planes image (xs / ys: the strides of the
- * fp32 image in values): the split-fp32 kernels then read the planes instead of splitting in the
- * kernel (same products, same order, bitwise the same output).  Sub-pixel convs (d->subpixel) on the
- * 4-wave path only; error otherwise.  neutron generator.py:24,29 (conv_layers.0 / .5). */
-int es_conv2d_fwd_planes(const es_conv_desc_t* d, const void* xp, const int64_t xs[4], const void* wk,
-                         const float* bias, void* y, es_dtype_t ydt, const int64_t ys[4], float* part,
-                         int64_t part_floats, int* chunks, es_stream_t stream);
-int es_conv2d_dgrad_planes(const es_conv_desc_t* d, const void* dyp, const int64_t ys[4], const void* wd, void* dx,
-                           es_dtype_t dxdt, const int64_t dxs[4], es_stream_t stream);
 /* Host-side count of MFMA conv kernels issued so far (ring / persistent / p256 / fp32 WGRAD).
  * Instrumentation only: lets a profiler state how many kernel launches one conv op was. */
 int64_t es_conv_launch_count(void);
-/* A/B knob of the split-fp32 FWD / DGRAD 256 x 128 tiles: 0 (default) = the 8-wave kernel, 1 = the
- * 4-wave kernel (one wave per SIMD, wave tiles 64 x 128; measured slower); same products in the same
- * order (bitwise equal outputs).  Returns the previous setting.  Replaces nothing of the reference (a
- * kernel choice for neutron generator.py:24,29 conv_layers.0 / .5). */
-int es_conv_set_spb4(int on);
-/* Opt-in (default 0, or ES_RING_BNRED=1): es_conv2d_dgrad_bnred on an fp32 ring DGRAD folds the
- * BatchNorm-backward reduction into the kernel's staged epilogue (bitwise equal dgrad output; measured
- * slower than the separate reduction pass).  Off, such calls report no partials and the
- * caller runs the reduction pass.  Returns the previous setting.  (The backward of neutron
- * generator.py:26-35's BatchNorm2d layers.) */
-int es_conv_set_ring_bnred(int on);
 /* Host-side tally of the MFMA work the conv entry points (es_conv2d_fwd / _dgrad / _wgrad /
  * _wgrad_det and their _stats / _bnred / _det variants) issued, as executed FLOPs (2 per MAC):
  * out[0] on the bf16 pipe (bf16 operands, and split-fp32: 6 plane products per fp32 product),
@@ -291,17 +258,6 @@ int es_norm_stats_finalize(const float* part, int chunks, int C, float eps, floa
 int es_norm_act_fwd(const es_view_t* x, es_dtype_t xdt, const es_norm_t* nm, const es_chain_t* ch,
                     const es_view_t* addend, es_dtype_t adt, const void* addend_ptr, const void* xp,
                     const es_view_t* y, es_dtype_t ydt, void* yp, es_stream_t stream);
-/* The dropout keep bits es_norm_act_fwd would write into ch->keep for x's shape, without the apply
- * (no-op without dropout).  For a BatchNorm whose apply runs in the consuming conv
- * (es_conv_norm_on_load); same Philox draws as neutron/generator.py:33-37's nn.Dropout there. */
-int es_norm_keep_bits(const es_view_t* x, const es_chain_t* ch, es_stream_t stream);
-/* Normalise-on-load for the following conv calls on this thread (nm == NULL clears): the activation
- * operand x handed to es_conv2d_fwd / es_conv2d_wgrad(_det) is the PRE-norm tensor h, and the conv
- * applies y = chain(BatchNorm(h)) (statistics nm, dropout keep bits / activation ch) as it loads it;
- * y is never stored.  Honoured by the thin Cout = 1 fp32 fwd / wgrad (the neutron generator's
- * conv_layers.13 on BatchNorm conv_layers.10 + Dropout + LeakyReLU, neutron/generator.py:33-38);
- * every other conv path returns ES_ERR_ARG while it is set. */
-int es_conv_norm_on_load(const es_norm_t* nm, const es_chain_t* ch);
 /* Backward of es_norm_act_fwd.  dy: gradient of y.  act_ref (optional): evaluate the activation
  * derivative on this stored tensor (the block output) instead of the recomputed pre-activation.
  * Writes dx (beta=1 accumulates), accumulates dgamma/dbeta (fp32, may be NULL) and, when dsum is

@@ -332,6 +332,8 @@ CASES = {
     "neutron_e1_b512": dict(arch="neutron", n_experts=1, batch=512, steps=1, compact=True),
     # BASELINE configs[2] batch size = the bench workload: step 0 at B = 1024
     "neutron_e1_b1024": dict(arch="neutron", n_experts=1, batch=1024, steps=1, compact=True),
+    # BASELINE configs[3] at its stated global batch: 4 experts, B = 2048, step 0
+    "neutron_e4_b2048": dict(arch="neutron", n_experts=4, batch=2048, steps=1, compact=True),
 }
 
 
