@@ -103,9 +103,19 @@ __device__ __forceinline__ uint32_t philox_word(uint64_t seed, uint32_t stream, 
   const uint32_t s = (uint32_t)(i & 3);
   return s == 0 ? r.x : (s == 1 ? r.y : (s == 2 ? r.z : r.w));
 }
-// stream + step * step_mul when the step lives on the device (captured train steps)
+// stream + step * step_mul when the step lives on the device (captured train steps), and the
+// index offset of a data-parallel rank's first sample when that lives on the device too
 __device__ __forceinline__ void resolve_stream(es_dropout_t& d) {
   if (d.enabled && d.step_ptr) d.stream += (uint32_t)(d.step_ptr[0] * d.step_mul);
+  if (d.enabled && d.index_ptr) d.index_offset += (uint64_t)d.index_ptr[0] * (uint64_t)d.index_mul;
+}
+
+// ---------------------------------------------------------------- dynamic batch (es_view_t.rows)
+// live images of an n-capacity batch whose count lives on the device (NULL: all n); wave-uniform
+__device__ __forceinline__ int live_rows(const int32_t* rows, int n) {
+  if (rows == nullptr) return n;
+  const int v = __builtin_amdgcn_readfirstlane(rows[0]);
+  return v < 0 ? 0 : (v < n ? v : n);
 }
 __device__ __forceinline__ bool dropout_keep(const es_dropout_t& d, uint64_t i) {
   return (philox_word(d.seed, d.stream, i + d.index_offset) >> 8) < d.threshold;

@@ -196,6 +196,7 @@ def deterministic() -> bool:
 # so the Python mirror is read back from C (packing the weight planes must follow the level the kernels run).
 _F32_SPLIT = None
 _SPLIT_LEVEL = 2
+_LIN_PIX = True      # ConvOp._pixel_view (tests compare it against the plain linear path)
 
 
 def set_f32_split(on: bool):
@@ -429,7 +430,7 @@ class ConvOp:
         the fp32 ring (>= 16 output pixels per image) and fall to the register-staged fp32-MFMA GEMM;
         the generators' fc2 (256 -> 21632 neutron, neutron/generator.py:17) is the case.  None when the
         layout does not apply."""
-        if self.R != 1 or self.S != 1 or self.up is not None or self.stride != 1 or self.pad != 0:
+        if not _LIN_PIX or self.R != 1 or self.S != 1 or self.up is not None or self.stride != 1 or self.pad != 0:
             return None
         N, Cc, H, W = x.dims
         dt = x.t.dtype

@@ -31,10 +31,18 @@ enum { ES_NORM_NONE = 0, ES_NORM_BN = 1, ES_NORM_GN = 2, ES_NORM_LN = 3 };
 
 typedef void* es_stream_t; /* hipStream_t */
 
-/* Logical 4-D view: element (n,c,h,w) lives at base + n*s[0] + c*s[1] + h*s[2] + w*s[3]. */
+/* Logical 4-D view: element (n,c,h,w) lives at base + n*s[0] + c*s[1] + h*s[2] + w*s[3].
+ * rows (optional, device int32): the LIVE batch count of a capacity-sized tensor.  A multi-expert
+ * step keeps each expert's activations in buffers of n = capacity images and the expert's image
+ * count on the device (es_expert_plan), so the step issues the same launches whatever the routing
+ * (no host synchronisation, one captured graph): every kernel given a view / descriptor with rows
+ * set works on images [0, min(rows[0], n)) only — images at or past it are neither read nor
+ * written and take no part in any reduction (BatchNorm statistics, weight gradients, losses).
+ * NULL: all n images (reference moe.py:121-207 runs each expert on exactly its B_e samples). */
 typedef struct {
   int n, c, h, w;
   int64_t s[4];
+  const int32_t* rows;
 } es_view_t;
 
 /* Counter-based dropout (expertsim/utils/philox.py).  keep(i) = (philox(seed, stream, i + index_offset)
@@ -54,6 +62,9 @@ typedef struct {
   const int32_t* step_ptr; /* device int32 or NULL */
   int32_t step_mul;
   uint64_t index_offset;
+  const int32_t* index_ptr; /* optional device int32: index_offset += index_ptr[0] * index_mul (a
+                               data-parallel rank's first sample of the expert, known on the device) */
+  int64_t index_mul;
 } es_dropout_t;
 
 const char* es_last_error(void);
@@ -84,6 +95,7 @@ typedef struct {
   int subpixel;        /* 1: the packed weights are the sub-pixel combination of a x2 upsample
                           conv (es_pack_conv_weight mode 2 for fwd, 3 for dgrad) and the conv runs
                           as 4 parity-class convs on the source grid (es_conv_subpixel_ok).      */
+  const int32_t* rows; /* optional device int32: live images of the N-capacity batch (es_view_t) */
 } es_conv_desc_t;
 
 /* y[n,k,p,q] = bias[k] + sum_{c,r,s} xu[n,c,p*stride-pad+r,q*stride-pad+s] * W[k,c,r,s]
