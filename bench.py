@@ -204,7 +204,7 @@ def make_step(moe, step_args, use_graph):
     if not use_graph:
         return eager_step, None
     from expertsim.graph import StepGraph
-    sg = StepGraph(moe, step_args, warmup=1)
+    sg = StepGraph(moe, step_args, warmup=1, allow_dp=True)
     return sg.replay, sg
 
 
@@ -308,9 +308,10 @@ def run_mode(args, precision, steps, warmup, dev, rank, world, ddp, probe_steps)
     real = t["real_images"].unsqueeze(1).contiguous()
     step_args = (0, t["cond"], real, t["true_positions"], t["std"], t["intensity"], oa, og, od, orr, None, dev)
     use_graph = args.graph == "on" or (args.graph == "auto" and not ddp)
-    if use_graph and args.experts > 1:
+    if use_graph:
         from expertsim.graph import graph_supported
-        use_graph = graph_supported(moe)
+        # several RCCL ranks: capture only when asked for (--graph on keeps the ranks in lockstep)
+        use_graph = graph_supported(moe, allow_dp=args.graph == "on")
     eager = lambda: moe.train_step(*step_args)
     for _ in range(warmup):
         eager()

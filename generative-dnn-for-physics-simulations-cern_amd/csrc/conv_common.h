@@ -77,7 +77,28 @@ struct ConvArgs {
                                 // (es_conv2d_*_det): into det_ws + z * M * Ng
   float* det_ws;
   int prio;                     // split-fp32 ring kernels: waves 4-7 at s_setprio 1 (VALU arbitration)
+  int nbase;                    // dynamic rows: the launch's first image within d.rows' count (chunks)
+  int mslot;                    // generic kernels (device-side): the launch's M, the split partials' stride
 };
+
+// Images of the launch that carry data: d.N, or with dynamic rows (es_conv_desc_t.rows, a device
+// count of the batch's live images) the part of [nbase, nbase + d.N) below that count.  Kernels
+// skip the tiles / K-steps past it and read its images as zeros (buffer num_records).
+__device__ __forceinline__ int conv_live(const ConvArgs& a) {
+  if (a.d.rows == nullptr) return a.d.N;
+  const int v = __builtin_amdgcn_readfirstlane(a.d.rows[0]) - a.nbase;
+  return v < 0 ? 0 : (v < a.d.N ? v : a.d.N);
+}
+
+// The generic GEMM kernels (conv_igemm.hip) shrink their problem to the live images: M (FWD /
+// DGRAD rows, image-major) or the K of a WGRAD (N*P*Q pixels).  mslot keeps the launch's M.
+__device__ __forceinline__ void conv_live_gemm(ConvArgs& a, int mode) {
+  a.mslot = a.M;
+  if (a.d.rows == nullptr) return;
+  const int nl = conv_live(a);
+  if (mode == MODE_WGRAD) a.Kd = nl * (a.Kd / a.d.N);
+  else a.M = nl * (a.M / a.d.N);
+}
 
 
 // es_conv2d_wgrad_det: the partial buffer offered to the generic (register-staged / thin) WGRAD

@@ -468,7 +468,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const f32x4 (&a
         if (ng >= a.Ng) continue;
         float v = acc[i][j][jj];
         if constexpr (MODE == MODE_WGRAD) {
-          if (a.det) ((float*)a.out)[((int64_t)blockIdx.z * a.M + m) * a.Ng + ng] = v;   // own partial slot
+          if (a.det) ((float*)a.out)[((int64_t)blockIdx.z * a.mslot + m) * a.Ng + ng] = v;   // own partial slot
           else atomicAdd((float*)a.out + (int64_t)m * a.Ng + ng, v);
         } else {
           if constexpr (MODE == MODE_FWD) {
@@ -476,7 +476,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const f32x4 (&a
           }
           const int64_t o = rowoff + (int64_t)ng * a.os[1];
           if (a.splitk) {
-            if (a.det) ((float*)a.det_ws)[(int64_t)blockIdx.z * a.M * a.Ng + o] = v;   // own partial slot
+            if (a.det) ((float*)a.det_ws)[(int64_t)blockIdx.z * a.mslot * a.Ng + o] = v;   // own partial slot
             else atomicAdd((float*)a.out + o, v);
           } else if (a.out_bf16) {
             bf16* y = (bf16*)a.out + o;
@@ -502,10 +502,11 @@ __global__ void __launch_bounds__(NTHREADS) conv_igemm_kernel(ConvArgs a) {
   typedef LdsImg<T, MODE, BN> LB;
   constexpr int BUF = LA::BYTES + LB::BYTES;   // one stage: A image then B image
 
+  conv_live_gemm(a, MODE);
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const int kbeg = blockIdx.z * a.k_per_split;
   const int kend = min(a.Kd, kbeg + a.k_per_split);
-  if (kbeg >= kend) return;
+  if ((kbeg >= kend || m0 >= a.M) && !a.det) return;   // (a partial slot is written even when empty)
   const int wid = threadIdx.x >> 6;
   const int wm0 = (wid >> 1) * (BM / 2), wn0 = (wid & 1) * (BN / 2);
 
@@ -600,14 +601,16 @@ __global__ void __launch_bounds__(NTHREADS) conv_glds_kernel(ConvArgs a) {
   constexpr int ABYTES = BM * 128, STAGE = (BM + BN) * 128;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const es_conv_desc_t& d = a.d;
+  conv_live_gemm(a, MODE);
 
   // XCD-aware tile order: consecutive tile ids on one XCD (bijective remap)
-  const int mt = (a.M + BM - 1) / BM;
+  const int mt = gridDim.x;
   const int nwg = mt * gridDim.y;
   const int orig = blockIdx.x + blockIdx.y * gridDim.x;
   const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
   const int m0 = (wgid % mt) * BM, n0 = (wgid / mt) * BN;
+  if (m0 >= a.M) return;   // rows of images past the live count (dynamic rows)
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm0 = (wid >> 1) * (BM / 2), wn0 = (wid & 1) * (BN / 2);
@@ -769,6 +772,7 @@ __global__ void __launch_bounds__(NTHREADS) conv_wgrad_glds_kernel(ConvArgs a) {
   constexpr int IMG = 64 * 256, STAGE = 2 * IMG;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const es_conv_desc_t& d = a.d;
+  conv_live_gemm(a, MODE_WGRAD);
 
   // XCD-aware order: blocks of one K split (same pixels) are consecutive on one XCD
   const int mt = gridDim.x, ntl = gridDim.y, tiles = mt * ntl;

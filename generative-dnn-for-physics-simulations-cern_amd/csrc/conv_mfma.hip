@@ -408,6 +408,7 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   // scratch [3][WGM][BN] floats, which no DMA targets
   __shared__ __attribute__((aligned(16))) char smem[RING + 3 * WGM * BN * 4 + JUNK];
   const es_conv_desc_t& d = a.d;
+  const int NL = conv_live(a);   // live images (dynamic rows)
   const SubPixel& sp = a.sp;
 
   // tile order: the column tiles of one row tile are consecutive (they share the gathered rows)
@@ -466,12 +467,26 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   const int PQ = gh * gw;
   const int gi = tl / TT;                                // image group: images NG gi ..
   const int pix0 = jt * NB;                              // first pixel of the tile
+  if (gi * NG >= NL) {   // past the live images (dynamic rows): an empty partial, no work
+    if (MODE == MODE_FWD && a.stats_part) {
+      for (int c = threadIdx.x; c < BN; c += NT) {
+        const int gc = n0 + c, cc = a.sp_merge ? gc / a.Ng : 0, ch = gc - cc * a.Ng;
+        if (cc < 4 && ch < a.Ng) {
+          float* pp = a.stats_part + (int64_t)(a.sp_merge ? tl * 4 + cc : tl) * 3 * a.Ng;
+          pp[ch] = 0.f;
+          pp[a.Ng + ch] = 0.f;
+          pp[2 * a.Ng + ch] = 0.f;
+        }
+      }
+    }
+    return;
+  }
 
   const int lane = threadIdx.x & 63, wid = uni(threadIdx.x >> 6);
   const int wm0 = (wid / WGN) * WM, wn0 = (wid % WGN) * WN;
   const int lrow = lane / CPR, pc = lane % CPR;
 
-  const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * EA));
+  const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(NL * a.as[0] * EA));
   // packed weights: row stride ldb (elements) and the class's block offset
   int ldb, bbase = 0, bbytes;
   if constexpr (SP && MODE == MODE_FWD) {
@@ -853,7 +868,7 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
     }
     return (int64_t)row_img(r) * a.os[0] + (int64_t)y * a.os[2] + (int64_t)x * a.os[3];
   };
-  auto row_ok = [&](int r) { return row_pix(r) < PQ && row_img(r) < d.N; };
+  auto row_ok = [&](int r) { return row_pix(r) < PQ && row_img(r) < NL; };
   // final values (bias added, rounded to the output dtype) back into acc
 #pragma unroll
   for (int j = 0; j < RN; ++j) {
@@ -980,7 +995,7 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
       for (int q = wid; q < BM / 2; q += 8) {
         const int t = ((2 * (q >> lgNG) + half) << lgNG) + (q & (NG - 1));
         const int pix = pix0 + (t >> lgNG), img = gi * NG + (t & (NG - 1));
-        if (colok && pix < PQ && img < d.N) {
+        if (colok && pix < PQ && img < NL) {
           int y = fdiv(pix, fgw), x = pix - y * gw;
           if constexpr (SP && MODE == MODE_FWD) {
             y = py0 + 2 * y;
@@ -1149,6 +1164,7 @@ __global__ void __launch_bounds__(RT) conv_persist_kernel(ConvArgs a, int ntiles
   char* const panel = smem;
   char* const ring = smem + PANEL;
   const es_conv_desc_t& d = a.d;
+  const int NL = conv_live(a);   // live images (dynamic rows)
   const int nch = MODE == MODE_FWD ? d.C : d.K;
   const int cpt = nch / BK, nk = a.Kd / BK;
   const int lane = threadIdx.x & 63, wid = uni(threadIdx.x >> 6);
@@ -1159,6 +1175,7 @@ __global__ void __launch_bounds__(RT) conv_persist_kernel(ConvArgs a, int ntiles
   const int NG = a.ng, PPG = NG / PROWS, NB = BM / NG;
   const int gh = MODE == MODE_FWD ? d.P : d.H, gw = MODE == MODE_FWD ? d.Q : d.W;
   const int PQ = gh * gw, TT = (PQ + NB - 1) / NB;
+  ntiles = min(ntiles, (NL + NG - 1) / NG * TT);          // the live image groups' tiles
   const int lgNG = uni(31 - __builtin_clz(NG));
   FastDiv fgw;
   {
@@ -1174,9 +1191,9 @@ __global__ void __launch_bounds__(RT) conv_persist_kernel(ConvArgs a, int ntiles
   const int my = t_hi - t_lo > lw ? (t_hi - t_lo - lw + L - 1) / L : 0;
   const int nsteps = my * nk;
 
-  const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * 2));
+  const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(NL * a.as[0] * 2));
   const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)(a.Ng * a.Kd * 2));
-  const __amdgpu_buffer_rsrc_t ores = mkres(a.out, (uint32_t)(d.N * a.os[0] * 2));
+  const __amdgpu_buffer_rsrc_t ores = mkres(a.out, (uint32_t)(NL * a.os[0] * 2));
   // the weight panel: K-step k occupies [BN rows][128 B] at panel + k * BN * 128 (ring B layout)
   for (int pi = wid; pi < nk * (BN / PROWS); pi += 8) {
     const int k = pi / (BN / PROWS), rb = pi - k * (BN / PROWS);
@@ -1256,8 +1273,8 @@ __global__ void __launch_bounds__(RT) conv_persist_kernel(ConvArgs a, int ntiles
   // the ring starts, like bcol)
   float bmu[8], bis[8], bsc[8], bsh[8], bs1[8], bs2[8];
   int4v pdy[NST];                                         // the previous tile's stored dy
-  const __amdgpu_buffer_rsrc_t hres = mkres(a.bnr_x, BNR ? (uint32_t)(d.N * a.os[0] * 2) : 0u);
-  const __amdgpu_buffer_rsrc_t kres = mkres(a.bnr_keep, BNR ? (uint32_t)((int64_t)d.N * PQ * (a.Ng / 8)) : 0u);
+  const __amdgpu_buffer_rsrc_t hres = mkres(a.bnr_x, BNR ? (uint32_t)(NL * a.os[0] * 2) : 0u);
+  const __amdgpu_buffer_rsrc_t kres = mkres(a.bnr_keep, BNR ? (uint32_t)((int64_t)NL * PQ * (a.Ng / 8)) : 0u);
   if constexpr (BNR) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -1327,7 +1344,7 @@ __global__ void __launch_bounds__(RT) conv_persist_kernel(ConvArgs a, int ntiles
     const int gi = t / TT, pix0 = (t - gi * TT) * NB;
     auto row_pix = [&](int r) { return pix0 + ((wm0 + r) >> lgNG); };
     auto row_img = [&](int r) { return gi * NG + ((wm0 + r) & (NG - 1)); };
-    auto row_ok = [&](int r) { return row_pix(r) < PQ && row_img(r) < d.N; };
+    auto row_ok = [&](int r) { return row_pix(r) < PQ && row_img(r) < NL; };
     if constexpr (BNR) {
       if (ci > 0) {
         // the previous tile's h / keep DMA: older than the NS - 1 steps issued since (nk >= NS - 1)
@@ -1578,6 +1595,7 @@ __global__ void __launch_bounds__(RT) conv_p256_kernel(ConvArgs a, int R) {
   constexpr int LR = 32 / NT;                                 // workgroups per column tile per XCD
   __shared__ __attribute__((aligned(16))) char smem[NS * SLOT + 8 * STAGE + BN * 4 + 2 * 3 * BN * 4];
   const es_conv_desc_t& d = a.d;
+  const int NL = conv_live(a);   // live images (dynamic rows)
   const SubPixel& sp = a.sp;
   const int lane = threadIdx.x & 63, wid = uni(threadIdx.x >> 6);
   const uint32_t sbias = lds_u32(smem + NS * SLOT + 8 * STAGE);   // [BN] floats
@@ -1591,12 +1609,13 @@ __global__ void __launch_bounds__(RT) conv_p256_kernel(ConvArgs a, int R) {
   // workgroup lw = NT l + ct takes column tile ct and every LR-th row tile from l
   const int xcd = blockIdx.x & 7, lw = blockIdx.x >> 3;
   const int ct = lw % NT, lr = lw / NT;
-  const int r_lo = (int)(((int64_t)R * xcd) >> 3), r_hi = (int)(((int64_t)R * (xcd + 1)) >> 3);
-  const int my = r_hi - r_lo > lr ? (r_hi - r_lo - lr + LR - 1) / LR : 0;
   const int n0 = ct * BN;
   const int NG = a.ng, PPG = NG / PROWS, NB = BM / NG;
   const int lgNG = uni(31 - __builtin_clz(NG));
   const int TT = sp.tile0[1], gh = sp.ph[0], gw = sp.pw[0], PQ = gh * gw;
+  R = min(R, (NL + NG - 1) / NG * TT);                   // the live image groups' row tiles
+  const int r_lo = (int)(((int64_t)R * xcd) >> 3), r_hi = (int)(((int64_t)R * (xcd + 1)) >> 3);
+  const int my = r_hi - r_lo > lr ? (r_hi - r_lo - lr + LR - 1) / LR : 0;
   const int oh0 = sp.oh[0], ow0 = sp.ow[0], kw = sp.dw[0];
   const int ldb = sp.dh[0] * sp.dw[0] * d.C, nk = ldb / BK;
   FastDiv fgw;
@@ -1611,9 +1630,9 @@ __global__ void __launch_bounds__(RT) conv_p256_kernel(ConvArgs a, int R) {
   const int py0 = sp.p0[0] + ((ecls >> 1) ? sp.p0[2] - sp.p0[0] : 0);
   const int px0 = sp.q0[0] + ((ecls & 1) ? sp.q0[1] - sp.q0[0] : 0);
 
-  const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * 2));
+  const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(NL * a.as[0] * 2));
   const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)(sp.tap0[4] * a.Ng * d.C * 2));
-  const __amdgpu_buffer_rsrc_t ores = mkres(a.out, (uint32_t)(d.N * a.os[0] * 2));
+  const __amdgpu_buffer_rsrc_t ores = mkres(a.out, (uint32_t)(NL * a.os[0] * 2));
   const int as0b = (int)a.as[0] * 2, as2b = (int)a.as[2] * 2, as3b = (int)a.as[3] * 2;
   const int os0 = (int)a.os[0], os2 = (int)a.os[2], os3 = (int)a.os[3];   // (N * os0 * 2 < 2^31: host)
   uint32_t blane[BPW];
@@ -1748,7 +1767,7 @@ __global__ void __launch_bounds__(RT) conv_p256_kernel(ConvArgs a, int R) {
         // branch-free: the address is computed for every row, padding rows store out of range
         const int t = wm0 + i * 16 + p * 8 + lr8;
         const int pix = pix0 + (t >> lgNG), img = gi * NG + (t & (NG - 1));
-        const bool ok = pix < PQ && img < d.N;
+        const bool ok = pix < PQ && img < NL;
         const int yy = fdiv(pix, fgw), xx = pix - yy * gw;
         const uint32_t voff = ok ? (uint32_t)(img * os0 + (py0 + 2 * yy) * os2 + (px0 + 2 * xx) * os3 + kc0 + lch * 8) * 2u : OOB;
         const int4v vv = p ? v1 : v0;
@@ -1891,8 +1910,9 @@ __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
   constexpr int ALPR = BM / 8, BLPR = BN / 8;   // lanes (16-byte chunks) per k-row
   __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT];
   const es_conv_desc_t& d = a.d;
+  const int NL = conv_live(a);   // live images (dynamic rows)
   const SubPixel& sp = a.sp;
-  const int G = (d.N + 63) >> 6;
+  const int G = (NL + 63) >> 6;
 
   // blocks of one K split (same pixels) are consecutive on one XCD
   const int mt = gridDim.x, ntl = gridDim.y, tiles = mt * ntl;
@@ -1916,14 +1936,15 @@ __global__ void __launch_bounds__(RT) wgrad_ring_kernel(ConvArgs a) {
     gq = d.Q;
     npix = d.P * d.Q;
   }
-  const int tbeg = split * a.k_per_split;       // in K-steps
-  const int tend = min(npix * G, tbeg + a.k_per_split);
+  const int kps = NL == a.d.N ? a.k_per_split : (npix * G + gridDim.z - 1) / gridDim.z;   // live K-steps
+  const int tbeg = split * kps;                  // in K-steps
+  const int tend = min(npix * G, tbeg + kps);
   if (tbeg >= tend) return;
 
   const int lane = threadIdx.x & 63, wid = uni(threadIdx.x >> 6);
   const int wm0 = (wid / WGN) * WM, wn0 = (wid % WGN) * WN;
-  const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * 2));
-  const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)(d.N * a.bs[0] * 2));
+  const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(NL * a.as[0] * 2));
+  const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)(NL * a.bs[0] * 2));
   const int as0b = (int)a.as[0] * 2, as2b = (int)a.as[2] * 2, as3b = (int)a.as[3] * 2;
   const int bs0b = (int)a.bs[0] * 2, bs2b = (int)a.bs[2] * 2, bs3b = (int)a.bs[3] * 2;
 
@@ -2070,8 +2091,9 @@ __global__ void __launch_bounds__(RT) wgrad_f32_kernel(ConvArgs a, float* __rest
   static_assert(ALPR >= 8 && BLPR >= 8, "the k-row swizzle flips 64-byte halves");
   __shared__ __attribute__((aligned(16))) char smem[NSW * SLOT];
   const es_conv_desc_t& d = a.d;
+  const int NL = conv_live(a);   // live images (dynamic rows)
   const SubPixel& sp = a.sp;
-  const int G = (d.N + KI - 1) / KI;
+  const int G = (NL + KI - 1) / KI;
 
   const int mt = gridDim.x, ntl = gridDim.y, tiles = mt * ntl;
   const int orig = blockIdx.x + (blockIdx.y + blockIdx.z * ntl) * mt;
@@ -2093,8 +2115,9 @@ __global__ void __launch_bounds__(RT) wgrad_f32_kernel(ConvArgs a, float* __rest
     gq = d.Q;
     npix = d.P * d.Q;
   }
-  const int tbeg = min(split * a.k_per_split, npix * G);
-  const int tend = min(npix * G, tbeg + a.k_per_split);
+  const int kps = NL == a.d.N ? a.k_per_split : (npix * G + gridDim.z - 1) / gridDim.z;   // live K-steps
+  const int tbeg = min(split * kps, npix * G);
+  const int tend = min(npix * G, tbeg + kps);
 
   const int lane = threadIdx.x & 63, wid = uni(threadIdx.x >> 6);
   const int wm0 = (wid / WGN) * WM, wn0 = (wid % WGN) * WN;
@@ -2106,8 +2129,8 @@ __global__ void __launch_bounds__(RT) wgrad_f32_kernel(ConvArgs a, float* __rest
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (tbeg < tend) {
-    const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * 4));
-    const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)(d.N * a.bs[0] * 4));
+    const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(NL * a.as[0] * 4));
+    const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)(NL * a.bs[0] * 4));
     const int as0b = (int)a.as[0] * 4, as2b = (int)a.as[2] * 4, as3b = (int)a.as[3] * 4;
     const int bs0b = (int)a.bs[0] * 4, bs2b = (int)a.bs[2] * 4, bs3b = (int)a.bs[3] * 4;
     uint32_t alane[APW], blane[BPW];
@@ -2330,10 +2353,12 @@ __global__ void __launch_bounds__(RT) wgrad_f32_col2_kernel(ConvArgs a, float* _
   __shared__ __attribute__((aligned(16))) char smem[NS * SLOT + 2 * ABUF];
   char* const abase = smem + NS * SLOT;
   const es_conv_desc_t& d = a.d;
-  const int G = (d.N + KI - 1) / KI, Q1 = d.Q + 1;
+  const int NL = conv_live(a);   // live images (dynamic rows)
+  const int G = (NL + KI - 1) / KI, Q1 = d.Q + 1;
   const int split = xcd_remap(blockIdx.z, gridDim.z);
   const int nst = G * d.P * Q1;
-  const int tbeg = min(split * a.k_per_split, nst), tend = min(nst, tbeg + a.k_per_split);
+  const int kps = NL == a.d.N ? a.k_per_split : (nst + gridDim.z - 1) / gridDim.z;   // live K-steps
+  const int tbeg = min(split * kps, nst), tend = min(nst, tbeg + kps);
 
   const int lane = threadIdx.x & 63, wid = uni(threadIdx.x >> 6);
   const int tap = wid >> 1, wtr = tap >> 1, wts = tap & 1, wc0 = (wid & 1) * 64;
@@ -2345,8 +2370,8 @@ __global__ void __launch_bounds__(RT) wgrad_f32_col2_kernel(ConvArgs a, float* _
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (tbeg < tend) {
-    const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * 4));
-    const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)(d.N * a.bs[0] * 4));
+    const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(NL * a.as[0] * 4));
+    const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)(NL * a.bs[0] * 4));
     const int as0b = (int)a.as[0] * 4, as2b = (int)a.as[2] * 4, as3b = (int)a.as[3] * 4;
     const int bs0b = (int)a.bs[0] * 4, bs2b = (int)a.bs[2] * 4, bs3b = (int)a.bs[3] * 4;
     // dy half-block of this wave: rows 16 (wid >> 1) + col16, images 4 (4 (wid & 1) + jj) + kl
@@ -2494,8 +2519,9 @@ __global__ void __launch_bounds__(RT) wgrad_coop_kernel(ConvArgs a, float* __res
   constexpr int PLANE = NB * 1024, PBUF = 3 * PLANE;
   __shared__ __attribute__((aligned(16))) char smem[2 * PBUF];
   const es_conv_desc_t& d = a.d;
+  const int NL = conv_live(a);   // live images (dynamic rows)
   const SubPixel& sp = a.sp;
-  const int G = (d.N + KI - 1) / KI;
+  const int G = (NL + KI - 1) / KI;
 
   const int mt = gridDim.x, ntl = gridDim.y, tiles = mt * ntl;
   const int orig = blockIdx.x + (blockIdx.y + blockIdx.z * ntl) * mt;
@@ -2517,8 +2543,9 @@ __global__ void __launch_bounds__(RT) wgrad_coop_kernel(ConvArgs a, float* __res
     gq = d.Q;
     npix = d.P * d.Q;
   }
-  const int tbeg = min(split * a.k_per_split, npix * G);
-  const int tend = min(npix * G, tbeg + a.k_per_split);
+  const int kps = NL == a.d.N ? a.k_per_split : (npix * G + gridDim.z - 1) / gridDim.z;   // live K-steps
+  const int tbeg = min(split * kps, npix * G);
+  const int tend = min(npix * G, tbeg + kps);
 
   const int lane = threadIdx.x & 63, wid = uni(threadIdx.x >> 6);
   const int wm0 = (wid / WGN) * WM, wn0 = (wid % WGN) * WN;
@@ -2530,8 +2557,8 @@ __global__ void __launch_bounds__(RT) wgrad_coop_kernel(ConvArgs a, float* __res
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (tbeg < tend) {
-    const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(d.N * a.as[0] * 4));
-    const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)(d.N * a.bs[0] * 4));
+    const __amdgpu_buffer_rsrc_t ares = mkres(a.a_src, (uint32_t)(NL * a.as[0] * 4));
+    const __amdgpu_buffer_rsrc_t bres = mkres(a.b_src, (uint32_t)(NL * a.bs[0] * 4));
     const int as0b = (int)a.as[0] * 4, as2b = (int)a.as[2] * 4, as3b = (int)a.as[3] * 4;
     const int bs0b = (int)a.bs[0] * 4, bs2b = (int)a.bs[2] * 4, bs3b = (int)a.bs[3] * 4;
     // half-block h of this wave: block b = (8 h + wid) / 2, k-half hh = wid & 1 (images
@@ -3199,6 +3226,7 @@ int es_conv_ring_launch_f32(ConvArgs& a, int mode, hipStream_t st) {
   for (int n0 = 0; n0 < N; n0 += nc) {
     ConvArgs c = a;
     c.d.N = std::min(nc, N - n0);
+    c.nbase = a.nbase + n0;
     c.a_src = (const char*)a.a_src + (int64_t)n0 * a.as[0] * ea;
     c.out = (char*)a.out + (int64_t)n0 * a.os[0] * esz;
     c.M = mode == MODE_FWD ? c.d.N * d.P * d.Q : (a.fold ? c.d.N * d.H * d.W : c.d.N * d.Hu * d.Wu);
@@ -3282,6 +3310,7 @@ int es_wgrad_f32_ring(const es_conv_desc_t& d, const void* dy, const int64_t ys[
     a.d = d;
     a.prio = SPL_PRIO;
     a.d.N = std::min(p.nc, d.N - n0);
+    a.nbase = n0;
     a.a_src = (const char*)dy + (int64_t)n0 * ys[0] * 4;
     a.b_src = (const char*)x + (int64_t)n0 * xs[0] * 4;
     for (int i = 0; i < 4; ++i) { a.as[i] = ys[i]; a.bs[i] = xs[i]; }

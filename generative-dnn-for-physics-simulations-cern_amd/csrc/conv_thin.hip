@@ -59,6 +59,13 @@ struct Thin {
   int det;                         // wgrad: block b stores its sums into out + b * (K*R*S*C) (no atomics)
 };
 
+// pixels of the live images (es_conv_desc_t.rows: a device count of the live images; the rows are
+// image-major, so they are a prefix of the M = N * pixels rows)
+__device__ __forceinline__ int thin_m(const Thin& t) {
+  if (t.d.rows == nullptr) return t.M;
+  return live_rows(t.d.rows, t.d.N) * (t.M / t.d.N);
+}
+
 __device__ __forceinline__ void pix3(int m, int A, int B, int& n, int& i, int& j) {
   j = m % B; const int t = m / B; i = t % A; n = t / A;
 }
@@ -70,6 +77,7 @@ template <typename T, typename TO, int RS>
 __global__ void __launch_bounds__(NT) c1_fwd(Thin t) {
   constexpr int VO = 16 / sizeof(TO);
   const es_conv_desc_t& d = t.d;
+  t.M = thin_m(t);   // dynamic rows: the live images' pixels
   __shared__ float wf[64 * RS], bs[64];
   for (int i = threadIdx.x; i < d.K * RS; i += NT) wf[i] = to_f(((const T*)t.w)[i]);
   for (int i = threadIdx.x; i < d.K; i += NT) bs[i] = t.bias ? t.bias[i] : 0.f;
@@ -107,6 +115,7 @@ template <typename T, typename TO, int RS>
 __global__ void __launch_bounds__(NT) c1_dgrad(Thin t) {
   constexpr int VN = V16<T>::N;
   const es_conv_desc_t& d = t.d;
+  t.M = thin_m(t);   // dynamic rows: the live images' pixels
   __shared__ float wf[64 * RS];
   for (int i = threadIdx.x; i < d.K * RS; i += NT) wf[i] = to_f(((const T*)t.w)[i]);
   __syncthreads();
@@ -152,6 +161,7 @@ __global__ void __launch_bounds__(NT) c1_dgrad(Thin t) {
 template <typename T, int RS>
 __global__ void __launch_bounds__(NT) c1_wgrad(Thin t) {
   const es_conv_desc_t& d = t.d;
+  t.M = thin_m(t);   // dynamic rows: the live images' pixels
   const int KO = d.K / 8;                 // 1..8, power of two (host-checked)
   const int ko = threadIdx.x % KO, pl = threadIdx.x / KO, PL = NT / KO;
   float acc[8][RS];
@@ -219,6 +229,7 @@ template <typename T, typename TO, int RS, int CH = 1>
 __global__ void __launch_bounds__(NT) k1_fwd(Thin t, int LP) {
   constexpr int VN = V16<T>::N;
   const es_conv_desc_t& d = t.d;
+  t.M = thin_m(t);   // dynamic rows: the live images' pixels
   __shared__ float wf[1024];
   for (int i = threadIdx.x; i < RS * d.C; i += NT) wf[i] = to_f(((const T*)t.w)[i]);   // [R][S][C]
   __syncthreads();
@@ -265,6 +276,7 @@ template <typename T, typename TO, int RS, int CH = 1>
 __global__ void __launch_bounds__(NT) k1_dgrad(Thin t, int LP) {
   constexpr int VN = V16<T>::N;
   const es_conv_desc_t& d = t.d;
+  t.M = thin_m(t);   // dynamic rows: the live images' pixels
   __shared__ float wf[1024];                                  // transposed to [R*S][C]
   for (int i = threadIdx.x; i < RS * d.C; i += NT) {
     const int c = i / RS, j = i % RS;
@@ -337,6 +349,7 @@ struct ThinBnr {
 template <typename T, int RS>
 __global__ void __launch_bounds__(NT) k1_dgrad_bnred(Thin t, int LP, ThinBnr b) {
   const es_conv_desc_t& d = t.d;
+  t.M = thin_m(t);   // dynamic rows: the live images' pixels
   __shared__ float wf[1024];                                  // transposed to [R*S][C]
   __shared__ float r1[NT * 8], r2[NT * 8];
   for (int i = threadIdx.x; i < RS * d.C; i += NT) {
@@ -418,6 +431,7 @@ template <typename T, int RS, int CH = 1>
 __global__ void __launch_bounds__(NT) k1_wgrad(Thin t, int LP) {
   constexpr int VN = V16<T>::N, VC = VN * CH;
   const es_conv_desc_t& d = t.d;
+  t.M = thin_m(t);   // dynamic rows: the live images' pixels
   const int PPB = NT / LP;
   const int l = threadIdx.x % LP;
   float acc[RS][VC];
@@ -497,6 +511,7 @@ __global__ void __launch_bounds__(NT) k1_wgrad(Thin t, int LP) {
 template <int KO, int CC>
 __global__ void __launch_bounds__(NT) small_fwd(Thin t) {
   const es_conv_desc_t& d = t.d;
+  t.M = thin_m(t);   // dynamic rows: the live images' pixels
   const int RS = d.R * d.S, C = CC > 0 ? CC : d.C;
   __shared__ float wf[9 * 64 * KO];                       // [rs][c][k]
   __shared__ float bs[KO];

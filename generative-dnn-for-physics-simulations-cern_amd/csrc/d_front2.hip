@@ -297,6 +297,7 @@ __global__ void __launch_bounds__(FT) dfront2_fwd_kernel(F2Args a) {
   __shared__ float red[NW * 24];
   __shared__ float st[4 * FG];                // GN1 mean, invstd, GN2 mean, invstd
   const int n = blockIdx.x, g = threadIdx.x & 7, u = threadIdx.x >> 3;
+  if (n >= live_rows(a.p.rows, gridDim.x)) return;   // a padding image (dynamic rows)
   const int NP1 = a.Hp * a.Wp, NO2 = a.Ho2 * a.Wo2;
   float* sv = a.save ? a.save + (int64_t)n * a.sv : nullptr;
   Quad q;
@@ -445,6 +446,7 @@ __global__ void __launch_bounds__(FT) dfront2_bwd_kernel(F2Args a) {
   float* h2 = R;
   float* dn = R + MAXH2 * H2S;
   const int n = blockIdx.x, g = threadIdx.x & 7, u = threadIdx.x >> 3;
+  if (n >= live_rows(a.p.rows, gridDim.x)) return;   // a padding image (dynamic rows; no partial)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float* part = WW ? a.part + (int64_t)n * NPART2 : nullptr;
   Quad q;
@@ -683,8 +685,10 @@ __global__ void __launch_bounds__(FT) dfront2_bwd_kernel(F2Args a) {
 struct F2Out {
   float *dw1, *db1, *dg1, *dbe1, *dw2, *db2, *dg2, *dbe2;
 };
-__global__ void __launch_bounds__(1024) dfront2_part_reduce(const float* __restrict__ part, int N, F2Out o) {
+__global__ void __launch_bounds__(1024) dfront2_part_reduce(const float* __restrict__ part, int N, F2Out o,
+                                                            const int32_t* rows) {
   __shared__ float red[16][64];
+  N = live_rows(rows, N);   // the live images' partials
   const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6, col = blockIdx.x * 64 + lane;
   float s = 0.f;
   if (col < NPART2)
@@ -779,7 +783,7 @@ extern "C" int es_dfront2_bwd(const float* img, const int64_t is[4], int N, int 
   ES_CHECK_LAUNCH();
   if (part) {
     const F2Out o{dw1, db1, dg1, dbe1, dw2, db2, dg2, dbe2};
-    hipLaunchKernelGGL(dfront2_part_reduce, dim3((NPART2 + 63) / 64), dim3(1024), 0, st, part, N, o);
+    hipLaunchKernelGGL(dfront2_part_reduce, dim3((NPART2 + 63) / 64), dim3(1024), 0, st, part, N, o, p->rows);
     ES_CHECK_LAUNCH();
   }
   return ES_OK;

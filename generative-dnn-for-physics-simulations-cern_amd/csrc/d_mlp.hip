@@ -169,7 +169,9 @@ __global__ void __launch_bounds__(MT) dmlp_fwd_kernel(MlpArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[SMEM];
   float (*t3)[P1] = (float (*)[P1])smem;        // (aliases the staged input after fc1)
   float (*t4)[P2] = (float (*)[P2])(smem + RB * P1);
+  a.B = live_rows(a.p.rows, a.B);               // dynamic rows: the live samples
   const int r0 = blockIdx.x * RB, nrow = min(RB, a.B - r0);
+  if (nrow <= 0) return;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, r16 = lane & 15, kq = lane >> 4;
   const es_dmlp_params_t& p = a.p;
   stage_x(a.X, a.xs, r0, nrow, a.F, smem);
@@ -248,7 +250,9 @@ __global__ void __launch_bounds__(MT) dmlp_bwd_kernel(MlpArgs a) {
   float (*g4)[P2] = (float (*)[P2])(smem + RB * P1);              // fc2 output gradient (dh4)
   float (*cs)[RB][P1] = (float (*)[RB][P1])(smem + RB * P1 + RB * P2);   // dgamma / dbeta terms
   float (*g3)[P1] = (float (*)[P1])(smem + SMEM);                 // dy3, then dh3
+  a.B = live_rows(a.p.rows, a.B);               // dynamic rows: the live samples
   const int r0 = blockIdx.x * RB, nrow = min(RB, a.B - r0);
+  if (nrow <= 0) return;                          // (dmlp_part_reduce skips its partial)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, r16 = lane & 15, kq = lane >> 4;
   const es_dmlp_params_t& p = a.p;
   const PartLayout L = part_layout(a.F);
@@ -436,8 +440,9 @@ struct MlpOut {
   float *dw1, *db1, *dg1, *dbe1, *dw2, *db2, *dg2, *dbe2, *dw3, *db3;
 };
 __global__ void __launch_bounds__(1024) dmlp_part_reduce(const float* __restrict__ part, int nwg, int F,
-                                                         MlpOut o) {
+                                                         MlpOut o, const int32_t* rows, int B) {
   __shared__ float red[16][64];
+  if (rows) nwg = min(nwg, (live_rows(rows, B) + RB - 1) / RB);   // the live samples' workgroups
   const PartLayout L = part_layout(F);
   const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6;
   const int64_t col = (int64_t)blockIdx.x * 64 + lane;
@@ -512,7 +517,7 @@ extern "C" int es_dmlp_bwd(const float* X, int64_t xs, int B, int F, const es_dm
   if (part) {
     const MlpOut o{dw1, db1, dg1, dbe1, dw2, db2, dg2, dbe2, dw3, db3};
     const int64_t n = part_layout(F).n;
-    hipLaunchKernelGGL(dmlp_part_reduce, dim3((unsigned)((n + 63) / 64)), dim3(1024), 0, st, part, nwg, F, o);
+    hipLaunchKernelGGL(dmlp_part_reduce, dim3((unsigned)((n + 63) / 64)), dim3(1024), 0, st, part, nwg, F, o, p->rows, B);
     ES_CHECK_LAUNCH();
   }
   return ES_OK;

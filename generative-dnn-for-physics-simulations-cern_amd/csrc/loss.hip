@@ -12,6 +12,7 @@ namespace {
 struct View {
   int n, c, h, w;
   int64_t s[4];
+  const int32_t* rows;   // live images (es_view_t.rows)
   __device__ __forceinline__ int64_t off(int in, int ic, int ih, int iw) const {
     return in * s[0] + ic * s[1] + ih * s[2] + iw * s[3];
   }
@@ -20,6 +21,7 @@ View mkview(const es_view_t* v) {
   View r;
   r.n = v->n; r.c = v->c; r.h = v->h; r.w = v->w;
   for (int i = 0; i < 4; ++i) r.s[i] = v->s[i];
+  r.rows = v->rows;
   return r;
 }
 __device__ __forceinline__ float ldf(const void* p, int bf, int64_t i) {
@@ -27,9 +29,14 @@ __device__ __forceinline__ float ldf(const void* p, int bf, int64_t i) {
 }
 __device__ __forceinline__ float signf_(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
 
-__global__ void __launch_bounds__(256) hinge_d_kernel(const float* ro, const float* fo, int n, const float* wp,
-                                                      float* out, float* dro, float* dfo) {
+__global__ void __launch_bounds__(256) hinge_d_kernel(const float* ro, const float* fo, int n, const int32_t* rows,
+                                                      const float* wp, float* out, float* dro, float* dfo) {
   __shared__ float sh[8];
+  n = live_rows(rows, n);
+  if (n == 0) {   // an expert without samples this step: loss 0 (moe.py:126-129)
+    if (threadIdx.x == 0) out[0] = 0.f;
+    return;
+  }
   const float w = wp[0];
   float a = 0.f, b = 0.f;
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
@@ -48,6 +55,7 @@ __global__ void __launch_bounds__(256) hinge_d_kernel(const float* ro, const flo
 __global__ void __launch_bounds__(256) expsum_kernel(View x, const void* xp, int bf, float* s) {
   __shared__ float sh[8];
   const int n = blockIdx.x;
+  if (n >= live_rows(x.rows, x.n)) return;
   const int per = x.c * x.h * x.w;
   float a = 0.f;
   for (int i = threadIdx.x; i < per; i += blockDim.x) {
@@ -60,7 +68,7 @@ __global__ void __launch_bounds__(256) expsum_kernel(View x, const void* xp, int
 
 __global__ void expsum_bwd_kernel(View x, const void* xp, int bf, const float* coef, View dx, float* dxp,
                                   float beta) {
-  const int64_t total = (int64_t)x.n * x.c * x.h * x.w;
+  const int64_t total = (int64_t)live_rows(x.rows ? x.rows : dx.rows, x.n) * x.c * x.h * x.w;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     const int w = e % x.w; int64_t t = e / x.w; const int h = t % x.h; t /= x.h; const int c = t % x.c;
     const int n = t / x.c;
@@ -81,7 +89,7 @@ __global__ void __launch_bounds__(256) gen_losses_a(es_gen_loss_t p, const float
                                                     const float* n1, const float* n2, float* div_out,
                                                     float* adn_out) {
   const int lane = threadIdx.x & 63, b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= p.n) return;
+  if (b >= live_rows(p.rows, p.n)) return;
   float adl = 0.f, adn = 0.f;
   for (int k = lane; k < p.latent; k += 64) adl += fabsf(l1[b * p.latent + k] - l2[b * p.latent + k]);
   for (int k = lane; k < p.noise; k += 64) adn += fabsf(n1[b * p.noise + k] - n2[b * p.noise + k]);
@@ -96,7 +104,11 @@ __global__ void __launch_bounds__(256) gen_losses_b(es_gen_loss_t p, const float
                                                     float* coef, float* dcoord, float* dl2) {
   __shared__ float sh[8];
   __shared__ float sdiv[4096], sadn[4096];  // n <= 4096 checked on host
-  const int n = p.n;
+  const int n = live_rows(p.rows, p.n);
+  if (n == 0) {   // an expert without samples this step: every metric 0 (moe.py:126-130)
+    if (threadIdx.x < 8) out[threadIdx.x] = 0.f;
+    return;
+  }
   const float w = wp[0];
   const float fn = (float)n;
   for (int b = threadIdx.x; b < n; b += blockDim.x) { sdiv[b] = coef[b]; sadn[b] = dfo[b]; }
@@ -159,7 +171,7 @@ __global__ void __launch_bounds__(256) gen_losses_b(es_gen_loss_t p, const float
 __global__ void __launch_bounds__(256) gen_losses_c(es_gen_loss_t p, const float* l1, const float* l2, float* dl1,
                                                     float* dl2) {
   const int lane = threadIdx.x & 63, b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= p.n) return;
+  if (b >= live_rows(p.rows, p.n)) return;
   const float g = dl2[b * p.latent];   // every lane's load precedes the wave's stores (data dependency)
   for (int k = lane; k < p.latent; k += 64) {
     const float sg = signf_(l1[b * p.latent + k] - l2[b * p.latent + k]);
@@ -409,17 +421,19 @@ __global__ void step_metrics_kernel(const float* mbuf, int E, const float* rl, c
 }
 
 // mean_intensities_in_batch_expert[mask] = s (moe.py:196-198): dst[rows[i]] = src[i]
-__global__ void scatter_rows_kernel(const float* src, const int32_t* rows, const int32_t* start, int n, float* dst) {
+__global__ void scatter_rows_kernel(const float* src, const int32_t* rows, const int32_t* start, int n, float* dst,
+                                    const int32_t* live) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (start) rows += start[0];
-  if (i < n) dst[rows ? rows[i] : i] = src[i];
+  if (i < live_rows(live, n)) dst[rows ? rows[i] : i] = src[i];
 }
 }  // namespace
 
-extern "C" int es_hinge_d(const float* ro, const float* fo, int n, const float* w_ptr, float* out, float* dro,
-                          float* dfo, es_stream_t stream) {
+extern "C" int es_hinge_d(const float* ro, const float* fo, int n, const int32_t* rows, const float* w_ptr, float* out,
+                          float* dro, float* dfo, es_stream_t stream) {
   ES_CHECK_ARG(n > 0, "hinge_d: n must be > 0");
-  hipLaunchKernelGGL(hinge_d_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, ro, fo, n, w_ptr, out, dro, dfo);
+  hipLaunchKernelGGL(hinge_d_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, ro, fo, n, rows, w_ptr, out, dro,
+                     dfo);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
@@ -510,7 +524,7 @@ extern "C" int es_dp_metrics_merge(const float* rows, int world, int E, float* o
 extern "C" int es_scatter_rows(const float* src, const int32_t* rows, int n, float* dst, es_stream_t stream) {
   if (n <= 0) return ES_OK;
   hipLaunchKernelGGL(scatter_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, src, rows,
-                     (const int32_t*)nullptr, n, dst);
+                     (const int32_t*)nullptr, n, dst, (const int32_t*)nullptr);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
@@ -534,12 +548,12 @@ extern "C" int es_step_metrics(const float* mbuf, int E, const float* rl, const 
   return ES_OK;
 }
 
-extern "C" int es_scatter_rows_at(const float* src, const int32_t* perm, const int32_t* start, int n, float* dst,
-                                  es_stream_t stream) {
+extern "C" int es_scatter_rows_at(const float* src, const int32_t* perm, const int32_t* start, int n,
+                                  const int32_t* live, float* dst, es_stream_t stream) {
   if (n <= 0) return ES_OK;
   ES_CHECK_ARG(perm && start, "scatter_rows_at: perm / start");
   hipLaunchKernelGGL(scatter_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, src, perm, start,
-                     n, dst);
+                     n, dst, live);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }

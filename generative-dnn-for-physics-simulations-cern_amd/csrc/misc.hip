@@ -24,16 +24,23 @@ namespace {
 struct View {
   int n, c, h, w;
   int64_t s[4];
+  const int32_t* rows;   // live images (es_view_t.rows; NULL: n)
   __device__ __forceinline__ int64_t off(int in, int ic, int ih, int iw) const {
     return in * s[0] + ic * s[1] + ih * s[2] + iw * s[3];
   }
+  __device__ __forceinline__ int live() const { return live_rows(rows, n); }
+  // elements of the live images
+  __device__ __forceinline__ int64_t live_total() const { return (int64_t)live() * c * h * w; }
 };
 View mkview(const es_view_t* v) {
   View r;
   r.n = v->n; r.c = v->c; r.h = v->h; r.w = v->w;
   for (int i = 0; i < 4; ++i) r.s[i] = v->s[i];
+  r.rows = v->rows;
   return r;
 }
+// the live-count pointer of a pair of views of one batch (either may carry it)
+const int32_t* rows_of(const es_view_t* a, const es_view_t* b) { return a->rows ? a->rows : (b ? b->rows : nullptr); }
 __device__ __forceinline__ float ldf(const void* p, int bf, int64_t i) {
   return bf ? (float)((const bf16*)p)[i] : ((const float*)p)[i];
 }
@@ -66,7 +73,7 @@ int grid_for(int64_t total) { return (int)std::min<int64_t>((total + 255) / 256,
 // ------------------------------------------------------------------------------------ max pool
 __global__ void maxpool_fwd_kernel(View x, const void* xp, int bf, int kh, int kw, int sh, int sw, View y,
                                    void* yp, uint8_t* idx) {
-  const int64_t total = (int64_t)y.n * y.c * y.h * y.w;
+  const int64_t total = y.live_total();
   const bool cl = y.s[1] == 1 && y.c > 1;
   GRID_STRIDE(e, total) {
     int n, c, h, w;
@@ -86,7 +93,7 @@ __global__ void maxpool_fwd_kernel(View x, const void* xp, int bf, int kh, int k
 // gather form: every input position sums the output windows whose argmax it is
 __global__ void maxpool_bwd_kernel(View dy, const void* dyp, int bf, const uint8_t* idx, int kh, int kw, int sh,
                                    int sw, View dx, void* dxp, float beta) {
-  const int64_t total = (int64_t)dx.n * dx.c * dx.h * dx.w;
+  const int64_t total = dx.live_total();
   const bool cl = dx.s[1] == 1 && dx.c > 1;
   const bool ycl = dy.s[1] == 1 && dy.c > 1;
   GRID_STRIDE(e, total) {
@@ -117,10 +124,10 @@ __global__ void maxpool_bwd_kernel(View dy, const void* dyp, int bf, const uint8
 template <typename T>
 __global__ void __launch_bounds__(256) maxpool_bwd_nhwc(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
                                                        int N, int C, int H, int W, int P, int Q, int kh, int kw,
-                                                       T* __restrict__ dx, float beta) {
+                                                       T* __restrict__ dx, float beta, const int32_t* rows) {
   constexpr int VN = 16 / sizeof(T);
   const int cv = C / VN;
-  const uint32_t total = (uint32_t)N * H * W * cv;
+  const uint32_t total = (uint32_t)live_rows(rows, N) * H * W * cv;
   for (uint32_t e = blockIdx.x * 256u + threadIdx.x; e < total; e += gridDim.x * 256u) {
     const uint32_t pix = e / cv;
     const int c0 = (int)(e - pix * cv) * VN;
@@ -159,10 +166,10 @@ __global__ void __launch_bounds__(256) maxpool_bwd_nhwc(const T* __restrict__ dy
 template <typename T>
 __global__ void __launch_bounds__(256) maxpool_fwd_nhwc(const T* __restrict__ x, int N, int C, int H, int W, int P,
                                                        int Q, int kh, int kw, int sh, int sw, T* __restrict__ y,
-                                                       uint8_t* __restrict__ idx) {
+                                                       uint8_t* __restrict__ idx, const int32_t* rows) {
   constexpr int VN = 16 / sizeof(T);
   const int cv = C / VN;
-  const uint32_t total = (uint32_t)N * P * Q * cv;
+  const uint32_t total = (uint32_t)live_rows(rows, N) * P * Q * cv;
   for (uint32_t e = blockIdx.x * 256u + threadIdx.x; e < total; e += gridDim.x * 256u) {
     const uint32_t pix = e / cv;
     const int c0 = (int)(e - pix * cv) * VN;
@@ -203,7 +210,7 @@ bool dense_nhwc(const es_view_t* v) {
 // ----------------------------------------------------------------------------- upsample bwd
 __global__ void upsample_bwd_kernel(View du, const void* dup, int ubf, const int32_t* hs, const int32_t* hc,
                                     const int32_t* ws, const int32_t* wc, View dx, void* dxp, int xbf, float beta) {
-  const int64_t total = (int64_t)dx.n * dx.c * dx.h * dx.w;
+  const int64_t total = dx.live_total();
   const bool cl = dx.s[1] == 1 && dx.c > 1;
   GRID_STRIDE(e, total) {
     int n, c, h, w;
@@ -226,9 +233,10 @@ template <typename T>
 __global__ void __launch_bounds__(256) upsample_fwd_nhwc(const T* __restrict__ x, int H, int W, int C,
                                                          const int32_t* __restrict__ hmap,
                                                          const int32_t* __restrict__ wmap, T* __restrict__ y,
-                                                         int64_t rows, int Hu, int Wu) {
+                                                         int64_t rows, int Hu, int Wu, int N, const int32_t* nrows) {
   constexpr int V = 16 / sizeof(T);
   const int cv = C / V;
+  if (nrows) rows = (int64_t)live_rows(nrows, N) * Hu * Wu;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < rows * cv; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = i / cv;
     const int c = (int)(i - r * cv) * V;
@@ -242,8 +250,10 @@ template <typename T, typename TO>
 __global__ void __launch_bounds__(256) upsample_bwd_nhwc(const T* __restrict__ du, int Hu, int Wu, int C,
                                                          const int32_t* __restrict__ hs, const int32_t* __restrict__ hc,
                                                          const int32_t* __restrict__ ws, const int32_t* __restrict__ wc,
-                                                         TO* __restrict__ dx, int64_t rows, int H, int W, float beta) {
+                                                         TO* __restrict__ dx, int64_t rows, int H, int W, float beta,
+                                                         int N, const int32_t* nrows) {
   const int cv = C / 4;
+  if (nrows) rows = (int64_t)live_rows(nrows, N) * H * W;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < rows * cv; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = i / cv;
     const int c = (int)(i - r * cv) * 4;
@@ -265,7 +275,7 @@ __global__ void __launch_bounds__(256) upsample_bwd_nhwc(const T* __restrict__ d
 
 // ------------------------------------------------------------------------------------- copy
 __global__ void copy_kernel(View x, const void* xp, int xbf, View y, void* yp, int ybf, float alpha, float beta) {
-  const int64_t total = (int64_t)x.n * x.c * x.h * x.w;
+  const int64_t total = (int64_t)live_rows(x.rows ? x.rows : y.rows, x.n) * x.c * x.h * x.w;
   const bool cl = y.s[1] == 1 && y.c > 1;
   GRID_STRIDE(e, total) {
     int n, c, h, w;
@@ -282,9 +292,11 @@ __global__ void copy_kernel(View x, const void* xp, int xbf, View y, void* yp, i
 // LDS tile, both sides read / written along contiguous rows (the generic element-wise copy above
 // divides per element and ran at ~1 TB/s).
 template <typename T>
-__global__ void __launch_bounds__(256) transpose_kernel(const T* __restrict__ x, T* __restrict__ y, int R, int S) {
+__global__ void __launch_bounds__(256) transpose_kernel(const T* __restrict__ x, T* __restrict__ y, int R, int S,
+                                                       const int32_t* rows) {
   __shared__ T tile[64][65];
   const int n = blockIdx.z, r0 = blockIdx.y * 64, s0 = blockIdx.x * 64;
+  if (n >= live_rows(rows, gridDim.z)) return;
   const T* xs = x + (int64_t)n * R * S;
   T* ys = y + (int64_t)n * R * S;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
@@ -320,9 +332,11 @@ bool try_transpose(const es_view_t* x, es_dtype_t xdt, const void* xp, const es_
   if (R * S * x->n * 4 >= (1ll << 31) || x->n > 65535) return false;
   const dim3 grid((unsigned)((S + 63) / 64), (unsigned)((R + 63) / 64), (unsigned)x->n);
   if (xdt == ES_BF16)
-    hipLaunchKernelGGL(transpose_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)xp, (bf16*)yp, (int)R, (int)S);
+    hipLaunchKernelGGL(transpose_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)xp, (bf16*)yp, (int)R, (int)S,
+                       rows_of(x, y));
   else
-    hipLaunchKernelGGL(transpose_kernel<float>, grid, dim3(256), 0, st, (const float*)xp, (float*)yp, (int)R, (int)S);
+    hipLaunchKernelGGL(transpose_kernel<float>, grid, dim3(256), 0, st, (const float*)xp, (float*)yp, (int)R, (int)S,
+                       rows_of(x, y));
   return true;
 }
 
@@ -330,7 +344,7 @@ bool try_transpose(const es_view_t* x, es_dtype_t xdt, const void* xp, const es_
 __global__ void avgpool_fwd_kernel(View x, const void* xp, int bf, View y, void* yp) {
   // one wave per (n, c)
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
-  if (wave >= x.n * x.c) return;
+  if (wave >= x.live() * x.c) return;
   const int n = wave / x.c, c = wave % x.c;
   const int hw = x.h * x.w;
   float s = 0.f;
@@ -339,7 +353,7 @@ __global__ void avgpool_fwd_kernel(View x, const void* xp, int bf, View y, void*
   if (lane == 0) ((float*)yp)[y.off(n, c, 0, 0)] = s / (float)hw;
 }
 __global__ void avgpool_bwd_kernel(View dy, const float* dyp, View dx, void* dxp, int bf, float beta) {
-  const int64_t total = (int64_t)dx.n * dx.c * dx.h * dx.w;
+  const int64_t total = (int64_t)live_rows(dx.rows ? dx.rows : dy.rows, dx.n) * dx.c * dx.h * dx.w;
   const bool cl = dx.s[1] == 1 && dx.c > 1;
   const float inv = 1.f / (float)(dx.h * dx.w);
   GRID_STRIDE(e, total) {
@@ -353,13 +367,18 @@ __global__ void avgpool_bwd_kernel(View dy, const float* dyp, View dx, void* dxp
 }
 
 __global__ void gather_rows_kernel(const float* src, int64_t sld, const int32_t* idx, const int32_t* start,
-                                   int rows, int cols, float* dst, int64_t dld) {
+                                   int rows, int cols, float* dst, int64_t dld, const int32_t* live) {
   const int64_t total = (int64_t)rows * cols;
   if (start) idx += start[0];   // the expert's first position in the dispatch permutation (device)
+  const int nl = live_rows(live, rows);   // rows past the live count (capacity padding): zeros
   GRID_STRIDE(e, total) {
     const int r = e / cols, c = e % cols;
-    const int sr = idx ? idx[r] : r;
-    dst[r * dld + c] = src[sr * sld + c];
+    float v = 0.f;
+    if (r < nl) {
+      const int sr = idx ? idx[r] : r;
+      v = src[sr * sld + c];
+    }
+    dst[r * dld + c] = v;
   }
 }
 
@@ -370,9 +389,9 @@ __device__ __forceinline__ void sn_power_body(const float* w, int h, int wd, flo
                                               int update, float* scratch, float* sh);
 
 __global__ void __launch_bounds__(1024) sn_power_kernel(const float* w, int h, int wd, float* u, float* v,
-                                                        float* sigma, int update, float* scratch) {
+                                                        float* sigma, int update, float* scratch, const int32_t* active) {
   __shared__ float sh[16];
-  sn_power_body(w, h, wd, u, v, sigma, update, scratch, sh);
+  sn_power_body(w, h, wd, u, v, sigma, update && (active == nullptr || active[0] != 0), scratch, sh);
 }
 
 // several small layers' power iterations in one launch (one block per layer): the discriminator's
@@ -384,10 +403,11 @@ struct SnJobs {
   float* buf[ES_SN_BATCH_MAX];
   int h[ES_SN_BATCH_MAX], wd[ES_SN_BATCH_MAX];
 };
-__global__ void __launch_bounds__(1024) sn_power_batch_kernel(SnJobs j, int update) {
+__global__ void __launch_bounds__(1024) sn_power_batch_kernel(SnJobs j, int update, const int32_t* active) {
   __shared__ float sh[16];
   const int b = blockIdx.x;
-  sn_power_body(j.w[b], j.h[b], j.wd[b], j.u[b], j.v[b], j.buf[b], update, j.buf[b] + 1, sh);
+  sn_power_body(j.w[b], j.h[b], j.wd[b], j.u[b], j.v[b], j.buf[b], update && (active == nullptr || active[0] != 0),
+                j.buf[b] + 1, sh);
 }
 
 __device__ __forceinline__ void sn_power_body(const float* w, int h, int wd, float* u, float* v, float* sigma,
@@ -463,6 +483,7 @@ __device__ __forceinline__ void sn_power_body(const float* w, int h, int wd, flo
 // t = W^T u : block = 64 columns x 4 row groups, LDS reduction over the row groups
 __global__ void __launch_bounds__(256) sn_wtu_kernel(const float* __restrict__ w, int h, int wd,
                                                      const float* __restrict__ u, float* __restrict__ vt) {
+  // (an inactive update still computes vt; sn_wv_kernel then reads the stored v instead)
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int j = blockIdx.x * 64 + cl;
   float t = 0.f;
@@ -476,8 +497,13 @@ __global__ void __launch_bounds__(256) sn_wtu_kernel(const float* __restrict__ w
 // wv = W (x * scale), one wave per row; scale = 1/||x|| when `normalize` (x = the new v, written
 // back normalised by block 0), else 1 (x = the stored v)
 __global__ void __launch_bounds__(256) sn_wv_kernel(const float* __restrict__ w, int h, int wd, const float* x,
-                                                    int normalize, float* v_out, float* __restrict__ wv) {
+                                                    int normalize, float* v_out, float* __restrict__ wv,
+                                                    const float* v_stored, const int32_t* active) {
   __shared__ float sh[8];
+  if (normalize && active && active[0] == 0) {   // inactive: sigma from the stored v, no update
+    normalize = 0;
+    x = v_stored;
+  }
   float sc = 1.f;
   if (normalize) {
     float ss = 0.f;
@@ -495,9 +521,9 @@ __global__ void __launch_bounds__(256) sn_wv_kernel(const float* __restrict__ w,
 }
 // u = wv / ||wv|| (update), sigma = u . wv
 __global__ void __launch_bounds__(256) sn_final_kernel(int h, int wd, const float* wv, float* u, const float* v,
-                                                       int update, float* sigma, float* snap) {
+                                                       int update, float* sigma, float* snap, const int32_t* active) {
   __shared__ float sh[8];
-  if (update) {
+  if (update && (active == nullptr || active[0] != 0)) {
     float ss = 0.f;
     for (int i = threadIdx.x; i < h; i += 256) ss += wv[i] * wv[i];
     const float nu = fmaxf(sqrtf(block_sum(ss, sh)), 1e-12f);
@@ -605,7 +631,8 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
 // step read on the device; bias corrections as torch computes them (double), per thread
 __global__ void adam_dev_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                 float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
-                                const int32_t* __restrict__ step_ptr, float gscale) {
+                                const int32_t* __restrict__ step_ptr, float gscale, const int32_t* active) {
+  if (active && active[0] == 0) return;   // an expert skipped this step (moe.py:126-135): no update
   const int step = step_ptr[0];
   const double bc1 = 1.0 - pow((double)b1, (double)step);
   const double bc2 = 1.0 - pow((double)b2, (double)step);
@@ -621,7 +648,51 @@ __global__ void adam_dev_kernel(float* __restrict__ p, const float* __restrict__
     p[i] = p[i] - step_size * (mi / (sqrtf(vi) / bc2_sqrt + eps));
   }
 }
-__global__ void counter_add_kernel(int32_t* c, int32_t v) { c[0] += v; }
+__global__ void counter_add_kernel(int32_t* c, int32_t v, const int32_t* flag) {
+  if (flag == nullptr || flag[0] != 0) c[0] += v;
+}
+__global__ void counter_add_i64_kernel(int64_t* c, int64_t v, const int32_t* flag) {
+  if (flag == nullptr || flag[0] != 0) c[0] += v;
+}
+
+// Multi-expert step plan (moe.py:97-135 on the device): from the local expert counts and, data
+// parallel, the all-gathered [world][E] counts, per expert e:
+//   rows[e]   live local rows of the expert's capacity buffers: local count when the expert trains
+//             (global count > 1, moe.py:126) and this rank runs it (>= min_local samples), else 0;
+//   active[e] 1 when the expert trains this step (its optimizers, BatchNorm running statistics and
+//             spectral-norm vectors update), else 0;
+//   n0[e]     this rank's first sample in the expert's global batch (randomness at global indices);
+//   w[e]      class_counts_adjusted = float(local count) / float(B) (moe.py:99-100, 522, 562);
+//   gcnt[e]   the global count (float; SyncBN / SDI normalisers);
+//   lcnt[e]   rows[e] as float (the data-parallel metric merge's per-rank weights).
+__global__ void expert_plan_kernel(const int32_t* counts, const int32_t* counts_all, int world, int rank, int E, int B,
+                                   int min_local, int32_t* rows, int32_t* active, int32_t* n0, float* w, float* gcnt,
+                                   float* lcnt) {
+  const int e = threadIdx.x;
+  if (e >= E) return;
+  int g = counts[e], before = 0;
+  if (counts_all) {
+    g = 0;
+    for (int r = 0; r < world; ++r) {
+      const int c = counts_all[r * E + e];
+      g += c;
+      if (r < rank) before += c;
+    }
+  }
+  const int loc = counts[e];
+  const int act = g > 1 ? 1 : 0;
+  const int nr = act && loc >= min_local ? loc : 0;
+  rows[e] = nr;
+  active[e] = act;
+  n0[e] = before;
+  w[e] = (float)loc / (float)B;
+  gcnt[e] = (float)g;
+  lcnt[e] = (float)nr;
+}
+__global__ void div_by_kernel(float* x, int n, const float* d) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = x[i] / fmaxf(d[0], 1.f);
+}
 
 // EMA of a flat parameter buffer (EMAHelper.update, loop.py:392-400): s = decay*s + (1-decay)*p with
 // the reference's two roundings and one add (contraction off: no FMA), float4 when aligned.
@@ -645,8 +716,9 @@ __global__ void ema_kernel(float* __restrict__ s, const float* __restrict__ p, i
 
 // ------------------------------------------------------------------------------------ RNG
 __global__ void randn_kernel(float* out, int64_t n, uint64_t seed, uint32_t sid, const int32_t* step_ptr,
-                             int32_t step_mul, int64_t pair0) {
+                             int32_t step_mul, int64_t pair0, const int32_t* off_ptr, int64_t off_pairs) {
   if (step_ptr) sid += (uint32_t)(step_ptr[0] * step_mul);
+  if (off_ptr) pair0 += (int64_t)off_ptr[0] * off_pairs;
   // Box-Muller on pairs: counter = global pair index (pair0 = offset / 2)
   const int64_t pairs = (n + 1) / 2;
   GRID_STRIDE(i, pairs) {
@@ -690,15 +762,17 @@ extern "C" int es_maxpool_fwd(const es_view_t* x, es_dtype_t dt, const void* xp,
     const unsigned grid = (unsigned)std::min<int64_t>((items + 255) / 256, 16384);
     if (dt == ES_BF16)
       hipLaunchKernelGGL(maxpool_fwd_nhwc<bf16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16*)xp,
-                         x->n, x->c, x->h, x->w, y->h, y->w, kh, kw, sh, sw, (bf16*)yp, idx);
+                         x->n, x->c, x->h, x->w, y->h, y->w, kh, kw, sh, sw, (bf16*)yp, idx, rows_of(x, y));
     else
       hipLaunchKernelGGL(maxpool_fwd_nhwc<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)xp,
-                         x->n, x->c, x->h, x->w, y->h, y->w, kh, kw, sh, sw, (float*)yp, idx);
+                         x->n, x->c, x->h, x->w, y->h, y->w, kh, kw, sh, sw, (float*)yp, idx, rows_of(x, y));
     ES_CHECK_LAUNCH();
     return ES_OK;
   }
+  View yv = mkview(y);
+  yv.rows = rows_of(x, y);
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
-                     mkview(x), xp, dt == ES_BF16, kh, kw, sh, sw, mkview(y), yp, idx);
+                     mkview(x), xp, dt == ES_BF16, kh, kw, sh, sw, yv, yp, idx);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
@@ -714,15 +788,17 @@ extern "C" int es_maxpool_bwd(const es_view_t* dy, es_dtype_t dt, const void* dy
     const unsigned grid = (unsigned)std::min<int64_t>((items + 255) / 256, 16384);
     if (dt == ES_BF16)
       hipLaunchKernelGGL(maxpool_bwd_nhwc<bf16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16*)dyp, idx,
-                         dx->n, dx->c, dx->h, dx->w, dy->h, dy->w, kh, kw, (bf16*)dxp, beta);
+                         dx->n, dx->c, dx->h, dx->w, dy->h, dy->w, kh, kw, (bf16*)dxp, beta, rows_of(dy, dx));
     else
       hipLaunchKernelGGL(maxpool_bwd_nhwc<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)dyp,
-                         idx, dx->n, dx->c, dx->h, dx->w, dy->h, dy->w, kh, kw, (float*)dxp, beta);
+                         idx, dx->n, dx->c, dx->h, dx->w, dy->h, dy->w, kh, kw, (float*)dxp, beta, rows_of(dy, dx));
     ES_CHECK_LAUNCH();
     return ES_OK;
   }
+  View dxv = mkview(dx);
+  dxv.rows = rows_of(dy, dx);
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
-                     mkview(dy), dyp, dt == ES_BF16, idx, kh, kw, sh, sw, mkview(dx), dxp, beta);
+                     mkview(dy), dyp, dt == ES_BF16, idx, kh, kw, sh, sw, dxv, dxp, beta);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
@@ -737,10 +813,10 @@ extern "C" int es_upsample_fwd(const es_view_t* x, es_dtype_t dt, const void* xp
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 16384);
   if (dt == ES_BF16)
     hipLaunchKernelGGL(upsample_fwd_nhwc<bf16>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16*)xp,
-                       x->h, x->w, x->c, hmap, wmap, (bf16*)yp, rows, y->h, y->w);
+                       x->h, x->w, x->c, hmap, wmap, (bf16*)yp, rows, y->h, y->w, y->n, rows_of(x, y));
   else
     hipLaunchKernelGGL(upsample_fwd_nhwc<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const float*)xp,
-                       x->h, x->w, x->c, hmap, wmap, (float*)yp, rows, y->h, y->w);
+                       x->h, x->w, x->c, hmap, wmap, (float*)yp, rows, y->h, y->w, y->n, rows_of(x, y));
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
@@ -754,7 +830,8 @@ extern "C" int es_upsample_bwd(const es_view_t* dxu, es_dtype_t dt, const void* 
     const int blocks = (int)std::min<int64_t>((rows * (dx->c / 4) + 255) / 256, 16384);
     hipStream_t st = (hipStream_t)stream;
 #define ES_UB(T, TO) hipLaunchKernelGGL((upsample_bwd_nhwc<T, TO>), dim3(blocks), dim3(256), 0, st, (const T*)dxup, \
-                                        dxu->h, dxu->w, dx->c, hstart, hcount, wstart, wcount, (TO*)dxp, rows, dx->h, dx->w, beta)
+                                        dxu->h, dxu->w, dx->c, hstart, hcount, wstart, wcount, (TO*)dxp, rows, dx->h, dx->w, beta, \
+                                        dx->n, rows_of(dxu, dx))
     if (dt == ES_BF16 && dxdt == ES_BF16) ES_UB(bf16, bf16);
     else if (dt == ES_BF16) ES_UB(bf16, float);
     else if (dxdt == ES_BF16) ES_UB(float, bf16);
@@ -763,8 +840,10 @@ extern "C" int es_upsample_bwd(const es_view_t* dxu, es_dtype_t dt, const void* 
     ES_CHECK_LAUNCH();
     return ES_OK;
   }
+  View dxv = mkview(dx);
+  dxv.rows = rows_of(dxu, dx);
   hipLaunchKernelGGL(upsample_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
-                     mkview(dxu), dxup, dt == ES_BF16, hstart, hcount, wstart, wcount, mkview(dx), dxp,
+                     mkview(dxu), dxup, dt == ES_BF16, hstart, hcount, wstart, wcount, dxv, dxp,
                      dxdt == ES_BF16, beta);
   ES_CHECK_LAUNCH();
   return ES_OK;
@@ -788,7 +867,9 @@ extern "C" int es_copy(const es_view_t* x, es_dtype_t xdt, const void* xp, const
 extern "C" int es_avgpool_fwd(const es_view_t* x, es_dtype_t dt, const void* xp, const es_view_t* y, void* yp,
                               es_stream_t stream) {
   const int waves = x->n * x->c;
-  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((waves + 3) / 4), dim3(256), 0, (hipStream_t)stream, mkview(x), xp,
+  View xv = mkview(x);
+  xv.rows = rows_of(x, y);
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((waves + 3) / 4), dim3(256), 0, (hipStream_t)stream, xv, xp,
                      dt == ES_BF16, mkview(y), yp);
   ES_CHECK_LAUNCH();
   return ES_OK;
@@ -808,24 +889,25 @@ extern "C" int es_gather_rows(const float* src, int64_t src_ld, const int32_t* i
   const int64_t total = (int64_t)rows * cols;
   if (total == 0) return ES_OK;
   hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, src, src_ld,
-                     idx, (const int32_t*)nullptr, rows, cols, dst, dst_ld);
+                     idx, (const int32_t*)nullptr, rows, cols, dst, dst_ld, (const int32_t*)nullptr);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
 
 extern "C" int es_gather_rows_at(const float* src, int64_t src_ld, const int32_t* perm, const int32_t* start,
-                                 int rows, int cols, float* dst, int64_t dst_ld, es_stream_t stream) {
+                                 int rows, int cols, float* dst, int64_t dst_ld, const int32_t* live,
+                                 es_stream_t stream) {
   const int64_t total = (int64_t)rows * cols;
   if (total == 0) return ES_OK;
   ES_CHECK_ARG(perm && start, "gather_rows_at: perm / start");
   hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, src, src_ld,
-                     perm, start, rows, cols, dst, dst_ld);
+                     perm, start, rows, cols, dst, dst_ld, live);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
 
 extern "C" int es_sn_power_iter(const float* w, int h, int wd, float* u, float* v, float* sigma, int update,
-                                es_stream_t stream) {
+                                const int32_t* active, es_stream_t stream) {
   // the caller's buffer: sigma[0], scratch [h + wd], then the snapshot of the u, v used [h + wd]
   // (1 + 2 (h + wd) floats)
   hipStream_t st = (hipStream_t)stream;
@@ -834,25 +916,26 @@ extern "C" int es_sn_power_iter(const float* w, int h, int wd, float* u, float* 
     float* vt = sigma + 1 + h;
     if (update) hipLaunchKernelGGL(sn_wtu_kernel, dim3((wd + 63) / 64), dim3(256), 0, st, w, h, wd, u, vt);
     hipLaunchKernelGGL(sn_wv_kernel, dim3((h + 3) / 4), dim3(256), 0, st, w, h, wd, update ? (const float*)vt : v,
-                       update, v, wv);
+                       update, v, wv, (const float*)v, active);
     hipLaunchKernelGGL(sn_final_kernel, dim3(1), dim3(256), 0, st, h, wd, (const float*)wv, u, (const float*)v, update,
-                       sigma, sigma + 1 + h + wd);
+                       sigma, sigma + 1 + h + wd, active);
   } else {
-    hipLaunchKernelGGL(sn_power_kernel, dim3(1), dim3(1024), 0, st, w, h, wd, u, v, sigma, update, sigma + 1);
+    hipLaunchKernelGGL(sn_power_kernel, dim3(1), dim3(1024), 0, st, w, h, wd, u, v, sigma, update, sigma + 1, active);
   }
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
 
 extern "C" int es_sn_power_iter_batch(int n, const float* const* w, const int* h, const int* wd, float* const* u,
-                                      float* const* v, float* const* buf, int update, es_stream_t stream) {
+                                      float* const* v, float* const* buf, int update, const int32_t* active,
+                                      es_stream_t stream) {
   ES_CHECK_ARG(n >= 1 && n <= ES_SN_BATCH_MAX, "sn_power_iter_batch: 1 <= n <= ES_SN_BATCH_MAX");
   SnJobs j{};
   for (int i = 0; i < n; ++i) {
     ES_CHECK_ARG((int64_t)h[i] * wd[i] < 16384, "sn_power_iter_batch: layer too large for one block");
     j.w[i] = w[i]; j.u[i] = u[i]; j.v[i] = v[i]; j.buf[i] = buf[i]; j.h[i] = h[i]; j.wd[i] = wd[i];
   }
-  hipLaunchKernelGGL(sn_power_batch_kernel, dim3(n), dim3(1024), 0, (hipStream_t)stream, j, update);
+  hipLaunchKernelGGL(sn_power_batch_kernel, dim3(n), dim3(1024), 0, (hipStream_t)stream, j, update, active);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
@@ -906,11 +989,12 @@ extern "C" int es_adam(float* p, const float* g, float* m, float* v, int64_t n, 
 }
 
 extern "C" int es_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
-                           float beta2, float eps, const int32_t* step_ptr, float grad_scale, es_stream_t stream) {
+                           float beta2, float eps, const int32_t* step_ptr, float grad_scale, const int32_t* active,
+                           es_stream_t stream) {
   ES_CHECK_ARG(step_ptr != nullptr, "adam_dev: step_ptr is NULL");
   if (n == 0) return ES_OK;
   hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr, beta1,
-                     beta2, eps, step_ptr, grad_scale);
+                     beta2, eps, step_ptr, grad_scale, active);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
@@ -930,7 +1014,17 @@ extern "C" int es_randn_dev(float* out, int64_t n, uint64_t seed, uint32_t strea
   if (n == 0) return ES_OK;
   ES_CHECK_ARG(offset >= 0 && offset % 2 == 0, "randn: offset %lld must be even and >= 0", (long long)offset);
   hipLaunchKernelGGL(randn_kernel, dim3(grid_for((n + 1) / 2)), dim3(256), 0, (hipStream_t)stream, out, n, seed,
-                     stream_id, step_ptr, step_mul, offset / 2);
+                     stream_id, step_ptr, step_mul, offset / 2, (const int32_t*)nullptr, (int64_t)0);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+extern "C" int es_randn_dev_at(float* out, int64_t n, uint64_t seed, uint32_t stream_id, const int32_t* step_ptr,
+                               int32_t step_mul, int64_t offset, const int32_t* off_ptr, int64_t off_mul,
+                               es_stream_t stream) {
+  if (n == 0) return ES_OK;
+  ES_CHECK_ARG(offset >= 0 && offset % 2 == 0 && off_mul % 2 == 0, "randn_dev_at: even offsets required");
+  hipLaunchKernelGGL(randn_kernel, dim3(grid_for((n + 1) / 2)), dim3(256), 0, (hipStream_t)stream, out, n, seed,
+                     stream_id, step_ptr, step_mul, offset / 2, off_ptr, off_mul / 2);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
@@ -953,7 +1047,33 @@ extern "C" int es_rand_exponential(float* out, int64_t n, uint64_t seed, uint32_
 }
 
 extern "C" int es_counter_add(int32_t* counter, int32_t v, es_stream_t stream) {
-  hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, counter, v);
+  return es_counter_add_if(counter, v, nullptr, stream);
+}
+extern "C" int es_counter_add_if(int32_t* counter, int32_t v, const int32_t* flag, es_stream_t stream) {
+  hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, counter, v, flag);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+extern "C" int es_counter_add_i64_if(int64_t* counter, int64_t v, const int32_t* flag, es_stream_t stream) {
+  hipLaunchKernelGGL(counter_add_i64_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, counter, v, flag);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+extern "C" int es_expert_plan(const int32_t* counts, const int32_t* counts_all, int world, int rank, int E, int B,
+                              int min_local, int32_t* rows, int32_t* active, int32_t* n0, float* w, float* gcnt,
+                              float* lcnt, es_stream_t stream) {
+  ES_CHECK_ARG(counts && rows && active && n0 && w && gcnt && lcnt && E >= 1 && E <= 1024 && B >= 1,
+               "expert_plan: bad arguments");
+  ES_CHECK_ARG(counts_all == nullptr || (world >= 1 && rank >= 0 && rank < world), "expert_plan: world / rank");
+  hipLaunchKernelGGL(expert_plan_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, counts, counts_all, world, rank,
+                     E, B, min_local, rows, active, n0, w, gcnt, lcnt);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+extern "C" int es_div_by(float* x, int n, const float* d, es_stream_t stream) {
+  ES_CHECK_ARG(x && d && n >= 0, "div_by: bad arguments");
+  if (n == 0) return ES_OK;
+  hipLaunchKernelGGL(div_by_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, x, n, d);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
@@ -963,4 +1083,20 @@ extern "C" int es_dropout_mask(uint8_t* out, int64_t n, const es_dropout_t* d, e
   hipLaunchKernelGGL(dropout_mask_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, out, n, *d);
   ES_CHECK_LAUNCH();
   return ES_OK;
+}
+
+// ABI check: sizeof of the structs the bindings mirror (0 view, 1 dropout, 2 conv desc, 3 norm,
+// 4 chain, 5 gen loss, 6 dfront2 params, 7 dmlp params); -1 for an unknown index
+extern "C" int64_t es_struct_size(int which) {
+  switch (which) {
+    case 0: return sizeof(es_view_t);
+    case 1: return sizeof(es_dropout_t);
+    case 2: return sizeof(es_conv_desc_t);
+    case 3: return sizeof(es_norm_t);
+    case 4: return sizeof(es_chain_t);
+    case 5: return sizeof(es_gen_loss_t);
+    case 6: return sizeof(es_dfront2_params_t);
+    case 7: return sizeof(es_dmlp_params_t);
+    default: return -1;
+  }
 }

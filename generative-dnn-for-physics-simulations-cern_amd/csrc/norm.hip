@@ -52,16 +52,31 @@ namespace {
 struct View {
   int n, c, h, w;
   int64_t s[4];
+  const int32_t* rows;   // dynamic rows: device count of the live samples (es_view_t.rows)
   __device__ __forceinline__ int64_t off(int in, int ic, int ih, int iw) const {
     return in * s[0] + ic * s[1] + ih * s[2] + iw * s[3];
   }
+  __device__ __forceinline__ int live() const { return live_rows(rows, n); }
 };
 View mkview(const es_view_t* v) {
   View r;
   r.n = v->n; r.c = v->c; r.h = v->h; r.w = v->w;
   for (int i = 0; i < 4; ++i) r.s[i] = v->s[i];
+  r.rows = v->rows;
   return r;
 }
+
+// A reduction's element count: c, or with dynamic rows (rows != NULL) c scaled to the live
+// samples of the n-sample capacity (c = n * per-sample count)
+struct Cnt {
+  float c;
+  const int32_t* rows;
+  int n;
+  __device__ __forceinline__ float get() const {
+    return rows ? (float)live_rows(rows, n) * (c / (float)n) : c;
+  }
+};
+Cnt mkcnt(float c, const es_view_t* v = nullptr) { return Cnt{c, v ? v->rows : nullptr, v ? v->n : 1}; }
 
 __device__ __forceinline__ float ldf(const void* p, int bf, int64_t i) {
   return bf ? (float)((const bf16*)p)[i] : ((const float*)p)[i];
@@ -185,6 +200,7 @@ __global__ void __launch_bounds__(256) colred_kernel(BwdIn b, int64_t rows, int6
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
   const int64_t r0 = blockIdx.y * rows_per_chunk;
+  if (v.rows) rows = (int64_t)v.live() * v.h * v.w;
   const int64_t r1 = min(rows, r0 + rows_per_chunk);
   float cnt = 0.f, a = 0.f, m2 = 0.f;   // STATS: Welford (cnt, mean, M2); BWD/SUM: (., s1, s2)
   if (c < C) {
@@ -236,6 +252,11 @@ __global__ void __launch_bounds__(256) colred_kernel(BwdIn b, int64_t rows, int6
 // BN stats finalize: merge chunk partials -> mean/invstd, running stats (torch semantics).
 __device__ __forceinline__ void bn_stats_store(int c, double n_, double s1, double s2, float eps, float* mean,
                                                float* invstd, float* rmean, float* rvar, float mom) {
+  if (n_ <= 0.0) {   // no live sample (dynamic rows): finite statistics, running stats untouched
+    mean[c] = 0.f;
+    invstd[c] = (float)(1.0 / sqrt((double)eps));
+    return;
+  }
   const double mt = s1 / n_;
   const double Mt = fmax(s2 - n_ * mt * mt, 0.0);
   const double var = Mt / n_;
@@ -261,6 +282,11 @@ __global__ void bn_finalize_kernel(const float* part, int chunks, int C, float e
     mu += dl * nb / nt;
     M += Mb + dl * dl * n_ * nb / nt;
     n_ = nt;
+  }
+  if (n_ <= 0.0) {   // no live sample (dynamic rows): finite statistics, running stats untouched
+    mean[c] = 0.f;
+    invstd[c] = (float)(1.0 / sqrt((double)eps));
+    return;
   }
   const double var = M / n_;
   mean[c] = (float)mu;
@@ -399,15 +425,16 @@ __global__ void __launch_bounds__(FIN_T) bn_finalize_block_kernel(const float* p
 }
 
 // out1 (+)= s1 (beta1: scale of old out1), out2 += s2; a1/a2 = gamma*s/cnt (BN backward)
-__device__ __forceinline__ void sums_store(int c, float s1, float s2, float cnt, const float* gamma, float* a1,
+__device__ __forceinline__ void sums_store(int c, float s1, float s2, Cnt cn, const float* gamma, float* a1,
                                            float* a2, float* out1, float* out2, float beta1) {
   const float g = gamma ? gamma[c] : 1.f;
+  const float cnt = fmaxf(cn.get(), 1.f);
   if (a1) { a1[c] = g * s1 / cnt; a2[c] = g * s2 / cnt; }
   if (out1) out1[c] = (beta1 != 0.f ? beta1 * out1[c] : 0.f) + s1;
   if (out2) out2[c] += s2;
 }
 
-__global__ void __launch_bounds__(FIN_T) sums_finalize_block_kernel(const float* part, int chunks, int C, float cnt,
+__global__ void __launch_bounds__(FIN_T) sums_finalize_block_kernel(const float* part, int chunks, int C, Cnt cnt,
                                                                     const float* gamma, float* a1, float* a2,
                                                                     float* out1, float* out2, float beta1) {
   const int c = blockIdx.x;
@@ -435,7 +462,7 @@ __global__ void __launch_bounds__(FIN_T) sums_finalize_block_kernel(const float*
 }
 
 // thread-per-channel form of the same (few chunks, or many channels: coalesced across channels)
-__global__ void __launch_bounds__(256) sums_finalize_kernel(const float* part, int chunks, int C, float cnt,
+__global__ void __launch_bounds__(256) sums_finalize_kernel(const float* part, int chunks, int C, Cnt cnt,
                                                             const float* gamma, float* a1, float* a2, float* out1,
                                                             float* out2, float beta1) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -471,7 +498,7 @@ void launch_bn_finalize(hipStream_t st, const float* part, int chunks, int C, fl
                        invstd, rmean, rvar, mom);
 }
 
-void launch_sums_finalize(hipStream_t st, const float* part, int chunks, int C, float cnt, const float* gamma,
+void launch_sums_finalize(hipStream_t st, const float* part, int chunks, int C, Cnt cnt, const float* gamma,
                           float* a1, float* a2, float* out1, float* out2, float beta1) {
   if (fin_block(chunks, C))
     hipLaunchKernelGGL(sums_finalize_block_kernel, dim3(C), dim3(FIN_T), 0, st, part, chunks, C, cnt, gamma, a1, a2,
@@ -502,7 +529,7 @@ __global__ void gn_finalize_kernel(const float* part, int N, int chunks, int C, 
     }
   }
   mean[i] = (float)mu;
-  invstd[i] = (float)(1.0 / sqrt(M / n_ + (double)eps));
+  invstd[i] = (float)(1.0 / sqrt((n_ > 0.0 ? M / n_ : 0.0) + (double)eps));   // (padding samples: n_ = 0)
 }
 
 // GroupNorm backward finalize from fast partials: a1/a2[n, g] = mean over the group of gamma*s
@@ -536,6 +563,7 @@ __global__ void __launch_bounds__(256) sum1_kernel(BwdIn b, int rows, float* par
   const View& v = b.x;
   __shared__ float sh[8];
   float s = 0.f;
+  if (v.rows) rows = v.live() * v.h * v.w;
   for (int r = blockIdx.x * 256 + threadIdx.x; r < rows; r += gridDim.x * 256) {
     const uint32_t t = (uint32_t)r / (uint32_t)v.w;
     const int w = r - (int)t * v.w, h = t % (uint32_t)v.h, n = t / (uint32_t)v.h;
@@ -554,6 +582,10 @@ __global__ void __launch_bounds__(256) segred_kernel(BwdIn b, float eps, float* 
   const int G = b.nm.kind == ES_NORM_GN ? b.nm.groups : 1;
   const int cg = v.c / G;
   const int n = blockIdx.x / G, g = blockIdx.x % G;
+  if (n >= v.live()) {   // a padding sample (dynamic rows): finite statistics, zero sums
+    if (threadIdx.x == 0) { o1[blockIdx.x] = 0.f; o2[blockIdx.x] = RED == RED_STATS ? rsqrtf(eps) : 0.f; }
+    return;
+  }
   const int64_t cnt = (int64_t)cg * v.h * v.w;
   const bool cl = v.s[1] == 1 && cg > 1;
   __shared__ float sh[8];
@@ -602,7 +634,8 @@ struct FwdArgs {
 
 __global__ void __launch_bounds__(256) norm_fwd_kernel(FwdArgs a) {
   resolve_stream(a.ch.drop);
-  const int64_t total = (int64_t)a.x.n * a.x.c * a.x.h * a.x.w;
+  // (both element orders have n slowest: the live samples' elements are a prefix)
+  const int64_t total = (int64_t)a.x.live() * a.x.c * a.x.h * a.x.w;
   const bool cl = a.x.s[1] == 1 && a.x.c > 1;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     int n, c, h, w;
@@ -625,7 +658,7 @@ struct BwdApply {
 __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(BwdApply a) {
   resolve_stream(a.b.ch.drop);
   const View& v = a.b.x;
-  const int64_t total = (int64_t)v.n * v.c * v.h * v.w;
+  const int64_t total = (int64_t)v.live() * v.c * v.h * v.w;
   const bool cl = v.s[1] == 1 && v.c > 1;
   __shared__ float sacc[1024];
   if (a.csum) {
@@ -670,7 +703,7 @@ BwdIn mk_bwdin(const es_view_t* x, es_dtype_t xdt, const void* xp, const es_norm
 // dsum += sum of the fast apply's per-block partials (s1 slot of [chunk][3][C])
 void fast_dsum_finalize(int C, int chunks, const float* part, float* dsum, hipStream_t st) {
   if (chunks <= 0 || dsum == nullptr) return;
-  launch_sums_finalize(st, part, chunks, C, 1.f, nullptr, (float*)nullptr, (float*)nullptr, dsum, (float*)nullptr, 1.f);
+  launch_sums_finalize(st, part, chunks, C, mkcnt(1.f), nullptr, (float*)nullptr, (float*)nullptr, dsum, (float*)nullptr, 1.f);
 }
 
 int64_t stats_groups(const es_view_t* x, int kind, int groups) {
@@ -714,9 +747,11 @@ __global__ void __launch_bounds__(256) stats_merge_kernel(const float* part, int
 }
 
 // a1 = gamma*s1/cnt, a2 = gamma*s2/cnt from (all-reduced) raw backward sums [2][C]
-__global__ void bn_scale_sums_kernel(const float* sums, int C, float cnt, const float* gamma, float* a1, float* a2) {
+__global__ void bn_scale_sums_kernel(const float* sums, int C, float cnt, const float* cnt_mul, const float* gamma,
+                                     float* a1, float* a2) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
+  if (cnt_mul) cnt *= fmaxf(cnt_mul[0], 1.f);   // device sample count x per-sample elements
   const float g = gamma ? gamma[c] : 1.f;
   a1[c] = g * sums[c] / cnt;
   a2[c] = g * sums[C + c] / cnt;
@@ -861,7 +896,7 @@ extern "C" int es_norm_act_bwd(const es_view_t* x, es_dtype_t xdt, const void* x
                        nm->gamma, g1, g2);
     if (dgamma || dbeta) {
       const int allc = x->n * fchunks;   // per-channel sums over every (n, chunk) partial
-      launch_sums_finalize(st, (const float*)part, allc, x->c, 1.f, nullptr, (float*)nullptr, (float*)nullptr, dbeta, dgamma, 1.f);
+      launch_sums_finalize(st, (const float*)part, allc, x->c, mkcnt(1.f), nullptr, (float*)nullptr, (float*)nullptr, dbeta, dgamma, 1.f);
     }
     if (dxp) fast_dsum_finalize(x->c, es_fast_norm_bwd_apply(x, fk, xdt, xp, dyp, dxp, nm, ch, g1, g2, dsum, part, st),
                                 part, dsum, st);
@@ -870,7 +905,7 @@ extern "C" int es_norm_act_bwd(const es_view_t* x, es_dtype_t xdt, const void* x
   }
   if (fast) {
     const int fchunks = es_fast_norm_bwd_reduce(x, 0, xdt, xp, dyp, nm, ch, part, st);
-    launch_sums_finalize(st, (const float*)part, fchunks, x->c, (float)rows, nm->gamma, g1, g2, dbeta, dgamma, 1.f);
+    launch_sums_finalize(st, (const float*)part, fchunks, x->c, mkcnt((float)rows, x), nm->gamma, g1, g2, dbeta, dgamma, 1.f);
     if (dxp) fast_dsum_finalize(x->c, es_fast_norm_bwd_apply(x, 0, xdt, xp, dyp, dxp, nm, ch, g1, g2, dsum, part, st),
                                 part, dsum, st);
     ES_CHECK_LAUNCH();
@@ -878,13 +913,13 @@ extern "C" int es_norm_act_bwd(const es_view_t* x, es_dtype_t xdt, const void* x
   }
   if (kind == ES_NORM_BN) {
     hipLaunchKernelGGL(colred_kernel<RED_BWD>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, part);
-    launch_sums_finalize(st, (const float*)part, chunks, x->c, (float)rows, nm->gamma, g1, g2, dbeta, dgamma, 1.f);
+    launch_sums_finalize(st, (const float*)part, chunks, x->c, mkcnt((float)rows, x), nm->gamma, g1, g2, dbeta, dgamma, 1.f);
     ap.a1 = g1; ap.a2 = g2;
   } else if (kind == ES_NORM_GN || kind == ES_NORM_LN) {
     hipLaunchKernelGGL(segred_kernel<RED_BWD>, dim3((unsigned)ng), dim3(256), 0, st, b, 0.f, g1, g2);
     if (dgamma || dbeta) {
       hipLaunchKernelGGL(colred_kernel<RED_BWD>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, part);
-      launch_sums_finalize(st, (const float*)part, chunks, x->c, (float)rows, nullptr, (float*)nullptr, (float*)nullptr, dbeta, dgamma, 1.f);
+      launch_sums_finalize(st, (const float*)part, chunks, x->c, mkcnt(1.f), nullptr, (float*)nullptr, (float*)nullptr, dbeta, dgamma, 1.f);
     }
     ap.a1 = g1; ap.a2 = g2;
   }
@@ -914,7 +949,7 @@ extern "C" int es_norm_act_bwd_sums(const es_view_t* x, es_dtype_t xdt, const vo
   float* part = (float*)ws;
   float* g1 = part + part_floats;
   float* g2 = g1 + x->c;
-  launch_sums_finalize(st, sums_part, chunks, x->c, (float)rows, nm->gamma, g1, g2, dbeta, dgamma, 1.f);
+  launch_sums_finalize(st, sums_part, chunks, x->c, mkcnt((float)rows, x), nm->gamma, g1, g2, dbeta, dgamma, 1.f);
   fast_dsum_finalize(x->c, es_fast_norm_bwd_apply(x, 0, xdt, xp, dyp, dxp, nm, ch, g1, g2, dsum, part, st), part,
                      dsum, st);
   ES_CHECK_LAUNCH();
@@ -940,13 +975,13 @@ extern "C" int es_channel_sum(const es_view_t* x, es_dtype_t xdt, const void* xp
     const int nb = std::min<int>(chunks, (int)((rows + 255) / 256));
     hipLaunchKernelGGL(sum1_kernel, dim3(nb), dim3(256), 0, st, b, (int)rows, (float*)ws);
     // (a single thread summing thousands of partials took ~75 us: a block for nb > 32)
-    launch_sums_finalize(st, (const float*)ws, nb, 1, 1.f, nullptr, (float*)nullptr, (float*)nullptr, out,
+    launch_sums_finalize(st, (const float*)ws, nb, 1, mkcnt(1.f), nullptr, (float*)nullptr, (float*)nullptr, out,
                          (float*)nullptr, beta);
     ES_CHECK_LAUNCH();
     return ES_OK;
   }
   hipLaunchKernelGGL(colred_kernel<RED_SUM>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, (float*)ws);
-  launch_sums_finalize(st, (const float*)ws, chunks, x->c, 1.f, nullptr, (float*)nullptr, (float*)nullptr, out, (float*)nullptr, beta);
+  launch_sums_finalize(st, (const float*)ws, chunks, x->c, mkcnt(1.f), nullptr, (float*)nullptr, (float*)nullptr, out, (float*)nullptr, beta);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
@@ -980,7 +1015,8 @@ extern "C" int es_norm_stats_local(const es_view_t* x, es_dtype_t xdt, const voi
 extern "C" int es_norm_bwd_sync(int phase, const es_view_t* x, es_dtype_t xdt, const void* xp, const es_norm_t* nm,
                                 const es_chain_t* ch, const es_view_t* dy, es_dtype_t dydt, const void* dyp,
                                 const es_view_t* dx, es_dtype_t dxdt, void* dxp, float* sums, float cnt,
-                                float* dgamma, float* dbeta, float* dsum, void* ws, es_stream_t stream) {
+                                const float* cnt_mul, float* dgamma, float* dbeta, float* dsum, void* ws,
+                                es_stream_t stream) {
   hipStream_t st = (hipStream_t)stream;
   ES_CHECK_ARG(nm && nm->kind == ES_NORM_BN, "norm_bwd_sync: BatchNorm only");
   ES_CHECK_ARG(phase == 0 || phase == 1, "norm_bwd_sync: phase 0 (sums) or 1 (apply)");
@@ -1004,13 +1040,13 @@ extern "C" int es_norm_bwd_sync(int phase, const es_view_t* x, es_dtype_t xdt, c
     else
       hipLaunchKernelGGL(colred_kernel<RED_BWD>, dim3(cb, chunks), dim3(256), 0, st, b, rows, per, part);
     // raw per-channel sums s1 = sum dnorm, s2 = sum dnorm*xhat (+ the local dbeta / dgamma)
-    launch_sums_finalize(st, (const float*)part, nchunks, x->c, 1.f, nullptr, sums, sums + x->c, dbeta, dgamma, 1.f);
+    launch_sums_finalize(st, (const float*)part, nchunks, x->c, mkcnt(1.f), nullptr, sums, sums + x->c, dbeta, dgamma, 1.f);
     ES_CHECK_LAUNCH();
     return ES_OK;
   }
   ES_CHECK_ARG(cnt > 0.f && dxp != nullptr, "norm_bwd_sync: apply needs cnt > 0 and dx");
   hipLaunchKernelGGL(bn_scale_sums_kernel, dim3((x->c + 255) / 256), dim3(256), 0, st, (const float*)sums, x->c,
-                     cnt, nm->gamma, g1, g2);
+                     cnt, cnt_mul, nm->gamma, g1, g2);
   if (fast) {
     fast_dsum_finalize(x->c, es_fast_norm_bwd_apply(x, 0, xdt, xp, dyp, dxp, nm, ch, g1, g2, dsum, part, st),
                        part, dsum, st);

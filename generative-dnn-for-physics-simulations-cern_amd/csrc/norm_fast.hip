@@ -67,6 +67,7 @@ struct FastArgs {
   int dfirst, act;
   float slope;
   uint8_t* keep;                              // dropout keep bits [rows][C/8] (written fwd, read bwd)
+  const int32_t* nrows;                       // dynamic rows: device count of the live samples (es_view_t.rows)
 };
 
 __device__ __forceinline__ float actf(const FastArgs& a, float v) {
@@ -313,7 +314,9 @@ __device__ __forceinline__ Geo geo(const FastArgs& a) {
   g.active = g.rg < g.RGB && g.cv < g.CV;
   g.c0 = g.cv * 8;
   g.rbase = (int)blockIdx.z * a.zrows;
-  g.rlim = min(a.rows, g.rbase + a.zrows);
+  // rows of the live samples (a prefix: rows are sample-major); GN slices past them are empty
+  const int rl = a.nrows ? live_rows(a.nrows, a.rows / a.HW) * a.HW : a.rows;
+  g.rlim = min(rl, g.rbase + a.zrows);
   return g;
 }
 
@@ -638,6 +641,7 @@ static FastArgs mk(const es_view_t* v, const es_chain_t* ch, int G) {
   a.G = G;
   a.cg = G ? v->c / G : 1;
   a.zrows = G ? a.HW : a.rows;
+  a.nrows = v->rows;
   if (ch) {
     a.drop = ch->drop; a.dfirst = ch->dropout_first; a.act = ch->act; a.slope = ch->slope;
     a.keep = ch->drop.enabled ? ch->keep : nullptr;

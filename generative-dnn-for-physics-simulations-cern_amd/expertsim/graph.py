@@ -1,4 +1,4 @@
-"""HIP-graph capture of one ``MoEWrapper.train_step`` (single process, n_experts == 1).
+"""HIP-graph capture of one ``MoEWrapper.train_step``.
 
 The step is ~600 kernel launches issued from Python; once the kernels are fast, the host issue
 time shows up as idle gaps on the GPU.  A captured graph replays the whole step with one launch.
@@ -10,30 +10,47 @@ next training step:
   * both counters are advanced by kernels inside the step.
 Inputs are the static tensors passed at capture time: copy new batches into them before replay.
 
-Data parallel (RCCL process group, n_experts == 1): the step's collectives -- the SyncBN
-statistics / backward-sum reductions, the bucketed gradient all-reduces on the process group's
-stream (joined back by ``wait``) and the metric all-gather -- are captured into the same graph, so a
-replay issues no host work and no host synchronisation (the global counts of E = 1 are known on the
-host without a collective, ``DataParallel.global_groups``).  Every rank must capture and replay in
-lockstep (same step count), as it issues the same collectives in the same order.
+Several experts: the step runs on dynamic rows (the expert sizes and the reference's ``B_e <= 1``
+skip rule are read on the device, MoEWrapper._plan), so it captures like a single-expert step; one
+process forks the experts' programs onto their own streams inside the graph.
 
-Not captured: n_experts > 1 (the expert sizes are read on the host for the reference's
-``B_e <= 1`` skip rule) and gloo process groups (their collectives go through the host).
+Data parallel (RCCL process group): the step's collectives -- the expert counts' all-gather, the
+SyncBN statistics / backward-sum reductions, the bucketed gradient all-reduces on the process
+group's stream (joined back by ``wait``) and the metric all-gather -- are captured into the same
+graph, so a replay issues no host work and no host synchronisation.  Every rank must capture and
+replay in lockstep (same step count, equal shard sizes), as it issues the same collectives in the
+same order: with more than one rank the capture is opt-in (``allow_dp``) and checks the shard sizes.
+
+Not captured: gloo process groups (their collectives go through the host).
 """
 from __future__ import annotations
 
 import torch
 
 
-def graph_supported(moe) -> bool:
-    """True when ``moe.train_step`` issues no host synchronisation and can be captured."""
-    return moe.n_experts == 1 and (moe.ddp is None or not moe.ddp.gloo)
+def graph_supported(moe, allow_dp: bool = False) -> bool:
+    """True when ``moe.train_step`` issues no host synchronisation and can be captured: one process,
+    or an RCCL group of one rank, or (``allow_dp``: the caller keeps the ranks in lockstep) several."""
+    if moe.ddp is None:
+        return True
+    if moe.ddp.gloo:
+        return False
+    return moe.ddp.world == 1 or allow_dp
 
 
 class StepGraph:
-    def __init__(self, moe, step_args, warmup: int = 2):
-        if not graph_supported(moe):
-            raise ValueError("StepGraph captures single-expert train steps (single process or RCCL data parallel)")
+    def __init__(self, moe, step_args, warmup: int = 2, allow_dp: bool = False):
+        if not graph_supported(moe, allow_dp):
+            raise ValueError("StepGraph: gloo groups are not captured; more than one RCCL rank needs allow_dp=True")
+        if moe.ddp is not None and moe.ddp.world > 1:
+            # the ranks' captured collectives must match: equal local batches (one check at capture)
+            import torch.distributed as dist
+            b = torch.tensor([int(step_args[1].shape[0])], dtype=torch.int64, device=step_args[1].device)
+            allb = [torch.zeros_like(b) for _ in range(moe.ddp.world)]
+            dist.all_gather(allb, b, group=moe.ddp.group)
+            sizes = [int(x.item()) for x in allb]
+            if len(set(sizes)) != 1:
+                raise ValueError(f"StepGraph: unequal local batch sizes across ranks {sizes}")
         self.moe = moe
         self.args = tuple(step_args)
         torch.cuda.synchronize()

@@ -23,20 +23,22 @@ NORM_NONE, NORM_BN, NORM_GN, NORM_LN = 0, 1, 2, 3
 
 
 class View(C.Structure):
-    _fields_ = [("n", C.c_int), ("c", C.c_int), ("h", C.c_int), ("w", C.c_int), ("s", C.c_int64 * 4)]
+    _fields_ = [("n", C.c_int), ("c", C.c_int), ("h", C.c_int), ("w", C.c_int), ("s", C.c_int64 * 4),
+                ("rows", C.c_void_p)]
 
 
 class Dropout(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("stream", C.c_uint32), ("threshold", C.c_uint32),
                 ("scale", C.c_float), ("enabled", C.c_int), ("step_ptr", C.c_void_p), ("step_mul", C.c_int32),
-                ("index_offset", C.c_uint64)]
+                ("index_offset", C.c_uint64), ("index_ptr", C.c_void_p), ("index_mul", C.c_int64)]
 
 
 class ConvDesc(C.Structure):
     _fields_ = [("N", C.c_int), ("C", C.c_int), ("H", C.c_int), ("W", C.c_int), ("Hu", C.c_int),
                 ("Wu", C.c_int), ("K", C.c_int), ("P", C.c_int), ("Q", C.c_int), ("R", C.c_int),
                 ("S", C.c_int), ("stride", C.c_int), ("pad", C.c_int), ("hmap", C.c_void_p),
-                ("wmap", C.c_void_p), ("up_h", C.c_int), ("up_w", C.c_int), ("subpixel", C.c_int)]
+                ("wmap", C.c_void_p), ("up_h", C.c_int), ("up_w", C.c_int), ("subpixel", C.c_int),
+                ("rows", C.c_void_p)]
 
 
 class Norm(C.Structure):
@@ -51,21 +53,23 @@ class Chain(C.Structure):
 
 class GenLoss(C.Structure):
     _fields_ = [("n", C.c_int), ("latent", C.c_int), ("noise", C.c_int), ("di_strength", C.c_float),
-                ("in_strength", C.c_float), ("aux_strength", C.c_float), ("std_mean", C.c_void_p)]
+                ("in_strength", C.c_float), ("aux_strength", C.c_float), ("std_mean", C.c_void_p),
+                ("rows", C.c_void_p)]
 
 
 class DFront2Params(C.Structure):
     _fields_ = [("w1", C.c_void_p), ("sigma1", C.c_void_p), ("b1", C.c_void_p), ("g1", C.c_void_p),
                 ("be1", C.c_void_p), ("w2", C.c_void_p), ("sigma2", C.c_void_p), ("b2", C.c_void_p),
                 ("g2", C.c_void_p), ("be2", C.c_void_p), ("eps1", C.c_float), ("eps2", C.c_float),
-                ("slope", C.c_float), ("ph", C.c_int), ("pw", C.c_int)]
+                ("slope", C.c_float), ("ph", C.c_int), ("pw", C.c_int), ("rows", C.c_void_p)]
 
 
 class DMlpParams(C.Structure):
     _fields_ = [("w1", C.c_void_p), ("sigma1", C.c_void_p), ("b1", C.c_void_p), ("g1", C.c_void_p),
                 ("be1", C.c_void_p), ("w2", C.c_void_p), ("sigma2", C.c_void_p), ("b2", C.c_void_p),
                 ("g2", C.c_void_p), ("be2", C.c_void_p), ("w3", C.c_void_p), ("sigma3", C.c_void_p),
-                ("b3", C.c_void_p), ("eps1", C.c_float), ("eps2", C.c_float), ("slope", C.c_float)]
+                ("b3", C.c_void_p), ("eps1", C.c_float), ("eps2", C.c_float), ("slope", C.c_float),
+                ("rows", C.c_void_p)]
 
 
 P = C.c_void_p
@@ -114,7 +118,7 @@ _SIGS = {
     "es_norm_stats_merge": (C.c_int, [P, C.c_int, C.c_int, P, P]),
     "es_norm_stats_local": (C.c_int, [P, C.c_int, P, P, P, P]),
     "es_norm_bwd_sync": (C.c_int, [C.c_int, P, C.c_int, P, P, P, P, C.c_int, P, P, C.c_int, P, P, C.c_float, P, P,
-                                   P, P, P]),
+                                   P, P, P, P]),
     "es_act_fwd": (C.c_int, [P, C.c_int, P, P, P, C.c_int, P, P]),
     "es_channel_sum_ws_bytes": (I64, [P]),
     "es_channel_sum": (C.c_int, [P, C.c_int, P, P, C.c_float, P, P]),
@@ -142,13 +146,13 @@ _SIGS = {
     "es_avgpool_fwd": (C.c_int, [P, C.c_int, P, P, P, P]),
     "es_avgpool_bwd": (C.c_int, [P, P, P, C.c_int, P, C.c_float, P]),
     "es_gather_rows": (C.c_int, [P, I64, P, C.c_int, C.c_int, P, I64, P]),
-    "es_gather_rows_at": (C.c_int, [P, I64, P, P, C.c_int, C.c_int, P, I64, P]),
-    "es_scatter_rows_at": (C.c_int, [P, P, P, C.c_int, P, P]),
-    "es_sn_power_iter": (C.c_int, [P, C.c_int, C.c_int, P, P, P, C.c_int, P]),
-    "es_sn_power_iter_batch": (C.c_int, [C.c_int, P, P, P, P, P, P, C.c_int, P]),
+    "es_gather_rows_at": (C.c_int, [P, I64, P, P, C.c_int, C.c_int, P, I64, P, P]),
+    "es_scatter_rows_at": (C.c_int, [P, P, P, C.c_int, P, P, P]),
+    "es_sn_power_iter": (C.c_int, [P, C.c_int, C.c_int, P, P, P, C.c_int, P, P]),
+    "es_sn_power_iter_batch": (C.c_int, [C.c_int, P, P, P, P, P, P, C.c_int, P, P]),
     "es_sn_bwd_batch": (C.c_int, [C.c_int, P, P, P, P, P, P, P, P, C.c_float, P]),
     "es_sn_bwd": (C.c_int, [P, P, C.c_int, C.c_int, P, P, P, P, C.c_float, P]),
-    "es_hinge_d": (C.c_int, [P, P, C.c_int, P, P, P, P, P]),
+    "es_hinge_d": (C.c_int, [P, P, C.c_int, P, P, P, P, P, P]),
     "es_image_expsum": (C.c_int, [P, C.c_int, P, P, P]),
     "es_channel_sums": (C.c_int, [P, C.c_int, P, C.c_int, P, P]),
     "es_gen_losses": (C.c_int, [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
@@ -164,13 +168,19 @@ _SIGS = {
     "es_scatter_rows": (C.c_int, [P, P, C.c_int, P, P]),
     "es_adam": (C.c_int, [P, P, P, P, I64, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int,
                           C.c_float, P]),
-    "es_adam_dev": (C.c_int, [P, P, P, P, I64, C.c_float, C.c_float, C.c_float, C.c_float, P, C.c_float, P]),
+    "es_adam_dev": (C.c_int, [P, P, P, P, I64, C.c_float, C.c_float, C.c_float, C.c_float, P, C.c_float, P, P]),
     "es_ema_update": (C.c_int, [P, P, I64, C.c_float, C.c_float, P]),
     "es_randn": (C.c_int, [P, I64, C.c_uint64, C.c_uint32, P]),
     "es_rand_exponential": (C.c_int, [P, I64, C.c_uint64, C.c_uint32, P]),
     "es_randn_dev": (C.c_int, [P, I64, C.c_uint64, C.c_uint32, P, C.c_int32, I64, P]),
     "es_rand_exponential_dev": (C.c_int, [P, I64, C.c_uint64, C.c_uint32, P, C.c_int32, I64, P]),
     "es_counter_add": (C.c_int, [P, C.c_int32, P]),
+    "es_randn_dev_at": (C.c_int, [P, I64, C.c_uint64, C.c_uint32, P, C.c_int32, I64, P, I64, P]),
+    "es_counter_add_if": (C.c_int, [P, C.c_int32, P, P]),
+    "es_counter_add_i64_if": (C.c_int, [P, I64, P, P]),
+    "es_expert_plan": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P, P, P]),
+    "es_div_by": (C.c_int, [P, C.c_int, P, P]),
+    "es_struct_size": (I64, [C.c_int]),
     "es_dropout_mask": (C.c_int, [P, I64, P, P]),
 }
 
@@ -181,6 +191,9 @@ class HipError(RuntimeError):
 
 def lib_path() -> str:
     return _LIB_PATH
+
+
+_ABI_STRUCTS = (View, Dropout, ConvDesc, Norm, Chain, GenLoss, DFront2Params, DMlpParams)
 
 
 def lib():
@@ -195,6 +208,10 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        for i, st in enumerate(_ABI_STRUCTS):   # the mirrors must match the header's layouts
+            if L.es_struct_size(i) != C.sizeof(st):
+                raise HipError(f"{st.__name__}: ctypes size {C.sizeof(st)} != C size {L.es_struct_size(i)} "
+                               f"(bindings out of date with include/expertsim_hip.h)")
         _lib = L
     return _lib
 
@@ -257,12 +274,73 @@ def strides4(s):
     return arr
 
 
+# Dynamic rows (a multi-expert step without host synchronisation): while set, the running expert's
+# buffers have a capacity of `cap` samples of which a device count (int32 [1]) is live; every view /
+# conv descriptor whose leading (sample) dimension is `cap` carries that count (es_view_t.rows,
+# es_conv_desc_t.rows) and the kernels skip the padding samples.  `active` (int32 [1], != 0 when the
+# expert trains this step) gates its optimizer, spectral-norm and batch-counter updates.
+_LIVE = None
+
+
+class live_rows:
+    """Context: the expert program that follows runs on `cap`-sample buffers with `rows` live."""
+
+    def __init__(self, cap: int, rows: torch.Tensor, active: torch.Tensor):
+        self.state = (int(cap), rows, active)
+
+    def __enter__(self):
+        global _LIVE
+        self.prev, _LIVE = _LIVE, self.state
+        return self
+
+    def __exit__(self, *exc):
+        global _LIVE
+        _LIVE = self.prev
+        return False
+
+
+def live_on() -> bool:
+    return _LIVE is not None
+
+
+def rows_ptr(n: int):
+    """The live-count pointer for a tensor of n samples (None outside a dynamic program or when n
+    is not the capacity)."""
+    if _LIVE is None or int(n) != _LIVE[0]:
+        return None
+    return _LIVE[1].data_ptr()
+
+
+def active_ptr():
+    """The running expert's active flag (device int32 [1]) as a pointer, or None (always active)."""
+    return None if _LIVE is None else C.c_void_p(_LIVE[2].data_ptr())
+
+
+def active_tensor():
+    return None if _LIVE is None else _LIVE[2]
+
+
 def make_view(dims, strides) -> View:
     v = View()
     v.n, v.c, v.h, v.w = (int(d) for d in dims)
     for i in range(4):
         v.s[i] = int(strides[i])
+    v.rows = rows_ptr(v.n)
     return v
+
+
+def set_index_offset(d: Dropout, n_offset, per: int):
+    """A dropout's logical index offset: n_offset (the first sample's index in the expert's global
+    batch) x elements per sample; n_offset may be a device int32 [1] (data-parallel dynamic rows:
+    es_dropout_t.index_ptr, the offset added on the device)."""
+    if isinstance(n_offset, torch.Tensor):
+        d.index_offset = 0
+        d.index_ptr = n_offset.data_ptr()
+        d.index_mul = int(per)
+    else:
+        d.index_offset = int(n_offset) * int(per)
+        d.index_ptr = None
+        d.index_mul = 0
 
 
 # Device step counter of the running train step (see set_step_counter): dropout structs built while

@@ -366,6 +366,7 @@ class ConvOp:
         d.K, d.R, d.S, d.stride, d.pad = self.K, self.R, self.S, self.stride, self.pad
         d.P = (d.Hu + 2 * self.pad - self.R) // self.stride + 1
         d.Q = (d.Wu + 2 * self.pad - self.S) // self.stride + 1
+        d.rows = hip.rows_ptr(N)
         return d
 
     def subpixel(self, d, dtype) -> bool:
@@ -431,6 +432,8 @@ class ConvOp:
         the generators' fc2 (256 -> 21632 neutron, neutron/generator.py:17) is the case.  None when the
         layout does not apply."""
         if not _LIN_PIX or self.R != 1 or self.S != 1 or self.up is not None or self.stride != 1 or self.pad != 0:
+            return None
+        if hip.live_on():   # dynamic rows count samples, not the view's 16-sample images
             return None
         N, Cc, H, W = x.dims
         dt = x.t.dtype
@@ -604,6 +607,10 @@ def count_batches(nbt, k):
 
 
 def _count_batch(nbt):
+    if hip.live_on():
+        # dynamic rows: +1 on the device when the running expert trains (a captured graph replays it)
+        hip.call("es_counter_add_i64_if", hip.ptr(nbt), 1, hip.active_ptr(), hip.stream_ptr())
+        return
     if _NBT_PENDING is None:
         nbt.add_(1)
     else:
@@ -722,14 +729,18 @@ class NormOp:
             assert act_ref is None and beta == 0.0, "SyncBN backward: no act_ref / accumulation"
             Cc = x.dims[1]
             sums = torch.empty(2, Cc, dtype=torch.float32, device=x.t.device)
-            args = lambda ph, cnt, dsm: (ph, C.byref(x.view), x.dt, x.ptr, C.byref(nm), C.byref(chain),
+            args = lambda ph, cnt, cmul, dsm: (ph, C.byref(x.view), x.dt, x.ptr, C.byref(nm), C.byref(chain),
                                          C.byref(dy.view), dy.dt, dy.ptr, C.byref(dx.view), dx.dt, dx.ptr,
-                                         hip.ptr(sums), float(cnt), hip.ptr(dgamma) if ph == 0 else None,
+                                         hip.ptr(sums), float(cnt), cmul, hip.ptr(dgamma) if ph == 0 else None,
                                          hip.ptr(dbeta) if ph == 0 else None, dsm, hip.ptr(wsb), hip.stream_ptr())
-            hip.call("es_norm_bwd_sync", *args(0, 0.0, None))
+            hip.call("es_norm_bwd_sync", *args(0, 0.0, None, None))
             sync.all_reduce_(sums)
             rows = x.dims[0] * x.dims[2] * x.dims[3]
-            hip.call("es_norm_bwd_sync", *args(1, sync.bn_rows(rows, x.dims[0]),
+            if hip.live_on():   # dynamic rows: rows per sample x the expert's global count (device)
+                cnt, cmul = x.dims[2] * x.dims[3], sync.global_count_ptr()
+            else:
+                cnt, cmul = sync.bn_rows(rows, x.dims[0]), None
+            hip.call("es_norm_bwd_sync", *args(1, cnt, cmul,
                                                 hip.ptr(dsum) if (dsum is not None and Cc <= 1024) else None))
             if dsum is not None and Cc > 1024:
                 channel_sum(dx, dsum, 1.0)
@@ -823,7 +834,7 @@ class SpectralNorm:
         h, wd = self.h, self.wd
         buf = torch.empty(1 + 2 * (h + wd), dtype=torch.float32, device=self.w.device)
         hip.call("es_sn_power_iter", hip.ptr(self.w), h, wd, hip.ptr(self.u), hip.ptr(self.v),
-                 hip.ptr(buf), 1 if update else 0, hip.stream_ptr())
+                 hip.ptr(buf), 1 if update else 0, hip.active_ptr(), hip.stream_ptr())
         # the kernel snapshots the u, v it used after the scratch (the next call updates them in place)
         o = 1 + h + wd
         return buf[:1], buf[o:o + h], buf[o + h:o + h + wd]
@@ -848,7 +859,7 @@ class SpectralNorm:
             hip.call("es_sn_power_iter_batch", n, arr([sns[i].w.data_ptr() for i in idx]),
                      (C.c_int * n)(*[sns[i].h for i in idx]), (C.c_int * n)(*[sns[i].wd for i in idx]),
                      arr([sns[i].u.data_ptr() for i in idx]), arr([sns[i].v.data_ptr() for i in idx]),
-                     arr([b.data_ptr() for b in bufs]), 1 if update else 0, hip.stream_ptr())
+                     arr([b.data_ptr() for b in bufs]), 1 if update else 0, hip.active_ptr(), hip.stream_ptr())
             for i, b in zip(idx, bufs):
                 h, wd = sns[i].h, sns[i].wd
                 o = 1 + h + wd

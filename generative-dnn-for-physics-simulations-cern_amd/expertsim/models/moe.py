@@ -8,8 +8,14 @@ Same constructor and ``train_step`` signature and the same metric keys (moe.py:4
 is an explicit program of HIP kernels (no autograd): router -> per expert {G fwd #1, D step
 (D(real), D(fake), hinge, D backward, fused Adam), G fwd #2, D(fake1), D(fake2), aux regressor,
 fused G losses, D/A/G backward, fused Adam} -> router loss + Adam.  Loss weights and metrics stay
-on the device; the only host synchronisation is the expert-size read when n_experts > 1
-(needed for the reference's ``B_e <= 1`` skip rule, moe.py:126).
+on the device and nothing synchronises with the host.
+
+Multi-expert steps (n_experts > 1) run on DYNAMIC ROWS: every expert's program is issued on buffers
+of the batch's capacity B with the expert's sample count read on the device (es_expert_plan:
+live rows, the reference's ``B_e <= 1`` skip rule of moe.py:126 as an ``active`` flag gating the
+expert's Adam / spectral-norm / batch-counter updates, loss weights, data-parallel offsets), so the
+step's launches do not depend on the routing: no host round trip, and single-process steps replay
+as one captured HIP graph per expert whatever the expert sizes (hip.live_rows).
 
 Randomness: noise / Gumbel draws come from device Philox streams unless ``noise_fn`` /
 ``gumbel_fn`` inject them (parity tests); dropout masks are Philox streams keyed by
@@ -107,11 +113,17 @@ class MoEWrapper(nn.Module):
     # stream indices of the step's draws: Gumbel 0, expert e's noise_1 / noise_2 1 + 2e / 2 + 2e
     # (fixed per call site: a captured per-expert graph draws the same streams in every step)
     def _noise(self, expert, which, shape, device, row0=0):
-        """row0: the rows' first index in the expert's global batch (data parallel)."""
+        """row0: the rows' first index in the expert's global batch (data parallel); a device int32 [1]
+        under dynamic rows (es_expert_plan n0)."""
         if self.noise_fn is not None:
-            return self.noise_fn(expert, which, shape).to(device=device, dtype=torch.float32).contiguous()
-        return self.rng.normal_at(torch.empty(shape, dtype=torch.float32, device=device), 1 + 2 * expert + which,
-                                  offset=row0 * shape[1])
+            z = self.noise_fn(expert, which, shape).to(device=device, dtype=torch.float32)
+            if z.shape[0] < shape[0]:    # dynamic rows: the injected draw covers the live rows only
+                z = torch.cat([z, torch.zeros(shape[0] - z.shape[0], *shape[1:], dtype=z.dtype, device=device)])
+            return z.contiguous()
+        out = torch.empty(shape, dtype=torch.float32, device=device)
+        if isinstance(row0, torch.Tensor):
+            return self.rng.normal_at(out, 1 + 2 * expert + which, off_ptr=row0, off_mul=shape[1])
+        return self.rng.normal_at(out, 1 + 2 * expert + which, offset=row0 * shape[1])
 
     def _gumbel(self, shape, device, row0=0):
         if self.gumbel_fn is not None:
@@ -218,22 +230,19 @@ class MoEWrapper(nn.Module):
         router_optimizer.zero_grad(set_to_none=True)
 
         # expert dispatch (moe.py:97-99,121-123): E == 1 needs no routing at all; otherwise the
-        # rows are grouped per expert on the device (es_router_dispatch) and only the E counts
-        # cross to the host (the reference's B_e <= 1 skip rule and the per-expert launch sizes)
+        # rows are grouped per expert on the device (es_router_dispatch) and the per-expert plan
+        # (live rows, skip rule, loss weights, data-parallel offsets) is computed on the device
+        plan = None
         if E == 1:
             groups = [(0, None, B)]
+            if ddp is not None:
+                groups = ddp.global_groups(groups, B)
         else:
             perm = self._buf("perm", (B,), torch.int32, dev)
             offs = self._buf("offs", (E + 1,), torch.int32, dev)
             hip.call("es_router_dispatch", hip.ptr(idx), B, E, hip.ptr(perm), hip.ptr(offs), hip.stream_ptr())
-            counts_h = counts.cpu().numpy()
-            groups = [(e, (perm, offs), int(counts_h[e])) for e in range(E)]
-        if ddp is not None:
-            groups = ddp.global_groups(groups, B)
-            if ddp.sync_bn and any(ddp.global_count(e) > 1 and ddp._local[e] == 0 for e in range(E)):
-                # every rank sees the same count matrix, so every rank raises here together
-                raise RuntimeError("sync_bn: a rank holds no sample of an active expert (its SyncBN "
-                                   "collectives could not be matched); use larger shards or sync_bn=False")
+            plan = self._plan(counts, B, dev)
+            groups = [(e, (perm, offs), B) for e in range(E)]
 
         # metrics buffer: per expert [total, gen, div, int, aux, std_int, mean_int, w, disc]
         # (persistent buffers: captured expert graphs write into them)
@@ -243,11 +252,34 @@ class MoEWrapper(nn.Module):
                          if E > 1 and float(rc.ed_strength) != 0.0 else None)
         if self._graphs is not None:
             self._graphs.begin()
+        # a whole step being captured (graph.StepGraph) with several experts and one process: the
+        # experts' programs fork onto their own streams inside the graph (no shared parameters,
+        # disjoint rows of the step's buffers), joined back before the router
+        fork = None
+        if plan is not None and ddp is None and self.expert_graphs_concurrent and torch.cuda.is_current_stream_capturing():
+            fork = self._fork_streams(E)
         for e, rows, be in groups:
+            og, od, oa = generator_optimizers[e], discriminator_optimizers[e], aux_reg_optimizers[e]
+            if plan is not None:
+                # dynamic rows: every expert's program is issued (B-sample capacity, live count and
+                # the B_e <= 1 skip rule read on the device), so one graph per expert serves every step
+                run = lambda e=e, rows=rows, og=og, od=od, oa=oa: self._expert_step(
+                    e, rows, B, B, cond, real_images, true_positions, std, intensity, og, od, oa, mbuf, step, dev,
+                    plan)
+                if fork is not None:
+                    with torch.cuda.stream(fork[e]):
+                        run()
+                elif self._graphs is not None and e in self._expert_eager:
+                    for o in (og, od, oa):
+                        o.prepare()      # (no lazy state creation inside a capture)
+                    self._graphs.run((e, B), run)
+                else:
+                    run()
+                    self._expert_eager.add(e)
+                continue
             be_global = be if ddp is None else ddp.global_count(e)
             if be_global <= 1:                                                   # moe.py:126-135
                 continue
-            og, od, oa = generator_optimizers[e], discriminator_optimizers[e], aux_reg_optimizers[e]
             # SyncBN: global batch statistics, so even one local sample runs
             if be > 1 or (ddp is not None and ddp.sync_bn and be >= 1):
                 run = lambda: self._expert_step(e, rows, be, B, cond, real_images, true_positions, std, intensity,
@@ -280,8 +312,13 @@ class MoEWrapper(nn.Module):
 
         if self._graphs is not None:
             self._graphs.join()
+        if fork is not None:
+            cur = torch.cuda.current_stream()
+            for st in fork:
+                cur.wait_stream(st)
         if ddp is not None:
-            ddp.merge_metrics(mbuf)          # the global batch's per-expert metrics on every rank
+            # the global batch's per-expert metrics on every rank
+            ddp.merge_metrics(mbuf, None if plan is None else plan["lcnt"])
 
         # ---- router (moe.py:213-449)
         rl = None
@@ -323,7 +360,9 @@ class MoEWrapper(nn.Module):
         self._eager_steps += 1
         hip.call("es_counter_add", hip.ptr(self._dstep), 1, hip.stream_ptr())
         # the metric dict (moe.py:480-502): one kernel over the expert rows and router terms
-        countsf = None if self.ddp is None else self.ddp.global_counts_tensor(dev)
+        countsf = None
+        if self.ddp is not None:
+            countsf = plan["gcnt"] if plan is not None else self.ddp.global_counts_tensor(dev)
         mvec = torch.empty(11 + 8 * E, dtype=torch.float32, device=dev)
         hip.call("es_step_metrics", hip.ptr(mbuf), E, hip.ptr(rl), hip.ptr(counts) if countsf is None else None,
                  hip.ptr(countsf), float(rc.gan_strength), float(rc.diff_strength), float(dec_w), flags,
@@ -338,39 +377,82 @@ class MoEWrapper(nn.Module):
         return {k: mvec[j] for j, k in enumerate(names)}
 
     # ---------------------------------------------------------------------------- one expert
-    def _expert_step(self, e, rows, be, B, cond, real, pos, std, intensity, opt_g, opt_d, opt_a, mbuf, step, dev):
+    def _fork_streams(self, E):
+        """One side stream per expert (kept across steps), each made to wait for the current stream."""
+        if getattr(self, "_side", None) is None or len(self._side) < E:
+            self._side = [torch.cuda.Stream() for _ in range(E)]
+        cur = torch.cuda.current_stream()
+        for st in self._side[:E]:
+            st.wait_stream(cur)
+        return self._side[:E]
+
+    def _plan(self, counts, B, dev):
+        """The multi-expert step plan on the device (es_expert_plan): per expert the live rows of this
+        process, the active flag (global count > 1, moe.py:126), the first global sample index, the
+        loss weight count/B (moe.py:99-100), the global and live counts.  Data parallel: the ranks'
+        counts are all-gathered on the device first (ddp.py)."""
+        E, ddp = self.n_experts, self.ddp
+        buf = lambda name, dt: self._buf(name, (E,), dt, dev)
+        plan = {k: buf("plan_" + k, torch.int32) for k in ("rows", "active", "n0")}
+        plan.update({k: buf("plan_" + k, torch.float32) for k in ("w", "gcnt", "lcnt")})
+        counts_all, world, rank, min_local = None, 1, 0, 2
+        if ddp is not None:
+            counts_all = ddp.all_gather(counts)
+            world, rank = ddp.world, ddp.rank
+            # a rank with too few local samples trains with zero rows (zero local gradients, the
+            # same collectives); SyncBN runs any non-empty shard (global statistics)
+            min_local = 1 if ddp.sync_bn else 2
+            ddp.set_plan(plan, B)
+        hip.call("es_expert_plan", hip.ptr(counts), hip.ptr(counts_all), world, rank, E, B, min_local,
+                 *[hip.ptr(plan[k]) for k in ("rows", "active", "n0", "w", "gcnt", "lcnt")], hip.stream_ptr())
+        return plan
+
+    def _expert_step(self, e, rows, be, B, cond, real, pos, std, intensity, opt_g, opt_d, opt_a, mbuf, step, dev,
+                     plan=None):
+        """plan (multi-expert steps): dynamic rows -- be = B is the capacity, the live count
+        plan["rows"][e] is read on the device."""
         G, D, A = self.generators[e], self.discriminators[e], self.aux_regs[e]
         H, W = real.shape[2], real.shape[3]
         ridx = None
+        live = None if plan is None else plan["rows"][e:e + 1]
         if rows is None:
             sc, sr, sp, ss, si = cond, real, pos, std, intensity
         else:
             # expert e's rows: perm[offs[e] : offs[e] + be] of the device dispatch, read at run time
+            # (dynamic rows: the first live[0] of them, the rest of the capacity zero-filled)
             perm, offs = rows
             ridx = (perm, offs[e:e + 1])
-            gather = lambda t, cols: _gather_rows(t, ridx, be, cols)
+            gather = lambda t, cols: _gather_rows(t, ridx, be, cols, live)
             sc, sp, ss, si = gather(cond, cond.shape[1]), gather(pos, 2), gather(std, 1), gather(intensity, 1)
             sr = gather(real.reshape(B, -1), H * W).view(be, 1, H, W)
         # class_counts_adjusted[i] as float32 (moe.py:99-100,522,562)
         # (DDP: local weight B_e^r / B_r; the all-reduce averages, see expertsim/train/ddp.py)
-        w_dev = self._weight_scalar(be, B, dev)
+        w_dev = self._weight_scalar(be, B, dev) if plan is None else plan["w"][e:e + 1]
         # the step term (step * 1024) is added on the device from self._dstep
         sb = lambda pid: philox.dropout_stream(0, e, pid, 0)
         seed = self.rng_seed
         ddp = self.ddp
-        n0 = ddp.sample_offset(e) if ddp is not None else 0     # first global sample index
+        n0 = 0                                                  # first global sample index
+        if ddp is not None:
+            n0 = ddp.sample_offset(e) if plan is None else plan["n0"][e:e + 1]
         sync = ddp is not None and ddp.sync_bn
         if sync:
             ddp.expert = e
             set_norm_sync(ddp)
         try:
-            self._expert_program(e, be, B, G, D, A, sc, sr, sp, ss, si, opt_g, opt_d, opt_a, mbuf, dev, w_dev,
-                                 sb, seed, n0, sync, rows, ridx)
+            if plan is None:
+                self._expert_program(e, be, B, G, D, A, sc, sr, sp, ss, si, opt_g, opt_d, opt_a, mbuf, dev, w_dev,
+                                     sb, seed, n0, sync, rows, ridx, None, None)
+            else:
+                with hip.live_rows(be, live, plan["active"][e:e + 1]):
+                    self._expert_program(e, be, B, G, D, A, sc, sr, sp, ss, si, opt_g, opt_d, opt_a, mbuf, dev,
+                                         w_dev, sb, seed, n0, sync, rows, ridx, live, plan["gcnt"][e:e + 1])
         finally:
             set_norm_sync(None)
 
     def _expert_program(self, e, be, B, G, D, A, sc, sr, sp, ss, si, opt_g, opt_d, opt_a, mbuf, dev, w_dev, sb,
-                        seed, n0, sync, rows, ridx):
+                        seed, n0, sync, rows, ridx, live, gcnt):
+        """live / gcnt (dynamic rows): the device live count and global count of the expert."""
         ddp = self.ddp
 
         # ---- generator forward #1 (moe.py:144-145)
@@ -382,8 +464,8 @@ class MoEWrapper(nn.Module):
         fo, _, dctx_f = D.fwd(fake1, sc)
         dro = torch.empty(be, 1, dtype=torch.float32, device=dev)
         dfo = torch.empty(be, 1, dtype=torch.float32, device=dev)
-        hip.call("es_hinge_d", ro.ptr, fo.ptr, be, hip.ptr(w_dev), hip.ptr(mbuf[e, 8:9]), hip.ptr(dro),
-                 hip.ptr(dfo), hip.stream_ptr())
+        hip.call("es_hinge_d", ro.ptr, fo.ptr, be, hip.ptr(live), hip.ptr(w_dev), hip.ptr(mbuf[e, 8:9]),
+                 hip.ptr(dro), hip.ptr(dfo), hip.stream_ptr())
         D.bwd(dctx_r, dout=Act.of(dro), weight_grads=True, input_grad=False)
         D.bwd(dctx_f, dout=Act.of(dfo), weight_grads=True, input_grad=False)
         n2 = self._noise(e, 1, (be, self.noise_dim), dev, row0=n0)
@@ -406,7 +488,7 @@ class MoEWrapper(nn.Module):
             if rows is None:
                 hip.call("es_scatter_rows", hip.ptr(s), None, be, hip.ptr(self._ed_feat), hip.stream_ptr())
             else:
-                hip.call("es_scatter_rows_at", hip.ptr(s), hip.ptr(ridx[0]), hip.ptr(ridx[1]), be,
+                hip.call("es_scatter_rows_at", hip.ptr(s), hip.ptr(ridx[0]), hip.ptr(ridx[1]), be, hip.ptr(live),
                          hip.ptr(self._ed_feat), hip.stream_ptr())
         coords, actx = A.fwd(fake1, seed=seed, stream_base=sb(philox.PASS_AUX), n_offset=n0)
         L = fl1.dims[1]
@@ -414,12 +496,16 @@ class MoEWrapper(nn.Module):
         p.n, p.latent, p.noise = be, L, self.noise_dim
         p.di_strength, p.in_strength = float(G.di_strength), float(G.in_strength)
         p.aux_strength = float(self.cfg.model.aux_reg.strength)
+        p.rows = live.data_ptr() if live is not None else None
         if sync:
             # SDI prefactor mean(std)^2 over the expert's global batch (moe.py:573-588)
             std_mean = torch.empty(1, dtype=torch.float32, device=dev)
             hip.call("es_router_colsum", hip.ptr(ss), be, 1, hip.ptr(std_mean), hip.stream_ptr())
             ddp.all_reduce_(std_mean)
-            copy_act(Act.of(std_mean.view(1, 1)), Act.of(std_mean.view(1, 1)), 1.0 / ddp.global_count(e), 0.0)
+            if gcnt is not None:     # dynamic rows: / the expert's global count (device)
+                hip.call("es_div_by", hip.ptr(std_mean), 1, hip.ptr(gcnt), hip.stream_ptr())
+            else:
+                copy_act(Act.of(std_mean.view(1, 1)), Act.of(std_mean.view(1, 1)), 1.0 / ddp.global_count(e), 0.0)
             p.std_mean = std_mean.data_ptr()
         dfo1 = torch.empty(be, 1, dtype=torch.float32, device=dev)
         dl1 = torch.empty(be, L, dtype=torch.float32, device=dev)
@@ -485,19 +571,21 @@ class MoEWrapper(nn.Module):
         return counts / expert_assignments.size(0)
 
 
-def _gather_rows(t: torch.Tensor, ridx, rows: int, cols: int) -> torch.Tensor:
-    """ridx = (dispatch permutation, device start position): rows perm[start : start + rows]."""
+def _gather_rows(t: torch.Tensor, ridx, rows: int, cols: int, live=None) -> torch.Tensor:
+    """ridx = (dispatch permutation, device start position): rows perm[start : start + rows]; with
+    live (device int32 [1]) only the first live[0] rows, the rest zeros."""
     perm, start = ridx
     out = torch.empty(rows, cols, dtype=torch.float32, device=t.device)
     src = t.reshape(t.shape[0], -1)
     hip.call("es_gather_rows_at", hip.ptr(src), src.stride(0), hip.ptr(perm), hip.ptr(start), rows, cols,
-             hip.ptr(out), cols, hip.stream_ptr())
+             hip.ptr(out), cols, hip.ptr(live), hip.stream_ptr())
     return out
 
 
 class ExpertGraphs:
     """HIP graphs of whole expert steps (gather, G fwd, D step + Adam, G step + Adam), one per
-    (expert, expert batch size, batch size).  A multi-expert step then issues ~40 launches from the
+    (expert, batch size): the expert's rows are dynamic (its live count is read on the device), so one
+    capture serves every routing.  A multi-expert step then issues ~40 launches from the
     host (router, dispatch, router loss + Adam, metrics) plus one graph replay per active expert,
     instead of ~450 launches per expert, and the experts' graphs run CONCURRENTLY, one HIP stream
     per expert: experts share no parameters and write disjoint rows of the step's buffers, and a
@@ -505,9 +593,9 @@ class ExpertGraphs:
     (its graphs replay one after another, so they may share temporaries; different experts'
     graphs may not).  Everything that changes between steps is read on the device: the step
     counters (dropout / noise streams, Adam bias corrections), the expert's rows (dispatch
-    permutation + device start), the batch (static input buffers).  The first occurrence of a key
-    is captured and then replayed; BatchNorm batch counts recorded at capture are re-applied on
-    every replay."""
+    permutation + device start + live count), the batch (static input buffers).  The first
+    occurrence of a key is captured and then replayed; BatchNorm batch counts are advanced on the
+    device inside the graph (gated on the expert's active flag)."""
 
     def __init__(self, max_graphs: int = 512, concurrent: bool = True):
         self.pools, self.streams = {}, {}

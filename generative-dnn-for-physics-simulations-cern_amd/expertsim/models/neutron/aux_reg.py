@@ -84,7 +84,7 @@ class AuxRegNeutron(ExpertModule):
         keep = c["keep"] = []   # dropout keep bits: drawn in the forward norm pass, re-read backward
 
         def bn(name, h, chain):
-            chain.drop.index_offset = int(n_offset) * h.dims[1] * h.dims[2] * h.dims[3]
+            hip.set_index_offset(chain.drop, n_offset, h.dims[1] * h.dims[2] * h.dims[3])
             keep.append(hip.attach_keep(chain, h.dims[0] * h.dims[2] * h.dims[3], h.dims[1], h.t.device))
             return o[name].fwd(h, chain, train=train)
         c["h1"] = o["c1"].fwd(x)

@@ -104,7 +104,7 @@ class GeneratorNeutron(ExpertModule):
         per_sample = ((1, 256), (1, F2), ((2 * k - 2) ** 2, 256), ((4 * k - 6) ** 2, 128), ((4 * k - 7) ** 2, 64))
         keep = [hip.attach_keep(ch[i], B * r, c, dev) for i, (r, c) in enumerate(per_sample)]
         for i, (r, c) in enumerate(per_sample):
-            ch[i].drop.index_offset = int(n_offset) * r * c
+            hip.set_index_offset(ch[i].drop, n_offset, r * c)
         h1 = o["fc1"].fwd(x0)
         y1, s1 = o["bn1"].fwd(h1, ch[0], train=train)
         h2 = o["fc2"].fwd(y1, bn_stats=train)        # (ring FWD over 16-row pixel blocks: stats in its epilogue)

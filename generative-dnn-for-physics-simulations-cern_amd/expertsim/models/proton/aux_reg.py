@@ -113,8 +113,10 @@ class AuxReg(ExpertModule):
             fc = c["f"].like_nhwc(cdt)
             copy_act(c["f"], fc)
         c["fc"] = fc
-        d0 = hip.dropout_struct(P_DROP, seed, stream_base + 0, enabled=train, index_offset=int(n_offset) * 128)
-        d1 = hip.dropout_struct(P_DROP, seed, stream_base + 1, enabled=train, index_offset=int(n_offset) * 64)
+        d0 = hip.dropout_struct(P_DROP, seed, stream_base + 0, enabled=train)
+        d1 = hip.dropout_struct(P_DROP, seed, stream_base + 1, enabled=train)
+        hip.set_index_offset(d0, n_offset, 128)
+        hip.set_index_offset(d1, n_offset, 64)
         c["ch0"] = hip.chain_struct(hip.ACT_LRELU, SLOPE, d0, dropout_first=False)
         c["ch1"] = hip.chain_struct(hip.ACT_LRELU, SLOPE, d1, dropout_first=False)
         c["r0"] = o["l0"].fwd(fc)

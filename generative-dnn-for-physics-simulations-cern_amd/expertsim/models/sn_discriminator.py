@@ -179,6 +179,8 @@ class SNDiscriminator(ExpertModule):
         lr = hip.chain_struct(hip.ACT_LRELU, SLOPE)
         x = img
         front = self.front_fused(img)               # the fused front reads the fp32 image directly
+        if front and hip.live_on() and not self.front2_fused(img):
+            front = False                           # (es_dfront_* has no live-row count: generic kernels)
         if img.t.dtype != cdt and not front:
             x = img.like_nhwc(cdt)
             copy_act(img, x)
@@ -188,6 +190,7 @@ class SNDiscriminator(ExpertModule):
         if front and self.front2_fused(x):
             # both conv blocks in one kernel: features straight into the fc1 input rows
             params = self._front2_params(sig)
+            params.rows = hip.rows_ptr(B)
             fstats = torch.empty(B * 32, dtype=torch.float32, device=dev)
             # activations the backward reads (pooled block-1 map, argmax conv values, block-2 map)
             nsave = hip.lib().es_dfront2_save_floats(x.dims[2], x.dims[3], *self.pool2)
@@ -243,6 +246,7 @@ class SNDiscriminator(ExpertModule):
         if self.fuse_mlp and cdt == torch.float32:
             F = X.dims[1]
             params = self._mlp_params(sig)
+            params.rows = hip.rows_ptr(B)
             f32 = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)
             h3, s3, h4, s4, lat, out = f32(B, 128), f32(B, 2), f32(B, 64), f32(B, 2), f32(B, 64), f32(B, 1)
             hip.call("es_dmlp_fwd", X.ptr, X.strides[0], B, F, C.byref(params), hip.ptr(h3), hip.ptr(s3),

@@ -58,14 +58,18 @@ class FusedAdam(torch.optim.Optimizer):
             grad_scale = getattr(self.module, "_grad_scale", 1.0)
         if self._dstep is None or self._dstep.device != flat.device:
             self._dstep = torch.full((1,), self._step, dtype=torch.int32, device=flat.device)
-        self._step += 1
+        # dynamic rows (multi-expert step): the update and the step count happen on the device only
+        # when the running expert trains (hip.active_ptr); the host count is then re-read lazily
+        active = hip.active_ptr()
+        if active is None:
+            self._step += 1
         g = self.param_groups[0]
         b1, b2 = g["betas"]
         # step counter advanced and read on the device, so a captured step replays correctly
-        hip.call("es_counter_add", hip.ptr(self._dstep), 1, hip.stream_ptr())
+        hip.call("es_counter_add_if", hip.ptr(self._dstep), 1, active, hip.stream_ptr())
         hip.call("es_adam_dev", hip.ptr(flat), hip.ptr(self.module.flat_grads), hip.ptr(self._m), hip.ptr(self._v),
                  flat.numel(), float(g["lr"]), float(b1), float(b2), float(g["eps"]), hip.ptr(self._dstep),
-                 float(grad_scale), hip.stream_ptr())
+                 float(grad_scale), active, hip.stream_ptr())
         self._step_t.fill_(float(self._step))
         self.module.invalidate()
         return None

@@ -61,8 +61,22 @@ class DeviceRNG:
                  hip.ptr(self.step_counter), STEP_MUL, int(offset), hip.stream_ptr())
         return out
 
-    def normal_at(self, out: torch.Tensor, index: int, offset: int = 0):
-        return self._draw_at("es_randn", out, index, offset)
+    def normal_at(self, out: torch.Tensor, index: int, offset: int = 0, off_ptr: torch.Tensor = None,
+                  off_mul: int = 0):
+        """off_ptr (device int32 [1]): the element offset is offset + off_ptr[0] * off_mul, read on the
+        device (a data-parallel rank's first sample of an expert under dynamic rows)."""
+        if off_ptr is None:
+            return self._draw_at("es_randn", out, index, offset)
+        hip.require_device(out)
+        if self.step_counter is None:
+            sid, sp, mul = self._next(), None, 0
+        else:
+            if not 0 <= index < STEP_MUL:
+                raise RuntimeError("DeviceRNG: stream index %d outside [0, %d)" % (index, STEP_MUL))
+            sid, sp, mul = (self.stream_base + index) & 0xFFFFFFFF, hip.ptr(self.step_counter), STEP_MUL
+        hip.call("es_randn_dev_at", hip.ptr(out), out.numel(), self.seed, sid, sp, mul, int(offset),
+                 hip.ptr(off_ptr), int(off_mul), hip.stream_ptr())
+        return out
 
     def exponential_at(self, out: torch.Tensor, index: int, offset: int = 0):
         return self._draw_at("es_rand_exponential", out, index, offset)

@@ -55,6 +55,7 @@ class DataParallel:
         self.local_batch = None
         self._counts_dev = {}
         self.expert = None         # expert whose step is running (global count for SyncBN)
+        self.plan = None           # multi-expert steps: the device plan (MoEWrapper._plan)
         self._pending = []         # async all-reduce works not yet waited for
         self.issued = []           # (module, lo, hi) of every gradient all-reduce (tests)
 
@@ -100,6 +101,15 @@ class DataParallel:
         self._counts = allc.sum(0)
         self._offsets = allc[:self.rank].sum(0) if self.rank else np.zeros(E, dtype=np.int64)
         return groups
+
+    def set_plan(self, plan, B_local):
+        """Multi-expert step: the per-expert counts live on the device (dynamic rows, no host copy)."""
+        self.plan = plan
+        self.local_batch = B_local
+
+    def global_count_ptr(self):
+        """Device float pointer to the running expert's global count (dynamic-rows SyncBN)."""
+        return hip.ptr(self.plan["gcnt"][self.expert:self.expert + 1])
 
     def global_count(self, e):
         return int(self._counts[e])
@@ -174,20 +184,26 @@ class DataParallel:
         return ready
 
     # ---------------------------------------------------------------- metrics
-    def merge_metrics(self, mbuf: torch.Tensor):
+    def merge_metrics(self, mbuf: torch.Tensor, lcnt: torch.Tensor = None):
         """mbuf [E, 9] (per expert: total, gen, div, int, aux, std_int, mean_int, w, disc) -> the
-        global-batch values, in place (es_dp_metrics_merge over the all-gathered rows)."""
+        global-batch values, in place (es_dp_metrics_merge over the all-gathered rows).  lcnt (device
+        [E] float, multi-expert steps): the rows each expert ran on this rank (0: not run)."""
         E = mbuf.shape[0]
         rows = torch.empty(E, 10, dtype=torch.float32, device=mbuf.device)
         rows[:, :9].copy_(mbuf)
-        ran = self._local >= (1 if self.sync_bn else 2)        # the ranks that ran the expert's step
-        n = np.where(ran, self._local, 0).astype(np.float32)
-        # cached per value on the device: a pageable host -> device copy_ synchronises the stream
-        # (it would drain the GPU at the end of every data-parallel step)
-        key = ("n", str(mbuf.device), tuple(float(v) for v in n))
-        if key not in self._counts_dev:
-            self._counts_dev[key] = torch.from_numpy(n).to(mbuf.device)
-        rows[:, 9].copy_(self._counts_dev[key])
+        if lcnt is not None:
+            rows[:, 9].copy_(lcnt)
+        else:
+            ran = self._local >= (1 if self.sync_bn else 2)        # the ranks that ran the expert's step
+            n = np.where(ran, self._local, 0).astype(np.float32)
+            # one expert (E == 1): the shard size, a device constant cached per value (a pageable
+            # host -> device copy_ would synchronise the stream at the end of every step)
+            key = ("n", str(mbuf.device), tuple(float(v) for v in n))
+            if key not in self._counts_dev:
+                if len(self._counts_dev) > 64:
+                    self._counts_dev.clear()
+                self._counts_dev[key] = torch.from_numpy(n).to(mbuf.device)
+            rows[:, 9].copy_(self._counts_dev[key])
         allr = self.all_gather(rows)
         hip.call("es_dp_metrics_merge", hip.ptr(allr), self.world, E, hip.ptr(mbuf), hip.stream_ptr())
         return mbuf

@@ -312,7 +312,8 @@ int es_norm_act_bwd_sums(const es_view_t* x, es_dtype_t xdt, const void* xp, con
  * (world partials -> mean / invstd / running stats).
  *   es_norm_bwd_sync phase 0: raw per-channel sums [2][C] (sum dnorm, sum dnorm*xhat) of the rank
  *   into `sums`, and the rank's dgamma / dbeta accumulation; the caller all-reduces `sums`;
- *   phase 1: dx from the global sums and the global row count `cnt` (+ dsum as es_norm_act_bwd).
+ *   phase 1: dx from the global sums and the global row count `cnt` (+ dsum as es_norm_act_bwd);
+ *   with cnt_mul (device float, dynamic rows) the count is cnt_mul[0] * cnt (cnt: per sample).
  * ws: es_norm_bwd_ws_bytes(x, ES_NORM_BN, 1). */
 int es_norm_stats_merge(const float* part, int chunks, int C, float* out, es_stream_t stream);
 int es_norm_stats_local(const es_view_t* x, es_dtype_t xdt, const void* xp, void* ws, float* out,
@@ -320,7 +321,8 @@ int es_norm_stats_local(const es_view_t* x, es_dtype_t xdt, const void* xp, void
 int es_norm_bwd_sync(int phase, const es_view_t* x, es_dtype_t xdt, const void* xp, const es_norm_t* nm,
                      const es_chain_t* ch, const es_view_t* dy, es_dtype_t dydt, const void* dyp,
                      const es_view_t* dx, es_dtype_t dxdt, void* dxp, float* sums, float cnt,
-                     float* dgamma, float* dbeta, float* dsum, void* ws, es_stream_t stream);
+                     const float* cnt_mul, float* dgamma, float* dbeta, float* dsum, void* ws,
+                     es_stream_t stream);
 
 /* Plain elementwise chain without normalisation (router LeakyReLU, final ReLU, casts):
  * y = chain(x). And its backward dx = beta*dx + dchain(dy) evaluated at x (or act_ref). */
@@ -373,6 +375,7 @@ typedef struct {
     const float* w2; const float* sigma2; const float* b2; const float* g2; const float* be2;  /* [16][32][3][3], GN(8,16) */
     float eps1, eps2, slope;
     int ph, pw;                       /* second pool window = stride (neutron 2x2, proton 2x1) */
+    const int32_t* rows;              /* optional device int32: live images of the N-image capacity */
 } es_dfront2_params_t;
 /* 1 when the fused path supports this geometry (H*W <= 2048, H-2 and W-2 even, pooled map <= 448
  * pixels, second conv map <= 368 pixels) */
@@ -405,6 +408,7 @@ typedef struct {
     const float* w2; const float* sigma2; const float* b2; const float* g2; const float* be2;  /* [64][128], LN(64) */
     const float* w3; const float* sigma3; const float* b3;                                    /* [1][64] */
     float eps1, eps2, slope;
+    const int32_t* rows;   /* optional device int32: live samples of the B-sample capacity */
 } es_dmlp_params_t;
 /* Forward over X [B][F] (row stride xs): writes h3 [B][128] (fc1 output), s3 [B][2] (LN1 mean,
  * invstd), h4 [B][64], s4 [B][2], lat [B][64] (the latent) and out [B] (the logit). */
@@ -444,9 +448,10 @@ int es_avgpool_bwd(const es_view_t* dy, const void* dyp, const es_view_t* dx, es
 int es_gather_rows(const float* src, int64_t src_ld, const int32_t* idx, int rows, int cols,
                    float* dst, int64_t dst_ld, es_stream_t stream);
 /* Same with idx = perm + start[0], start read on the device (es_router_dispatch's offsets): the
- * per-expert gather of a captured expert graph (moe.py:121-143). */
+ * per-expert gather of a multi-expert step (moe.py:121-143).  live (optional, device int32): only the
+ * first live[0] of the `rows` (capacity) rows are gathered, the rest are written as zeros. */
 int es_gather_rows_at(const float* src, int64_t src_ld, const int32_t* perm, const int32_t* start, int rows,
-                      int cols, float* dst, int64_t dst_ld, es_stream_t stream);
+                      int cols, float* dst, int64_t dst_ld, const int32_t* live, es_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Spectral norm (torch.nn.utils.spectral_norm, n_power_iterations=1, eps=1e-12) for every
@@ -455,13 +460,16 @@ int es_gather_rows_at(const float* src, int64_t src_ld, const int32_t* perm, con
  * sigma points to 1 + 2*(h + wd) floats: sigma[0], scratch, then a snapshot of the u [h] and
  * v [wd] this call used (what es_sn_bwd needs once the next call has updated u, v in place).
  * ---------------------------------------------------------------------------------------- */
+/* active (optional, device int32): with active[0] == 0 the call computes sigma from the stored u, v
+ * and updates nothing (an expert that does not train this step, moe.py:126-135). */
 int es_sn_power_iter(const float* w, int h, int wd, float* u, float* v, float* sigma, int update,
-                     es_stream_t stream);
+                     const int32_t* active, es_stream_t stream);
 /* es_sn_power_iter for n <= ES_SN_BATCH_MAX small layers (h*wd < 16384 each) in ONE launch; the
  * arrays are host arrays of device pointers / sizes, buf[i] as es_sn_power_iter's sigma buffer. */
 #define ES_SN_BATCH_MAX 8
 int es_sn_power_iter_batch(int n, const float* const* w, const int* h, const int* wd, float* const* u,
-                           float* const* v, float* const* buf, int update, es_stream_t stream);
+                           float* const* v, float* const* buf, int update, const int32_t* active,
+                           es_stream_t stream);
 /* es_sn_bwd for n <= ES_SN_BATCH_MAX small layers in ONE launch (host arrays of device pointers). */
 int es_sn_bwd_batch(int n, const float* const* w, const float* const* g, const int* h, const int* wd,
                     const float* const* u, const float* const* v, const float* const* sigma, float* const* dw,
@@ -475,9 +483,10 @@ int es_sn_bwd(const float* w, const float* g, int h, int wd, const float* u, con
  * Losses (moe.py:506-642, proton/aux_reg.py:42-45, train/utils.py:623-642) and their gradients.
  * ---------------------------------------------------------------------------------------- */
 /* Discriminator hinge (moe.py:518-523): out[0] = w*(mean relu(1-ro) + mean relu(1+fo));
- * dro/dfo = gradients of out[0].  w is read from device memory (w_ptr[0]) to avoid host syncs. */
-int es_hinge_d(const float* ro, const float* fo, int n, const float* w_ptr, float* out, float* dro,
-               float* dfo, es_stream_t stream);
+ * dro/dfo = gradients of out[0].  w is read from device memory (w_ptr[0]) to avoid host syncs.
+ * rows (optional, device int32): the live count of the n-capacity batch (0: out[0] = 0). */
+int es_hinge_d(const float* ro, const float* fo, int n, const int32_t* rows, const float* w_ptr, float* out,
+               float* dro, float* dfo, es_stream_t stream);
 /* per-sample photon sum s[b] = sum_{h,w} (exp(x)-1) of the generated image (moe.py:611-616) */
 int es_image_expsum(const es_view_t* x, es_dtype_t dt, const void* xp, float* s, es_stream_t stream);
 /* Generator-step losses (moe.py:544-563): gen hinge, SDI diversity, intensity L1, log-cosh aux,
@@ -488,6 +497,7 @@ typedef struct {
   float di_strength, in_strength, aux_strength;
   const float* std_mean; /* optional device scalar: mean(std) over the expert's GLOBAL batch (data
                             parallel, SDI prefactor); NULL: the mean over these n samples */
+  const int32_t* rows;   /* optional device int32: live samples of the n-capacity batch (0: metrics 0) */
 } es_gen_loss_t;
 int es_gen_losses(const es_gen_loss_t* p, const float* fo, const float* l1, const float* l2,
                   const float* n1, const float* n2, const float* std_, const float* s,
@@ -542,8 +552,8 @@ int es_dp_metrics_merge(const float* rows, int world, int E, float* out, es_stre
 int es_scatter_rows(const float* src, const int32_t* rows, int n, float* dst, es_stream_t stream);
 /* Same with the rows read from a dispatch permutation at a DEVICE start position (perm + start[0]),
  * so a captured per-expert graph stays valid whatever the expert's offset in a later step. */
-int es_scatter_rows_at(const float* src, const int32_t* perm, const int32_t* start, int n, float* dst,
-                       es_stream_t stream);
+int es_scatter_rows_at(const float* src, const int32_t* perm, const int32_t* start, int n, const int32_t* live,
+                       float* dst, es_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Optimizer (torch.optim.Adam, created at train/training_setup.py:20-40, stepped at
@@ -552,9 +562,11 @@ int es_scatter_rows_at(const float* src, const int32_t* perm, const int32_t* sta
 int es_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
             float beta2, float eps, int step, float grad_scale, es_stream_t stream);
 /* Same update with the (1-based) step read on the device from step_ptr[0]; bias corrections
- * computed in the kernel (for captured train steps). */
+ * computed in the kernel (for captured train steps).  active (optional, device int32): no update when
+ * active[0] == 0 (an expert skipped this step, moe.py:126-135). */
 int es_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
-                float beta2, float eps, const int32_t* step_ptr, float grad_scale, es_stream_t stream);
+                float beta2, float eps, const int32_t* step_ptr, float grad_scale, const int32_t* active,
+                es_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Random numbers (torch.randn at moe.py:144,535; exponential_ inside F.gumbel_softmax):
@@ -570,8 +582,32 @@ int es_randn_dev(float* out, int64_t n, uint64_t seed, uint32_t stream_id, const
                  int32_t step_mul, int64_t offset, es_stream_t stream);
 int es_rand_exponential_dev(float* out, int64_t n, uint64_t seed, uint32_t stream_id,
                             const int32_t* step_ptr, int32_t step_mul, int64_t offset, es_stream_t stream);
-/* counter[0] += v on the device (step counters of a captured train step). */
+/* es_randn_dev whose element offset adds off_ptr[0] * off_mul on the device (a data-parallel rank's
+ * first sample of an expert, es_expert_plan n0; offsets even). */
+int es_randn_dev_at(float* out, int64_t n, uint64_t seed, uint32_t stream_id, const int32_t* step_ptr,
+                    int32_t step_mul, int64_t offset, const int32_t* off_ptr, int64_t off_mul, es_stream_t stream);
+/* counter[0] += v on the device (step counters of a captured train step); the _if forms only when
+ * flag[0] != 0 (flag NULL: always) -- an expert's optimizer steps and BatchNorm num_batches_tracked
+ * counters advance only when it trains (moe.py:126-135). */
 int es_counter_add(int32_t* counter, int32_t v, es_stream_t stream);
+int es_counter_add_if(int32_t* counter, int32_t v, const int32_t* flag, es_stream_t stream);
+int es_counter_add_i64_if(int64_t* counter, int64_t v, const int32_t* flag, es_stream_t stream);
+/* Multi-expert step plan on the device (moe.py:97-135 without the host round trip): from counts [E]
+ * (this rank's expert counts, es_router_gumbel) and, data parallel, counts_all [world][E] (all ranks'
+ * counts, all-gathered on the device; NULL on one process), for each expert e: rows[e] = this rank's
+ * live rows (its count if the expert trains -- global count > 1 -- and the count is >= min_local, else
+ * 0), active[e] (the expert trains), n0[e] (this rank's first sample of the expert's global batch),
+ * w[e] = float(count) / float(B) (class_counts_adjusted, moe.py:99-100), gcnt[e] (global count, float),
+ * lcnt[e] (rows[e] as float). */
+int es_expert_plan(const int32_t* counts, const int32_t* counts_all, int world, int rank, int E, int B,
+                   int min_local, int32_t* rows, int32_t* active, int32_t* n0, float* w, float* gcnt,
+                   float* lcnt, es_stream_t stream);
+/* sizeof of the ABI structs (0 es_view_t, 1 es_dropout_t, 2 es_conv_desc_t, 3 es_norm_t, 4 es_chain_t,
+ * 5 es_gen_loss_t, 6 es_dfront2_params_t, 7 es_dmlp_params_t; -1 unknown): the bindings check their
+ * mirrors against it on load. */
+int64_t es_struct_size(int which);
+/* x[i] /= max(d[0], 1) for i < n (a sum over an expert's global batch -> its mean, d = the device count) */
+int es_div_by(float* x, int n, const float* d, es_stream_t stream);
 /* EMA of a flat parameter buffer — replaces EMAHelper.update (expertsim/train/loop.py:392-400):
  * shadow[i] = decay*shadow[i] + one_minus_decay*p[i], each product rounded, then one add. */
 int es_ema_update(float* shadow, const float* p, int64_t n, float decay, float one_minus_decay,
