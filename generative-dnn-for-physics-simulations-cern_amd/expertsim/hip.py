@@ -320,6 +320,12 @@ def active_tensor():
     return None if _LIVE is None else _LIVE[2]
 
 
+def live_count():
+    """The running expert's live rows as a host int (synchronises; tests and debugging only), or None
+    outside a dynamic-rows program."""
+    return None if _LIVE is None else int(_LIVE[1].item())
+
+
 def make_view(dims, strides) -> View:
     v = View()
     v.n, v.c, v.h, v.w = (int(d) for d in dims)

@@ -80,6 +80,10 @@ class Act:
             base = base.reshape(-1) if base.is_contiguous() else base
         return torch.as_strided(self.t, self.dims, self.strides, self.t.storage_offset())
 
+    def head(self, n):
+        """The first n samples (same memory)."""
+        return Act(self.t, (int(n), *self.dims[1:]), self.strides)
+
     def rows2d(self):
         n, c, h, w = self.dims
         assert h == 1 and w == 1

@@ -116,7 +116,11 @@ class MoEWrapper(nn.Module):
         """row0: the rows' first index in the expert's global batch (data parallel); a device int32 [1]
         under dynamic rows (es_expert_plan n0)."""
         if self.noise_fn is not None:
-            z = self.noise_fn(expert, which, shape).to(device=device, dtype=torch.float32)
+            try:
+                z = self.noise_fn(expert, which, shape)
+            except KeyError:      # injected draws of the reference's active experts only: an expert
+                z = torch.zeros(0, *shape[1:])   # it skipped runs on zero live rows here
+            z = z.to(device=device, dtype=torch.float32)
             if z.shape[0] < shape[0]:    # dynamic rows: the injected draw covers the live rows only
                 z = torch.cat([z, torch.zeros(shape[0] - z.shape[0], *shape[1:], dtype=z.dtype, device=device)])
             return z.contiguous()

@@ -20,6 +20,7 @@ DEV = "cuda"
 def test_neutron56_step_matches_oracle_restatement(E, B):
     import bench
     from oracle import expertsim_oracle as O
+    from expertsim import hip
     from expertsim.utils.synthetic import make_batch
     moe, (og, od, oa, orr), cfg = bench.build("neutron56", E, "fp32", 1234, torch.device(DEV))
     assert moe.image_shape == (56, 56) and moe.discriminators[0].flat_dim == 2304
@@ -38,7 +39,8 @@ def test_neutron56_step_matches_oracle_restatement(E, B):
 
     def rec(*a, **k):
         out = orig(*a, **k)
-        imgs.append(out[0].torch_nchw().detach().cpu().numpy())
+        n = hip.live_count()     # dynamic rows (E > 1): the first n of the capacity batch
+        imgs.append(out[0].torch_nchw()[:n].detach().cpu().numpy())
         return out
     moe.generators[0].fwd = rec
     t = lambda k: torch.from_numpy(b[k]).to(DEV)
