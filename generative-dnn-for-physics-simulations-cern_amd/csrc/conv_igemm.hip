@@ -603,14 +603,15 @@ __global__ void __launch_bounds__(NTHREADS) conv_glds_kernel(ConvArgs a) {
   const es_conv_desc_t& d = a.d;
   conv_live_gemm(a, MODE);
 
-  // XCD-aware tile order: consecutive tile ids on one XCD (bijective remap)
-  const int mt = gridDim.x;
+  // XCD-aware tile order: consecutive tile ids on one XCD (bijective remap).  Dynamic rows: over the
+  // live row tiles only (the rest exit), so that they spread over every XCD
+  const int mt = (a.M + BM - 1) / BM;
   const int nwg = mt * gridDim.y;
   const int orig = blockIdx.x + blockIdx.y * gridDim.x;
+  if (orig >= nwg) return;
   const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
   const int m0 = (wgid % mt) * BM, n0 = (wgid / mt) * BN;
-  if (m0 >= a.M) return;   // rows of images past the live count (dynamic rows)
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm0 = (wid >> 1) * (BM / 2), wn0 = (wid & 1) * (BN / 2);

@@ -411,10 +411,6 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   const int NL = conv_live(a);   // live images (dynamic rows)
   const SubPixel& sp = a.sp;
 
-  // tile order: the column tiles of one row tile are consecutive (they share the gathered rows)
-  const int nt = gridDim.y;
-  const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * nt);
-  const int tl = wg / nt, n0 = (wg % nt) * BN;
   // Row order: image groups g of NG = a.ng images (8..64); inside a group, per class (SP FWD: 4
   // parity classes, else one) the class's pixels in tiles of NB = BM/NG pixels (each class
   // segment padded to whole tiles); a tile is NG images x NB pixels, a DMA piece (8 rows) is 8
@@ -423,17 +419,26 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
   // footprint inside one XCD's L2).
   const int NG = a.ng, PPG = NG / PROWS;                 // pieces per pixel
   const int NB = BM / NG;
-  int cls = 0, gh, gw, TT, jt;
+  int TT;                                                // row tiles per image group
+  if constexpr (MODE == MODE_FWD && SP) TT = a.sp_merge ? sp.tile0[1] : (a.sp_tpc > 0 ? 4 * a.sp_tpc : sp.tile0[4]);
+  else if constexpr (MODE == MODE_FWD) TT = (d.P * d.Q + NB - 1) / NB;
+  else TT = ((a.fold ? d.H * d.W : d.Hu * d.Wu) + NB - 1) / NB;
+  // tile order: the column tiles of one row tile are consecutive (they share the gathered rows).
+  // Dynamic rows: the tiles of the live image groups (a prefix) are the ones remapped over the
+  // XCDs, so that they spread over the whole chip; the others exit below.
+  const int nt = gridDim.y, ntot = gridDim.x * nt, lin = blockIdx.x + blockIdx.y * gridDim.x;
+  const int nlive = NL == d.N ? ntot : min(ntot, (NL + NG - 1) / NG * TT * nt);
+  const int wg = lin < nlive ? xcd_remap(lin, nlive) : lin;
+  const int tl = wg / nt, n0 = (wg % nt) * BN;
+  int cls = 0, gh, gw, jt;
   if constexpr (MODE == MODE_FWD && SP) {
     if (a.sp_merge) {
       // merged classes: the rows are the (shared) source pixels of class 0's geometry, the
       // columns (class, channel); the class is resolved per wave in the epilogue
-      TT = sp.tile0[1];
       jt = tl % TT;
     } else if (a.sp_tpc > 0) {
       // class-interleaved: tile r = 4 jt + class, so the 4 class tiles of the same source
       // pixels run back to back (one XCD, shared L2); classes with fewer tiles skip the tail
-      TT = 4 * a.sp_tpc;
       const int r = tl % TT;
       cls = r & 3;
       jt = r >> 2;
@@ -446,7 +451,6 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
         return;
       }
     } else {
-      TT = sp.tile0[4];
       const int r = tl % TT;
       cls = (r >= sp.tile0[1]) + (r >= sp.tile0[2]) + (r >= sp.tile0[3]);
       jt = r - sp.tile0[cls];
@@ -461,7 +465,6 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
       gh = a.fold ? d.H : d.Hu;
       gw = a.fold ? d.W : d.Wu;
     }
-    TT = (gh * gw + NB - 1) / NB;
     jt = tl % TT;
   }
   const int PQ = gh * gw;
