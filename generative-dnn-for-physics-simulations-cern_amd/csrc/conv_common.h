@@ -86,8 +86,16 @@ struct ConvArgs {
 // skip the tiles / K-steps past it and read its images as zeros (buffer num_records).
 __device__ __forceinline__ int conv_live(const ConvArgs& a) {
   if (a.d.rows == nullptr) return a.d.N;
-  const int v = __builtin_amdgcn_readfirstlane(a.d.rows[0]) - a.nbase;
-  return v < 0 ? 0 : (v < a.d.N ? v : a.d.N);
+  const int px = a.d.rows_px > 0 ? a.d.rows_px : 1;
+  const int v = __builtin_amdgcn_readfirstlane(a.d.rows[0]) - a.nbase * px;
+  const int img = (v + px - 1) / px;       // (pixel rows: the images holding a live one)
+  return v <= 0 ? 0 : (img < a.d.N ? img : a.d.N);
+}
+// rows_px > 0: the live pixel rows (samples) of the launch, image-major; else INT_MAX (whole images)
+__device__ __forceinline__ int conv_live_px(const ConvArgs& a) {
+  if (a.d.rows == nullptr || a.d.rows_px <= 0) return 0x7fffffff;
+  const int v = __builtin_amdgcn_readfirstlane(a.d.rows[0]) - a.nbase * a.d.rows_px;
+  return v < 0 ? 0 : v;
 }
 
 // The generic GEMM kernels (conv_igemm.hip) shrink their problem to the live images: M (FWD /
@@ -95,9 +103,9 @@ __device__ __forceinline__ int conv_live(const ConvArgs& a) {
 __device__ __forceinline__ void conv_live_gemm(ConvArgs& a, int mode) {
   a.mslot = a.M;
   if (a.d.rows == nullptr) return;
-  const int nl = conv_live(a);
-  if (mode == MODE_WGRAD) a.Kd = nl * (a.Kd / a.d.N);
-  else a.M = nl * (a.M / a.d.N);
+  const int nl = conv_live(a), npx = conv_live_px(a);
+  if (mode == MODE_WGRAD) a.Kd = min(nl * (a.Kd / a.d.N), npx);
+  else a.M = min(nl * (a.M / a.d.N), npx);
 }
 
 

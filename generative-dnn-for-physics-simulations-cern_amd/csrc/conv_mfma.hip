@@ -871,7 +871,8 @@ __global__ void __launch_bounds__(RT) conv_ring_kernel(ConvArgs a) {
     }
     return (int64_t)row_img(r) * a.os[0] + (int64_t)y * a.os[2] + (int64_t)x * a.os[3];
   };
-  auto row_ok = [&](int r) { return row_pix(r) < PQ && row_img(r) < NL; };
+  const int NLP = conv_live_px(a);   // pixel rows (rows_px > 0): image i pixel p live when i*PQ + p < NLP
+  auto row_ok = [&](int r) { return row_pix(r) < PQ && row_img(r) < NL && row_img(r) * PQ + row_pix(r) < NLP; };
   // final values (bias added, rounded to the output dtype) back into acc
 #pragma unroll
   for (int j = 0; j < RN; ++j) {

@@ -63,6 +63,7 @@ struct Thin {
 // image-major, so they are a prefix of the M = N * pixels rows)
 __device__ __forceinline__ int thin_m(const Thin& t) {
   if (t.d.rows == nullptr) return t.M;
+  if (t.d.rows_px > 0) return min(t.M, max(__builtin_amdgcn_readfirstlane(t.d.rows[0]), 0));   // pixel rows
   return live_rows(t.d.rows, t.d.N) * (t.M / t.d.N);
 }
 

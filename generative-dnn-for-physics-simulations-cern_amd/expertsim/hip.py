@@ -38,7 +38,7 @@ class ConvDesc(C.Structure):
                 ("Wu", C.c_int), ("K", C.c_int), ("P", C.c_int), ("Q", C.c_int), ("R", C.c_int),
                 ("S", C.c_int), ("stride", C.c_int), ("pad", C.c_int), ("hmap", C.c_void_p),
                 ("wmap", C.c_void_p), ("up_h", C.c_int), ("up_w", C.c_int), ("subpixel", C.c_int),
-                ("rows", C.c_void_p)]
+                ("rows", C.c_void_p), ("rows_px", C.c_int)]
 
 
 class Norm(C.Structure):

@@ -20,9 +20,10 @@ from . import hip
 class Act:
     """Logical (N, C, H, W) tensor over a flat device buffer with explicit element strides."""
 
-    __slots__ = ("t", "dims", "strides", "bn_part", "bn_sums")
+    __slots__ = ("t", "dims", "strides", "bn_part", "bn_sums", "px")
 
     def __init__(self, t: torch.Tensor, dims, strides):
+        self.px = 0               # > 0: each image's P*Q pixels are px consecutive samples (pixel view)
         self.bn_part = None       # (partials, chunks) of fused BatchNorm statistics (ConvOp.fwd)
         self.bn_sums = None       # (partials, chunks, norm) of a fused BatchNorm-backward reduction (ConvOp.dgrad)
         self.t = t
@@ -371,6 +372,8 @@ class ConvOp:
         d.P = (d.Hu + 2 * self.pad - self.R) // self.stride + 1
         d.Q = (d.Wu + 2 * self.pad - self.S) // self.stride + 1
         d.rows = hip.rows_ptr(N)
+        if x.px:   # a pixel view (ConvOp._pixel_view): the live count is in samples = pixels
+            d.rows, d.rows_px = hip.rows_ptr(N * x.px), x.px
         return d
 
     def subpixel(self, d, dtype) -> bool:
@@ -437,15 +440,15 @@ class ConvOp:
         layout does not apply."""
         if not _LIN_PIX or self.R != 1 or self.S != 1 or self.up is not None or self.stride != 1 or self.pad != 0:
             return None
-        if hip.live_on():   # dynamic rows count samples, not the view's 16-sample images
-            return None
         N, Cc, H, W = x.dims
         dt = x.t.dtype
         if H != 1 or W != 1 or N % 16 or N < 256 or self.K < 1024 or self.K % 64 or x.strides[:2] != (Cc, 1):
             return None
         if not ((dt == torch.float32 and f32_split_level() > 0 and Cc % 32 == 0) or (dt == torch.bfloat16 and Cc % 64 == 0)):
             return None
-        return Act(x.t, (N // 16, Cc, 16, 1), (16 * Cc, 1, Cc, Cc))
+        v = Act(x.t, (N // 16, Cc, 16, 1), (16 * Cc, 1, Cc, Cc))
+        v.px = 16       # (dynamic rows count samples: the view's pixels)
+        return v
 
     def _linear_det(self, d, ng, out: Act) -> bool:
         """A linear (1x1 conv of 1x1 images) with a dense fp32 output of <= 4096 columns: the GEMMs

@@ -78,6 +78,7 @@ class MoEWrapper(nn.Module):
         self._w_cache = {}         # class_counts_adjusted device scalars
         self.expert_graphs = bool(cfg_get(cfg, "train.expert_graphs", True))
         self.expert_graphs_concurrent = True
+        self.expert_streams = None  # captured multi-expert steps: concurrent expert streams (None: E)
         self._egraphs = None       # ExpertGraphs (n_experts > 1, single process)
         self._graphs = None
         self._static = None
@@ -318,7 +319,7 @@ class MoEWrapper(nn.Module):
             self._graphs.join()
         if fork is not None:
             cur = torch.cuda.current_stream()
-            for st in fork:
+            for st in set(fork):
                 cur.wait_stream(st)
         if ddp is not None:
             # the global batch's per-expert metrics on every rank
@@ -382,13 +383,15 @@ class MoEWrapper(nn.Module):
 
     # ---------------------------------------------------------------------------- one expert
     def _fork_streams(self, E):
-        """One side stream per expert (kept across steps), each made to wait for the current stream."""
-        if getattr(self, "_side", None) is None or len(self._side) < E:
-            self._side = [torch.cuda.Stream() for _ in range(E)]
+        """Side streams for the experts (kept across steps; expert e on stream e mod S, S =
+        expert_streams or E), each made to wait for the current stream."""
+        S = max(1, min(E, self.expert_streams or E))
+        if getattr(self, "_side", None) is None or len(self._side) < S:
+            self._side = [torch.cuda.Stream() for _ in range(S)]
         cur = torch.cuda.current_stream()
-        for st in self._side[:E]:
+        for st in self._side[:S]:
             st.wait_stream(cur)
-        return self._side[:E]
+        return [self._side[e % S] for e in range(E)]
 
     def _plan(self, counts, B, dev):
         """The multi-expert step plan on the device (es_expert_plan): per expert the live rows of this

@@ -96,6 +96,9 @@ typedef struct {
                           conv (es_pack_conv_weight mode 2 for fwd, 3 for dgrad) and the conv runs
                           as 4 parity-class convs on the source grid (es_conv_subpixel_ok).      */
   const int32_t* rows; /* optional device int32: live images of the N-capacity batch (es_view_t) */
+  int rows_px;         /* > 0: rows counts SAMPLES that are the P*Q == rows_px pixels of each image
+                          (a linear over 16-sample pixel blocks, layers.ConvOp._pixel_view): image i
+                          pixel p is live when i*rows_px + p < rows[0]                             */
 } es_conv_desc_t;
 
 /* y[n,k,p,q] = bias[k] + sum_{c,r,s} xu[n,c,p*stride-pad+r,q*stride-pad+s] * W[k,c,r,s]

@@ -61,6 +61,7 @@ CONV = [
     (40, 9, 1, 44, 44, 32, 3, 1, 0, None),          # Cin = 1 (thin)
     (40, 17, 32, 21, 21, 16, 3, 1, 0, None),        # D conv_layers.4 (generic igemm)
     (40, 17, 256, 1, 1, 1024, 1, 1, 0, None),       # a linear (generic / split-K det)
+    (512, 203, 256, 1, 1, 1024, 1, 1, 0, None),     # a wide linear: FWD over 16-sample pixel blocks
 ]
 
 
@@ -105,6 +106,15 @@ def test_conv_dynamic_rows(case, mode):
     torch.cuda.synchronize()
     live = lambda a: a.torch_nchw()[:n].float()
     assert _rel(live(y), yr.torch_nchw().float()) <= tol
+    if y.bn_part is not None:   # fused BatchNorm partials of the FWD epilogue: the live rows only
+        part, chunks = y.bn_part
+        st = torch.empty(3, Cout, device=DEV)
+        hip.call("es_norm_stats_merge", hip.ptr(part), chunks, Cout, hip.ptr(st), hip.stream_ptr())
+        yv = yr.torch_nchw().double().permute(1, 0, 2, 3).reshape(Cout, -1)
+        mu = yv.mean(1)
+        assert torch.equal(st[0].cpu(), torch.full((Cout,), float(yv.shape[1])))
+        assert _rel(st[1].cpu(), mu.cpu()) <= 1e-5
+        assert _rel(st[2].cpu(), ((yv - mu[:, None]) ** 2).sum(1).cpu()) <= 1e-4
     assert _rel(live(dx), dxr.torch_nchw().float()) <= tol
     assert _rel(dw, dwr) <= tol and _rel(db, dbr) <= tol
     assert torch.isfinite(dw).all() and torch.isfinite(db).all()
