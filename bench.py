@@ -367,6 +367,11 @@ def main():
                     help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse several ranks "
                          "on one GPU)")
     args = ap.parse_args()
+    # measured lines come from the default build and kernel paths only: no ES_* environment override
+    # (ES_LIB would load another build; INTEGRATION.md §2 lists the test hooks)
+    stray = sorted(k for k in os.environ if k.startswith("ES_"))
+    if stray:
+        sys.exit(f"bench.py: refusing to run with experimental switches set: {', '.join(stray)}")
     global FP32_MFMA
     FP32_MFMA = args.fp32_mfma
 
@@ -405,7 +410,8 @@ def main():
                                            3 if probe_steps else 0)
         other = {"dtype": other_p, "value": round(vo, 2), "unit": "images/s", "steps": args.other_steps,
                  "ms_per_step": round(dto / args.other_steps * 1e3, 3), "step_launch": launcho,
-                 "step_mfma_frac": step_exec_frac(roofo, dto / args.other_steps * 1e3),
+                 "step_pipe_busy_frac": step_exec_frac(roofo, dto / args.other_steps * 1e3),
+                 "step_mfma_frac": round(STEP_FLOP_PER_IMAGE[args.arch] * vo / 1e12 / PEAK_TFLOPS[other_p], 4),
                  "roofline": roofo,
                  "note": ("bf16 performance mode: bf16 GEMM operands, fp32 accumulation / statistics / "
                           "parameters; validated statistically (tests/test_bf16_stats_gpu.py)" if other_p == "bf16"
@@ -424,10 +430,14 @@ def main():
                        "global_batch": args.batch * world, "image": IMAGE[args.arch],
                        "parallelism": f"dp{world}", "sync_bn": bool(args.sync_bn) if ddp else None},
             "step_tflops_alg": round(step_flops / 1e12, 2),
-            "step_mfma_frac": step_exec_frac(roof, dt / args.steps * 1e3),
-            "step_mfma_frac_note": "executed conv MFMA FLOPs per step (bf16 pipe incl. split-fp32 plane products "
-                                   "at 2500 TF, exact fp32 MFMA at 157.3 TF) / step time; step_tflops_alg = the "
-                                   "reference's 10.573 GFLOP/image x images/s (an algorithmic rate)",
+            "step_mfma_frac": round(step_flops / 1e12 / PEAK_TFLOPS[args.precision], 4),
+            "step_pipe_busy_frac": step_exec_frac(roof, dt / args.steps * 1e3),
+            "step_frac_note": "step_mfma_frac = the reference's FLOPs per step (step_tflops_alg: "
+                              f"{STEP_FLOP_PER_IMAGE[args.arch] / 1e9:.3f} GFLOP/image x images/s) / the dense peak "
+                              "of the mode's arithmetic type (fp32 157.3, bf16 2500 TFLOP/s), comparable across "
+                              "rounds; step_pipe_busy_frac = EXECUTED conv MFMA FLOPs per step (bf16 pipe incl. "
+                              "split-fp32 plane products at 2500 TF, exact fp32 MFMA at 157.3 TF) / step time, how "
+                              "busy the pipes the convs run on would be at peak",
             "roofline": roof,
         }
         if args.precision == "fp32":

@@ -504,8 +504,8 @@ class ConvOp:
             return dx
         dxu = Act.nhwc(N, Cc, d.Hu, d.Wu, torch.float32, dy.t.device)
         if self._resized(x):   # the plain conv's dgrad w.r.t. the materialised resized input
-            self._plain_op().dgrad(dy, Act(x.t, (N, Cc, d.Hu, d.Wu), (d.Hu * d.Wu * Cc, 1, d.Wu * Cc, Cc)),
-                                   dx_dtype=torch.float32, inv_scale=inv_scale, dx=dxu)
+            # (x of the plain dgrad only gives the input geometry: dxu, exactly that shape and storage)
+            self._plain_op().dgrad(dy, dxu, dx_dtype=torch.float32, inv_scale=inv_scale, dx=dxu)
         else:
           with _probed(self.label and self.label + ".dgrad"):
             hip.call("es_conv2d_dgrad", C.byref(d), dy.dt, dy.ptr, hip.strides4(dy.strides), hip.ptr(wd),

@@ -29,7 +29,6 @@ step of the global batch.
 """
 from __future__ import annotations
 
-import os
 
 import copy
 import ctypes as C
@@ -78,7 +77,6 @@ class MoEWrapper(nn.Module):
         self._w_cache = {}         # class_counts_adjusted device scalars
         self.expert_graphs = bool(cfg_get(cfg, "train.expert_graphs", True))
         self.expert_graphs_concurrent = True
-        self.expert_streams = None  # captured multi-expert steps: concurrent expert streams (None: E)
         self._egraphs = None       # ExpertGraphs (n_experts > 1, single process)
         self._graphs = None
         self._static = None
@@ -90,7 +88,7 @@ class MoEWrapper(nn.Module):
         self.deterministic = bool(cfg_get(cfg, "train.deterministic", True))
         # fp32 conv arithmetic: "exact" (v_mfma_f32_16x16x4_f32) or "split" (three bf16 planes per
         # operand, six plane products on the bf16 MFMA; es_conv_set_f32_split)
-        self.fp32_mfma = os.environ.get("ES_FP32_MFMA") or str(cfg_get(cfg, "train.fp32_mfma", "split"))
+        self.fp32_mfma = str(cfg_get(cfg, "train.fp32_mfma", "split"))
         if self.fp32_mfma not in ("exact", "split"):
             raise ValueError(f"train.fp32_mfma must be exact or split, got {self.fp32_mfma!r}")
         self.set_precision(cfg_get(cfg, "train.precision", "fp32"))
@@ -383,15 +381,15 @@ class MoEWrapper(nn.Module):
 
     # ---------------------------------------------------------------------------- one expert
     def _fork_streams(self, E):
-        """Side streams for the experts (kept across steps; expert e on stream e mod S, S =
-        expert_streams or E), each made to wait for the current stream."""
-        S = max(1, min(E, self.expert_streams or E))
-        if getattr(self, "_side", None) is None or len(self._side) < S:
-            self._side = [torch.cuda.Stream() for _ in range(S)]
+        """One side stream per expert (kept across steps), each made to wait for the current stream.
+        (Measured, E = 4 B = 512 fp32: 2 / 3 / 4 streams 31.4 / 32.8 / 28.9 ms per step; 8 hardware
+        queues instead of 4: 35.3 ms.)"""
+        if getattr(self, "_side", None) is None or len(self._side) < E:
+            self._side = [torch.cuda.Stream() for _ in range(E)]
         cur = torch.cuda.current_stream()
-        for st in self._side[:S]:
+        for st in self._side[:E]:
             st.wait_stream(cur)
-        return [self._side[e % S] for e in range(E)]
+        return self._side[:E]
 
     def _plan(self, counts, B, dev):
         """The multi-expert step plan on the device (es_expert_plan): per expert the live rows of this

@@ -87,3 +87,57 @@ def test_large_batch_step0_matches_reference(case):
         comp = label[3]
         tol = max(TOL["neutron"], A_STEP0_TOL.get("neutron", 0.0)) if comp == "A" else TOL["neutron"]
         _check(grad_errors(g, 0, label, grads, "neutron", comp), tol, (case, 0, label), abs_tol=abs_tol)
+
+
+def test_e4_b2048_step0_matches_reference():
+    """BASELINE configs[3] (E = 4, B = 2048) on one GPU against the reference's own step 0
+    (tests/golden/neutron_e4_b2048.npz): the multi-expert step on dynamic rows (capacity 2048 per
+    expert, live counts on the device).  Metrics, generated images, D outputs / latents, aux coords
+    <= 1e-4 relative; every optimizer's parameter gradients as the B = 512 / 1024 cases."""
+    g = Golden("neutron_e4_b2048")
+    assert g.E == 4 and g.B == 2048
+    moe, (og, od, oa, orr), cfg = _build(g)
+    rec = _record(moe)
+    store = {}
+    labels = {}
+    for e in range(g.E):
+        labels[f"optG{e}"] = (og[e], moe.generators[e])
+        labels[f"optD{e}"] = (od[e], moe.discriminators[e])
+        labels[f"optA{e}"] = (oa[e], moe.aux_regs[e])
+    _capture(labels, store)
+    inp = g.inputs(0)
+    nz = g.noise(0)
+    moe.noise_fn = lambda e, w, shape: torch.from_numpy(nz[(e, w)])
+    gum = torch.from_numpy(g.gumbel(0))
+    moe.gumbel_fn = lambda shape: gum
+    t = lambda k: torch.from_numpy(inp[k]).to(DEV)
+    met = moe.train_step(g.epoch, t("cond"), t("real_images").unsqueeze(1), t("true_positions"), t("std"),
+                         t("intensity"), oa, og, od, orr, None, DEV)
+    torch.cuda.synchronize()
+    met = {k: float(v) for k, v in met.items()}
+    gm = g.metrics(0)
+    assert set(met) == set(gm)
+    for k, v in gm.items():
+        assert abs(met[k] - v) <= 1e-4 * max(abs(v), 1e-3), (k, met[k], v)
+    errs = {}
+    for e in range(g.E):
+        for c, (img, _) in enumerate(rec.get(f"G{e}", [])):
+            errs[f"G{e}.{c}"] = _ck_err(img.torch_nchw().cpu().numpy(), g[f"s0/G{e}/call{c}/out0_ck"])
+        for c, (out, lat, _) in enumerate(rec.get(f"D{e}", [])):
+            ref = f"s0/D{e}/call{c}/out0"
+            mine = out.rows2d().cpu().numpy()
+            errs[f"D{e}.{c}.out"] = _rel(mine, g[ref]) if g.has(ref) else _ck_err(mine, g[ref + "_ck"])
+            errs[f"D{e}.{c}.latent"] = _ck_err(lat.rows2d().cpu().numpy(), g[f"s0/D{e}/call{c}/out1_ck"])
+        for c, (coords, _) in enumerate(rec.get(f"A{e}", [])):
+            ref = f"s0/A{e}/call{c}/out0"
+            mine = coords.rows2d().cpu().numpy()
+            errs[f"A{e}.{c}"] = _rel(mine, g[ref]) if g.has(ref) else _ck_err(mine, g[ref + "_ck"])
+    print("E=4 B=2048 output errors:", {k: f"{v:.2e}" for k, v in errs.items()})
+    assert errs and all(e <= 1e-4 for e in errs.values()), errs
+    want = {k.split("/")[1] for k in g.keys("s0/") if "/grad/" in k} - {"optR"}
+    assert set(store) == want, (sorted(store), sorted(want))
+    abs_tol = 1e-5 * max(1.0, g.B / g.E / 512)
+    for label, grads in store.items():
+        comp = label[3]
+        tol = max(TOL["neutron"], A_STEP0_TOL.get("neutron", 0.0)) if comp == "A" else TOL["neutron"]
+        _check(grad_errors(g, 0, label, grads, "neutron", comp), tol, ("e4_b2048", 0, label), abs_tol=abs_tol)

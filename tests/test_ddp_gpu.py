@@ -36,7 +36,7 @@ def _free_port():
     return p
 
 
-def _run(E, B, rank=0, ddp=None):
+def _run(E, B, rank=0, ddp=None, b_global=B_GLOBAL, steps=STEPS):
     import bench
     from expertsim.utils.synthetic import make_batch
     dev = torch.device("cuda", 0)
@@ -45,8 +45,8 @@ def _run(E, B, rank=0, ddp=None):
         moe.ddp = ddp
         moe.rank = ddp.rank
     out = []
-    for s in range(STEPS):
-        b = make_batch(B_GLOBAL, "neutron", seed=70 + s)
+    for s in range(steps):
+        b = make_batch(b_global, "neutron", seed=70 + s)
         rows = slice(rank * B, (rank + 1) * B)
         t = {k: torch.from_numpy(v[rows].copy()).to(dev) for k, v in b.items()}
         m = moe.train_step(0, t["cond"], t["real_images"].unsqueeze(1), t["true_positions"], t["std"],
@@ -72,7 +72,7 @@ def _run(E, B, rank=0, ddp=None):
     return out, lr
 
 
-def _worker(rank, world, port, q, E, sync):
+def _worker(rank, world, port, q, E, sync, b_global=B_GLOBAL, steps=STEPS):
     import sys
     from conftest import PKG_DIR, REPO
     for p in (PKG_DIR, REPO):
@@ -84,21 +84,21 @@ def _worker(rank, world, port, q, E, sync):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from expertsim.train.ddp import DataParallel
     try:
-        res, _ = _run(E, B_GLOBAL // world, rank, DataParallel(sync_bn=sync))
+        res, _ = _run(E, b_global // world, rank, DataParallel(sync_bn=sync), b_global, steps)
         q.put((rank, res, None))
     except Exception as e:         # report instead of hanging the parent
         q.put((rank, None, repr(e)))
     dist.destroy_process_group()
 
 
-def _spawn(E, sync):
+def _spawn(E, sync, world=WORLD, b_global=B_GLOBAL, steps=STEPS):
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q, E, sync)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, E, sync, b_global, steps)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted((q.get(timeout=240) for _ in range(WORLD)), key=lambda r: r[0])
+    res = sorted((q.get(timeout=400) for _ in range(world)), key=lambda r: r[0])
     for p in procs:
         p.join(timeout=60)
     for rank, r, err in res:
@@ -128,3 +128,18 @@ def test_ddp_sync_bn_matches_single_device(E):
     print(f"E={E}: DP(sync-BN) vs single (metric rel, param / lr): {dev}; DP(per-rank BN): {local}")
     assert dev[0][0] <= 1e-4 and dev[0][1] <= 2.0 + 1e-3
     assert dev[1][0] <= 2e-2 and dev[1][1] <= 4.0 + 1e-3
+
+
+@pytest.mark.timeout(900)
+def test_ddp4_syncbn_e4_b2048_matches_single_device():
+    """BASELINE configs[3] data parallel: 4 ranks x 512 (gloo on the one GPU, SyncBN, dynamic-rows
+    multi-expert step) against ONE process on the global batch of 2048, step 0: every metric <= 1e-4
+    relative, parameters <= 2 lr (Adam's first step), the ranks bitwise equal to each other."""
+    single, lr = _run(4, 2048, b_global=2048, steps=1)
+    dp = _spawn(4, True, world=4, b_global=2048, steps=1)
+    for r in range(1, 4):
+        assert dp[0][0][0] == dp[r][0][0]
+        assert all(np.array_equal(dp[0][0][1][n], dp[r][0][1][n]) for n in dp[0][0][1])
+    dev = _deviation(single, dp[0], lr)
+    print("E=4 B=2048, 4-rank SyncBN vs single (metric rel, param / lr):", dev)
+    assert dev[0][0] <= 1e-4 and dev[0][1] <= 2.0 + 1e-3

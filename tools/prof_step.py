@@ -24,12 +24,10 @@ def main():
     ap.add_argument("--precision", default="fp32")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--serial", action="store_true")
-    ap.add_argument("--streams", type=int, default=0)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     moe, (og, od, oa, orr), cfg = bench.build(a.arch, a.experts, a.precision, 1234, dev)
     moe.expert_graphs_concurrent = not a.serial
-    moe.expert_streams = a.streams or None
     b = make_batch(a.batch, a.arch, seed=1000)
     t = {k: torch.from_numpy(v).to(dev) for k, v in b.items()}
     args = (0, t["cond"], t["real_images"].unsqueeze(1).contiguous(), t["true_positions"], t["std"], t["intensity"],
@@ -44,7 +42,7 @@ def main():
         sg.replay()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
-    print(f"E={a.experts} B={a.batch} {a.precision} serial={a.serial} streams={a.streams}: {dt * 1e3:.2f} ms/step")
+    print(f"E={a.experts} B={a.batch} {a.precision} serial={a.serial}: {dt * 1e3:.2f} ms/step")
 
 
 if __name__ == "__main__":
