@@ -13,8 +13,13 @@ gradient buffer each FusedAdam reads) and compared with SURVEY.md §8(c)'s contr
     residual biases) — is checked absolutely: ||g|| <= 1e-5;
   * step 0 is the contract step.  At step 1 every parameter has moved by +-lr through Adam's
     first step whatever its gradient's size (SURVEY.md §8(c) hard part (c)), so rounding-level
-    sign flips of tiny step-0 gradients change the step-1 gradients; they are held to the
-    STEP1_TOL norm-relative bound (the reference's own sensitivity, see test_train_step_gpu.py).
+    sign flips of tiny step-0 gradients change the step-1 gradients.  Their bound is the
+    reference's OWN sensitivity, per parameter: tools/grad_sensitivity.py reruns the oracle
+    (bit-exact to the goldens) with every linear / conv output of both steps perturbed by 1e-6
+    relative (the HIP path's own deviation from the reference) and records the worst step-1 error
+    against the goldens over 6 trials (tests/golden/sensitivity_<case>_s1.json); a parameter is held
+    to max(step-0 bound, 3 x that).  (proton_e1_b8's G conv_layers.11.bias: HIP 0.093 in round 4,
+    the reference itself 0.076 under the perturbation -- the step-1 spread, not a defect.)
 
 A second test drives the same step through the reference's nn.Module API — ``G(noise, cond)``,
 ``D(img, cond)``, ``A(img)``, losses in torch, ``loss.backward()``, ``opt.step()`` — i.e. the
@@ -51,12 +56,6 @@ CASE_TOL = {"proton_e3_b12": 1e-2}
 # proton 1.7e-5 (r03b).
 A_STEP0_TOL = {"neutron": 1e-2}
 A_ORACLE_TOL = {"neutron": 1e-2, "proton": 1e-3}
-# step-1 gradients, per case: ~2x the fixed outcome of the deterministic fp32 mode (r04d, worst
-# parameter per case: neutron_e1_b8 1.6e-2 (A conv1.weight), neutron_e3_b12 0.127 (expert 1 A
-# conv1_bd.weight; B_e = 2-4 BatchNorm after Adam's +-lr first step), proton_e1_b8 0.093 (G
-# conv_layers.11.bias), proton_e3_b12 1.7e-2); round 3 held every case to 0.25
-STEP1_TOL = {"neutron_e1_b8": 0.05, "neutron_e3_b12": 0.25, "neutron_e3_b12_router": 0.25, "proton_e1_b8": 0.2,
-             "proton_e3_b12": 0.05}
 # noise-only set after Adam's +-lr first step: BatchNorm over B_e = 2 samples (neutron_e3 step 1
 # experts 0 and 2) has invstd up to ~1e3, so the analytically-zero bias sums cancel at ~1e-4
 # (measured 2.0e-5 and 1.06e-4 on fc1.0.bias)
@@ -104,7 +103,18 @@ def grad_errors(g: Golden, s, label, grads, arch, comp):
     return out
 
 
-def _check(errs, tol, what, abs_tol=1e-5):
+def sensitivity(case, step):
+    """The reference's own gradient sensitivity for a case and step (tests/golden/sensitivity_*.json,
+    tools/grad_sensitivity.py: the oracle with every linear / conv output perturbed by 1e-6 relative,
+    worst error against the goldens over its trials), {"optG0/name": err}; {} when not measured."""
+    import json
+    import os
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"sensitivity_{case}_s{step}.json")
+    return json.load(open(p))["worst"] if os.path.exists(p) else {}
+
+
+def _check(errs, tol, what, abs_tol=1e-5, sens=None, label=None):
+    """sens (per-parameter reference sensitivity): a parameter's bound is max(tol, 3 x sens)."""
     worst = max((e for e in errs if e[1] == "rel"), key=lambda e: e[2], default=None)
     print(what, "worst rel:", worst, "worst abs:",
           max((e for e in errs if e[1] == "abs"), key=lambda e: e[2], default=None))
@@ -113,7 +123,8 @@ def _check(errs, tol, what, abs_tol=1e-5):
         if kind == "abs":
             assert e <= abs_tol, (what, n, e)
         else:
-            assert e <= tol, (what, n, e)
+            bound = max(tol, 3.0 * (sens or {}).get(f"{label}/{n}", 0.0))
+            assert e <= bound, (what, n, e, bound)
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -141,12 +152,14 @@ def test_step_gradients_match_reference(case):
         torch.cuda.synchronize()
         want = {k.split("/")[1] for k in g.keys(f"s{s}/") if "/grad/" in k}
         assert set(store) == want, (s, sorted(store), sorted(want))
-        tol = CASE_TOL.get(case, TOL[g.arch]) if s == 0 else STEP1_TOL[case]
+        tol = CASE_TOL.get(case, TOL[g.arch])
+        sens = sensitivity(case, s) if s > 0 else None
+        assert s == 0 or sens, f"{case}: no step-{s} sensitivity fixture (tools/grad_sensitivity.py)"
         for label, grads in store.items():
             comp = label[3]
             lt = max(tol, A_STEP0_TOL.get(g.arch, 0.0)) if comp == "A" and s == 0 else tol
             _check(grad_errors(g, s, label, grads, g.arch, comp), lt, (case, s, label),
-                   abs_tol=1e-5 if s == 0 else STEP1_ABS)
+                   abs_tol=1e-5 if s == 0 else STEP1_ABS, sens=sens, label=label)
 
 
 @pytest.mark.parametrize("case", [c for c in CASES if "_e1_" in c])
