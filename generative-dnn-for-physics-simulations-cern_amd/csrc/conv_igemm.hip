@@ -888,8 +888,11 @@ int launch(ConvArgs& a, bool avec, bool bvec, hipStream_t st) {
     // fp32 parity mode: the 8-wave LDS-DMA ring kernels on v_mfma_f32_16x16x4_f32 (conv_mfma.hip)
     // for real convolutions whose K-steps are one tap x 32 channels
     const int nch = MODE == MODE_FWD ? a.d.C : a.d.K;
+    // (the gathered grid's pixels per image: >= 8 keeps the row tiles' padding small; the aux
+    // regressor's conv4 has a 1 x 15 output and a 3 x 17 input; linears take the pixel view)
+    const int gpix = MODE == MODE_FWD ? a.d.P * a.d.Q : a.d.Hu * a.d.Wu;
     if (avec && bvec && nch % 32 == 0 && a.Kd % 32 == 0 && a.d.stride <= 2 && a.d.hmap == nullptr &&
-        a.d.P * a.d.Q >= 16 && a.M >= 128 && !g_no_glds) {
+        gpix >= 8 && a.M >= 128 && !g_no_glds) {
       a.k_per_split = a.Kd;
       a.splitk = 0;
       const int rc = es_conv_ring_launch_f32(a, MODE, st);

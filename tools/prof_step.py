@@ -4,13 +4,15 @@ usage: python tools/prof_step.py --experts 4 --batch 512 [--serial] [--steps 10]
 --serial: a multi-expert step's experts run one after another inside the graph (no stream fork),
 so that kernel durations in a profile are not stretched by concurrent experts."""
 import argparse
+import os
 import sys
 import time
 
 import torch
 
-sys.path.insert(0, "generative-dnn-for-physics-simulations-cern_amd")
-sys.path.insert(0, ".")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "generative-dnn-for-physics-simulations-cern_amd"))
+sys.path.insert(0, ROOT)
 import bench
 from expertsim.graph import StepGraph
 from expertsim.utils.synthetic import make_batch
@@ -24,6 +26,8 @@ def main():
     ap.add_argument("--precision", default="fp32")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--serial", action="store_true")
+    ap.add_argument("--sync", action="store_true", help="synchronise after every replay (PMC passes: one "
+                    "replay's packets in flight)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     moe, (og, od, oa, orr), cfg = bench.build(a.arch, a.experts, a.precision, 1234, dev)
@@ -40,6 +44,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         sg.replay()
+        if a.sync:
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
     print(f"E={a.experts} B={a.batch} {a.precision} serial={a.serial}: {dt * 1e3:.2f} ms/step")
