@@ -135,11 +135,23 @@ __device__ __forceinline__ f32x4 mm16_rowb(const float* A, int PA, const float* 
 
 // stage rows r0 .. r0 + nrow - 1 of X (rows past the batch and columns past F: zeros) as a
 // [RB][x_pitch(F)] tile in LDS, coalesced along the rows
+// (8 loads in flight per thread before their LDS stores: the tile is ~40 loads per thread, and one
+// load-store pair per trip left every trip waiting on a global round trip)
 __device__ __forceinline__ void stage_x(const float* X, int64_t xs, int r0, int nrow, int F, float* t) {
-  const int PX = x_pitch(F), W = PX - 4;
-  for (int i = threadIdx.x; i < RB * W; i += MT) {
-    const int r = i / W, k = i - r * W;
-    t[r * PX + k] = (r < nrow && k < F) ? X[(int64_t)(r0 + r) * xs + k] : 0.f;
+  constexpr int U = 8;
+  const int PX = x_pitch(F), W = PX - 4, n = RB * W;
+  for (int i0 = threadIdx.x; i0 < n; i0 += U * MT) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * MT, r = i / W, k = i - r * W;
+      v[u] = (i < n && r < nrow && k < F) ? X[(int64_t)(r0 + r) * xs + k] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * MT, r = i / W, k = i - r * W;
+      if (i < n) t[r * PX + k] = v[u];
+    }
   }
 }
 
@@ -418,13 +430,33 @@ __global__ void __launch_bounds__(MT) dmlp_bwd_kernel(MlpArgs a) {
   }
   if (WDX) {
     // dX = dh3 W1 / sigma1: column tiles of k over the waves, K = 128
+    // (a lane's 32 W1 values of the next column tile (rows i = 4 j + kq) are loaded before the current
+    // tile's MFMAs: one global round trip per tile, overlapped, instead of one per 8 k; the two
+    // accumulator chains and their order are mm16's)
     const float inv = p.sigma1 ? 1.f / p.sigma1[0] : 1.f;
+    constexpr int NJ = H1 / 4;
+    float bw[NJ];
+    auto load_w = [&](int k0) {
+      const int k = k0 + r16;
+      const int kc = k < a.F ? k : 0;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bw[j] = p.w1[(int64_t)(4 * j + kq) * a.F + kc];
+    };
+    if (wid * 16 < a.F) load_w(wid * 16);
     for (int k0 = wid * 16; k0 < a.F; k0 += MNW * 16) {
       const int k = k0 + r16;
       const bool kin = k < a.F;
-      const int kc = kin ? k : 0;
-      const f32x4 acc =
-          mm16(H1, [&](int i) { return g3[r16][i]; }, [&](int i) { return p.w1[(int64_t)i * a.F + kc] * inv; });
+      float bc[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bc[j] = bw[j];
+      if (k0 + MNW * 16 < a.F) load_w(k0 + MNW * 16);
+      f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < NJ; j += 2) {
+        c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(g3[r16][4 * j + kq], bc[j] * inv, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(g3[r16][4 * j + 4 + kq], bc[j + 1] * inv, c1, 0, 0, 0);
+      }
+      const f32x4 acc = c0 + c1;
       if (kin)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
