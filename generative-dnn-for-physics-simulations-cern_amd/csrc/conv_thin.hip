@@ -427,12 +427,83 @@ __global__ void __launch_bounds__(NT) k1_dgrad_bnred(Thin t, int LP, ThinBnr b) 
   }
 }
 
-// wgrad: dw[r][s][c] = sum over pixels of dy[pix] * x[pix + (r,s)][c]; lane = CH channel chunks
+// Input-major forms of the Cout == 1 forward and weight gradient.  The output-major kernels above
+// read every input pixel once per tap (4x for 2x2 taps, through L2 / MALL) and ran at ~2.4 TB/s of
+// unique input; these read each input pixel ONCE.
+// fwd: one workgroup per image.  Per input pixel, the RS partial dots t_j = <x, w_j> (reduced over the
+// LP lanes of the pixel) go to LDS; then y(p, q) = bias + sum_j t_j(p - pad + r_j, q - pad + s_j).
+constexpr int K1_TP_FLOATS = 9216;   // LDS floats of the per-tap partial dots (RS * H * W)
+template <typename T, typename TO, int RS>
+__global__ void __launch_bounds__(NT) k1_fwd_img(Thin t, int LP) {
+  constexpr int VN = V16<T>::N;
+  const es_conv_desc_t& d = t.d;
+  const int n = blockIdx.x;
+  if (n >= live_rows(d.rows, d.N)) return;   // dynamic rows: a padding image
+  __shared__ float wf[1024];                 // [R][S][C]
+  __shared__ float tp[K1_TP_FLOATS];         // [RS][H * W]
+  for (int i = threadIdx.x; i < RS * d.C; i += NT) wf[i] = to_f(((const T*)t.w)[i]);
+  __syncthreads();
+  const int HW = d.H * d.W, PPB = NT / LP, l = threadIdx.x % LP;
+  const T* xn = (const T*)t.a + n * t.as[0] + l * VN;
+  constexpr int U = 4;                       // four pixels per trip: their loads issue together
+  for (int m0 = 0; m0 < HW; m0 += U * PPB) {
+    float v[U][VN];
+    int mm[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int m = m0 + u * PPB + threadIdx.x / LP;
+      mm[u] = m;
+      const int mc = m < HW ? m : 0;
+      const int h = mc / d.W, w = mc - h * d.W;
+      const T* px = xn + h * t.as[2] + w * t.as[3];
+      if constexpr (VN == 8) {
+        ld8<T>(px, v[u]);
+      } else {
+        const float4 q4 = *(const float4*)px;
+        v[u][0] = q4.x; v[u][1] = q4.y; v[u][2] = q4.z; v[u][3] = q4.w;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float s[RS];
+#pragma unroll
+      for (int j = 0; j < RS; ++j) {
+        const float* wr = wf + j * d.C + l * VN;
+        float a = 0.f;
+#pragma unroll
+        for (int e = 0; e < VN; ++e) a += v[u][e] * wr[e];
+        s[j] = a;
+      }
+      for (int o = LP >> 1; o > 0; o >>= 1)
+#pragma unroll
+        for (int j = 0; j < RS; ++j) s[j] += __shfl_xor(s[j], o, 64);
+      if (l == 0 && mm[u] < HW)
+#pragma unroll
+        for (int j = 0; j < RS; ++j) tp[j * HW + mm[u]] = s[j];
+    }
+  }
+  __syncthreads();
+  const float b0 = t.bias ? t.bias[0] : 0.f;
+  TO* yn = (TO*)t.out + n * t.os[0];
+  for (int o = threadIdx.x; o < d.P * d.Q; o += NT) {
+    const int p = o / d.Q, q = o - p * d.Q;
+    float y = 0.f;
+#pragma unroll
+    for (int j = 0; j < RS; ++j) {
+      const int h = p - d.pad + j / d.S, w = q - d.pad + j % d.S;
+      if ((unsigned)h < (unsigned)d.H && (unsigned)w < (unsigned)d.W) y += tp[j * HW + h * d.W + w];
+    }
+    yn[p * t.os[2] + q * t.os[3]] = from_f<TO>(y + b0);
+  }
+}
+
+// wgrad: dw[r][s][c] = sum over input pixels (h, w) of x[h][w][c] * dy[h + pad - r][w + pad - s]
+// (the dy values are 4-byte L2 hits; x is streamed once, 16-byte chunks)
 template <typename T, int RS, int CH = 1>
-__global__ void __launch_bounds__(NT) k1_wgrad(Thin t, int LP) {
+__global__ void __launch_bounds__(NT) k1_wgrad_in(Thin t, int LP) {
   constexpr int VN = V16<T>::N, VC = VN * CH;
   const es_conv_desc_t& d = t.d;
-  t.M = thin_m(t);   // dynamic rows: the live images' pixels
+  const int Mi = live_rows(d.rows, d.N) * d.H * d.W;   // the live images' input pixels
   const int PPB = NT / LP;
   const int l = threadIdx.x % LP;
   float acc[RS][VC];
@@ -440,35 +511,34 @@ __global__ void __launch_bounds__(NT) k1_wgrad(Thin t, int LP) {
   for (int j = 0; j < RS; ++j)
 #pragma unroll
     for (int e = 0; e < VC; ++e) acc[j][e] = 0.f;
-  // two pixels per trip (one with CH > 1): the tap loads are issued before the FMAs
-  constexpr int U = CH > 1 ? 1 : 2;
+  constexpr int U = CH > 1 ? 2 : 4;
   const int stride = gridDim.x * PPB;
-  for (int m0 = blockIdx.x * PPB + threadIdx.x / LP; m0 < t.M; m0 += U * stride) {
-    float gj[U][RS];
-    float v[U][RS][VC];
+  for (int m0 = blockIdx.x * PPB + threadIdx.x / LP; m0 < Mi; m0 += U * stride) {
+    float g[U][RS];
+    float v[U][VC];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int mu = m0 + u * stride;
-      const bool live = mu < t.M;
-      int n, p, q;
-      pix3(live ? mu : m0, d.P, d.Q, n, p, q);
-      const float g = to_f(((const T*)t.a)[n * t.as[0] + p * t.as[2] + q * t.as[3]]);
-      const T* x = (const T*)t.b + n * t.bs[0] + l * VC;
+      const bool live = mu < Mi;
+      int n, h, w;
+      pix3(live ? mu : m0, d.H, d.W, n, h, w);
+      const T* px = (const T*)t.b + n * t.bs[0] + h * t.bs[2] + w * t.bs[3] + l * VC;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        if constexpr (VN == 8) {
+          ld8<T>(px + c * VN, &v[u][c * VN]);
+        } else {
+          const float4 q4 = *(const float4*)(px + c * VN);
+          v[u][c * 4 + 0] = q4.x; v[u][c * 4 + 1] = q4.y; v[u][c * 4 + 2] = q4.z; v[u][c * 4 + 3] = q4.w;
+        }
+      }
+      const T* dyn = (const T*)t.a + n * t.as[0];
 #pragma unroll
       for (int j = 0; j < RS; ++j) {
-        const int hu = p - d.pad + j / d.S, wu = q - d.pad + j % d.S;
-        const bool ok = live && hu >= 0 && hu < d.H && wu >= 0 && wu < d.W;
-        const T* px = x + (ok ? hu * t.bs[2] + wu * t.bs[3] : 0);   // clamped: loads issue together
-        gj[u][j] = ok ? g : 0.f;
-#pragma unroll
-        for (int c = 0; c < CH; ++c) {
-          if constexpr (VN == 8) {
-            ld8<T>(px + c * VN, &v[u][j][c * VN]);
-          } else {
-            const float4 w4 = *(const float4*)(px + c * VN);
-            v[u][j][c * 4 + 0] = w4.x; v[u][j][c * 4 + 1] = w4.y; v[u][j][c * 4 + 2] = w4.z; v[u][j][c * 4 + 3] = w4.w;
-          }
-        }
+        const int p = h + d.pad - j / d.S, q = w + d.pad - j % d.S;
+        const bool ok = live && (unsigned)p < (unsigned)d.P && (unsigned)q < (unsigned)d.Q;
+        const float gv = to_f(dyn[ok ? p * t.as[2] + q * t.as[3] : 0]);   // clamped: loads issue together
+        g[u][j] = ok ? gv : 0.f;
       }
     }
 #pragma unroll
@@ -476,7 +546,7 @@ __global__ void __launch_bounds__(NT) k1_wgrad(Thin t, int LP) {
 #pragma unroll
       for (int j = 0; j < RS; ++j)
 #pragma unroll
-        for (int e = 0; e < VC; ++e) acc[j][e] += gj[u][j] * v[u][j][e];
+        for (int e = 0; e < VC; ++e) acc[j][e] += g[u][j] * v[u][e];
   }
 #pragma unroll
   for (int j = 0; j < RS; ++j)
@@ -593,7 +663,10 @@ unsigned capped(unsigned b, int cap) { return cap > 0 ? std::min<unsigned>(b, (u
 // channel chunks per lane of the Cout == 1 kernels: 1 = one 16-byte chunk per lane (C / VN lanes per
 // pixel); 2 / 4 = fewer lanes per pixel, more loads in flight per lane, fewer shuffle rounds.  Measured
 // on conv_layers.13 at B = 1024 fp32 (us, CH = 1 / 2 / 4): fwd 241 / 226 / 414, dgrad 218 / 323 / 586,
-// wgrad 207 / 169 / 197 -> fwd 2, dgrad 1, wgrad 2
+// wgrad 207 / 169 / 197 (output-major kernels) -> fwd 2 (the output-major fallback), dgrad 1, wgrad 2.
+// The input-major kernels (round 5, conv_layers.13 at B = 1024, us fp32 / bf16): fwd 236 / 91 -> 156 / 82
+// (one workgroup per image, 4 pixels per trip); wgrad 170 / 159 -> 132 / 87 at CH = 2 with 2 pixels
+// per trip (CH = 1 with 4 pixels per trip: 171 / 106)
 constexpr int K1_CH = 2, K1_CH_DG = 1, K1_CH_WG = 2;
 // CH usable for C / VN chunks (LP = chunks / CH >= 1, a power of two)
 int k1_ch(int chunks, int want) {
@@ -615,6 +688,8 @@ void launch_fwd(const Thin& t, int rs, int LP, hipStream_t st) {
     const dim3 grid(blocks(t.M, NT / (d.K / (16 / (int)sizeof(TO)))));
     if (rs == 4) hipLaunchKernelGGL((c1_fwd<T, TO, 4>), grid, dim3(NT), 0, st, t);
     else hipLaunchKernelGGL((c1_fwd<T, TO, 9>), grid, dim3(NT), 0, st, t);
+  } else if (rs == 4 && rs * d.H * d.W <= K1_TP_FLOATS && pow2(LP) && LP <= 64) {
+    hipLaunchKernelGGL((k1_fwd_img<T, TO, 4>), dim3(d.N), dim3(NT), 0, st, t, LP);
   } else {
     const int ch = k1_ch(LP, K1_CH), lp = LP / ch;
     const dim3 grid(capped(blocks(t.M, NT / lp), K1_GRID));
@@ -659,8 +734,8 @@ void launch_wgrad(const Thin& t, int rs, int LP, hipStream_t st) {
     else hipLaunchKernelGGL((c1_wgrad<T, 9>), grid, dim3(NT), 0, st, t);
   } else {
     ES_K1_CH_DISPATCH(ch, {
-      if (rs == 4) hipLaunchKernelGGL((k1_wgrad<T, 4, CH>), grid, dim3(NT), 0, st, t, lp);
-      else hipLaunchKernelGGL((k1_wgrad<T, 9, CH>), grid, dim3(NT), 0, st, t, lp);
+      if (rs == 4) hipLaunchKernelGGL((k1_wgrad_in<T, 4, CH>), grid, dim3(NT), 0, st, t, lp);
+      else hipLaunchKernelGGL((k1_wgrad_in<T, 9, CH>), grid, dim3(NT), 0, st, t, lp);
     });
   }
 }
