@@ -371,37 +371,52 @@ __global__ void __launch_bounds__(NT) k1_dgrad_bnred(Thin t, int LP, ThinBnr b) 
   }
   __syncthreads();
   const float dsc = b.drop ? b.scale : 1.f;
-  for (int m = blockIdx.x * PPB + threadIdx.x / LP; m < t.M; m += gridDim.x * PPB) {
-    int n, h, w;
-    pix3(m, d.H, d.W, n, h, w);
-    const T* dy = (const T*)t.a + n * t.as[0];
-    const int64_t off = n * t.os[0] + h * t.os[2] + w * t.os[3] + l * 8;
-    float hv[8];
-    ld8<T>((const T*)b.x + off, hv);                          // issued before the tap loads' FMAs
-    const uint32_t kb = b.drop ? (uint32_t)b.keep[(int64_t)m * (d.C / 8) + l] : 0xFFu;
-    float acc[8];
+  // two pixels per trip (their h / keep / dy loads issue together; the bf16 form was latency-bound)
+  constexpr int U = 2;
+  const int stride = gridDim.x * PPB;
+  for (int m0 = blockIdx.x * PPB + threadIdx.x / LP; m0 < t.M; m0 += U * stride) {
+    float hv[U][8], acc[U][8];
+    uint32_t kb[U];
+    int64_t off[U];
+    bool lv[U];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    for (int u = 0; u < U; ++u) {
+      const int m = m0 + u * stride;
+      lv[u] = m < t.M;
+      const int mc = lv[u] ? m : m0;
+      int n, h, w;
+      pix3(mc, d.H, d.W, n, h, w);
+      const T* dy = (const T*)t.a + n * t.as[0];
+      off[u] = n * t.os[0] + h * t.os[2] + w * t.os[3] + l * 8;
+      ld8<T>((const T*)b.x + off[u], hv[u]);                  // issued before the tap loads' FMAs
+      kb[u] = b.drop ? (uint32_t)b.keep[(int64_t)mc * (d.C / 8) + l] : 0xFFu;
 #pragma unroll
-    for (int j = 0; j < RS; ++j) {
-      const int ph = h + d.pad - j / d.S, pw = w + d.pad - j % d.S;
-      const bool ok = ph >= 0 && pw >= 0 && ph < d.P && pw < d.Q;
-      const float gv = to_f(dy[ok ? ph * t.as[2] + pw * t.as[3] : 0]);
-      const float g = ok ? gv : 0.f;
-      const float* wr = wf + j * d.C + l * 8;
+      for (int e = 0; e < 8; ++e) acc[u][e] = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += g * wr[e];
+      for (int j = 0; j < RS; ++j) {
+        const int ph = h + d.pad - j / d.S, pw = w + d.pad - j % d.S;
+        const bool ok = ph >= 0 && pw >= 0 && ph < d.P && pw < d.Q;
+        const float gv = to_f(dy[ok ? ph * t.as[2] + pw * t.as[3] : 0]);
+        const float g = ok ? gv : 0.f;
+        const float* wr = wf + j * d.C + l * 8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[u][e] += g * wr[e];
+      }
     }
-    st8<T>((T*)t.out + off, acc);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float dv = std::is_same<T, bf16>::value ? (float)(bf16)acc[e] : acc[e], v = hv[e];   // the stored dx
-      const bool keep = (kb >> e) & 1u;
-      const float z = v * sc[e] + sh[e];
-      const float zs = b.drop && b.dfirst ? z * b.scale : z;
-      const float dn = keep ? dv * (zs > 0.f ? 1.f : b.slope) * dsc : 0.f;
-      s1[e] += dn;
-      s2[e] += dn * ((v - mu[e]) * is[e]);
+    for (int u = 0; u < U; ++u) {
+      if (!lv[u]) continue;
+      st8<T>((T*)t.out + off[u], acc[u]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float dv = std::is_same<T, bf16>::value ? (float)(bf16)acc[u][e] : acc[u][e], v = hv[u][e];   // the stored dx
+        const bool keep = (kb[u] >> e) & 1u;
+        const float z = v * sc[e] + sh[e];
+        const float zs = b.drop && b.dfirst ? z * b.scale : z;
+        const float dn = keep ? dv * (zs > 0.f ? 1.f : b.slope) * dsc : 0.f;
+        s1[e] += dn;
+        s2[e] += dn * ((v - mu[e]) * is[e]);
+      }
     }
   }
 #pragma unroll
