@@ -84,30 +84,43 @@ __global__ void __launch_bounds__(NT) c1_fwd(Thin t) {
   for (int i = threadIdx.x; i < d.K; i += NT) bs[i] = t.bias ? t.bias[i] : 0.f;
   __syncthreads();
   const int LP = d.K / VO, PPB = NT / LP;
-  const int m = blockIdx.x * PPB + threadIdx.x / LP, k0 = (threadIdx.x % LP) * VO;
-  if (m >= t.M) return;
-  int n, p, q;
-  pix3(m, d.P, d.Q, n, p, q);
-  const T* x = (const T*)t.a + n * t.as[0];
-  float xv[RS];
+  const int k0 = (threadIdx.x % LP) * VO;
+  // grid-stride over the pixels, two per trip (a block per 32 pixels spent its time staging the
+  // weights: 56 k blocks at B = 1024)
+  constexpr int U = 2;
+  const int stride = gridDim.x * PPB;
+  for (int m0 = blockIdx.x * PPB + threadIdx.x / LP; m0 < t.M; m0 += U * stride) {
+    float xv[U][RS];
+    int nn[U], pp[U], qq[U];
 #pragma unroll
-  for (int j = 0; j < RS; ++j) {
-    const int hu = p * d.stride - d.pad + j / d.S, wu = q * d.stride - d.pad + j % d.S;
-    const bool ok = hu >= 0 && hu < d.H && wu >= 0 && wu < d.W;
-    const float v = to_f(x[ok ? hu * t.as[2] + wu * t.as[3] : 0]);   // clamped: loads issue together
-    xv[j] = ok ? v : 0.f;
+    for (int u = 0; u < U; ++u) {
+      const int m = m0 + u * stride;
+      pix3(m < t.M ? m : m0, d.P, d.Q, nn[u], pp[u], qq[u]);
+      const T* x = (const T*)t.a + nn[u] * t.as[0];
+#pragma unroll
+      for (int j = 0; j < RS; ++j) {
+        const int hu = pp[u] * d.stride - d.pad + j / d.S, wu = qq[u] * d.stride - d.pad + j % d.S;
+        const bool ok = hu >= 0 && hu < d.H && wu >= 0 && wu < d.W;
+        const float v = to_f(x[ok ? hu * t.as[2] + wu * t.as[3] : 0]);   // clamped: loads issue together
+        xv[u][j] = ok ? v : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (m0 + u * stride >= t.M) break;
+      float o[8];
+#pragma unroll
+      for (int kk = 0; kk < VO; ++kk) {
+        float sacc = bs[k0 + kk];
+#pragma unroll
+        for (int j = 0; j < RS; ++j) sacc += xv[u][j] * wf[(k0 + kk) * RS + j];
+        o[kk] = sacc;
+      }
+      TO* y = (TO*)t.out + nn[u] * t.os[0] + pp[u] * t.os[2] + qq[u] * t.os[3] + k0;
+      if constexpr (VO == 8) st8<TO>(y, o);
+      else *(float4*)y = make_float4(o[0], o[1], o[2], o[3]);
+    }
   }
-  float o[8];
-#pragma unroll
-  for (int kk = 0; kk < VO; ++kk) {
-    float s = bs[k0 + kk];
-#pragma unroll
-    for (int j = 0; j < RS; ++j) s += xv[j] * wf[(k0 + kk) * RS + j];
-    o[kk] = s;
-  }
-  TO* y = (TO*)t.out + n * t.os[0] + p * t.os[2] + q * t.os[3] + k0;
-  if constexpr (VO == 8) st8<TO>(y, o);
-  else *(float4*)y = make_float4(o[0], o[1], o[2], o[3]);
 }
 
 // dgrad: LP = K / VN lanes per input pixel; lane l dots its 16-byte chunk of each tap's dy row
@@ -154,6 +167,77 @@ __global__ void __launch_bounds__(NT) c1_dgrad(Thin t) {
     TO* o = (TO*)t.out + n * t.os[0] + h * t.os[2] + w * t.os[3];
     if (t.beta != 0.f) acc += t.beta * to_f(*o);
     *o = from_f<TO>(acc);
+  }
+}
+
+// dgrad, workgroup per image: each dy pixel is read once; its RS partial dots t_j = <dy, w[:, j]>
+// (reduced over the LP lanes of the pixel) go to LDS, then dx(h, w) = sum_j t_j(h + pad - r_j, w + pad - s_j)
+// (stride 1).  The pixel-major kernel above re-read every dy row once per tap (9x).
+constexpr int C1_TP_FLOATS = 16384;   // LDS floats of the per-tap partial dots (RS * P * Q)
+template <typename T, typename TO, int RS>
+__global__ void __launch_bounds__(NT) c1_dgrad_img(Thin t) {
+  constexpr int VN = V16<T>::N;
+  const es_conv_desc_t& d = t.d;
+  const int n = blockIdx.x;
+  if (n >= live_rows(d.rows, d.N)) return;   // dynamic rows: a padding image
+  __shared__ float wf[64 * RS];              // [k][rs] (dgrad packing [C = 1][R][S][K] read as [rs][k])
+  __shared__ float tp[C1_TP_FLOATS];         // [RS][P * Q]
+  for (int i = threadIdx.x; i < d.K * RS; i += NT) {
+    const int j = i / d.K, k = i - j * d.K;
+    wf[k * RS + j] = to_f(((const T*)t.w)[i]);
+  }
+  __syncthreads();
+  const int PQ = d.P * d.Q, LP = d.K / VN, PPB = NT / LP, l = threadIdx.x % LP;
+  const T* dyn = (const T*)t.a + n * t.as[0] + l * VN;
+  constexpr int U = 2;
+  for (int m0 = 0; m0 < PQ; m0 += U * PPB) {
+    float v[U][VN];
+    int mm[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int m = m0 + u * PPB + threadIdx.x / LP;
+      mm[u] = m;
+      const int mc = m < PQ ? m : 0;
+      const int p = mc / d.Q, q = mc - p * d.Q;
+      const T* px = dyn + p * t.as[2] + q * t.as[3];
+      if constexpr (VN == 8) {
+        ld8<T>(px, v[u]);
+      } else {
+        const float4 q4 = *(const float4*)px;
+        v[u][0] = q4.x; v[u][1] = q4.y; v[u][2] = q4.z; v[u][3] = q4.w;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float sj[RS];
+#pragma unroll
+      for (int j = 0; j < RS; ++j) {
+        float a = 0.f;
+#pragma unroll
+        for (int e = 0; e < VN; ++e) a += v[u][e] * wf[(l * VN + e) * RS + j];
+        sj[j] = a;
+      }
+      for (int o = LP >> 1; o > 0; o >>= 1)
+#pragma unroll
+        for (int j = 0; j < RS; ++j) sj[j] += __shfl_xor(sj[j], o, 64);
+      if (l == 0 && mm[u] < PQ)
+#pragma unroll
+        for (int j = 0; j < RS; ++j) tp[j * PQ + mm[u]] = sj[j];
+    }
+  }
+  __syncthreads();
+  TO* xo = (TO*)t.out + n * t.os[0];
+  for (int o = threadIdx.x; o < d.H * d.W; o += NT) {
+    const int h = o / d.W, w = o - h * d.W;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < RS; ++j) {
+      const int ph = h + d.pad - j / d.S, pw = w + d.pad - j % d.S;
+      if ((unsigned)ph < (unsigned)d.P && (unsigned)pw < (unsigned)d.Q) acc += tp[j * PQ + ph * d.Q + pw];
+    }
+    TO* dst = xo + h * t.os[2] + w * t.os[3];
+    if (t.beta != 0.f) acc += t.beta * to_f(*dst);
+    *dst = from_f<TO>(acc);
   }
 }
 
@@ -672,7 +756,7 @@ bool k1_ok(const es_conv_desc_t* d, int rs, int vn) {
 
 unsigned blocks(int64_t items, int per) { return (unsigned)((items + per - 1) / per); }
 // grid caps of the grid-stride thin kernels (re-measured round 4, kept)
-constexpr int K1_GRID = 2048, THIN_WGRID = 1024;
+constexpr int K1_GRID = 2048, THIN_WGRID = 1024, C1_GRID = 2048;
 unsigned capped(unsigned b, int cap) { return cap > 0 ? std::min<unsigned>(b, (unsigned)cap) : b; }
 
 // channel chunks per lane of the Cout == 1 kernels: 1 = one 16-byte chunk per lane (C / VN lanes per
@@ -700,7 +784,7 @@ template <typename T, typename TO>
 void launch_fwd(const Thin& t, int rs, int LP, hipStream_t st) {
   const es_conv_desc_t& d = t.d;
   if (d.C == 1) {
-    const dim3 grid(blocks(t.M, NT / (d.K / (16 / (int)sizeof(TO)))));
+    const dim3 grid(capped(blocks(t.M, NT / (d.K / (16 / (int)sizeof(TO)))), C1_GRID));
     if (rs == 4) hipLaunchKernelGGL((c1_fwd<T, TO, 4>), grid, dim3(NT), 0, st, t);
     else hipLaunchKernelGGL((c1_fwd<T, TO, 9>), grid, dim3(NT), 0, st, t);
   } else if (rs == 4 && rs * d.H * d.W <= K1_TP_FLOATS && pow2(LP) && LP <= 64) {
@@ -718,7 +802,10 @@ void launch_fwd(const Thin& t, int rs, int LP, hipStream_t st) {
 template <typename T, typename TO>
 void launch_dgrad(const Thin& t, int rs, int LP, hipStream_t st) {
   const es_conv_desc_t& d = t.d;
-  if (d.C == 1) {
+  if (d.C == 1 && d.stride == 1 && rs * d.P * d.Q <= C1_TP_FLOATS) {
+    if (rs == 4) hipLaunchKernelGGL((c1_dgrad_img<T, TO, 4>), dim3(d.N), dim3(NT), 0, st, t);
+    else hipLaunchKernelGGL((c1_dgrad_img<T, TO, 9>), dim3(d.N), dim3(NT), 0, st, t);
+  } else if (d.C == 1) {
     const dim3 grid(blocks(t.M, NT / (d.K / V16<T>::N)));
     if (rs == 4) hipLaunchKernelGGL((c1_dgrad<T, TO, 4>), grid, dim3(NT), 0, st, t);
     else hipLaunchKernelGGL((c1_dgrad<T, TO, 9>), grid, dim3(NT), 0, st, t);
