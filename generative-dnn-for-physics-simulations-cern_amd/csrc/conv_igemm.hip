@@ -26,6 +26,7 @@
 #include <cstdlib>
 
 #include "conv_common.h"
+#include "split_fp32.h"
 
 // direct kernels for one-input-channel / one-output-channel convolutions (conv_thin.hip)
 int es_thin_conv_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x, const int64_t xs[4], const void* wk,
@@ -356,11 +357,32 @@ struct Stager {
 // ---------------------------------------------------------------------------------------------
 // MFMA micro-kernel on one K-step held in LDS
 // ---------------------------------------------------------------------------------------------
-template <typename T, int RM, int RN>
+template <typename T, int RM, int RN, bool SPL = false>
 __device__ __forceinline__ void mma_kstep(const char* As, const char* Bs, int wm0, int wn0,
                                           f32x4 (&acc)[RM][RN]) {
   const int lane = threadIdx.x & 63;
   const int r16 = lane & 15, g = lane >> 4;
+  if constexpr (sizeof(T) == 4 && SPL) {
+    // split-fp32 (split_fp32.h): a lane's 16-byte chunks g and g + 4 of its row are the same 8 k of
+    // the K-step's 32 as the exact path's two chunk reads; split into three bf16 planes, one
+    // v_mfma_f32_16x16x32_bf16 K-step (6 plane products) per tile
+    bf16x8 ap[RM][3], bp[RN][3];
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      const char* r = As + (wm0 + i * 16 + r16) * ROW_BYTES;
+      split8(*(const f32x4*)(r + g * 16), *(const f32x4*)(r + (g + 4) * 16), ap[i]);
+    }
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const char* r = Bs + (wn0 + j * 16 + r16) * ROW_BYTES;
+      split8(*(const f32x4*)(r + g * 16), *(const f32x4*)(r + (g + 4) * 16), bp[j]);
+    }
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) acc[i][j] = mfma_split6(ap[i], bp[j], acc[i][j]);
+    return;
+  }
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
     const int seg = kk * 4 + g;
@@ -493,7 +515,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const f32x4 (&a
   }
 }
 
-template <typename T, int MODE, int BM, int BN, bool AVEC, bool BVEC>
+template <typename T, int MODE, int BM, int BN, bool AVEC, bool BVEC, bool SPL = false>
 __global__ void __launch_bounds__(NTHREADS) conv_igemm_kernel(ConvArgs a) {
   constexpr int BK = KSTEP_BYTES / sizeof(T);
   constexpr int RM = BM / 32, RN = BN / 32;   // 16x16 tiles per wave (2x2 wave grid)
@@ -535,7 +557,7 @@ __global__ void __launch_bounds__(NTHREADS) conv_igemm_kernel(ConvArgs a) {
     if constexpr (LA::TR)
       mma_kstep_tr<RM, RN, BM, BN>(smem + cur * BUF, smem + cur * BUF + LA::BYTES, wm0, wn0, acc);
     else
-      mma_kstep<T, RM, RN>(smem + cur * BUF, smem + cur * BUF + LA::BYTES, wm0, wn0, acc);
+      mma_kstep<T, RM, RN, SPL>(smem + cur * BUF, smem + cur * BUF + LA::BYTES, wm0, wn0, acc);
     if (more) {
       sa.store(smem + (cur ^ 1) * BUF);
       sb.store(smem + (cur ^ 1) * BUF + LA::BYTES);
@@ -727,14 +749,22 @@ template <typename T, int MODE, int BM, int BN>
 int launch_tile(const ConvArgs& a, bool avec, bool bvec, hipStream_t st, int splits) {
   dim3 grid((a.M + BM - 1) / BM, (a.Ng + BN - 1) / BN, splits);
   const size_t lds = 2 * (LdsImg<T, MODE, BM>::BYTES + LdsImg<T, MODE, BN>::BYTES);
-#define ES_LAUNCH(AV, BV)                                                                     \
-  hipLaunchKernelGGL((conv_igemm_kernel<T, MODE, BM, BN, AV, BV>), grid, dim3(NTHREADS), lds, \
-                     st, a)
+  // fp32 operands in the split-fp32 mode (es_conv_set_f32_split): the six bf16 plane products per
+  // K-step instead of eight exact v_mfma_f32_16x16x4_f32 (the linears, the aux regressor's 32-channel
+  // conv2 weight gradient and the other shapes the ring kernels do not take)
+  const bool spl = sizeof(T) == 4 && g_f32_split != 0;
+#define ES_LAUNCH(AV, BV)                                                                                     \
+  do {                                                                                                      \
+    if (spl) hipLaunchKernelGGL((conv_igemm_kernel<T, MODE, BM, BN, AV, BV, sizeof(T) == 4>), grid,          \
+                                dim3(NTHREADS), lds, st, a);                                                \
+    else hipLaunchKernelGGL((conv_igemm_kernel<T, MODE, BM, BN, AV, BV>), grid, dim3(NTHREADS), lds, st, a); \
+  } while (0)
   if (avec && bvec) ES_LAUNCH(true, true);
   else if (avec) ES_LAUNCH(true, false);
   else if (bvec) ES_LAUNCH(false, true);
   else ES_LAUNCH(false, false);
 #undef ES_LAUNCH
+  if (spl) g_ring_hit |= 2;   // (executed-work tally: the bf16 pipe, 6 products)
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
