@@ -144,8 +144,6 @@ extern thread_local StatsRequest g_stats_req;
 // which ring path the last conv launch took (host, per thread; es_conv_exec_flops accounting):
 // bit 0 a ring kernel ran, bit 1 split-fp32 planes, bit 2 the sub-pixel decomposition
 extern thread_local int g_ring_hit;
-// the fp32 mode's MFMA arithmetic (es_conv_set_f32_split): 0 exact fp32, 1 / 2 split-fp32 (conv_mfma.hip)
-extern int g_f32_split;
 
 // split-fp32 weight planes: byte offset of the planes behind an fp32 packing of n elements
 extern "C" int64_t es_weight_planes_offset(int64_t n);

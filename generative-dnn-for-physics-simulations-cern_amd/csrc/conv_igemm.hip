@@ -26,7 +26,6 @@
 #include <cstdlib>
 
 #include "conv_common.h"
-#include "split_fp32.h"
 
 // direct kernels for one-input-channel / one-output-channel convolutions (conv_thin.hip)
 int es_thin_conv_fwd(const es_conv_desc_t* d, es_dtype_t dt, const void* x, const int64_t xs[4], const void* wk,
@@ -357,32 +356,11 @@ struct Stager {
 // ---------------------------------------------------------------------------------------------
 // MFMA micro-kernel on one K-step held in LDS
 // ---------------------------------------------------------------------------------------------
-template <typename T, int RM, int RN, bool SPL = false>
+template <typename T, int RM, int RN>
 __device__ __forceinline__ void mma_kstep(const char* As, const char* Bs, int wm0, int wn0,
                                           f32x4 (&acc)[RM][RN]) {
   const int lane = threadIdx.x & 63;
   const int r16 = lane & 15, g = lane >> 4;
-  if constexpr (sizeof(T) == 4 && SPL) {
-    // split-fp32 (split_fp32.h): a lane's 16-byte chunks g and g + 4 of its row are the same 8 k of
-    // the K-step's 32 as the exact path's two chunk reads; split into three bf16 planes, one
-    // v_mfma_f32_16x16x32_bf16 K-step (6 plane products) per tile
-    bf16x8 ap[RM][3], bp[RN][3];
-#pragma unroll
-    for (int i = 0; i < RM; ++i) {
-      const char* r = As + (wm0 + i * 16 + r16) * ROW_BYTES;
-      split8(*(const f32x4*)(r + g * 16), *(const f32x4*)(r + (g + 4) * 16), ap[i]);
-    }
-#pragma unroll
-    for (int j = 0; j < RN; ++j) {
-      const char* r = Bs + (wn0 + j * 16 + r16) * ROW_BYTES;
-      split8(*(const f32x4*)(r + g * 16), *(const f32x4*)(r + (g + 4) * 16), bp[j]);
-    }
-#pragma unroll
-    for (int i = 0; i < RM; ++i)
-#pragma unroll
-      for (int j = 0; j < RN; ++j) acc[i][j] = mfma_split6(ap[i], bp[j], acc[i][j]);
-    return;
-  }
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
     const int seg = kk * 4 + g;
@@ -515,7 +493,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const f32x4 (&a
   }
 }
 
-template <typename T, int MODE, int BM, int BN, bool AVEC, bool BVEC, bool SPL = false>
+template <typename T, int MODE, int BM, int BN, bool AVEC, bool BVEC>
 __global__ void __launch_bounds__(NTHREADS) conv_igemm_kernel(ConvArgs a) {
   constexpr int BK = KSTEP_BYTES / sizeof(T);
   constexpr int RM = BM / 32, RN = BN / 32;   // 16x16 tiles per wave (2x2 wave grid)
@@ -557,7 +535,7 @@ __global__ void __launch_bounds__(NTHREADS) conv_igemm_kernel(ConvArgs a) {
     if constexpr (LA::TR)
       mma_kstep_tr<RM, RN, BM, BN>(smem + cur * BUF, smem + cur * BUF + LA::BYTES, wm0, wn0, acc);
     else
-      mma_kstep<T, RM, RN, SPL>(smem + cur * BUF, smem + cur * BUF + LA::BYTES, wm0, wn0, acc);
+      mma_kstep<T, RM, RN>(smem + cur * BUF, smem + cur * BUF + LA::BYTES, wm0, wn0, acc);
     if (more) {
       sa.store(smem + (cur ^ 1) * BUF);
       sb.store(smem + (cur ^ 1) * BUF + LA::BYTES);
@@ -749,22 +727,14 @@ template <typename T, int MODE, int BM, int BN>
 int launch_tile(const ConvArgs& a, bool avec, bool bvec, hipStream_t st, int splits) {
   dim3 grid((a.M + BM - 1) / BM, (a.Ng + BN - 1) / BN, splits);
   const size_t lds = 2 * (LdsImg<T, MODE, BM>::BYTES + LdsImg<T, MODE, BN>::BYTES);
-  // fp32 operands in the split-fp32 mode (es_conv_set_f32_split): the six bf16 plane products per
-  // K-step instead of eight exact v_mfma_f32_16x16x4_f32 (the linears, the aux regressor's 32-channel
-  // conv2 weight gradient and the other shapes the ring kernels do not take)
-  const bool spl = sizeof(T) == 4 && g_f32_split != 0;
-#define ES_LAUNCH(AV, BV)                                                                                     \
-  do {                                                                                                      \
-    if (spl) hipLaunchKernelGGL((conv_igemm_kernel<T, MODE, BM, BN, AV, BV, sizeof(T) == 4>), grid,          \
-                                dim3(NTHREADS), lds, st, a);                                                \
-    else hipLaunchKernelGGL((conv_igemm_kernel<T, MODE, BM, BN, AV, BV>), grid, dim3(NTHREADS), lds, st, a); \
-  } while (0)
+#define ES_LAUNCH(AV, BV)                                                                     \
+  hipLaunchKernelGGL((conv_igemm_kernel<T, MODE, BM, BN, AV, BV>), grid, dim3(NTHREADS), lds, \
+                     st, a)
   if (avec && bvec) ES_LAUNCH(true, true);
   else if (avec) ES_LAUNCH(true, false);
   else if (bvec) ES_LAUNCH(false, true);
   else ES_LAUNCH(false, false);
 #undef ES_LAUNCH
-  if (spl) g_ring_hit |= 2;   // (executed-work tally: the bf16 pipe, 6 products)
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
@@ -1347,6 +1317,7 @@ __device__ __forceinline__ float subpixel_weight(const float* __restrict__ w, in
 }
 
 // taps of class t: dh = ((a + R - 1) >> 1) + 1, dw likewise
+__host__ __device__ __forceinline__ int64_t es_weight_planes_offset_d(int64_t n) { return (n * 4 + 255) / 256 * 256; }
 __device__ __forceinline__ int sp_dh(int t, int R) { return (((t >> 1) + R - 1) >> 1) + 1; }
 __device__ __forceinline__ int sp_dw(int t, int S) { return (((t & 1) + S - 1) >> 1) + 1; }
 
@@ -1521,6 +1492,124 @@ __global__ void pack_planes_kernel(const float* __restrict__ w, int64_t nblk, bf
 }
 
 extern "C" int64_t es_weight_planes_offset(int64_t n) { return (n * 4 + 255) / 256 * 256; }
+
+namespace {
+// Batched packing (es_pack_conv_weights): blockIdx.y = job; each thread computes packed element i
+// with the element-wise kernels' index math and writes it in the job's dtype, and for split-fp32
+// jobs also its three bf16 plane values (the inverse of pack_planes_kernel's k permutation: block
+// position p -> plane slot 8 (p / 4) + p % 4 for p < 16, 8 ((p - 16) / 4) + 4 + p % 4 otherwise).
+constexpr int PACK_MAXJ = 32;
+struct PackJobs {
+  es_pack_job_t j[PACK_MAXJ];
+};
+__global__ void __launch_bounds__(256) pack_batch_kernel(PackJobs jobs) {
+  const es_pack_job_t& jb = jobs.j[blockIdx.y];
+  const int K = jb.K, C = jb.C, R = jb.R, S = jb.S, mode = jb.mode;
+  int tap0[5] = {0, 0, 0, 0, 0};
+  int64_t n;
+  if (mode >= 2) {
+    for (int t = 0; t < 4; ++t) tap0[t + 1] = tap0[t] + sp_dh(t, R) * sp_dw(t, S);
+    n = (int64_t)K * C * tap0[4];
+  } else {
+    n = (int64_t)K * C * R * S;
+  }
+  const int64_t nplan = jb.planes ? (n / 32) * 32 : 0;
+  bf16* planes = (bf16*)((char*)jb.out + es_weight_planes_offset_d(n));
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float v;
+    if (mode >= 2) {
+      int k, c, tap;
+      if (mode == 2) {
+        const int64_t kc = (int64_t)K * C;
+        const int t = (i >= tap0[1] * kc) + (i >= tap0[2] * kc) + (i >= tap0[3] * kc);
+        const int64_t rem = i - tap0[t] * kc;
+        const int nde = sp_dh(t, R) * sp_dw(t, S);
+        k = (int)(rem / ((int64_t)nde * C));
+        const int r2 = (int)(rem - (int64_t)k * nde * C);
+        const int de = r2 / C;
+        c = r2 - de * C;
+        tap = tap0[t] + de;
+      } else {
+        const int taps = tap0[4];
+        c = (int)(i / ((int64_t)taps * K));
+        const int r2 = (int)(i - (int64_t)c * taps * K);
+        tap = r2 / K;
+        k = r2 - tap * K;
+      }
+      const int t = (tap >= tap0[1]) + (tap >= tap0[2]) + (tap >= tap0[3]);
+      const int de = tap - tap0[t], dw = sp_dw(t, S);
+      const int dd = de / dw, ee = de - dd * dw;
+      v = subpixel_weight(jb.w, k, c, C, R, S, t, dd, ee);
+    } else {
+      int k, c, r, s_;
+      const uint32_t i32 = (uint32_t)i;
+      if (mode == 0) {
+        uint32_t t = i32 / C; c = i32 - t * C; s_ = t % S; t /= S; r = t % R; k = t / R;
+      } else {
+        uint32_t t = i32 / K; k = i32 - t * K; s_ = t % S; t /= S; r = t % R; c = t / R;
+      }
+      v = jb.w[(((int64_t)k * C + c) * R + r) * S + s_];
+    }
+    if (jb.dt == ES_BF16) {
+      ((bf16*)jb.out)[i] = (bf16)v;
+    } else {
+      ((float*)jb.out)[i] = v;
+      if (i < nplan) {
+        const int p = (int)(i & 31);
+        const int q = p < 16 ? 8 * (p >> 2) + (p & 3) : 8 * ((p - 16) >> 2) + 4 + (p & 3);
+        const bf16 h = (bf16)v;
+        const float rr = v - (float)h;
+        const bf16 m = (bf16)rr;
+        const bf16 l = (bf16)(rr - (float)m);
+        bf16* o = planes + (i >> 5) * 96 + q;
+        o[0] = h;
+        o[32] = m;
+        o[64] = l;
+      }
+    }
+  }
+}
+}  // namespace
+
+extern "C" int es_pack_conv_weights(const es_pack_job_t* jobs, int n, es_stream_t stream) {
+  ES_CHECK_ARG(n >= 0 && (n == 0 || jobs != nullptr), "pack batch: bad job list");
+  hipStream_t st = (hipStream_t)stream;
+  PackJobs batch{};
+  int nb = 0;
+  int64_t maxn = 0;
+  auto flush = [&]() -> int {
+    if (nb == 0) return ES_OK;
+    const int blocks = (int)std::min<int64_t>((maxn + 255) / 256, 512);
+    hipLaunchKernelGGL(pack_batch_kernel, dim3(blocks, nb), dim3(256), 0, st, batch);
+    ES_CHECK_LAUNCH();
+    nb = 0;
+    maxn = 0;
+    return ES_OK;
+  };
+  for (int q = 0; q < n; ++q) {
+    const es_pack_job_t& jb = jobs[q];
+    ES_CHECK_ARG(jb.w && jb.out && jb.mode >= 0 && jb.mode <= 3 && jb.K > 0 && jb.C > 0 && jb.R > 0 && jb.S > 0,
+                 "pack batch: bad job %d", q);
+    ES_CHECK_ARG(jb.dt == ES_F32 || jb.dt == ES_BF16, "pack batch: job %d dtype", q);
+    ES_CHECK_ARG(!jb.planes || jb.dt == ES_F32, "pack batch: planes need an fp32 packing (job %d)", q);
+    const int64_t ne = (int64_t)jb.K * jb.C * (jb.mode >= 2 ? es_subpixel_taps(jb.R, jb.S) : jb.R * jb.S);
+    ES_CHECK_ARG(ne < (1ll << 31), "pack batch: weight too large (job %d)", q);
+    if (jb.mode == 1 && (int64_t)jb.C * jb.R * jb.S >= 4096) {
+      // a large transpose (the wide linears): the LDS-tiled kernel, then its planes
+      if (int rc = es_pack_conv_weight(jb.w, jb.K, jb.C, jb.R, jb.S, 1, nullptr, nullptr, jb.out, (es_dtype_t)jb.dt,
+                                       stream))
+        return rc;
+      if (jb.planes)
+        if (int rc = es_pack_weight_planes((const float*)jb.out, ne, jb.out, stream)) return rc;
+      continue;
+    }
+    batch.j[nb++] = jb;
+    maxn = std::max(maxn, ne);
+    if (nb == PACK_MAXJ)
+      if (int rc = flush()) return rc;
+  }
+  return flush();
+}
 
 extern "C" int es_pack_weight_planes(const float* packed, int64_t n, void* base, es_stream_t stream) {
   const int64_t nblk = n / 32;

@@ -3137,15 +3137,14 @@ int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
 // (conv_layers.5's output gradient at B = 1024 is 1.1 GB) run as launches over image chunks on
 // offset base pointers (chunks of whole 64-image groups).
 // ---------------------------------------------------------------------------------------------
-// fp32 MFMA arithmetic of the ring kernels and the generic fp32 GEMMs (conv_igemm.hip): 0 = exact fp32
-// (v_mfma_f32_16x16x4_f32), 1 = split-fp32 (three bf16 planes, 6 products on v_mfma_f32_16x16x32_bf16);
-// es_conv_set_f32_split / ES_F32_SPLIT
-int g_f32_split = 0;
 namespace {
 int g_f32_chunk = 0;   // test knob (es_conv_set_f32_chunk): at most this many images per fp32 launch
+// fp32 MFMA arithmetic of the ring kernels: 0 = exact fp32 (v_mfma_f32_16x16x4_f32), 1 = split-fp32
+// (three bf16 planes, 6 products on v_mfma_f32_16x16x32_bf16); es_conv_set_f32_split / ES_F32_SPLIT
 // (Plain functions, not lambdas: hipcc numbers the namespace-scope lambdas of a second anonymous
 // namespace block from #1 again, and the duplicate symbols resolved to the first block's lambdas, so
 // these globals were initialised by other variables' initialisers.)
+int g_f32_split = 0;
 // split-fp32 kernels: static s_setprio 1 for waves 4-7 (measured against 0: equal within noise, kept)
 constexpr int SPL_PRIO = 1;
 // images per launch: equal chunks (whole 64-image groups where the limit allows) below the limit

@@ -1097,6 +1097,7 @@ extern "C" int64_t es_struct_size(int which) {
     case 5: return sizeof(es_gen_loss_t);
     case 6: return sizeof(es_dfront2_params_t);
     case 7: return sizeof(es_dmlp_params_t);
+    case 8: return sizeof(es_pack_job_t);
     default: return -1;
   }
 }

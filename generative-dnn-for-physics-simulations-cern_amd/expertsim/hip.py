@@ -72,6 +72,11 @@ class DMlpParams(C.Structure):
                 ("rows", C.c_void_p)]
 
 
+class PackJob(C.Structure):
+    _fields_ = [("w", C.c_void_p), ("K", C.c_int), ("C", C.c_int), ("R", C.c_int), ("S", C.c_int),
+                ("mode", C.c_int), ("dt", C.c_int), ("planes", C.c_int), ("out", C.c_void_p)]
+
+
 P = C.c_void_p
 I64 = C.c_int64
 _SIGS = {
@@ -101,6 +106,7 @@ _SIGS = {
     "es_conv_set_f32_split": (C.c_int, [C.c_int]),
     "es_weight_planes_offset": (C.c_int64, [C.c_int64]),
     "es_pack_weight_planes": (C.c_int, [P, C.c_int64, P, P]),
+    "es_pack_conv_weights": (C.c_int, [P, C.c_int, P]),
     "es_conv_launch_count": (C.c_int64, []),
     "es_conv_exec_flops": (C.c_int, [C.POINTER(C.c_double), C.c_int]),
     "es_pack_conv_weight": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, C.c_int, P]),
@@ -193,7 +199,7 @@ def lib_path() -> str:
     return _LIB_PATH
 
 
-_ABI_STRUCTS = (View, Dropout, ConvDesc, Norm, Chain, GenLoss, DFront2Params, DMlpParams)
+_ABI_STRUCTS = (View, Dropout, ConvDesc, Norm, Chain, GenLoss, DFront2Params, DMlpParams, PackJob)
 
 
 def lib():

@@ -165,6 +165,23 @@ def _exec_tally():
     return list(out)
 
 
+def repack_ops(ops):
+    """After a weight update: rebuild every cached weight packing of these ConvOps in place with one
+    batched launch per 32 packings (es_pack_conv_weights) instead of one or two launches per layout
+    at the next use; ops without a packing yet pack lazily as before.  Ops sharing a packing dict
+    (a resized conv and its plain op) are packed once."""
+    jobs, seen = [], set()
+    for op in ops:
+        pk = getattr(op, "_packed", None)
+        if not pk or id(pk) in seen or not hasattr(op, "repack_jobs"):
+            continue
+        seen.add(id(pk))
+        jobs += op.repack_jobs()
+    if jobs:
+        arr = (hip.PackJob * len(jobs))(*jobs)
+        hip.call("es_pack_conv_weights", arr, len(jobs), hip.stream_ptr())
+
+
 def copy_act(src: Act, dst: Act, alpha=1.0, beta=0.0):
     hip.call("es_copy", C.byref(src.view), src.dt, src.ptr, C.byref(dst.view), dst.dt, dst.ptr,
              float(alpha), float(beta), hip.stream_ptr())
@@ -306,6 +323,17 @@ class ConvOp:
 
     def invalidate(self):
         self._packed.clear()
+
+    def repack_jobs(self):
+        """The es_pack_conv_weights jobs that rebuild this op's cached packings in place (the
+        weights changed, the layouts and buffers did not)."""
+        jobs = []
+        for (dtype, mode, planes), out in self._packed.items():
+            j = hip.PackJob()
+            j.w, j.K, j.C, j.R, j.S, j.mode = self.weight.data_ptr(), self.K, self.C, self.R, self.S, mode
+            j.dt, j.planes, j.out = hip.dt_of(out), int(planes), out.data_ptr()
+            jobs.append(j)
+        return jobs
 
     def _resized(self, x: Act) -> bool:
         """Materialise the resize for this call: dense NHWC input with 16-byte channel chunks."""

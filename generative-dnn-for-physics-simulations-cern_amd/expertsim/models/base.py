@@ -120,11 +120,12 @@ class ExpertModule(nn.Module):
         return self._ops
 
     def invalidate(self):
-        """Called after every optimizer step: packed GEMM weights must be rebuilt."""
+        """Called after every optimizer step: packed GEMM weights must be rebuilt.  The packings
+        already made are rebuilt in place right here, batched (layers.repack_ops: one launch for the
+        module instead of one or two per layout at its next use)."""
         if self._ops is not None:
-            for op in self._ops.values():
-                if hasattr(op, "invalidate"):
-                    op.invalidate()
+            from ..layers import repack_ops
+            repack_ops(self._ops.values())
 
     def _apply(self, fn, *args, **kwargs):
         out = super()._apply(fn, *args, **kwargs)

@@ -224,6 +224,20 @@ int es_conv_exec_flops(double out[3], int reset);
 int es_pack_conv_weight(const float* w, int K, int C, int R, int S, int mode,
                         const float* inv_scale, const int32_t* col_perm, void* out, es_dtype_t dt,
                         es_stream_t stream);
+/* One weight packing of es_pack_conv_weight (scale 1, no column permutation), with the split-fp32
+ * planes behind it when planes != 0 (es_pack_weight_planes); out is the packing's buffer. */
+typedef struct {
+  const float* w;
+  int K, C, R, S, mode;
+  int dt;     /* es_dtype_t of the packing */
+  int planes; /* fp32 only: also write the bf16 planes at out + es_weight_planes_offset(n) */
+  void* out;
+} es_pack_job_t;
+/* The packings of every layer of a module rebuilt after a weight update (MoE optimizer steps) in one
+ * launch per 32 jobs instead of one or two per layout (jobs: host array).  Same values as
+ * es_pack_conv_weight + es_pack_weight_planes per job; the large mode-1 transposes keep their
+ * LDS-tiled kernel. */
+int es_pack_conv_weights(const es_pack_job_t* jobs, int n, es_stream_t stream);
 /* grad[k][c][r][s] = beta*grad + dw[k][r][s][c] * (inv_scale ? 1/inv_scale[0] : 1) */
 int es_unpack_conv_grad(const float* dw, int K, int C, int R, int S, const int32_t* col_perm,
                         float* grad, float beta, es_stream_t stream);
