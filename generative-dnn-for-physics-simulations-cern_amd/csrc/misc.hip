@@ -1054,6 +1054,34 @@ extern "C" int es_counter_add_if(int32_t* counter, int32_t v, const int32_t* fla
   ES_CHECK_LAUNCH();
   return ES_OK;
 }
+namespace {
+constexpr int NBT_MAX = 64;
+struct CounterJobs {
+  int64_t* c[NBT_MAX];
+  int64_t v[NBT_MAX];
+};
+__global__ void counters_add_i64_kernel(CounterJobs j, int n, const int32_t* flag) {
+  if (flag && flag[0] == 0) return;
+  const int i = threadIdx.x;
+  if (i < n) j.c[i][0] += j.v[i];
+}
+}  // namespace
+extern "C" int es_counters_add_i64_if(int64_t* const* counters, const int64_t* v, int n, const int32_t* flag,
+                                      es_stream_t stream) {
+  ES_CHECK_ARG(n >= 0 && (n == 0 || (counters && v)), "counters_add: bad arguments");
+  for (int b = 0; b < n; b += NBT_MAX) {
+    CounterJobs j{};
+    const int m = n - b < NBT_MAX ? n - b : NBT_MAX;
+    for (int i = 0; i < m; ++i) {
+      ES_CHECK_ARG(counters[b + i] != nullptr, "counters_add: null counter %d", b + i);
+      j.c[i] = counters[b + i];
+      j.v[i] = v[b + i];
+    }
+    hipLaunchKernelGGL(counters_add_i64_kernel, dim3(1), dim3(NBT_MAX), 0, (hipStream_t)stream, j, m, flag);
+    ES_CHECK_LAUNCH();
+  }
+  return ES_OK;
+}
 extern "C" int es_counter_add_i64_if(int64_t* counter, int64_t v, const int32_t* flag, es_stream_t stream) {
   hipLaunchKernelGGL(counter_add_i64_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, counter, v, flag);
   ES_CHECK_LAUNCH();

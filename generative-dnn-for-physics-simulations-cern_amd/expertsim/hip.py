@@ -184,6 +184,7 @@ _SIGS = {
     "es_randn_dev_at": (C.c_int, [P, I64, C.c_uint64, C.c_uint32, P, C.c_int32, I64, P, I64, P]),
     "es_counter_add_if": (C.c_int, [P, C.c_int32, P, P]),
     "es_counter_add_i64_if": (C.c_int, [P, I64, P, P]),
+    "es_counters_add_i64_if": (C.c_int, [P, P, C.c_int, P, P]),
     "es_expert_plan": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P, P, P]),
     "es_div_by": (C.c_int, [P, C.c_int, P, P]),
     "es_struct_size": (I64, [C.c_int]),

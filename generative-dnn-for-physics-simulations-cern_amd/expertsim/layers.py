@@ -641,10 +641,39 @@ def count_batches(nbt, k):
         _count_batch(nbt)
 
 
+# dynamic rows: the counts of one expert program, applied on the device in one launch at its end
+_LIVE_NBT = None
+
+
+class batch_live_counts:
+    """Inside an expert program on dynamic rows: collect the BatchNorm batch counts and add them on
+    the device in one launch when the program ends (es_counters_add_i64_if, gated on the expert's
+    active flag) instead of one launch per train-mode BatchNorm forward."""
+
+    def __enter__(self):
+        global _LIVE_NBT
+        self.prev, _LIVE_NBT = _LIVE_NBT, {}
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        global _LIVE_NBT
+        pending, _LIVE_NBT = _LIVE_NBT, self.prev
+        if exc_type is None and pending:
+            items = list(pending.values())
+            ptrs = (C.c_void_p * len(items))(*[t.data_ptr() for t, _ in items])
+            vals = (C.c_int64 * len(items))(*[k for _, k in items])
+            hip.call("es_counters_add_i64_if", ptrs, vals, len(items), hip.active_ptr(), hip.stream_ptr())
+        return False
+
+
 def _count_batch(nbt):
     if hip.live_on():
         # dynamic rows: +1 on the device when the running expert trains (a captured graph replays it)
-        hip.call("es_counter_add_i64_if", hip.ptr(nbt), 1, hip.active_ptr(), hip.stream_ptr())
+        if _LIVE_NBT is not None:
+            t, k = _LIVE_NBT.get(id(nbt), (nbt, 0))
+            _LIVE_NBT[id(nbt)] = (t, k + 1)
+        else:
+            hip.call("es_counter_add_i64_if", hip.ptr(nbt), 1, hip.active_ptr(), hip.stream_ptr())
         return
     if _NBT_PENDING is None:
         nbt.add_(1)

@@ -39,7 +39,8 @@ from torch import nn
 
 from .. import hip
 from ..config import cfg_get
-from ..layers import Act, copy_act, defer_num_batches, set_deterministic, set_f32_split, set_norm_sync
+from ..layers import (Act, batch_live_counts, copy_act, defer_num_batches, set_deterministic, set_f32_split,
+                      set_norm_sync)
 from ..rng import DeviceRNG
 from ..utils import philox
 
@@ -449,7 +450,7 @@ class MoEWrapper(nn.Module):
                 self._expert_program(e, be, B, G, D, A, sc, sr, sp, ss, si, opt_g, opt_d, opt_a, mbuf, dev, w_dev,
                                      sb, seed, n0, sync, rows, ridx, None, None)
             else:
-                with hip.live_rows(be, live, plan["active"][e:e + 1]):
+                with hip.live_rows(be, live, plan["active"][e:e + 1]), batch_live_counts():
                     self._expert_program(e, be, B, G, D, A, sc, sr, sp, ss, si, opt_g, opt_d, opt_a, mbuf, dev,
                                          w_dev, sb, seed, n0, sync, rows, ridx, live, plan["gcnt"][e:e + 1])
         finally:

@@ -609,6 +609,10 @@ int es_randn_dev_at(float* out, int64_t n, uint64_t seed, uint32_t stream_id, co
 int es_counter_add(int32_t* counter, int32_t v, es_stream_t stream);
 int es_counter_add_if(int32_t* counter, int32_t v, const int32_t* flag, es_stream_t stream);
 int es_counter_add_i64_if(int64_t* counter, int64_t v, const int32_t* flag, es_stream_t stream);
+/* es_counter_add_i64_if over n counters in one launch (host arrays of device pointers / addends): the
+ * BatchNorm num_batches_tracked counts of one expert program (dynamic rows) applied together. */
+int es_counters_add_i64_if(int64_t* const* counters, const int64_t* v, int n, const int32_t* flag,
+                           es_stream_t stream);
 /* Multi-expert step plan on the device (moe.py:97-135 without the host round trip): from counts [E]
  * (this rank's expert counts, es_router_gumbel) and, data parallel, counts_all [world][E] (all ranks'
  * counts, all-gathered on the device; NULL on one process), for each expert e: rows[e] = this rank's

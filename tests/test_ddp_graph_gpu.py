@@ -77,15 +77,17 @@ def _worker(port, q):
             dist.destroy_process_group()
 
 
-@pytest.mark.timeout(300)
+@pytest.mark.timeout(240)
 def test_ddp_graph_replay_matches_eager_rccl_world1():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=_worker, args=(_free_port(), q))
     p.start()
     try:
-        runs, err = q.get(timeout=240)
-        p.join(timeout=60)
+        # (the worker takes ~15 s; a stuck RCCL init is reported within 150 s, before a runner's
+        # silence limit would take it for a hung GPU)
+        runs, err = q.get(timeout=150)
+        p.join(timeout=30)
     finally:
         if p.is_alive():           # a stuck worker must not outlive the test holding the GPU
             p.kill()
