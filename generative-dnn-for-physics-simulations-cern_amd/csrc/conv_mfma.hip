@@ -2966,7 +2966,9 @@ int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
   // short-K FWD (<= 8 K-steps, e.g. conv_layers.9: 2x2 taps x 128 channels): 128 x 64 tiles (72 KiB
   // of LDS, two workgroups per CU) so one tile's fill and epilogue overlap another's MFMAs
   // (measured 201 -> 177 us; the same rule on the DGRAD of that conv was slower)
-  const bool shortk = mode == MODE_FWD && !sp_weights && a.Kd / 64 <= 8;
+  // (bf16 only: the fp32 kernels' K-steps are 32 channels, so the same conv has 16 of them and takes
+  // the 256-row tiles: conv_layers.9 FWD 1109 -> 1064 us per op at B = 1024, round 5)
+  const bool shortk = mode == MODE_FWD && !sp_weights && a.Kd / 64 <= 8 && EB == 2;
   // persistent short-K kernel (conv_persist_kernel): FWD / DGRAD, stride 1, no upsample / sub-pixel,
   // <= 8 K-steps, the whole weight panel (nk x Ng x 128 B) within 64 KiB, dense 16-byte output rows
   {
