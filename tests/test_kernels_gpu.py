@@ -978,3 +978,41 @@ def test_router_dispatch_is_stable_grouping(B, E):
     counts = np.bincount(idx.numpy(), minlength=E)
     assert np.array_equal(perm.cpu().numpy(), want)
     assert np.array_equal(offs.cpu().numpy(), np.concatenate([[0], np.cumsum(counts)]))
+
+
+def test_batched_weight_repack_matches_single_packs():
+    """es_pack_conv_weights (the optimizer step's batched repack, layers.repack_ops) writes the same
+    bytes as es_pack_conv_weight (+ es_pack_weight_planes) per job: every mode, both dtypes, the
+    split-fp32 planes, and a wide mode-1 transpose (the LDS-tiled kernel inside the batch)."""
+    import ctypes as C
+    from expertsim import hip
+    hip.lib()
+    g = torch.Generator().manual_seed(3)
+    shapes = [(128, 256, 3, 3, 2), (128, 256, 3, 3, 3), (64, 128, 2, 2, 0), (64, 128, 2, 2, 1),
+              (32, 1, 3, 3, 0), (1, 64, 2, 2, 1), (4096, 256, 1, 1, 0), (4096, 256, 1, 1, 1), (48, 20, 3, 3, 1)]
+    jobs, refs, outs = [], [], []
+    for K, Cc, R, S, mode in shapes:
+        w = torch.randn(K, Cc, R, S, generator=g).to(DEV)
+        n = K * Cc * (hip.lib().es_subpixel_taps(R, S) if mode >= 2 else R * S)
+        for dtype in (torch.float32, torch.bfloat16):
+            planes = dtype == torch.float32
+            total = (int(hip.lib().es_weight_planes_offset(n)) + 6 * n + 3) // 4 if planes else n
+            ref = torch.zeros(total, dtype=dtype, device=DEV)
+            hip.call("es_pack_conv_weight", hip.ptr(w), K, Cc, R, S, mode, None, None, hip.ptr(ref), hip.dt_of(ref),
+                     hip.stream_ptr())
+            if planes:
+                hip.call("es_pack_weight_planes", hip.ptr(ref), n, hip.ptr(ref), hip.stream_ptr())
+            out = torch.zeros_like(ref)
+            j = hip.PackJob()
+            j.w, j.K, j.C, j.R, j.S, j.mode = w.data_ptr(), K, Cc, R, S, mode
+            j.dt, j.planes, j.out = hip.dt_of(out), int(planes), out.data_ptr()
+            jobs.append(j)
+            refs.append(ref)
+            outs.append((out, w))
+    arr = (hip.PackJob * len(jobs))(*jobs)
+    hip.call("es_pack_conv_weights", arr, len(jobs), hip.stream_ptr())
+    torch.cuda.synchronize()
+    for (out, _), ref, (K, Cc, R, S, mode) in zip(outs, refs, [s for s in shapes for _ in (0, 1)]):
+        assert torch.equal(out.view(torch.int16) if out.dtype == torch.bfloat16 else out.view(torch.int32),
+                           ref.view(torch.int16) if ref.dtype == torch.bfloat16 else ref.view(torch.int32)), \
+            (K, Cc, R, S, mode, out.dtype)
