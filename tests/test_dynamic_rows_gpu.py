@@ -203,3 +203,49 @@ def test_norm_dynamic_rows(case, sync):
     assert float((ds - dsr).abs().max()) <= 1e-5 * float(dxr.torch_nchw().abs().sum()) / Cc
     if kind == "bn":
         assert _rel(nm.rm, nr.rm) <= 1e-6 and _rel(nm.rv, nr.rv) <= 1e-6
+
+
+def test_batched_batchnorm_counts_multi_expert():
+    """Dynamic rows: an expert program's BatchNorm num_batches_tracked increments are applied on the
+    device in one launch at its end (layers.batch_live_counts -> es_counters_add_i64_if), gated on the
+    expert's active flag.  After two E = 3 steps every generator BatchNorm of an expert that trained in
+    both counts 4 (two generator forwards per step, moe.py:145,538), every aux BatchNorm 2, and the
+    counts equal the per-forward launches' (the unbatched path)."""
+    import bench
+    from expertsim import layers
+    from expertsim.utils.synthetic import make_batch
+    b = make_batch(96, "neutron", seed=4)
+    t = {k: torch.from_numpy(v).to(DEV) for k, v in b.items()}
+    real = t["real_images"].unsqueeze(1).contiguous()
+    counts = []
+    for batched in (True, False):
+        moe, (og, od, oa, orr), cfg = bench.build("neutron", 3, "fp32", 11, torch.device(DEV))
+        moe.expert_graphs = False
+        orig = layers.batch_live_counts
+        if not batched:
+            class _Off:
+                def __enter__(self):
+                    return self
+
+                def __exit__(self, *a):
+                    return False
+            import expertsim.models.moe as M
+            M.batch_live_counts = _Off
+        try:
+            args = (0, t["cond"], real, t["true_positions"], t["std"], t["intensity"], oa, og, od, orr, None, DEV)
+            for _ in range(2):
+                m = moe.train_step(*args)
+        finally:
+            import expertsim.models.moe as M
+            M.batch_live_counts = orig
+        torch.cuda.synchronize()
+        nbt = {n: int(v) for n, v in moe.state_dict().items() if n.endswith("num_batches_tracked")}
+        counts.append(nbt)
+        active = [float(m[f"n_choosen_experts_mean_epoch_{i}"]) > 1 for i in range(3)]
+        for n, v in nbt.items():
+            e = int(n.split(".")[1])
+            if n.startswith("generators.") and active[e]:
+                assert v in (2, 4), (n, v)      # 2 per step the expert trained
+            if n.startswith("aux_regs.") and active[e]:
+                assert v in (1, 2), (n, v)
+    assert counts[0] == counts[1]
