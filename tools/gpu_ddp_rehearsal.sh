@@ -11,8 +11,8 @@ run() {
     echo "$name rc=$rc"
     return $rc
 }
-run nccl1 python -u bench.py --ddp --steps 20 --fp32-steps 5 --no-cpu-baseline &&
-run nccl1_sync python -u bench.py --ddp --sync-bn --steps 20 --fp32-steps 0 --no-cpu-baseline --no-probe &&
+run nccl1 python -u bench.py --ddp --steps 20 --other-steps 5 --no-cpu-baseline &&
+run nccl1_sync python -u bench.py --ddp --sync-bn --steps 20 --other-steps 0 --no-cpu-baseline --no-probe &&
 run gloo2 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
     --master-port 29611 bench.py --gpus 2 --backend gloo --batch 256 --steps 10 --warmup 3 &&
 run gloo2_e4 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
