@@ -2804,7 +2804,8 @@ bool dense_small(const int64_t s[4], int n, int c, int h, int w) { return dense_
 
 // Tuning constants, each chosen by alternating A/B on whole train steps:
 //   * short-K FWD (<= 8 K-steps, e.g. conv_layers.9): 128 x 64 tiles, two workgroups per CU (201 -> 177 us);
-//   * image-group size 64 of the row order (64 > 16 > 8 on the whole step; 8 for an isolated FWD);
+//   * image-group size 64 of the row order (64 > 16 > 8 on the whole step; 8 for an isolated FWD),
+//     16 under dynamic rows;
 //   * sub-pixel FWD: class-interleaved tile order (14.45 -> 14.33 ms per step), one 256 x 256 GEMM over
 //     (class, channel) columns when the 4 classes share their geometry;
 //   * 256 x 256 tiles with 32-deep K-steps for FWD / DGRAD with >= 256 output columns;
@@ -2812,6 +2813,12 @@ bool dense_small(const int64_t s[4], int n, int c, int h, int w) { return dense_
 //     with fused statistics, 376 vs 364 us) and the persistent 256 x 256 merged sub-pixel FWD.
 // The switches below are test hooks (es_conv_set_*: the kernel tests compare the paths bitwise).
 constexpr int RING_NG = 64;
+// Dynamic rows (multi-expert steps: capacity-B launches, a device count of live images): groups of
+// 16 images, so the last, partly live group of an expert's rows carries at most 15 dead images
+// through the MFMAs instead of up to 63 (E = 4, B = 512: 28.1 -> 26.8 ms/step fp32, 13.07 -> 12.69
+// bf16, alternating against 64 and 32 on one box; profiles/r05_ngdyn_ab.log).  16 is also the
+// smallest group the 32-deep K-step kernels' 16-row DMA pieces allow.
+constexpr int RING_NG_DYN = 16;
 bool g_subpixel_off = false;
 bool g_ring256 = true;
 bool g_persist = true;
@@ -2958,8 +2965,8 @@ int ring_fd(ConvArgs& a, int mode, hipStream_t st) {
   if ((int64_t)a.Ng * a.Kd * EB * (sp_weights ? 2 : 1) >= (1ll << 30)) return sp_weights ? -1 : 0;
   // image group size of the row order (see conv_ring_kernel).  Measured on the whole train step
   // (tools/gpu_ab.sh, one box): 64 > 16 > 8 for both FWD and DGRAD, although an isolated FWD
-  // prefers 8 (less MALL traffic).  ES_RING_NG overrides it (measurement).
-  a.ng = RING_NG;
+  // prefers 8 (less MALL traffic).  Dynamic rows take 16 (RING_NG_DYN).
+  a.ng = d.rows ? RING_NG_DYN : RING_NG;
   while (a.ng > 8 && a.ng / 2 >= d.N) a.ng /= 2;   // small batches (per-expert shards): no empty rows
   const int NGI = (d.N + a.ng - 1) / a.ng;
   const int nt128 = (a.Ng + 127) / 128;
