@@ -54,6 +54,9 @@ def _rel(a, b):
 CONV = [
     # (N, n, Cin, H, W, Cout, k, stride, pad, upsample)
     (70, 37, 128, 13, 13, 256, 3, 1, 0, (2, 2)),    # neutron G conv_layers.0 (sub-pixel ring)
+    # conv_layers.5 at an E = 4, B = 512 expert's scale: 256-row tiles over 16-image groups (the
+    # dynamic-rows row order), 203 live = 12 whole groups + 11 images of a 13th
+    (512, 203, 256, 24, 24, 128, 3, 1, 0, (2, 2)),
     (70, 37, 128, 46, 46, 64, 2, 1, 0, None),       # conv_layers.9 (ring / split-fp32 col WGRAD)
     (70, 70, 128, 46, 46, 64, 2, 1, 0, None),       # every row live
     (70, 0, 128, 46, 46, 64, 2, 1, 0, None),        # no row live
