@@ -312,7 +312,8 @@ def live_on() -> bool:
 
 def rows_ptr(n: int):
     """The live-count pointer for a tensor of n samples (None outside a dynamic program or when n
-    is not the capacity)."""
+    is not the capacity).  Callers pass sample counts only: a view whose leading dimension is not a
+    sample dimension is built with sample=False (layers.Act), whatever its size."""
     if _LIVE is None or int(n) != _LIVE[0]:
         return None
     return _LIVE[1].data_ptr()
@@ -333,12 +334,14 @@ def live_count():
     return None if _LIVE is None else int(_LIVE[1].item())
 
 
-def make_view(dims, strides) -> View:
+def make_view(dims, strides, sample: bool = True) -> View:
+    """sample: the leading dimension counts samples (layers.Act.sample); only such a view of the
+    running expert's capacity carries its live count."""
     v = View()
     v.n, v.c, v.h, v.w = (int(d) for d in dims)
     for i in range(4):
         v.s[i] = int(strides[i])
-    v.rows = rows_ptr(v.n)
+    v.rows = rows_ptr(v.n) if sample else None
     return v
 
 

@@ -20,10 +20,13 @@ from . import hip
 class Act:
     """Logical (N, C, H, W) tensor over a flat device buffer with explicit element strides."""
 
-    __slots__ = ("t", "dims", "strides", "bn_part", "bn_sums", "px")
+    __slots__ = ("t", "dims", "strides", "bn_part", "bn_sums", "px", "sample")
 
-    def __init__(self, t: torch.Tensor, dims, strides):
+    def __init__(self, t: torch.Tensor, dims, strides, sample: bool = True):
         self.px = 0               # > 0: each image's P*Q pixels are px consecutive samples (pixel view)
+        # sample-major: dims[0] counts samples, so inside a dynamic-rows expert program a view of
+        # capacity rows carries the live count (hip.make_view); False for any other leading dimension
+        self.sample = bool(sample)
         self.bn_part = None       # (partials, chunks) of fused BatchNorm statistics (ConvOp.fwd)
         self.bn_sums = None       # (partials, chunks, norm) of a fused BatchNorm-backward reduction (ConvOp.dgrad)
         self.t = t
@@ -57,7 +60,7 @@ class Act:
     # ---- properties
     @property
     def view(self):
-        return hip.make_view(self.dims, self.strides)
+        return hip.make_view(self.dims, self.strides, self.sample)
 
     @property
     def dt(self):
@@ -83,7 +86,7 @@ class Act:
 
     def head(self, n):
         """The first n samples (same memory)."""
-        return Act(self.t, (int(n), *self.dims[1:]), self.strides)
+        return Act(self.t, (int(n), *self.dims[1:]), self.strides, self.sample)
 
     def rows2d(self):
         n, c, h, w = self.dims

@@ -30,6 +30,7 @@ step of the global batch.
 from __future__ import annotations
 
 
+import contextlib
 import copy
 import ctypes as C
 
@@ -196,8 +197,9 @@ class MoEWrapper(nn.Module):
             # per-expert HIP graphs (ExpertGraphs): the batch lives in static buffers the graphs read
             cond, real_images, true_positions, std, intensity = self._static_inputs(
                 dev, cond, real_images, true_positions, std, intensity)
-            if self._egraphs is None:
-                self._egraphs = ExpertGraphs(concurrent=self.expert_graphs_concurrent)
+            conc = self._experts_concurrent(E, B)
+            if self._egraphs is None or self._egraphs.concurrent != conc:
+                self._egraphs = ExpertGraphs(concurrent=conc)
             self._graphs = self._egraphs
         rc = self.cfg.model.router
         if self._dstep is None or self._dstep.device != dev:
@@ -256,11 +258,20 @@ class MoEWrapper(nn.Module):
                          if E > 1 and float(rc.ed_strength) != 0.0 else None)
         if self._graphs is not None:
             self._graphs.begin()
-        # a whole step being captured (graph.StepGraph) with several experts and one process: the
-        # experts' programs fork onto their own streams inside the graph (no shared parameters,
-        # disjoint rows of the step's buffers), joined back before the router
+        # several experts: their programs fork onto their own streams (no shared parameters, disjoint
+        # rows of the step's buffers), joined back before the router -- inside a whole-step capture
+        # of one process (graph.StepGraph), and in eager data-parallel steps, where each expert's
+        # collectives run on a communicator of its own (ddp.expert_groups).  (Eager single-process
+        # steps replay the experts' own graphs concurrently instead, ExpertGraphs.)  A captured
+        # data-parallel step runs its experts one after another: torch's ProcessGroupNCCL aborts when
+        # collectives are issued from forked streams inside a capture (measured: its watchdog queried
+        # an event recorded in the capture, "operation not permitted on an event last recorded in a
+        # capturing stream"; a segmentation fault with its event cache off; tools/ddp_e4_probe.py)
         fork = None
-        if plan is not None and ddp is None and self.expert_graphs_concurrent and torch.cuda.is_current_stream_capturing():
+        capturing = torch.cuda.is_current_stream_capturing()
+        if plan is not None and self._experts_concurrent(E, B) and capturing == (ddp is None):
+            if ddp is not None:
+                ddp.ensure_expert_groups(E)
             fork = self._fork_streams(E)
         for e, rows, be in groups:
             og, od, oa = generator_optimizers[e], discriminator_optimizers[e], aux_reg_optimizers[e]
@@ -381,6 +392,23 @@ class MoEWrapper(nn.Module):
         return {k: mvec[j] for j, k in enumerate(names)}
 
     # ---------------------------------------------------------------------------- one expert
+    # auto: concurrent experts while E x B capacity images of activations stay below this many
+    # (each concurrent expert holds its own capacity-B buffers); serial experts share one set
+    SERIAL_EXPERT_IMAGES = 16384
+
+    def _experts_concurrent(self, E, B):
+        """Run the experts' programs concurrently (own streams / graphs / memory) or one after another
+        (one stream, buffers reused from expert to expert: activation memory of one capacity-B program
+        instead of E).  train.expert_streams: auto | concurrent | serial."""
+        if not self.expert_graphs_concurrent:
+            return False
+        mode = str(cfg_get(self.cfg, "train.expert_streams", "auto"))
+        if mode not in ("auto", "concurrent", "serial"):
+            raise ValueError(f"train.expert_streams must be auto, concurrent or serial, got {mode!r}")
+        if mode == "auto":
+            return E * B <= self.SERIAL_EXPERT_IMAGES
+        return mode == "concurrent"
+
     def _fork_streams(self, E):
         """One side stream per expert (kept across steps), each made to wait for the current stream.
         (Measured, E = 4 B = 512 fp32: 2 / 3 / 4 streams 31.4 / 32.8 / 28.9 ms per step; 8 hardware
@@ -442,19 +470,22 @@ class MoEWrapper(nn.Module):
         if ddp is not None:
             n0 = ddp.sample_offset(e) if plan is None else plan["n0"][e:e + 1]
         sync = ddp is not None and ddp.sync_bn
-        if sync:
-            ddp.expert = e
-            set_norm_sync(ddp)
-        try:
-            if plan is None:
-                self._expert_program(e, be, B, G, D, A, sc, sr, sp, ss, si, opt_g, opt_d, opt_a, mbuf, dev, w_dev,
-                                     sb, seed, n0, sync, rows, ridx, None, None)
-            else:
-                with hip.live_rows(be, live, plan["active"][e:e + 1]), batch_live_counts():
+        # data parallel: the expert's collectives (SyncBN, SDI mean, gradient buckets) run on its own
+        # communicator when the experts run concurrently (ddp.expert_groups), else on the main group
+        scope = ddp.on_expert(e) if ddp is not None else contextlib.nullcontext()
+        with scope:
+            if sync:
+                set_norm_sync(ddp)
+            try:
+                if plan is None:
                     self._expert_program(e, be, B, G, D, A, sc, sr, sp, ss, si, opt_g, opt_d, opt_a, mbuf, dev,
-                                         w_dev, sb, seed, n0, sync, rows, ridx, live, plan["gcnt"][e:e + 1])
-        finally:
-            set_norm_sync(None)
+                                         w_dev, sb, seed, n0, sync, rows, ridx, None, None)
+                else:
+                    with hip.live_rows(be, live, plan["active"][e:e + 1]), batch_live_counts():
+                        self._expert_program(e, be, B, G, D, A, sc, sr, sp, ss, si, opt_g, opt_d, opt_a, mbuf,
+                                             dev, w_dev, sb, seed, n0, sync, rows, ridx, live, plan["gcnt"][e:e + 1])
+            finally:
+                set_norm_sync(None)
 
     def _expert_program(self, e, be, B, G, D, A, sc, sr, sp, ss, si, opt_g, opt_d, opt_a, mbuf, dev, w_dev, sb,
                         seed, n0, sync, rows, ridx, live, gcnt):
@@ -511,7 +542,8 @@ class MoEWrapper(nn.Module):
             if gcnt is not None:     # dynamic rows: / the expert's global count (device)
                 hip.call("es_div_by", hip.ptr(std_mean), 1, hip.ptr(gcnt), hip.stream_ptr())
             else:
-                copy_act(Act.of(std_mean.view(1, 1)), Act.of(std_mean.view(1, 1)), 1.0 / ddp.global_count(e), 0.0)
+                sm = Act(std_mean, (1, 1, 1, 1), (1, 1, 1, 1), sample=False)
+                copy_act(sm, sm, 1.0 / ddp.global_count(e), 0.0)
             p.std_mean = std_mean.data_ptr()
         dfo1 = torch.empty(be, 1, dtype=torch.float32, device=dev)
         dl1 = torch.empty(be, L, dtype=torch.float32, device=dev)
@@ -597,7 +629,8 @@ class ExpertGraphs:
     per expert: experts share no parameters and write disjoint rows of the step's buffers, and a
     quarter-batch expert alone leaves most of the chip idle.  Each expert has its own memory pool
     (its graphs replay one after another, so they may share temporaries; different experts'
-    graphs may not).  Everything that changes between steps is read on the device: the step
+    graphs may not; serial experts, concurrent=False, share one stream and one pool).  Everything
+    that changes between steps is read on the device: the step
     counters (dropout / noise streams, Adam bias corrections), the expert's rows (dispatch
     permutation + device start + live count), the batch (static input buffers).  The first
     occurrence of a key is captured and then replayed; BatchNorm batch counts are advanced on the
@@ -626,9 +659,11 @@ class ExpertGraphs:
         from ..layers import count_batches, nbt_added, nbt_snapshot
         e = key[0]
         if e not in self.streams:
-            shared = None if self.concurrent or not self.streams else next(iter(self.streams.values()))
-            self.streams[e] = shared or torch.cuda.Stream()
-            self.pools[e] = torch.cuda.graph_pool_handle()
+            # serial: every expert's graph replays on one stream, one after another, so they share
+            # one memory pool too (a graph's temporaries are dead once its replay has finished)
+            first = None if self.concurrent or not self.streams else next(iter(self.streams))
+            self.streams[e] = self.streams[first] if first is not None else torch.cuda.Stream()
+            self.pools[e] = self.pools[first] if first is not None else torch.cuda.graph_pool_handle()
         st = self.streams[e]
         st.wait_event(self._ready)
         entry = self.graphs.get(key)

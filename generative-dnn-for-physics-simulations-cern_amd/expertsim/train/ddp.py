@@ -31,9 +31,18 @@ data-parallel over a node's GPUs.  Semantics:
   * gradient all-reduces overlap the compute (``allreduce_async`` on the process group's stream):
     the discriminator's with the second generator forward, the aux regressor's with the generator
     backward, and the generator's in >= 1 MB buckets issued as its second backward finalises each
-    layer group (``bucketer``; the flat buffer's tail first); the optimizer steps wait for them.
+    layer group (``bucketer``; the flat buffer's tail first); the optimizer steps wait for them;
+  * multi-expert steps run the experts CONCURRENTLY (each expert's program on its own HIP stream,
+    reference per-expert loop moe.py:121-207): every expert gets a process group of its own over
+    the same ranks (``expert_groups``, created once, in the same order on every rank), and its SyncBN
+    gathers / backward sums, SDI mean and gradient buckets run on that communicator
+    (``on_expert``), so no communicator is shared by two streams.  Each communicator still sees the
+    same per-rank issue order (an expert's program is issued in full before the next); the routing
+    counts, router and metric collectives stay on the main group, outside the fork.
 """
 from __future__ import annotations
+
+import contextlib
 
 import numpy as np
 import torch
@@ -44,29 +53,62 @@ from .. import hip
 
 class DataParallel:
     def __init__(self, world_size=None, rank=None, group=None, sync_bn=False):
-        self.group = group
+        self.group = group         # the main group (routing counts, router, metrics)
         self.world = world_size if world_size is not None else dist.get_world_size(group)
         self.rank = rank if rank is not None else dist.get_rank(group)
         self.sync_bn = bool(sync_bn)
         self.gloo = dist.get_backend(group) != "nccl"
-        self._counts = None        # global count per expert
+        self._counts = None        # global count per expert (single-expert steps)
         self._offsets = None       # this rank's first global sample index per expert
         self._local = None         # local count per expert
         self.local_batch = None
         self._counts_dev = {}
         self.expert = None         # expert whose step is running (global count for SyncBN)
         self.plan = None           # multi-expert steps: the device plan (MoEWrapper._plan)
+        self.expert_groups = None  # one process group per expert (concurrent experts)
+        self._cur = None           # the group of the running expert (None: the main group)
         self._pending = []         # async all-reduce works not yet waited for
         self.issued = []           # (module, lo, hi) of every gradient all-reduce (tests)
+
+    # ---------------------------------------------------------------- per-expert communicators
+    def ensure_expert_groups(self, E: int):
+        """One process group per expert over the main group's ranks.  dist.new_group is collective
+        over the world: every rank calls this at the same point of the same step (the first
+        multi-expert step, before any capture)."""
+        if self.expert_groups is not None and len(self.expert_groups) >= E:
+            return self.expert_groups
+        ranks = None if self.group is None else dist.get_process_group_ranks(self.group)
+        have = list(self.expert_groups or [])
+        while len(have) < E:
+            have.append(dist.new_group(ranks=ranks))
+        self.expert_groups = have
+        return have
+
+    @contextlib.contextmanager
+    def on_expert(self, e: int, own_group: bool = True):
+        """The collectives issued inside run on expert e's communicator (``own_group``) and
+        SyncBN reads expert e's global count."""
+        prev = (self.expert, self._cur)
+        self.expert = e
+        if own_group and self.expert_groups is not None:
+            self._cur = self.expert_groups[e]
+        try:
+            yield self
+        finally:
+            self.expert, self._cur = prev
+
+    @property
+    def cur_group(self):
+        return self.group if self._cur is None else self._cur
 
     # ---------------------------------------------------------------- collectives on device tensors
     def all_reduce_(self, t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
         if self.gloo and t.is_cuda:        # gloo (CPU tests / single-GPU rehearsals): via the host
             h = t.cpu()
-            dist.all_reduce(h, op=op, group=self.group)
+            dist.all_reduce(h, op=op, group=self.cur_group)
             t.copy_(h)
         else:
-            dist.all_reduce(t, op=op, group=self.group)
+            dist.all_reduce(t, op=op, group=self.cur_group)
         return t
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
@@ -75,31 +117,22 @@ class DataParallel:
         if self.gloo:
             src = t.cpu() if t.is_cuda else t
             parts = [torch.empty_like(src) for _ in range(self.world)]
-            dist.all_gather(parts, src, group=self.group)
+            dist.all_gather(parts, src, group=self.cur_group)
             return torch.stack(parts).to(t.device)
         out = torch.empty((self.world, *t.shape), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t, group=self.group)
+        dist.all_gather_into_tensor(out, t, group=self.cur_group)
         return out
 
     # ---------------------------------------------------------------- routing bookkeeping
     def global_groups(self, groups, B_local):
-        """Global per-expert counts and this rank's sample offsets (one small all-gather for E > 1)."""
-        E = len(groups)
+        """Single-expert step: the global count and this rank's sample offset (equal shards:
+        DistributedSampler(drop_last=True) and bench.py give them) -- no collective, no host sync.
+        Multi-expert steps keep their counts on the device (set_plan)."""
+        assert len(groups) == 1, "multi-expert steps use the device plan (MoEWrapper._plan)"
         self.local_batch = B_local
-        if E == 1:
-            # one expert holds every sample: equal shards (DistributedSampler(drop_last=True) and
-            # bench.py give them) -- no collective, no host sync
-            self._counts = np.array([B_local * self.world], dtype=np.int64)
-            self._offsets = np.array([B_local * self.rank], dtype=np.int64)
-            self._local = np.array([B_local], dtype=np.int64)
-            return groups
-        local = torch.tensor([g[2] for g in groups], dtype=torch.int64)
-        if not self.gloo:
-            local = local.to(torch.device("cuda", torch.cuda.current_device()))
-        allc = self.all_gather(local).cpu().numpy()     # [world, E] (the routing host sync)
-        self._local = allc[self.rank]
-        self._counts = allc.sum(0)
-        self._offsets = allc[:self.rank].sum(0) if self.rank else np.zeros(E, dtype=np.int64)
+        self._counts = np.array([B_local * self.world], dtype=np.int64)
+        self._offsets = np.array([B_local * self.rank], dtype=np.int64)
+        self._local = np.array([B_local], dtype=np.int64)
         return groups
 
     def set_plan(self, plan, B_local):
@@ -159,7 +192,7 @@ class DataParallel:
             if self.gloo:
                 self.all_reduce_(g[lo:hi])
             else:
-                self._pending.append(dist.all_reduce(g[lo:hi], group=self.group, async_op=True))
+                self._pending.append(dist.all_reduce(g[lo:hi], group=self.cur_group, async_op=True))
             self.issued.append((module, lo, hi))
         module._grad_scale = 1.0 / self.world if average else 1.0
 

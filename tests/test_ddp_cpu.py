@@ -57,16 +57,24 @@ def _bookkeeping_worker(rank, world, port, q):
     _init(rank, world, port)
     from expertsim.train.ddp import DataParallel
     ddp = DataParallel()
-    # rank 0 routes 5 / 1 / 0 samples to experts 0..2, rank 1 routes 2 / 0 / 4
-    local = {0: [5, 1, 0], 1: [2, 0, 4]}[rank]
-    groups = [(e, None, c) for e, c in enumerate(local)]
-    ddp.global_groups(groups, 6)
-    counts = [ddp.global_count(e) for e in range(3)]
-    offsets = [ddp.sample_offset(e) for e in range(3)]
-    active = [c > 1 for c in counts]
+    # single-expert step: equal shards of 6, no collective
+    ddp.global_groups([(0, None, 6)], 6)
+    counts, offsets = [ddp.global_count(0)], [ddp.sample_offset(0)]
     m = _FakeModule(rank)
     ddp.allreduce_grads(m)
-    q.put((rank, counts, offsets, active, ddp.global_batch, float(m.flat_grads[0]), m._grad_scale))
+    # multi-expert steps: one communicator per expert (concurrent experts), the main group outside
+    groups = ddp.ensure_expert_groups(3)
+    assert ddp.ensure_expert_groups(2) is groups and len(set(map(id, groups))) == 3
+    sums = []
+    for e in (2, 0, 1):
+        with ddp.on_expert(e):
+            assert ddp.cur_group is groups[e] and ddp.expert == e
+            t = torch.tensor([float(10 * e + rank)])
+            ddp.all_reduce_(t)
+            g = ddp.all_gather(torch.tensor([float(e), float(rank)]))
+            sums.append((e, float(t[0]), g.tolist()))
+    assert ddp.cur_group is None and ddp.expert is None
+    q.put((rank, counts, offsets, ddp.global_batch, float(m.flat_grads[0]), m._grad_scale, sums))
     dist.destroy_process_group()
 
 
@@ -86,13 +94,14 @@ def _spawn(fn, world, *args):
 
 def test_ddp_bookkeeping_world2():
     res = _spawn(_bookkeeping_worker, 2)
-    for rank, counts, offsets, active, gb, g0, scale in res:
-        assert counts == [7, 1, 4]
-        assert offsets == ([0, 0, 0] if rank == 0 else [5, 1, 0])
-        assert active == [True, False, True]
+    for rank, counts, offsets, gb, g0, scale, sums in res:
+        assert counts == [12]
+        assert offsets == [6 * rank]
         assert gb == 12
         assert g0 == 3.0            # 1 + 2 summed; averaging happens inside Adam via grad_scale
         assert scale == 0.5
+        # each expert's collectives ran on its own communicator (issued 2, 0, 1 on both ranks)
+        assert sums == [(e, 20.0 * e + 1.0, [[e, 0.0], [e, 1.0]]) for e in (2, 0, 1)]
 
 
 # ------------------------------------------------------------------------------ oracle semantics

@@ -36,7 +36,9 @@ def _free_port():
     return p
 
 
-def _run(E, B, rank=0, ddp=None, b_global=B_GLOBAL, steps=STEPS):
+def _run(E, B, rank=0, ddp=None, b_global=B_GLOBAL, steps=STEPS, expo=None):
+    """expo: injected Exp(1) draws of the router's Gumbel noise for the GLOBAL batch (numpy
+    [b_global, E]); this process reads its rows."""
     import bench
     from expertsim.utils.synthetic import make_batch
     dev = torch.device("cuda", 0)
@@ -44,6 +46,9 @@ def _run(E, B, rank=0, ddp=None, b_global=B_GLOBAL, steps=STEPS):
     if ddp is not None:
         moe.ddp = ddp
         moe.rank = ddp.rank
+    if expo is not None:
+        mine = torch.from_numpy(expo[rank * B:(rank + 1) * B].copy())
+        moe.gumbel_fn = lambda shape: mine
     out = []
     for s in range(steps):
         b = make_batch(b_global, "neutron", seed=70 + s)
@@ -72,7 +77,7 @@ def _run(E, B, rank=0, ddp=None, b_global=B_GLOBAL, steps=STEPS):
     return out, lr
 
 
-def _worker(rank, world, port, q, E, sync, b_global=B_GLOBAL, steps=STEPS):
+def _worker(rank, world, port, q, E, sync, b_global=B_GLOBAL, steps=STEPS, expo=None):
     import sys
     from conftest import PKG_DIR, REPO
     for p in (PKG_DIR, REPO):
@@ -84,18 +89,19 @@ def _worker(rank, world, port, q, E, sync, b_global=B_GLOBAL, steps=STEPS):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from expertsim.train.ddp import DataParallel
     try:
-        res, _ = _run(E, b_global // world, rank, DataParallel(sync_bn=sync), b_global, steps)
+        res, _ = _run(E, b_global // world, rank, DataParallel(sync_bn=sync), b_global, steps, expo)
         q.put((rank, res, None))
     except Exception as e:         # report instead of hanging the parent
         q.put((rank, None, repr(e)))
     dist.destroy_process_group()
 
 
-def _spawn(E, sync, world=WORLD, b_global=B_GLOBAL, steps=STEPS):
+def _spawn(E, sync, world=WORLD, b_global=B_GLOBAL, steps=STEPS, expo=None):
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, E, sync, b_global, steps)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, E, sync, b_global, steps, expo))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = sorted((q.get(timeout=400) for _ in range(world)), key=lambda r: r[0])
@@ -143,3 +149,48 @@ def test_ddp4_syncbn_e4_b2048_matches_single_device():
     dev = _deviation(single, dp[0], lr)
     print("E=4 B=2048, 4-rank SyncBN vs single (metric rel, param / lr):", dev)
     assert dev[0][0] <= 1e-4 and dev[0][1] <= 2.0 + 1e-3
+
+
+def _skewed_expo(sync, E=3, B=B_GLOBAL):
+    """Gumbel Exp(1) draws that force the routing (an Exp draw of 1e-30 is a Gumbel of +69, far above
+    any logit): rank 0's samples (the first half) go to experts 0 / 1 only -- or, for the per-rank
+    BatchNorm mode, exactly one of them to expert 2 --, rank 1's samples to all three experts."""
+    g = torch.Generator().manual_seed(9)
+    expo = torch.empty(B, E).exponential_(generator=g)
+    for j in range(B):
+        if j < B // 2:
+            k = 2 if (not sync and j == 0) else j % 2
+        else:
+            k = j % 3
+        expo[j, k] = 1e-30
+    return expo.numpy()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("sync", [True, False])
+def test_ddp_rank_without_expert_samples(sync):
+    """a rank that holds no sample (SyncBN) or a single sample (per-rank BatchNorm) of an
+    expert that is active globally.  That rank runs the expert's program on zero live rows (BatchNorm
+    partials of count 0, losses and metric weight 0, zero gradients) but joins every collective of
+    the expert's communicator, so the ranks stay bitwise equal; with SyncBN the step equals the
+    single-device step of the global batch (the same injected routing)."""
+    E = 3
+    expo = _skewed_expo(sync)
+    dp = _spawn(E, sync, expo=expo)
+    for (m0, p0), (m1, p1) in zip(dp[0], dp[1]):
+        assert m0 == m1
+        assert all(np.array_equal(p0[n], p1[n]) for n in p0)
+        assert all(np.isfinite(v) for v in m0.values()), m0
+    n2 = 16 + (0 if sync else 1)
+    for m, _ in dp[0]:
+        assert m["n_choosen_experts_mean_epoch_2"] == n2, m
+    if sync:
+        single, lr = _run(E, B_GLOBAL, expo=expo)
+        dev = _deviation(single, dp[0], lr)
+        print("rank 0 without expert-2 samples, SyncBN vs single (metric rel, param / lr):", dev)
+        assert dev[0][0] <= 1e-4 and dev[0][1] <= 2.0 + 1e-3
+        assert dev[1][0] <= 2e-2 and dev[1][1] <= 4.0 + 1e-3
+    else:
+        # expert 2 trained from rank 1's gradients (rank 0 contributed zeros through the same buckets)
+        (_, p_first), (_, p_last) = dp[0][0], dp[0][-1]
+        assert any(not np.array_equal(p_first[n], p_last[n]) for n in p_first if n.startswith("generators.2."))

@@ -28,7 +28,7 @@ def _free_port():
     return p
 
 
-def _worker(port, q):
+def _worker(port, q, E, B):
     import sys
     from conftest import PKG_DIR, REPO
     for p in (PKG_DIR, REPO):
@@ -45,12 +45,12 @@ def _worker(port, q):
         from expertsim.graph import StepGraph, graph_supported
         from expertsim.train.ddp import DataParallel
         from expertsim.utils.synthetic import make_batch
-        b = make_batch(64, "neutron", seed=5)
+        b = make_batch(B, "neutron", seed=5)
         t = {k: torch.from_numpy(v).to(dev) for k, v in b.items()}
         real = t["real_images"].unsqueeze(1).contiguous()
         runs = []
         for mode in ("eager", "graph"):
-            moe, (og, od, oa, orr), cfg = bench.build("neutron", 1, "fp32", 1234, dev)
+            moe, (og, od, oa, orr), cfg = bench.build("neutron", E, "fp32", 1234, dev)
             moe.ddp = DataParallel(sync_bn=True)
             moe.rank = 0
             assert graph_supported(moe)
@@ -60,6 +60,8 @@ def _worker(port, q):
                     m = moe.train_step(*args)
             else:
                 sg = StepGraph(moe, args, warmup=1)
+                if E > 1:      # the experts forked onto their own streams and communicators
+                    assert moe._side is not None and len(moe.ddp.expert_groups) == E
                 for _ in range(2):
                     m = sg.replay()
                 sg.sync_host_state([*og, *od, *oa, orr])
@@ -68,7 +70,7 @@ def _worker(port, q):
             runs.append(({k: float(v) for k, v in m.items()},
                          # numpy: pickled by value (torch CPU tensors travel as shared-memory fds,
                          # which need the worker alive when the parent unpickles them)
-                         {n: p.detach().cpu().numpy().copy() for n, p in moe.named_parameters()}))
+                         {n: p.detach().cpu().numpy().copy() for n, p in moe.state_dict().items()}))
         q.put((runs, None))
     except Exception as e:         # report instead of hanging the parent
         q.put((None, repr(e)))
@@ -78,10 +80,14 @@ def _worker(port, q):
 
 
 @pytest.mark.timeout(240)
-def test_ddp_graph_replay_matches_eager_rccl_world1():
+@pytest.mark.parametrize("E,B", [(1, 64), (4, 512)])
+def test_ddp_graph_replay_matches_eager_rccl_world1(E, B):
+    """E = 4, B = 512 with SyncBN (BASELINE configs[3]'s per-GPU shard): the experts' programs run
+    forked on their own streams, each with its own RCCL communicator, in the eager steps and inside
+    the captured graph alike."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_worker, args=(_free_port(), q))
+    p = ctx.Process(target=_worker, args=(_free_port(), q, E, B))
     p.start()
     try:
         # (the worker takes ~15 s; a stuck RCCL init is reported within 150 s, before a runner's
