@@ -158,6 +158,9 @@ int es_conv_ring_launch_f32(ConvArgs& a, int mode, hipStream_t st);
 int64_t es_wgrad_f32_ring_floats(const es_conv_desc_t& d, const int64_t ys[4], const int64_t xs[4]);
 int es_wgrad_f32_ring(const es_conv_desc_t& d, const void* dy, const int64_t ys[4], const void* x,
                       const int64_t xs[4], float* dw, float beta, float* ws, int64_t ws_floats, hipStream_t st);
+// the wave-specialised split-fp32 WGRAD partial kernel (conv_wgrad_ws.hip), 128 x bn tiles over grid
+// (row tiles, column tiles, K splits); 1 launched, 0 not eligible
+int es_wgrad_ws_launch(int bn, bool sp, dim3 grid, const ConvArgs& a, float* wsc, int ngt, hipStream_t st);
 // ordered sum of per-split partials ws[split][K][R*S*C] into dW (torch layout [K][C][R][S])
 void es_wgrad_reduce_plain(const float* ws, int splits, int K, int C, int R, int S, float* dw, float beta,
                            hipStream_t st);

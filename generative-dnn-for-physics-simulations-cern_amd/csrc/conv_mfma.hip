@@ -36,6 +36,7 @@
 #include <type_traits>
 
 #include "conv_common.h"
+#include "ring_common.h"
 #include "split_fp32.h"
 
 
@@ -43,7 +44,6 @@ namespace {
 
 constexpr int RT = 512;   // threads per workgroup (8 waves)
 constexpr int NSLOT = 3;  // ring depth
-constexpr uint32_t OOB = 0x80000000u;   // buffer offset past every num_records (< 2^31 bytes)
 // split-fp32 SPB loop (8-wave FWD / DGRAD): column tiles of B planes read ahead of their MFMAs
 constexpr int SPB_PFD = 2;
 // SPB loop: column tile at which waves 4-7 issue their step's DMA (capped at RN - 1; waves 0-3 issue
@@ -58,33 +58,9 @@ constexpr int SPB_DMA_HI = 6;
 
 // es_conv_set_ring(0) routes these shapes to the 4-wave kernels of conv_igemm.hip (tests)
 bool g_ring_off = false;
-
-typedef __attribute__((address_space(3))) void lds_void;
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t mkres(const void* p, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
-}
-// 64 lanes x 16 bytes -> LDS at lds_wave_base + 16 * lane (M0-based, lane-linear)
-__device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, char* lds_wave_base) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_wave_base, 16, (int)voff, 0, 0, 0);
-}
-
-// s_barrier without __syncthreads()'s workgroup fence: that fence makes the compiler drain every
-// in-flight LDS-DMA (vmcnt(0)), which would serialise the ring.  The ring's own vmcnt wait before
-// the barrier is what publishes a wave's pieces; the asm memory clobber keeps the compiler from
-// moving LDS accesses across it.
-__device__ __forceinline__ void ring_barrier() { asm volatile("s_barrier" ::: "memory"); }
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// bijective remap: consecutive ids land on one XCD (round-robin dispatch over 8 XCDs)
-__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
-  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
-  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-}
+// split-fp32 WGRAD with 128-row tiles: the wave-specialised kernel (1) or wgrad_coop_kernel (0);
+// bitwise the same partials (es_conv_set_wgrad_ws, tests / A-B)
+int g_wgrad_ws = 1;
 
 // first argument type of a lambda's call operator (the fragment set of a ring's load lambda)
 template <typename F>
@@ -94,7 +70,6 @@ struct lambda_arg<R (C::*)(A0, As...) const> {
   typedef A0 type;
 };
 
-__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // Per-class sub-pixel values in registers: 4 x int16 packed in one 64-bit scalar, read with a
 // shift.  Indexing the kernel-argument arrays with a runtime class makes hipcc reload them
@@ -3289,7 +3264,8 @@ int es_wgrad_f32_ring(const es_conv_desc_t& d, const void* dy, const int64_t ys[
       ++g_conv_launches;
 #define ES_WC(BN)                                                                                          \
   do {                                                                                                     \
-    if (p.sp) hipLaunchKernelGGL((wgrad_coop_kernel<128, BN, true>), grid, dim3(RT), 0, st, a, wsc, p.ngt); \
+    if (g_wgrad_ws && es_wgrad_ws_launch(BN, p.sp, grid, a, wsc, p.ngt, st) == 1) {                       \
+    } else if (p.sp) hipLaunchKernelGGL((wgrad_coop_kernel<128, BN, true>), grid, dim3(RT), 0, st, a, wsc, p.ngt); \
     else hipLaunchKernelGGL((wgrad_coop_kernel<128, BN, false>), grid, dim3(RT), 0, st, a, wsc, p.ngt);     \
   } while (0)
       if (p.bn == 256) ES_WC(256);
@@ -3335,6 +3311,12 @@ void es_wgrad_reduce_plain(const float* ws, int splits, int K, int C, int R, int
 extern "C" int es_conv_set_f32_chunk(int images) {
   const int old = g_f32_chunk;
   g_f32_chunk = images > 0 ? images : 0;
+  return old;
+}
+
+extern "C" int es_conv_set_wgrad_ws(int on) {
+  const int old = g_wgrad_ws;
+  g_wgrad_ws = on ? 1 : 0;
   return old;
 }
 

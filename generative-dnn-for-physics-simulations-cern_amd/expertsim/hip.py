@@ -104,6 +104,7 @@ _SIGS = {
     "es_conv2d_dgrad_det": (C.c_int, [P, C.c_int, P, P, P, P, C.c_int, P, P, I64, P]),
     "es_conv_set_f32_chunk": (C.c_int, [C.c_int]),
     "es_conv_set_f32_split": (C.c_int, [C.c_int]),
+    "es_conv_set_wgrad_ws": (C.c_int, [C.c_int]),
     "es_weight_planes_offset": (C.c_int64, [C.c_int64]),
     "es_pack_weight_planes": (C.c_int, [P, C.c_int64, P, P]),
     "es_pack_conv_weights": (C.c_int, [P, C.c_int, P]),

@@ -178,6 +178,11 @@ int es_conv2d_fwd_det(const es_conv_desc_t* d, es_dtype_t dt, const void* x, con
 int es_conv2d_dgrad_det(const es_conv_desc_t* d, es_dtype_t dt, const void* dy, const int64_t ys[4], const void* wd,
                         void* dxu, es_dtype_t dxdt, const int64_t dxs[4], void* ws, int64_t ws_bytes,
                         es_stream_t stream);
+/* split-fp32 WGRAD with 128-row tiles: 1 (default) the wave-specialised kernel (waves 0-3 MFMA only,
+waves 4-7 load + split), 0 the cooperative kernel (every wave loads, splits and multiplies); the
+two give bitwise equal weight gradients.  Returns the previous setting.  Replaces nothing in the
+reference (a kernel choice for ATen convolution_backward's weight gradient). */
+int es_conv_set_wgrad_ws(int on);
 /* Deterministic mode on / off (returns the previous setting): fp32 FWD / DGRAD take no split-K
  * float atomics, the generic norm backward's conv-bias sums become an ordered column reduction.
  * MoEWrapper turns it on in the fp32 parity mode (train.deterministic, default on). */

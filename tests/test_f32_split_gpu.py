@@ -198,3 +198,24 @@ def test_wide_linear_pixel_view_bf16():
     mean, invstd = bn.stats(y)
     assert rel(mean.cpu(), got.mean(0).cpu()) < 1e-3
     assert rel(invstd.cpu(), torch.rsqrt(got.var(0, unbiased=False) + 1e-5).cpu()) < 1e-3
+
+
+@pytest.mark.parametrize("case", [CASES[0], CASES[1], CASES[3], CASES[5], CASES[7],
+                                  (130, 256, 24, 24, 128, 3, 1, 0, 2), (33, 128, 13, 13, 256, 3, 1, 0, 2)])
+def test_wave_specialised_wgrad_bitwise(case, det):
+    """wgrad_ws_kernel (waves 0-3 MFMA, waves 4-7 load + split, es_conv_set_wgrad_ws(1), the default)
+    against wgrad_coop_kernel (every wave loads, splits and multiplies): the same planes, K order and
+    products, so bitwise the same weight / bias gradients, and within the fp64 bound."""
+    from expertsim import layers
+    hip = _hip()
+    x, w, b, gy, y, gx, gw, gb = _ref(case, seed=5)
+    layers.set_f32_split(True)
+    old = hip.lib().es_conv_set_wgrad_ws(0)
+    try:
+        coop = _run(case, x, w, b, gy)[3:]
+        hip.lib().es_conv_set_wgrad_ws(1)
+        wsk = _run(case, x, w, b, gy)[3:]
+    finally:
+        hip.lib().es_conv_set_wgrad_ws(old)
+    assert torch.equal(coop[0], wsk[0]) and torch.equal(coop[1], wsk[1])
+    assert rel(wsk[0].double(), gw) < 2e-5
