@@ -62,7 +62,11 @@ class StepGraph:
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        # thread_local: the capture does not forbid other threads' HIP calls -- the process group's
+        # watchdog thread keeps querying the events of the eager steps' collectives while this thread
+        # captures (in "global" mode that query failed the capture: hipErrorStreamCaptureUnsupported,
+        # data-parallel E = 4 at world size 1, bench.py --graph on)
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.metrics = moe.train_step(*self.args)
         # capturing ran the Python side of one step without executing it on the device
         moe.step_count -= 1

@@ -63,38 +63,62 @@ def test_neutron56_step_matches_oracle_restatement(E, B):
 def test_neutron56_e8_b4096_full_size():
     """BASELINE configs[4] at its stated size on ONE GPU: neutron56, 8 experts, B = 4096 (the whole
     global batch that configs[4] shards over 8 GPUs).  Parity unpinned (no reference accepts 56x56);
-    property checks over two eager steps on dynamic rows (every expert at capacity B, live counts on the
-    device; per-expert graphs off: eight captured capacity-4096 programs exceed the card, their private
-    pools held 115 GB when tried): finite metrics, the expert counts summing to the batch, every
-    parameter and BatchNorm buffer finite, the trained experts' parameters moved."""
+    property checks over one eager step and two replays of the whole step captured as ONE HIP graph
+    (dynamic rows: every expert at capacity B, live counts on the device).  E x B = 32768 capacity
+    images run the experts one after another (train.expert_streams auto -> serial), so the step's
+    activations are one capacity-B program's, reused expert after expert inside the capture (eight
+    concurrent capacity-4096 programs held 115 GB of graph pools in round 5).  Checks: finite metrics,
+    the expert counts summing to the batch, every parameter and BatchNorm buffer finite, the trained
+    experts' parameters moved, the replays equal to eager steps of a second model (bitwise, fp32
+    deterministic), and the peak device memory reported."""
     import time
     import bench
+    from expertsim.graph import StepGraph
     from expertsim.utils.synthetic import make_batch
     E, B = 8, 4096
-    moe, (og, od, oa, orr), cfg = bench.build("neutron56", E, "fp32", 1234, torch.device(DEV))
-    moe.expert_graphs = False
-    before = {n: p.detach().clone() for n, p in moe.named_parameters()}
     b = make_batch(B, "neutron56", seed=5)
     t = lambda k: torch.from_numpy(b[k]).to(DEV)
-    args = (0, t("cond"), t("real_images").unsqueeze(1).contiguous(), t("true_positions"), t("std"),
-            t("intensity"), oa, og, od, orr, None, DEV)
-    moe.train_step(*args)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    met = moe.train_step(*args)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    met = {k: float(v) for k, v in met.items()}
-    print(f"neutron56 E=8 B=4096 eager step: {dt * 1e3:.1f} ms ({B / dt:.0f} images/s), "
-          f"peak memory {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB")
-    assert all(np.isfinite(v) for v in met.values()), met
-    counts = [met[f"n_choosen_experts_mean_epoch_{i}"] for i in range(E)]
-    assert sum(counts) == pytest.approx(B), counts
-    moved = 0
-    for n, p in moe.named_parameters():
-        assert torch.isfinite(p).all(), n
-        moved += int(not torch.equal(p.detach(), before[n]))
-    for n, buf in moe.named_buffers():
-        if buf.is_floating_point():
-            assert torch.isfinite(buf).all(), n
-    assert moved > len(before) // 2, (moved, len(before))
+    runs = []
+    for mode in ("graph", "eager"):
+        torch.cuda.empty_cache()
+        torch.cuda.reset_peak_memory_stats()
+        moe, (og, od, oa, orr), cfg = bench.build("neutron56", E, "fp32", 1234, torch.device(DEV))
+        assert not moe._experts_concurrent(E, B)
+        before = {n: p.detach().clone() for n, p in moe.named_parameters()}
+        args = (0, t("cond"), t("real_images").unsqueeze(1).contiguous(), t("true_positions"), t("std"),
+                t("intensity"), oa, og, od, orr, None, DEV)
+        moe.expert_graphs = False
+        moe.train_step(*args)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if mode == "graph":
+            sg = StepGraph(moe, args, warmup=0)
+            for _ in range(2):
+                met = sg.replay()
+            sg.sync_host_state([*og, *od, *oa, orr])
+        else:
+            for _ in range(2):
+                met = moe.train_step(*args)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / 2
+        met = {k: float(v) for k, v in met.items()}
+        peak = torch.cuda.max_memory_allocated() / 2**30
+        print(f"neutron56 E=8 B=4096 {mode}: {dt * 1e3:.1f} ms/step ({B / dt:.0f} images/s; the graph's includes "
+              f"its capture), peak memory {peak:.1f} GiB")
+        assert all(np.isfinite(v) for v in met.values()), met
+        counts = [met[f"n_choosen_experts_mean_epoch_{i}"] for i in range(E)]
+        assert sum(counts) == pytest.approx(B), counts
+        moved = 0
+        for n, p in moe.named_parameters():
+            assert torch.isfinite(p).all(), n
+            moved += int(not torch.equal(p.detach(), before[n]))
+        for n, buf in moe.named_buffers():
+            if buf.is_floating_point():
+                assert torch.isfinite(buf).all(), n
+        assert moved > len(before) // 2, (moved, len(before))
+        runs.append((met, {n: x.detach().cpu() for n, x in moe.state_dict().items()}, peak))
+        del moe, og, od, oa, orr, args
+    (mg, sg_, pg), (me, se, pe) = runs
+    assert mg == me
+    assert all(torch.equal(sg_[n], se[n]) for n in se)
+    assert pg < 160.0, pg
