@@ -79,7 +79,9 @@ def test_neutron56_e8_b4096_full_size():
     b = make_batch(B, "neutron56", seed=5)
     t = lambda k: torch.from_numpy(b[k]).to(DEV)
     runs = []
+    sg = None
     for mode in ("graph", "eager"):
+        sg = None                        # (the previous model's graph and its pool)
         torch.cuda.empty_cache()
         torch.cuda.reset_peak_memory_stats()
         moe, (og, od, oa, orr), cfg = bench.build("neutron56", E, "fp32", 1234, torch.device(DEV))
@@ -117,7 +119,7 @@ def test_neutron56_e8_b4096_full_size():
                 assert torch.isfinite(buf).all(), n
         assert moved > len(before) // 2, (moved, len(before))
         runs.append((met, {n: x.detach().cpu() for n, x in moe.state_dict().items()}, peak))
-        del moe, og, od, oa, orr, args
+        del moe, og, od, oa, orr, args, met
     (mg, sg_, pg), (me, se, pe) = runs
     assert mg == me
     assert all(torch.equal(sg_[n], se[n]) for n in se)
