@@ -216,27 +216,72 @@ def exec_flops(reset=False):
     return list(out)
 
 
-def probe_dominant(moe, eager_step, steps, arch, batch, precision):
+def probe_dominant(moe, eager_step, steps, arch, batch, precision, experts=1):
     """Per-launch HIP events around the probed generator convs' ops (on their launch stream) over eager
     steps of the same model and batch -> the roofline object of the op with the largest total time.
     Executed MFMA work per op comes from the library's own tally (es_conv_exec_flops, read around each
     op: sub-pixel 4-class convs, split-fp32's 6 plane products, exact fp32 MFMA), so `achieved` is
-    executed FLOPs / kernel time against the dense peak of the pipe the op ran on."""
+    executed FLOPs / kernel time against the dense peak of the pipe the op ran on.
+    experts > 1: every expert's ops are probed in eager steps (experts one after another, no graphs);
+    an expert's op runs on capacity-B buffers with its routed count B_e live (dynamic rows), so its
+    algorithmic and executed work are scaled by B_e / B (the step's counts, averaged over the probe
+    steps; the <= 15 padding images of its last row group are not counted) and the op types are
+    summed over the experts (label "G*.<layer>.<pass>")."""
     import torch
     from expertsim import layers
     keys = list(PROBED[arch])
-    probe = layers.KernelProbe([f"G0.{k}.{m}" for k in keys for m in ("fwd", "dgrad", "wgrad")])
+    probe = layers.KernelProbe([f"G{e}.{k}.{m}" for e in range(experts) for k in keys
+                                for m in ("fwd", "dgrad", "wgrad")])
     layers.set_probe(probe)
     exec_flops(reset=True)
-    for _ in range(steps):
+    graphs = moe.expert_graphs
+    moe.expert_graphs = False
+    counts = []
+    try:
+        # one unprobed step first: the eager (graph-free) path allocates its own buffers on first use
+        layers.set_probe(None)
         eager_step()
+        torch.cuda.synchronize()
+        exec_flops(reset=True)
+        layers.set_probe(probe)
+        for _ in range(steps):
+            met = eager_step()
+            if experts > 1:
+                counts.append([met[f"n_choosen_experts_mean_epoch_{e}"] for e in range(experts)])
+    finally:
+        moe.expert_graphs = graphs
     torch.cuda.synchronize()
     ef = [v / steps for v in exec_flops(reset=True)]
     layers.set_probe(None)
-    stats = probe.summary()
+    raw = probe.summary()
+    if experts > 1:
+        # each image is routed to one expert: B_e / B = the expert's share of the step's counts (under
+        # data parallelism the counts are global, the share the same in expectation)
+        tot = [sum(float(x) for x in c) for c in counts]
+        live = [sum(float(c[e]) / t for c, t in zip(counts, tot)) / len(counts) for e in range(experts)]
+        # the experts share one architecture: the capacity-B tally of a step is E x one expert's, its
+        # live work sum_e B_e / B of one expert's
+        ef = [v * sum(live) / experts for v in ef]
+        stats = {}
+        for lab, v in raw.items():
+            e = int(lab.split(".")[0][1:])
+            op = "G*." + lab.split(".", 1)[1]
+            agg = stats.setdefault(op, {"count": 0, "total_ms": 0.0, "exec": [0.0, 0.0, 0.0], "alg": 0.0,
+                                        "kernel_launches_per_op": v.get("kernel_launches_per_op")})
+            agg["count"] += v["count"]
+            agg["total_ms"] += v["total_ms"]
+            ex = v.get("exec_flops_per_op", [0.0, 0.0, 0.0])
+            agg["exec"] = [a + x * live[e] * v["count"] for a, x in zip(agg["exec"], ex)]
+            agg["alg"] += PROBED[arch][op.split(".")[1]] * batch * live[e] * v["count"]
+        for agg in stats.values():
+            agg["avg_ms"] = agg["total_ms"] / agg["count"]
+            agg["exec_flops_per_op"] = [x / agg["count"] for x in agg["exec"]]
+            agg["alg_per_op"] = agg["alg"] / agg["count"]
+    else:
+        stats = raw
 
     def rate(label, v):
-        alg = PROBED[arch][label.split(".")[1]] * batch
+        alg = v.get("alg_per_op", PROBED[arch][label.split(".")[1]] * batch)
         ex = v.get("exec_flops_per_op", [alg, 0.0, 0.0])
         pipe = "bf16" if ex[0] >= ex[1] else "fp32"
         exe = ex[0] if pipe == "bf16" else ex[1]
@@ -249,7 +294,8 @@ def probe_dominant(moe, eager_step, steps, arch, batch, precision):
     layer = LAYER_NAME[dom.split(".")[1]]
     split = precision == "fp32" and pipe == "bf16"
     traffic, tnote, mfma_busy = None, None, None
-    tj_path = traffic_json(arch, batch, precision, dom.split(".")[-1]) if dom.split(".")[1] == "c5" else None
+    tj_path = (traffic_json(arch, batch, precision, dom.split(".")[-1])
+               if dom.split(".")[1] == "c5" and experts == 1 else None)
     if tj_path:
         tj = json.load(open(tj_path))
         traffic = tj["traffic_bytes"]
@@ -259,6 +305,8 @@ def probe_dominant(moe, eager_step, steps, arch, batch, precision):
     kname = ("bf16 MFMA" if precision == "bf16" else
              "split-fp32, 6 x v_mfma_f32_16x16x32_bf16 per fp32 product" if split else
              "fp32, v_mfma_f32_16x16x4_f32")
+    out_note = (f"; {experts} experts on dynamic rows: the op type summed over the experts' eager ops, work "
+                f"scaled by each expert's mean live fraction {[round(x, 3) for x in live]}" if experts > 1 else "")
     return {"bound": "mfma", "kernel": f"{dom} (generator {layer}, {kname})",
             "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_note": tnote,
@@ -267,7 +315,8 @@ def probe_dominant(moe, eager_step, steps, arch, batch, precision):
                     f"read around the op; the reference's FLOPs are {alg:.4g}: sub-pixel 4-class convs execute "
                     f"es_subpixel_taps / 4RS of them, split-fp32 6 bf16 products per fp32 product) / op time, "
                     f"against the dense {pipe} MFMA peak {peak} TFLOP/s (MI355X_MICROARCH.md); "
-                    "achieved_fp32_equiv_alg = the reference's FLOPs / op time (an algorithmic rate, not a utilisation)",
+                    "achieved_fp32_equiv_alg = the reference's FLOPs / op time (an algorithmic rate, not a utilisation)"
+                    + out_note,
             "mfma_busy_pmc": mfma_busy,
             "flop_per_launch": alg, "exec_flop_per_launch": exe,
             "avg_ms": round(avg_ms, 4), "launches": stats[dom]["count"],
@@ -316,13 +365,20 @@ def run_mode(args, precision, steps, warmup, dev, rank, world, ddp, probe_steps)
         from expertsim.graph import graph_supported
         # several RCCL ranks: capture only when asked for (--graph on keeps the ranks in lockstep)
         use_graph = graph_supported(moe, allow_dp=args.graph == "on")
-    eager = lambda: moe.train_step(*step_args)
+    eager = lambda: moe.train_step(*step_args)   # (returns the metric dict)
     for _ in range(warmup):
         eager()
     step, sg = make_step(moe, step_args, use_graph)
     dt = timed(step, steps, world)
     if sg is not None:
         sg.sync_host_state([*og, *od, *oa, orr])
+    # the probe's eager steps run without the captured graphs: release their pools first
+    del step, sg
+    step = sg = None
+    if getattr(moe, "_egraphs", None) is not None:
+        moe._egraphs.clear()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
     if world > 1:
         tt = torch.tensor([dt], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -331,7 +387,7 @@ def run_mode(args, precision, steps, warmup, dev, rank, world, ddp, probe_steps)
     if probe_steps:
         # every rank runs the probed eager steps (their gradient all-reduces are collectives);
         # rank 0 reports
-        roof = probe_dominant(moe, eager, probe_steps, args.arch, args.batch, precision)
+        roof = probe_dominant(moe, eager, probe_steps, args.arch, args.batch, precision, args.experts)
         if rank != 0:
             roof = None
     value = args.batch * world * steps / dt
@@ -404,10 +460,9 @@ def main():
         else:
             dist.init_process_group("gloo", rank=rank, world_size=world)
 
-    # E > 1: the experts run on dynamic rows (capacity-B launches over a device count of live rows,
-    # replayed as per-expert graphs), where the host-side probe can neither see the ops nor count
-    # their live work: the roofline object is quoted on the E = 1 headline
-    probe_steps = 0 if args.no_probe or args.experts > 1 else 5
+    # E > 1: the probe runs eager steps (the experts' ops visible to the host) and scales each expert's
+    # work by its routed share of the batch (dynamic rows)
+    probe_steps = 0 if args.no_probe else 5
     value, dt, roof, launch = run_mode(args, args.precision, args.steps, args.warmup, dev, rank, world, ddp,
                                        probe_steps)
     other = None
@@ -448,9 +503,6 @@ def main():
                               "157.3 TF) / step time, how busy the pipes the convs run on would be at peak",
             "roofline": roof,
         }
-        if roof is None and args.experts > 1 and not args.no_probe:
-            out["roofline_note"] = ("n_experts > 1: per-expert ops run on dynamic rows (device-side live "
-                                    "counts), not probed; the roofline is quoted on the E = 1 workload")
         if args.precision == "fp32":
             out["fp32_mfma"] = FP32_MFMA
             out["precision_note"] = (

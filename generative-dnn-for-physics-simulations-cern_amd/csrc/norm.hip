@@ -22,7 +22,7 @@ bool es_fast_dense_nhwc(const es_view_t* v);
 int64_t es_fast_part_floats(const es_view_t* v, int G);
 int es_fast_norm_stats(const es_view_t* v, int G, es_dtype_t dt, const void* xp, float* part, hipStream_t st);
 void es_fast_norm_fwd(const es_view_t* v, int G, es_dtype_t dt, const void* xp, void* yp, const es_norm_t* nm,
-                      const es_chain_t* ch, hipStream_t st);
+                      const es_chain_t* ch, bool keep_ready, hipStream_t st);
 void es_fast_keep_bits(const es_view_t* v, const es_chain_t* ch, hipStream_t st);
 int es_fast_norm_bwd_reduce(const es_view_t* v, int G, es_dtype_t dt, const void* xp, const void* dyp,
                             const es_norm_t* nm, const es_chain_t* ch, float* part, hipStream_t st);
@@ -823,12 +823,14 @@ extern "C" int es_norm_act_fwd(const es_view_t* x, es_dtype_t xdt, const es_norm
   const int fk = nm ? fast_kind(x, nm->kind, nm->groups) : -1;
   const bool bits = ch && ch->keep && ch->drop.enabled;
   ES_CHECK_ARG(!bits || x->c % 8 == 0, "norm_act_fwd: dropout keep bits need C %% 8 == 0");
+  const bool ready = bits && ch->keep_ready;
   if (fk >= 0 && !addend_ptr && xdt == ydt && same_view(x, y)) {
-    es_fast_norm_fwd(x, fk, xdt, xp, yp, nm, ch, (hipStream_t)stream);
+    es_fast_norm_fwd(x, fk, xdt, xp, yp, nm, ch, ready, (hipStream_t)stream);
     ES_CHECK_LAUNCH();
     return ES_OK;
   }
-  if (bits) es_fast_keep_bits(x, ch, (hipStream_t)stream);   // the generic kernel draws the same mask
+  // the generic kernel draws the same mask in the pass; the bits for the backward are stored here
+  if (bits && !ready) es_fast_keep_bits(x, ch, (hipStream_t)stream);
   FwdArgs a{};
   a.x = mkview(x); a.xp = xp; a.xbf = xdt == ES_BF16;
   a.y = mkview(y); a.yp = yp; a.ybf = ydt == ES_BF16;
@@ -837,6 +839,14 @@ extern "C" int es_norm_act_fwd(const es_view_t* x, es_dtype_t xdt, const es_norm
   a.nm = mknorm(nm, x->c); a.ch = mkchain(ch);
   const int64_t total = (int64_t)x->n * x->c * x->h * x->w;
   hipLaunchKernelGGL(norm_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, a);
+  ES_CHECK_LAUNCH();
+  return ES_OK;
+}
+
+extern "C" int es_dropout_keep_bits(const es_view_t* x, const es_chain_t* ch, es_stream_t stream) {
+  ES_CHECK_ARG(x && ch && ch->keep && ch->drop.enabled, "dropout_keep_bits: needs an enabled dropout with keep");
+  ES_CHECK_ARG(x->c % 8 == 0, "dropout_keep_bits: C %% 8 == 0 required (C = %d)", x->c);
+  es_fast_keep_bits(x, ch, (hipStream_t)stream);
   ES_CHECK_LAUNCH();
   return ES_OK;
 }

@@ -660,14 +660,15 @@ int es_fast_norm_stats(const es_view_t* v, int G, es_dtype_t dt, const void* xp,
   return chunks;
 }
 
+// keep_ready: a.keep already holds the mask (es_dropout_keep_bits): KM_BITS reads it, no Philox
 void es_fast_norm_fwd(const es_view_t* v, int G, es_dtype_t dt, const void* xp, void* yp, const es_norm_t* nm,
-                      const es_chain_t* ch, hipStream_t st) {
+                      const es_chain_t* ch, bool keep_ready, hipStream_t st) {
   dim3 grid; int chunks;
   fast_geometry(v, G, grid, chunks);
   FastArgs a = mk(v, ch, G);
   a.x = xp; a.out = yp;
   a.mean = nm->mean; a.invstd = nm->invstd; a.gamma = nm->gamma; a.beta = nm->beta;
-  ES_KM_DISPATCH(a, bn_fwd_fast, dt, grid, st, false);
+  ES_KM_DISPATCH(a, bn_fwd_fast, dt, grid, st, keep_ready);
 }
 
 // dropout keep bits alone (for a forward that did not run the fast kernels): same bits as

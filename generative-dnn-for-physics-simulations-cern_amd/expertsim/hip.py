@@ -48,7 +48,7 @@ class Norm(C.Structure):
 
 class Chain(C.Structure):
     _fields_ = [("drop", Dropout), ("dropout_first", C.c_int), ("act", C.c_int), ("slope", C.c_float),
-                ("keep", C.c_void_p)]
+                ("keep", C.c_void_p), ("keep_ready", C.c_int)]
 
 
 class GenLoss(C.Structure):
@@ -127,6 +127,7 @@ _SIGS = {
     "es_norm_bwd_sync": (C.c_int, [C.c_int, P, C.c_int, P, P, P, P, C.c_int, P, P, C.c_int, P, P, C.c_float, P, P,
                                    P, P, P, P]),
     "es_act_fwd": (C.c_int, [P, C.c_int, P, P, P, C.c_int, P, P]),
+    "es_dropout_keep_bits": (C.c_int, [P, P, P]),
     "es_channel_sum_ws_bytes": (I64, [P]),
     "es_channel_sum": (C.c_int, [P, C.c_int, P, P, C.c_float, P, P]),
     "es_maxpool_fwd": (C.c_int, [P, C.c_int, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P]),

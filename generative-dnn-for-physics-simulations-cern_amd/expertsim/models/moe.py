@@ -420,6 +420,18 @@ class MoEWrapper(nn.Module):
             st.wait_stream(cur)
         return self._side[:E]
 
+    def _bits_stream(self, e, G):
+        """Side stream of expert e for the ahead-of-time dropout draw (train.dropout_ahead), or None
+        (switched off, or a generator without keep_plan / draw_keep)."""
+        if not bool(cfg_get(self.cfg, "train.dropout_ahead", False)) or not hasattr(G, "draw_keep"):
+            return None
+        if getattr(self, "_bits_side", None) is None:
+            self._bits_side = {}
+        st = self._bits_side.get(e)
+        if st is None:
+            st = self._bits_side[e] = torch.cuda.Stream()
+        return st
+
     def _plan(self, counts, B, dev):
         """The multi-expert step plan on the device (es_expert_plan): per expert the live rows of this
         process, the active flag (global count > 1, moe.py:126), the first global sample index, the
@@ -495,6 +507,14 @@ class MoEWrapper(nn.Module):
         # ---- generator forward #1 (moe.py:144-145)
         n1 = self._noise(e, 0, (be, self.noise_dim), dev, row0=n0)
         fake1, gctx1 = G.fwd(n1, sc, seed=seed, stream_base=sb(philox.PASS_G1), n_offset=n0)
+        # the second forward's dropout masks are data-independent: drawn on a side stream during the
+        # discriminator step (latency-bound kernels), read by that forward's norm passes
+        pre2, bits_side = {}, self._bits_stream(e, G)
+        if bits_side is not None:
+            pre2 = {"pre": G.keep_plan(be, dev, seed=seed, stream_base=sb(philox.PASS_G2), n_offset=n0)}
+            bits_side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(bits_side):
+                G.draw_keep(pre2["pre"], be)
 
         # ---- discriminator step (moe.py:506-527)
         ro, _, dctx_r = D.fwd(Act.of(sr), sc)
@@ -506,15 +526,17 @@ class MoEWrapper(nn.Module):
         D.bwd(dctx_r, dout=Act.of(dro), weight_grads=True, input_grad=False)
         D.bwd(dctx_f, dout=Act.of(dfo), weight_grads=True, input_grad=False)
         n2 = self._noise(e, 1, (be, self.noise_dim), dev, row0=n0)
+        if bits_side is not None:
+            torch.cuda.current_stream().wait_stream(bits_side)
         if ddp is None:
             opt_d.step()
             # ---- generator step (moe.py:529-571)
-            fake2, gctx2 = G.fwd(n2, sc, seed=seed, stream_base=sb(philox.PASS_G2), n_offset=n0)
+            fake2, gctx2 = G.fwd(n2, sc, seed=seed, stream_base=sb(philox.PASS_G2), n_offset=n0, **pre2)
         else:
             # data parallel: D's gradient all-reduce overlaps the second generator forward (which
             # does not read D); D's Adam waits for it
             ddp.allreduce_async(D)
-            fake2, gctx2 = G.fwd(n2, sc, seed=seed, stream_base=sb(philox.PASS_G2), n_offset=n0)
+            fake2, gctx2 = G.fwd(n2, sc, seed=seed, stream_base=sb(philox.PASS_G2), n_offset=n0, **pre2)
             ddp.wait_all()
             opt_d.step()
         fo1, fl1, dctx1 = D.fwd(fake1, sc)

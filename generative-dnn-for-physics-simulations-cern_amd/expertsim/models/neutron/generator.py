@@ -18,6 +18,8 @@ Dropout masks come from Philox streams (expertsim/utils/philox.py), layer index 
 from __future__ import annotations
 
 
+import ctypes as C
+
 import torch
 from torch import nn
 
@@ -86,10 +88,41 @@ class GeneratorNeutron(ExpertModule):
         return hip.chain_struct(hip.ACT_LRELU, SLOPE, d, dropout_first=True)
 
     # --------------------------------------------------------------------------- forward
-    def fwd(self, noise: torch.Tensor, cond: torch.Tensor, seed=0, stream_base=0, train=True, n_offset=0):
+    def _norm_shapes(self):
+        """(channels, side) of the five normalised tensors, the order of the dropout layers 0..4."""
+        k = self.base
+        return ((256, 1), (self.fc2_features, 1), (256, 2 * k - 2), (128, 4 * k - 6), (64, 4 * k - 7))
+
+    def keep_plan(self, B, dev, seed=0, stream_base=0, train=True, n_offset=0):
+        """The five dropout chains of one forward and their keep-bit buffers [rows][C/8] (allocated on
+        the current stream): the forward norm passes draw the masks into them, the backward re-reads
+        them.  Returns (chains, buffers)."""
+        ch = [self._chain(seed, stream_base, i, train) for i in range(5)]
+        keep = [hip.attach_keep(ch[i], B * s * s, c, dev) for i, (c, s) in enumerate(self._norm_shapes())]
+        for i, (c, s) in enumerate(self._norm_shapes()):
+            hip.set_index_offset(ch[i].drop, n_offset, s * s * c)
+        return ch, keep
+
+    def draw_keep(self, plan, B):
+        """Draw a keep_plan's masks now, on the current stream (es_dropout_keep_bits: the bits the
+        norm passes would draw), and mark the chains so the forward reads them.  The caller runs this
+        on a side stream beside work that leaves the chip's VALUs idle and joins it before fwd(pre=plan)
+        (moe.MoEWrapper: the second forward's masks during the discriminator step)."""
+        ch, keep = plan
+        for i, (c, s) in enumerate(self._norm_shapes()):
+            if keep[i] is None:
+                continue
+            v = hip.make_view((B, c, s, s), (s * s * c, 1, s * c, c))
+            hip.call("es_dropout_keep_bits", C.byref(v), C.byref(ch[i]), hip.stream_ptr())
+            ch[i].keep_ready = 1
+        return plan
+
+    def fwd(self, noise: torch.Tensor, cond: torch.Tensor, seed=0, stream_base=0, train=True, n_offset=0,
+            pre=None):
         """noise [B,10] fp32, cond [B,9] fp32 (device) -> (image Act [B,1,44,44] fp32 NHWC, ctx).
         n_offset: index of the first sample in the expert's global batch (data parallel: dropout
-        masks are drawn at the global sample index, expertsim/utils/philox.py)."""
+        masks are drawn at the global sample index, expertsim/utils/philox.py).  pre: a keep_plan of
+        the same arguments whose masks draw_keep has drawn (the norm passes read them)."""
         o = self.ops()
         k, F2 = self.base, self.fc2_features
         cdt = self.compute_dtype
@@ -99,12 +132,9 @@ class GeneratorNeutron(ExpertModule):
         x0m = x0.t.view(B, -1)
         copy_act(Act.of(noise), Act.of(x0m[:, :self.noise_dim]))
         copy_act(Act.of(cond), Act.of(x0m[:, self.noise_dim:]))
-        ch = [self._chain(seed, stream_base, i, train) for i in range(5)]
-        # dropout keep bits, drawn once in the forward norm pass and re-read by the backward
-        per_sample = ((1, 256), (1, F2), ((2 * k - 2) ** 2, 256), ((4 * k - 6) ** 2, 128), ((4 * k - 7) ** 2, 64))
-        keep = [hip.attach_keep(ch[i], B * r, c, dev) for i, (r, c) in enumerate(per_sample)]
-        for i, (r, c) in enumerate(per_sample):
-            hip.set_index_offset(ch[i].drop, n_offset, r * c)
+        # dropout keep bits, drawn once (in the forward norm pass, or ahead by draw_keep) and re-read
+        # by the backward
+        ch, keep = pre if pre is not None else self.keep_plan(B, dev, seed, stream_base, train, n_offset)
         h1 = o["fc1"].fwd(x0)
         y1, s1 = o["bn1"].fwd(h1, ch[0], train=train)
         h2 = o["fc2"].fwd(y1, bn_stats=train)        # (ring FWD over 16-row pixel blocks: stats in its epilogue)

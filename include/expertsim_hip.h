@@ -275,6 +275,9 @@ typedef struct {
   uint8_t* keep;     /* optional device dropout keep bits, layout [n*h*w][c/8] (bit c%8 of byte
                         (row, c/8)), c % 8 == 0 required: es_norm_act_fwd writes the mask it draws,
                         es_norm_act_bwd then reads it instead of re-running Philox (same mask)   */
+  int keep_ready;    /* 1: keep already holds this chain's mask (es_dropout_keep_bits, e.g. drawn on a
+                        side stream ahead of the forward): es_norm_act_fwd reads it instead of
+                        drawing it                                                                */
 } es_chain_t;
 
 /* Batch statistics of x (train-mode BN / GN / LN), written to mean/invstd per stats group.
@@ -348,6 +351,11 @@ int es_norm_bwd_sync(int phase, const es_view_t* x, es_dtype_t xdt, const void* 
 
 /* Plain elementwise chain without normalisation (router LeakyReLU, final ReLU, casts):
  * y = chain(x). And its backward dx = beta*dx + dchain(dy) evaluated at x (or act_ref). */
+/* Draw the dropout keep bits of chain ch over x's geometry (n, c, h, w; dynamic rows: the live
+ * samples of x->rows) into ch->keep -- the mask es_norm_act_fwd would draw for the same chain.  A
+ * forward given the chain with keep_ready = 1 then reads them (reference: the nn.Dropout masks of
+ * neutron/generator.py:13-36, drawn ahead of their layer; bit-identical to the in-pass draw). */
+int es_dropout_keep_bits(const es_view_t* x, const es_chain_t* ch, es_stream_t stream);
 int es_act_fwd(const es_view_t* x, es_dtype_t xdt, const void* xp, const es_chain_t* ch,
                const es_view_t* y, es_dtype_t ydt, void* yp, es_stream_t stream);
 
