@@ -2887,17 +2887,32 @@ extern "C" int es_conv_subpixel_ok(const es_conv_desc_t* d, es_dtype_t dt) {
   // fp32: the ring launches over image chunks below 1 GiB (es_conv_ring_launch_f32)
   if (dt == ES_F32) return wbytes < (1ll << 30) && (int64_t)d->H * d->W * d->C * eb < (1ll << 24) &&
                            (int64_t)d->P * d->Q * d->K * eb < (1ll << 24);
-  return xbytes < (1ll << 30) && ybytes < (1ll << 30) && wbytes < (1ll << 30);
+  // (bf16 too: operands of >= 1 GiB run as image chunks, es_conv_ring_launch; the merged 256 x 256
+  // kernel's 32-bit output offsets are checked where it is chosen)
+  (void)xbytes; (void)ybytes;
+  return wbytes < (1ll << 30) && (int64_t)d->H * d->W * d->C * eb < (1ll << 24) &&
+         (int64_t)d->P * d->Q * d->K * eb < (1ll << 24);
 }
 
 template <typename T, int SPL = 0>
 int ring_fd(ConvArgs& a, int mode, hipStream_t st);
+namespace {
+int chunk_images(int64_t img_bytes, int N);
+int ring_launch_chunks(ConvArgs& a, int mode, int nc, hipStream_t st);
+}  // namespace
 
 int es_conv_ring_launch(ConvArgs& a, int mode, hipStream_t st) {
   const es_conv_desc_t& d = a.d;
   const bool sp_weights = d.subpixel != 0;   // FWD / DGRAD operands packed for the sub-pixel path
   if (g_ring_off && !sp_weights) return 0;
   if (d.hmap != nullptr || d.stride > 2 || a.splitk) return sp_weights ? -1 : 0;
+  // gathered operands of >= 1 GiB (a capacity-2048 expert's conv_layers.5 output gradient is 1.1 GB
+  // in bf16): launches over image chunks below the limit, as the fp32 ring does
+  {
+    const int64_t img = (mode == MODE_WGRAD ? std::max<int64_t>(a.as[0], a.bs[0]) : a.as[0]) * 2;
+    const int nc = chunk_images(img, d.N);
+    if (nc < d.N) return ring_launch_chunks(a, mode, nc, st);
+  }
   if (mode == MODE_WGRAD) {
     if (!dense_small(a.as, d.N, d.K, d.P, d.Q) || !dense_small(a.bs, d.N, d.C, d.H, d.W)) return 0;
     const bool sp = !g_subpixel_off && d.up_h == 2 && d.up_w == 2 && d.stride == 1;
@@ -3141,6 +3156,53 @@ int chunk_images(int64_t img_bytes, int N) {
   int64_t nc = (N + nchunks - 1) / nchunks;
   if (nc % 64 && (nc + 63) / 64 * 64 <= lim) nc = (nc + 63) / 64 * 64;
   return (int)nc;
+}
+}  // namespace
+
+namespace {
+// bf16 ring launches over image chunks (es_conv_ring_launch): each chunk on offset base pointers
+// with its first image as the dynamic-rows base; FWD statistics partials appended chunk after
+// chunk; the fused BatchNorm-backward reduction of the persistent DGRAD is not offered to chunked
+// launches (the caller runs the reduction pass).  WGRAD: the chunks' atomic accumulations into dW.
+int ring_launch_chunks(ConvArgs& a, int mode, int nc, hipStream_t st) {
+  const es_conv_desc_t& d = a.d;
+  const int N = d.N;
+  const int esz = a.out_bf16 ? 2 : 4;
+  const StatsRequest req = g_stats_req;
+  const BnRedRequest bnr = g_bnr_req;
+  g_bnr_req.part = nullptr;
+  int used = 0, rc = 1;
+  bool stats_ok = req.part != nullptr;
+  for (int n0 = 0; n0 < N; n0 += nc) {
+    ConvArgs c = a;
+    c.d.N = std::min(nc, N - n0);
+    c.nbase = a.nbase + n0;
+    c.a_src = (const char*)a.a_src + (int64_t)n0 * a.as[0] * 2;
+    if (mode == MODE_WGRAD) {
+      c.b_src = (const char*)a.b_src + (int64_t)n0 * a.bs[0] * 2;
+      c.Kd = c.d.N * d.P * d.Q;
+    } else {
+      c.out = (char*)a.out + (int64_t)n0 * a.os[0] * esz;
+      c.M = mode == MODE_FWD ? c.d.N * d.P * d.Q : (a.fold ? c.d.N * d.H * d.W : c.d.N * d.Hu * d.Wu);
+    }
+    if (req.part) g_stats_req = StatsRequest{req.part + (int64_t)used * 3 * a.Ng, req.floats - (int64_t)used * 3 * a.Ng, 0};
+    rc = es_conv_ring_launch(c, mode, st);
+    if (rc <= 0) {
+      if (n0 > 0) {
+        es_set_error("conv bf16 ring: image chunk at %d not eligible", n0);
+        rc = -1;
+      }
+      break;
+    }
+    if (req.part) {
+      stats_ok = stats_ok && g_stats_req.chunks > 0;
+      used += g_stats_req.chunks;
+    }
+  }
+  g_stats_req = StatsRequest{req.part, req.floats, rc > 0 && stats_ok ? used : 0};
+  g_bnr_req = bnr;
+  g_bnr_req.chunks = 0;
+  return rc;
 }
 }  // namespace
 

@@ -422,8 +422,11 @@ class MoEWrapper(nn.Module):
 
     def _bits_stream(self, e, G):
         """Side stream of expert e for the ahead-of-time dropout draw (train.dropout_ahead), or None
-        (switched off, or a generator without keep_plan / draw_keep)."""
-        if not bool(cfg_get(self.cfg, "train.dropout_ahead", False)) or not hasattr(G, "draw_keep"):
+        (switched off, a generator without keep_plan / draw_keep, or several experts: a whole-step
+        capture with the experts forked AND the draw forked from each expert's stream ended in a
+        segmentation fault in capture_end, tools/gpu_r06r.sh; the draw measured slower anyway)."""
+        if (not bool(cfg_get(self.cfg, "train.dropout_ahead", False)) or not hasattr(G, "draw_keep")
+                or self.n_experts > 1):
             return None
         if getattr(self, "_bits_side", None) is None:
             self._bits_side = {}

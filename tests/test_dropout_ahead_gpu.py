@@ -5,8 +5,8 @@ same training steps as masks drawn inside the norm passes.
 Reference: the nn.Dropout layers of neutron/generator.py:13-36 (one mask per layer and forward).
 The masks are data-independent Philox draws keyed on (seed, stream, step, logical index), so the
 ahead-of-time draw must be bit-identical: fp32 parity mode (deterministic reductions), every metric,
-parameter and buffer compared bitwise after every step -- captured whole-step graph (E = 1) and
-dynamic rows with 4 experts (eager, live counts read on the device).
+parameter and buffer compared bitwise after every step, eager and in a captured whole-step graph.
+The draw is single-expert only (MoEWrapper._bits_stream).
 """
 import pytest
 import torch
@@ -65,8 +65,8 @@ def test_dropout_ahead_graph_e1_matches_in_pass_draw():
 
 
 @pytest.mark.timeout(240)
-def test_dropout_ahead_dynamic_rows_e4():
-    """E = 4, B = 256 on dynamic rows (the draw covers each expert's live rows only)."""
-    ref = _run(4, 256, 2, ahead=False, graph=False, seed=32)
-    got = _run(4, 256, 2, ahead=True, graph=False, seed=32)
+def test_dropout_ahead_eager_e1_b512():
+    """E = 1, B = 512, eager steps both ways (the side-stream fork outside any capture)."""
+    ref = _run(1, 512, 2, ahead=False, graph=False, seed=32)
+    got = _run(1, 512, 2, ahead=True, graph=False, seed=32)
     _compare(ref, got)
