@@ -15,7 +15,8 @@ LAYERS = {"c0": (128, 13, 13, 256, 24, 24, 3), "c5": (256, 24, 24, 128, 46, 46, 
           "c9": (128, 46, 46, 64, 45, 45, 2),
           "p1": (512, 18, 10, 256, 35, 19, 4), "p5": (256, 35, 19, 128, 55, 29, 4)}
 NAMES = {"fwd": ("conv_ring_kernel<0", "upsample_fwd_nhwc"), "dgrad": ("conv_ring_kernel<1", "upsample_bwd_nhwc"),
-         "wgrad": ("wgrad_f32_kernel", "wgrad_f32_col_kernel", "wgrad_f32_col2_kernel", "wgrad_coop_kernel", "wgrad_reduce_kernel")}
+         "wgrad": ("wgrad_f32_kernel", "wgrad_f32_col_kernel", "wgrad_f32_col2_kernel", "wgrad_coop_kernel", "wgrad_ws_kernel",
+                   "wgrad_reduce_kernel")}
 
 
 def rows(d, counter, names):
