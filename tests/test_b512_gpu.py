@@ -149,3 +149,35 @@ def test_e4_b2048_step0_matches_reference():
         tol = max(TOL["neutron"], A_STEP0_TOL.get("neutron", 0.0)) if comp == "A" else TOL["neutron"]
         _check(grad_errors(g, 0, label, grads, "neutron", comp), tol, ("e4_b2048", 0, label), abs_tol=abs_tol,
                sens=sens, label=label)
+
+
+# bf16 mode at configs[3]'s size (statistical parity mode, SURVEY.md §8(c) last row): measured max
+# relative deviation of the averaged losses from the reference's fp32 step 0, printed below
+BF16_STEP0_TOL = 5e-2
+
+
+def test_e4_b2048_step0_bf16_close_to_reference():
+    """BASELINE configs[3] (E = 4, B = 2048) in the bf16 performance mode: a capacity-2048 expert's
+    conv_layers.5 output gradient is 1.1 GB in bf16, so its FWD / DGRAD / WGRAD run as image-chunked
+    ring launches (es_conv_ring_launch; tests/test_bf16_chunks_gpu.py at the kernel level).  bf16
+    operands are not elementwise-comparable with the reference's fp32: the step's averaged losses
+    against the reference's step 0 within BF16_STEP0_TOL relative, every metric finite."""
+    import math
+    g = Golden("neutron_e4_b2048")
+    moe, (og, od, oa, orr), cfg = _build(g, precision="bf16")
+    inp = g.inputs(0)
+    nz = g.noise(0)
+    moe.noise_fn = lambda e, w, shape: torch.from_numpy(nz[(e, w)])
+    gum = torch.from_numpy(g.gumbel(0))
+    moe.gumbel_fn = lambda shape: gum
+    t = lambda k: torch.from_numpy(inp[k]).to(DEV)
+    met = moe.train_step(g.epoch, t("cond"), t("real_images").unsqueeze(1), t("true_positions"), t("std"),
+                         t("intensity"), oa, og, od, orr, None, DEV)
+    torch.cuda.synchronize()
+    met = {k: float(v) for k, v in met.items()}
+    gm = g.metrics(0)
+    assert all(math.isfinite(v) for v in met.values()), met
+    keys = ("gen_loss", "disc_loss", "div_loss", "intensity_loss", "aux_reg_loss")
+    dev = {k: abs(met[k] - gm[k]) / max(abs(gm[k]), 1e-3) for k in keys}
+    print("bf16 E=4 B=2048 step-0 relative deviation:", {k: f"{v:.2e}" for k, v in dev.items()})
+    assert all(v <= BF16_STEP0_TOL for v in dev.values()), dev

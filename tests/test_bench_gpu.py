@@ -1,6 +1,6 @@
 """bench.py end to end (the driver's contract): one JSON line on stdout with the metric, the whole-job
 value, the roofline object of the probed generator conv and the other-precision leg; for E > 1
-(dynamic rows, per-expert graphs) the roofline is not probed and says why.  Small batches and few
+(dynamic rows) the roofline sums each c5 op type over the experts' eager ops.  Small batches and few
 steps: this checks the control flow and the line's shape, not the numbers."""
 import json
 import os
@@ -39,4 +39,7 @@ def test_bench_line_e1():
 def test_bench_line_multi_expert():
     d = _bench("--experts", "4", "--batch", "128", "--steps", "3", "--warmup", "2", "--other-steps", "0")
     assert d["config"]["n_experts"] == 4 and d["value"] > 0
-    assert d["roofline"] is None and "dynamic rows" in d["roofline_note"]
+    # the E > 1 roofline: every expert's c5 ops probed in eager steps, work scaled by the routed shares
+    r = d["roofline"]
+    assert r["kernel"].startswith("G*.c5.") and "dynamic rows" in r["note"] and 0 < r["frac"] < 1, r
+    assert set(r["all_probed"]) == {"G*.c5.fwd", "G*.c5.dgrad", "G*.c5.wgrad"}

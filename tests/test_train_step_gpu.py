@@ -31,12 +31,12 @@ STEP1_TOL = {"neutron_e1_b8": 2e-4, "neutron_e3_b12": 5e-3, "proton_e1_b8": 3.9e
              "neutron_e3_b12_router": 5e-3}
 
 
-def _build(g: Golden):
+def _build(g: Golden, precision="fp32"):
     from expertsim.config import inject_shared, load_config
     from expertsim.models import build_model
     from expertsim.models.moe import MoEWrapper
     from expertsim.train.training_setup import setup_optimizers
-    ov = [f"model.architecture={g.arch}", f"model.n_experts={g.E}", "train.precision=fp32",
+    ov = [f"model.architecture={g.arch}", f"model.n_experts={g.E}", f"train.precision={precision}",
           f"train.rng_seed={g.seed}", "model.router.diff_strength=1e-6", *g.overrides()]
     cfg = inject_shared(load_config(overrides=ov))
     torch.manual_seed(g.seed)
