@@ -187,8 +187,8 @@ int es_conv_set_wgrad_ws(int on);
  * float atomics, the generic norm backward's conv-bias sums become an ordered column reduction.
  * MoEWrapper turns it on in the fp32 parity mode (train.deterministic, default on). */
 int es_set_deterministic(int on);
-/* Test knob: fp32 ring convolutions launch over chunks of at most `images` images (0: only as the
- * 1 GiB operand limit requires); returns the previous value. */
+/* Test knob: ring convolutions (fp32 and bf16) launch over chunks of at most `images` images (0: only
+ * as the 1 GiB operand limit requires); returns the previous value. */
 int es_conv_set_f32_chunk(int images);
 /* fp32 MFMA arithmetic of the ring convolutions (returns the previous setting): 0 = exact fp32
  * (v_mfma_f32_16x16x4_f32), 1 = split-fp32: each fp32 operand is the exact sum of three bf16
