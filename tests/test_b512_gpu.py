@@ -151,9 +151,10 @@ def test_e4_b2048_step0_matches_reference():
                sens=sens, label=label)
 
 
-# bf16 mode at configs[3]'s size (statistical parity mode, SURVEY.md §8(c) last row): measured max
-# relative deviation of the averaged losses from the reference's fp32 step 0, printed below
-BF16_STEP0_TOL = 5e-2
+# bf16 mode at configs[3]'s size (statistical parity mode, SURVEY.md §8(c) last row): relative
+# deviation of the averaged losses from the reference's fp32 step 0, measured (r06w) gen 1.4e-4,
+# disc 1.1e-4, div 1.3e-4, intensity 3.9e-4, aux 8.6e-7 -- the bound keeps > 10x of margin
+BF16_STEP0_TOL = 5e-3
 
 
 def test_e4_b2048_step0_bf16_close_to_reference():
