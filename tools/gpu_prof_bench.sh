@@ -9,6 +9,6 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/benchprof_$tag
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace -d $O/raw -o run -- python3 $R/bench.py "$@" > $O/bench.log 2>&1 || exit $?
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/raw -o run -- python3 $R/bench.py "$@" > $O/bench.log 2>&1 || exit $?
 db=$(find $O/raw -name '*.db' | head -1)
 python3 $R/tools/prof_summary.py $db 60 > $O/summary.md && rm -rf $O/raw

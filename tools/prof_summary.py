@@ -28,6 +28,17 @@ def main(path, top=25):
     print(f"kernels {len(rows)}  summed {summed / 1e3:.1f} ms  busy(union) {busy / 1e6:.1f} ms  span {span / 1e3:.1f} ms")
     for n, (cnt, us) in sorted(tot.items(), key=lambda kv: -kv[1][1])[:top]:
         print(f"{us / 1e3:9.2f} ms {cnt:6d} x {us / cnt:8.1f} us  {n[:150]}")
+    # one template instance can serve several layers (e.g. conv_layers.0 and .5 FWD): the top kernels
+    # split by launch grid
+    cols = [r[1] for r in c.execute("pragma table_info(kernels)").fetchall()]
+    grid = [k for k in cols if k.startswith("grid_size")] or [k for k in cols if "grid" in k]
+    if grid:
+        print("\nby launch grid (" + ", ".join(grid) + "):")
+        for n, _ in sorted(tot.items(), key=lambda kv: -kv[1][1])[:min(top, 12)]:
+            q = f"select {', '.join(grid)}, count(*), sum(end - start) from kernels where name = ? group by {', '.join(grid)}"
+            for row in c.execute(q, (n,)).fetchall():
+                g, cnt, ns = row[:-2], row[-2], row[-1]
+                print(f"{ns / 1e6:9.2f} ms {cnt:6d} x {ns / 1e3 / cnt:8.1f} us  grid {tuple(g)}  {n[:110]}")
 
 
 if __name__ == "__main__":
