@@ -25,6 +25,8 @@ Not captured: gloo process groups (their collectives go through the host).
 """
 from __future__ import annotations
 
+import time
+
 import torch
 
 
@@ -61,6 +63,12 @@ class StepGraph:
                 moe.train_step(*self.args)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
+        if moe.ddp is not None and not moe.ddp.gloo:
+            # let the process group's watchdog retire the eager steps' collectives (it polls every
+            # ~100 ms) so that it queries no event while this thread captures: a watchdog query during
+            # a capture aborted the process group once ("operation not permitted on an event last
+            # recorded in a capturing stream", test_ddp_graph_gpu.py, 1 of 4 runs at E = 1)
+            time.sleep(0.5)
         self.graph = torch.cuda.CUDAGraph()
         # thread_local: the capture does not forbid other threads' HIP calls -- the process group's
         # watchdog thread keeps querying the events of the eager steps' collectives while this thread
