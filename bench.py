@@ -216,6 +216,38 @@ def exec_flops(reset=False):
     return list(out)
 
 
+def aggregate_expert_ops(raw, counts, ef, arch, batch):
+    """Multi-expert probe: per-expert op summaries {"G<e>.<layer>.<pass>": {count, total_ms,
+    exec_flops_per_op, ...}} of capacity-B launches -> per op type "G*.<layer>.<pass>" with each
+    expert's work scaled by its routed share B_e / B.  counts: per probe step, the E routed counts.
+    ef: the step's capacity-B executed-work tally [bf16 pipe, fp32 MFMA, VALU].  Returns (stats,
+    live shares, ef scaled to the live work)."""
+    experts = len(counts[0])
+    # each image is routed to one expert: B_e / B = the expert's share of the step's counts (under
+    # data parallelism the counts are global, the share the same in expectation)
+    tot = [sum(c) for c in counts]
+    live = [sum(c[e] / t for c, t in zip(counts, tot)) / len(counts) for e in range(experts)]
+    # the experts share one architecture: the capacity-B tally of a step is E x one expert's, its
+    # live work sum_e B_e / B of one expert's
+    ef = [v * sum(live) / experts for v in ef]
+    stats = {}
+    for lab, v in raw.items():
+        e = int(lab.split(".")[0][1:])
+        op = "G*." + lab.split(".", 1)[1]
+        agg = stats.setdefault(op, {"count": 0, "total_ms": 0.0, "exec": [0.0, 0.0, 0.0], "alg": 0.0,
+                                    "kernel_launches_per_op": v.get("kernel_launches_per_op")})
+        agg["count"] += v["count"]
+        agg["total_ms"] += v["total_ms"]
+        ex = v.get("exec_flops_per_op", [0.0, 0.0, 0.0])
+        agg["exec"] = [a + x * live[e] * v["count"] for a, x in zip(agg["exec"], ex)]
+        agg["alg"] += PROBED[arch][op.split(".")[1]] * batch * live[e] * v["count"]
+    for agg in stats.values():
+        agg["avg_ms"] = agg["total_ms"] / agg["count"]
+        agg["exec_flops_per_op"] = [x / agg["count"] for x in agg["exec"]]
+        agg["alg_per_op"] = agg["alg"] / agg["count"]
+    return stats, live, ef
+
+
 def probe_dominant(moe, eager_step, steps, arch, batch, precision, experts=1):
     """Per-launch HIP events around the probed generator convs' ops (on their launch stream) over eager
     steps of the same model and batch -> the roofline object of the op with the largest total time.
@@ -255,28 +287,7 @@ def probe_dominant(moe, eager_step, steps, arch, batch, precision, experts=1):
     layers.set_probe(None)
     raw = probe.summary()
     if experts > 1:
-        # each image is routed to one expert: B_e / B = the expert's share of the step's counts (under
-        # data parallelism the counts are global, the share the same in expectation)
-        tot = [sum(float(x) for x in c) for c in counts]
-        live = [sum(float(c[e]) / t for c, t in zip(counts, tot)) / len(counts) for e in range(experts)]
-        # the experts share one architecture: the capacity-B tally of a step is E x one expert's, its
-        # live work sum_e B_e / B of one expert's
-        ef = [v * sum(live) / experts for v in ef]
-        stats = {}
-        for lab, v in raw.items():
-            e = int(lab.split(".")[0][1:])
-            op = "G*." + lab.split(".", 1)[1]
-            agg = stats.setdefault(op, {"count": 0, "total_ms": 0.0, "exec": [0.0, 0.0, 0.0], "alg": 0.0,
-                                        "kernel_launches_per_op": v.get("kernel_launches_per_op")})
-            agg["count"] += v["count"]
-            agg["total_ms"] += v["total_ms"]
-            ex = v.get("exec_flops_per_op", [0.0, 0.0, 0.0])
-            agg["exec"] = [a + x * live[e] * v["count"] for a, x in zip(agg["exec"], ex)]
-            agg["alg"] += PROBED[arch][op.split(".")[1]] * batch * live[e] * v["count"]
-        for agg in stats.values():
-            agg["avg_ms"] = agg["total_ms"] / agg["count"]
-            agg["exec_flops_per_op"] = [x / agg["count"] for x in agg["exec"]]
-            agg["alg_per_op"] = agg["alg"] / agg["count"]
+        stats, live, ef = aggregate_expert_ops(raw, [[float(x) for x in c] for c in counts], ef, arch, batch)
     else:
         stats = raw
 
