@@ -3,7 +3,9 @@
 usage: python tools/cfg_ab.py --key train.dropout_ahead --vals false,true [--batch 1024]
        [--experts 1] [--precision fp32] [--rounds 3] [--reps 30]
 One model per value (same seed), each captured as a StepGraph; the rounds alternate the values and
-print ms/step per value per round, so box drift hits every value alike."""
+print ms/step per value per round, so box drift hits every value alike.  A key starting with "es_"
+is a library switch (es_conv_set_*): set to the value while that model's steps are captured (the
+dispatch is baked into the graph)."""
 import argparse
 import os
 import sys
@@ -47,11 +49,15 @@ def main():
     runs = []
     for v in [parse(x) for x in a.vals.split(",")]:
         moe, (og, od, oa, orr), cfg = bench.build(a.arch, a.experts, a.precision, 1234, dev)
-        node = cfg
-        *path, leaf = a.key.split(".")
-        for p in path:
-            node = getattr(node, p)
-        setattr(node, leaf, v)
+        if a.key.startswith("es_"):
+            from expertsim import hip
+            getattr(hip.lib(), a.key)(int(v))
+        else:
+            node = cfg
+            *path, leaf = a.key.split(".")
+            for p in path:
+                node = getattr(node, p)
+            setattr(node, leaf, v)
         args = (0, t["cond"], real, t["true_positions"], t["std"], t["intensity"], oa, og, od, orr, None, dev)
         for _ in range(2):
             moe.train_step(*args)
